@@ -1,0 +1,217 @@
+#!/usr/bin/env python3
+"""bench.py -- headline benchmark of the MI355X offline-render + STFT path.
+
+Metric (BASELINE.json): Msamples/s of the offline render + 8192-point FFT on
+48 kHz stereo, at 1/2/4/8 GPUs, and the fraction of the HBM roofline.
+
+One step = one pass of the hot path over one batch of synthetic input that
+is already resident in HBM:
+
+    IR_test render (B = 512, the reference's 10 ms @ 48 kHz block,
+    wasapi_audio.cpp:456-457) of 1 h of 48 kHz stereo per GPU, and the
+    8192-point Hann STFT (hop 4096, 4097 bins) of that render,
+    = dsp_render_stft(...): ramp-table kernel + fused render/STFT kernel
+      + render tail kernel.
+
+Multi-GPU (launched by torch.distributed.run): the file is N hours long and
+every rank renders its own hour (time-chunk sharding with an N - H = 4096
+sample halo) -- no data-path collective, weak scaling.  With
+--gather the outputs are additionally gathered to rank 0 over RCCL (xGMI)
+and that time is reported separately ("gather_ms"), outside `value`.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--minutes M]
+                       [--no-cpu-baseline] [--gather]
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "dsp-bench_amd"))
+
+METRIC = "Msamples/s offline render+8192-pt FFT, 48kHz stereo, 1/2/4/8 GPU; %HBM roofline"
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+SR, CH, B, N_FFT, HOP = 48_000, 2, 512, 8192, 4096
+K_BINS = N_FFT // 2 + 1
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--minutes", type=float, default=60.0, help="audio per GPU (default 1 h)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
+    ap.add_argument("--gather", action="store_true", help="also time an RCCL gather to rank 0")
+    return ap.parse_args()
+
+
+def cpu_baseline(seconds_budget: float):
+    """The oracle (C restatement, fp32 FFT) on the host cores: render IR_test
+    block by block through the restated callback + fp32 STFT, on a bounded
+    sample of the same workload (chunks of 60 s stereo until the budget)."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import numpy as np
+    import oracle as o
+    threads = min(16, os.cpu_count() or 1)
+    chunk = SR * 60
+    plug = o.restated_plugin("IR_test")
+    done = 0
+    t0 = time.perf_counter()
+    zero = np.zeros(chunk, np.float32)
+    while True:
+        out = o.render_offline([zero, zero], CH, B, float(SR), plug)
+        for c in range(CH):
+            o.c_stft_mag_f32(out[c], N_FFT, HOP, o.WIN_HANN, K_BINS, nthreads=threads)
+        done += CH * chunk
+        el = time.perf_counter() - t0
+        if el >= seconds_budget or done >= CH * SR * 3600:
+            break
+    return {"value": done / el / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port",
+            "sample": f"{done // CH / SR:.0f} s of 48 kHz stereo, IR_test render (restated callback, "
+                      f"1 thread) + fp32 radix-2 STFT ({threads} OpenMP threads), oracle/oracle.c"}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    import dspbench as d
+
+    L = int(round(args.minutes * 60 * SR))
+    L -= L % HOP  # whole hops per rank
+    halo = N_FFT - HOP
+    # rank r owns samples [r L, (r+1) L) of an (N * minutes)-long file and
+    # reads a halo of the next rank's first 4096 samples (the last rank has none)
+    L_in = L + (halo if rank < world - 1 else 0)
+    g = torch.Generator(device=dev).manual_seed(1234 + rank)
+    x = (torch.rand((CH, L_in), device=dev, generator=g) * 2 - 1) * 0.1  # synthetic WAV
+    nb = d.num_blocks(L_in, B)
+    F = d.stft_frames(nb * B, N_FFT, HOP)
+    out = torch.empty((CH, nb * B), device=dev)
+    mag = torch.empty((CH, F, K_BINS), device=dev)
+    plugin = d.Plugin.ir_test(0.9, 0.002)
+    stream = torch.cuda.current_stream(dev)
+    soff = rank * L
+
+    def step():
+        d.render_stft(x, CH, B, float(SR), plugin, N=N_FFT, H=HOP, window=d.DSP_WIN_HANN,
+                      K=K_BINS, out=out, mag=mag, sample_offset=soff)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    lib = d.lib()
+    lib.dsp_kernel_timing(None, None, None)  # clear
+    lib.dsp_kernel_timing_enable(1)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    lib.dsp_kernel_timing_enable(0)
+    k_ms, k_n, k_bytes = C.c_double(), C.c_uint64(), C.c_uint64()
+    lib.dsp_kernel_timing(C.byref(k_ms), C.byref(k_n), C.byref(k_bytes))
+    ev_ms = ev0.elapsed_time(ev1)
+
+    step_s = max(wall, ev_ms / 1e3) / args.steps
+    t = torch.tensor([step_s], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    step_s = float(t.item())
+
+    samples_per_rank = CH * L  # owned samples (the halo is re-rendered, not counted)
+    value = samples_per_rank * world / step_s / 1e6
+
+    kernel_avg_ms = k_ms.value / max(1, k_n.value)
+    bytes_per_launch = k_bytes.value / max(1, k_n.value)
+    achieved = bytes_per_launch / (kernel_avg_ms / 1e3) / 1e9 if kernel_avg_ms > 0 else 0.0
+
+    gather_ms = None
+    if args.gather and world > 1:
+        torch.cuda.synchronize()
+        dist.barrier()
+        tg = time.perf_counter()
+        owned = out[:, :L].contiguous()
+        bufs = [torch.empty_like(owned) for _ in range(world)] if rank == 0 else None
+        dist.gather(owned, bufs, dst=0)
+        fm = mag[:, : L // HOP].contiguous()
+        mbufs = [torch.empty_like(fm) for _ in range(world)] if rank == 0 else None
+        dist.gather(fm, mbufs, dst=0)
+        torch.cuda.synchronize()
+        dist.barrier()
+        gather_ms = (time.perf_counter() - tg) * 1e3
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args.cpu_seconds)
+
+    if rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "Msamples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(step_s * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (uniform noise WAV in HBM; IR_test output is input-independent)",
+            "config": {
+                "workload": "IR_test render (B=512) + 8192-pt Hann STFT, hop 4096, 4097 bins, "
+                            f"{args.minutes:g} min of 48 kHz stereo per GPU",
+                "plugin": "IR_test (gain 0.9, step 0.002)",
+                "samples_per_gpu": samples_per_rank,
+                "frames_per_gpu": CH * F,
+                "sharding": "time-chunk per GPU, 4096-sample halo, no data-path collective",
+                "gather_ms": None if gather_ms is None else round(gather_ms, 3),
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "stft8192_kernel<render> (fused render + window + FFT + |X|)",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                "traffic": None,
+                "kernel_avg_ms": round(kernel_avg_ms, 5),
+                "algorithmic_bytes_per_launch": int(bytes_per_launch),
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

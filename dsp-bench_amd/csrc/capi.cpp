@@ -1,0 +1,776 @@
+// capi.cpp -- the extern "C" boundary of libdspbench (include/dspbench/dspbench.h).
+//
+// Validates arguments, owns the per-device constant tables (twiddles,
+// windows: the analogue of the IPP FFT spec / plan cache of dsp.cpp:84-95 and
+// IPP_FFT_Context, structs.h:170-178), maps a dsp_plugin onto a kernel and
+// launches on the caller's stream.  Fails loudly (negative status) on
+// anything it cannot run on the GPU -- there is no CPU path here.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <tuple>
+#include <vector>
+
+#include "kernels.hpp"
+
+namespace dspb {
+
+static thread_local char g_last_error[512] = "";
+
+void set_last_error(const char *fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_last_error, sizeof g_last_error, fmt, ap);
+    va_end(ap);
+}
+
+int hip_fail(hipError_t e, const char *what) {
+    set_last_error("%s: %s", what, hipGetErrorString(e));
+    return e == hipErrorOutOfMemory ? DSP_ERR_NOMEM : DSP_ERR_HIP;
+}
+
+static int invalid(const char *fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_last_error, sizeof g_last_error, fmt, ap);
+    va_end(ap);
+    return DSP_ERR_INVALID;
+}
+
+// ---------------------------------------------------------------------------
+// per-device resources
+// ---------------------------------------------------------------------------
+struct DeviceRes {
+    v2f *tw8192 = nullptr;                                    // exp(-2 pi i k / 8192)
+    std::map<std::tuple<int, uint32_t, uint32_t>, float *> windows;  // (kind, N, valid)
+    std::map<void *, std::pair<float *, size_t>> scratch;     // per stream
+};
+
+static std::mutex g_mu;
+static std::map<int, DeviceRes> g_res;
+
+static int current_device(int *dev) {
+    DSPB_HIP(hipGetDevice(dev));
+    return DSP_OK;
+}
+
+// RAII: make ex->device current for the call, restore afterwards.
+struct DeviceGuard {
+    int prev = -1;
+    int dev = -1;
+    int status = DSP_OK;
+    explicit DeviceGuard(const dsp_exec *ex) {
+        hipError_t e = hipGetDevice(&prev);
+        if (e != hipSuccess) { status = hip_fail(e, "hipGetDevice"); return; }
+        dev = prev;
+        if (ex && ex->device >= 0 && ex->device != prev) {
+            e = hipSetDevice(ex->device);
+            if (e != hipSuccess) { status = hip_fail(e, "hipSetDevice"); return; }
+            dev = ex->device;
+        }
+    }
+    ~DeviceGuard() {
+        if (prev >= 0 && dev != prev) (void)hipSetDevice(prev);
+    }
+};
+
+static int get_tw(int dev, const v2f **out) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    DeviceRes &r = g_res[dev];
+    if (!r.tw8192) {
+        std::vector<v2f> h(8192);
+        for (int k = 0; k < 8192; ++k) {
+            const double a = -2.0 * M_PI * (double)k / 8192.0;
+            h[k] = v2f{(float)std::cos(a), (float)std::sin(a)};
+        }
+        // exact zeros / ones at the quarter turns
+        h[0] = v2f{1.f, 0.f}; h[2048] = v2f{0.f, -1.f};
+        h[4096] = v2f{-1.f, 0.f}; h[6144] = v2f{0.f, 1.f};
+        DSPB_HIP(hipMalloc(&r.tw8192, sizeof(v2f) * 8192));
+        DSPB_HIP(hipMemcpy(r.tw8192, h.data(), sizeof(v2f) * 8192, hipMemcpyHostToDevice));
+    }
+    *out = r.tw8192;
+    return DSP_OK;
+}
+
+// Window of length `valid` (symmetric, ref ippsWinHamming_32f convention)
+// zero-padded to N.  Computed in double, rounded once to float.
+static int get_window(int dev, int kind, uint32_t N, uint32_t valid, const float **out) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    DeviceRes &r = g_res[dev];
+    auto key = std::make_tuple(kind, N, valid);
+    auto it = r.windows.find(key);
+    if (it != r.windows.end()) { *out = it->second; return DSP_OK; }
+    double a = 0.54, b = 0.46;
+    if (kind == DSP_WIN_HANN) { a = 0.5; b = 0.5; }
+    else if (kind == DSP_WIN_RECT) { a = 1.0; b = 0.0; }
+    std::vector<float> h(N, 0.f);
+    for (uint32_t n = 0; n < valid; ++n)
+        h[n] = valid == 1 ? 1.f
+                          : (float)(a - b * std::cos(2.0 * M_PI * (double)n / (double)(valid - 1)));
+    float *d = nullptr;
+    DSPB_HIP(hipMalloc(&d, sizeof(float) * N));
+    DSPB_HIP(hipMemcpy(d, h.data(), sizeof(float) * N, hipMemcpyHostToDevice));
+    r.windows[key] = d;
+    *out = d;
+    return DSP_OK;
+}
+
+// Stream-ordered scratch: calls on one stream are serialised by the stream,
+// so one buffer per (device, stream) is enough.
+static int get_scratch(int dev, hipStream_t s, size_t bytes, float **out) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    DeviceRes &r = g_res[dev];
+    auto &slot = r.scratch[(void *)s];
+    if (slot.second < bytes) {
+        if (slot.first) {
+            DSPB_HIP(hipStreamSynchronize(s));
+            DSPB_HIP(hipFree(slot.first));
+        }
+        slot.first = nullptr;
+        slot.second = 0;
+        DSPB_HIP(hipMalloc(&slot.first, bytes));
+        slot.second = bytes;
+    }
+    *out = slot.first;
+    return DSP_OK;
+}
+
+// ---------------------------------------------------------------------------
+// optional per-launch timing of the dominant kernel (HIP events on the
+// launch stream), read back by dsp_kernel_timing(); used by bench.py
+// ---------------------------------------------------------------------------
+struct TimedLaunch {
+    hipEvent_t start, stop;
+    uint64_t bytes;
+};
+static bool g_timing = false;
+static std::vector<TimedLaunch> g_timed;
+
+static int timing_begin(hipStream_t s, TimedLaunch *t) {
+    if (!g_timing) return DSP_OK;
+    DSPB_HIP(hipEventCreate(&t->start));
+    DSPB_HIP(hipEventCreate(&t->stop));
+    DSPB_HIP(hipEventRecord(t->start, s));
+    return DSP_OK;
+}
+
+static int timing_end(hipStream_t s, TimedLaunch *t, uint64_t bytes) {
+    if (!g_timing) return DSP_OK;
+    DSPB_HIP(hipEventRecord(t->stop, s));
+    t->bytes = bytes;
+    std::lock_guard<std::mutex> lk(g_mu);
+    g_timed.push_back(*t);
+    return DSP_OK;
+}
+
+static bool is_pow2(uint64_t n) { return n && !(n & (n - 1)); }
+static uint32_t ilog2(uint64_t n) { uint32_t l = 0; while ((1ull << l) < n) ++l; return l; }
+static bool aligned(const void *p, size_t a) { return ((uintptr_t)p % a) == 0; }
+
+// ---------------------------------------------------------------------------
+// plugin -> sample map
+// ---------------------------------------------------------------------------
+static int plugin_map(const dsp_plugin *p, uint32_t B, int dev, hipStream_t s, SampleMap *m) {
+    m->kind = MapKind::Noop;
+    m->a = 1.f;
+    m->table = nullptr;
+    m->B = B;
+    m->b_mask = is_pow2(B) ? B - 1 : 0;
+    if (!p) return DSP_OK;  // no plugin loaded: the file plays through (audio.cpp:144)
+    float v0 = 0.f, v1 = 0.f;
+    switch (p->kind) {
+    case DSP_PLUGIN_NOOP:
+        return DSP_OK;
+    case DSP_PLUGIN_GAIN:  // build/gain_test.cpp: Parameters{float gain}
+        if (!p->params || p->params_size < 4) return invalid("GAIN plugin needs a 4-byte params blob");
+        std::memcpy(&v0, p->params, 4);
+        m->kind = MapKind::Gain;
+        m->a = v0;
+        return DSP_OK;
+    case DSP_PLUGIN_STATIC_GAIN:  // test/static_gain_plugin.cpp: State{float gain}
+        if (!p->state || p->state_size < 4) return invalid("STATIC_GAIN plugin needs a 4-byte state blob");
+        std::memcpy(&v0, p->state, 4);
+        m->kind = MapKind::Gain;
+        m->a = v0;
+        return DSP_OK;
+    case DSP_PLUGIN_IR_RAMP: {  // build/IR_test.cpp: Parameters{float gain; float step}
+        if (!p->params || p->params_size < 8) return invalid("IR_RAMP plugin needs an 8-byte params blob");
+        std::memcpy(&v0, p->params, 4);
+        std::memcpy(&v1, (const char *)p->params + 4, 4);
+        float *table = nullptr;
+        int st = get_scratch(dev, s, sizeof(float) * B, &table);
+        if (st) return st;
+        st = launch_ramp_table(table, B, v0, v1, s);
+        if (st) return st;
+        m->kind = MapKind::Ramp;
+        m->table = table;
+        return DSP_OK;
+    }
+    case DSP_PLUGIN_GENERIC:
+        set_last_error("DSP_PLUGIN_GENERIC: generic GPU dispatch is not in this build");
+        return DSP_ERR_UNSUPPORTED;
+    default:
+        return invalid("unknown plugin kind %d", p->kind);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// host-buffer staging (DSP_EXEC_HOST_BUFFERS)
+// ---------------------------------------------------------------------------
+struct Staged {
+    std::vector<float *> dev;
+    ~Staged() {
+        for (float *p : dev)
+            if (p) (void)hipFree(p);
+    }
+    int alloc(size_t n_floats, float **out) {
+        float *p = nullptr;
+        if (n_floats == 0) n_floats = 1;
+        DSPB_HIP(hipMalloc(&p, n_floats * sizeof(float)));
+        dev.push_back(p);
+        *out = p;
+        return DSP_OK;
+    }
+};
+
+static hipStream_t stream_of(const dsp_exec *ex) { return ex ? (hipStream_t)ex->stream : nullptr; }
+static bool host_mode(const dsp_exec *ex) { return ex && (ex->flags & DSP_EXEC_HOST_BUFFERS); }
+static uint64_t goff_of(const dsp_exec *ex) { return ex ? ex->sample_offset : 0; }
+
+static int finish(const dsp_exec *ex) {
+    if (ex && (ex->flags & (DSP_EXEC_SYNC | DSP_EXEC_HOST_BUFFERS)))
+        DSPB_HIP(hipStreamSynchronize(stream_of(ex)));
+    return DSP_OK;
+}
+
+// ---------------------------------------------------------------------------
+// core device-pointer implementations
+// ---------------------------------------------------------------------------
+static int render_device(const float *const *in, uint32_t in_ch, uint64_t L, float *const *out,
+                         uint32_t C, uint32_t B, const SampleMap &map, uint64_t start,
+                         uint64_t goff, hipStream_t s) {
+    const uint64_t nblocks = (L + B - 1) / B;
+    const uint64_t end = nblocks * B;
+    for (uint32_t c0 = 0; c0 < C; c0 += kMaxChannels) {
+        const uint32_t cn = (C - c0) < (uint32_t)kMaxChannels ? (C - c0) : kMaxChannels;
+        RenderArgs A{};
+        bool vec = (start % 4) == 0;
+        A.in_ch = 0;
+        for (uint32_t j = 0; j < cn; ++j) {
+            A.out.p[j] = out[c0 + j];
+            vec = vec && aligned(out[c0 + j], 16);
+            if (c0 + j < in_ch) {
+                A.in.p[j] = in[c0 + j];
+                A.in_ch = j + 1;
+                vec = vec && aligned(in[c0 + j], 16);
+            }
+        }
+        A.L = L;
+        A.start = start;
+        A.end = end;
+        A.map = map;
+        A.goff = goff;
+        int st = launch_render(A, cn, vec, s);
+        if (st) return st;
+    }
+    return DSP_OK;
+}
+
+static int check_stft_args(uint32_t N, uint32_t H, uint32_t K, uint64_t ld) {
+    if (!is_pow2(N) || N < 4 || N > 8192) return invalid("N=%u must be a power of two in [4, 8192]", N);
+    if (H == 0) return invalid("hop H must be > 0");
+    if (K == 0 || (K > N / 2 + 1 && K != N)) return invalid("K=%u must be <= N/2+1 or == N", K);
+    if (ld < K) return invalid("ld=%llu < K=%u", (unsigned long long)ld, K);
+    return DSP_OK;
+}
+
+static int stft_device(const float *const *in, uint32_t C, uint64_t L, uint32_t N, uint32_t H,
+                       int window, uint32_t K, float *const *mag, uint64_t ld, int dev,
+                       hipStream_t s) {
+    const uint64_t F = dsp_stft_frame_count(L, N, H);
+    if (F == 0) return DSP_OK;
+    const v2f *tw = nullptr;
+    const float *win = nullptr;
+    int st = get_tw(dev, &tw);
+    if (st) return st;
+    st = get_window(dev, window, N, N, &win);
+    if (st) return st;
+    bool fast = (N == 8192) && (H % 2 == 0);
+    for (uint32_t c = 0; c < C; ++c) fast = fast && aligned(in[c], 8);
+    for (uint32_t c0 = 0; c0 < C; c0 += kMaxChannels) {
+        const uint32_t cn = (C - c0) < (uint32_t)kMaxChannels ? (C - c0) : kMaxChannels;
+        if (fast) {
+            Stft8kArgs A{};
+            for (uint32_t j = 0; j < cn; ++j) {
+                A.in.p[j] = in[c0 + j];
+                A.mag.p[j] = mag[c0 + j];
+            }
+            A.in_ch = cn;
+            A.L = L;
+            A.F = F;
+            A.H = H;
+            A.K = K;
+            A.ld = ld;
+            A.valid = N;
+            A.win2 = reinterpret_cast<const v2f *>(win);
+            A.tw = tw;
+            A.scale = (float)(1.0 / std::sqrt((double)N));
+            TimedLaunch tl{};
+            if ((st = timing_begin(s, &tl))) return st;
+            st = launch_stft8192(A, cn, false, true, s);
+            if (st) return st;
+            // algorithmic bytes: frame input read once per hop + magnitudes
+            st = timing_end(s, &tl, (uint64_t)cn * F * ((uint64_t)H * 4 + (uint64_t)K * 4));
+        } else {
+            GenericFftArgs A{};
+            for (uint32_t j = 0; j < cn; ++j) {
+                A.sig.p[j] = in[c0 + j];
+                A.mag.p[j] = mag[c0 + j];
+            }
+            A.frame_hop = H;
+            A.valid = N;
+            A.win = win;
+            A.n = N;
+            A.log2n = ilog2(N);
+            A.dir = -1;
+            A.tw = tw;
+            A.scale = (float)(1.0 / std::sqrt((double)N));
+            A.K = K;
+            A.ld = ld;
+            A.mode = 2;
+            st = launch_fft_generic(A, F, cn, s);
+        }
+        if (st) return st;
+    }
+    return DSP_OK;
+}
+
+}  // namespace dspb
+
+using namespace dspb;
+
+// ===========================================================================
+// extern "C"
+// ===========================================================================
+extern "C" {
+
+int dsp_abi_version(void) { return DSPBENCH_ABI_VERSION; }
+
+void dsp_kernel_timing_enable(int on) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    g_timing = on != 0;
+}
+
+int dsp_kernel_timing(double *total_ms, uint64_t *launches, uint64_t *bytes) {
+    std::vector<TimedLaunch> v;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        v.swap(g_timed);
+    }
+    double ms = 0.0;
+    uint64_t b = 0;
+    for (auto &t : v) {
+        float e = 0.f;
+        DSPB_HIP(hipEventSynchronize(t.stop));
+        DSPB_HIP(hipEventElapsedTime(&e, t.start, t.stop));
+        ms += e;
+        b += t.bytes;
+        (void)hipEventDestroy(t.start);
+        (void)hipEventDestroy(t.stop);
+    }
+    if (total_ms) *total_ms = ms;
+    if (launches) *launches = v.size();
+    if (bytes) *bytes = b;
+    return DSP_OK;
+}
+
+const char *dsp_last_error(void) { return g_last_error; }
+
+const char *dsp_status_string(int s) {
+    switch (s) {
+    case DSP_OK: return "ok";
+    case DSP_ERR_INVALID: return "invalid argument";
+    case DSP_ERR_HIP: return "HIP runtime error";
+    case DSP_ERR_UNSUPPORTED: return "unsupported";
+    case DSP_ERR_NOMEM: return "out of device memory";
+    case DSP_ERR_NO_DEVICE: return "no device";
+    default: return "unknown status";
+    }
+}
+
+int dsp_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+uint64_t dsp_stft_frame_count(uint64_t L, uint32_t N, uint32_t H) {
+    if (N == 0 || H == 0 || L < N) return 0;
+    return (L - N) / H + 1;
+}
+
+int dsp_render_offline(const float *const *in, uint32_t in_channels, uint64_t L,
+                       float *const *out, uint32_t C, uint32_t B, float sr,
+                       const dsp_plugin *plugin, const dsp_exec *ex) {
+    (void)sr;  // none of the map kernels reads the sample rate
+    if (B == 0) return invalid("block size B must be > 0");
+    if (C == 0) return DSP_OK;
+    if (!out) return invalid("out is NULL");
+    for (uint32_t c = 0; c < C; ++c)
+        if (!out[c]) return invalid("out[%u] is NULL", c);
+    if (in_channels && !in) return invalid("in is NULL");
+    for (uint32_t c = 0; c < in_channels; ++c)
+        if (!in[c]) return invalid("in[%u] is NULL", c);
+    if (ex && ex->sample_offset % B) return invalid("sample_offset must be a multiple of B");
+    DeviceGuard g(ex);
+    if (g.status) return g.status;
+    hipStream_t s = stream_of(ex);
+    const uint64_t nblocks = (L + B - 1) / B;
+    const uint64_t Lr = nblocks * B;
+
+    std::vector<const float *> din(in_channels);
+    std::vector<float *> dout(C);
+    Staged stage;
+    if (host_mode(ex)) {
+        for (uint32_t c = 0; c < in_channels; ++c) {
+            float *d;
+            int st = stage.alloc(L, &d);
+            if (st) return st;
+            DSPB_HIP(hipMemcpyAsync(d, in[c], L * sizeof(float), hipMemcpyHostToDevice, s));
+            din[c] = d;
+        }
+        for (uint32_t c = 0; c < C; ++c) {
+            int st = stage.alloc(Lr, &dout[c]);
+            if (st) return st;
+        }
+    } else {
+        for (uint32_t c = 0; c < in_channels; ++c) din[c] = in[c];
+        for (uint32_t c = 0; c < C; ++c) dout[c] = out[c];
+    }
+    SampleMap map;
+    int st = plugin_map(plugin, B, g.dev, s, &map);
+    if (st) return st;
+    st = render_device(din.data(), in_channels, L, dout.data(), C, B, map, 0, goff_of(ex), s);
+    if (st) return st;
+    if (host_mode(ex))
+        for (uint32_t c = 0; c < C; ++c)
+            DSPB_HIP(hipMemcpyAsync(out[c], dout[c], Lr * sizeof(float), hipMemcpyDeviceToHost, s));
+    return finish(ex);
+}
+
+int dsp_stft_magnitude(const float *const *in, uint32_t C, uint64_t L, uint32_t N, uint32_t H,
+                       int32_t window, uint32_t K, float *const *mag, uint64_t ld,
+                       const dsp_exec *ex) {
+    int st = check_stft_args(N, H, K, ld);
+    if (st) return st;
+    if (C == 0) return DSP_OK;
+    if (!in || !mag) return invalid("in / mag is NULL");
+    for (uint32_t c = 0; c < C; ++c)
+        if (!in[c] || !mag[c]) return invalid("in[%u] / mag[%u] is NULL", c, c);
+    DeviceGuard g(ex);
+    if (g.status) return g.status;
+    hipStream_t s = stream_of(ex);
+    const uint64_t F = dsp_stft_frame_count(L, N, H);
+    std::vector<const float *> din(C);
+    std::vector<float *> dmag(C);
+    Staged stage;
+    if (host_mode(ex)) {
+        for (uint32_t c = 0; c < C; ++c) {
+            float *d;
+            if ((st = stage.alloc(L, &d))) return st;
+            DSPB_HIP(hipMemcpyAsync(d, in[c], L * sizeof(float), hipMemcpyHostToDevice, s));
+            din[c] = d;
+            if ((st = stage.alloc(F * ld, &dmag[c]))) return st;
+        }
+    } else {
+        for (uint32_t c = 0; c < C; ++c) { din[c] = in[c]; dmag[c] = mag[c]; }
+    }
+    st = stft_device(din.data(), C, L, N, H, window, K, dmag.data(), ld, g.dev, s);
+    if (st) return st;
+    if (host_mode(ex) && F)
+        for (uint32_t c = 0; c < C; ++c)
+            DSPB_HIP(hipMemcpyAsync(mag[c], dmag[c], F * ld * sizeof(float), hipMemcpyDeviceToHost, s));
+    return finish(ex);
+}
+
+int dsp_render_stft(const float *const *in, uint32_t in_channels, uint64_t L,
+                    float *const *out, uint32_t C, uint32_t B, float sr,
+                    const dsp_plugin *plugin, uint32_t N, uint32_t H, int32_t window,
+                    uint32_t K, float *const *mag, uint64_t ld, const dsp_exec *ex) {
+    (void)sr;
+    if (B == 0) return invalid("block size B must be > 0");
+    int st = check_stft_args(N, H, K, ld);
+    if (st) return st;
+    if (C == 0) return DSP_OK;
+    if (!out || !mag) return invalid("out / mag is NULL");
+    for (uint32_t c = 0; c < C; ++c)
+        if (!out[c] || !mag[c]) return invalid("out[%u] / mag[%u] is NULL", c, c);
+    if (in_channels && !in) return invalid("in is NULL");
+    for (uint32_t c = 0; c < in_channels; ++c)
+        if (!in[c]) return invalid("in[%u] is NULL", c);
+    if (ex && ex->sample_offset % B) return invalid("sample_offset must be a multiple of B");
+    DeviceGuard g(ex);
+    if (g.status) return g.status;
+    hipStream_t s = stream_of(ex);
+    const uint64_t nblocks = (L + B - 1) / B;
+    const uint64_t Lr = nblocks * B;
+    const uint64_t F = dsp_stft_frame_count(Lr, N, H);
+
+    std::vector<const float *> din(in_channels);
+    std::vector<float *> dout(C), dmag(C);
+    Staged stage;
+    if (host_mode(ex)) {
+        for (uint32_t c = 0; c < in_channels; ++c) {
+            float *d;
+            if ((st = stage.alloc(L, &d))) return st;
+            DSPB_HIP(hipMemcpyAsync(d, in[c], L * sizeof(float), hipMemcpyHostToDevice, s));
+            din[c] = d;
+        }
+        for (uint32_t c = 0; c < C; ++c) {
+            if ((st = stage.alloc(Lr, &dout[c]))) return st;
+            if ((st = stage.alloc(F * ld, &dmag[c]))) return st;
+        }
+    } else {
+        for (uint32_t c = 0; c < in_channels; ++c) din[c] = in[c];
+        for (uint32_t c = 0; c < C; ++c) { dout[c] = out[c]; dmag[c] = mag[c]; }
+    }
+    SampleMap map;
+    if ((st = plugin_map(plugin, B, g.dev, s, &map))) return st;
+    const uint64_t goff = goff_of(ex);
+
+    bool fused = (N == 8192) && (H % 128 == 0) && (H <= N) && (goff % 2 == 0) && F > 0;
+    for (uint32_t c = 0; c < C; ++c) fused = fused && aligned(dout[c], 8);
+    for (uint32_t c = 0; c < in_channels; ++c) fused = fused && aligned(din[c], 8);
+
+    if (!fused) {
+        st = render_device(din.data(), in_channels, L, dout.data(), C, B, map, 0, goff, s);
+        if (st) return st;
+        st = stft_device(dout.data(), C, Lr, N, H, window, K, dmag.data(), ld, g.dev, s);
+        if (st) return st;
+    } else {
+        const v2f *tw = nullptr;
+        const float *win = nullptr;
+        if ((st = get_tw(g.dev, &tw))) return st;
+        if ((st = get_window(g.dev, window, N, N, &win))) return st;
+        for (uint32_t c0 = 0; c0 < C; c0 += kMaxChannels) {
+            const uint32_t cn = (C - c0) < (uint32_t)kMaxChannels ? (C - c0) : kMaxChannels;
+            Stft8kArgs A{};
+            A.in_ch = 0;
+            for (uint32_t j = 0; j < cn; ++j) {
+                A.out.p[j] = dout[c0 + j];
+                A.mag.p[j] = dmag[c0 + j];
+                if (c0 + j < in_channels) {
+                    A.in.p[j] = din[c0 + j];
+                    A.in_ch = j + 1;
+                }
+            }
+            A.L = L;
+            A.F = F;
+            A.H = H;
+            A.K = K;
+            A.ld = ld;
+            A.valid = N;
+            A.win2 = reinterpret_cast<const v2f *>(win);
+            A.tw = tw;
+            A.scale = (float)(1.0 / std::sqrt((double)N));
+            A.map = map;
+            A.goff = goff;
+            TimedLaunch tl{};
+            if ((st = timing_begin(s, &tl))) return st;
+            if ((st = launch_stft8192(A, cn, true, true, s))) return st;
+            // algorithmic bytes: render write 4 B + magnitudes 4 K/H B
+            // per hop sample, plus the file read when the map uses its input
+            const uint64_t hop_samples = (uint64_t)cn * F * H;
+            uint64_t bytes = hop_samples * 4 + (uint64_t)cn * F * K * 4;
+            if (map.kind != MapKind::Ramp) bytes += (uint64_t)A.in_ch * F * H * 4;
+            if ((st = timing_end(s, &tl, bytes))) return st;
+        }
+        // the render tail no frame owns: [F*H, Lr)
+        st = render_device(din.data(), in_channels, L, dout.data(), C, B, map, F * (uint64_t)H,
+                           goff, s);
+        if (st) return st;
+    }
+    if (host_mode(ex)) {
+        for (uint32_t c = 0; c < C; ++c) {
+            DSPB_HIP(hipMemcpyAsync(out[c], dout[c], Lr * sizeof(float), hipMemcpyDeviceToHost, s));
+            if (F)
+                DSPB_HIP(hipMemcpyAsync(mag[c], dmag[c], F * ld * sizeof(float),
+                                        hipMemcpyDeviceToHost, s));
+        }
+    }
+    return finish(ex);
+}
+
+int dsp_ir_analysis(const dsp_plugin *plugin, uint32_t C, float sr, uint32_t ir_len,
+                    float *const *ir_out, float *mag, const dsp_exec *ex) {
+    (void)sr;
+    if (C == 0 || ir_len == 0) return invalid("C and ir_len must be > 0");
+    if (!is_pow2(ir_len) || 4ull * ir_len > 8192) return invalid("4*ir_len must be a power of two <= 8192");
+    if (!ir_out || !mag) return invalid("ir_out / mag is NULL");
+    for (uint32_t c = 0; c < C; ++c)
+        if (!ir_out[c]) return invalid("ir_out[%u] is NULL", c);
+    DeviceGuard g(ex);
+    if (g.status) return g.status;
+    hipStream_t s = stream_of(ex);
+    const uint32_t n = 4 * ir_len;
+    std::vector<float *> dir(C);
+    float *dmag = mag;
+    Staged stage;
+    int st;
+    if (host_mode(ex)) {
+        for (uint32_t c = 0; c < C; ++c)
+            if ((st = stage.alloc(ir_len, &dir[c]))) return st;
+        if ((st = stage.alloc(n, &dmag))) return st;
+    } else {
+        for (uint32_t c = 0; c < C; ++c) dir[c] = ir_out[c];
+    }
+    // compute_IR (plugin.cpp:27-34): IR[c] = delta, then one callback of ir_len
+    static const float one = 1.0f;
+    for (uint32_t c = 0; c < C; ++c) {
+        DSPB_HIP(hipMemsetAsync(dir[c], 0, ir_len * sizeof(float), s));
+        DSPB_HIP(hipMemcpyAsync(dir[c], &one, sizeof(float), hipMemcpyHostToDevice, s));
+    }
+    SampleMap map;
+    if ((st = plugin_map(plugin, ir_len, g.dev, s, &map))) return st;
+    std::vector<const float *> cin(dir.begin(), dir.end());
+    if ((st = render_device(cin.data(), C, ir_len, dir.data(), C, ir_len, map, 0, 0, s))) return st;
+
+    // fft_perform_and_get_magnitude (dsp.cpp:53-66): channel 0 only
+    const v2f *tw = nullptr;
+    const float *win = nullptr;
+    if ((st = get_tw(g.dev, &tw))) return st;
+    if ((st = get_window(g.dev, DSP_WIN_HAMMING, n, ir_len, &win))) return st;
+    if (n == 8192 && aligned(dir[0], 8)) {
+        Stft8kArgs A{};
+        A.in.p[0] = dir[0];
+        A.in_ch = 1;
+        A.L = ir_len;
+        A.mag.p[0] = dmag;
+        A.F = 1;
+        A.H = n;
+        A.K = n;  // all bins, as the reference stores them (dsp.cpp:65)
+        A.ld = n;
+        A.valid = ir_len;
+        A.win2 = reinterpret_cast<const v2f *>(win);
+        A.tw = tw;
+        A.scale = (float)(1.0 / std::sqrt((double)n));
+        if ((st = launch_stft8192(A, 1, false, false, s))) return st;
+    } else {
+        GenericFftArgs A{};
+        A.sig.p[0] = dir[0];
+        A.frame_hop = 0;
+        A.valid = ir_len;
+        A.win = win;
+        A.n = n;
+        A.log2n = ilog2(n);
+        A.dir = -1;
+        A.tw = tw;
+        A.scale = (float)(1.0 / std::sqrt((double)n));
+        A.mag.p[0] = dmag;
+        A.K = n;
+        A.ld = n;
+        A.mode = 2;
+        if ((st = launch_fft_generic(A, 1, 1, s))) return st;
+    }
+    if (host_mode(ex)) {
+        for (uint32_t c = 0; c < C; ++c)
+            DSPB_HIP(hipMemcpyAsync(ir_out[c], dir[c], ir_len * sizeof(float), hipMemcpyDeviceToHost, s));
+        DSPB_HIP(hipMemcpyAsync(mag, dmag, n * sizeof(float), hipMemcpyDeviceToHost, s));
+    }
+    return finish(ex);
+}
+
+static int fft_service(const float *re_in, const float *im_in, float *re_out, float *im_out,
+                       uint32_t n, int dir, const dsp_exec *ex) {
+    if (!is_pow2(n) || n < 2 || n > 8192) return invalid("n=%u must be a power of two in [2, 8192]", n);
+    DeviceGuard g(ex);
+    if (g.status) return g.status;
+    hipStream_t s = stream_of(ex);
+    const v2f *tw = nullptr;
+    int st = get_tw(g.dev, &tw);
+    if (st) return st;
+    Staged stage;
+    const float *dre = re_in, *dim = im_in;
+    float *dro = re_out, *dio = im_out;
+    if (host_mode(ex)) {
+        float *a, *b;
+        if ((st = stage.alloc(n, &a))) return st;
+        DSPB_HIP(hipMemcpyAsync(a, re_in, n * sizeof(float), hipMemcpyHostToDevice, s));
+        dre = a;
+        if (im_in) {
+            if ((st = stage.alloc(n, &b))) return st;
+            DSPB_HIP(hipMemcpyAsync(b, im_in, n * sizeof(float), hipMemcpyHostToDevice, s));
+            dim = b;
+        }
+        if ((st = stage.alloc(n, &dro))) return st;
+        if (im_out && (st = stage.alloc(n, &dio))) return st;
+    }
+    GenericFftArgs A{};
+    A.re_in = dre;
+    A.im_in = dim;
+    A.n = n;
+    A.log2n = ilog2(n);
+    A.dir = dir;
+    A.tw = tw;
+    A.scale = (float)(1.0 / std::sqrt((double)n));
+    A.re_out = dro;
+    A.im_out = dio;
+    A.mode = im_out ? 0 : 1;
+    if ((st = launch_fft_generic(A, 1, 1, s))) return st;
+    if (host_mode(ex)) {
+        DSPB_HIP(hipMemcpyAsync(re_out, dro, n * sizeof(float), hipMemcpyDeviceToHost, s));
+        if (im_out)
+            DSPB_HIP(hipMemcpyAsync(im_out, dio, n * sizeof(float), hipMemcpyDeviceToHost, s));
+    }
+    return finish(ex);
+}
+
+int dsp_fft_forward(const float *in, float *re, float *im, uint32_t n, const dsp_exec *ex) {
+    if (!in || !re || !im) return invalid("fft_forward: NULL buffer");
+    return fft_service(in, nullptr, re, im, n, -1, ex);
+}
+
+int dsp_fft_reverse(const float *re, const float *im, float *out, uint32_t n, const dsp_exec *ex) {
+    if (!re || !im || !out) return invalid("fft_reverse: NULL buffer");
+    return fft_service(re, im, out, nullptr, n, +1, ex);
+}
+
+int dsp_gain(const float *in, float *out, float gain, uint64_t n, const dsp_exec *ex) {
+    if (!in || !out) return invalid("NULL buffer");
+    DeviceGuard g(ex);
+    if (g.status) return g.status;
+    int st = launch_gain(in, out, gain, n, stream_of(ex));
+    return st ? st : finish(ex);
+}
+
+int dsp_copy(const float *in, float *out, uint64_t n, const dsp_exec *ex) {
+    if (!in || !out) return invalid("NULL buffer");
+    DeviceGuard g(ex);
+    if (g.status) return g.status;
+    DSPB_HIP(hipMemcpyAsync(out, in, n * sizeof(float), hipMemcpyDeviceToDevice, stream_of(ex)));
+    return finish(ex);
+}
+
+int dsp_set(float value, float *out, uint64_t n, const dsp_exec *ex) {
+    if (!out) return invalid("NULL buffer");
+    DeviceGuard g(ex);
+    if (g.status) return g.status;
+    int st = launch_set(value, out, n, stream_of(ex));
+    return st ? st : finish(ex);
+}
+
+int dsp_magnitude(const float *re, const float *im, float *out, uint64_t n, const dsp_exec *ex) {
+    if (!re || !im || !out) return invalid("NULL buffer");
+    DeviceGuard g(ex);
+    if (g.status) return g.status;
+    int st = launch_magnitude(re, im, out, n, stream_of(ex));
+    return st ? st : finish(ex);
+}
+
+}  // extern "C"

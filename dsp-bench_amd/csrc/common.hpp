@@ -1,0 +1,63 @@
+// common.hpp -- shared definitions for the CDNA4 kernels of libdspbench.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "dspbench/dspbench.h"
+
+namespace dspb {
+
+constexpr int kMaxChannels = 16;  // channels per launch; the C ABI loops above this
+
+// Channel pointer tables passed by value as kernel arguments.
+struct ChanIn {
+    const float *p[kMaxChannels];
+};
+struct ChanOut {
+    float *p[kMaxChannels];
+};
+
+// Per-sample plugin maps that the render / fused kernels specialise on.
+// `table` is the IR_test ramp (B floats) computed on the device by
+// ramp_table_kernel; the others use the scalar `a`.
+enum class MapKind : int { Noop = 0, Gain = 1, Ramp = 3 };
+
+struct SampleMap {
+    MapKind kind;
+    float a;             // gain (Gain)
+    const float *table;  // ramp table (Ramp)
+    uint32_t B;          // block size
+    uint32_t b_mask;     // B - 1 when B is a power of two, else 0
+};
+
+__device__ __forceinline__ uint32_t block_pos(const SampleMap &m, uint64_t gi) {
+    return m.b_mask ? (uint32_t)(gi & m.b_mask) : (uint32_t)(gi % m.B);
+}
+
+// out = callback(file sample) for one sample at global index gi.
+// `base` is already 0 past EOF / for channels the file lacks.
+__device__ __forceinline__ float apply_map(const SampleMap &m, float base, uint64_t gi) {
+    switch (m.kind) {
+    case MapKind::Gain:
+        return base * m.a;  // single fp32 multiply: bit-exact vs gain_test
+    case MapKind::Ramp:
+        return m.table[block_pos(m, gi)];
+    default:
+        return base;
+    }
+}
+
+}  // namespace dspb
+
+// Host-side error plumbing shared by the C ABI translation units.
+namespace dspb {
+void set_last_error(const char *fmt, ...);
+int hip_fail(hipError_t e, const char *what);
+}  // namespace dspb
+
+#define DSPB_HIP(call)                                                 \
+    do {                                                               \
+        hipError_t _e = (call);                                        \
+        if (_e != hipSuccess) return ::dspb::hip_fail(_e, #call);      \
+    } while (0)

@@ -1,0 +1,68 @@
+// kernels.hpp -- kernel argument blocks and launchers shared by the HIP
+// translation units and the C ABI (capi.cpp).
+#pragma once
+#include "common.hpp"
+
+namespace dspb {
+
+typedef float v2f __attribute__((ext_vector_type(2)));
+
+struct RenderArgs {
+    ChanIn in;
+    uint32_t in_ch;
+    uint64_t L;      // file samples available from in[c][0]
+    ChanOut out;
+    uint64_t start;  // first local sample to render
+    uint64_t end;    // one past the last (nblocks * B)
+    SampleMap map;
+    uint64_t goff;   // global index of local sample 0
+};
+
+struct Stft8kArgs {
+    ChanIn in;           // signal (memory source) or WAV file (fused)
+    uint32_t in_ch;      // channels present in `in`
+    uint64_t L;          // valid samples in in[c] (file length when fused)
+    ChanOut out;         // fused: render output
+    ChanOut mag;         // magnitudes, row f at mag[c] + f * ld
+    uint64_t F;          // frames per channel
+    uint32_t H;          // hop
+    uint32_t K;          // bins stored (<= 4097, or 8192 = mirrored all-bins)
+    uint64_t ld;         // row stride of mag
+    uint32_t valid;      // samples of a frame that exist (8192, or IR length)
+    const v2f *win2;     // window as 4096 float2 (w[2m], w[2m+1]), zero past valid
+    const v2f *tw;       // T8192[k] = exp(-2 pi i k / 8192), k < 8192
+    float scale;         // 1 / sqrt(8192)
+    SampleMap map;       // fused render map
+    uint64_t goff;       // global sample index of in[c][0] / out[c][0]
+};
+
+struct GenericFftArgs {
+    // input: either split complex (re, im[may be null]) or real frames
+    const float *re_in;
+    const float *im_in;
+    ChanIn sig;          // real frames: signal channels (STFT / IR)
+    uint64_t frame_hop;  // samples between frames
+    uint32_t valid;      // samples per frame that exist (zero beyond)
+    const float *win;    // window (n floats, may be null)
+    uint32_t n, log2n;
+    int dir;             // -1 forward, +1 inverse
+    const v2f *tw;       // T8192
+    float scale;
+    // output: split complex, real part only, or magnitude rows
+    float *re_out;
+    float *im_out;
+    ChanOut mag;
+    uint32_t K;
+    uint64_t ld;
+    int mode;  // 0: complex->complex, 1: complex->real part, 2: frames->mag
+};
+
+int launch_ramp_table(float *table, uint32_t B, float gain, float step, hipStream_t s);
+int launch_render(const RenderArgs &A, uint32_t C, bool vec, hipStream_t s);
+int launch_stft8192(const Stft8kArgs &A, uint32_t C, bool fused, bool full, hipStream_t s);
+int launch_fft_generic(const GenericFftArgs &A, uint64_t transforms, uint32_t C, hipStream_t s);
+int launch_gain(const float *in, float *out, float g, uint64_t n, hipStream_t s);
+int launch_set(float v, float *out, uint64_t n, hipStream_t s);
+int launch_magnitude(const float *re, const float *im, float *out, uint64_t n, hipStream_t s);
+
+}  // namespace dspb

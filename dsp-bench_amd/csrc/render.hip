@@ -1,0 +1,183 @@
+// render.hip -- CDNA4 kernels for the offline block render.
+//
+// Replaces the per-block render loop of the reference: render_audio
+// (audio.cpp:13-175) pumped in whole blocks of B samples
+// (wasapi_audio.cpp:223-251) with the plugin's audio_callback applied in
+// place (audio.cpp:160-165).
+//
+// The offline render of an L-sample file is nblocks = ceil(L/B) blocks; the
+// block semantics collapse to a per-sample rule for every sample i of the
+// padded render [0, nblocks*B):
+//
+//     base[c][i] = (c < file_channels && i < L) ? file[c][i] : 0.0f
+//     out[c][i]  = callback(base)[c][i]
+//
+// For the stock plugins whose callback is a per-sample map that rule is one
+// streaming kernel: 16-byte loads and stores, four float4 per thread in
+// flight, grid-stride over a capped grid (HBM-bound, no reuse to tile for).
+//
+// IR_test's callback is a sequential double recurrence that restarts at
+// every block (build/IR_test.cpp:47-58), so its output is input-independent
+// and B-periodic.  ramp_table_kernel runs that recurrence on the device,
+// exactly as written (one lane, B dependent f64 subtractions), and the
+// render broadcasts the B-entry table: 4 B/sample of HBM writes, no reads.
+#include "kernels.hpp"
+
+namespace dspb {
+
+__global__ void ramp_table_kernel(float *table, uint32_t B, float gain, float step) {
+    if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    double g = (double)gain;         // double gain = param.gain;
+    const double s = (double)step;   // gain -= param.step (float promoted)
+    for (uint32_t i = 0; i < B; ++i) {
+        table[i] = (float)g;         // out_buffer[channel][sample] = gain;
+        g = g - s;
+    }
+}
+
+
+template <MapKind K>
+__device__ __forceinline__ float4 render4(const RenderArgs &A, const float *x, uint64_t i) {
+    float4 b = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (K != MapKind::Ramp && x != nullptr) {
+        if (i + 4 <= A.L) {
+            b = *reinterpret_cast<const float4 *>(x + i);
+        } else {
+            if (i + 0 < A.L) b.x = x[i + 0];
+            if (i + 1 < A.L) b.y = x[i + 1];
+            if (i + 2 < A.L) b.z = x[i + 2];
+        }
+    }
+    if (K == MapKind::Noop) return b;
+    SampleMap m = A.map;
+    m.kind = K;
+    const uint64_t g = A.goff + i;
+    return make_float4(apply_map(m, b.x, g), apply_map(m, b.y, g + 1),
+                       apply_map(m, b.z, g + 2), apply_map(m, b.w, g + 3));
+}
+
+// Vector path: start % 4 == 0 and every pointer 16-byte aligned.
+template <MapKind K>
+__global__ __launch_bounds__(256) void render_vec_kernel(RenderArgs A) {
+    constexpr int U = 4;
+    const uint32_t c = blockIdx.y;
+    const float *x = (c < A.in_ch) ? A.in.p[c] : nullptr;
+    float *o = A.out.p[c];
+    const uint64_t n4 = (A.end - A.start) >> 2;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; q + (U - 1) * stride < n4; q += U * stride) {
+        float4 r[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) r[u] = render4<K>(A, x, A.start + 4 * (q + u * stride));
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            *reinterpret_cast<float4 *>(o + A.start + 4 * (q + u * stride)) = r[u];
+    }
+    for (; q < n4; q += stride)
+        *reinterpret_cast<float4 *>(o + A.start + 4 * q) = render4<K>(A, x, A.start + 4 * q);
+    // scalar tail (end - start not a multiple of 4)
+    if (blockIdx.x == 0 && threadIdx.x < ((A.end - A.start) & 3)) {
+        const uint64_t i = A.start + 4 * n4 + threadIdx.x;
+        const float b = (K != MapKind::Ramp && x != nullptr && i < A.L) ? x[i] : 0.f;
+        SampleMap m = A.map;
+        m.kind = K;
+        o[i] = apply_map(m, b, A.goff + i);
+    }
+}
+
+// Scalar path for unaligned pointers or odd starts.
+template <MapKind K>
+__global__ __launch_bounds__(256) void render_scalar_kernel(RenderArgs A) {
+    const uint32_t c = blockIdx.y;
+    const float *x = (c < A.in_ch) ? A.in.p[c] : nullptr;
+    float *o = A.out.p[c];
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    SampleMap m = A.map;
+    m.kind = K;
+    for (uint64_t i = A.start + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < A.end;
+         i += stride) {
+        const float b = (K != MapKind::Ramp && x != nullptr && i < A.L) ? x[i] : 0.f;
+        o[i] = apply_map(m, b, A.goff + i);
+    }
+}
+
+// Elementwise services (dsp.cpp:171-181, 166-168, 208-210).
+__global__ __launch_bounds__(256) void gain_kernel(const float *in, float *out, float g,
+                                                   uint64_t n) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * blockDim.x)
+        out[i] = in[i] * g;
+}
+__global__ __launch_bounds__(256) void set_kernel(float v, float *out, uint64_t n) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * blockDim.x)
+        out[i] = v;
+}
+__global__ __launch_bounds__(256) void magnitude_kernel(const float *re, const float *im,
+                                                        float *out, uint64_t n) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * blockDim.x)
+        out[i] = __builtin_sqrtf(re[i] * re[i] + im[i] * im[i]);
+}
+
+static uint32_t stream_grid(uint64_t work_items) {
+    // 256 CUs x 8 blocks: enough to saturate HBM, grid-stride the rest.
+    uint64_t g = (work_items + 255) / 256;
+    if (g > 2048) g = 2048;
+    return g ? (uint32_t)g : 1u;
+}
+
+int launch_ramp_table(float *table, uint32_t B, float gain, float step, hipStream_t s) {
+    hipLaunchKernelGGL(ramp_table_kernel, dim3(1), dim3(64), 0, s, table, B, gain, step);
+    DSPB_HIP(hipGetLastError());
+    return DSP_OK;
+}
+
+int launch_render(const RenderArgs &A, uint32_t C, bool vec, hipStream_t s) {
+    if (A.end <= A.start || C == 0) return DSP_OK;
+    const uint64_t items = vec ? (A.end - A.start + 3) / 4 : (A.end - A.start);
+    uint32_t gx = stream_grid(items);
+    gx = (gx + C - 1) / C;  // keep ~2048 blocks in total across channels
+    if (gx == 0) gx = 1;
+    dim3 grid(gx, C), block(256);
+#define DSPB_RENDER_CASE(KIND)                                                            \
+    case KIND:                                                                            \
+        if (vec)                                                                          \
+            hipLaunchKernelGGL(render_vec_kernel<KIND>, grid, block, 0, s, A);            \
+        else                                                                              \
+            hipLaunchKernelGGL(render_scalar_kernel<KIND>, grid, block, 0, s, A);         \
+        break;
+    switch (A.map.kind) {
+        DSPB_RENDER_CASE(MapKind::Noop)
+        DSPB_RENDER_CASE(MapKind::Gain)
+        DSPB_RENDER_CASE(MapKind::Ramp)
+    default:
+        return DSP_ERR_INVALID;
+    }
+#undef DSPB_RENDER_CASE
+    DSPB_HIP(hipGetLastError());
+    return DSP_OK;
+}
+
+int launch_gain(const float *in, float *out, float g, uint64_t n, hipStream_t s) {
+    if (!n) return DSP_OK;
+    hipLaunchKernelGGL(gain_kernel, dim3(stream_grid(n)), dim3(256), 0, s, in, out, g, n);
+    DSPB_HIP(hipGetLastError());
+    return DSP_OK;
+}
+int launch_set(float v, float *out, uint64_t n, hipStream_t s) {
+    if (!n) return DSP_OK;
+    hipLaunchKernelGGL(set_kernel, dim3(stream_grid(n)), dim3(256), 0, s, v, out, n);
+    DSPB_HIP(hipGetLastError());
+    return DSP_OK;
+}
+int launch_magnitude(const float *re, const float *im, float *out, uint64_t n,
+                     hipStream_t s) {
+    if (!n) return DSP_OK;
+    hipLaunchKernelGGL(magnitude_kernel, dim3(stream_grid(n)), dim3(256), 0, s, re, im, out, n);
+    DSPB_HIP(hipGetLastError());
+    return DSP_OK;
+}
+
+}  // namespace dspb

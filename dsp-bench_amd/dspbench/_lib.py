@@ -1,0 +1,113 @@
+"""ctypes binding of libdspbench.so (include/dspbench/dspbench.h, host.h).
+
+The library is the product: there is no Python or CPU fallback behind these
+functions.  If the shared object is missing the import fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))  # dsp-bench_amd/
+REPO_ROOT = os.path.dirname(PKG_ROOT)
+LIB_PATH = os.environ.get("DSPBENCH_LIB", os.path.join(PKG_ROOT, "libdspbench.so"))
+
+DSP_OK = 0
+DSP_ERR_INVALID = -1
+DSP_ERR_HIP = -2
+DSP_ERR_UNSUPPORTED = -3
+DSP_ERR_NOMEM = -4
+DSP_ERR_NO_DEVICE = -5
+
+DSP_WIN_HAMMING, DSP_WIN_HANN, DSP_WIN_RECT = 0, 1, 2
+
+DSP_PLUGIN_NOOP = 0
+DSP_PLUGIN_GAIN = 1
+DSP_PLUGIN_STATIC_GAIN = 2
+DSP_PLUGIN_IR_RAMP = 3
+DSP_PLUGIN_GENERIC = 16
+
+DSP_EXEC_HOST_BUFFERS = 0x1
+DSP_EXEC_SYNC = 0x2
+
+
+class DspError(RuntimeError):
+    def __init__(self, status: int, what: str, detail: str):
+        super().__init__(f"{what}: status {status} ({detail})")
+        self.status = status
+
+
+class dsp_plugin(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("params_size", C.c_uint32), ("params", C.c_void_p),
+                ("state_size", C.c_uint32), ("state", C.c_void_p), ("module", C.c_void_p)]
+
+
+class dsp_exec(C.Structure):
+    _fields_ = [("device", C.c_int32), ("flags", C.c_uint32), ("stream", C.c_void_p),
+                ("sample_offset", C.c_uint64)]
+
+
+FPP = C.POINTER(C.POINTER(C.c_float))
+FP = C.POINTER(C.c_float)
+
+# name -> (restype, argtypes)
+_SIGS = {
+    "dsp_abi_version": (C.c_int, []),
+    "dsp_status_string": (C.c_char_p, [C.c_int]),
+    "dsp_last_error": (C.c_char_p, []),
+    "dsp_device_count": (C.c_int, []),
+    "dsp_stft_frame_count": (C.c_uint64, [C.c_uint64, C.c_uint32, C.c_uint32]),
+    "dsp_render_offline": (C.c_int, [FPP, C.c_uint32, C.c_uint64, FPP, C.c_uint32, C.c_uint32,
+                                     C.c_float, C.POINTER(dsp_plugin), C.POINTER(dsp_exec)]),
+    "dsp_stft_magnitude": (C.c_int, [FPP, C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint32,
+                                     C.c_int32, C.c_uint32, FPP, C.c_uint64, C.POINTER(dsp_exec)]),
+    "dsp_render_stft": (C.c_int, [FPP, C.c_uint32, C.c_uint64, FPP, C.c_uint32, C.c_uint32,
+                                  C.c_float, C.POINTER(dsp_plugin), C.c_uint32, C.c_uint32,
+                                  C.c_int32, C.c_uint32, FPP, C.c_uint64, C.POINTER(dsp_exec)]),
+    "dsp_ir_analysis": (C.c_int, [C.POINTER(dsp_plugin), C.c_uint32, C.c_float, C.c_uint32,
+                                  FPP, FP, C.POINTER(dsp_exec)]),
+    "dsp_fft_forward": (C.c_int, [FP, FP, FP, C.c_uint32, C.POINTER(dsp_exec)]),
+    "dsp_fft_reverse": (C.c_int, [FP, FP, FP, C.c_uint32, C.POINTER(dsp_exec)]),
+    "dsp_gain": (C.c_int, [FP, FP, C.c_float, C.c_uint64, C.POINTER(dsp_exec)]),
+    "dsp_copy": (C.c_int, [FP, FP, C.c_uint64, C.POINTER(dsp_exec)]),
+    "dsp_set": (C.c_int, [C.c_float, FP, C.c_uint64, C.POINTER(dsp_exec)]),
+    "dsp_magnitude": (C.c_int, [FP, FP, FP, C.c_uint64, C.POINTER(dsp_exec)]),
+    "dsp_kernel_timing_enable": (None, [C.c_int]),
+    "dsp_kernel_timing": (C.c_int, [C.POINTER(C.c_double), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+    "dsp_initializer_create": (C.c_void_p, [C.c_size_t, C.c_int]),
+    "dsp_initializer_reset": (None, [C.c_void_p]),
+    "dsp_initializer_used": (C.c_size_t, [C.c_void_p]),
+    "dsp_initializer_destroy": (None, [C.c_void_p]),
+    "dsp_host_report": (None, [C.c_char_p, C.c_int]),
+}
+
+_lib: C.CDLL | None = None
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"libdspbench.so not built at {LIB_PATH} "
+                              "(run `make -C dsp-bench_amd` or __graft_entry__.build())")
+        L = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(status: int, what: str) -> None:
+    if status != DSP_OK:
+        L = lib()
+        raise DspError(status, what, f"{L.dsp_status_string(status).decode()}: "
+                                     f"{L.dsp_last_error().decode()}")
+
+
+def chan_table(ptrs) -> C.Array:
+    t = (FP * max(1, len(ptrs)))()
+    for i, p in enumerate(ptrs):
+        t[i] = C.cast(C.c_void_p(p), FP)
+    return t

@@ -1,0 +1,165 @@
+/*
+ * dspbench.h -- C ABI of the MI355X offline-render + spectrum path.
+ *
+ * libdspbench.so exports everything declared here plus every host service of
+ * plugin_header.h.  Plain pointers and sizes only; no torch, no C++ types.
+ *
+ * What each entry point replaces in the reference (odecaux/DSP-Bench):
+ *
+ *   dsp_render_offline  render_audio called back to back with a fixed block
+ *                       size until EOF (audio.cpp:13-175, block pump of
+ *                       wasapi_audio.cpp:223-251).  The reference has no
+ *                       offline renderer (README.md:16 TODO); semantics are
+ *                       exactly those of SURVEY §3.1 (i)-(v), one-shot mode.
+ *   dsp_stft_magnitude  windowing -> fft_forward -> pythagore_array per frame
+ *                       (dsp.cpp:69-72, 74-103, 166-168) over frames of hop H.
+ *   dsp_render_stft     the two above fused: render, keep the render, and
+ *                       the spectrum of the rendered signal (headline path).
+ *   dsp_ir_analysis     compute_IR (plugin.cpp:17-58) followed by
+ *                       fft_perform_and_get_magnitude (dsp.cpp:53-66).
+ *   dsp_fft_forward /   fft_forward / fft_reverse (dsp.cpp:74-132) with the
+ *   dsp_fft_reverse     same split re/im layout and 1/sqrt(N) scaling.
+ *
+ * Plugin dispatch: a plugin reaches the GPU as a dsp_plugin.  For the stock
+ * plugins whose audio_callback is a per-sample map the `kind` selects a
+ * specialised kernel that reads the plugin's own parameter / state blob at
+ * the struct offsets the plugin declares (gain_test: Parameters{float gain},
+ * IR_test: Parameters{float gain; float step}, static_gain_plugin:
+ * State{float gain}).  DSP_PLUGIN_GENERIC runs the plugin's compiled
+ * audio_callback itself on the GPU (module built by the plugin compiler).
+ *
+ * Errors: every entry point returns DSP_OK (0) or a negative dsp_status.
+ * Nothing aborts; HIP errors are mapped to DSP_ERR_HIP and the HIP error
+ * string is kept in dsp_last_error().
+ */
+#ifndef DSPBENCH_H
+#define DSPBENCH_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DSPBENCH_ABI_VERSION 1
+
+enum dsp_status {
+    DSP_OK = 0,
+    DSP_ERR_INVALID = -1,     /* bad argument (null pointer, size, alignment) */
+    DSP_ERR_HIP = -2,         /* a HIP runtime call failed */
+    DSP_ERR_UNSUPPORTED = -3, /* valid request this build does not implement */
+    DSP_ERR_NOMEM = -4,       /* device allocation failed */
+    DSP_ERR_NO_DEVICE = -5    /* no gfx950 device visible */
+};
+
+/* Windows.  Symmetric convention w[n] = a - b cos(2 pi n / (N - 1)), the
+ * convention of ippsWinHamming_32f (dsp.cpp:71). */
+enum dsp_window {
+    DSP_WIN_HAMMING = 0, /* 0.54 / 0.46: reference parity window */
+    DSP_WIN_HANN = 1,    /* 0.5 / 0.5: benchmark window (BASELINE cfg 4) */
+    DSP_WIN_RECT = 2
+};
+
+enum dsp_plugin_kind {
+    DSP_PLUGIN_NOOP = 0,        /* test/no_op.cpp */
+    DSP_PLUGIN_GAIN = 1,        /* build/gain_test.cpp: out *= params.gain (f32 @0) */
+    DSP_PLUGIN_STATIC_GAIN = 2, /* test/static_gain_plugin.cpp: out *= state.gain (f32 @0) */
+    DSP_PLUGIN_IR_RAMP = 3,     /* build/IR_test.cpp: out[s] = (float)g_s, g -= step (f32 @0, @4) */
+    DSP_PLUGIN_GENERIC = 16     /* compiled audio_callback run on the GPU (module) */
+};
+
+typedef struct dsp_plugin {
+    int32_t kind;          /* dsp_plugin_kind */
+    uint32_t params_size;  /* bytes of the Parameters blob */
+    const void *params;    /* host pointer to the Parameters blob */
+    uint32_t state_size;   /* bytes of the State blob */
+    void *state;           /* host pointer to the State blob */
+    const void *module;    /* DSP_PLUGIN_GENERIC: dsp_module handle, else NULL */
+} dsp_plugin;
+
+/* Execution context (ref has none: single-threaded per audio thread). */
+#define DSP_EXEC_HOST_BUFFERS 0x1u /* in/out/mag are host pointers: stage via HBM */
+#define DSP_EXEC_SYNC 0x2u         /* synchronise the stream before returning */
+
+typedef struct dsp_exec {
+    int32_t device;         /* HIP device ordinal; -1 = current device */
+    uint32_t flags;         /* DSP_EXEC_* */
+    void *stream;           /* hipStream_t; NULL = the legacy default stream */
+    uint64_t sample_offset; /* global index of in[c][0] (time-chunk shards);
+                               must be a multiple of the block size B */
+} dsp_exec;
+
+/* Number of frames of an STFT over L samples: L >= N ? (L - N) / H + 1 : 0. */
+uint64_t dsp_stft_frame_count(uint64_t L, uint32_t N, uint32_t H);
+
+/* Offline render, one-shot:
+ *   nblocks = ceil(L / B); out[c] holds nblocks * B floats.
+ *   Block b: out = file[cursor .. cursor+B) for c < in_channels, zero past
+ *   EOF and for c >= in_channels, then audio_callback(out, C, B, sr).
+ * in[c] (c < in_channels) hold L floats.  in_channels may be 0 (silence). */
+int dsp_render_offline(const float *const *in, uint32_t in_channels, uint64_t L,
+                       float *const *out, uint32_t C, uint32_t B, float sr,
+                       const dsp_plugin *plugin, const dsp_exec *ex);
+
+/* STFT magnitude over C planar channels of L samples:
+ *   F = dsp_stft_frame_count(L, N, H); mag[c][f * ld + k] = |X_f[k]| / sqrt(N)
+ *   for k < K, X_f = DFT_N(w * in[c][f*H .. f*H + N)).
+ * K <= N/2 + 1 for real input (K = N/2 + 1 = 4097 at N = 8192), or K = N
+ * for the reference's all-bins layout (dsp.cpp:65; mirror |X[N-k]| = |X[k]|).
+ * N = 8192 runs the CDNA4 wave-per-frame kernel; other powers of two <= 8192
+ * run the generic LDS kernel. */
+int dsp_stft_magnitude(const float *const *in, uint32_t C, uint64_t L, uint32_t N,
+                       uint32_t H, int32_t window, uint32_t K, float *const *mag,
+                       uint64_t ld, const dsp_exec *ex);
+
+/* Render + STFT of the render, fused when the plugin is a per-sample map
+ * (NOOP / GAIN / STATIC_GAIN / IR_RAMP) and N = 8192, H % B == 0.
+ * Output = dsp_render_offline's out + dsp_stft_magnitude(out, ..., nblocks*B). */
+int dsp_render_stft(const float *const *in, uint32_t in_channels, uint64_t L,
+                    float *const *out, uint32_t C, uint32_t B, float sr,
+                    const dsp_plugin *plugin, uint32_t N, uint32_t H,
+                    int32_t window, uint32_t K, float *const *mag, uint64_t ld,
+                    const dsp_exec *ex);
+
+/* IR analysis: ir_out[c][0..ir_len) = audio_callback(delta) for every
+ * channel (plugin.cpp:27-54), then mag[0 .. 4*ir_len) = |FFT_{4 ir_len}(
+ * hamming(ir_len) * ir_out[0], zero padded)| / sqrt(4 ir_len) (dsp.cpp:53-66).
+ * ir_len = 2048 in the reference (hardcoded_values.h:27). */
+int dsp_ir_analysis(const dsp_plugin *plugin, uint32_t C, float sr, uint32_t ir_len,
+                    float *const *ir_out, float *mag, const dsp_exec *ex);
+
+/* Complex FFT services (dsp.cpp:74-132): n a power of two <= 8192.
+ * forward: re + i*im = DFT(in + 0i) / sqrt(n)
+ * reverse: out = Re(IDFT(re + i*im)) / sqrt(n) */
+int dsp_fft_forward(const float *in, float *re, float *im, uint32_t n,
+                    const dsp_exec *ex);
+int dsp_fft_reverse(const float *re, const float *im, float *out, uint32_t n,
+                    const dsp_exec *ex);
+
+/* Elementwise services on device buffers (dsp.cpp:171-181, 208-210, 248-250). */
+int dsp_gain(const float *in, float *out, float gain, uint64_t n, const dsp_exec *ex);
+int dsp_copy(const float *in, float *out, uint64_t n, const dsp_exec *ex);
+int dsp_set(float value, float *out, uint64_t n, const dsp_exec *ex);
+int dsp_magnitude(const float *re, const float *im, float *out, uint64_t n,
+                  const dsp_exec *ex);
+
+/* Kernel timing: when enabled, every launch of the dominant kernel of
+ * dsp_render_stft / dsp_stft_magnitude (the 8192-point wave-per-frame kernel)
+ * is bracketed by HIP events on its stream.  dsp_kernel_timing() waits for
+ * them, returns the summed duration, the launch count and the algorithmic
+ * bytes of those launches, and clears the record. */
+void dsp_kernel_timing_enable(int on);
+int dsp_kernel_timing(double *total_ms, uint64_t *launches, uint64_t *bytes);
+
+/* Diagnostics. */
+int dsp_abi_version(void);
+const char *dsp_status_string(int status);
+const char *dsp_last_error(void);
+int dsp_device_count(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DSPBENCH_H */

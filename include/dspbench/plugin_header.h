@@ -1,0 +1,118 @@
+/*
+ * plugin_header.h -- the plugin-facing ABI of dspbench-mi355x.
+ *
+ * Source-compatible with the header every DSP-Bench plugin includes
+ * (reference: build/plugin_header.h:1-113).  A stock plugin such as
+ * gain_test.cpp or IR_test.cpp compiles against this file unchanged:
+ *
+ *   - parameter annotation macros   (ref build/plugin_header.h:7-13)
+ *   - scalar typedefs / constants   (ref build/plugin_header.h:16-25)
+ *   - extern "C" host services      (ref build/plugin_header.h:27-111)
+ *
+ * Every service below is exported by libdspbench.so (dsp-bench_amd/host/
+ * host_services.cpp).  The FFT services (fft_forward / fft_reverse) run on
+ * the GPU through the same HIP kernel family as the STFT path.
+ *
+ * When a plugin is compiled for the GPU (generic dispatch, see
+ * dsp-bench_amd/dspbench/plugin_compiler.py) this header is included inside
+ * a `#pragma clang force_cuda_host_device` region, so the declarations also
+ * get __device__ counterparts from include/dspbench/plugin_device.h.
+ */
+#ifndef DSPBENCH_PLUGIN_HEADER_H
+#define DSPBENCH_PLUGIN_HEADER_H
+
+/* ---- parameter annotations: parsed into a descriptor by the plugin compiler.
+ * The annotate strings are part of the contract (ref compiler.cpp:944-1164):
+ * "Int <min> <max>", "Float <min> <max> [log]", "Enum". */
+#define INT_PARAM(lo, hi)       __attribute__((annotate("Int " #lo " " #hi))) int
+#define FLOAT_PARAM(lo, hi)     __attribute__((annotate("Float " #lo " " #hi))) float
+#define FLOAT_PARAM_LOG(lo, hi) __attribute__((annotate("Float " #lo " " #hi " " "log"))) float
+#define ENUM_PARAM(enum_type)   __attribute__((annotate("Enum"))) enum_type
+
+typedef float        real32;
+typedef unsigned int u32;
+typedef int          i32;
+
+/* Rounded constants with the exact float values plugins were tuned against. */
+const float pi            = 3.141593f;
+const float two_pi        = 6.283185f;
+const float half_pi       = 1.570796f;
+const float quarter_pi    = 0.7853982f;
+const float three_half_pi = 4.7123889f;
+const float inv_two_pi    = 0.1591549f;
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* -- allocation from the host arena (opaque initialization_context) -- */
+float  *allocate_buffer(int num_sample, void *initialization_context);
+float **allocate_buffers(int num_samples, int num_channels, void *initialization_context);
+void   *allocate_bytes(int num_bytes, void *initialization_context);
+
+/* -- scalar math, double -- */
+double sin_64(double);   double cos_64(double);   double tan_64(double);
+double fabs_64(double);  double pow_64(double, double);
+double fmod_64(double, double);
+double ceil_64(double);  double floor_64(double); double sqrt_64(double);
+double exp_64(double);   double log10_64(double); double log_64(double);
+double asin_64(double);  double acos_64(double);  double atan_64(double);
+double atan2_64(double, double);
+double sinh_64(double);  double cosh_64(double);  double tanh_64(double);
+
+/* -- scalar math, float -- */
+float sin_32(float);   float cos_32(float);   float tan_32(float);
+float fabs_32(float);  float pow_32(float, float);
+float fmod_32(float, float);
+float ceil_32(float);  float floor_32(float); float sqrt_32(float);
+float exp_32(float);   float log10_32(float); float log_32(float);
+float asin_32(float);  float acos_32(float);  float atan_32(float);
+float atan2_32(float, float);
+float sinh_32(float);  float cosh_32(float);  float tanh_32(float);
+
+/* -- generators -- */
+void phasor_32_array(real32 *out, real32 ampl, real32 freq, i32 sample_count, real32 *phase_in_out);
+void sin_32_array(real32 *out, real32 ampl, real32 freq, i32 sample_count, real32 *phase_in_out);
+void triangle_32_array(real32 *out, real32 ampl, real32 freq, i32 sample_count, real32 *phase_in_out);
+void random_uniform_32_array(real32 *out, i32 sample_count, void *rng);
+
+/* -- array moves -- */
+void copy_array(real32 *in, real32 *out, i32 sample_count);
+void set_array(real32 val, real32 *out, i32 sample_count);
+void zero_array(real32 *out, i32 sample_count);
+void add_array(real32 *in_a, real32 *in_b, real32 *out, i32 sample_count);
+void product_array(real32 *in_a, real32 *in_b, real32 *out, i32 sample_count);
+
+/* -- out-of-place elementwise -- */
+void gain_32_array(real32 *in, real32 *out, real32 gain, i32 sample_count);
+void dc_offset_32_array(real32 *in, real32 *out, real32 offset, i32 sample_count);
+void sqrt_32_array(real32 *in, real32 *out, i32 sample_count);
+void abs_32_array(real32 *in, real32 *out, i32 sample_count);
+void to_db_32_array(real32 *in, real32 *out, i32 sample_count);
+void from_db_32_array(real32 *in, real32 *out, i32 sample_count);
+void ln_32_array(real32 *in, real32 *out, i32 sample_count);
+void log2_32_array(real32 *in, real32 *out, i32 sample_count);
+void log10_32_array(real32 *in, real32 *out, i32 sample_count);
+
+/* -- in-place elementwise -- */
+void gain_ip_32_array(real32 *in_out, real32 gain, i32 sample_count);
+void dc_offset_ip_32_array(real32 *in_out, real32 offset, i32 sample_count);
+void sqrt_ip_32_array(real32 *in_out, i32 sample_count);
+void abs_ip_32_array(real32 *in_out, i32 sample_count);
+void log2_ip_32_array(real32 *in_out, i32 sample_count);
+void log10_ip_32_array(real32 *in_out, i32 sample_count);
+
+/* -- magnitude of split complex -- */
+void pythagore_array(real32 *in_x, real32 *in_y, real32 *out, i32 sample_count);
+
+/* -- spectral services (GPU-backed in libdspbench) -- */
+void *fft_initialize(void *initialization_context);
+void  windowing_hamming(real32 *in, real32 *out, i32 sample_count);
+void  fft_forward(real32 *in, real32 *out_real, real32 *out_im, i32 input_sample_count, void *fft_context);
+void  fft_reverse(real32 *in_real, real32 *in_im, real32 *out, i32 input_sample_count, void *fft_context);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DSPBENCH_PLUGIN_HEADER_H */

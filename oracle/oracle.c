@@ -1,0 +1,438 @@
+/*
+ * oracle.c -- CPU restatement of the DSP-Bench hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY (see oracle.h).  Built into oracle/liboracle.so
+ * by oracle/Makefile; loaded by tests/ and by bench.py's cpu_baseline leg.
+ */
+#include "oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+static uint64_t min_u64(uint64_t a, uint64_t b) { return a < b ? a : b; }
+
+/* ------------------------------------------------------------------------ */
+/* Render loop                                                              */
+/* ------------------------------------------------------------------------ */
+
+/* One call of render_audio in one-shot mode (ref audio.cpp:13-99,134-165).
+ * `playing` mirrors ctx->audio_file_play; it is cleared at EOF
+ * (ref audio.cpp:94-98). */
+static void render_block_oneshot(const float *const *file, uint32_t file_channels,
+                                 uint64_t L, uint64_t *cursor, int *playing,
+                                 float **blk, uint32_t C, uint32_t B, float sr,
+                                 oracle_callback_t cb, void *params, void *state)
+{
+    /* ref audio.cpp:16-19 -- zero every device channel first */
+    for (uint32_t c = 0; c < C; ++c)
+        memset(blk[c], 0, (size_t)B * sizeof(float));
+
+    if (*playing) {
+        uint64_t to_write_ch = file_channels < C ? file_channels : C; /* :65 */
+        uint64_t left = L - *cursor;                                   /* :74 */
+        uint64_t n = min_u64(left, B);                                 /* :75 */
+        for (uint64_t c = 0; c < to_write_ch; ++c)                     /* :78-81 */
+            memcpy(blk[c], file[c] + *cursor, (size_t)n * sizeof(float));
+        for (uint64_t c = 0; c < to_write_ch; ++c)                     /* :84-90 */
+            for (uint64_t s = n; s < B; ++s) blk[c][s] = 0.0f;
+        *cursor += n;                                                  /* :92 */
+        if (n == left) {                                               /* :94-98 */
+            *playing = 0;
+            *cursor = 0;
+        }
+        for (uint64_t c = to_write_ch; c < C; ++c)                     /* :138-141 */
+            memset(blk[c], 0, (size_t)B * sizeof(float));
+    }
+    if (cb) cb(params, state, blk, C, B, sr);                          /* :160-165 */
+}
+
+uint64_t oracle_render_offline(const float *const *file, uint32_t file_channels,
+                               uint64_t L, float **out, uint32_t C, uint32_t B,
+                               float sr, oracle_callback_t cb, void *params,
+                               void *state)
+{
+    if (B == 0 || C == 0) return 0;
+    uint64_t nblocks = (L + B - 1) / B;
+    uint64_t cursor = 0;
+    int playing = 1;
+    float *blk[256];
+    if (C > 256) return 0;
+    for (uint64_t b = 0; b < nblocks; ++b) {
+        for (uint32_t c = 0; c < C; ++c) blk[c] = out[c] + b * (uint64_t)B;
+        render_block_oneshot(file, file_channels, L, &cursor, &playing, blk, C,
+                             B, sr, cb, params, state);
+    }
+    return nblocks;
+}
+
+uint64_t oracle_render_loop(const float *const *file, uint32_t file_channels,
+                            uint64_t L, uint64_t cursor, float **out, uint32_t C,
+                            uint32_t B, uint64_t nblocks, float sr,
+                            oracle_callback_t cb, void *params, void *state)
+{
+    float *blk[256];
+    if (C > 256 || L == 0) return cursor; /* ref audio.cpp:104 spins forever on L==0 */
+    uint64_t to_write_ch = file_channels < C ? file_channels : C;
+    for (uint64_t b = 0; b < nblocks; ++b) {
+        for (uint32_t c = 0; c < C; ++c) {
+            blk[c] = out[c] + b * (uint64_t)B;
+            memset(blk[c], 0, (size_t)B * sizeof(float));
+        }
+        uint64_t written = 0;                                          /* :102 */
+        while (written < B) {                                          /* :104-131 */
+            uint64_t left_file = L - cursor;
+            uint64_t left_buf = B - written;
+            if (left_file > left_buf) {
+                for (uint64_t c = 0; c < to_write_ch; ++c)
+                    memcpy(blk[c] + written, file[c] + cursor, left_buf * sizeof(float));
+                cursor += left_buf;
+                written += left_buf;
+            } else {
+                for (uint64_t c = 0; c < to_write_ch; ++c)
+                    memcpy(blk[c] + written, file[c] + cursor, left_file * sizeof(float));
+                written += left_file;
+                cursor = 0;
+            }
+        }
+        if (cb) cb(params, state, blk, C, B, sr);
+    }
+    return cursor;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Stock plugin bodies                                                      */
+/* ------------------------------------------------------------------------ */
+
+/* build/gain_test.cpp:39-58: sample-major, out *= (float)param.gain */
+void oracle_cb_gain_test(void *params, void *state, float **out, unsigned C,
+                         unsigned n, float sr)
+{
+    (void)state; (void)sr;
+    float gain = ((const float *)params)[0];
+    for (unsigned s = 0; s < n; ++s)
+        for (unsigned c = 0; c < C; ++c) out[c][s] *= gain;
+}
+
+/* test/static_gain_plugin.cpp:27-40: channel-major, out *= state.gain */
+void oracle_cb_static_gain(void *params, void *state, float **out, unsigned C,
+                           unsigned n, float sr)
+{
+    (void)params; (void)sr;
+    float gain = ((const float *)state)[0];
+    for (unsigned c = 0; c < C; ++c)
+        for (unsigned s = 0; s < n; ++s) out[c][s] *= gain;
+}
+
+/* build/IR_test.cpp:40-60: double recurrence g -= step, restarts per call,
+ * input ignored. */
+void oracle_cb_ir_test(void *params, void *state, float **out, unsigned C,
+                       unsigned n, float sr)
+{
+    (void)state; (void)sr;
+    const float *p = (const float *)params;
+    volatile double g = (double)p[0]; /* keep the sequential double chain */
+    double step = (double)p[1];
+    for (unsigned s = 0; s < n; ++s) {
+        float v = (float)g;
+        for (unsigned c = 0; c < C; ++c) out[c][s] = v;
+        g = g - step;
+    }
+}
+
+/* test/no_op.cpp: nothing */
+void oracle_cb_no_op(void *params, void *state, float **out, unsigned C,
+                     unsigned n, float sr)
+{
+    (void)params; (void)state; (void)out; (void)C; (void)n; (void)sr;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Windows                                                                  */
+/* ------------------------------------------------------------------------ */
+
+static void win_coeffs(int kind, double *a, double *b)
+{
+    if (kind == ORACLE_WIN_HANN) { *a = 0.5; *b = 0.5; }
+    else if (kind == ORACLE_WIN_RECT) { *a = 1.0; *b = 0.0; }
+    else { *a = 0.54; *b = 0.46; }
+}
+
+void oracle_window_f64(int kind, uint32_t n, double *w)
+{
+    double a, b;
+    win_coeffs(kind, &a, &b);
+    if (n == 1) { w[0] = 1.0; return; }
+    for (uint32_t i = 0; i < n; ++i)
+        w[i] = a - b * cos(2.0 * M_PI * (double)i / (double)(n - 1));
+}
+
+void oracle_window_f32(int kind, uint32_t n, float *w)
+{
+    double a, b;
+    win_coeffs(kind, &a, &b);
+    if (n == 1) { w[0] = 1.0f; return; }
+    for (uint32_t i = 0; i < n; ++i)
+        w[i] = (float)(a - b * cos(2.0 * M_PI * (double)i / (double)(n - 1)));
+}
+
+/* ------------------------------------------------------------------------ */
+/* FFT: iterative radix-2, decimation in time, accurate twiddles             */
+/* ------------------------------------------------------------------------ */
+
+static uint32_t ilog2_u32(uint32_t n) { uint32_t l = 0; while ((1u << l) < n) ++l; return l; }
+
+static uint32_t bitrev(uint32_t x, uint32_t bits)
+{
+    uint32_t r = 0;
+    for (uint32_t i = 0; i < bits; ++i) { r = (r << 1) | (x & 1u); x >>= 1; }
+    return r;
+}
+
+#define DEFINE_FFT(NAME, T, SQRT)                                                \
+    void NAME(T *re, T *im, uint32_t n, int dir)                                 \
+    {                                                                            \
+        uint32_t bits = ilog2_u32(n);                                            \
+        for (uint32_t i = 0; i < n; ++i) {                                       \
+            uint32_t j = bitrev(i, bits);                                        \
+            if (j > i) {                                                         \
+                T t = re[i]; re[i] = re[j]; re[j] = t;                           \
+                t = im[i]; im[i] = im[j]; im[j] = t;                             \
+            }                                                                    \
+        }                                                                        \
+        for (uint32_t len = 2; len <= n; len <<= 1) {                            \
+            uint32_t half = len >> 1;                                            \
+            for (uint32_t k = 0; k < half; ++k) {                                \
+                double ang = (double)dir * 2.0 * M_PI * (double)k / (double)len; \
+                T wr = (T)cos(ang), wi = (T)sin(ang);                            \
+                for (uint32_t i = k; i < n; i += len) {                          \
+                    uint32_t j = i + half;                                       \
+                    T xr = re[j] * wr - im[j] * wi;                              \
+                    T xi = re[j] * wi + im[j] * wr;                              \
+                    re[j] = re[i] - xr; im[j] = im[i] - xi;                      \
+                    re[i] = re[i] + xr; im[i] = im[i] + xi;                      \
+                }                                                                \
+            }                                                                    \
+        }                                                                        \
+        T s = (T)(1.0 / SQRT((double)n));                                        \
+        for (uint32_t i = 0; i < n; ++i) { re[i] *= s; im[i] *= s; }             \
+    }
+
+DEFINE_FFT(oracle_fft_f64, double, sqrt)
+DEFINE_FFT(oracle_fft_f32, float, sqrt)
+
+void oracle_fft_forward_f64(const float *in, double *re, double *im, uint32_t n)
+{
+    for (uint32_t i = 0; i < n; ++i) { re[i] = in[i]; im[i] = 0.0; } /* ref dsp.cpp:97 */
+    oracle_fft_f64(re, im, n, -1);
+}
+
+void oracle_fft_reverse_f64(const float *re_in, const float *im_in, double *out,
+                            uint32_t n)
+{
+    double *re = (double *)malloc(sizeof(double) * n);
+    double *im = (double *)malloc(sizeof(double) * n);
+    for (uint32_t i = 0; i < n; ++i) { re[i] = re_in[i]; im[i] = im_in[i]; }
+    oracle_fft_f64(re, im, n, +1);
+    for (uint32_t i = 0; i < n; ++i) out[i] = re[i]; /* ref dsp.cpp:126-129 */
+    free(re); free(im);
+}
+
+/* ref dsp.cpp:53-66 */
+void oracle_ir_magnitude_f64(const float *ir0, uint32_t ir_len, double *mag)
+{
+    uint32_t n = ir_len * 4;
+    double *w = (double *)malloc(sizeof(double) * ir_len);
+    double *re = (double *)calloc(n, sizeof(double));
+    double *im = (double *)calloc(n, sizeof(double));
+    oracle_window_f64(ORACLE_WIN_HAMMING, ir_len, w);
+    for (uint32_t i = 0; i < ir_len; ++i) re[i] = (double)ir0[i] * w[i]; /* :56-59 */
+    oracle_fft_f64(re, im, n, -1);                                         /* :61-64 */
+    for (uint32_t k = 0; k < n; ++k) mag[k] = sqrt(re[k] * re[k] + im[k] * im[k]); /* :65 */
+    free(w); free(re); free(im);
+}
+
+/* ------------------------------------------------------------------------ */
+/* STFT                                                                     */
+/* ------------------------------------------------------------------------ */
+
+uint64_t oracle_stft_frames(uint64_t L, uint32_t N, uint32_t H)
+{
+    if (N == 0 || H == 0 || L < N) return 0;
+    return (L - N) / H + 1;
+}
+
+void oracle_stft_mag_f64(const float *x, uint64_t L, uint32_t N, uint32_t H,
+                         int win, uint32_t K, uint64_t ld, double *mag)
+{
+    uint64_t F = oracle_stft_frames(L, N, H);
+    double *w = (double *)malloc(sizeof(double) * N);
+    oracle_window_f64(win, N, w);
+#pragma omp parallel
+    {
+        double *re = (double *)malloc(sizeof(double) * N);
+        double *im = (double *)malloc(sizeof(double) * N);
+#pragma omp for schedule(static)
+        for (int64_t f = 0; f < (int64_t)F; ++f) {
+            const float *fr = x + (uint64_t)f * H;
+            for (uint32_t i = 0; i < N; ++i) { re[i] = (double)fr[i] * w[i]; im[i] = 0.0; }
+            oracle_fft_f64(re, im, N, -1);
+            for (uint32_t k = 0; k < K; ++k)
+                mag[(uint64_t)f * ld + k] = sqrt(re[k] * re[k] + im[k] * im[k]);
+        }
+        free(re); free(im);
+    }
+    free(w);
+}
+
+/* fp32 CPU baseline: real-input packing z[m] = x[2m] + i x[2m+1], one
+ * N/2-point complex FFT, then the split X[k] = A[k] Z[k] + B[k] conj Z[M-k]. */
+typedef struct {
+    uint32_t M, bits;
+    uint32_t *rev;
+    float *twr, *twi;   /* e^{-2 pi i k / M}, k < M/2 */
+    float *splr, *spli; /* e^{-2 pi i k / N}, k <= M */
+} fft32_plan;
+
+static void plan32_init(fft32_plan *p, uint32_t N)
+{
+    p->M = N / 2;
+    p->bits = ilog2_u32(p->M);
+    p->rev = (uint32_t *)malloc(sizeof(uint32_t) * p->M);
+    for (uint32_t i = 0; i < p->M; ++i) p->rev[i] = bitrev(i, p->bits);
+    p->twr = (float *)malloc(sizeof(float) * (p->M / 2 + 1));
+    p->twi = (float *)malloc(sizeof(float) * (p->M / 2 + 1));
+    for (uint32_t k = 0; k <= p->M / 2; ++k) {
+        double a = -2.0 * M_PI * (double)k / (double)p->M;
+        p->twr[k] = (float)cos(a); p->twi[k] = (float)sin(a);
+    }
+    p->splr = (float *)malloc(sizeof(float) * (p->M + 1));
+    p->spli = (float *)malloc(sizeof(float) * (p->M + 1));
+    for (uint32_t k = 0; k <= p->M; ++k) {
+        double a = -2.0 * M_PI * (double)k / (double)N;
+        p->splr[k] = (float)cos(a); p->spli[k] = (float)sin(a);
+    }
+}
+
+static void plan32_free(fft32_plan *p)
+{
+    free(p->rev); free(p->twr); free(p->twi); free(p->splr); free(p->spli);
+}
+
+static void fft32_run(const fft32_plan *p, float *re, float *im)
+{
+    uint32_t M = p->M;
+    for (uint32_t i = 0; i < M; ++i) {
+        uint32_t j = p->rev[i];
+        if (j > i) {
+            float t = re[i]; re[i] = re[j]; re[j] = t;
+            t = im[i]; im[i] = im[j]; im[j] = t;
+        }
+    }
+    for (uint32_t len = 2, tstep = M / 2; len <= M; len <<= 1, tstep >>= 1) {
+        uint32_t half = len >> 1;
+        for (uint32_t i0 = 0; i0 < M; i0 += len) {
+            for (uint32_t k = 0; k < half; ++k) {
+                float wr = p->twr[k * tstep], wi = p->twi[k * tstep];
+                uint32_t i = i0 + k, j = i + half;
+                float xr = re[j] * wr - im[j] * wi;
+                float xi = re[j] * wi + im[j] * wr;
+                re[j] = re[i] - xr; im[j] = im[i] - xi;
+                re[i] += xr; im[i] += xi;
+            }
+        }
+    }
+}
+
+void oracle_stft_mag_f32(const float *x, uint64_t L, uint32_t N, uint32_t H,
+                         int win, uint32_t K, uint64_t ld, float *mag,
+                         int nthreads)
+{
+    uint64_t F = oracle_stft_frames(L, N, H);
+    fft32_plan p;
+    plan32_init(&p, N);
+    float *w = (float *)malloc(sizeof(float) * N);
+    oracle_window_f32(win, N, w);
+    const float scale = (float)(1.0 / sqrt((double)N));
+    const uint32_t M = p.M;
+#ifdef _OPENMP
+    if (nthreads <= 0) nthreads = omp_get_max_threads();
+#else
+    nthreads = 1;
+#endif
+#pragma omp parallel num_threads(nthreads)
+    {
+        float *re = (float *)malloc(sizeof(float) * M);
+        float *im = (float *)malloc(sizeof(float) * M);
+#pragma omp for schedule(static)
+        for (int64_t f = 0; f < (int64_t)F; ++f) {
+            const float *fr = x + (uint64_t)f * H;
+            for (uint32_t m = 0; m < M; ++m) {
+                re[m] = fr[2 * m] * w[2 * m];
+                im[m] = fr[2 * m + 1] * w[2 * m + 1];
+            }
+            fft32_run(&p, re, im);
+            float *row = mag + (uint64_t)f * ld;
+            for (uint32_t k = 0; k < K && k <= M; ++k) {
+                uint32_t km = (k == 0 || k == M) ? 0 : M - k;
+                uint32_t kk = (k == M) ? 0 : k;
+                float zr = re[kk], zi = im[kk];
+                float cr = re[km], ci = -im[km];
+                /* E = (Z[k] + conj Z[M-k]) / 2, O = (Z[k] - conj Z[M-k]) / (2i) */
+                float er = 0.5f * (zr + cr), ei = 0.5f * (zi + ci);
+                float dr = 0.5f * (zr - cr), di = 0.5f * (zi - ci);
+                float orr = di, oi = -dr;
+                float tr = p.splr[k], ti = p.spli[k];
+                float xr = er + (orr * tr - oi * ti);
+                float xi = ei + (orr * ti + oi * tr);
+                row[k] = sqrtf(xr * xr + xi * xi) * scale;
+            }
+        }
+        free(re); free(im);
+    }
+    free(w);
+    plan32_free(&p);
+}
+
+/* ------------------------------------------------------------------------ */
+/* Parameter normalisation (ref plugin.h:173-233)                            */
+/* ------------------------------------------------------------------------ */
+
+float oracle_normalize_int(int32_t lo, int32_t hi, float value)
+{
+    return (float)(value - (float)lo) / (float)(hi - lo);
+}
+
+int32_t oracle_denormalize_int(int32_t lo, int32_t hi, float nv)
+{
+    return (int32_t)(nv * (float)(hi - lo) + (float)lo);
+}
+
+float oracle_normalize_float(float lo, float hi, int is_log, float value)
+{
+    if (value < lo) value = lo;
+    if (value > hi) value = hi;
+    if (value == lo) return 0.0f;
+    if (is_log) return logf(value / lo) / logf(hi / lo);
+    return (value - lo) / (hi - lo);
+}
+
+float oracle_denormalize_float(float lo, float hi, int is_log, float nv)
+{
+    if (is_log) return lo * expf(nv * logf(hi / lo));
+    return nv * (hi - lo) + lo;
+}
+
+float oracle_normalize_enum_index(uint32_t num_entries, int32_t index)
+{
+    if (num_entries == 1) return 0.0f;
+    return (float)index / (float)(num_entries - 1);
+}
+
+uint32_t oracle_denormalize_enum_index(uint32_t num_entries, float nv)
+{
+    return (uint32_t)(nv * (float)(num_entries - 1));
+}

@@ -1,0 +1,40 @@
+#!/bin/bash
+# tools/gpu_session.sh -- one gpurun session: GPU tests, smoke, bench, profile.
+# Every GPU step has its own time limit; a crash / abort / timeout ends the
+# session (no further GPU work), a plain test failure (exit 1) does not.
+#   usage: bash tools/gpu_session.sh [tests|bench|prof|all] [tag]
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+mode=${1:-all}
+tag=${2:-r01}
+out=gpurun_out
+mkdir -p $out
+
+fatal() {  # exit codes that mean the GPU step crashed or hung
+    case $1 in 0|1|5) return 1;; *) return 0;; esac
+}
+
+run() {  # run <name> <seconds> <cmd...>
+    local name=$1 secs=$2; shift 2
+    echo "=== $name ($(date +%T))"
+    timeout -k 10 "$secs" "$@" > "$out/$name.log" 2>&1
+    local rc=$?
+    echo "=== $name rc=$rc"
+    tail -n 25 "$out/$name.log"
+    if fatal $rc; then echo "FATAL rc=$rc in $name: stopping"; exit $rc; fi
+    return 0
+}
+
+if [[ $mode == tests || $mode == all ]]; then
+    run pytest_gpu 900 python -m pytest tests -m gpu -q -x --timeout=600
+    run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+fi
+if [[ $mode == bench || $mode == all || $mode == prof ]]; then
+    run bench 600 python bench.py --steps 20 --warmup 5
+fi
+if [[ $mode == prof || $mode == all ]]; then
+    run rocprof_stats 600 rocprofv3 --kernel-trace --stats -d $out/prof_$tag -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline
+    find $out/prof_$tag -name "*kernel_stats.csv" | head -5
+fi
+echo "=== done"
