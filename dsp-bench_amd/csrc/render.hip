@@ -29,6 +29,7 @@ __global__ void ramp_table_kernel(float *table, uint32_t B, float gain, float st
     if (blockIdx.x != 0 || threadIdx.x != 0) return;
     double g = (double)gain;         // double gain = param.gain;
     const double s = (double)step;   // gain -= param.step (float promoted)
+#pragma unroll 16
     for (uint32_t i = 0; i < B; ++i) {
         table[i] = (float)g;         // out_buffer[channel][sample] = gain;
         g = g - s;

@@ -126,7 +126,50 @@ __device__ __forceinline__ uint32_t xcd_remap(uint32_t bid, uint32_t nwg) {
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
 }
 
-template <int SRC, bool FULL, int KM>
+// Fused render source: the frame's 8192 samples are produced by the
+// per-sample plugin map (render.hip's rule) instead of read back from HBM.
+template <MapKind MK, bool POW2>
+__device__ __forceinline__ void render_frame(const Stft8kArgs &A, const float *x, uint64_t fs,
+                                             uint32_t lane, v2f (&v)[64]) {
+    const uint64_t gbase = A.goff + fs;  // global index of the frame's sample 0
+    if constexpr (MK == MapKind::Ramp) {
+        const float *T = A.map.table;    // IR_test ramp, one block long
+        if constexpr (POW2) {            // B >= 2: (p & mask) is even, p + 1 in range
+            const uint32_t p0 = (uint32_t)gbase + 2u * lane;
+#pragma unroll
+            for (int b = 0; b < 64; ++b)
+                v[b] = *reinterpret_cast<const v2f *>(T + ((p0 + 128u * (uint32_t)b) & A.map.b_mask));
+        } else {
+            const uint32_t Bn = A.map.B;
+            uint32_t p = (uint32_t)((gbase + 2u * lane) % Bn);
+#pragma unroll
+            for (int b = 0; b < 64; ++b) {
+                const uint32_t q = (p + 1 == Bn) ? 0u : p + 1;
+                v[b] = v2f{T[p], T[q]};
+                p += 128u;
+                while (p >= Bn) p -= Bn;
+            }
+        }
+    } else {
+        if (x != nullptr && fs + 8192u <= A.L) {  // wave-uniform: whole frame inside the file
+#pragma unroll
+            for (int b = 0; b < 64; ++b)
+                v[b] = reinterpret_cast<const v2f *>(x + fs + 128u * (uint32_t)b)[lane];
+        } else {  // EOF inside the frame (or no file channel): zero past L
+#pragma unroll
+            for (int b = 0; b < 64; ++b) {
+                const uint64_t li = fs + 2u * lane + 128u * (uint32_t)b;
+                v[b] = v2f{(x && li < A.L) ? x[li] : 0.f, (x && li + 1 < A.L) ? x[li + 1] : 0.f};
+            }
+        }
+        if constexpr (MK == MapKind::Gain) {
+#pragma unroll
+            for (int b = 0; b < 64; ++b) v[b] *= A.map.a;  // one fp32 multiply per sample
+        }
+    }
+}
+
+template <int SRC, bool FULL, int KM, MapKind MK = MapKind::Noop, bool POW2 = true>
 __global__ __launch_bounds__(256, 2) void stft8192_kernel(Stft8kArgs A) {
     __shared__ float lds_all[4][64 * 65];
     const uint32_t lane = threadIdx.x & 63u;
@@ -142,32 +185,21 @@ __global__ __launch_bounds__(256, 2) void stft8192_kernel(Stft8kArgs A) {
 
     // ---- 1. load (+ fused render) + window --------------------------------
     v2f v[64];
+    if constexpr (SRC == kSrcMemory) {
 #pragma unroll
-    for (int b = 0; b < 64; ++b) {
-        const uint32_t s = 2u * lane + 128u * (uint32_t)b;  // sample in frame
-        v2f xv;
-        if constexpr (SRC == kSrcMemory) {
-            if (FULL || s < A.valid) {
-                xv = reinterpret_cast<const v2f *>(x + fs + 128u * (uint32_t)b)[lane];
-            } else {
-                xv = v2f{0.f, 0.f};
-            }
-        } else {
-            const uint64_t li = fs + s;  // local sample index
-            v2f base = v2f{0.f, 0.f};
-            if (A.map.kind != MapKind::Ramp && x != nullptr) {
-                if (li + 1 < A.L) {
-                    base = *reinterpret_cast<const v2f *>(x + li);
-                } else if (li < A.L) {
-                    base.x = x[li];
-                }
-            }
-            xv.x = apply_map(A.map, base.x, A.goff + li);
-            xv.y = apply_map(A.map, base.y, A.goff + li + 1);
-            if (128u * (uint32_t)b < A.H)  // this frame owns the hop [fs, fs+H)
-                *reinterpret_cast<v2f *>(A.out.p[c] + li) = xv;
+        for (int b = 0; b < 64; ++b) {
+            if (FULL || 2u * lane + 128u * (uint32_t)b < A.valid)
+                v[b] = reinterpret_cast<const v2f *>(x + fs + 128u * (uint32_t)b)[lane];
+            else
+                v[b] = v2f{0.f, 0.f};
         }
-        v[b] = xv;
+    } else {
+        render_frame<MK, POW2>(A, x, fs, lane, v);
+        // this frame owns the render of its hop [fs, fs + H)
+        float *o = A.out.p[c] + fs;
+#pragma unroll
+        for (int b = 0; b < 64; ++b)
+            if (128u * (uint32_t)b < A.H) reinterpret_cast<v2f *>(o + 128u * (uint32_t)b)[lane] = v[b];
     }
     // window, in groups of 16 so the window loads (L2-resident table) do not
     // all become live at once next to the 128 data registers
@@ -320,6 +352,16 @@ __global__ __launch_bounds__(256) void fft_generic_kernel(GenericFftArgs A) {
 // ---------------------------------------------------------------------------
 // launchers (called from capi.cpp)
 // ---------------------------------------------------------------------------
+template <int SRC, bool FULL, MapKind MK, bool POW2>
+static void launch_km(int km, dim3 grid, dim3 block, hipStream_t stream, const Stft8kArgs &A) {
+    if (km == kKHalf)
+        hipLaunchKernelGGL((stft8192_kernel<SRC, FULL, kKHalf, MK, POW2>), grid, block, 0, stream, A);
+    else if (km == kKMirror)
+        hipLaunchKernelGGL((stft8192_kernel<SRC, FULL, kKMirror, MK, POW2>), grid, block, 0, stream, A);
+    else
+        hipLaunchKernelGGL((stft8192_kernel<SRC, FULL, kKPartial, MK, POW2>), grid, block, 0, stream, A);
+}
+
 int launch_stft8192(const Stft8kArgs &A, uint32_t C, bool fused, bool full,
                     hipStream_t stream) {
     if (A.F == 0 || C == 0) return DSP_OK;
@@ -327,22 +369,22 @@ int launch_stft8192(const Stft8kArgs &A, uint32_t C, bool fused, bool full,
     if (groups > 0x7fffffffull) return DSP_ERR_INVALID;
     dim3 grid((uint32_t)groups, C), block(256);
     const int km = A.K == 4097u ? kKHalf : (A.K == 8192u ? kKMirror : kKPartial);
-#define DSPB_STFT_LAUNCH(SRC, FULL)                                                         \
-    do {                                                                                  \
-        if (km == kKHalf)                                                                 \
-            hipLaunchKernelGGL((stft8192_kernel<SRC, FULL, kKHalf>), grid, block, 0, stream, A);    \
-        else if (km == kKMirror)                                                          \
-            hipLaunchKernelGGL((stft8192_kernel<SRC, FULL, kKMirror>), grid, block, 0, stream, A);  \
-        else                                                                              \
-            hipLaunchKernelGGL((stft8192_kernel<SRC, FULL, kKPartial>), grid, block, 0, stream, A); \
-    } while (0)
-    if (fused)
-        DSPB_STFT_LAUNCH(kSrcRender, true);
-    else if (full)
-        DSPB_STFT_LAUNCH(kSrcMemory, true);
-    else
-        DSPB_STFT_LAUNCH(kSrcMemory, false);
-#undef DSPB_STFT_LAUNCH
+    const bool pow2 = A.map.b_mask != 0 && A.map.B >= 2;
+    if (fused) {
+        switch (A.map.kind) {
+        case MapKind::Noop: launch_km<kSrcRender, true, MapKind::Noop, true>(km, grid, block, stream, A); break;
+        case MapKind::Gain: launch_km<kSrcRender, true, MapKind::Gain, true>(km, grid, block, stream, A); break;
+        case MapKind::Ramp:
+            if (pow2) launch_km<kSrcRender, true, MapKind::Ramp, true>(km, grid, block, stream, A);
+            else launch_km<kSrcRender, true, MapKind::Ramp, false>(km, grid, block, stream, A);
+            break;
+        default: return DSP_ERR_INVALID;
+        }
+    } else if (full) {
+        launch_km<kSrcMemory, true, MapKind::Noop, true>(km, grid, block, stream, A);
+    } else {
+        launch_km<kSrcMemory, false, MapKind::Noop, true>(km, grid, block, stream, A);
+    }
     DSPB_HIP(hipGetLastError());
     return DSP_OK;
 }

@@ -132,8 +132,9 @@ def test_stft_sine_tone_peak(torch_cuda, oracle):
 
 
 @pytest.mark.parametrize("pname", ["IR_test", "gain_test", "static_gain_plugin", "no_op"])
-def test_render_stft_fused(torch_cuda, oracle, pname):
-    L, B = 8192 * 6 + 777, 512
+@pytest.mark.parametrize("B", [512, 384, 1, 4096])
+def test_render_stft_fused(torch_cuda, oracle, pname, B):
+    L = 8192 * 6 + 777
     x = rnd((2, L), 31)
     out, mag = d.render_stft(to_dev(torch_cuda, x), 2, B, 48000.0, PLUGINS[pname][0](),
                              window=d.DSP_WIN_HANN)
