@@ -49,6 +49,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
     ap.add_argument("--gather", action="store_true", help="also time an RCCL gather to rank 0")
+    ap.add_argument("--workload", default="headline", choices=["headline", "stft96k", "gain10min"],
+                    help="headline = IR_test + STFT 48 kHz (the metric); stft96k = BASELINE cfg 4 "
+                         "(STFT of 1 h stereo 96 kHz from HBM); gain10min = cfg 2 render")
     return ap.parse_args()
 
 
@@ -94,25 +97,42 @@ def main():
 
     import dspbench as d
 
-    L = int(round(args.minutes * 60 * SR))
+    wl = args.workload
+    sr = 96_000 if wl == "stft96k" else SR
+    minutes = args.minutes if wl != "gain10min" or args.minutes != 60.0 else 10.0
+    L = int(round(minutes * 60 * sr))
     L -= L % HOP  # whole hops per rank
-    halo = N_FFT - HOP
+    halo = N_FFT - HOP if wl != "gain10min" else 0
     # rank r owns samples [r L, (r+1) L) of an (N * minutes)-long file and
     # reads a halo of the next rank's first 4096 samples (the last rank has none)
     L_in = L + (halo if rank < world - 1 else 0)
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     x = (torch.rand((CH, L_in), device=dev, generator=g) * 2 - 1) * 0.1  # synthetic WAV
     nb = d.num_blocks(L_in, B)
-    F = d.stft_frames(nb * B, N_FFT, HOP)
-    out = torch.empty((CH, nb * B), device=dev)
-    mag = torch.empty((CH, F, K_BINS), device=dev)
-    plugin = d.Plugin.ir_test(0.9, 0.002)
+    F = d.stft_frames(nb * B if wl == "headline" else L_in, N_FFT, HOP)
+    out = torch.empty((CH, nb * B), device=dev) if wl != "stft96k" else None
+    mag = torch.empty((CH, F, K_BINS), device=dev) if wl != "gain10min" else None
+    plugin = d.Plugin.ir_test(0.9, 0.002) if wl == "headline" else d.Plugin.gain_test(0.2)
     stream = torch.cuda.current_stream(dev)
     soff = rank * L
 
-    def step():
-        d.render_stft(x, CH, B, float(SR), plugin, N=N_FFT, H=HOP, window=d.DSP_WIN_HANN,
-                      K=K_BINS, out=out, mag=mag, sample_offset=soff)
+    if wl == "headline":
+        def step():
+            d.render_stft(x, CH, B, float(sr), plugin, N=N_FFT, H=HOP, window=d.DSP_WIN_HANN,
+                          K=K_BINS, out=out, mag=mag, sample_offset=soff)
+        workload = ("IR_test render (B=512) + 8192-pt Hann STFT, hop 4096, 4097 bins, "
+                    f"{minutes:g} min of 48 kHz stereo per GPU")
+        kname = "stft8192_kernel<render> (fused render + window + FFT + |X|)"
+    elif wl == "stft96k":
+        def step():
+            d.stft_magnitude(x, N=N_FFT, H=HOP, window=d.DSP_WIN_HANN, K=K_BINS, out=mag)
+        workload = f"8192-pt Hann STFT, hop 4096, 4097 bins, {minutes:g} min of 96 kHz stereo per GPU (cfg 4)"
+        kname = "stft8192_kernel<memory> (window + FFT + |X|)"
+    else:
+        def step():
+            d.render_offline(x, CH, B, float(sr), plugin, out=out)
+        workload = f"gain_test render (B=512), {minutes:g} min of 48 kHz stereo per GPU (cfg 2)"
+        kname = "render_vec_kernel<Gain>"
 
     for _ in range(args.warmup):
         step()
@@ -158,18 +178,20 @@ def main():
         torch.cuda.synchronize()
         dist.barrier()
         tg = time.perf_counter()
-        owned = out[:, :L].contiguous()
-        bufs = [torch.empty_like(owned) for _ in range(world)] if rank == 0 else None
-        dist.gather(owned, bufs, dst=0)
-        fm = mag[:, : L // HOP].contiguous()
-        mbufs = [torch.empty_like(fm) for _ in range(world)] if rank == 0 else None
-        dist.gather(fm, mbufs, dst=0)
+        if out is not None:
+            owned = out[:, :L].contiguous()
+            bufs = [torch.empty_like(owned) for _ in range(world)] if rank == 0 else None
+            dist.gather(owned, bufs, dst=0)
+        if mag is not None:
+            fm = mag[:, : L // HOP].contiguous()
+            mbufs = [torch.empty_like(fm) for _ in range(world)] if rank == 0 else None
+            dist.gather(fm, mbufs, dst=0)
         torch.cuda.synchronize()
         dist.barrier()
         gather_ms = (time.perf_counter() - tg) * 1e3
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and wl == "headline":
         cpu = cpu_baseline(args.cpu_seconds)
 
     if rank == 0:
@@ -187,17 +209,16 @@ def main():
             "dtype": "f32",
             "data": "synthetic (uniform noise WAV in HBM; IR_test output is input-independent)",
             "config": {
-                "workload": "IR_test render (B=512) + 8192-pt Hann STFT, hop 4096, 4097 bins, "
-                            f"{args.minutes:g} min of 48 kHz stereo per GPU",
-                "plugin": "IR_test (gain 0.9, step 0.002)",
+                "workload": workload,
+                "plugin": plugin.name,
                 "samples_per_gpu": samples_per_rank,
-                "frames_per_gpu": CH * F,
+                "frames_per_gpu": CH * F if mag is not None else 0,
                 "sharding": "time-chunk per GPU, 4096-sample halo, no data-path collective",
                 "gather_ms": None if gather_ms is None else round(gather_ms, 3),
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "stft8192_kernel<render> (fused render + window + FFT + |X|)",
+                "kernel": kname,
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s",

@@ -11,6 +11,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <algorithm>
 #include <map>
 #include <mutex>
 #include <tuple>
@@ -456,8 +457,15 @@ int dsp_render_offline(const float *const *in, uint32_t in_channels, uint64_t L,
     SampleMap map;
     int st = plugin_map(plugin, B, g.dev, s, &map);
     if (st) return st;
+    TimedLaunch tl{};
+    if ((st = timing_begin(s, &tl))) return st;
     st = render_device(din.data(), in_channels, L, dout.data(), C, B, map, 0, goff_of(ex), s);
     if (st) return st;
+    {   // algorithmic bytes: file read (unless the map ignores its input) + render write
+        uint64_t bytes = (uint64_t)C * Lr * 4;
+        if (map.kind != MapKind::Ramp) bytes += (uint64_t)std::min(in_channels, C) * L * 4;
+        if ((st = timing_end(s, &tl, bytes))) return st;
+    }
     if (host_mode(ex))
         for (uint32_t c = 0; c < C; ++c)
             DSPB_HIP(hipMemcpyAsync(out[c], dout[c], Lr * sizeof(float), hipMemcpyDeviceToHost, s));
