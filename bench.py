@@ -49,6 +49,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
     ap.add_argument("--gather", action="store_true", help="also time an RCCL gather to rank 0")
+    ap.add_argument("--stft-variant", type=int, default=1, choices=[0, 1],
+                    help="8192-pt kernel: 0 = wave per frame, 1 = two waves per frame")
     ap.add_argument("--workload", default="headline", choices=["headline", "stft96k", "gain10min"],
                     help="headline = IR_test + STFT 48 kHz (the metric); stft96k = BASELINE cfg 4 "
                          "(STFT of 1 h stereo 96 kHz from HBM); gain10min = cfg 2 render")
@@ -96,6 +98,7 @@ def main():
     torch.cuda.set_device(dev)
 
     import dspbench as d
+    d.lib().dsp_stft_kernel_variant(args.stft_variant)
 
     wl = args.workload
     sr = 96_000 if wl == "stft96k" else SR

@@ -151,6 +151,15 @@ struct TimedLaunch {
     uint64_t bytes;
 };
 static bool g_timing = false;
+// which 8192-point kernel: 0 = one wave per frame (spectral.hip),
+// 1 = two waves per frame (stft_pair.hip)
+static int g_stft_variant = 1;
+
+static int launch_stft(const Stft8kArgs &A, uint32_t C, bool fused, bool full, hipStream_t s) {
+    if (g_stft_variant == 1) return launch_stft8192_pair(A, C, fused, s);
+    return launch_stft8192(A, C, fused, full, s);
+}
+
 static std::vector<TimedLaunch> g_timed;
 
 static int timing_begin(hipStream_t s, TimedLaunch *t) {
@@ -324,7 +333,7 @@ static int stft_device(const float *const *in, uint32_t C, uint64_t L, uint32_t 
             A.scale = (float)(1.0 / std::sqrt((double)N));
             TimedLaunch tl{};
             if ((st = timing_begin(s, &tl))) return st;
-            st = launch_stft8192(A, cn, false, true, s);
+            st = launch_stft(A, cn, false, true, s);
             if (st) return st;
             // algorithmic bytes: frame input read once per hop + magnitudes
             st = timing_end(s, &tl, (uint64_t)cn * F * ((uint64_t)H * 4 + (uint64_t)K * 4));
@@ -362,6 +371,13 @@ using namespace dspb;
 extern "C" {
 
 int dsp_abi_version(void) { return DSPBENCH_ABI_VERSION; }
+
+int dsp_stft_kernel_variant(int v) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    const int old = g_stft_variant;
+    if (v == 0 || v == 1) g_stft_variant = v;
+    return old;
+}
 
 void dsp_kernel_timing_enable(int on) {
     std::lock_guard<std::mutex> lk(g_mu);
@@ -591,7 +607,7 @@ int dsp_render_stft(const float *const *in, uint32_t in_channels, uint64_t L,
             A.goff = goff;
             TimedLaunch tl{};
             if ((st = timing_begin(s, &tl))) return st;
-            if ((st = launch_stft8192(A, cn, true, true, s))) return st;
+            if ((st = launch_stft(A, cn, true, true, s))) return st;
             // algorithmic bytes: render write 4 B + magnitudes 4 K/H B
             // per hop sample, plus the file read when the map uses its input
             const uint64_t hop_samples = (uint64_t)cn * F * H;
@@ -668,7 +684,7 @@ int dsp_ir_analysis(const dsp_plugin *plugin, uint32_t C, float sr, uint32_t ir_
         A.win2 = reinterpret_cast<const v2f *>(win);
         A.tw = tw;
         A.scale = (float)(1.0 / std::sqrt((double)n));
-        if ((st = launch_stft8192(A, 1, false, false, s))) return st;
+        if ((st = launch_stft(A, 1, false, false, s))) return st;
     } else {
         GenericFftArgs A{};
         A.sig.p[0] = dir[0];

@@ -152,6 +152,11 @@ int dsp_magnitude(const float *re, const float *im, float *out, uint64_t n,
 void dsp_kernel_timing_enable(int on);
 int dsp_kernel_timing(double *total_ms, uint64_t *launches, uint64_t *bytes);
 
+/* Select the 8192-point kernel (A/B and tests): 0 = one wavefront per frame,
+ * 1 = two wavefronts per frame (default).  Other values only query.
+ * Returns the previous selection. */
+int dsp_stft_kernel_variant(int variant);
+
 /* Diagnostics. */
 int dsp_abi_version(void);
 const char *dsp_status_string(int status);

@@ -29,6 +29,15 @@ def rnd(shape, seed):
     return np.random.default_rng(seed).uniform(-1.0, 1.0, size=shape).astype(np.float32)
 
 
+@pytest.fixture(params=[0, 1], ids=["wave", "pair"])
+def variant(request):
+    """Run the test on both 8192-point kernels (dsp_stft_kernel_variant)."""
+    L = d.lib()
+    old = L.dsp_stft_kernel_variant(request.param)
+    yield request.param
+    L.dsp_stft_kernel_variant(old)
+
+
 def to_dev(torch, x):
     return torch.from_numpy(np.ascontiguousarray(x)).cuda()
 
@@ -101,7 +110,7 @@ def test_render_matches_reference_plugin_so(torch_cuda, oracle):
 @pytest.mark.parametrize("window", [d.DSP_WIN_HANN, d.DSP_WIN_HAMMING])
 @pytest.mark.parametrize("K", [4097, 8192, 1000])
 @pytest.mark.parametrize("H", [4096, 2048, 8192, 1000])
-def test_stft_8192_vs_f64(torch_cuda, oracle, window, K, H):
+def test_stft_8192_vs_f64(torch_cuda, oracle, window, K, H, variant):
     L = 8192 * 3 + 1234
     x = rnd((2, L), 21)
     mag = d.stft_magnitude(to_dev(torch_cuda, x), N=8192, H=H, window=window, K=K).cpu().numpy()
@@ -121,7 +130,7 @@ def test_stft_generic_sizes(torch_cuda, oracle, N):
     assert peak_rel_err(mag[0], ref) <= PEAK_REL_TOL
 
 
-def test_stft_sine_tone_peak(torch_cuda, oracle):
+def test_stft_sine_tone_peak(torch_cuda, oracle, variant):
     """A pure tone: peak bin, and sidelobes relative to the peak."""
     n = np.arange(8192 * 4)
     x = (0.5 * np.sin(2 * np.pi * 1000.25 / 48000 * n)).astype(np.float32)[None]
@@ -133,7 +142,7 @@ def test_stft_sine_tone_peak(torch_cuda, oracle):
 
 @pytest.mark.parametrize("pname", ["IR_test", "gain_test", "static_gain_plugin", "no_op"])
 @pytest.mark.parametrize("B", [512, 384, 1, 4096])
-def test_render_stft_fused(torch_cuda, oracle, pname, B):
+def test_render_stft_fused(torch_cuda, oracle, pname, B, variant):
     L = 8192 * 6 + 777
     x = rnd((2, L), 31)
     out, mag = d.render_stft(to_dev(torch_cuda, x), 2, B, 48000.0, PLUGINS[pname][0](),
@@ -148,7 +157,7 @@ def test_render_stft_fused(torch_cuda, oracle, pname, B):
         assert peak_rel_err(mag[c], mref) <= PEAK_REL_TOL
 
 
-def test_render_stft_shards_match_whole(torch_cuda):
+def test_render_stft_shards_match_whole(torch_cuda, variant):
     """Time-chunk sharding with a halo: each shard's frames and
     render equal the corresponding slice of the unsharded result."""
     torch = torch_cuda
@@ -168,7 +177,7 @@ def test_render_stft_shards_match_whole(torch_cuda):
         assert torch.equal(mag_s, mag_all[:, f0:f0 + nf])
 
 
-def test_ir_analysis_gain_flat(torch_cuda, oracle):
+def test_ir_analysis_gain_flat(torch_cuda, oracle, variant):
     """K4: IR of gain_test(0.2) = 0.2 delta; w[0] = 0.08 -> flat 0.2*0.08/sqrt(8192)."""
     ir, mag = d.ir_analysis(d.Plugin.gain_test(0.2), 2, 48000.0)
     expect = np.zeros((2, 2048), np.float32)
@@ -179,7 +188,7 @@ def test_ir_analysis_gain_flat(torch_cuda, oracle):
     assert np.max(np.abs(mag - flat)) <= 1e-6 * flat * 8
 
 
-def test_ir_analysis_ir_test_kat(torch_cuda, oracle):
+def test_ir_analysis_ir_test_kat(torch_cuda, oracle, variant):
     """K5: IR_test(0.9, 0.002) magnitudes at bins 0, 1, 2, 4096, 8191."""
     ir, mag = d.ir_analysis(d.Plugin.ir_test(0.9, 0.002), 1, 48000.0)
     ramp = oracle.ir_ramp_reference(0.9, 0.002, 2048)
@@ -228,7 +237,7 @@ def test_full_size_gain_render_10min(torch_cuda):
     assert torch.equal(out, x * torch.tensor(0.2, dtype=torch.float32, device="cuda"))
 
 
-def test_full_size_ir_test_stft_1h(torch_cuda, oracle):
+def test_full_size_ir_test_stft_1h(torch_cuda, oracle, variant):
     """Headline workload at full size: 1 h stereo 48 kHz through IR_test +
     8192-pt Hann STFT (hop 4096).  Properties: the render is the B-periodic
     ramp everywhere; every frame of a B-periodic signal with B | H is the same
