@@ -48,7 +48,7 @@ static int invalid(const char *fmt, ...) {
 // ---------------------------------------------------------------------------
 struct DeviceRes {
     v2f *tw8192 = nullptr;                                    // exp(-2 pi i k / 8192)
-    std::map<std::tuple<int, uint32_t, uint32_t>, float *> windows;  // (kind, N, valid)
+    std::map<std::tuple<int, uint32_t, uint32_t, float>, float *> windows;  // (kind, N, valid, scale)
     std::map<void *, std::pair<float *, size_t>> scratch;     // per stream
 };
 
@@ -101,10 +101,11 @@ static int get_tw(int dev, const v2f **out) {
 
 // Window of length `valid` (symmetric, ref ippsWinHamming_32f convention)
 // zero-padded to N.  Computed in double, rounded once to float.
-static int get_window(int dev, int kind, uint32_t N, uint32_t valid, const float **out) {
+static int get_window(int dev, int kind, uint32_t N, uint32_t valid, const float **out,
+                      double scale = 1.0) {
     std::lock_guard<std::mutex> lk(g_mu);
     DeviceRes &r = g_res[dev];
-    auto key = std::make_tuple(kind, N, valid);
+    auto key = std::make_tuple(kind, N, valid, (float)scale);
     auto it = r.windows.find(key);
     if (it != r.windows.end()) { *out = it->second; return DSP_OK; }
     double a = 0.54, b = 0.46;
@@ -112,8 +113,8 @@ static int get_window(int dev, int kind, uint32_t N, uint32_t valid, const float
     else if (kind == DSP_WIN_RECT) { a = 1.0; b = 0.0; }
     std::vector<float> h(N, 0.f);
     for (uint32_t n = 0; n < valid; ++n)
-        h[n] = valid == 1 ? 1.f
-                          : (float)(a - b * std::cos(2.0 * M_PI * (double)n / (double)(valid - 1)));
+        h[n] = valid == 1 ? (float)scale
+                          : (float)(scale * (a - b * std::cos(2.0 * M_PI * (double)n / (double)(valid - 1))));
     float *d = nullptr;
     DSPB_HIP(hipMalloc(&d, sizeof(float) * N));
     DSPB_HIP(hipMemcpy(d, h.data(), sizeof(float) * N, hipMemcpyHostToDevice));
@@ -151,11 +152,18 @@ struct TimedLaunch {
     uint64_t bytes;
 };
 static bool g_timing = false;
-// which 8192-point kernel: 0 = one wave per frame (spectral.hip),
-// 1 = two waves per frame (stft_pair.hip)
-static int g_stft_variant = 1;
+// which 8192-point kernel: 0 = one wave per frame, packed (spectral.hip),
+// 1 = two waves per frame (stft_pair.hip), 2 = one wave per frame, scalar
+// SoA with a pre-scaled window (stft_soa.hip)
+static int g_stft_variant = 2;
+
+// the SoA kernel folds 0.5/sqrt(N) into the window
+static float window_prescale(uint32_t N) {
+    return g_stft_variant == 2 ? (float)(0.5 / std::sqrt((double)N)) : 1.0f;
+}
 
 static int launch_stft(const Stft8kArgs &A, uint32_t C, bool fused, bool full, hipStream_t s) {
+    if (g_stft_variant == 2) return launch_stft8192_soa(A, C, fused, s);
     if (g_stft_variant == 1) return launch_stft8192_pair(A, C, fused, s);
     return launch_stft8192(A, C, fused, full, s);
 }
@@ -309,10 +317,10 @@ static int stft_device(const float *const *in, uint32_t C, uint64_t L, uint32_t 
     const float *win = nullptr;
     int st = get_tw(dev, &tw);
     if (st) return st;
-    st = get_window(dev, window, N, N, &win);
-    if (st) return st;
     bool fast = (N == 8192) && (H % 2 == 0);
     for (uint32_t c = 0; c < C; ++c) fast = fast && aligned(in[c], 8);
+    st = get_window(dev, window, N, N, &win, fast ? window_prescale(N) : 1.0);
+    if (st) return st;
     for (uint32_t c0 = 0; c0 < C; c0 += kMaxChannels) {
         const uint32_t cn = (C - c0) < (uint32_t)kMaxChannels ? (C - c0) : kMaxChannels;
         if (fast) {
@@ -375,7 +383,7 @@ int dsp_abi_version(void) { return DSPBENCH_ABI_VERSION; }
 int dsp_stft_kernel_variant(int v) {
     std::lock_guard<std::mutex> lk(g_mu);
     const int old = g_stft_variant;
-    if (v == 0 || v == 1) g_stft_variant = v;
+    if (v >= 0 && v <= 2) g_stft_variant = v;
     return old;
 }
 
@@ -581,7 +589,7 @@ int dsp_render_stft(const float *const *in, uint32_t in_channels, uint64_t L,
         const v2f *tw = nullptr;
         const float *win = nullptr;
         if ((st = get_tw(g.dev, &tw))) return st;
-        if ((st = get_window(g.dev, window, N, N, &win))) return st;
+        if ((st = get_window(g.dev, window, N, N, &win, window_prescale(N)))) return st;
         for (uint32_t c0 = 0; c0 < C; c0 += kMaxChannels) {
             const uint32_t cn = (C - c0) < (uint32_t)kMaxChannels ? (C - c0) : kMaxChannels;
             Stft8kArgs A{};
@@ -669,8 +677,10 @@ int dsp_ir_analysis(const dsp_plugin *plugin, uint32_t C, float sr, uint32_t ir_
     const v2f *tw = nullptr;
     const float *win = nullptr;
     if ((st = get_tw(g.dev, &tw))) return st;
-    if ((st = get_window(g.dev, DSP_WIN_HAMMING, n, ir_len, &win))) return st;
-    if (n == 8192 && aligned(dir[0], 8)) {
+    const bool fast_ir = n == 8192 && aligned(dir[0], 8);
+    if ((st = get_window(g.dev, DSP_WIN_HAMMING, n, ir_len, &win, fast_ir ? window_prescale(n) : 1.0)))
+        return st;
+    if (fast_ir) {
         Stft8kArgs A{};
         A.in.p[0] = dir[0];
         A.in_ch = 1;

@@ -1,0 +1,306 @@
+// stft_soa.hip -- 8192-point STFT kernel, one wavefront per frame, scalar
+// (structure-of-arrays) arithmetic.
+//
+// Same 64 x 64 four-step transform as stft8192_kernel (spectral.hip), written
+// for the CDNA4 VALU as it is actually priced (PMC: ~4 cycles per VALU
+// instruction, packed or not): complex values live as two scalar registers,
+// so multiplying by -i, conjugating and swapping halves are register
+// renames / source modifiers instead of v_mov + v_xor pairs, and the
+// translation unit is built with -fno-slp-vectorize so nothing is re-packed.
+//
+// Further savings over the packed kernel:
+//   * the window table is pre-scaled by 0.5/sqrt(N) (both the IPP
+//     DIV_BY_SQRTN scale and the 1/2 of the real-input split), so no
+//     per-bin scale multiply;
+//   * the real-input split produces X[k] and X[M-k] from ONE (E, W^k O)
+//     pair: X[k] = E + T, X[M-k] = conj(E - T) -- half the partner fetches
+//     (ds_bpermute), twiddles and products; lane 0 pairs within its own
+//     registers (column 0) and adds the self-paired bin k = 2048.
+#include "fft_device.hpp"
+
+namespace dspb {
+
+struct cx {
+    float r, i;
+};
+__device__ __forceinline__ cx operator+(cx a, cx b) { return cx{a.r + b.r, a.i + b.i}; }
+__device__ __forceinline__ cx operator-(cx a, cx b) { return cx{a.r - b.r, a.i - b.i}; }
+__device__ __forceinline__ cx mulc(cx a, float c, float s) {  // a * (c + i s)
+    return cx{__builtin_fmaf(a.r, c, -a.i * s), __builtin_fmaf(a.r, s, a.i * c)};
+}
+__device__ __forceinline__ cx mulc(cx a, cx w) { return mulc(a, w.r, w.i); }
+__device__ __forceinline__ cx negi(cx a) { return cx{a.i, -a.r}; }  // -i a
+
+__device__ __forceinline__ void sdft4(cx &a, cx &b, cx &c, cx &d) {
+    const cx t0 = a + c, t1 = a - c, t2 = b + d, t3 = negi(b - d);
+    a = t0 + t2;
+    c = t0 - t2;
+    b = t1 + t3;
+    d = t1 - t3;
+}
+
+__device__ __forceinline__ void sdft8(cx &u0, cx &u1, cx &u2, cx &u3, cx &u4, cx &u5, cx &u6,
+                                      cx &u7) {
+    cx e0 = u0, e1 = u2, e2 = u4, e3 = u6;
+    cx o0 = u1, o1 = u3, o2 = u5, o3 = u7;
+    sdft4(e0, e1, e2, e3);
+    sdft4(o0, o1, o2, o3);
+    const float r = 0x1.6a09e6p-1f;
+    const cx w1 = cx{(o1.r + o1.i) * r, (o1.i - o1.r) * r};
+    const cx w2 = negi(o2);
+    const cx w3 = cx{(o3.i - o3.r) * r, -(o3.r + o3.i) * r};
+    u0 = e0 + o0; u4 = e0 - o0;
+    u1 = e1 + w1; u5 = e1 - w1;
+    u2 = e2 + w2; u6 = e2 - w2;
+    u3 = e3 + w3; u7 = e3 - w3;
+}
+
+__device__ __forceinline__ cx stw64(cx a, int m) {  // a * W64^m, m compile-time
+    if (m == 0) return a;
+    if (m == 16) return negi(a);
+    if (m == 32) return cx{-a.r, -a.i};
+    if (m == 48) return cx{-a.i, a.r};
+    return mulc(a, kW64_re[m], kW64_im[m]);
+}
+
+// 64-point DFT, natural order in, X[k] at v[perm64(k)] out (8 x 8).
+__device__ __forceinline__ void sdft64(cx (&v)[64]) {
+#pragma unroll
+    for (int b2 = 0; b2 < 8; ++b2) {
+        __builtin_amdgcn_sched_barrier(0);
+        sdft8(v[b2], v[8 + b2], v[16 + b2], v[24 + b2], v[32 + b2], v[40 + b2], v[48 + b2],
+              v[56 + b2]);
+    }
+#pragma unroll
+    for (int k1 = 1; k1 < 8; ++k1)
+#pragma unroll
+        for (int b2 = 1; b2 < 8; ++b2) v[8 * k1 + b2] = stw64(v[8 * k1 + b2], b2 * k1);
+#pragma unroll
+    for (int k1 = 0; k1 < 8; ++k1) {
+        __builtin_amdgcn_sched_barrier(0);
+        sdft8(v[8 * k1], v[8 * k1 + 1], v[8 * k1 + 2], v[8 * k1 + 3], v[8 * k1 + 4],
+              v[8 * k1 + 5], v[8 * k1 + 6], v[8 * k1 + 7]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+template <MapKind MK, bool POW2>
+__device__ __forceinline__ void s_render_frame(const Stft8kArgs &A, const float *x, uint64_t fs,
+                                               uint32_t lane, cx (&v)[64]) {
+    const uint64_t gbase = A.goff + fs;
+    if constexpr (MK == MapKind::Ramp) {
+        const float *T = A.map.table;
+        if constexpr (POW2) {
+            const uint32_t p0 = (uint32_t)gbase + 2u * lane;
+#pragma unroll
+            for (int b = 0; b < 64; ++b) {
+                const v2f t =
+                    *reinterpret_cast<const v2f *>(T + ((p0 + 128u * (uint32_t)b) & A.map.b_mask));
+                v[b] = cx{t.x, t.y};
+            }
+        } else {
+            const uint32_t Bn = A.map.B;
+            uint32_t p = (uint32_t)((gbase + 2u * lane) % Bn);
+#pragma unroll
+            for (int b = 0; b < 64; ++b) {
+                const uint32_t q = (p + 1 == Bn) ? 0u : p + 1;
+                v[b] = cx{T[p], T[q]};
+                p += 128u;
+                while (p >= Bn) p -= Bn;
+            }
+        }
+    } else {
+        if (x != nullptr && fs + 8192u <= A.L) {
+#pragma unroll
+            for (int b = 0; b < 64; ++b) {
+                const v2f t = reinterpret_cast<const v2f *>(x + fs + 128u * (uint32_t)b)[lane];
+                v[b] = cx{t.x, t.y};
+            }
+        } else {
+#pragma unroll
+            for (int b = 0; b < 64; ++b) {
+                const uint64_t li = fs + 2u * lane + 128u * (uint32_t)b;
+                v[b] = cx{(x && li < A.L) ? x[li] : 0.f, (x && li + 1 < A.L) ? x[li + 1] : 0.f};
+            }
+        }
+        if constexpr (MK == MapKind::Gain) {
+#pragma unroll
+            for (int b = 0; b < 64; ++b) v[b] = cx{v[b].r * A.map.a, v[b].i * A.map.a};
+        }
+    }
+}
+
+template <int SRC, int KM, MapKind MK, bool POW2>
+__global__ __launch_bounds__(256, 2) void stft8192_soa_kernel(Stft8kArgs A) {
+    __shared__ float lds_all[4][64 * 65];
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t ch = blockIdx.y;
+    const uint64_t f = (uint64_t)xcd_remap(blockIdx.x, gridDim.x) * 4u + wave;
+    if (f >= A.F) return;  // whole wave leaves; nothing below waits on other waves
+    float *lds = lds_all[wave];
+    const uint64_t fs = f * (uint64_t)A.H;
+    const float *x = (ch < A.in_ch) ? A.in.p[ch] : nullptr;
+
+    // ---- 1. load (+ fused render), window (pre-scaled by 0.5/sqrt N) ------
+    cx v[64];
+    if constexpr (SRC == kSrcMemory) {
+        if (A.valid >= 8192u) {
+#pragma unroll
+            for (int b = 0; b < 64; ++b) {
+                const v2f t = reinterpret_cast<const v2f *>(x + fs + 128u * (uint32_t)b)[lane];
+                v[b] = cx{t.x, t.y};
+            }
+        } else {
+#pragma unroll
+            for (int b = 0; b < 64; ++b) {
+                const uint32_t s = 2u * lane + 128u * (uint32_t)b;
+                v2f t = v2f{0.f, 0.f};
+                if (s < A.valid) t = reinterpret_cast<const v2f *>(x + fs + 128u * (uint32_t)b)[lane];
+                v[b] = cx{t.x, t.y};
+            }
+        }
+    } else {
+        s_render_frame<MK, POW2>(A, x, fs, lane, v);
+        float *o = A.out.p[ch] + fs;
+#pragma unroll
+        for (int b = 0; b < 64; ++b)
+            if (128u * (uint32_t)b < A.H)
+                reinterpret_cast<v2f *>(o + 128u * (uint32_t)b)[lane] = v2f{v[b].r, v[b].i};
+    }
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int b = 16 * g; b < 16 * g + 16; ++b) {
+            const v2f w = (A.win2 + 64u * (uint32_t)b)[lane];
+            v[b] = cx{v[b].r * w.x, v[b].i * w.y};
+        }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+
+    // ---- 2. DFT64 over b -------------------------------------------------
+    sdft64(v);
+
+    // ---- 3. twiddle W4096^(a kb) = W^(a lo) W^(8 a hi), kb = lo + 8 hi ------
+    {
+        cx tlo[8], thi[8];
+#pragma unroll
+        for (int j = 1; j < 8; ++j) {
+            const v2f a = A.tw[2u * lane * (uint32_t)j];
+            const v2f b = A.tw[16u * lane * (uint32_t)j];
+            tlo[j] = cx{a.x, a.y};
+            thi[j] = cx{b.x, b.y};
+        }
+#pragma unroll
+        for (int hi = 0; hi < 8; ++hi) {
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int lo = 0; lo < 8; ++lo) {
+                const int kb = lo + 8 * hi;
+                if (kb == 0) continue;
+                const cx w = lo ? (hi ? mulc(tlo[lo], thi[hi]) : tlo[lo]) : thi[hi];
+                v[perm64(kb)] = mulc(v[perm64(kb)], w);
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+
+    // ---- 4. transpose through LDS, in place (re, then im) ----------------
+#pragma unroll
+    for (int kb = 0; kb < 64; ++kb) lds[lane * 65u + kb] = v[perm64(kb)].r;
+    lds_fence();
+#pragma unroll
+    for (int a = 0; a < 64; ++a) v[a].r = lds[a * 65 + lane];
+    lds_fence();
+#pragma unroll
+    for (int kb = 0; kb < 64; ++kb) lds[lane * 65u + kb] = v[perm64(kb)].i;
+    lds_fence();
+#pragma unroll
+    for (int a = 0; a < 64; ++a) v[a].i = lds[a * 65 + lane];
+
+    // ---- 5. DFT64 over a: Z[lane + 64 ka] at v[perm64(ka)] --------------
+    sdft64(v);
+
+    // ---- 6. paired real split: (k, M-k), k = lane + 64 ka, ka < 32 -----------
+    float *mrow = A.mag.p[ch] + f * A.ld;
+    const uint32_t src = ((64u - lane) & 63u) * 4u;
+    const bool l0 = lane == 0;
+    const v2f wl2 = A.tw[lane];  // W8192^lane
+    const cx wl = cx{wl2.x, wl2.y};
+#pragma unroll
+    for (int ka = 0; ka < 32; ++ka) {
+        if ((ka & 7) == 0) __builtin_amdgcn_sched_barrier(0);
+        const cx zp = v[perm64(63 - ka)];
+        const float tr = bperm(src, zp.r), ti = bperm(src, zp.i);
+        // lane 0 (column 0): Z[M - 64 ka] = its own Z[64 ((64 - ka) & 63)]
+        const cx own = v[perm64((64 - ka) & 63)];
+        const cx P = cx{l0 ? own.r : tr, l0 ? own.i : ti};
+        const cx Z = v[perm64(ka)];
+        const cx E = cx{Z.r + P.r, Z.i - P.i};  // 2 E   (P conjugated)
+        const cx D = cx{Z.r - P.r, Z.i + P.i};  // 2 i O
+        const cx tw = ka == 0 ? wl : mulc(wl, kW128_re[ka], kW128_im[ka]);  // W8192^k
+        const cx T = mulc(negi(D), tw);         // 2 W^k O
+        const cx X1 = E + T;                    // 2 X[k]
+        const cx X2 = E - T;                    // 2 conj X[M - k]
+        const float m1 = __builtin_amdgcn_sqrtf(__builtin_fmaf(X1.r, X1.r, X1.i * X1.i));
+        const float m2 = __builtin_amdgcn_sqrtf(__builtin_fmaf(X2.r, X2.r, X2.i * X2.i));
+        const uint32_t k1 = lane + 64u * (uint32_t)ka;  // < 2048
+        const uint32_t k2 = 4096u - k1;                 // > 2048 (4096 at k1 = 0)
+        if constexpr (KM == kKPartial) {
+            if (k1 < A.K) mrow[k1] = m1;
+            if (k2 < A.K) mrow[k2] = m2;
+        } else {
+            (mrow + 64u * (uint32_t)ka)[lane] = m1;
+            (mrow + 4096u - 64u * (uint32_t)ka)[-(int)lane] = m2;
+            if constexpr (KM == kKMirror) {
+                // |X[8192 - k]| = |X[k]|: bins 4096..8191 (k1 = 0 rewrites bin 0)
+                mrow[k1 == 0 ? 0u : 8192u - k1] = m1;
+                (mrow + 4096u + 64u * (uint32_t)ka)[lane] = m2;
+            }
+        }
+    }
+    if (l0) {  // the self-paired bin k = 2048: |X| = 2 |Z[2048]| (scaled)
+        const cx Z = v[perm64(32)];
+        const float m = 2.f * __builtin_amdgcn_sqrtf(__builtin_fmaf(Z.r, Z.r, Z.i * Z.i));
+        if (KM != kKPartial || 2048u < A.K) mrow[2048] = m;
+        if (KM == kKMirror) mrow[6144] = m;
+    }
+}
+
+template <int SRC, MapKind MK, bool POW2>
+static void launch_soa_km(int km, dim3 grid, hipStream_t s, const Stft8kArgs &A) {
+    if (km == kKHalf)
+        hipLaunchKernelGGL((stft8192_soa_kernel<SRC, kKHalf, MK, POW2>), grid, dim3(256), 0, s, A);
+    else if (km == kKMirror)
+        hipLaunchKernelGGL((stft8192_soa_kernel<SRC, kKMirror, MK, POW2>), grid, dim3(256), 0, s, A);
+    else
+        hipLaunchKernelGGL((stft8192_soa_kernel<SRC, kKPartial, MK, POW2>), grid, dim3(256), 0, s, A);
+}
+
+// A.win2 must hold the window pre-scaled by 0.5 / sqrt(8192).
+int launch_stft8192_soa(const Stft8kArgs &A, uint32_t C, bool fused, hipStream_t stream) {
+    if (A.F == 0 || C == 0) return DSP_OK;
+    const uint64_t groups = (A.F + 3) / 4;
+    if (groups > 0x7fffffffull) return DSP_ERR_INVALID;
+    dim3 grid((uint32_t)groups, C);
+    const int km = A.K == 4097u ? kKHalf : (A.K == 8192u ? kKMirror : kKPartial);
+    const bool pow2 = A.map.b_mask != 0 && A.map.B >= 2;
+    if (fused) {
+        switch (A.map.kind) {
+        case MapKind::Noop: launch_soa_km<kSrcRender, MapKind::Noop, true>(km, grid, stream, A); break;
+        case MapKind::Gain: launch_soa_km<kSrcRender, MapKind::Gain, true>(km, grid, stream, A); break;
+        case MapKind::Ramp:
+            if (pow2) launch_soa_km<kSrcRender, MapKind::Ramp, true>(km, grid, stream, A);
+            else launch_soa_km<kSrcRender, MapKind::Ramp, false>(km, grid, stream, A);
+            break;
+        default: return DSP_ERR_INVALID;
+        }
+    } else {
+        launch_soa_km<kSrcMemory, MapKind::Noop, true>(km, grid, stream, A);
+    }
+    DSPB_HIP(hipGetLastError());
+    return DSP_OK;
+}
+
+}  // namespace dspb
