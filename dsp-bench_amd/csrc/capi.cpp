@@ -154,15 +154,17 @@ struct TimedLaunch {
 static bool g_timing = false;
 // which 8192-point kernel: 0 = one wave per frame, packed (spectral.hip),
 // 1 = two waves per frame (stft_pair.hip), 2 = one wave per frame, scalar
-// SoA with a pre-scaled window (stft_soa.hip)
+// SoA with a pre-scaled window (stft_soa.hip), 3 = two waves per frame,
+// scalar SoA (stft_pair_soa.hip)
 static int g_stft_variant = 2;
 
 // the SoA kernel folds 0.5/sqrt(N) into the window
 static float window_prescale(uint32_t N) {
-    return g_stft_variant == 2 ? (float)(0.5 / std::sqrt((double)N)) : 1.0f;
+    return g_stft_variant >= 2 ? (float)(0.5 / std::sqrt((double)N)) : 1.0f;
 }
 
 static int launch_stft(const Stft8kArgs &A, uint32_t C, bool fused, bool full, hipStream_t s) {
+    if (g_stft_variant == 3) return launch_stft8192_pair_soa(A, C, fused, s);
     if (g_stft_variant == 2) return launch_stft8192_soa(A, C, fused, s);
     if (g_stft_variant == 1) return launch_stft8192_pair(A, C, fused, s);
     return launch_stft8192(A, C, fused, full, s);
@@ -383,7 +385,7 @@ int dsp_abi_version(void) { return DSPBENCH_ABI_VERSION; }
 int dsp_stft_kernel_variant(int v) {
     std::lock_guard<std::mutex> lk(g_mu);
     const int old = g_stft_variant;
-    if (v >= 0 && v <= 2) g_stft_variant = v;
+    if (v >= 0 && v <= 3) g_stft_variant = v;
     return old;
 }
 
