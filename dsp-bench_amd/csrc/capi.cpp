@@ -155,7 +155,8 @@ static bool g_timing = false;
 // which 8192-point kernel: 0 = one wave per frame, packed (spectral.hip),
 // 1 = two waves per frame (stft_pair.hip), 2 = one wave per frame, scalar
 // SoA with a pre-scaled window (stft_soa.hip), 3 = two waves per frame,
-// scalar SoA (stft_pair_soa.hip)
+// scalar SoA (stft_pair_soa.hip), 4 = two frames packed per VGPR pair,
+// two waves per frame pair (stft_pair2.hip)
 static int g_stft_variant = 2;
 
 // the SoA kernel folds 0.5/sqrt(N) into the window
@@ -164,6 +165,7 @@ static float window_prescale(uint32_t N) {
 }
 
 static int launch_stft(const Stft8kArgs &A, uint32_t C, bool fused, bool full, hipStream_t s) {
+    if (g_stft_variant == 4) return launch_stft8192_pair2(A, C, fused, s);
     if (g_stft_variant == 3) return launch_stft8192_pair_soa(A, C, fused, s);
     if (g_stft_variant == 2) return launch_stft8192_soa(A, C, fused, s);
     if (g_stft_variant == 1) return launch_stft8192_pair(A, C, fused, s);
@@ -385,7 +387,7 @@ int dsp_abi_version(void) { return DSPBENCH_ABI_VERSION; }
 int dsp_stft_kernel_variant(int v) {
     std::lock_guard<std::mutex> lk(g_mu);
     const int old = g_stft_variant;
-    if (v >= 0 && v <= 3) g_stft_variant = v;
+    if (v >= 0 && v <= 4) g_stft_variant = v;
     return old;
 }
 

@@ -1,0 +1,78 @@
+// fft_x2.hpp -- FFT building blocks on TWO FRAMES AT ONCE.
+//
+// A cx2 holds the same complex element of two different frames:
+//   r = (Re frame0, Re frame1), i = (Im frame0, Im frame1)
+// so every complex operation is a pair of v_pk_*_f32 instructions that do
+// useful work in both halves, and -i / conjugation / negation are register
+// renames plus neg modifiers -- no v_mov / v_xor to re-pair halves.  On
+// CDNA4 a wave issues about one VALU instruction per 4 cycles packed or not
+// (PMC-measured), so this halves the issue cost of the transform.
+#pragma once
+#include "fft_device.hpp"
+
+namespace dspb {
+
+struct cx2 {
+    v2f r, i;
+};
+__device__ __forceinline__ cx2 operator+(cx2 a, cx2 b) { return cx2{a.r + b.r, a.i + b.i}; }
+__device__ __forceinline__ cx2 operator-(cx2 a, cx2 b) { return cx2{a.r - b.r, a.i - b.i}; }
+__device__ __forceinline__ cx2 negi(cx2 a) { return cx2{a.i, -a.r}; }  // -i a
+// a * (c + i s), c and s the same for both frames
+__device__ __forceinline__ cx2 mulc2(cx2 a, float c, float s) {
+    return cx2{a.r * c - a.i * s, a.r * s + a.i * c};
+}
+
+__device__ __forceinline__ void x2dft4(cx2 &a, cx2 &b, cx2 &c, cx2 &d) {
+    const cx2 t0 = a + c, t1 = a - c, t2 = b + d, t3 = negi(b - d);
+    a = t0 + t2;
+    c = t0 - t2;
+    b = t1 + t3;
+    d = t1 - t3;
+}
+
+__device__ __forceinline__ void x2dft8(cx2 &u0, cx2 &u1, cx2 &u2, cx2 &u3, cx2 &u4, cx2 &u5,
+                                       cx2 &u6, cx2 &u7) {
+    cx2 e0 = u0, e1 = u2, e2 = u4, e3 = u6;
+    cx2 o0 = u1, o1 = u3, o2 = u5, o3 = u7;
+    x2dft4(e0, e1, e2, e3);
+    x2dft4(o0, o1, o2, o3);
+    const float r = 0x1.6a09e6p-1f;
+    const cx2 w1 = cx2{(o1.r + o1.i) * r, (o1.i - o1.r) * r};
+    const cx2 w2 = negi(o2);
+    const cx2 w3 = cx2{(o3.i - o3.r) * r, -((o3.r + o3.i) * r)};
+    u0 = e0 + o0; u4 = e0 - o0;
+    u1 = e1 + w1; u5 = e1 - w1;
+    u2 = e2 + w2; u6 = e2 - w2;
+    u3 = e3 + w3; u7 = e3 - w3;
+}
+
+__device__ __forceinline__ cx2 x2tw64(cx2 a, int m) {  // a * W64^m, m compile-time
+    if (m == 0) return a;
+    if (m == 16) return negi(a);
+    if (m == 32) return cx2{-a.r, -a.i};
+    if (m == 48) return cx2{-a.i, a.r};
+    return mulc2(a, kW64_re[m], kW64_im[m]);
+}
+
+// 32-point DFT, natural order in, X[k] at v[perm32(k)] out (8 x 4).
+__device__ __forceinline__ void x2dft32(cx2 (&v)[32]) {
+#pragma unroll
+    for (int j2 = 0; j2 < 4; ++j2) {
+        __builtin_amdgcn_sched_barrier(0);
+        x2dft8(v[j2], v[4 + j2], v[8 + j2], v[12 + j2], v[16 + j2], v[20 + j2], v[24 + j2],
+               v[28 + j2]);
+    }
+#pragma unroll
+    for (int k1 = 1; k1 < 8; ++k1)
+#pragma unroll
+        for (int j2 = 1; j2 < 4; ++j2) v[4 * k1 + j2] = x2tw64(v[4 * k1 + j2], 2 * j2 * k1);
+#pragma unroll
+    for (int k1 = 0; k1 < 8; ++k1) {
+        __builtin_amdgcn_sched_barrier(0);
+        x2dft4(v[4 * k1], v[4 * k1 + 1], v[4 * k1 + 2], v[4 * k1 + 3]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+}  // namespace dspb

@@ -29,7 +29,7 @@ def rnd(shape, seed):
     return np.random.default_rng(seed).uniform(-1.0, 1.0, size=shape).astype(np.float32)
 
 
-@pytest.fixture(params=[0, 1, 2, 3], ids=["wave", "pair", "soa", "pairsoa"])
+@pytest.fixture(params=[0, 1, 2, 3, 4], ids=["wave", "pair", "soa", "pairsoa", "pair2"])
 def variant(request):
     """Run the test on both 8192-point kernels (dsp_stft_kernel_variant)."""
     L = d.lib()
