@@ -48,6 +48,7 @@ static int invalid(const char *fmt, ...) {
 // ---------------------------------------------------------------------------
 struct DeviceRes {
     v2f *tw8192 = nullptr;                                    // exp(-2 pi i k / 8192)
+    float4 *wbase = nullptr;  // (cos, sin)(theta 2l), (cos, sin)(theta (2l+1)), theta = 2 pi / 8191
     std::map<std::tuple<int, uint32_t, uint32_t, float>, float *> windows;  // (kind, N, valid, scale)
     std::map<void *, std::pair<float *, size_t>> scratch;     // per stream
 };
@@ -123,6 +124,34 @@ static int get_window(int dev, int kind, uint32_t N, uint32_t valid, const float
     return DSP_OK;
 }
 
+static float window_prescale(uint32_t N);
+
+// Inputs of the computed-window kernels (stft_soa.hip kOptWinComp): per-lane
+// base angles and the (pre-scaled) cosine-window coefficients.
+static int set_wincomp(int dev, int kind, Stft8kArgs *A) {
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        DeviceRes &r = g_res[dev];
+        if (!r.wbase) {
+            std::vector<float4> h(64);
+            const double th = 2.0 * M_PI / 8191.0;
+            for (int l = 0; l < 64; ++l)
+                h[l] = float4{(float)std::cos(th * 2 * l), (float)std::sin(th * 2 * l),
+                              (float)std::cos(th * (2 * l + 1)), (float)std::sin(th * (2 * l + 1))};
+            DSPB_HIP(hipMalloc(&r.wbase, sizeof(float4) * 64));
+            DSPB_HIP(hipMemcpy(r.wbase, h.data(), sizeof(float4) * 64, hipMemcpyHostToDevice));
+        }
+        A->wbase = r.wbase;
+    }
+    double a = 0.54, b = 0.46;
+    if (kind == DSP_WIN_HANN) { a = 0.5; b = 0.5; }
+    else if (kind == DSP_WIN_RECT) { a = 1.0; b = 0.0; }
+    const double sc = window_prescale(8192);
+    A->wa = (float)(a * sc);
+    A->wb = (float)(b * sc);
+    return DSP_OK;
+}
+
 // Stream-ordered scratch: calls on one stream are serialised by the stream,
 // so one buffer per (device, stream) is enough.
 static int get_scratch(int dev, hipStream_t s, size_t bytes, float **out) {
@@ -158,6 +187,7 @@ static bool g_timing = false;
 // scalar SoA (stft_pair_soa.hip), 4 = two frames packed per VGPR pair,
 // two waves per frame pair (stft_pair2.hip)
 static int g_stft_variant = 2;
+static int g_soa_opt = 0;  // stft_soa.hip OPT bits (A/B)
 
 // the SoA kernel folds 0.5/sqrt(N) into the window
 static float window_prescale(uint32_t N) {
@@ -167,7 +197,7 @@ static float window_prescale(uint32_t N) {
 static int launch_stft(const Stft8kArgs &A, uint32_t C, bool fused, bool full, hipStream_t s) {
     if (g_stft_variant == 4) return launch_stft8192_pair2(A, C, fused, s);
     if (g_stft_variant == 3) return launch_stft8192_pair_soa(A, C, fused, s);
-    if (g_stft_variant == 2) return launch_stft8192_soa(A, C, fused, s);
+    if (g_stft_variant == 2) return launch_stft8192_soa(A, C, fused, g_soa_opt, s);
     if (g_stft_variant == 1) return launch_stft8192_pair(A, C, fused, s);
     return launch_stft8192(A, C, fused, full, s);
 }
@@ -343,6 +373,7 @@ static int stft_device(const float *const *in, uint32_t C, uint64_t L, uint32_t 
             A.win2 = reinterpret_cast<const v2f *>(win);
             A.tw = tw;
             A.scale = (float)(1.0 / std::sqrt((double)N));
+            if ((st = set_wincomp(dev, window, &A))) return st;
             TimedLaunch tl{};
             if ((st = timing_begin(s, &tl))) return st;
             st = launch_stft(A, cn, false, true, s);
@@ -383,6 +414,13 @@ using namespace dspb;
 extern "C" {
 
 int dsp_abi_version(void) { return DSPBENCH_ABI_VERSION; }
+
+int dsp_stft_soa_options(int opt) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    const int old = g_soa_opt;
+    if (opt >= 0 && opt <= 7) g_soa_opt = opt;
+    return old;
+}
 
 int dsp_stft_kernel_variant(int v) {
     std::lock_guard<std::mutex> lk(g_mu);
@@ -615,6 +653,7 @@ int dsp_render_stft(const float *const *in, uint32_t in_channels, uint64_t L,
             A.win2 = reinterpret_cast<const v2f *>(win);
             A.tw = tw;
             A.scale = (float)(1.0 / std::sqrt((double)N));
+            if ((st = set_wincomp(g.dev, window, &A))) return st;
             A.map = map;
             A.goff = goff;
             TimedLaunch tl{};

@@ -5,6 +5,21 @@
 
 namespace dspb {
 
+// Phase clocks for the diagnostic build (tools/stamps.hip): lane 0 of each
+// wave records s_memtime at phase boundaries.  Compiled out otherwise.
+#ifdef DSPB_STAMPS
+#define DSPB_STAMP(A, f, lane, i)                                                         \
+    do {                                                                                \
+        __builtin_amdgcn_sched_barrier(0);                                              \
+        uint64_t t_;                                                                    \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");        \
+        if ((lane) == 0) (A).stamps[(f) * 8 + (i)] = t_;                                \
+        __builtin_amdgcn_sched_barrier(0);                                              \
+    } while (0)
+#else
+#define DSPB_STAMP(A, f, lane, i) do { } while (0)
+#endif
+
 __device__ __forceinline__ v2f cmul(v2f a, v2f b) {
     return v2f{a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x};
 }

@@ -51,10 +51,12 @@ __device__ __forceinline__ cx stw64(cx a, int m) {  // a * W64^m, m compile-time
 }
 
 // 64-point DFT, natural order in, X[k] at v[perm64(k)] out (8 x 8).
+// BAR: pin one DFT8 at a time (bounds register pressure, costs ILP).
+template <bool BAR = true>
 __device__ __forceinline__ void sdft64(cx (&v)[64]) {
 #pragma unroll
     for (int b2 = 0; b2 < 8; ++b2) {
-        __builtin_amdgcn_sched_barrier(0);
+        if (BAR) __builtin_amdgcn_sched_barrier(0);
         sdft8(v[b2], v[8 + b2], v[16 + b2], v[24 + b2], v[32 + b2], v[40 + b2], v[48 + b2],
               v[56 + b2]);
     }
@@ -64,7 +66,7 @@ __device__ __forceinline__ void sdft64(cx (&v)[64]) {
         for (int b2 = 1; b2 < 8; ++b2) v[8 * k1 + b2] = stw64(v[8 * k1 + b2], b2 * k1);
 #pragma unroll
     for (int k1 = 0; k1 < 8; ++k1) {
-        __builtin_amdgcn_sched_barrier(0);
+        if (BAR) __builtin_amdgcn_sched_barrier(0);
         sdft8(v[8 * k1], v[8 * k1 + 1], v[8 * k1 + 2], v[8 * k1 + 3], v[8 * k1 + 4],
               v[8 * k1 + 5], v[8 * k1 + 6], v[8 * k1 + 7]);
     }

@@ -34,6 +34,9 @@ struct Stft8kArgs {
     float scale;         // 1 / sqrt(8192)
     SampleMap map;       // fused render map
     uint64_t goff;       // global sample index of in[c][0] / out[c][0]
+    uint64_t *stamps;    // diagnostic builds only (-DDSPB_STAMPS): per-frame phase clocks
+    const float4 *wbase; // computed-window variants: (cos, sin) of theta (2 lane), theta (2 lane + 1)
+    float wa, wb;        // window w = wa - wb cos(theta n), pre-scaled
 };
 
 struct GenericFftArgs {
@@ -61,7 +64,7 @@ int launch_ramp_table(float *table, uint32_t B, float gain, float step, hipStrea
 int launch_render(const RenderArgs &A, uint32_t C, bool vec, hipStream_t s);
 int launch_stft8192(const Stft8kArgs &A, uint32_t C, bool fused, bool full, hipStream_t s);
 int launch_stft8192_pair(const Stft8kArgs &A, uint32_t C, bool fused, hipStream_t s);
-int launch_stft8192_soa(const Stft8kArgs &A, uint32_t C, bool fused, hipStream_t s);
+int launch_stft8192_soa(const Stft8kArgs &A, uint32_t C, bool fused, int opt, hipStream_t s);
 int launch_stft8192_pair_soa(const Stft8kArgs &A, uint32_t C, bool fused, hipStream_t s);
 int launch_stft8192_pair2(const Stft8kArgs &A, uint32_t C, bool fused, hipStream_t s);
 int launch_fft_generic(const GenericFftArgs &A, uint64_t transforms, uint32_t C, hipStream_t s);

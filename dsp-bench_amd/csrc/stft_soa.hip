@@ -66,7 +66,11 @@ __device__ __forceinline__ void s_render_frame(const Stft8kArgs &A, const float 
     }
 }
 
-template <int SRC, int KM, MapKind MK, bool POW2>
+// OPT bits (A/B-selectable, see dsp_stft_soa_options):
+enum { kOptNoBar = 1, kOptPrefetchTw = 2, kOptWinComp = 4 };
+constexpr int kSoaDefaultOpt = 0;
+
+template <int SRC, int KM, MapKind MK, bool POW2, int OPT>
 __global__ __launch_bounds__(256, 2) void stft8192_soa_kernel(Stft8kArgs A) {
     __shared__ float lds_all[4][64 * 65];
     const uint32_t lane = threadIdx.x & 63u;
@@ -75,8 +79,24 @@ __global__ __launch_bounds__(256, 2) void stft8192_soa_kernel(Stft8kArgs A) {
     const uint64_t f = (uint64_t)xcd_remap(blockIdx.x, gridDim.x) * 4u + wave;
     if (f >= A.F) return;  // whole wave leaves; nothing below waits on other waves
     float *lds = lds_all[wave];
+    DSPB_STAMP(A, f, lane, 0);
     const uint64_t fs = f * (uint64_t)A.H;
     const float *x = (ch < A.in_ch) ? A.in.p[ch] : nullptr;
+
+    // twiddle factors W4096^(a lo), W4096^(8 a hi) for step 3 (early: their
+    // L2 latency then hides under the frame load and the first DFT)
+    cx tlo[8], thi[8];
+    if constexpr (OPT & kOptPrefetchTw) {
+#pragma unroll
+        for (int j = 1; j < 8; ++j) {
+            const v2f a = A.tw[2u * lane * (uint32_t)j];
+            const v2f b = A.tw[16u * lane * (uint32_t)j];
+            tlo[j] = cx{a.x, a.y};
+            thi[j] = cx{b.x, b.y};
+        }
+    }
+    float4 wbase = float4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (OPT & kOptWinComp) wbase = A.wbase[lane];
 
     // ---- 1. load (+ fused render), window (pre-scaled by 0.5/sqrt N) ------
     cx v[64];
@@ -104,29 +124,43 @@ __global__ __launch_bounds__(256, 2) void stft8192_soa_kernel(Stft8kArgs A) {
             if (128u * (uint32_t)b < A.H)
                 reinterpret_cast<v2f *>(o + 128u * (uint32_t)b)[lane] = v2f{v[b].r, v[b].i};
     }
+    if constexpr (OPT & kOptWinComp) {
+        // w(n) = wa - wb cos(theta n), n = 2 lane + e + 128 b:
+        // cos(alpha_e + beta_b) = C_e cos(beta_b) - S_e sin(beta_b)
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-        __builtin_amdgcn_sched_barrier(0);
+        for (int b = 0; b < 64; ++b) {
+            const float t0 = __builtin_fmaf(wbase.x, kWinB_c[b], -wbase.y * kWinB_s[b]);
+            const float t1 = __builtin_fmaf(wbase.z, kWinB_c[b], -wbase.w * kWinB_s[b]);
+            v[b] = cx{v[b].r * __builtin_fmaf(-A.wb, t0, A.wa), v[b].i * __builtin_fmaf(-A.wb, t1, A.wa)};
+        }
+    } else {
 #pragma unroll
-        for (int b = 16 * g; b < 16 * g + 16; ++b) {
-            const v2f w = (A.win2 + 64u * (uint32_t)b)[lane];
-            v[b] = cx{v[b].r * w.x, v[b].i * w.y};
+        for (int g = 0; g < 4; ++g) {
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int b = 16 * g; b < 16 * g + 16; ++b) {
+                const v2f w = (A.win2 + 64u * (uint32_t)b)[lane];
+                v[b] = cx{v[b].r * w.x, v[b].i * w.y};
+            }
         }
     }
     __builtin_amdgcn_sched_barrier(0);
 
+    DSPB_STAMP(A, f, lane, 1);
     // ---- 2. DFT64 over b -------------------------------------------------
-    sdft64(v);
+    sdft64<!(OPT & kOptNoBar)>(v);
+    DSPB_STAMP(A, f, lane, 2);
 
     // ---- 3. twiddle W4096^(a kb) = W^(a lo) W^(8 a hi), kb = lo + 8 hi ------
     {
-        cx tlo[8], thi[8];
+        if constexpr (!(OPT & kOptPrefetchTw)) {
 #pragma unroll
-        for (int j = 1; j < 8; ++j) {
-            const v2f a = A.tw[2u * lane * (uint32_t)j];
-            const v2f b = A.tw[16u * lane * (uint32_t)j];
-            tlo[j] = cx{a.x, a.y};
-            thi[j] = cx{b.x, b.y};
+            for (int j = 1; j < 8; ++j) {
+                const v2f a = A.tw[2u * lane * (uint32_t)j];
+                const v2f b = A.tw[16u * lane * (uint32_t)j];
+                tlo[j] = cx{a.x, a.y};
+                thi[j] = cx{b.x, b.y};
+            }
         }
 #pragma unroll
         for (int hi = 0; hi < 8; ++hi) {
@@ -142,6 +176,7 @@ __global__ __launch_bounds__(256, 2) void stft8192_soa_kernel(Stft8kArgs A) {
         __builtin_amdgcn_sched_barrier(0);
     }
 
+    DSPB_STAMP(A, f, lane, 3);
     // ---- 4. transpose through LDS, in place (re, then im) ----------------
 #pragma unroll
     for (int kb = 0; kb < 64; ++kb) lds[lane * 65u + kb] = v[perm64(kb)].r;
@@ -155,8 +190,10 @@ __global__ __launch_bounds__(256, 2) void stft8192_soa_kernel(Stft8kArgs A) {
 #pragma unroll
     for (int a = 0; a < 64; ++a) v[a].i = lds[a * 65 + lane];
 
+    DSPB_STAMP(A, f, lane, 4);
     // ---- 5. DFT64 over a: Z[lane + 64 ka] at v[perm64(ka)] --------------
-    sdft64(v);
+    sdft64<!(OPT & kOptNoBar)>(v);
+    DSPB_STAMP(A, f, lane, 5);
 
     // ---- 6. paired real split: (k, M-k), k = lane + 64 ka, ka < 32 -----------
     float *mrow = A.mag.p[ch] + f * A.ld;
@@ -202,38 +239,61 @@ __global__ __launch_bounds__(256, 2) void stft8192_soa_kernel(Stft8kArgs A) {
         if (KM != kKPartial || 2048u < A.K) mrow[2048] = m;
         if (KM == kKMirror) mrow[6144] = m;
     }
+    DSPB_STAMP(A, f, lane, 6);
 }
 
-template <int SRC, MapKind MK, bool POW2>
+template <int SRC, MapKind MK, bool POW2, int OPT>
 static void launch_soa_km(int km, dim3 grid, hipStream_t s, const Stft8kArgs &A) {
     if (km == kKHalf)
-        hipLaunchKernelGGL((stft8192_soa_kernel<SRC, kKHalf, MK, POW2>), grid, dim3(256), 0, s, A);
+        hipLaunchKernelGGL((stft8192_soa_kernel<SRC, kKHalf, MK, POW2, OPT>), grid, dim3(256), 0, s, A);
     else if (km == kKMirror)
-        hipLaunchKernelGGL((stft8192_soa_kernel<SRC, kKMirror, MK, POW2>), grid, dim3(256), 0, s, A);
+        hipLaunchKernelGGL((stft8192_soa_kernel<SRC, kKMirror, MK, POW2, OPT>), grid, dim3(256), 0, s, A);
     else
-        hipLaunchKernelGGL((stft8192_soa_kernel<SRC, kKPartial, MK, POW2>), grid, dim3(256), 0, s, A);
+        hipLaunchKernelGGL((stft8192_soa_kernel<SRC, kKPartial, MK, POW2, OPT>), grid, dim3(256), 0, s, A);
 }
 
-// A.win2 must hold the window pre-scaled by 0.5 / sqrt(8192).
-int launch_stft8192_soa(const Stft8kArgs &A, uint32_t C, bool fused, hipStream_t stream) {
+// the headline shapes (IR_test-fused and memory-source, 4097 bins) can run
+// every OPT combination for A/B; everything else runs kSoaDefaultOpt
+template <int SRC, MapKind MK>
+static void launch_soa_ab(int opt, dim3 grid, hipStream_t s, const Stft8kArgs &A) {
+    switch (opt & 7) {
+    case 0: hipLaunchKernelGGL((stft8192_soa_kernel<SRC, kKHalf, MK, true, 0>), grid, dim3(256), 0, s, A); break;
+    case 1: hipLaunchKernelGGL((stft8192_soa_kernel<SRC, kKHalf, MK, true, 1>), grid, dim3(256), 0, s, A); break;
+    case 2: hipLaunchKernelGGL((stft8192_soa_kernel<SRC, kKHalf, MK, true, 2>), grid, dim3(256), 0, s, A); break;
+    case 3: hipLaunchKernelGGL((stft8192_soa_kernel<SRC, kKHalf, MK, true, 3>), grid, dim3(256), 0, s, A); break;
+    case 4: hipLaunchKernelGGL((stft8192_soa_kernel<SRC, kKHalf, MK, true, 4>), grid, dim3(256), 0, s, A); break;
+    case 5: hipLaunchKernelGGL((stft8192_soa_kernel<SRC, kKHalf, MK, true, 5>), grid, dim3(256), 0, s, A); break;
+    case 6: hipLaunchKernelGGL((stft8192_soa_kernel<SRC, kKHalf, MK, true, 6>), grid, dim3(256), 0, s, A); break;
+    default: hipLaunchKernelGGL((stft8192_soa_kernel<SRC, kKHalf, MK, true, 7>), grid, dim3(256), 0, s, A); break;
+    }
+}
+
+// A.win2 must hold the window pre-scaled by 0.5 / sqrt(8192); with
+// kOptWinComp also A.wbase / A.wa / A.wb (valid == 8192 only).
+int launch_stft8192_soa(const Stft8kArgs &A, uint32_t C, bool fused, int opt, hipStream_t stream) {
     if (A.F == 0 || C == 0) return DSP_OK;
     const uint64_t groups = (A.F + 3) / 4;
     if (groups > 0x7fffffffull) return DSP_ERR_INVALID;
     dim3 grid((uint32_t)groups, C);
     const int km = A.K == 4097u ? kKHalf : (A.K == 8192u ? kKMirror : kKPartial);
     const bool pow2 = A.map.b_mask != 0 && A.map.B >= 2;
+    if (A.valid < 8192u || !A.wbase) opt &= ~kOptWinComp;  // computed window: full frames only
+    constexpr int D = kSoaDefaultOpt;
     if (fused) {
         switch (A.map.kind) {
-        case MapKind::Noop: launch_soa_km<kSrcRender, MapKind::Noop, true>(km, grid, stream, A); break;
-        case MapKind::Gain: launch_soa_km<kSrcRender, MapKind::Gain, true>(km, grid, stream, A); break;
+        case MapKind::Noop: launch_soa_km<kSrcRender, MapKind::Noop, true, D & 3>(km, grid, stream, A); break;
+        case MapKind::Gain: launch_soa_km<kSrcRender, MapKind::Gain, true, D & 3>(km, grid, stream, A); break;
         case MapKind::Ramp:
-            if (pow2) launch_soa_km<kSrcRender, MapKind::Ramp, true>(km, grid, stream, A);
-            else launch_soa_km<kSrcRender, MapKind::Ramp, false>(km, grid, stream, A);
+            if (pow2 && km == kKHalf) launch_soa_ab<kSrcRender, MapKind::Ramp>(opt, grid, stream, A);
+            else if (pow2) launch_soa_km<kSrcRender, MapKind::Ramp, true, D & 3>(km, grid, stream, A);
+            else launch_soa_km<kSrcRender, MapKind::Ramp, false, D & 3>(km, grid, stream, A);
             break;
         default: return DSP_ERR_INVALID;
         }
+    } else if (km == kKHalf) {
+        launch_soa_ab<kSrcMemory, MapKind::Noop>(opt, grid, stream, A);
     } else {
-        launch_soa_km<kSrcMemory, MapKind::Noop, true>(km, grid, stream, A);
+        launch_soa_km<kSrcMemory, MapKind::Noop, true, D & 3>(km, grid, stream, A);
     }
     DSPB_HIP(hipGetLastError());
     return DSP_OK;

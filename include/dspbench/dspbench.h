@@ -157,6 +157,12 @@ int dsp_kernel_timing(double *total_ms, uint64_t *launches, uint64_t *bytes);
  * Returns the previous selection. */
 int dsp_stft_kernel_variant(int variant);
 
+/* Option bits of variant 2 (A/B): 1 = no scheduling barrier inside the
+ * register DFTs, 2 = prefetch the stage twiddles with the frame load,
+ * 4 = compute the window (angle addition) instead of loading it.
+ * Returns the previous options. */
+int dsp_stft_soa_options(int options);
+
 /* Diagnostics. */
 int dsp_abi_version(void);
 const char *dsp_status_string(int status);

@@ -256,3 +256,25 @@ def test_full_size_ir_test_stft_1h(torch_cuda, oracle, variant):
             assert peak_rel_err(mag[c, f].cpu().numpy(), ref0) <= PEAK_REL_TOL
         spread = (mag[c] - mag[c, :1]).abs().max().item()
         assert spread <= 1e-6 * float(ref0.max())
+
+
+@pytest.mark.parametrize("opt", range(8))
+def test_soa_kernel_options(torch_cuda, oracle, opt):
+    """Every A/B option combination of the SoA kernel (dsp_stft_soa_options)
+    on the fused IR_test path and the memory path, 4097 bins."""
+    L = d.lib()
+    oldv, oldo = L.dsp_stft_kernel_variant(2), L.dsp_stft_soa_options(opt)
+    try:
+        n, B = 8192 * 5 + 99, 512
+        x = rnd((2, n), 61)
+        for win in (d.DSP_WIN_HANN, d.DSP_WIN_HAMMING):
+            out, mag = d.render_stft(to_dev(torch_cuda, x), 2, B, 48000.0, d.Plugin.ir_test(), window=win)
+            ref = oracle.render_offline([x[0], x[1]], 2, B, 48000.0, oracle.restated_plugin("IR_test"))
+            assert np.array_equal(out.cpu().numpy(), ref)
+            mref = oracle.np_stft_mag(ref[0], 8192, 4096, win, 4097)
+            assert peak_rel_err(mag.cpu().numpy()[0], mref) <= PEAK_REL_TOL
+            m2 = d.stft_magnitude(to_dev(torch_cuda, x), window=win).cpu().numpy()
+            assert peak_rel_err(m2[1], oracle.np_stft_mag(x[1], 8192, 4096, win, 4097)) <= PEAK_REL_TOL
+    finally:
+        L.dsp_stft_kernel_variant(oldv)
+        L.dsp_stft_soa_options(oldo)
