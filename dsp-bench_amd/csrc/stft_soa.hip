@@ -68,6 +68,12 @@ __device__ __forceinline__ void s_render_frame(const Stft8kArgs &A, const float 
 
 // OPT bits (A/B-selectable, see dsp_stft_soa_options):
 enum { kOptNoBar = 1, kOptPrefetchTw = 2, kOptWinComp = 4 };
+// Phase ablation for the diagnostic build (tools/stamps.hip): skip pieces
+// to price them.  DSPB_ABLATE is 0 in every shipped build.
+#ifndef DSPB_ABLATE
+#define DSPB_ABLATE 0
+#endif
+enum { kAbLoad = 1, kAbWindow = 2, kAbDft1 = 4, kAbTw = 8, kAbLds = 16, kAbDft2 = 32, kAbSplit = 64 };
 constexpr int kSoaDefaultOpt = 0;
 
 template <int SRC, int KM, MapKind MK, bool POW2, int OPT>
@@ -116,6 +122,9 @@ __global__ __launch_bounds__(256, 2) void stft8192_soa_kernel(Stft8kArgs A) {
                 v[b] = cx{t.x, t.y};
             }
         }
+    } else if (DSPB_ABLATE & kAbLoad) {
+#pragma unroll
+        for (int b = 0; b < 64; ++b) v[b] = cx{(float)lane * 1e-3f + b, (float)b * 1e-3f - lane};
     } else {
         s_render_frame<MK, POW2>(A, x, fs, lane, v);
         float *o = A.out.p[ch] + fs;
@@ -124,7 +133,8 @@ __global__ __launch_bounds__(256, 2) void stft8192_soa_kernel(Stft8kArgs A) {
             if (128u * (uint32_t)b < A.H)
                 reinterpret_cast<v2f *>(o + 128u * (uint32_t)b)[lane] = v2f{v[b].r, v[b].i};
     }
-    if constexpr (OPT & kOptWinComp) {
+    if constexpr (DSPB_ABLATE & kAbWindow) {
+    } else if constexpr (OPT & kOptWinComp) {
         // w(n) = wa - wb cos(theta n), n = 2 lane + e + 128 b:
         // cos(alpha_e + beta_b) = C_e cos(beta_b) - S_e sin(beta_b)
 #pragma unroll
@@ -148,7 +158,7 @@ __global__ __launch_bounds__(256, 2) void stft8192_soa_kernel(Stft8kArgs A) {
 
     DSPB_STAMP(A, f, lane, 1);
     // ---- 2. DFT64 over b -------------------------------------------------
-    sdft64<!(OPT & kOptNoBar)>(v);
+    if (!(DSPB_ABLATE & kAbDft1)) sdft64<!(OPT & kOptNoBar)>(v);
     DSPB_STAMP(A, f, lane, 2);
 
     // ---- 3. twiddle W4096^(a kb) = W^(a lo) W^(8 a hi), kb = lo + 8 hi ------
@@ -164,6 +174,7 @@ __global__ __launch_bounds__(256, 2) void stft8192_soa_kernel(Stft8kArgs A) {
         }
 #pragma unroll
         for (int hi = 0; hi < 8; ++hi) {
+            if (DSPB_ABLATE & kAbTw) break;
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int lo = 0; lo < 8; ++lo) {
@@ -178,6 +189,7 @@ __global__ __launch_bounds__(256, 2) void stft8192_soa_kernel(Stft8kArgs A) {
 
     DSPB_STAMP(A, f, lane, 3);
     // ---- 4. transpose through LDS, in place (re, then im) ----------------
+    if constexpr (!(DSPB_ABLATE & kAbLds)) {
 #pragma unroll
     for (int kb = 0; kb < 64; ++kb) lds[lane * 65u + kb] = v[perm64(kb)].r;
     lds_fence();
@@ -189,14 +201,21 @@ __global__ __launch_bounds__(256, 2) void stft8192_soa_kernel(Stft8kArgs A) {
     lds_fence();
 #pragma unroll
     for (int a = 0; a < 64; ++a) v[a].i = lds[a * 65 + lane];
+    }
 
     DSPB_STAMP(A, f, lane, 4);
     // ---- 5. DFT64 over a: Z[lane + 64 ka] at v[perm64(ka)] --------------
-    sdft64<!(OPT & kOptNoBar)>(v);
+    if (!(DSPB_ABLATE & kAbDft2)) sdft64<!(OPT & kOptNoBar)>(v);
     DSPB_STAMP(A, f, lane, 5);
 
     // ---- 6. paired real split: (k, M-k), k = lane + 64 ka, ka < 32 -----------
     float *mrow = A.mag.p[ch] + f * A.ld;
+    if constexpr (DSPB_ABLATE & kAbSplit) {
+#pragma unroll
+        for (int ka = 0; ka < 64; ++ka) (mrow + 64u * (uint32_t)ka)[lane] = v[ka].r + v[ka].i;
+        DSPB_STAMP(A, f, lane, 6);
+        return;
+    }
     const uint32_t src = ((64u - lane) & 63u) * 4u;
     const bool l0 = lane == 0;
     const v2f wl2 = A.tw[lane];  // W8192^lane

@@ -10,6 +10,9 @@
 #include <algorithm>
 #include <cstdlib>
 
+#ifndef STAMP_OPT
+#define STAMP_OPT 0
+#endif
 #include "stft_soa.hip"
 
 namespace dspb {
@@ -65,7 +68,7 @@ int main(int argc, char **argv) {
     float ms = 0;
     for (int it = 0; it < 5; ++it) {
         CK(hipEventRecord(e0));
-        hipLaunchKernelGGL((stft8192_soa_kernel<kSrcRender, kKHalf, MapKind::Ramp, true>), grid, dim3(256), 0, 0, A);
+        hipLaunchKernelGGL((stft8192_soa_kernel<kSrcRender, kKHalf, MapKind::Ramp, true, STAMP_OPT>), grid, dim3(256), 0, 0, A);
         CK(hipEventRecord(e1));
         CK(hipEventSynchronize(e1));
         CK(hipEventElapsedTime(&ms, e0, e1));
