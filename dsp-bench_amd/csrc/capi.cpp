@@ -47,7 +47,7 @@ static int invalid(const char *fmt, ...) {
 // per-device resources
 // ---------------------------------------------------------------------------
 struct DeviceRes {
-    v2f *tw8192 = nullptr;                                    // exp(-2 pi i k / 8192)
+    v2f *tw8192 = nullptr;  // exp(-2 pi i k / 8192), then 896 lane-major stage twiddles
     float4 *wbase = nullptr;  // (cos, sin)(theta 2l), (cos, sin)(theta (2l+1)), theta = 2 pi / 8191
     std::map<std::tuple<int, uint32_t, uint32_t, float>, float *> windows;  // (kind, N, valid, scale)
     std::map<void *, std::pair<float *, size_t>> scratch;     // per stream
@@ -93,8 +93,14 @@ static int get_tw(int dev, const v2f **out) {
         // exact zeros / ones at the quarter turns
         h[0] = v2f{1.f, 0.f}; h[2048] = v2f{0.f, -1.f};
         h[4096] = v2f{-1.f, 0.f}; h[6144] = v2f{0.f, 1.f};
-        DSPB_HIP(hipMalloc(&r.tw8192, sizeof(v2f) * 8192));
-        DSPB_HIP(hipMemcpy(r.tw8192, h.data(), sizeof(v2f) * 8192, hipMemcpyHostToDevice));
+        // lane-major stage twiddles of the 64 x 64 step (stft_soa.hip):
+        // [8192 + 64 (j-1) + l] = T[2 l j], [8192 + 448 + 64 (j-1) + l] = T[16 l j]
+        for (int j = 1; j < 8; ++j)
+            for (int l = 0; l < 64; ++l) h.push_back(h[(2 * l * j) & 8191]);
+        for (int j = 1; j < 8; ++j)
+            for (int l = 0; l < 64; ++l) h.push_back(h[(16 * l * j) & 8191]);
+        DSPB_HIP(hipMalloc(&r.tw8192, sizeof(v2f) * h.size()));
+        DSPB_HIP(hipMemcpy(r.tw8192, h.data(), sizeof(v2f) * h.size(), hipMemcpyHostToDevice));
     }
     *out = r.tw8192;
     return DSP_OK;
@@ -187,7 +193,7 @@ static bool g_timing = false;
 // scalar SoA (stft_pair_soa.hip), 4 = two frames packed per VGPR pair,
 // two waves per frame pair (stft_pair2.hip)
 static int g_stft_variant = 2;
-static int g_soa_opt = 0;  // stft_soa.hip OPT bits (A/B)
+static int g_soa_opt = 14;  // stft_soa.hip OPT bits (A/B), default kSoaDefaultOpt
 
 // the SoA kernel folds 0.5/sqrt(N) into the window
 static float window_prescale(uint32_t N) {
@@ -418,7 +424,7 @@ int dsp_abi_version(void) { return DSPBENCH_ABI_VERSION; }
 int dsp_stft_soa_options(int opt) {
     std::lock_guard<std::mutex> lk(g_mu);
     const int old = g_soa_opt;
-    if (opt >= 0 && opt <= 7) g_soa_opt = opt;
+    if (opt >= 0 && opt <= 15) g_soa_opt = opt;
     return old;
 }
 

@@ -67,18 +67,27 @@ __device__ __forceinline__ void s_render_frame(const Stft8kArgs &A, const float 
 }
 
 // OPT bits (A/B-selectable, see dsp_stft_soa_options):
-enum { kOptNoBar = 1, kOptPrefetchTw = 2, kOptWinComp = 4 };
+//   kOptNoBar      no scheduling barriers inside the DFT64 passes
+//   kOptPrefetchTw stage twiddles from the lane-major table, issued first
+//   kOptWinComp    window computed from per-lane base angles (no table loads)
+//   kOptLdsTable   IR ramp table staged through the wave's LDS tile (pow2 B
+//                  <= 4096): 2 coalesced loads per lane instead of 64 gathers
+enum { kOptNoBar = 1, kOptPrefetchTw = 2, kOptWinComp = 4, kOptLdsTable = 8 };
 // Phase ablation for the diagnostic build (tools/stamps.hip): skip pieces
 // to price them.  DSPB_ABLATE is 0 in every shipped build.
 #ifndef DSPB_ABLATE
 #define DSPB_ABLATE 0
 #endif
 enum { kAbLoad = 1, kAbWindow = 2, kAbDft1 = 4, kAbTw = 8, kAbLds = 16, kAbDft2 = 32, kAbSplit = 64 };
-constexpr int kSoaDefaultOpt = 0;
+// default for the A/B-switchable headline shapes (tools/ab_soa.py, MI355X:
+// fused 0.73 -> 0.65 ms, memory 0.78 -> 0.71 ms per stereo hour vs 0);
+// other shapes run kSoaKmOpt (no computed window: partial frames allowed)
+constexpr int kSoaDefaultOpt = kOptPrefetchTw | kOptWinComp | kOptLdsTable;
+constexpr int kSoaKmOpt = kOptLdsTable;
 
 template <int SRC, int KM, MapKind MK, bool POW2, int OPT>
 __global__ __launch_bounds__(256, 2) void stft8192_soa_kernel(Stft8kArgs A) {
-    __shared__ float lds_all[4][64 * 65];
+    __shared__ __attribute__((aligned(16))) float lds_all[4][64 * 65];
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t ch = blockIdx.y;
@@ -95,8 +104,9 @@ __global__ __launch_bounds__(256, 2) void stft8192_soa_kernel(Stft8kArgs A) {
     if constexpr (OPT & kOptPrefetchTw) {
 #pragma unroll
         for (int j = 1; j < 8; ++j) {
-            const v2f a = A.tw[2u * lane * (uint32_t)j];
-            const v2f b = A.tw[16u * lane * (uint32_t)j];
+            // lane-major copies (capi.cpp get_tw): one coalesced 512-B row each
+            const v2f a = (A.tw + 8192u + 64u * (uint32_t)(j - 1))[lane];
+            const v2f b = (A.tw + 8192u + 448u + 64u * (uint32_t)(j - 1))[lane];
             tlo[j] = cx{a.x, a.y};
             thi[j] = cx{b.x, b.y};
         }
@@ -126,7 +136,39 @@ __global__ __launch_bounds__(256, 2) void stft8192_soa_kernel(Stft8kArgs A) {
 #pragma unroll
         for (int b = 0; b < 64; ++b) v[b] = cx{(float)lane * 1e-3f + b, (float)b * 1e-3f - lane};
     } else {
-        s_render_frame<MK, POW2>(A, x, fs, lane, v);
+        if constexpr ((OPT & kOptLdsTable) && MK == MapKind::Ramp && POW2) {
+            if (A.map.B >= 4u && A.map.B <= 4096u) {
+                const uint32_t q4 = A.map.B >> 2;  // float4s in the table
+                const float4 *T4 = reinterpret_cast<const float4 *>(A.map.table);
+                // groups of 4 float4 per lane: all loads of a group in flight
+                // together (B = 512 is one group, half of it masked off)
+                for (uint32_t g = 0; 256u * g < q4; ++g) {
+                    float4 t4[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const uint32_t i = lane + 64u * (4u * g + (uint32_t)u);
+                        t4[u] = T4[i < q4 ? i : 0u];
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const uint32_t i = lane + 64u * (4u * g + (uint32_t)u);
+                        if (i < q4) reinterpret_cast<float4 *>(lds)[i] = t4[u];
+                    }
+                }
+                lds_fence();
+                const uint32_t p0 = (uint32_t)(A.goff + fs) + 2u * lane;
+#pragma unroll
+                for (int b = 0; b < 64; ++b) {
+                    const v2f t = *reinterpret_cast<const v2f *>(
+                        lds + ((p0 + 128u * (uint32_t)b) & A.map.b_mask));
+                    v[b] = cx{t.x, t.y};
+                }
+            } else {
+                s_render_frame<MK, POW2>(A, x, fs, lane, v);
+            }
+        } else {
+            s_render_frame<MK, POW2>(A, x, fs, lane, v);
+        }
         float *o = A.out.p[ch] + fs;
 #pragma unroll
         for (int b = 0; b < 64; ++b)
@@ -275,15 +317,15 @@ static void launch_soa_km(int km, dim3 grid, hipStream_t s, const Stft8kArgs &A)
 // every OPT combination for A/B; everything else runs kSoaDefaultOpt
 template <int SRC, MapKind MK>
 static void launch_soa_ab(int opt, dim3 grid, hipStream_t s, const Stft8kArgs &A) {
-    switch (opt & 7) {
+    switch (opt & 14) {
     case 0: hipLaunchKernelGGL((stft8192_soa_kernel<SRC, kKHalf, MK, true, 0>), grid, dim3(256), 0, s, A); break;
-    case 1: hipLaunchKernelGGL((stft8192_soa_kernel<SRC, kKHalf, MK, true, 1>), grid, dim3(256), 0, s, A); break;
     case 2: hipLaunchKernelGGL((stft8192_soa_kernel<SRC, kKHalf, MK, true, 2>), grid, dim3(256), 0, s, A); break;
-    case 3: hipLaunchKernelGGL((stft8192_soa_kernel<SRC, kKHalf, MK, true, 3>), grid, dim3(256), 0, s, A); break;
     case 4: hipLaunchKernelGGL((stft8192_soa_kernel<SRC, kKHalf, MK, true, 4>), grid, dim3(256), 0, s, A); break;
-    case 5: hipLaunchKernelGGL((stft8192_soa_kernel<SRC, kKHalf, MK, true, 5>), grid, dim3(256), 0, s, A); break;
     case 6: hipLaunchKernelGGL((stft8192_soa_kernel<SRC, kKHalf, MK, true, 6>), grid, dim3(256), 0, s, A); break;
-    default: hipLaunchKernelGGL((stft8192_soa_kernel<SRC, kKHalf, MK, true, 7>), grid, dim3(256), 0, s, A); break;
+    case 8: hipLaunchKernelGGL((stft8192_soa_kernel<SRC, kKHalf, MK, true, 8>), grid, dim3(256), 0, s, A); break;
+    case 10: hipLaunchKernelGGL((stft8192_soa_kernel<SRC, kKHalf, MK, true, 10>), grid, dim3(256), 0, s, A); break;
+    case 12: hipLaunchKernelGGL((stft8192_soa_kernel<SRC, kKHalf, MK, true, 12>), grid, dim3(256), 0, s, A); break;
+    default: hipLaunchKernelGGL((stft8192_soa_kernel<SRC, kKHalf, MK, true, 14>), grid, dim3(256), 0, s, A); break;
     }
 }
 
@@ -296,23 +338,25 @@ int launch_stft8192_soa(const Stft8kArgs &A, uint32_t C, bool fused, int opt, hi
     dim3 grid((uint32_t)groups, C);
     const int km = A.K == 4097u ? kKHalf : (A.K == 8192u ? kKMirror : kKPartial);
     const bool pow2 = A.map.b_mask != 0 && A.map.B >= 2;
-    if (A.valid < 8192u || !A.wbase) opt &= ~kOptWinComp;  // computed window: full frames only
-    constexpr int D = kSoaDefaultOpt;
+    // computed window: full frames only (the twiddle prefetch is a loss
+    // without it: too many loads in flight)
+    if (A.valid < 8192u || !A.wbase) opt &= ~(kOptWinComp | kOptPrefetchTw);
+    constexpr int D = kSoaKmOpt;
     if (fused) {
         switch (A.map.kind) {
-        case MapKind::Noop: launch_soa_km<kSrcRender, MapKind::Noop, true, D & 3>(km, grid, stream, A); break;
-        case MapKind::Gain: launch_soa_km<kSrcRender, MapKind::Gain, true, D & 3>(km, grid, stream, A); break;
+        case MapKind::Noop: launch_soa_km<kSrcRender, MapKind::Noop, true, D>(km, grid, stream, A); break;
+        case MapKind::Gain: launch_soa_km<kSrcRender, MapKind::Gain, true, D>(km, grid, stream, A); break;
         case MapKind::Ramp:
             if (pow2 && km == kKHalf) launch_soa_ab<kSrcRender, MapKind::Ramp>(opt, grid, stream, A);
-            else if (pow2) launch_soa_km<kSrcRender, MapKind::Ramp, true, D & 3>(km, grid, stream, A);
-            else launch_soa_km<kSrcRender, MapKind::Ramp, false, D & 3>(km, grid, stream, A);
+            else if (pow2) launch_soa_km<kSrcRender, MapKind::Ramp, true, D>(km, grid, stream, A);
+            else launch_soa_km<kSrcRender, MapKind::Ramp, false, D>(km, grid, stream, A);
             break;
         default: return DSP_ERR_INVALID;
         }
     } else if (km == kKHalf) {
         launch_soa_ab<kSrcMemory, MapKind::Noop>(opt, grid, stream, A);
     } else {
-        launch_soa_km<kSrcMemory, MapKind::Noop, true, D & 3>(km, grid, stream, A);
+        launch_soa_km<kSrcMemory, MapKind::Noop, true, D>(km, grid, stream, A);
     }
     DSPB_HIP(hipGetLastError());
     return DSP_OK;

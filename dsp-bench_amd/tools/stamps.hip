@@ -3,6 +3,7 @@
 // for phase SHARES only (the stamps themselves fence the schedule).
 //   build: hipcc --offload-arch=gfx950 -O3 -fno-slp-vectorize -DDSPB_STAMPS
 //          -I../include -Icsrc tools/stamps.hip -o build/stamps
+//   ablation set: bash tools/build_ablation.sh <opt>  (build/stamps_ab<mask>)
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -45,8 +46,20 @@ int main(int argc, char **argv) {
     CK(hipMemcpy(table, ht.data(), B * 4, hipMemcpyHostToDevice));
     std::vector<v2f> htw(8192);
     for (int k = 0; k < 8192; ++k) htw[k] = v2f{(float)cos(-2 * M_PI * k / 8192), (float)sin(-2 * M_PI * k / 8192)};
-    CK(hipMalloc(&tw, 8192 * 8));
-    CK(hipMemcpy(tw, htw.data(), 8192 * 8, hipMemcpyHostToDevice));
+    for (int j = 1; j < 8; ++j)  // lane-major stage twiddles (as capi.cpp get_tw)
+        for (int l = 0; l < 64; ++l) htw.push_back(htw[(2 * l * j) & 8191]);
+    for (int j = 1; j < 8; ++j)
+        for (int l = 0; l < 64; ++l) htw.push_back(htw[(16 * l * j) & 8191]);
+    CK(hipMalloc(&tw, htw.size() * 8));
+    CK(hipMemcpy(tw, htw.data(), htw.size() * 8, hipMemcpyHostToDevice));
+    std::vector<float4> hb(64);
+    const double th = 2.0 * M_PI / 8191.0;
+    for (int l = 0; l < 64; ++l)
+        hb[l] = float4{(float)cos(th * 2 * l), (float)sin(th * 2 * l), (float)cos(th * (2 * l + 1)),
+                       (float)sin(th * (2 * l + 1))};
+    float4 *wbase;
+    CK(hipMalloc(&wbase, 64 * sizeof(float4)));
+    CK(hipMemcpy(wbase, hb.data(), 64 * sizeof(float4), hipMemcpyHostToDevice));
     std::vector<float> hw(N);
     for (uint32_t n = 0; n < N; ++n) hw[n] = (float)(0.5 / sqrt(8192.0) * (0.5 - 0.5 * cos(2 * M_PI * n / (N - 1))));
     CK(hipMalloc(&win, N * 4));
@@ -60,6 +73,9 @@ int main(int argc, char **argv) {
     A.F = F; A.H = H; A.K = 4097; A.ld = 4097; A.valid = N;
     A.win2 = reinterpret_cast<const v2f *>(win);
     A.tw = tw;
+    A.wbase = wbase;
+    A.wa = (float)(0.5 * 0.5 / sqrt(8192.0));
+    A.wb = A.wa;
     A.map.kind = MapKind::Ramp; A.map.table = table; A.map.B = B; A.map.b_mask = B - 1;
     A.stamps = stamps;
     dim3 grid((uint32_t)((F + 3) / 4), 1);  // one channel: stamps indexed by frame

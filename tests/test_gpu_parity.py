@@ -258,14 +258,16 @@ def test_full_size_ir_test_stft_1h(torch_cuda, oracle, variant):
         assert spread <= 1e-6 * float(ref0.max())
 
 
-@pytest.mark.parametrize("opt", range(8))
-def test_soa_kernel_options(torch_cuda, oracle, opt):
+@pytest.mark.parametrize("B", [2, 64, 512, 4096, 8192])
+@pytest.mark.parametrize("opt", range(0, 16, 2))
+def test_soa_kernel_options(torch_cuda, oracle, opt, B):
     """Every A/B option combination of the SoA kernel (dsp_stft_soa_options)
-    on the fused IR_test path and the memory path, 4097 bins."""
+    on the fused IR_test path (ramp table in LDS for 4 <= B <= 4096, global
+    gathers otherwise) and the memory path, 4097 bins."""
     L = d.lib()
     oldv, oldo = L.dsp_stft_kernel_variant(2), L.dsp_stft_soa_options(opt)
     try:
-        n, B = 8192 * 5 + 99, 512
+        n = 8192 * 5 + 99
         x = rnd((2, n), 61)
         for win in (d.DSP_WIN_HANN, d.DSP_WIN_HAMMING):
             out, mag = d.render_stft(to_dev(torch_cuda, x), 2, B, 48000.0, d.Plugin.ir_test(), window=win)

@@ -17,7 +17,7 @@ out = torch.empty((2, nb * 512), device="cuda")
 mag = torch.empty((2, F, 4097), device="cuda")
 lib = d.lib()
 lib.dsp_stft_kernel_variant(2)
-opts = [int(a) for a in sys.argv[2:]] or list(range(8))
+opts = [int(a) for a in sys.argv[2:]] or list(range(0, 16, 2))
 res = {}
 for rnd in range(int(sys.argv[1]) if len(sys.argv) > 1 else 6):
     for o in opts:
