@@ -105,20 +105,24 @@ def main():
     sr = 96_000 if wl == "stft96k" else SR
     minutes = args.minutes if wl != "gain10min" or args.minutes != 60.0 else 10.0
     L = int(round(minutes * 60 * sr))
-    L -= L % HOP  # whole hops per rank
-    halo = N_FFT - HOP if wl != "gain10min" else 0
-    # rank r owns samples [r L, (r+1) L) of an (N * minutes)-long file and
-    # reads a halo of the next rank's first 4096 samples (the last rank has none)
-    L_in = L + (halo if rank < world - 1 else 0)
+    L -= L % HOP  # whole hops per rank (HOP is a multiple of B)
+    # the file is world * L samples long; rank r owns [r L, (r+1) L) and
+    # reads a halo of the next rank's first N - H samples (dspbench/shard.py)
+    sh = d.shard.plan(world * L, world, rank, B, N_FFT if wl != "gain10min" else HOP, HOP,
+                      render=(wl == "headline"))
+    assert sh.owned == L, (sh, L)
+    L_in = sh.read_len
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     x = (torch.rand((CH, L_in), device=dev, generator=g) * 2 - 1) * 0.1  # synthetic WAV
     nb = d.num_blocks(L_in, B)
     F = d.stft_frames(nb * B if wl == "headline" else L_in, N_FFT, HOP)
     out = torch.empty((CH, nb * B), device=dev) if wl != "stft96k" else None
-    mag = torch.empty((CH, F, K_BINS), device=dev) if wl != "gain10min" else None
+    # rows: the last rank owns one frame less (no halo); equal-sized rows keep
+    # the optional gather a plain dist.gather
+    mag = torch.empty((CH, max(F, L // HOP), K_BINS), device=dev) if wl != "gain10min" else None
     plugin = d.Plugin.ir_test(0.9, 0.002) if wl == "headline" else d.Plugin.gain_test(0.2)
     stream = torch.cuda.current_stream(dev)
-    soff = rank * L
+    soff = sh.start
 
     if wl == "headline":
         def step():
