@@ -32,7 +32,9 @@ void set_last_error(const char *fmt, ...) {
 
 int hip_fail(hipError_t e, const char *what) {
     set_last_error("%s: %s", what, hipGetErrorString(e));
-    return e == hipErrorOutOfMemory ? DSP_ERR_NOMEM : DSP_ERR_HIP;
+    if (e == hipErrorOutOfMemory) return DSP_ERR_NOMEM;
+    if (e == hipErrorNoDevice || e == hipErrorInvalidDevice) return DSP_ERR_NO_DEVICE;
+    return DSP_ERR_HIP;
 }
 
 static int invalid(const char *fmt, ...) {
