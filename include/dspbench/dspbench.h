@@ -25,8 +25,9 @@
  * specialised kernel that reads the plugin's own parameter / state blob at
  * the struct offsets the plugin declares (gain_test: Parameters{float gain},
  * IR_test: Parameters{float gain; float step}, static_gain_plugin:
- * State{float gain}).  DSP_PLUGIN_GENERIC runs the plugin's compiled
- * audio_callback itself on the GPU (module built by the plugin compiler).
+ * State{float gain}).  DSP_PLUGIN_GENERIC (the plugin's own compiled
+ * audio_callback run on the GPU) is reserved: this build returns
+ * DSP_ERR_UNSUPPORTED for it ("next").
  *
  * Errors: every entry point returns DSP_OK (0) or a negative dsp_status.
  * Nothing aborts; HIP errors are mapped to DSP_ERR_HIP and the HIP error
@@ -153,14 +154,17 @@ void dsp_kernel_timing_enable(int on);
 int dsp_kernel_timing(double *total_ms, uint64_t *launches, uint64_t *bytes);
 
 /* Select the 8192-point kernel (A/B and tests): 0 = one wavefront per frame,
- * 1 = two wavefronts per frame (default).  Other values only query.
+ * packed float2 math; 1 = two wavefronts per frame; 2 = one wavefront per
+ * frame, scalar structure-of-arrays math (default); 3 = variant 2 split over
+ * two wavefronts; 4 = two frames per wavefront.  Other values only query.
  * Returns the previous selection. */
 int dsp_stft_kernel_variant(int variant);
 
 /* Option bits of variant 2 (A/B): 1 = no scheduling barrier inside the
- * register DFTs, 2 = prefetch the stage twiddles with the frame load,
- * 4 = compute the window (angle addition) instead of loading it.
- * Returns the previous options. */
+ * register DFTs, 2 = prefetch the stage twiddles (lane-major table) with the
+ * frame load, 4 = compute the window (angle addition) instead of loading it,
+ * 8 = stage the IR_RAMP block table through LDS.  Default 14.  Values
+ * outside 0..15 only query.  Returns the previous options. */
 int dsp_stft_soa_options(int options);
 
 /* Diagnostics. */

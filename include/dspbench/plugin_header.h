@@ -12,11 +12,6 @@
  * Every service below is exported by libdspbench.so (dsp-bench_amd/host/
  * host_services.cpp).  The FFT services (fft_forward / fft_reverse) run on
  * the GPU through the same HIP kernel family as the STFT path.
- *
- * When a plugin is compiled for the GPU (generic dispatch, see
- * dsp-bench_amd/dspbench/plugin_compiler.py) this header is included inside
- * a `#pragma clang force_cuda_host_device` region, so the declarations also
- * get __device__ counterparts from include/dspbench/plugin_device.h.
  */
 #ifndef DSPBENCH_PLUGIN_HEADER_H
 #define DSPBENCH_PLUGIN_HEADER_H

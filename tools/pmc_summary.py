@@ -1,11 +1,18 @@
 """Summarise rocprofv3 --pmc counter CSVs: per kernel, mean per dispatch, and
-per-wave / derived figures (quad-cycle counters -> cycles)."""
+per-wave / derived figures (quad-cycle counters -> cycles).
+  usage: python tools/pmc_summary.py <pmc dir> [--json out.json]
+--json writes {kernel: {counter means..., "hbm_bytes", "fetch_bytes",
+"write_bytes"}} with the gfx950 corrections of MI355X_MICROARCH.md (HBM):
+FETCH_SIZE (KiB) x 2, WRITE_SIZE (KiB) as is."""
 import collections
 import csv
 import glob
+import json
 import sys
 
 root = sys.argv[1]
+js = sys.argv[sys.argv.index("--json") + 1] if "--json" in sys.argv else None
+summary = {}
 agg = collections.defaultdict(lambda: collections.defaultdict(list))
 for p in sorted(glob.glob(f"{root}/p*/run_counter_collection.csv")):
     for r in csv.DictReader(open(p)):
@@ -28,3 +35,9 @@ for k, d in agg.items():
         f = m.get("FETCH_SIZE", 0) * 1024 * 2  # gfx950: FETCH_SIZE reads 1/2 of streamed bytes
         wr = m.get("WRITE_SIZE", 0) * 1024
         print(f"   HBM bytes (FETCH x2 + WRITE) = {f + wr:.4g}  (fetch {f:.4g}, write {wr:.4g})")
+        m.update(hbm_bytes=f + wr, fetch_bytes=f, write_bytes=wr)
+    m["dispatches"] = max(len(v) for v in d.values())
+    summary[k] = m
+if js:
+    json.dump({"source": root, "note": "per-dispatch means; FETCH_SIZE x2 (gfx950), WRITE_SIZE exact",
+               "kernels": summary}, open(js, "w"), indent=1)
