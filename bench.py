@@ -49,9 +49,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
     ap.add_argument("--gather", action="store_true", help="also time an RCCL gather to rank 0")
-    ap.add_argument("--stft-variant", type=int, default=2, choices=[0, 1, 2, 3, 4],
-                    help="8192-pt kernel: 0 = wave/frame packed, 1 = two waves/frame, "
-                         "2 = wave/frame scalar SoA (default)")
+    ap.add_argument("--stft-variant", type=int, default=2, choices=[0, 1, 2, 3, 4, 5],
+                    help="8192-pt kernel (dsp_stft_kernel_variant): 2 = wave/frame scalar SoA, "
+                         "5 = wave/frame packed even/odd pairs")
     ap.add_argument("--workload", default="headline", choices=["headline", "stft96k", "gain10min"],
                     help="headline = IR_test + STFT 48 kHz (the metric); stft96k = BASELINE cfg 4 "
                          "(STFT of 1 h stereo 96 kHz from HBM); gain10min = cfg 2 render")

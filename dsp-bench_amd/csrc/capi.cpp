@@ -101,6 +101,14 @@ static int get_tw(int dev, const v2f **out) {
             for (int l = 0; l < 64; ++l) h.push_back(h[(2 * l * j) & 8191]);
         for (int j = 1; j < 8; ++j)
             for (int l = 0; l < 64; ++l) h.push_back(h[(16 * l * j) & 8191]);
+        // stft_pk.hip pairs, one float4 per (hi, lane), hi < 4:
+        // (re T[16 l hi], re T[16 l (hi + 4)], im T[16 l hi], im T[16 l (hi + 4)])
+        for (int hi = 0; hi < 4; ++hi)
+            for (int l = 0; l < 64; ++l) {
+                const v2f a = h[(16 * l * hi) & 8191], b = h[(16 * l * (hi + 4)) & 8191];
+                h.push_back(v2f{a.x, b.x});
+                h.push_back(v2f{a.y, b.y});
+            }
         DSPB_HIP(hipMalloc(&r.tw8192, sizeof(v2f) * h.size()));
         DSPB_HIP(hipMemcpy(r.tw8192, h.data(), sizeof(v2f) * h.size(), hipMemcpyHostToDevice));
     }
@@ -203,6 +211,7 @@ static float window_prescale(uint32_t N) {
 }
 
 static int launch_stft(const Stft8kArgs &A, uint32_t C, bool fused, bool full, hipStream_t s) {
+    if (g_stft_variant == 5) return launch_stft8192_pk(A, C, fused, s);
     if (g_stft_variant == 4) return launch_stft8192_pair2(A, C, fused, s);
     if (g_stft_variant == 3) return launch_stft8192_pair_soa(A, C, fused, s);
     if (g_stft_variant == 2) return launch_stft8192_soa(A, C, fused, g_soa_opt, s);
@@ -433,7 +442,7 @@ int dsp_stft_soa_options(int opt) {
 int dsp_stft_kernel_variant(int v) {
     std::lock_guard<std::mutex> lk(g_mu);
     const int old = g_stft_variant;
-    if (v >= 0 && v <= 4) g_stft_variant = v;
+    if (v >= 0 && v <= 5) g_stft_variant = v;
     return old;
 }
 

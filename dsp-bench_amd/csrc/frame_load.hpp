@@ -1,0 +1,91 @@
+// frame_load.hpp -- the rendered samples of one 8192-point frame, for the
+// one-wave-per-frame kernels (stft_soa.hip, stft_pk.hip).
+//
+// Lane l gets v[b] = (x[2l + 128b], x[2l + 128b + 1]) of the frame starting
+// at local sample fs, where x is the signal after the plugin's sample map:
+//   Ramp (IR_test, ref build/IR_test.cpp:40-60): table[(global sample) mod B]
+//   Gain / Noop: the input (zero past EOF or for missing channels) * gain.
+#pragma once
+#include "fft_soa.hpp"
+
+namespace dspb {
+
+template <MapKind MK, bool POW2>
+__device__ __forceinline__ void s_render_frame(const Stft8kArgs &A, const float *x, uint64_t fs,
+                                               uint32_t lane, cx (&v)[64]) {
+    const uint64_t gbase = A.goff + fs;
+    if constexpr (MK == MapKind::Ramp) {
+        const float *T = A.map.table;
+        if constexpr (POW2) {
+            const uint32_t p0 = (uint32_t)gbase + 2u * lane;
+#pragma unroll
+            for (int b = 0; b < 64; ++b) {
+                const v2f t =
+                    *reinterpret_cast<const v2f *>(T + ((p0 + 128u * (uint32_t)b) & A.map.b_mask));
+                v[b] = cx{t.x, t.y};
+            }
+        } else {
+            const uint32_t Bn = A.map.B;
+            uint32_t p = (uint32_t)((gbase + 2u * lane) % Bn);
+#pragma unroll
+            for (int b = 0; b < 64; ++b) {
+                const uint32_t q = (p + 1 == Bn) ? 0u : p + 1;
+                v[b] = cx{T[p], T[q]};
+                p += 128u;
+                while (p >= Bn) p -= Bn;
+            }
+        }
+    } else {
+        if (x != nullptr && fs + 8192u <= A.L) {
+#pragma unroll
+            for (int b = 0; b < 64; ++b) {
+                const v2f t = reinterpret_cast<const v2f *>(x + fs + 128u * (uint32_t)b)[lane];
+                v[b] = cx{t.x, t.y};
+            }
+        } else {
+#pragma unroll
+            for (int b = 0; b < 64; ++b) {
+                const uint64_t li = fs + 2u * lane + 128u * (uint32_t)b;
+                v[b] = cx{(x && li < A.L) ? x[li] : 0.f, (x && li + 1 < A.L) ? x[li + 1] : 0.f};
+            }
+        }
+        if constexpr (MK == MapKind::Gain) {
+#pragma unroll
+            for (int b = 0; b < 64; ++b) v[b] = cx{v[b].r * A.map.a, v[b].i * A.map.a};
+        }
+    }
+}
+
+// IR ramp from a block table staged in the wave's LDS tile (pow2 B, 4 <= B
+// <= 4096): two coalesced float4 loads per lane (B = 512) instead of 64
+// scattered 8-byte gathers; the tile is free until the transpose.
+__device__ __forceinline__ void lds_table_frame(const Stft8kArgs &A, float *lds, uint64_t fs,
+                                                uint32_t lane, cx (&v)[64]) {
+    const uint32_t q4 = A.map.B >> 2;  // float4s in the table
+    const float4 *T4 = reinterpret_cast<const float4 *>(A.map.table);
+    // groups of 4 float4 per lane: all loads of a group in flight
+    // together (B = 512 is one group, half of it masked off)
+    for (uint32_t g = 0; 256u * g < q4; ++g) {
+        float4 t4[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t i = lane + 64u * (4u * g + (uint32_t)u);
+            t4[u] = T4[i < q4 ? i : 0u];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t i = lane + 64u * (4u * g + (uint32_t)u);
+            if (i < q4) reinterpret_cast<float4 *>(lds)[i] = t4[u];
+        }
+    }
+    lds_fence();
+    const uint32_t p0 = (uint32_t)(A.goff + fs) + 2u * lane;
+#pragma unroll
+    for (int b = 0; b < 64; ++b) {
+        const v2f t = *reinterpret_cast<const v2f *>(
+            lds + ((p0 + 128u * (uint32_t)b) & A.map.b_mask));
+        v[b] = cx{t.x, t.y};
+    }
+}
+
+}  // namespace dspb

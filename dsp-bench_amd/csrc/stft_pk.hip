@@ -1,0 +1,274 @@
+// stft_pk.hip -- 8192-point STFT, one wavefront per frame, PACKED fp32 math.
+//
+// On gfx950 a wave issues one VALU instruction per ~4 cycles whether it is
+// v_add_f32 or v_pk_add_f32 (tools/valu_probe.hip: 4.1 vs 4.2 cycles), and
+// the scalar SoA kernel (stft_soa.hip) is VALU-bound (PMC: 3979 VALU per
+// frame, two waves saturate the SIMD).  This kernel runs the same 64 x 64
+// four-step transform with two independent sub-problems in the two halves
+// of every VGPR pair, so the butterflies cost half the instructions:
+//
+//   DFT64 over b as radix-2 DIT: Y[k] = E[k] + W64^k O[k],
+//   Y[k+32] = E[k] - W64^k O[k], E/O = DFT32 of the even/odd b.  The
+//   pair P[j] = (v[2j], v[2j+1]) (one cx2: re halves, im halves) carries the
+//   even and the odd sequence, x2dft32 transforms both at once, one scalar
+//   combine step writes (Y[k], Y[k+32]) into the halves of Q[k] -- the
+//   two columns kb = k, k + 32 that share the stage twiddle's low digit.
+//   Stage twiddles, the LDS transpose (two dwords per pair) and the second
+//   DFT64 use the same pairing; the real split pairs (ka, ka + 16).
+//
+// Loads, render, window and stores are those of stft_soa.hip with options
+// 14 (LDS ramp table, lane-major twiddles issued first, computed window).
+#include "fft_x2.hpp"
+#include "frame_load.hpp"
+
+namespace dspb {
+
+// both halves: a * w
+__device__ __forceinline__ cx2 cmul2(cx2 a, cx2 w) {
+    return cx2{a.r * w.r - a.i * w.i, a.r * w.i + a.i * w.r};
+}
+// (c + i s) broadcast times both halves of w
+__device__ __forceinline__ cx2 cmulb(cx c, cx2 w) {
+    return cx2{c.r * w.r - c.i * w.i, c.r * w.i + c.i * w.r};
+}
+
+// radix-2 DIT combine of a transformed pair: halves (E[k], O[k]) at
+// a[perm32(k)] -> (Y[k], Y[k+32]) as scalars
+__device__ __forceinline__ void combine64(const cx2 (&a)[32], cx (&yp)[32], cx (&ym)[32]) {
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+        const cx2 p = a[perm32(k)];
+        const cx e = cx{p.r.x, p.i.x};
+        const cx t = stw64(cx{p.r.y, p.i.y}, k);
+        yp[k] = e + t;
+        ym[k] = e - t;
+    }
+}
+
+template <int SRC, int KM, MapKind MK, bool POW2, bool WINC>
+__global__ __launch_bounds__(256, 2) void stft8192_pk_kernel(Stft8kArgs A) {
+    __shared__ __attribute__((aligned(16))) float lds_all[4][64 * 65];
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t ch = blockIdx.y;
+    const uint64_t f = (uint64_t)xcd_remap(blockIdx.x, gridDim.x) * 4u + wave;
+    if (f >= A.F) return;  // whole wave leaves; nothing below waits on other waves
+    float *lds = lds_all[wave];
+    const uint64_t fs = f * (uint64_t)A.H;
+    const float *x = (ch < A.in_ch) ? A.in.p[ch] : nullptr;
+
+    // ---- 0. constants, issued before the frame -----------------------------
+    // tlo[j] = W4096^(l j), thp[h] = (W4096^(8 l h), W4096^(8 l (h + 4)))
+    // (capi.cpp get_tw: lane-major rows after T8192)
+    cx tlo[8];
+#pragma unroll
+    for (int j = 1; j < 8; ++j) {
+        const v2f a = (A.tw + 8192u + 64u * (uint32_t)(j - 1))[lane];
+        tlo[j] = cx{a.x, a.y};
+    }
+    cx2 thp[4];
+    const float4 *tp4 = reinterpret_cast<const float4 *>(A.tw + 8192u + 896u);
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+        const float4 t = tp4[64u * (uint32_t)h + lane];
+        thp[h] = cx2{v2f{t.x, t.y}, v2f{t.z, t.w}};
+    }
+    float4 wbase = float4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (WINC) wbase = A.wbase[lane];
+
+    // ---- 1. frame (+ fused render) -----------------------------------------
+    cx v[64];
+    if constexpr (SRC == kSrcMemory) {
+        if (A.valid >= 8192u) {
+#pragma unroll
+            for (int b = 0; b < 64; ++b) {
+                const v2f t = reinterpret_cast<const v2f *>(x + fs + 128u * (uint32_t)b)[lane];
+                v[b] = cx{t.x, t.y};
+            }
+        } else {
+#pragma unroll
+            for (int b = 0; b < 64; ++b) {
+                const uint32_t s = 2u * lane + 128u * (uint32_t)b;
+                v2f t = v2f{0.f, 0.f};
+                if (s < A.valid) t = reinterpret_cast<const v2f *>(x + fs + 128u * (uint32_t)b)[lane];
+                v[b] = cx{t.x, t.y};
+            }
+        }
+    } else {
+        if constexpr (MK == MapKind::Ramp && POW2) {
+            if (A.map.B >= 4u && A.map.B <= 4096u) lds_table_frame(A, lds, fs, lane, v);
+            else s_render_frame<MK, POW2>(A, x, fs, lane, v);
+        } else {
+            s_render_frame<MK, POW2>(A, x, fs, lane, v);
+        }
+        float *o = A.out.p[ch] + fs;
+#pragma unroll
+        for (int b = 0; b < 64; ++b)
+            if (128u * (uint32_t)b < A.H)
+                reinterpret_cast<v2f *>(o + 128u * (uint32_t)b)[lane] = v2f{v[b].r, v[b].i};
+    }
+
+    // ---- 2. window (pre-scaled by 0.5/sqrt N), packed into even/odd pairs ---
+    cx2 P[32];
+    {
+        const v2f bc = v2f{wbase.x, wbase.z}, bs = v2f{wbase.y, wbase.w};
+#pragma unroll
+        for (int j = 0; j < 32; ++j) {
+            v2f w[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int b = 2 * j + h;
+                if constexpr (WINC) {
+                    // w(n) = wa - wb cos(theta n), n = 2 lane + {0, 1} + 128 b
+                    const v2f t = bc * kWinB_c[b] - bs * kWinB_s[b];
+                    w[h] = A.wa - A.wb * t;
+                } else {
+                    w[h] = (A.win2 + 64u * (uint32_t)b)[lane];
+                }
+            }
+            P[j] = cx2{v2f{v[2 * j].r * w[0].x, v[2 * j + 1].r * w[1].x},
+                       v2f{v[2 * j].i * w[0].y, v[2 * j + 1].i * w[1].y}};
+        }
+    }
+
+    // ---- 3. DFT64 over b: even/odd DFT32 in the halves, then combine --------
+    x2dft32(P);
+    cx2 Q[32];  // Q[k] = (Y[k], Y[k+32]) * (W4096^(l k), W4096^(l (k+32)))
+    {
+        cx yp[32], ym[32];
+        combine64(P, yp, ym);
+#pragma unroll
+        for (int k = 0; k < 32; ++k) {
+            __builtin_amdgcn_sched_barrier(0);
+            const cx2 y = cx2{v2f{yp[k].r, ym[k].r}, v2f{yp[k].i, ym[k].i}};
+            const int lo = k & 7, hi = k >> 3;
+            const cx2 w = lo ? cmulb(tlo[lo], thp[hi]) : thp[hi];
+            Q[k] = cmul2(y, w);
+        }
+    }
+
+    // ---- 4. transpose through LDS: row l, column kb -> column l, row a -----
+    cx2 R[32];  // R[j] = (u[2j], u[2j+1]), u[a] = row a of column l
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+        lds[lane * 65u + k] = Q[k].r.x;
+        lds[lane * 65u + k + 32] = Q[k].r.y;
+    }
+    lds_fence();
+#pragma unroll
+    for (int j = 0; j < 32; ++j) R[j].r = v2f{lds[(2 * j) * 65 + lane], lds[(2 * j + 1) * 65 + lane]};
+    lds_fence();
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+        lds[lane * 65u + k] = Q[k].i.x;
+        lds[lane * 65u + k + 32] = Q[k].i.y;
+    }
+    lds_fence();
+#pragma unroll
+    for (int j = 0; j < 32; ++j) R[j].i = v2f{lds[(2 * j) * 65 + lane], lds[(2 * j + 1) * 65 + lane]};
+
+    // ---- 5. DFT64 over a: Z[l + 64 ka] = zp[ka] (ka < 32), zm[ka - 32] ------
+    x2dft32(R);
+    cx zp[32], zm[32];
+    combine64(R, zp, zm);
+
+    // ---- 6. paired real split over (ka, ka + 16), ka < 16 ------------------
+    // X[k] = E + T and X[M-k] = conj(E - T), k = l + 64 ka, partner
+    // Z[M - k] = Z[63 - ka] of lane 64 - l (lane 0: its own Z[64 - ka]).
+    float *mrow = A.mag.p[ch] + f * A.ld;
+    const uint32_t src = ((64u - lane) & 63u) * 4u;
+    const bool l0 = lane == 0;
+    const v2f wl2 = A.tw[lane];  // W8192^l
+    const cx wl = cx{wl2.x, wl2.y};
+#pragma unroll
+    for (int ka = 0; ka < 16; ++ka) {
+        __builtin_amdgcn_sched_barrier(0);
+        // (select on values: a select of two array addresses would keep
+        // zp/zm in scratch)
+        const cx a0 = ka == 0 ? zp[0] : zm[32 - ka], b0 = zm[31 - ka];
+        const cx a1 = zm[16 - ka], b1 = zm[15 - ka];
+        const cx s0 = cx{l0 ? a0.r : b0.r, l0 ? a0.i : b0.i};
+        const cx s1 = cx{l0 ? a1.r : b1.r, l0 ? a1.i : b1.i};
+        const cx2 Pp = cx2{v2f{bperm(src, s0.r), bperm(src, s1.r)}, v2f{bperm(src, s0.i), bperm(src, s1.i)}};
+        const cx2 Z = cx2{v2f{zp[ka].r, zp[ka + 16].r}, v2f{zp[ka].i, zp[ka + 16].i}};
+        const cx2 E = cx2{Z.r + Pp.r, Z.i - Pp.i};  // 2 E   (partner conjugated)
+        const cx2 D = cx2{Z.r - Pp.r, Z.i + Pp.i};  // 2 i O
+        const cx2 tw = cmulb(wl, cx2{v2f{kW128_re[ka], kW128_re[ka + 16]},
+                                     v2f{kW128_im[ka], kW128_im[ka + 16]}});  // W8192^k
+        const cx2 T = cmul2(negi(D), tw);  // 2 W^k O
+        const cx2 X1 = E + T;              // 2 X[k]
+        const cx2 X2 = E - T;              // 2 conj X[M - k]
+        const v2f q1 = X1.r * X1.r + X1.i * X1.i;
+        const v2f q2 = X2.r * X2.r + X2.i * X2.i;
+        const float m1[2] = {__builtin_amdgcn_sqrtf(q1.x), __builtin_amdgcn_sqrtf(q1.y)};
+        const float m2[2] = {__builtin_amdgcn_sqrtf(q2.x), __builtin_amdgcn_sqrtf(q2.y)};
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const uint32_t kk = (uint32_t)(ka + 16 * h);
+            const uint32_t k1 = lane + 64u * kk;  // < 2048
+            const uint32_t k2 = 4096u - k1;        // > 2048 (4096 at k1 = 0)
+            if constexpr (KM == kKPartial) {
+                if (k1 < A.K) mrow[k1] = m1[h];
+                if (k2 < A.K) mrow[k2] = m2[h];
+            } else {
+                (mrow + 64u * kk)[lane] = m1[h];
+                (mrow + 4096u - 64u * kk)[-(int)lane] = m2[h];
+                if constexpr (KM == kKMirror) {
+                    mrow[k1 == 0 ? 0u : 8192u - k1] = m1[h];
+                    (mrow + 4096u + 64u * kk)[lane] = m2[h];
+                }
+            }
+        }
+    }
+    if (l0) {  // the self-paired bin k = 2048: |X| = 2 |Z[2048]| (scaled), Z[2048] = zm[0]
+        const cx Z = zm[0];
+        const float m = 2.f * __builtin_amdgcn_sqrtf(__builtin_fmaf(Z.r, Z.r, Z.i * Z.i));
+        if (KM != kKPartial || 2048u < A.K) mrow[2048] = m;
+        if (KM == kKMirror) mrow[6144] = m;
+    }
+}
+
+template <int SRC, MapKind MK, bool POW2, bool WINC>
+static void launch_pk_km(int km, dim3 grid, hipStream_t s, const Stft8kArgs &A) {
+    if (km == kKHalf)
+        hipLaunchKernelGGL((stft8192_pk_kernel<SRC, kKHalf, MK, POW2, WINC>), grid, dim3(256), 0, s, A);
+    else if (km == kKMirror)
+        hipLaunchKernelGGL((stft8192_pk_kernel<SRC, kKMirror, MK, POW2, WINC>), grid, dim3(256), 0, s, A);
+    else
+        hipLaunchKernelGGL((stft8192_pk_kernel<SRC, kKPartial, MK, POW2, WINC>), grid, dim3(256), 0, s, A);
+}
+
+// A.win2: the window pre-scaled by 0.5 / sqrt(8192); the computed window
+// (A.wbase, A.wa, A.wb) serves the full-frame 4097-bin shapes.
+int launch_stft8192_pk(const Stft8kArgs &A, uint32_t C, bool fused, hipStream_t stream) {
+    if (A.F == 0 || C == 0) return DSP_OK;
+    const uint64_t groups = (A.F + 3) / 4;
+    if (groups > 0x7fffffffull) return DSP_ERR_INVALID;
+    dim3 grid((uint32_t)groups, C);
+    const int km = A.K == 4097u ? kKHalf : (A.K == 8192u ? kKMirror : kKPartial);
+    const bool pow2 = A.map.b_mask != 0 && A.map.B >= 2;
+    const bool winc = A.valid >= 8192u && A.wbase != nullptr && km == kKHalf;
+    if (fused) {
+        switch (A.map.kind) {
+        case MapKind::Noop: launch_pk_km<kSrcRender, MapKind::Noop, true, false>(km, grid, stream, A); break;
+        case MapKind::Gain: launch_pk_km<kSrcRender, MapKind::Gain, true, false>(km, grid, stream, A); break;
+        case MapKind::Ramp:
+            if (pow2 && winc)
+                hipLaunchKernelGGL((stft8192_pk_kernel<kSrcRender, kKHalf, MapKind::Ramp, true, true>), grid,
+                                   dim3(256), 0, stream, A);
+            else if (pow2) launch_pk_km<kSrcRender, MapKind::Ramp, true, false>(km, grid, stream, A);
+            else launch_pk_km<kSrcRender, MapKind::Ramp, false, false>(km, grid, stream, A);
+            break;
+        default: return DSP_ERR_INVALID;
+        }
+    } else if (winc) {
+        hipLaunchKernelGGL((stft8192_pk_kernel<kSrcMemory, kKHalf, MapKind::Noop, true, true>), grid, dim3(256),
+                           0, stream, A);
+    } else {
+        launch_pk_km<kSrcMemory, MapKind::Noop, true, false>(km, grid, stream, A);
+    }
+    DSPB_HIP(hipGetLastError());
+    return DSP_OK;
+}
+
+}  // namespace dspb

@@ -17,54 +17,9 @@
 //     (ds_bpermute), twiddles and products; lane 0 pairs within its own
 //     registers (column 0) and adds the self-paired bin k = 2048.
 #include "fft_soa.hpp"
+#include "frame_load.hpp"
 
 namespace dspb {
-
-template <MapKind MK, bool POW2>
-__device__ __forceinline__ void s_render_frame(const Stft8kArgs &A, const float *x, uint64_t fs,
-                                               uint32_t lane, cx (&v)[64]) {
-    const uint64_t gbase = A.goff + fs;
-    if constexpr (MK == MapKind::Ramp) {
-        const float *T = A.map.table;
-        if constexpr (POW2) {
-            const uint32_t p0 = (uint32_t)gbase + 2u * lane;
-#pragma unroll
-            for (int b = 0; b < 64; ++b) {
-                const v2f t =
-                    *reinterpret_cast<const v2f *>(T + ((p0 + 128u * (uint32_t)b) & A.map.b_mask));
-                v[b] = cx{t.x, t.y};
-            }
-        } else {
-            const uint32_t Bn = A.map.B;
-            uint32_t p = (uint32_t)((gbase + 2u * lane) % Bn);
-#pragma unroll
-            for (int b = 0; b < 64; ++b) {
-                const uint32_t q = (p + 1 == Bn) ? 0u : p + 1;
-                v[b] = cx{T[p], T[q]};
-                p += 128u;
-                while (p >= Bn) p -= Bn;
-            }
-        }
-    } else {
-        if (x != nullptr && fs + 8192u <= A.L) {
-#pragma unroll
-            for (int b = 0; b < 64; ++b) {
-                const v2f t = reinterpret_cast<const v2f *>(x + fs + 128u * (uint32_t)b)[lane];
-                v[b] = cx{t.x, t.y};
-            }
-        } else {
-#pragma unroll
-            for (int b = 0; b < 64; ++b) {
-                const uint64_t li = fs + 2u * lane + 128u * (uint32_t)b;
-                v[b] = cx{(x && li < A.L) ? x[li] : 0.f, (x && li + 1 < A.L) ? x[li + 1] : 0.f};
-            }
-        }
-        if constexpr (MK == MapKind::Gain) {
-#pragma unroll
-            for (int b = 0; b < 64; ++b) v[b] = cx{v[b].r * A.map.a, v[b].i * A.map.a};
-        }
-    }
-}
 
 // OPT bits (A/B-selectable, see dsp_stft_soa_options):
 //   kOptNoBar      no scheduling barriers inside the DFT64 passes
@@ -138,31 +93,7 @@ __global__ __launch_bounds__(256, 2) void stft8192_soa_kernel(Stft8kArgs A) {
     } else {
         if constexpr ((OPT & kOptLdsTable) && MK == MapKind::Ramp && POW2) {
             if (A.map.B >= 4u && A.map.B <= 4096u) {
-                const uint32_t q4 = A.map.B >> 2;  // float4s in the table
-                const float4 *T4 = reinterpret_cast<const float4 *>(A.map.table);
-                // groups of 4 float4 per lane: all loads of a group in flight
-                // together (B = 512 is one group, half of it masked off)
-                for (uint32_t g = 0; 256u * g < q4; ++g) {
-                    float4 t4[4];
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        const uint32_t i = lane + 64u * (4u * g + (uint32_t)u);
-                        t4[u] = T4[i < q4 ? i : 0u];
-                    }
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        const uint32_t i = lane + 64u * (4u * g + (uint32_t)u);
-                        if (i < q4) reinterpret_cast<float4 *>(lds)[i] = t4[u];
-                    }
-                }
-                lds_fence();
-                const uint32_t p0 = (uint32_t)(A.goff + fs) + 2u * lane;
-#pragma unroll
-                for (int b = 0; b < 64; ++b) {
-                    const v2f t = *reinterpret_cast<const v2f *>(
-                        lds + ((p0 + 128u * (uint32_t)b) & A.map.b_mask));
-                    v[b] = cx{t.x, t.y};
-                }
+                lds_table_frame(A, lds, fs, lane, v);
             } else {
                 s_render_frame<MK, POW2>(A, x, fs, lane, v);
             }

@@ -1,5 +1,6 @@
 // tools/valu_probe.hip -- VALU issue-rate probe: independent v_add_f32 or
 // v_pk_add_f32 chains, k waves per SIMD, no memory in the loop.
+// Build with -fno-slp-vectorize, or the scalar chains get packed.
 #include <hip/hip_runtime.h>
 #include <cstdio>
 typedef float v2f __attribute__((ext_vector_type(2)));

@@ -29,9 +29,9 @@ def rnd(shape, seed):
     return np.random.default_rng(seed).uniform(-1.0, 1.0, size=shape).astype(np.float32)
 
 
-@pytest.fixture(params=[0, 1, 2, 3, 4], ids=["wave", "pair", "soa", "pairsoa", "pair2"])
+@pytest.fixture(params=[0, 1, 2, 3, 4, 5], ids=["wave", "pair", "soa", "pairsoa", "pair2", "pk"])
 def variant(request):
-    """Run the test on both 8192-point kernels (dsp_stft_kernel_variant)."""
+    """Run the test on every 8192-point kernel (dsp_stft_kernel_variant)."""
     L = d.lib()
     old = L.dsp_stft_kernel_variant(request.param)
     yield request.param

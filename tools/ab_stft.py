@@ -17,7 +17,7 @@ F = d.stft_frames(nb * 512, 8192, 4096)
 out = torch.empty((2, nb * 512), device="cuda")
 mag = torch.empty((2, F, 4097), device="cuda")
 lib = d.lib()
-VARIANTS = (0, 2, 3, 4)
+VARIANTS = tuple(int(a) for a in sys.argv[2:]) or (2, 4, 5)
 res = {k: [] for v in VARIANTS for k in (v, f"mem{v}")}
 for rnd in range(int(sys.argv[1]) if len(sys.argv) > 1 else 8):
     for v in VARIANTS:
