@@ -49,7 +49,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
     ap.add_argument("--gather", action="store_true", help="also time an RCCL gather to rank 0")
-    ap.add_argument("--stft-variant", type=int, default=2, choices=[0, 1, 2, 3, 4, 5],
+    ap.add_argument("--stft-variant", type=int, default=5, choices=[0, 1, 2, 3, 4, 5],
                     help="8192-pt kernel (dsp_stft_kernel_variant): 2 = wave/frame scalar SoA, "
                          "5 = wave/frame packed even/odd pairs")
     ap.add_argument("--workload", default="headline", choices=["headline", "stft96k", "gain10min"],

@@ -202,7 +202,7 @@ static bool g_timing = false;
 // SoA with a pre-scaled window (stft_soa.hip), 3 = two waves per frame,
 // scalar SoA (stft_pair_soa.hip), 4 = two frames packed per VGPR pair,
 // two waves per frame pair (stft_pair2.hip)
-static int g_stft_variant = 2;
+static int g_stft_variant = 5;
 static int g_soa_opt = 14;  // stft_soa.hip OPT bits (A/B), default kSoaDefaultOpt
 
 // the SoA kernel folds 0.5/sqrt(N) into the window
@@ -211,7 +211,7 @@ static float window_prescale(uint32_t N) {
 }
 
 static int launch_stft(const Stft8kArgs &A, uint32_t C, bool fused, bool full, hipStream_t s) {
-    if (g_stft_variant == 5) return launch_stft8192_pk(A, C, fused, s);
+    if (g_stft_variant == 5) return launch_stft8192_pk(A, C, fused, g_soa_opt >> 4, s);
     if (g_stft_variant == 4) return launch_stft8192_pair2(A, C, fused, s);
     if (g_stft_variant == 3) return launch_stft8192_pair_soa(A, C, fused, s);
     if (g_stft_variant == 2) return launch_stft8192_soa(A, C, fused, g_soa_opt, s);
@@ -435,7 +435,7 @@ int dsp_abi_version(void) { return DSPBENCH_ABI_VERSION; }
 int dsp_stft_soa_options(int opt) {
     std::lock_guard<std::mutex> lk(g_mu);
     const int old = g_soa_opt;
-    if (opt >= 0 && opt <= 15) g_soa_opt = opt;
+    if (opt >= 0 && opt <= 127) g_soa_opt = opt;
     return old;
 }
 

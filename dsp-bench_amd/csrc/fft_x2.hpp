@@ -56,10 +56,12 @@ __device__ __forceinline__ cx2 x2tw64(cx2 a, int m) {  // a * W64^m, m compile-t
 }
 
 // 32-point DFT, natural order in, X[k] at v[perm32(k)] out (8 x 4).
+// BAR: pin one DFT8 / DFT4 at a time (bounds register pressure, costs ILP).
+template <bool BAR = true>
 __device__ __forceinline__ void x2dft32(cx2 (&v)[32]) {
 #pragma unroll
     for (int j2 = 0; j2 < 4; ++j2) {
-        __builtin_amdgcn_sched_barrier(0);
+        if (BAR) __builtin_amdgcn_sched_barrier(0);
         x2dft8(v[j2], v[4 + j2], v[8 + j2], v[12 + j2], v[16 + j2], v[20 + j2], v[24 + j2],
                v[28 + j2]);
     }
@@ -69,7 +71,7 @@ __device__ __forceinline__ void x2dft32(cx2 (&v)[32]) {
         for (int j2 = 1; j2 < 4; ++j2) v[4 * k1 + j2] = x2tw64(v[4 * k1 + j2], 2 * j2 * k1);
 #pragma unroll
     for (int k1 = 0; k1 < 8; ++k1) {
-        __builtin_amdgcn_sched_barrier(0);
+        if (BAR) __builtin_amdgcn_sched_barrier(0);
         x2dft4(v[4 * k1], v[4 * k1 + 1], v[4 * k1 + 2], v[4 * k1 + 3]);
     }
     __builtin_amdgcn_sched_barrier(0);

@@ -45,7 +45,45 @@ __device__ __forceinline__ void combine64(const cx2 (&a)[32], cx (&yp)[32], cx (
     }
 }
 
-template <int SRC, int KM, MapKind MK, bool POW2, bool WINC>
+// the same combine, packed: y[k] = (Y[k], Y[k+32]) as one cx2.  The odd
+// half is twiddled in place (the even half rides along times 1), then each
+// butterfly is one v_pk_fma: (e, e) + (t, t) * (1, -1).
+template <int K>
+__device__ __forceinline__ cx2 combine1(cx2 p) {
+    const v2f pm = v2f{1.f, -1.f};
+    v2f tr, ti;  // (t, t) where t = O W64^K, as splats of one register half
+    if constexpr (K == 0) {
+        tr = v2f{p.r.y, p.r.y};
+        ti = v2f{p.i.y, p.i.y};
+    } else if constexpr (K == 16) {  // t = -i O = (O.i, -O.r)
+        tr = v2f{p.i.y, p.i.y};
+        ti = -v2f{p.r.y, p.r.y};
+    } else {
+        const v2f w = v2f{1.f, kW64_re[K]}, s = v2f{0.f, kW64_im[K]};
+        const v2f qr = p.r * w - p.i * s, qi = p.r * s + p.i * w;  // (e, t) per part
+        tr = v2f{qr.y, qr.y};
+        ti = v2f{qi.y, qi.y};
+    }
+    return cx2{tr * pm + v2f{p.r.x, p.r.x}, ti * pm + v2f{p.i.x, p.i.x}};
+}
+template <int K = 0>
+__device__ __forceinline__ void combine64p(const cx2 (&a)[32], cx2 (&y)[32]) {
+    if constexpr (K < 32) {
+        y[K] = combine1<K>(a[perm32(K)]);
+        combine64p<K + 1>(a, y);
+    }
+}
+
+// OPT bits (A/B, dsp_stft_soa_options >> 4): 1 = no scheduling barriers in
+// the DFT32s, 2 = none in the twiddle loop, 4 = none in the split loop
+enum { kPkNoBarDft = 1, kPkNoBarTw = 2, kPkNoBarSplit = 4 };
+constexpr int kPkDefaultOpt = 0;
+
+// PER (Ramp, pow2 B <= 4096): the frame's sample pairs repeat every PER
+// values of b (PER = max(1, B / 128)), so only v[0 .. PER) are fetched from
+// the block table -- 4 gathers at B = 512 -- and v[b] = v[b mod PER] is a
+// register alias.  PER = 0: generic path.
+template <int SRC, int KM, MapKind MK, bool POW2, bool WINC, int PER = 0, int OPT = kPkDefaultOpt>
 __global__ __launch_bounds__(256, 2) void stft8192_pk_kernel(Stft8kArgs A) {
     __shared__ __attribute__((aligned(16))) float lds_all[4][64 * 65];
     const uint32_t lane = threadIdx.x & 63u;
@@ -95,7 +133,16 @@ __global__ __launch_bounds__(256, 2) void stft8192_pk_kernel(Stft8kArgs A) {
             }
         }
     } else {
-        if constexpr (MK == MapKind::Ramp && POW2) {
+        if constexpr (MK == MapKind::Ramp && PER > 0) {
+            const uint32_t p0 = (uint32_t)(A.goff + fs) + 2u * lane;
+#pragma unroll
+            for (int b = 0; b < PER; ++b) {
+                const v2f t = *reinterpret_cast<const v2f *>(A.map.table + ((p0 + 128u * (uint32_t)b) & A.map.b_mask));
+                v[b] = cx{t.x, t.y};
+            }
+#pragma unroll
+            for (int b = PER; b < 64; ++b) v[b] = v[b % PER];
+        } else if constexpr (MK == MapKind::Ramp && POW2) {
             if (A.map.B >= 4u && A.map.B <= 4096u) lds_table_frame(A, lds, fs, lane, v);
             else s_render_frame<MK, POW2>(A, x, fs, lane, v);
         } else {
@@ -132,15 +179,15 @@ __global__ __launch_bounds__(256, 2) void stft8192_pk_kernel(Stft8kArgs A) {
     }
 
     // ---- 3. DFT64 over b: even/odd DFT32 in the halves, then combine --------
-    x2dft32(P);
+    x2dft32<!(OPT & kPkNoBarDft)>(P);
     cx2 Q[32];  // Q[k] = (Y[k], Y[k+32]) * (W4096^(l k), W4096^(l (k+32)))
     {
-        cx yp[32], ym[32];
-        combine64(P, yp, ym);
+        cx2 Y[32];
+        combine64p(P, Y);
 #pragma unroll
         for (int k = 0; k < 32; ++k) {
-            __builtin_amdgcn_sched_barrier(0);
-            const cx2 y = cx2{v2f{yp[k].r, ym[k].r}, v2f{yp[k].i, ym[k].i}};
+            if (!(OPT & kPkNoBarTw)) __builtin_amdgcn_sched_barrier(0);
+            const cx2 y = Y[k];
             const int lo = k & 7, hi = k >> 3;
             const cx2 w = lo ? cmulb(tlo[lo], thp[hi]) : thp[hi];
             Q[k] = cmul2(y, w);
@@ -168,7 +215,7 @@ __global__ __launch_bounds__(256, 2) void stft8192_pk_kernel(Stft8kArgs A) {
     for (int j = 0; j < 32; ++j) R[j].i = v2f{lds[(2 * j) * 65 + lane], lds[(2 * j + 1) * 65 + lane]};
 
     // ---- 5. DFT64 over a: Z[l + 64 ka] = zp[ka] (ka < 32), zm[ka - 32] ------
-    x2dft32(R);
+    x2dft32<!(OPT & kPkNoBarDft)>(R);
     cx zp[32], zm[32];
     combine64(R, zp, zm);
 
@@ -182,7 +229,7 @@ __global__ __launch_bounds__(256, 2) void stft8192_pk_kernel(Stft8kArgs A) {
     const cx wl = cx{wl2.x, wl2.y};
 #pragma unroll
     for (int ka = 0; ka < 16; ++ka) {
-        __builtin_amdgcn_sched_barrier(0);
+        if (!(OPT & kPkNoBarSplit)) __builtin_amdgcn_sched_barrier(0);
         // (select on values: a select of two array addresses would keep
         // zp/zm in scratch)
         const cx a0 = ka == 0 ? zp[0] : zm[32 - ka], b0 = zm[31 - ka];
@@ -240,7 +287,8 @@ static void launch_pk_km(int km, dim3 grid, hipStream_t s, const Stft8kArgs &A) 
 
 // A.win2: the window pre-scaled by 0.5 / sqrt(8192); the computed window
 // (A.wbase, A.wa, A.wb) serves the full-frame 4097-bin shapes.
-int launch_stft8192_pk(const Stft8kArgs &A, uint32_t C, bool fused, hipStream_t stream) {
+int launch_stft8192_pk(const Stft8kArgs &A, uint32_t C, bool fused, int opt, hipStream_t stream) {
+    (void)opt;
     if (A.F == 0 || C == 0) return DSP_OK;
     const uint64_t groups = (A.F + 3) / 4;
     if (groups > 0x7fffffffull) return DSP_ERR_INVALID;
@@ -253,9 +301,22 @@ int launch_stft8192_pk(const Stft8kArgs &A, uint32_t C, bool fused, hipStream_t 
         case MapKind::Noop: launch_pk_km<kSrcRender, MapKind::Noop, true, false>(km, grid, stream, A); break;
         case MapKind::Gain: launch_pk_km<kSrcRender, MapKind::Gain, true, false>(km, grid, stream, A); break;
         case MapKind::Ramp:
-            if (pow2 && winc)
-                hipLaunchKernelGGL((stft8192_pk_kernel<kSrcRender, kKHalf, MapKind::Ramp, true, true>), grid,
-                                   dim3(256), 0, stream, A);
+            if (pow2 && winc) {
+                // period of the block table in units of 128 samples
+                const uint32_t per = A.map.B <= 128u ? 1u : A.map.B / 128u;
+#define DSPB_PK_PER(p) \
+    hipLaunchKernelGGL((stft8192_pk_kernel<kSrcRender, kKHalf, MapKind::Ramp, true, true, p>), grid, dim3(256), \
+                       0, stream, A)
+                switch (per) {
+                case 1: DSPB_PK_PER(1); break;
+                case 2: DSPB_PK_PER(2); break;
+                case 4: DSPB_PK_PER(4); break;
+                case 8: DSPB_PK_PER(8); break;
+                case 16: DSPB_PK_PER(16); break;
+                default: DSPB_PK_PER(0); break;
+                }
+#undef DSPB_PK_PER
+            }
             else if (pow2) launch_pk_km<kSrcRender, MapKind::Ramp, true, false>(km, grid, stream, A);
             else launch_pk_km<kSrcRender, MapKind::Ramp, false, false>(km, grid, stream, A);
             break;

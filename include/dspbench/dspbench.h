@@ -155,8 +155,10 @@ int dsp_kernel_timing(double *total_ms, uint64_t *launches, uint64_t *bytes);
 
 /* Select the 8192-point kernel (A/B and tests): 0 = one wavefront per frame,
  * packed float2 math; 1 = two wavefronts per frame; 2 = one wavefront per
- * frame, scalar structure-of-arrays math (default); 3 = variant 2 split over
- * two wavefronts; 4 = two frames per wavefront.  Other values only query.
+ * frame, scalar structure-of-arrays math; 3 = variant 2 split over two
+ * wavefronts; 4 = two frames per wavefront pair; 5 = one wavefront per
+ * frame, even/odd halves in packed VGPR pairs (default).  Other values
+ * only query.
  * Returns the previous selection. */
 int dsp_stft_kernel_variant(int variant);
 
@@ -164,7 +166,7 @@ int dsp_stft_kernel_variant(int variant);
  * register DFTs, 2 = prefetch the stage twiddles (lane-major table) with the
  * frame load, 4 = compute the window (angle addition) instead of loading it,
  * 8 = stage the IR_RAMP block table through LDS.  Default 14.  Values
- * outside 0..15 only query.  Returns the previous options. */
+ * outside 0..127 only query.  Returns the previous options. */
 int dsp_stft_soa_options(int options);
 
 /* Diagnostics. */

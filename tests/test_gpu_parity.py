@@ -280,3 +280,22 @@ def test_soa_kernel_options(torch_cuda, oracle, opt, B):
     finally:
         L.dsp_stft_kernel_variant(oldv)
         L.dsp_stft_soa_options(oldo)
+
+
+@pytest.mark.parametrize("B", [2, 64, 128, 256, 1024, 2048, 4096, 8192])
+def test_pk_ramp_table_periods(torch_cuda, oracle, B):
+    """Packed kernel (variant 5): the IR_test block table is fetched once
+    per period of B / 128 columns and aliased (stft_pk.hip PER)."""
+    L = d.lib()
+    oldv = L.dsp_stft_kernel_variant(5)
+    try:
+        n = 8192 * 4 + 777
+        x = rnd((2, n), 62)
+        out, mag = d.render_stft(to_dev(torch_cuda, x), 2, B, 48000.0, d.Plugin.ir_test(0.7, 0.001),
+                                 window=d.DSP_WIN_HANN, sample_offset=B * 3)
+        ref = oracle.render_offline([x[0], x[1]], 2, B, 48000.0, oracle.restated_plugin("IR_test", [0.7, 0.001]))
+        assert np.array_equal(out.cpu().numpy(), ref)
+        mref = oracle.np_stft_mag(ref[1], 8192, 4096, d.DSP_WIN_HANN, 4097)
+        assert peak_rel_err(mag.cpu().numpy()[1], mref) <= PEAK_REL_TOL
+    finally:
+        L.dsp_stft_kernel_variant(oldv)

@@ -1,4 +1,7 @@
-"""Interleaved in-process A/B of the SoA kernel option bits (rule 24)."""
+"""Interleaved in-process A/B of the kernel option bits (rule 24).
+  usage: python tools/ab_soa.py ROUNDS [vVARIANT] [opts...]
+variant 2: opts are dsp_stft_soa_options values; variant 5: opts are the
+packed kernel's bits (passed as 14 | opt << 4)."""
 import ctypes as C
 import os
 import statistics
@@ -16,12 +19,16 @@ F = d.stft_frames(nb * 512, 8192, 4096)
 out = torch.empty((2, nb * 512), device="cuda")
 mag = torch.empty((2, F, 4097), device="cuda")
 lib = d.lib()
-lib.dsp_stft_kernel_variant(2)
-opts = [int(a) for a in sys.argv[2:]] or list(range(0, 16, 2))
+args = sys.argv[2:]
+variant = 2
+if args and args[0].startswith("v"):
+    variant, args = int(args[0][1:]), args[1:]
+lib.dsp_stft_kernel_variant(variant)
+opts = [int(a) for a in args] or (list(range(0, 16, 2)) if variant == 2 else list(range(8)))
 res = {}
 for rnd in range(int(sys.argv[1]) if len(sys.argv) > 1 else 6):
     for o in opts:
-        lib.dsp_stft_soa_options(o)
+        lib.dsp_stft_soa_options(o if variant == 2 else 14 | (o << 4))
         for kind in ("fused", "mem"):
             def run():
                 if kind == "fused":
