@@ -36,6 +36,8 @@ sys.path.insert(0, os.path.join(REPO, "dsp-bench_amd"))
 
 METRIC = "Msamples/s offline render+8192-pt FFT, 48kHz stereo, 1/2/4/8 GPU; %HBM roofline"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+KERNELS = {0: "stft8192_kernel", 1: "stft8192_pair_kernel", 2: "stft8192_soa_kernel",
+           3: "stft8192_pair_soa_kernel", 4: "stft8192_pair2_kernel", 5: "stft8192_pk_kernel"}
 SR, CH, B, N_FFT, HOP = 48_000, 2, 512, 8192, 4096
 K_BINS = N_FFT // 2 + 1
 
@@ -56,6 +58,21 @@ def parse():
                     help="headline = IR_test + STFT 48 kHz (the metric); stft96k = BASELINE cfg 4 "
                          "(STFT of 1 h stereo 96 kHz from HBM); gain10min = cfg 2 render")
     return ap.parse_args()
+
+
+def pmc_traffic(workload: str, kernel: str, src: int):
+    """HBM bytes per launch of `kernel` from the committed PMC summary of the
+    same bench command (tools/pmc.sh + tools/pmc_summary.py --json, FETCH_SIZE
+    x2 + WRITE_SIZE per MI355X_MICROARCH.md), or (None, None)."""
+    import glob
+    paths = sorted(glob.glob(os.path.join(REPO, "profiles", f"r*_pmc_{workload}.json")))
+    if not paths:
+        return None, None
+    doc = json.load(open(paths[-1]))
+    for name, m in doc.get("kernels", {}).items():
+        if f"{kernel}<{src}," in name and "hbm_bytes" in m:
+            return float(m["hbm_bytes"]), os.path.relpath(paths[-1], REPO)
+    return None, None
 
 
 def cpu_baseline(seconds_budget: float):
@@ -130,12 +147,12 @@ def main():
                           K=K_BINS, out=out, mag=mag, sample_offset=soff)
         workload = ("IR_test render (B=512) + 8192-pt Hann STFT, hop 4096, 4097 bins, "
                     f"{minutes:g} min of 48 kHz stereo per GPU")
-        kname = "stft8192_kernel<render> (fused render + window + FFT + |X|)"
+        kname = f"{KERNELS[args.stft_variant]}<render> (fused render + window + FFT + |X|)"
     elif wl == "stft96k":
         def step():
             d.stft_magnitude(x, N=N_FFT, H=HOP, window=d.DSP_WIN_HANN, K=K_BINS, out=mag)
         workload = f"8192-pt Hann STFT, hop 4096, 4097 bins, {minutes:g} min of 96 kHz stereo per GPU (cfg 4)"
-        kname = "stft8192_kernel<memory> (window + FFT + |X|)"
+        kname = f"{KERNELS[args.stft_variant]}<memory> (window + FFT + |X|)"
     else:
         def step():
             d.render_offline(x, CH, B, float(sr), plugin, out=out)
@@ -198,6 +215,10 @@ def main():
         dist.barrier()
         gather_ms = (time.perf_counter() - tg) * 1e3
 
+    traffic, traffic_src = (None, None)
+    if wl != "gain10min":
+        traffic, traffic_src = pmc_traffic(wl, KERNELS[args.stft_variant], 1 if wl == "headline" else 0)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and wl == "headline":
         cpu = cpu_baseline(args.cpu_seconds)
@@ -231,9 +252,13 @@ def main():
                 "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                "traffic": None,
+                "traffic": None if traffic is None else round(traffic / 1e9, 4),
+                "traffic_unit": "GB per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
+                "traffic_source": traffic_src,
                 "kernel_avg_ms": round(kernel_avg_ms, 5),
                 "algorithmic_bytes_per_launch": int(bytes_per_launch),
+                "algorithmic": "fused: C*F*(4H + 4K) B (render write + |X| write; IR_test reads no input); "
+                               "memory: C*F*(4H + 4K) B (each sample read once + |X| write)",
             },
             "cpu_baseline": cpu,
         }
