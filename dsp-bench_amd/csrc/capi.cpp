@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "kernels.hpp"
+#include "dspbench/wav.h"
 
 namespace dspb {
 
@@ -865,6 +866,88 @@ int dsp_magnitude(const float *re, const float *im, float *out, uint64_t n, cons
     if (g.status) return g.status;
     int st = launch_magnitude(re, im, out, n, stream_of(ex));
     return st ? st : finish(ex);
+}
+
+// ---------------------------------------------------------------------------
+// WAV payload decode / encode (wav.h)
+// ---------------------------------------------------------------------------
+static int wav_fmt_ok(uint16_t format, uint16_t bits) {
+    return (format == DSP_WAV_FORMAT_PCM && (bits == 16 || bits == 24 || bits == 32)) ||
+           (format == DSP_WAV_FORMAT_FLOAT && bits == 32);
+}
+
+int dsp_wav_decode(const void *payload, const dsp_wav_info *info, uint64_t frame0, uint64_t frames,
+                   float *const *out, const dsp_exec *ex) {
+    if (!info || !wav_fmt_ok(info->format, info->bits_per_sample)) return invalid("bad dsp_wav_info format");
+    const uint32_t C = info->channels;
+    if (C == 0 || C > (uint32_t)kMaxChannels) return invalid("channels must be 1..%d", kMaxChannels);
+    if (frame0 > info->frames || frames > info->frames - frame0) return invalid("frame range past the payload");
+    if (frames == 0) return DSP_OK;
+    if (!payload || !out) return invalid("NULL buffer");
+    for (uint32_t c = 0; c < C; ++c)
+        if (!out[c]) return invalid("out[%u] is NULL", c);
+    DeviceGuard g(ex);
+    if (g.status) return g.status;
+    hipStream_t s = stream_of(ex);
+    const uint64_t ba = (uint64_t)C * (info->bits_per_sample / 8u);
+    const uint8_t *src = (const uint8_t *)payload;
+    uint64_t f0 = frame0;
+    ChanOut o{};
+    Staged stage;
+    if (host_mode(ex)) {
+        float *d;
+        int st = stage.alloc((frames * ba + 3) / 4, &d);
+        if (st) return st;
+        DSPB_HIP(hipMemcpyAsync(d, src + frame0 * ba, frames * ba, hipMemcpyHostToDevice, s));
+        src = (const uint8_t *)d;
+        f0 = 0;
+        for (uint32_t c = 0; c < C; ++c)
+            if ((st = stage.alloc(frames, &o.p[c]))) return st;
+    } else {
+        for (uint32_t c = 0; c < C; ++c) o.p[c] = out[c];
+    }
+    bool al = true;
+    for (uint32_t c = 0; c < C; ++c) al = al && aligned(o.p[c], 16);
+    int st = launch_wav_decode(src, C, info->bits_per_sample, info->format == DSP_WAV_FORMAT_FLOAT, f0,
+                               frames, o, al, s);
+    if (st) return st;
+    if (host_mode(ex))
+        for (uint32_t c = 0; c < C; ++c)
+            DSPB_HIP(hipMemcpyAsync(out[c], o.p[c], frames * sizeof(float), hipMemcpyDeviceToHost, s));
+    return finish(ex);
+}
+
+int dsp_wav_encode(const float *const *in, uint32_t C, uint64_t frames, uint16_t format, uint16_t bits,
+                   void *payload, const dsp_exec *ex) {
+    if (!wav_fmt_ok(format, bits)) return invalid("unsupported WAV sample format");
+    if (C == 0 || C > (uint32_t)kMaxChannels) return invalid("channels must be 1..%d", kMaxChannels);
+    if (frames == 0) return DSP_OK;
+    if (!in || !payload) return invalid("NULL buffer");
+    for (uint32_t c = 0; c < C; ++c)
+        if (!in[c]) return invalid("in[%u] is NULL", c);
+    DeviceGuard g(ex);
+    if (g.status) return g.status;
+    hipStream_t s = stream_of(ex);
+    const uint64_t bytes = frames * C * (bits / 8u);
+    uint8_t *dst = (uint8_t *)payload;
+    ChanOut i{};
+    Staged stage;
+    if (host_mode(ex)) {
+        float *d;
+        int st = stage.alloc((bytes + 3) / 4, &d);
+        if (st) return st;
+        dst = (uint8_t *)d;
+        for (uint32_t c = 0; c < C; ++c) {
+            if ((st = stage.alloc(frames, &i.p[c]))) return st;
+            DSPB_HIP(hipMemcpyAsync(i.p[c], in[c], frames * sizeof(float), hipMemcpyHostToDevice, s));
+        }
+    } else {
+        for (uint32_t c = 0; c < C; ++c) i.p[c] = const_cast<float *>(in[c]);
+    }
+    int st = launch_wav_encode(dst, C, bits, format == DSP_WAV_FORMAT_FLOAT, frames, i, s);
+    if (st) return st;
+    if (host_mode(ex)) DSPB_HIP(hipMemcpyAsync(payload, dst, bytes, hipMemcpyDeviceToHost, s));
+    return finish(ex);
 }
 
 }  // extern "C"

@@ -67,6 +67,10 @@ int launch_stft8192_pair(const Stft8kArgs &A, uint32_t C, bool fused, hipStream_
 int launch_stft8192_soa(const Stft8kArgs &A, uint32_t C, bool fused, int opt, hipStream_t s);
 int launch_stft8192_pair_soa(const Stft8kArgs &A, uint32_t C, bool fused, hipStream_t s);
 int launch_stft8192_pair2(const Stft8kArgs &A, uint32_t C, bool fused, hipStream_t s);
+int launch_wav_decode(const uint8_t *payload, uint32_t C, uint16_t bits, bool is_float, uint64_t frame0,
+                      uint64_t frames, const ChanOut &out, bool out_aligned16, hipStream_t s);
+int launch_wav_encode(uint8_t *payload, uint32_t C, uint16_t bits, bool is_float, uint64_t frames,
+                      const ChanOut &in, hipStream_t s);
 int launch_stft8192_pk(const Stft8kArgs &A, uint32_t C, bool fused, int opt, hipStream_t s);
 int launch_fft_generic(const GenericFftArgs &A, uint64_t transforms, uint32_t C, hipStream_t s);
 int launch_gain(const float *in, float *out, float g, uint64_t n, hipStream_t s);

@@ -37,7 +37,7 @@ enum { kAbLoad = 1, kAbWindow = 2, kAbDft1 = 4, kAbTw = 8, kAbLds = 16, kAbDft2 
 // default for the A/B-switchable headline shapes (tools/ab_soa.py, MI355X:
 // fused 0.73 -> 0.65 ms, memory 0.78 -> 0.71 ms per stereo hour vs 0);
 // other shapes run kSoaKmOpt (no computed window: partial frames allowed)
-constexpr int kSoaDefaultOpt = kOptPrefetchTw | kOptWinComp | kOptLdsTable;
+[[maybe_unused]] constexpr int kSoaDefaultOpt = kOptPrefetchTw | kOptWinComp | kOptLdsTable;
 constexpr int kSoaKmOpt = kOptLdsTable;
 
 template <int SRC, int KM, MapKind MK, bool POW2, int OPT>

@@ -6,8 +6,8 @@ from ._lib import (DSP_WIN_HAMMING, DSP_WIN_HANN, DSP_WIN_RECT, DspError, LIB_PA
                    lib)
 from .api import (IR_BUFFER_LENGTH, Plugin, fft_forward, fft_reverse, ir_analysis,  # noqa: F401
                   num_blocks, render_offline, render_stft, stft_frames, stft_magnitude)
-from . import shard  # noqa: F401
+from . import shard, wav  # noqa: F401
 
 __all__ = ["Plugin", "render_offline", "stft_magnitude", "render_stft", "ir_analysis",
            "fft_forward", "fft_reverse", "stft_frames", "num_blocks", "lib", "DspError",
-           "DSP_WIN_HAMMING", "DSP_WIN_HANN", "DSP_WIN_RECT", "IR_BUFFER_LENGTH", "shard"]
+           "DSP_WIN_HAMMING", "DSP_WIN_HANN", "DSP_WIN_RECT", "IR_BUFFER_LENGTH", "shard", "wav"]

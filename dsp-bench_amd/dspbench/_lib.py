@@ -1,4 +1,4 @@
-"""ctypes binding of libdspbench.so (include/dspbench/dspbench.h, host.h).
+"""ctypes binding of libdspbench.so (include/dspbench/dspbench.h, host.h, wav.h).
 
 The library is the product: there is no Python or CPU fallback behind these
 functions.  If the shared object is missing the import fails loudly.
@@ -47,6 +47,19 @@ class dsp_exec(C.Structure):
                 ("sample_offset", C.c_uint64)]
 
 
+DSP_WAV_FORMAT_PCM = 1
+DSP_WAV_FORMAT_FLOAT = 3
+DSP_WAV_MAX_DATA_CHUNKS = 8
+
+
+class dsp_wav_info(C.Structure):
+    _fields_ = [("format", C.c_uint16), ("channels", C.c_uint16), ("sample_rate", C.c_uint32),
+                ("bits_per_sample", C.c_uint16), ("block_align", C.c_uint16), ("frames", C.c_uint64),
+                ("data_bytes", C.c_uint64), ("n_data_chunks", C.c_uint32),
+                ("data_offset", C.c_uint64 * DSP_WAV_MAX_DATA_CHUNKS),
+                ("data_size", C.c_uint64 * DSP_WAV_MAX_DATA_CHUNKS)]
+
+
 FPP = C.POINTER(C.POINTER(C.c_float))
 FP = C.POINTER(C.c_float)
 
@@ -81,6 +94,13 @@ _SIGS = {
     "dsp_initializer_used": (C.c_size_t, [C.c_void_p]),
     "dsp_initializer_destroy": (None, [C.c_void_p]),
     "dsp_host_report": (None, [C.c_char_p, C.c_int]),
+    "dsp_wav_parse": (C.c_int, [C.c_void_p, C.c_uint64, C.POINTER(dsp_wav_info)]),
+    "dsp_wav_decode": (C.c_int, [C.c_void_p, C.POINTER(dsp_wav_info), C.c_uint64, C.c_uint64, FPP,
+                                 C.POINTER(dsp_exec)]),
+    "dsp_wav_encode": (C.c_int, [FPP, C.c_uint32, C.c_uint64, C.c_uint16, C.c_uint16, C.c_void_p,
+                                 C.POINTER(dsp_exec)]),
+    "dsp_wav_write_header": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint16, C.c_uint16, C.c_uint32,
+                                       C.c_uint16, C.c_uint64]),
 }
 
 _lib: C.CDLL | None = None

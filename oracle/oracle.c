@@ -436,3 +436,61 @@ uint32_t oracle_denormalize_enum_index(uint32_t num_entries, float nv)
 {
     return (uint32_t)(nv * (float)(num_entries - 1));
 }
+
+/* ------------------------------------------------------------------------ */
+/* WAV sample decode, restating ref audio.h:66-110                           */
+/* ------------------------------------------------------------------------ */
+
+void oracle_pcm_to_float(int bits, int is_float, const void *src, float *dst, uint64_t n) {
+    const uint8_t *d = (const uint8_t *)src;
+    for (uint64_t i = 0; i < n; ++i) {
+        if (is_float) { /* format 3: the bytes are the floats (wav_reader.h:186-189) */
+            memcpy(&dst[i], d + 4 * i, 4);
+        } else if (bits == 16) {
+            /* value = d0 << 16 | d1 << 24, / (float)(2^31 - 1) == 2^31 in float */
+            const int32_t v = (int32_t)((uint32_t)d[2 * i] << 16 | (uint32_t)d[2 * i + 1] << 24);
+            dst[i] = (float)v / 2147483648.0f;
+        } else if (bits == 24) {
+            /* value = d2 << 24 | d1 << 16 | d0 << 8, divided in DOUBLE by 2^31 - 1 */
+            const uint8_t *p = d + 3 * i;
+            const int32_t v = (int32_t)((uint32_t)p[2] << 24 | (uint32_t)p[1] << 16 | (uint32_t)p[0] << 8);
+            dst[i] = (float)((double)v / 2147483647.0);
+        } else { /* 32 */
+            const uint8_t *p = d + 4 * i;
+            const int32_t v = (int32_t)((uint32_t)p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16 |
+                                        (uint32_t)p[3] << 24);
+            dst[i] = (float)v / 2147483648.0f;
+        }
+    }
+}
+
+void oracle_deinterleave(float *const *dst, const float *src, uint64_t frames, uint32_t C) {
+    for (uint64_t f = 0; f < frames; ++f)
+        for (uint32_t c = 0; c < C; ++c) dst[c][f] = src[f * C + c];
+}
+
+static int64_t round_clip(double x, int64_t lo, int64_t hi) {
+    double r = nearbyint(x); /* default rounding mode: half to even */
+    if (r < (double)lo) r = (double)lo;
+    if (r > (double)hi) r = (double)hi;
+    return (int64_t)r;
+}
+
+void oracle_float_to_pcm(int bits, int is_float, const float *src, void *dst, uint64_t n) {
+    uint8_t *d = (uint8_t *)dst;
+    for (uint64_t i = 0; i < n; ++i) {
+        if (is_float) {
+            memcpy(d + 4 * i, &src[i], 4);
+        } else if (bits == 16) {
+            const int64_t v = round_clip((double)src[i] * 32768.0, -32768, 32767);
+            d[2 * i] = (uint8_t)(v & 0xff);
+            d[2 * i + 1] = (uint8_t)((v >> 8) & 0xff);
+        } else if (bits == 24) {
+            const int64_t v = round_clip((double)src[i] * 8388608.0, -8388608, 8388607);
+            for (int b = 0; b < 3; ++b) d[3 * i + b] = (uint8_t)((v >> (8 * b)) & 0xff);
+        } else {
+            const int64_t v = round_clip((double)src[i] * 2147483648.0, -2147483648LL, 2147483647LL);
+            for (int b = 0; b < 4; ++b) d[4 * i + b] = (uint8_t)((v >> (8 * b)) & 0xff);
+        }
+    }
+}

@@ -99,6 +99,16 @@ float    oracle_denormalize_float(float lo, float hi, int is_log, float nv);
 float    oracle_normalize_enum_index(uint32_t num_entries, int32_t index);
 uint32_t oracle_denormalize_enum_index(uint32_t num_entries, float nv);
 
+/* WAV sample decode (ref audio.h:66-110 + wav_reader.h:163-199): n
+ * interleaved samples of `bits` (16 / 24 / 32 PCM, or 32 with is_float =
+ * format 3) at src -> float at dst, then deinterleaved into C planar rows. */
+void oracle_pcm_to_float(int bits, int is_float, const void *src, float *dst, uint64_t n);
+void oracle_deinterleave(float *const *dst, const float *src, uint64_t frames, uint32_t C);
+/* The inverse for the WAV writer (not in the reference, which only renders
+ * to the device): float -> PCM with round-half-even and clipping to the
+ * integer range, or raw float (bits 32, is_float). */
+void oracle_float_to_pcm(int bits, int is_float, const float *src, void *dst, uint64_t n);
+
 #ifdef __cplusplus
 }
 #endif

@@ -281,3 +281,47 @@ def ir_ramp_reference(gain: float, step: float, n: int) -> np.ndarray:
         out[i] = np.float32(g)
         g = g - s
     return out
+
+
+# --------------------------------------------------------------------------
+# WAV sample decode (ref audio.h:66-133)
+# --------------------------------------------------------------------------
+
+def pcm_to_float(raw: np.ndarray, bits: int, is_float: bool = False) -> np.ndarray:
+    """oracle_pcm_to_float over a byte array (restated converters)."""
+    raw = np.ascontiguousarray(raw, np.uint8)
+    n = raw.size // (bits // 8)
+    out = np.empty(n, np.float32)
+    L = lib()
+    L.oracle_pcm_to_float.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_uint64]
+    L.oracle_pcm_to_float(bits, int(is_float), _ptr(raw), _ptr(out), n)
+    return out
+
+
+def float_to_pcm(x: np.ndarray, bits: int, is_float: bool = False) -> np.ndarray:
+    x = np.ascontiguousarray(x, np.float32)
+    out = np.empty(x.size * (bits // 8), np.uint8)
+    L = lib()
+    L.oracle_float_to_pcm.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_uint64]
+    L.oracle_float_to_pcm(bits, int(is_float), _ptr(x), _ptr(out), x.size)
+    return out
+
+
+def deinterleave(x: np.ndarray, channels: int) -> np.ndarray:
+    return np.ascontiguousarray(x.reshape(-1, channels).T)
+
+
+def ref_audio_available() -> bool:
+    return os.path.exists(os.path.join(REF_DIR, "libref_audio.so"))
+
+
+def ref_convert(raw: np.ndarray, bits: int) -> np.ndarray:
+    """The reference's own convertInt{16,24,32}ToFloat (oracle/_ref/libref_audio.so)."""
+    raw = np.ascontiguousarray(raw, np.uint8)
+    n = raw.size // (bits // 8)
+    out = np.empty(n, np.float32)
+    R = C.CDLL(os.path.join(REF_DIR, "libref_audio.so"))
+    fn = getattr(R, f"ref_convert_int{bits}")
+    fn.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
+    fn(_ptr(raw), _ptr(out), n)
+    return out

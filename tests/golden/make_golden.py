@@ -20,6 +20,9 @@ Where each vector comes from:
   S1  5-frame Hann STFT (N 8192, H 4096, 4097 bins) of a seeded sweep + noise,
       float64 numpy (IPP is absent: DIV_BY_SQRTN and sqrt(re^2+im^2) restated)
   P1  sine_test (stateful) callback, 4 blocks of 512, 2 ch (generic dispatch)
+  W1  WAV sample decode through the reference's own convertInt16/24/32ToFloat
+      (audio.h:66-110, oracle/_ref/libref_audio.so): every int16 code, every
+      int24 code, 2^20 seeded int32 codes + edges -- SHA-256 of the floats
 
 Usage: python tests/golden/make_golden.py   (writes next to this file)
 """
@@ -56,6 +59,16 @@ def signal_sweep(seed: int, n: int, sr: float = 96000.0) -> np.ndarray:
     ph = 2 * np.pi * f0 * T / k * (np.exp(t / T * k) - 1)
     noise = np.random.default_rng(seed).standard_normal(n) * 0.1
     return (0.1 * (np.sin(ph) + noise)).astype(np.float32)
+
+
+def wav_code_sets() -> dict:
+    """Little-endian sample bytes: all int16, all int24, 2^20 int32 (+ edges)."""
+    c16 = np.arange(1 << 16, dtype=np.uint32).astype("<u2").view(np.uint8)
+    c = np.arange(1 << 24, dtype=np.uint32)
+    c24 = np.stack([c & 0xff, (c >> 8) & 0xff, (c >> 16) & 0xff], axis=1).astype(np.uint8).ravel()
+    r = np.random.default_rng(5).integers(0, 1 << 32, 1 << 20, dtype=np.uint64).astype(np.uint32)
+    r[:6] = [0, 1, 0x7fffffff, 0x80000000, 0xffffffff, 0x40000000]
+    return {16: c16, 24: c24, 32: r.astype("<u4").view(np.uint8)}
 
 
 def main():
@@ -110,6 +123,13 @@ def main():
         blocks.append(o.callback_once(sp.as_oracle(), np.zeros((2, 512), np.float32), 48000.0))
     arrays["p1_sine_test"] = np.concatenate(blocks, axis=1)
     arrays["p1_sine_test_params"] = sp.params.copy()
+
+    # W1 -- WAV decode through the reference's converters
+    meta["wav_decode"] = {}
+    for bits, raw in wav_code_sets().items():
+        out = o.ref_convert(raw, bits)
+        meta["wav_decode"][str(bits)] = {"n": int(out.size), "sha256": sha(out),
+                                         "first": [float(v) for v in out[:4]]}
 
     meta["k4_flat"] = 0.2 * 0.08 / np.sqrt(8192.0)
     meta["k5_bins"] = {str(k): float(arrays["k5_mag"][k]) for k in (0, 1, 2, 4096, 8191)}
