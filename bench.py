@@ -54,9 +54,11 @@ def parse():
     ap.add_argument("--stft-variant", type=int, default=5, choices=[0, 1, 2, 3, 4, 5],
                     help="8192-pt kernel (dsp_stft_kernel_variant): 2 = wave/frame scalar SoA, "
                          "5 = wave/frame packed even/odd pairs")
-    ap.add_argument("--workload", default="headline", choices=["headline", "stft96k", "gain10min"],
+    ap.add_argument("--workload", default="headline",
+                    choices=["headline", "stft96k", "gain10min", "wav16", "wav24"],
                     help="headline = IR_test + STFT 48 kHz (the metric); stft96k = BASELINE cfg 4 "
-                         "(STFT of 1 h stereo 96 kHz from HBM); gain10min = cfg 2 render")
+                         "(STFT of 1 h stereo 96 kHz from HBM); gain10min = cfg 2 render; "
+                         "wav16 / wav24 = GPU decode of a 1 h stereo int16 / int24 WAV payload")
     return ap.parse_args()
 
 
@@ -125,7 +127,7 @@ def main():
     L -= L % HOP  # whole hops per rank (HOP is a multiple of B)
     # the file is world * L samples long; rank r owns [r L, (r+1) L) and
     # reads a halo of the next rank's first N - H samples (dspbench/shard.py)
-    sh = d.shard.plan(world * L, world, rank, B, N_FFT if wl != "gain10min" else HOP, HOP,
+    sh = d.shard.plan(world * L, world, rank, B, N_FFT if wl in ("headline", "stft96k") else HOP, HOP,
                       render=(wl == "headline"))
     assert sh.owned == L, (sh, L)
     L_in = sh.read_len
@@ -133,14 +135,16 @@ def main():
     x = (torch.rand((CH, L_in), device=dev, generator=g) * 2 - 1) * 0.1  # synthetic WAV
     nb = d.num_blocks(L_in, B)
     F = d.stft_frames(nb * B if wl == "headline" else L_in, N_FFT, HOP)
-    out = torch.empty((CH, nb * B), device=dev) if wl != "stft96k" else None
+    out = torch.empty((CH, nb * B), device=dev) if wl in ("headline", "gain10min") else None
     # rows: the last rank owns one frame less (no halo); equal-sized rows keep
     # the optional gather a plain dist.gather
-    mag = torch.empty((CH, max(F, L // HOP), K_BINS), device=dev) if wl != "gain10min" else None
+    mag = torch.empty((CH, max(F, L // HOP), K_BINS), device=dev) if wl in ("headline", "stft96k") else None
     plugin = d.Plugin.ir_test(0.9, 0.002) if wl == "headline" else d.Plugin.gain_test(0.2)
     stream = torch.cuda.current_stream(dev)
     soff = sh.start
 
+    lib0 = d.lib()
+    alg_bytes = None  # set where the library's own launch timing does not apply
     if wl == "headline":
         def step():
             d.render_stft(x, CH, B, float(sr), plugin, N=N_FFT, H=HOP, window=d.DSP_WIN_HANN,
@@ -153,11 +157,28 @@ def main():
             d.stft_magnitude(x, N=N_FFT, H=HOP, window=d.DSP_WIN_HANN, K=K_BINS, out=mag)
         workload = f"8192-pt Hann STFT, hop 4096, 4097 bins, {minutes:g} min of 96 kHz stereo per GPU (cfg 4)"
         kname = f"{KERNELS[args.stft_variant]}<memory> (window + FFT + |X|)"
-    else:
+    elif wl == "gain10min":
         def step():
             d.render_offline(x, CH, B, float(sr), plugin, out=out)
         workload = f"gain_test render (B=512), {minutes:g} min of 48 kHz stereo per GPU (cfg 2)"
         kname = "render_vec_kernel<Gain>"
+        alg_bytes = CH * L_in * 8  # read + write
+    else:
+        bits = 16 if wl == "wav16" else 24
+        pay = torch.randint(0, 256, (CH * L_in * bits // 8,), dtype=torch.uint8, device=dev, generator=g)
+        info = d._lib.dsp_wav_info(format=1, channels=CH, sample_rate=sr, bits_per_sample=bits,
+                                   block_align=CH * bits // 8, frames=L_in, data_bytes=pay.numel(),
+                                   n_data_chunks=1)
+        wout = torch.empty((CH, L_in), device=dev)
+        wptrs = d._lib.chan_table([wout[c].data_ptr() for c in range(CH)])
+        wex = d.api._exec(wout)
+
+        def step():
+            d._lib.check(lib0.dsp_wav_decode(C.c_void_p(pay.data_ptr()), C.byref(info), 0, L_in, wptrs,
+                                             C.byref(wex)), "dsp_wav_decode")
+        workload = f"WAV int{bits} stereo payload -> planar float (decode + deinterleave), {minutes:g} min of 48 kHz per GPU"
+        kname = f"wav_decode_kernel<{bits}, PCM, 2 ch>"
+        alg_bytes = CH * L_in * (bits // 8 + 4)
 
     for _ in range(args.warmup):
         step()
@@ -196,6 +217,9 @@ def main():
 
     kernel_avg_ms = k_ms.value / max(1, k_n.value)
     bytes_per_launch = k_bytes.value / max(1, k_n.value)
+    if k_n.value == 0 and alg_bytes is not None:  # one kernel per step, timed by the step events
+        kernel_avg_ms = ev_ms / args.steps
+        bytes_per_launch = alg_bytes
     achieved = bytes_per_launch / (kernel_avg_ms / 1e3) / 1e9 if kernel_avg_ms > 0 else 0.0
 
     gather_ms = None
@@ -216,7 +240,7 @@ def main():
         gather_ms = (time.perf_counter() - tg) * 1e3
 
     traffic, traffic_src = (None, None)
-    if wl != "gain10min":
+    if wl in ("headline", "stft96k"):
         traffic, traffic_src = pmc_traffic(wl, KERNELS[args.stft_variant], 1 if wl == "headline" else 0)
 
     cpu = None

@@ -950,4 +950,63 @@ int dsp_wav_encode(const float *const *in, uint32_t C, uint64_t frames, uint16_t
     return finish(ex);
 }
 
+// ---------------------------------------------------------------------------
+// display reductions
+// ---------------------------------------------------------------------------
+int dsp_minmax_decimate(const float *x, uint64_t n, uint32_t pixels, float *vmax, float *vmin,
+                        const dsp_exec *ex) {
+    if (pixels == 0) return DSP_OK;
+    if (!vmax || !vmin || (n && !x)) return invalid("NULL buffer");
+    if (pixels > (1u << 24) || n >= (1ull << 39)) return invalid("pixels <= 2^24 and n < 2^39");
+    DeviceGuard g(ex);
+    if (g.status) return g.status;
+    hipStream_t s = stream_of(ex);
+    const float *dx = x;
+    float *dmax = vmax, *dmin = vmin;
+    Staged stage;
+    if (host_mode(ex)) {
+        float *t;
+        int st;
+        if ((st = stage.alloc(n, &t))) return st;
+        if (n) DSPB_HIP(hipMemcpyAsync(t, x, n * sizeof(float), hipMemcpyHostToDevice, s));
+        dx = t;
+        if ((st = stage.alloc(pixels, &dmax)) || (st = stage.alloc(pixels, &dmin))) return st;
+    }
+    int st = launch_minmax(dx, n, pixels, dmax, dmin, s);
+    if (st) return st;
+    if (host_mode(ex)) {
+        DSPB_HIP(hipMemcpyAsync(vmax, dmax, pixels * sizeof(float), hipMemcpyDeviceToHost, s));
+        DSPB_HIP(hipMemcpyAsync(vmin, dmin, pixels * sizeof(float), hipMemcpyDeviceToHost, s));
+    }
+    return finish(ex);
+}
+
+int dsp_spectrogram_decimate(const float *mag, uint64_t F, uint32_t K, uint64_t ld, uint32_t pixels,
+                             float *out, const dsp_exec *ex) {
+    if (pixels == 0 || K == 0) return DSP_OK;
+    if (!out || (F && !mag)) return invalid("NULL buffer");
+    if (ld < K) return invalid("ld < K");
+    if (pixels > (1u << 24) || F >= (1ull << 39)) return invalid("pixels <= 2^24 and F < 2^39");
+    DeviceGuard g(ex);
+    if (g.status) return g.status;
+    hipStream_t s = stream_of(ex);
+    const float *dm = mag;
+    float *dout = out;
+    Staged stage;
+    if (host_mode(ex)) {
+        float *t;
+        int st;
+        const uint64_t nin = F ? (F - 1) * ld + K : 0;
+        if ((st = stage.alloc(nin, &t))) return st;
+        if (nin) DSPB_HIP(hipMemcpyAsync(t, mag, nin * sizeof(float), hipMemcpyHostToDevice, s));
+        dm = t;
+        if ((st = stage.alloc((uint64_t)pixels * K, &dout))) return st;
+    }
+    int st = launch_spectro(dm, F, K, ld, pixels, dout, s);
+    if (st) return st;
+    if (host_mode(ex))
+        DSPB_HIP(hipMemcpyAsync(out, dout, (uint64_t)pixels * K * sizeof(float), hipMemcpyDeviceToHost, s));
+    return finish(ex);
+}
+
 }  // extern "C"

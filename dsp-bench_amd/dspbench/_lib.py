@@ -94,6 +94,9 @@ _SIGS = {
     "dsp_initializer_used": (C.c_size_t, [C.c_void_p]),
     "dsp_initializer_destroy": (None, [C.c_void_p]),
     "dsp_host_report": (None, [C.c_char_p, C.c_int]),
+    "dsp_minmax_decimate": (C.c_int, [FP, C.c_uint64, C.c_uint32, FP, FP, C.POINTER(dsp_exec)]),
+    "dsp_spectrogram_decimate": (C.c_int, [FP, C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint32, FP,
+                                           C.POINTER(dsp_exec)]),
     "dsp_wav_parse": (C.c_int, [C.c_void_p, C.c_uint64, C.POINTER(dsp_wav_info)]),
     "dsp_wav_decode": (C.c_int, [C.c_void_p, C.POINTER(dsp_wav_info), C.c_uint64, C.c_uint64, FPP,
                                  C.POINTER(dsp_exec)]),

@@ -225,3 +225,31 @@ def fft_reverse(re, im):
     ex = _exec(re if _is_torch(re) else None)
     check(L.lib().dsp_fft_reverse(_fp(re), _fp(im), _fp(out), n, C.byref(ex)), "dsp_fft_reverse")
     return out
+
+
+# --------------------------------------------------------------------------
+# display reductions (long-file overviews)
+# --------------------------------------------------------------------------
+
+def minmax_decimate(x, pixels: int):
+    """Per-pixel (max, min) of a 1-D signal, the reference's IR view
+    (opengl.h:877-890).  Returns (vmax [pixels], vmin [pixels])."""
+    ref = x if _is_torch(x) else None
+    vmax = _alloc_like(ref, (max(pixels, 1),))
+    vmin = _alloc_like(ref, (max(pixels, 1),))
+    ex = _exec(ref)
+    st = L.lib().dsp_minmax_decimate(_fp(x), x.shape[0], pixels, _fp(vmax), _fp(vmin), C.byref(ex))
+    check(st, "dsp_minmax_decimate")
+    return vmax[:pixels], vmin[:pixels]
+
+
+def spectrogram_decimate(mag, pixels: int):
+    """[F, K] magnitudes (row stride = mag's) -> [pixels, K] column maxima."""
+    ref = mag if _is_torch(mag) else None
+    F, K = int(mag.shape[0]), int(mag.shape[1])
+    ld = (mag.stride(0) if _is_torch(mag) else mag.strides[0] // 4)
+    out = _alloc_like(ref, (max(pixels, 1), K))
+    ex = _exec(ref)
+    st = L.lib().dsp_spectrogram_decimate(_fp(mag), F, K, ld, pixels, _fp(out), C.byref(ex))
+    check(st, "dsp_spectrogram_decimate")
+    return out[:pixels]

@@ -42,7 +42,10 @@ def decode(data, info: dsp_wav_info, frame0: int = 0, frames: int | None = None,
     if device is not None:
         import torch
         if not _is_torch(data):
-            data = torch.from_numpy(np.ascontiguousarray(data)).to(device)
+            import warnings
+            with warnings.catch_warnings():  # read-only memmap: only read, never written
+                warnings.simplefilter("ignore", UserWarning)
+                data = torch.from_numpy(np.ascontiguousarray(data)).to(device)
         out = torch.empty((info.channels, max(frames, 1)), dtype=torch.float32, device=data.device)
         ptrs = [out[c].data_ptr() for c in range(info.channels)]
         ex = _exec(out)

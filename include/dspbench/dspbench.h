@@ -145,6 +145,18 @@ int dsp_set(float value, float *out, uint64_t n, const dsp_exec *ex);
 int dsp_magnitude(const float *re, const float *im, float *out, uint64_t n,
                   const dsp_exec *ex);
 
+/* Display reductions for long-file overviews.
+ * minmax: the IR / waveform view's per-pixel extremes (opengl.h:877-890):
+ *   vmax[p] = max(-1, max x[s]), vmin[p] = min(+1, min x[s]) over the
+ *   samples s with s * pixels / n == p (the reference's initial values; the
+ *   index product is 64-bit here, the reference's u32 product wraps).
+ * spectrogram: out[p * K + k] = max of mag[f * ld + k] over the frames f
+ *   with f * pixels / F == p (0 for an empty column). */
+int dsp_minmax_decimate(const float *x, uint64_t n, uint32_t pixels, float *vmax, float *vmin,
+                        const dsp_exec *ex);
+int dsp_spectrogram_decimate(const float *mag, uint64_t F, uint32_t K, uint64_t ld,
+                             uint32_t pixels, float *out, const dsp_exec *ex);
+
 /* Kernel timing: when enabled, every launch of the dominant kernel of
  * dsp_render_stft / dsp_stft_magnitude (the 8192-point wave-per-frame kernel)
  * is bracketed by HIP events on its stream.  dsp_kernel_timing() waits for

@@ -494,3 +494,35 @@ void oracle_float_to_pcm(int bits, int is_float, const float *src, void *dst, ui
         }
     }
 }
+
+/* ------------------------------------------------------------------------ */
+/* Display reductions                                                         */
+/* ------------------------------------------------------------------------ */
+
+/* IR waveform min/max per pixel, restating opengl.h:877-890: every pixel
+ * starts at {max = -1, min = +1} (the reference's init), then sample s goes
+ * to pixel s * P / n.  The index product is 64-bit here (the reference's
+ * u32 product wraps once s * P >= 2^32). */
+void oracle_minmax_decimate(const float *x, uint64_t n, uint32_t P, float *vmax, float *vmin) {
+    for (uint32_t p = 0; p < P; ++p) {
+        vmax[p] = -1.0f;
+        vmin[p] = 1.0f;
+    }
+    for (uint64_t s = 0; s < n; ++s) {
+        const uint64_t p = s * (uint64_t)P / n;
+        if (x[s] > vmax[p]) vmax[p] = x[s];
+        if (x[s] < vmin[p]) vmin[p] = x[s];
+    }
+}
+
+/* Spectrogram overview: column p = max over the frames f with f * P / F == p
+ * of mag[f * ld + k], k < K. */
+void oracle_spectrogram_decimate(const float *mag, uint64_t F, uint32_t K, uint64_t ld, uint32_t P,
+                                 float *out) {
+    for (uint64_t i = 0; i < (uint64_t)P * K; ++i) out[i] = 0.0f;
+    for (uint64_t f = 0; f < F; ++f) {
+        const uint64_t p = f * (uint64_t)P / F;
+        for (uint32_t k = 0; k < K; ++k)
+            if (mag[f * ld + k] > out[p * K + k]) out[p * K + k] = mag[f * ld + k];
+    }
+}

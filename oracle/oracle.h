@@ -109,6 +109,11 @@ void oracle_deinterleave(float *const *dst, const float *src, uint64_t frames, u
  * integer range, or raw float (bits 32, is_float). */
 void oracle_float_to_pcm(int bits, int is_float, const float *src, void *dst, uint64_t n);
 
+/* Display reductions (ref opengl.h:877-890, draw.h:150-160). */
+void oracle_minmax_decimate(const float *x, uint64_t n, uint32_t P, float *vmax, float *vmin);
+void oracle_spectrogram_decimate(const float *mag, uint64_t F, uint32_t K, uint64_t ld, uint32_t P,
+                                 float *out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -325,3 +325,28 @@ def ref_convert(raw: np.ndarray, bits: int) -> np.ndarray:
     fn.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
     fn(_ptr(raw), _ptr(out), n)
     return out
+
+
+# --------------------------------------------------------------------------
+# display reductions (ref opengl.h:877-890)
+# --------------------------------------------------------------------------
+
+def minmax_decimate(x: np.ndarray, pixels: int):
+    x = np.ascontiguousarray(x, np.float32)
+    vmax = np.empty(pixels, np.float32)
+    vmin = np.empty(pixels, np.float32)
+    L = lib()
+    L.oracle_minmax_decimate.argtypes = [C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p, C.c_void_p]
+    L.oracle_minmax_decimate(_ptr(x), x.size, pixels, _ptr(vmax), _ptr(vmin))
+    return vmax, vmin
+
+
+def spectrogram_decimate(mag: np.ndarray, pixels: int) -> np.ndarray:
+    mag = np.ascontiguousarray(mag, np.float32)
+    F, K = mag.shape
+    out = np.empty((pixels, K), np.float32)
+    L = lib()
+    L.oracle_spectrogram_decimate.argtypes = [C.c_void_p, C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint32,
+                                              C.c_void_p]
+    L.oracle_spectrogram_decimate(_ptr(mag), F, K, K, pixels, _ptr(out))
+    return out
