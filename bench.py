@@ -36,6 +36,7 @@ sys.path.insert(0, os.path.join(REPO, "dsp-bench_amd"))
 
 METRIC = "Msamples/s offline render+8192-pt FFT, 48kHz stereo, 1/2/4/8 GPU; %HBM roofline"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+FP32_PEAK_TFLOPS = 157.3  # MI355X FP32 vector (packed) peak, same table
 KERNELS = {0: "stft8192_kernel", 1: "stft8192_pair_kernel", 2: "stft8192_soa_kernel",
            3: "stft8192_pair_soa_kernel", 4: "stft8192_pair2_kernel", 5: "stft8192_pk_kernel"}
 SR, CH, B, N_FFT, HOP = 48_000, 2, 512, 8192, 4096
@@ -55,7 +56,7 @@ def parse():
                     help="8192-pt kernel (dsp_stft_kernel_variant): 2 = wave/frame scalar SoA, "
                          "5 = wave/frame packed even/odd pairs")
     ap.add_argument("--workload", default="headline",
-                    choices=["headline", "stft96k", "gain10min", "wav16", "wav24"],
+                    choices=["headline", "stft96k", "gain10min", "fir1024", "wav16", "wav24"],
                     help="headline = IR_test + STFT 48 kHz (the metric); stft96k = BASELINE cfg 4 "
                          "(STFT of 1 h stereo 96 kHz from HBM); gain10min = cfg 2 render; "
                          "wav16 / wav24 = GPU decode of a 1 h stereo int16 / int24 WAV payload")
@@ -122,7 +123,7 @@ def main():
 
     wl = args.workload
     sr = 96_000 if wl == "stft96k" else SR
-    minutes = args.minutes if wl != "gain10min" or args.minutes != 60.0 else 10.0
+    minutes = args.minutes if wl not in ("gain10min", "fir1024") or args.minutes != 60.0 else 10.0
     L = int(round(minutes * 60 * sr))
     L -= L % HOP  # whole hops per rank (HOP is a multiple of B)
     # the file is world * L samples long; rank r owns [r L, (r+1) L) and
@@ -135,7 +136,7 @@ def main():
     x = (torch.rand((CH, L_in), device=dev, generator=g) * 2 - 1) * 0.1  # synthetic WAV
     nb = d.num_blocks(L_in, B)
     F = d.stft_frames(nb * B if wl == "headline" else L_in, N_FFT, HOP)
-    out = torch.empty((CH, nb * B), device=dev) if wl in ("headline", "gain10min") else None
+    out = torch.empty((CH, nb * B), device=dev) if wl in ("headline", "gain10min", "fir1024") else None
     # rows: the last rank owns one frame less (no halo); equal-sized rows keep
     # the optional gather a plain dist.gather
     mag = torch.empty((CH, max(F, L // HOP), K_BINS), device=dev) if wl in ("headline", "stft96k") else None
@@ -145,6 +146,7 @@ def main():
 
     lib0 = d.lib()
     alg_bytes = None  # set where the library's own launch timing does not apply
+    alg_flops = None  # FLOP-bound workloads (fir1024)
     if wl == "headline":
         def step():
             d.render_stft(x, CH, B, float(sr), plugin, N=N_FFT, H=HOP, window=d.DSP_WIN_HANN,
@@ -157,6 +159,17 @@ def main():
             d.stft_magnitude(x, N=N_FFT, H=HOP, window=d.DSP_WIN_HANN, K=K_BINS, out=mag)
         workload = f"8192-pt Hann STFT, hop 4096, 4097 bins, {minutes:g} min of 96 kHz stereo per GPU (cfg 4)"
         kname = f"{KERNELS[args.stft_variant]}<memory> (window + FFT + |X|)"
+    elif wl == "fir1024":
+        # BASELINE configs[2] / SURVEY cfg 3b: 1024 taps = compute_IR(IR_test)[0:1024]
+        ir, _ = d.ir_analysis(d.Plugin.ir_test(0.9, 0.002), C_out=1, sr=float(sr), device=dev)
+        fplug = d.Plugin.fir(ir[0, :1024].cpu().numpy())
+
+        def step():
+            d.render_offline(x, CH, B, float(sr), fplug, out=out)
+        workload = (f"FIR render, 1024 taps = compute_IR(IR_test)[0:1024], B=512, {minutes:g} min of "
+                    "48 kHz stereo per GPU (cfg 3b)")
+        kname = "fir_kernel (packed fp32 direct form)"
+        alg_flops = 2.0 * 1024 * CH * nb * B
     elif wl == "gain10min":
         def step():
             d.render_offline(x, CH, B, float(sr), plugin, out=out)
@@ -269,7 +282,17 @@ def main():
                 "sharding": "time-chunk per GPU, 4096-sample halo, no data-path collective",
                 "gather_ms": None if gather_ms is None else round(gather_ms, 3),
             },
-            "roofline": {
+            "roofline": ({
+                "bound": "fp32-vector",
+                "kernel": kname,
+                "achieved": round(alg_flops / (kernel_avg_ms / 1e3) / 1e12, 2),
+                "peak": FP32_PEAK_TFLOPS,
+                "unit": "TFLOP/s",
+                "frac": round(alg_flops / (kernel_avg_ms / 1e3) / 1e12 / FP32_PEAK_TFLOPS, 4),
+                "traffic": None,
+                "kernel_avg_ms": round(kernel_avg_ms, 5),
+                "algorithmic": "2 * taps FLOP per output sample",
+            } if alg_flops is not None else {
                 "bound": "hbm",
                 "kernel": kname,
                 "achieved": round(achieved, 1),
@@ -283,7 +306,7 @@ def main():
                 "algorithmic_bytes_per_launch": int(bytes_per_launch),
                 "algorithmic": "fused: C*F*(4H + 4K) B (render write + |X| write; IR_test reads no input); "
                                "memory: C*F*(4H + 4K) B (each sample read once + |X| write)",
-            },
+            }),
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -252,6 +252,8 @@ static int plugin_map(const dsp_plugin *p, uint32_t B, int dev, hipStream_t s, S
     m->table = nullptr;
     m->B = B;
     m->b_mask = is_pow2(B) ? B - 1 : 0;
+    m->taps = nullptr;
+    m->ntaps8 = 0;
     if (!p) return DSP_OK;  // no plugin loaded: the file plays through (audio.cpp:144)
     float v0 = 0.f, v1 = 0.f;
     switch (p->kind) {
@@ -280,6 +282,23 @@ static int plugin_map(const dsp_plugin *p, uint32_t B, int dev, hipStream_t s, S
         if (st) return st;
         m->kind = MapKind::Ramp;
         m->table = table;
+        return DSP_OK;
+    }
+    case DSP_PLUGIN_FIR: {  // build-defined cfg 3b: Parameters{float taps[T]}
+        const uint32_t T = p->params_size / 4;
+        if (!p->params || T == 0 || p->params_size % 4 || T > 4096)
+            return invalid("FIR plugin needs 1..4096 float taps as its params blob");
+        const uint32_t T8 = (T + 7) & ~7u;
+        std::vector<float> h(T8, 0.f);
+        std::memcpy(h.data(), p->params, 4 * (size_t)T);
+        float *taps = nullptr;
+        int st = get_scratch(dev, s, sizeof(float) * T8, &taps);
+        if (st) return st;
+        DSPB_HIP(hipMemcpyAsync(taps, h.data(), sizeof(float) * T8, hipMemcpyHostToDevice, s));
+        DSPB_HIP(hipStreamSynchronize(s));  // h is a stack buffer
+        m->kind = MapKind::Fir;
+        m->taps = taps;
+        m->ntaps8 = T8;
         return DSP_OK;
     }
     case DSP_PLUGIN_GENERIC:
@@ -327,6 +346,15 @@ static int render_device(const float *const *in, uint32_t in_ch, uint64_t L, flo
                          uint64_t goff, hipStream_t s) {
     const uint64_t nblocks = (L + B - 1) / B;
     const uint64_t end = nblocks * B;
+    if (map.kind == MapKind::Fir) {  // convolution from the start of the file
+        if (start != 0 || goff != 0) return invalid("FIR render: whole files only (sample_offset 0)");
+        for (uint32_t c = 0; c < C; ++c) {
+            int st = launch_fir(c < in_ch ? in[c] : nullptr, L, out[c], end, map.taps, map.ntaps8,
+                                aligned(out[c], 16), s);
+            if (st) return st;
+        }
+        return DSP_OK;
+    }
     for (uint32_t c0 = 0; c0 < C; c0 += kMaxChannels) {
         const uint32_t cn = (C - c0) < (uint32_t)kMaxChannels ? (C - c0) : kMaxChannels;
         RenderArgs A{};
@@ -636,7 +664,8 @@ int dsp_render_stft(const float *const *in, uint32_t in_channels, uint64_t L,
     if ((st = plugin_map(plugin, B, g.dev, s, &map))) return st;
     const uint64_t goff = goff_of(ex);
 
-    bool fused = (N == 8192) && (H % 128 == 0) && (H <= N) && (goff % 2 == 0) && F > 0;
+    bool fused = (N == 8192) && (H % 128 == 0) && (H <= N) && (goff % 2 == 0) && F > 0 &&
+                 map.kind != MapKind::Fir;
     for (uint32_t c = 0; c < C; ++c) fused = fused && aligned(dout[c], 8);
     for (uint32_t c = 0; c < in_channels; ++c) fused = fused && aligned(din[c], 8);
 

@@ -21,7 +21,7 @@ struct ChanOut {
 // Per-sample plugin maps that the render / fused kernels specialise on.
 // `table` is the IR_test ramp (B floats) computed on the device by
 // ramp_table_kernel; the others use the scalar `a`.
-enum class MapKind : int { Noop = 0, Gain = 1, Ramp = 3 };
+enum class MapKind : int { Noop = 0, Gain = 1, Ramp = 3, Fir = 4 };
 
 struct SampleMap {
     MapKind kind;
@@ -29,6 +29,8 @@ struct SampleMap {
     const float *table;  // ramp table (Ramp)
     uint32_t B;          // block size
     uint32_t b_mask;     // B - 1 when B is a power of two, else 0
+    const float *taps;   // FIR taps, zero-padded to ntaps8 (Fir; not a per-sample map)
+    uint32_t ntaps8;
 };
 
 __device__ __forceinline__ uint32_t block_pos(const SampleMap &m, uint64_t gi) {

@@ -1,0 +1,90 @@
+// fir.hip -- direct-form FIR render (BASELINE cfg 3 / SURVEY 8(d) cfg 3b:
+// a 1024-tap FIR whose taps are compute_IR(IR_test)[0:1024]).
+//
+//   y[n] = sum_{k < T} h[k] x[n - k],  x[m] = 0 for m < 0 and m >= L
+//
+// which is exactly what a stateful FIR plugin pumped block by block from the
+// start of the file computes (state = the last T - 1 inputs, zero at
+// start; one-shot render, zero past EOF, audio.cpp:13-175).  The reference
+// ships no FIR; this is the build-defined cfg 3b.
+//
+// FP32 vector-FLOP bound (2T flop per sample), so the inner loop is packed:
+// thread t of a 256-thread workgroup owns the 16 outputs b..b+15 as 8 VGPR
+// pairs acc[i] = (y[b+i], y[b+8+i]); the input pairs P[q] = (x[b+q],
+// x[b+8+q]) slide one position per tap, so each tap is one ds_read_b64
+// (the new pair, from an LDS copy holding (x[m], x[m+8]) side by side) + 8 v_pk_fma_f32 with the tap broadcast from an SGPR.  The
+// workgroup's 4096 outputs read their 4096 + T - 1 inputs once from HBM into
+// LDS.  Accumulation order per output: k = 0, 1, ..., T - 1.
+#include "kernels.hpp"
+
+namespace dspb {
+
+constexpr int kFirTile = 4096;  // outputs per workgroup (256 threads x 16)
+constexpr int kFirMaxTaps = 4096;
+
+__global__ __launch_bounds__(256) void fir_kernel(const float *__restrict__ x, uint64_t L, float *__restrict__ y,
+                                                  uint64_t Ly, const float *__restrict__ h, uint32_t T8,
+                                                  bool vec) {
+    // xs2[j] = (x[base + j], x[base + j + 8]): the input pair of a tap is one
+    // ds_read_b64 straight into the VGPR pair the v_pk_fma reads
+    extern __shared__ v2f xs2[];
+    const uint64_t n0 = (uint64_t)blockIdx.x * kFirTile;
+    const uint32_t t = threadIdx.x;
+    const uint32_t nx = kFirTile + T8 + 8;
+    const int64_t base = (int64_t)n0 - (int64_t)(T8 - 1);
+    for (uint32_t j = t; j < nx; j += 256) {
+        const int64_t m0 = base + j, m1 = m0 + 8;
+        const float a = (x != nullptr && m0 >= 0 && (uint64_t)m0 < L) ? x[m0] : 0.f;
+        const float b = (x != nullptr && m1 >= 0 && (uint64_t)m1 < L) ? x[m1] : 0.f;
+        xs2[j] = v2f{a, b};
+    }
+    __syncthreads();
+
+    const uint32_t o = 16u * t + T8 - 1;  // xs2 index of (x[b], x[b + 8])
+    v2f acc[8];
+    v2f win[8];  // win[q & 7] = P[q] = (x[b + q], x[b + 8 + q])
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        acc[i] = v2f{0.f, 0.f};
+        win[i] = xs2[o + i];
+    }
+    for (uint32_t k0 = 0; k0 < T8; k0 += 8) {
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk) {
+            const uint32_t k = k0 + kk;
+            if (k > 0) win[(8 - kk) & 7] = xs2[o - k];  // P[-k]
+            const float hk = h[k];                       // uniform: SGPR
+#pragma unroll
+            for (int i = 0; i < 8; ++i) acc[i] = win[(i - kk) & 7] * v2f{hk, hk} + acc[i];
+        }
+    }
+    const uint64_t b = n0 + 16u * t;
+    if (vec && b + 16 <= Ly) {
+        float4 *y4 = reinterpret_cast<float4 *>(y + b);
+        y4[0] = float4{acc[0].x, acc[1].x, acc[2].x, acc[3].x};
+        y4[1] = float4{acc[4].x, acc[5].x, acc[6].x, acc[7].x};
+        y4[2] = float4{acc[0].y, acc[1].y, acc[2].y, acc[3].y};
+        y4[3] = float4{acc[4].y, acc[5].y, acc[6].y, acc[7].y};
+    } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            if (b + i < Ly) y[b + i] = acc[i].x;
+            if (b + 8 + i < Ly) y[b + 8 + i] = acc[i].y;
+        }
+    }
+}
+
+// h8: T8 = ceil(T / 8) * 8 taps (zero-padded), device memory
+int launch_fir(const float *x, uint64_t L, float *y, uint64_t Ly, const float *h8, uint32_t T8,
+               bool y_aligned16, hipStream_t s) {
+    if (Ly == 0) return DSP_OK;
+    if (T8 == 0 || T8 % 8 || T8 > (uint32_t)kFirMaxTaps) return DSP_ERR_INVALID;
+    const uint64_t groups = (Ly + kFirTile - 1) / kFirTile;
+    if (groups > 0x7fffffffull) return DSP_ERR_INVALID;
+    const size_t lds = sizeof(v2f) * (kFirTile + T8 + 8);
+    hipLaunchKernelGGL(fir_kernel, dim3((uint32_t)groups), dim3(256), lds, s, x, L, y, Ly, h8, T8, y_aligned16);
+    DSPB_HIP(hipGetLastError());
+    return DSP_OK;
+}
+
+}  // namespace dspb

@@ -67,6 +67,8 @@ int launch_stft8192_pair(const Stft8kArgs &A, uint32_t C, bool fused, hipStream_
 int launch_stft8192_soa(const Stft8kArgs &A, uint32_t C, bool fused, int opt, hipStream_t s);
 int launch_stft8192_pair_soa(const Stft8kArgs &A, uint32_t C, bool fused, hipStream_t s);
 int launch_stft8192_pair2(const Stft8kArgs &A, uint32_t C, bool fused, hipStream_t s);
+int launch_fir(const float *x, uint64_t L, float *y, uint64_t Ly, const float *h8, uint32_t T8,
+               bool y_aligned16, hipStream_t s);
 int launch_minmax(const float *x, uint64_t n, uint32_t P, float *vmax, float *vmin, hipStream_t s);
 int launch_spectro(const float *mag, uint64_t F, uint32_t K, uint64_t ld, uint32_t P, float *out,
                    hipStream_t s);

@@ -58,6 +58,12 @@ class Plugin:
     def no_op() -> "Plugin":
         return Plugin(L.DSP_PLUGIN_NOOP, b"", b"", "no_op")
 
+    @staticmethod
+    def fir(taps) -> "Plugin":
+        """Build-defined FIR (cfg 3b): y[n] = sum_k taps[k] x[n - k]."""
+        t = np.ascontiguousarray(np.asarray(taps, dtype=np.float32))
+        return Plugin(L.DSP_PLUGIN_FIR, t.tobytes(), b"", f"fir{t.size}")
+
     def as_struct(self) -> dsp_plugin:
         p = C.create_string_buffer(self.params, max(1, len(self.params)))
         s = C.create_string_buffer(self.state, max(1, len(self.state)))

@@ -526,3 +526,21 @@ void oracle_spectrogram_decimate(const float *mag, uint64_t F, uint32_t K, uint6
             if (mag[f * ld + k] > out[p * K + k]) out[p * K + k] = mag[f * ld + k];
     }
 }
+
+/* ------------------------------------------------------------------------ */
+/* FIR (build-defined cfg 3b)                                                 */
+/* ------------------------------------------------------------------------ */
+
+/* y[n] = sum_{k<T} h[k] x[n-k] for n < Ly, x = 0 outside [0, L); double
+ * accumulation (the float64 reference the fp32 GPU sum is checked against). */
+void oracle_fir_f64(const float *x, uint64_t L, const float *h, uint32_t T, double *y, uint64_t Ly) {
+    #pragma omp parallel for schedule(static)
+    for (int64_t n = 0; n < (int64_t)Ly; ++n) {
+        double acc = 0.0;
+        for (uint32_t k = 0; k < T && (uint64_t)k <= (uint64_t)n; ++k) {
+            const uint64_t m = (uint64_t)n - k;
+            if (x && m < L) acc += (double)h[k] * (double)x[m];
+        }
+        y[n] = acc;
+    }
+}

@@ -114,6 +114,9 @@ void oracle_minmax_decimate(const float *x, uint64_t n, uint32_t P, float *vmax,
 void oracle_spectrogram_decimate(const float *mag, uint64_t F, uint32_t K, uint64_t ld, uint32_t P,
                                  float *out);
 
+/* FIR render (build-defined cfg 3b), float64 accumulation. */
+void oracle_fir_f64(const float *x, uint64_t L, const float *h, uint32_t T, double *y, uint64_t Ly);
+
 #ifdef __cplusplus
 }
 #endif

@@ -350,3 +350,16 @@ def spectrogram_decimate(mag: np.ndarray, pixels: int) -> np.ndarray:
                                               C.c_void_p]
     L.oracle_spectrogram_decimate(_ptr(mag), F, K, K, pixels, _ptr(out))
     return out
+
+
+def fir_f64(x, taps, Ly: int | None = None) -> np.ndarray:
+    """y[n] = sum_k taps[k] x[n - k] (x = 0 outside the file), float64."""
+    x = np.ascontiguousarray(x, np.float32) if x is not None else None
+    h = np.ascontiguousarray(taps, np.float32)
+    L_ = 0 if x is None else x.size
+    Ly = L_ if Ly is None else Ly
+    y = np.empty(max(Ly, 1), np.float64)
+    Lb = lib()
+    Lb.oracle_fir_f64.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint64]
+    Lb.oracle_fir_f64(_ptr(x) if x is not None else None, L_, _ptr(h), h.size, _ptr(y), Ly)
+    return y[:Ly]

@@ -1,0 +1,103 @@
+"""FIR render (build-defined cfg 3b, BASELINE configs[2]): a 1024-tap FIR
+whose taps are compute_IR(IR_test)[0:1024], over 48 kHz stereo in 512-sample
+blocks.  The reference ships no FIR plugin; the oracle is the float64
+convolution (oracle_fir_f64, pinned to numpy.convolve on CPU).
+
+Tolerance (floating point): the GPU sums the T products of each output in
+order k = 0..T-1 in fp32 with FMAs, so |y - y64| <= (T + 1) u sum_k
+|h_k x_{n-k}| with u = 2^-24 -- checked per sample against that bound.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import dspbench as d
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+G = np.load(os.path.join(HERE, "golden", "golden_v1.npz"))
+U = 2.0 ** -24
+
+
+def cfg3b_taps():
+    return G["ir_IR_test"][0][:1024].copy()   # compute_IR(IR_test) of the reference plugin
+
+
+def check_fir(oracle, y, x, taps, Ly):
+    y64 = oracle.fir_f64(x, taps, Ly)
+    bound = oracle.fir_f64(np.abs(x) if x is not None else None, np.abs(taps), Ly) * (len(taps) + 1) * U
+    err = np.abs(y.astype(np.float64) - y64)
+    assert np.all(err <= bound + 1e-30), float(np.max(err - bound))
+
+
+def test_oracle_fir_is_numpy_convolve(oracle):
+    rng = np.random.default_rng(0)
+    x, h = rng.standard_normal(3000).astype(np.float32), rng.standard_normal(77).astype(np.float32)
+    ref = np.convolve(x.astype(np.float64), h.astype(np.float64))[:3072]
+    want = np.zeros(3072)
+    want[:ref.size] = ref
+    assert np.max(np.abs(oracle.fir_f64(x, h, 3072) - want)) < 1e-12
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("T", [1, 7, 8, 64, 1024, 1031, 4096])
+@pytest.mark.parametrize("L,B", [(100, 512), (5000, 100), (70_001, 512)])
+def test_gpu_fir_render(torch_cuda, oracle, T, L, B):
+    rng = np.random.default_rng(T * 7 + L)
+    x = rng.uniform(-1, 1, (2, L)).astype(np.float32)
+    taps = (rng.standard_normal(T) / np.sqrt(T)).astype(np.float32)
+    out = d.render_offline(torch_cuda.from_numpy(x).cuda(), 2, B, 48000.0, d.Plugin.fir(taps)).cpu().numpy()
+    Ly = -(-L // B) * B
+    assert out.shape == (2, Ly)
+    for c in range(2):
+        check_fir(oracle, out[c], x[c], taps, Ly)
+    host = d.render_offline(x, 2, B, 48000.0, d.Plugin.fir(taps))          # host buffers
+    assert np.array_equal(host, out)
+
+
+@pytest.mark.gpu
+def test_gpu_fir_channels_and_missing_input(torch_cuda, oracle):
+    x = np.random.default_rng(5).uniform(-1, 1, (1, 9000)).astype(np.float32)
+    taps = cfg3b_taps()
+    out = d.render_offline(torch_cuda.from_numpy(x).cuda(), 3, 512, 48000.0, d.Plugin.fir(taps)).cpu().numpy()
+    check_fir(oracle, out[0], x[0], taps, out.shape[1])
+    assert not out[1:].any()   # extra channels: zero input through the FIR
+
+
+@pytest.mark.gpu
+def test_gpu_fir_cfg3b_full_size(torch_cuda, oracle):
+    """cfg 3b at full size: 10 min of 48 kHz stereo, B = 512, the 1024 IR_test
+    taps; 4000 sampled outputs + both ends against float64."""
+    torch = torch_cuda
+    L = 28_800_000
+    g = torch.Generator(device="cuda").manual_seed(2)
+    x = torch.rand((2, L), device="cuda", generator=g) * 2 - 1
+    taps = cfg3b_taps()
+    out = d.render_offline(x, 2, 512, 48000.0, d.Plugin.fir(taps))
+    rng = np.random.default_rng(1)
+    idx = np.concatenate([np.arange(2048), np.arange(L - 2048, L), rng.integers(0, L, 4000)])
+    for c in range(2):
+        xc = x[c].cpu().numpy()
+        y = out[c].cpu().numpy()
+        for n in idx[::7]:
+            lo = max(0, n - 1023)
+            seg = xc[lo:n + 1][::-1].astype(np.float64)
+            ref = float(np.dot(taps[:seg.size].astype(np.float64), seg))
+            bnd = 1025 * U * float(np.dot(np.abs(taps[:seg.size]).astype(np.float64), np.abs(seg)))
+            assert abs(float(y[n]) - ref) <= bnd + 1e-30
+
+
+@pytest.mark.gpu
+def test_gpu_fir_stft_and_ir(torch_cuda, oracle):
+    torch = torch_cuda
+    taps = cfg3b_taps()
+    x = np.random.default_rng(8).uniform(-1, 1, (2, 8192 * 3)).astype(np.float32)
+    out, mag = d.render_stft(torch.from_numpy(x).cuda(), 2, 512, 48000.0, d.Plugin.fir(taps))
+    o = out.cpu().numpy()
+    check_fir(oracle, o[1], x[1], taps, o.shape[1])
+    mref = oracle.np_stft_mag(o[1], 8192, 4096, d.DSP_WIN_HANN, 4097)
+    m = mag.cpu().numpy()[1]
+    assert np.max(np.abs(m - mref)) <= 1e-6 * np.max(mref)
+    ir, imag = d.ir_analysis(d.Plugin.fir(taps), C_out=2, device="cuda")    # IR of a FIR = its taps
+    assert np.array_equal(ir.cpu().numpy()[0, :1024], taps) and not ir.cpu().numpy()[0, 1024:].any()
+    assert np.max(np.abs(imag.cpu().numpy() - oracle.np_ir_magnitude(taps, 2048))) <= 1e-6 * 14.1
