@@ -202,3 +202,15 @@ def test_windowing_hamming_service(svc, oracle):
     y = np.empty_like(x)
     svc.windowing_hamming(x.ctypes.data, y.ctypes.data, 2048)
     assert np.max(np.abs(y - oracle.np_window(oracle.WIN_HAMMING, 2048))) <= 6e-8
+
+
+def test_library_has_no_unresolved_internal_symbols():
+    """Every symbol of the library's own namespace is defined in it (a
+    kernel file missing from the Makefile shows up here, not at dlopen on
+    the GPU box with immediate binding)."""
+    import subprocess
+    out = subprocess.run(["nm", "-D", "--undefined-only", _lib.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    bad = [l for l in out.splitlines() if "dspb" in l or " dsp_" in l]
+    assert not bad, bad
+    C.CDLL(_lib.LIB_PATH, mode=os.RTLD_NOW)
