@@ -286,9 +286,9 @@ static int plugin_map(const dsp_plugin *p, uint32_t B, int dev, hipStream_t s, S
     }
     case DSP_PLUGIN_FIR: {  // build-defined cfg 3b: Parameters{float taps[T]}
         const uint32_t T = p->params_size / 4;
-        if (!p->params || T == 0 || p->params_size % 4 || T > 4096)
-            return invalid("FIR plugin needs 1..4096 float taps as its params blob");
-        const uint32_t T8 = (T + 7) & ~7u;
+        if (!p->params || T == 0 || p->params_size % 4 || T > 2048)
+            return invalid("FIR plugin needs 1..2048 float taps as its params blob");
+        const uint32_t T8 = (T + 15) & ~15u;  // zero-padded to 16 (fir.hip)
         std::vector<float> h(T8, 0.f);
         std::memcpy(h.data(), p->params, 4 * (size_t)T);
         float *taps = nullptr;

@@ -29,7 +29,7 @@ struct SampleMap {
     const float *table;  // ramp table (Ramp)
     uint32_t B;          // block size
     uint32_t b_mask;     // B - 1 when B is a power of two, else 0
-    const float *taps;   // FIR taps, zero-padded to ntaps8 (Fir; not a per-sample map)
+    const float *taps;   // FIR taps, zero-padded to ntaps8 = ceil(T/16)*16 (Fir; not a per-sample map)
     uint32_t ntaps8;
 };
 

@@ -20,40 +20,47 @@
 namespace dspb {
 
 constexpr int kFirTile = 4096;  // outputs per workgroup (256 threads x 16)
-constexpr int kFirMaxTaps = 4096;
+constexpr int kFirMaxTaps = 2048;  // LDS: (4096 + T + 8) * 17 / 16 pairs <= 64 KB
+
+// LDS layout: pair e at e + (e >> 4) -- one pad slot every 16 pairs, so the
+// 64 lanes of a tap (pairs 16 t + c) hit 17 t + c' and spread over all banks
+// (unpadded, every lane 128 B apart: a 32-way bank conflict).
+__device__ __forceinline__ uint32_t fir_slot(uint32_t e) { return e + (e >> 4); }
 
 __global__ __launch_bounds__(256) void fir_kernel(const float *__restrict__ x, uint64_t L, float *__restrict__ y,
-                                                  uint64_t Ly, const float *__restrict__ h, uint32_t T8,
+                                                  uint64_t Ly, const float *__restrict__ h, uint32_t T16,
                                                   bool vec) {
-    // xs2[j] = (x[base + j], x[base + j + 8]): the input pair of a tap is one
+    // pair e = (x[base + e], x[base + e + 8]): the input pair of a tap is one
     // ds_read_b64 straight into the VGPR pair the v_pk_fma reads
     extern __shared__ v2f xs2[];
     const uint64_t n0 = (uint64_t)blockIdx.x * kFirTile;
     const uint32_t t = threadIdx.x;
-    const uint32_t nx = kFirTile + T8 + 8;
-    const int64_t base = (int64_t)n0 - (int64_t)(T8 - 1);
+    const uint32_t nx = kFirTile + T16 + 8;
+    const int64_t base = (int64_t)n0 - (int64_t)(T16 - 1);
     for (uint32_t j = t; j < nx; j += 256) {
         const int64_t m0 = base + j, m1 = m0 + 8;
         const float a = (x != nullptr && m0 >= 0 && (uint64_t)m0 < L) ? x[m0] : 0.f;
         const float b = (x != nullptr && m1 >= 0 && (uint64_t)m1 < L) ? x[m1] : 0.f;
-        xs2[j] = v2f{a, b};
+        xs2[fir_slot(j)] = v2f{a, b};
     }
     __syncthreads();
 
-    const uint32_t o = 16u * t + T8 - 1;  // xs2 index of (x[b], x[b + 8])
+    const uint32_t o = 16u * t + T16 - 1;  // pair index of (x[b], x[b + 8]); o % 16 == 15
     v2f acc[8];
     v2f win[8];  // win[q & 7] = P[q] = (x[b + q], x[b + 8 + q])
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
         acc[i] = v2f{0.f, 0.f};
-        win[i] = xs2[o + i];
+        win[i] = xs2[fir_slot(o + i)];
     }
-    for (uint32_t k0 = 0; k0 < T8; k0 += 8) {
+    for (uint32_t k0 = 0; k0 < T16; k0 += 16) {
+        // pairs o - k0 - kk, kk < 16, share o - k0's 16-block: slot = s0 - kk
+        const v2f *row = xs2 + fir_slot(o - k0);
 #pragma unroll
-        for (int kk = 0; kk < 8; ++kk) {
+        for (int kk = 0; kk < 16; ++kk) {
             const uint32_t k = k0 + kk;
-            if (k > 0) win[(8 - kk) & 7] = xs2[o - k];  // P[-k]
-            const float hk = h[k];                       // uniform: SGPR
+            if (k > 0) win[(8 - kk) & 7] = row[-kk];  // P[-k]
+            const float hk = h[k];                    // uniform: SGPR
 #pragma unroll
             for (int i = 0; i < 8; ++i) acc[i] = win[(i - kk) & 7] * v2f{hk, hk} + acc[i];
         }
@@ -74,15 +81,16 @@ __global__ __launch_bounds__(256) void fir_kernel(const float *__restrict__ x, u
     }
 }
 
-// h8: T8 = ceil(T / 8) * 8 taps (zero-padded), device memory
-int launch_fir(const float *x, uint64_t L, float *y, uint64_t Ly, const float *h8, uint32_t T8,
+// h16: T16 = ceil(T / 16) * 16 taps (zero-padded), device memory
+int launch_fir(const float *x, uint64_t L, float *y, uint64_t Ly, const float *h16, uint32_t T16,
                bool y_aligned16, hipStream_t s) {
     if (Ly == 0) return DSP_OK;
-    if (T8 == 0 || T8 % 8 || T8 > (uint32_t)kFirMaxTaps) return DSP_ERR_INVALID;
+    if (T16 == 0 || T16 % 16 || T16 > (uint32_t)kFirMaxTaps) return DSP_ERR_INVALID;
     const uint64_t groups = (Ly + kFirTile - 1) / kFirTile;
     if (groups > 0x7fffffffull) return DSP_ERR_INVALID;
-    const size_t lds = sizeof(v2f) * (kFirTile + T8 + 8);
-    hipLaunchKernelGGL(fir_kernel, dim3((uint32_t)groups), dim3(256), lds, s, x, L, y, Ly, h8, T8, y_aligned16);
+    const uint32_t nx = kFirTile + T16 + 8;
+    const size_t lds = sizeof(v2f) * (nx + nx / 16 + 1);
+    hipLaunchKernelGGL(fir_kernel, dim3((uint32_t)groups), dim3(256), lds, s, x, L, y, Ly, h16, T16, y_aligned16);
     DSPB_HIP(hipGetLastError());
     return DSP_OK;
 }

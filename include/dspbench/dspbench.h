@@ -68,7 +68,7 @@ enum dsp_plugin_kind {
     DSP_PLUGIN_STATIC_GAIN = 2, /* test/static_gain_plugin.cpp: out *= state.gain (f32 @0) */
     DSP_PLUGIN_IR_RAMP = 3,     /* build/IR_test.cpp: out[s] = (float)g_s, g -= step (f32 @0, @4) */
     DSP_PLUGIN_FIR = 4,         /* build-defined cfg 3b: y[n] = sum_k taps[k] x[n-k], params = float taps[T],
-                                   T <= 4096; state carries across blocks, so whole files only
+                                   T <= 2048; state carries across blocks, so whole files only
                                    (sample_offset 0; shard by channel) */
     DSP_PLUGIN_GENERIC = 16     /* compiled audio_callback run on the GPU (module) */
 };
