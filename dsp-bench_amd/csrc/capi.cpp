@@ -246,7 +246,8 @@ static bool aligned(const void *p, size_t a) { return ((uintptr_t)p % a) == 0; }
 // ---------------------------------------------------------------------------
 // plugin -> sample map
 // ---------------------------------------------------------------------------
-static int plugin_map(const dsp_plugin *p, uint32_t B, int dev, hipStream_t s, SampleMap *m) {
+static int plugin_map(const dsp_plugin *p, uint32_t B, int dev, hipStream_t s, SampleMap *m,
+                      float sr = 48000.f) {
     m->kind = MapKind::Noop;
     m->a = 1.f;
     m->table = nullptr;
@@ -254,6 +255,10 @@ static int plugin_map(const dsp_plugin *p, uint32_t B, int dev, hipStream_t s, S
     m->b_mask = is_pow2(B) ? B - 1 : 0;
     m->taps = nullptr;
     m->ntaps8 = 0;
+    m->module = nullptr;
+    m->gparams = nullptr;
+    m->gparams_size = 0;
+    m->sr = sr;
     if (!p) return DSP_OK;  // no plugin loaded: the file plays through (audio.cpp:144)
     float v0 = 0.f, v1 = 0.f;
     switch (p->kind) {
@@ -301,9 +306,13 @@ static int plugin_map(const dsp_plugin *p, uint32_t B, int dev, hipStream_t s, S
         m->ntaps8 = T8;
         return DSP_OK;
     }
-    case DSP_PLUGIN_GENERIC:
-        set_last_error("DSP_PLUGIN_GENERIC: generic GPU dispatch is not in this build");
-        return DSP_ERR_UNSUPPORTED;
+    case DSP_PLUGIN_GENERIC:  // the plugin's own audio_callback, compiled for gfx950 (module.h)
+        if (!p->module) return invalid("GENERIC plugin needs a loaded dsp_module");
+        m->kind = MapKind::Generic;
+        m->module = const_cast<void *>(p->module);
+        m->gparams = p->params;
+        m->gparams_size = p->params_size;
+        return DSP_OK;
     default:
         return invalid("unknown plugin kind %d", p->kind);
     }
@@ -346,6 +355,11 @@ static int render_device(const float *const *in, uint32_t in_ch, uint64_t L, flo
                          uint64_t goff, hipStream_t s) {
     const uint64_t nblocks = (L + B - 1) / B;
     const uint64_t end = nblocks * B;
+    if (map.kind == MapKind::Generic) {
+        if (start != 0) return invalid("GENERIC render: the fused tail path does not apply");
+        return module_render((::dsp_module *)map.module, map.gparams, map.gparams_size, in, in_ch, L, out, C, B,
+                             map.sr, goff, s);
+    }
     if (map.kind == MapKind::Fir) {  // convolution from the start of the file
         if (start != 0 || goff != 0) return invalid("FIR render: whole files only (sample_offset 0)");
         for (uint32_t c = 0; c < C; ++c) {
@@ -531,7 +545,7 @@ uint64_t dsp_stft_frame_count(uint64_t L, uint32_t N, uint32_t H) {
 int dsp_render_offline(const float *const *in, uint32_t in_channels, uint64_t L,
                        float *const *out, uint32_t C, uint32_t B, float sr,
                        const dsp_plugin *plugin, const dsp_exec *ex) {
-    (void)sr;  // none of the map kernels reads the sample rate
+    // (only a GENERIC plugin reads the sample rate)
     if (B == 0) return invalid("block size B must be > 0");
     if (C == 0) return DSP_OK;
     if (!out) return invalid("out is NULL");
@@ -567,7 +581,7 @@ int dsp_render_offline(const float *const *in, uint32_t in_channels, uint64_t L,
         for (uint32_t c = 0; c < C; ++c) dout[c] = out[c];
     }
     SampleMap map;
-    int st = plugin_map(plugin, B, g.dev, s, &map);
+    int st = plugin_map(plugin, B, g.dev, s, &map, sr);
     if (st) return st;
     TimedLaunch tl{};
     if ((st = timing_begin(s, &tl))) return st;
@@ -623,7 +637,7 @@ int dsp_render_stft(const float *const *in, uint32_t in_channels, uint64_t L,
                     float *const *out, uint32_t C, uint32_t B, float sr,
                     const dsp_plugin *plugin, uint32_t N, uint32_t H, int32_t window,
                     uint32_t K, float *const *mag, uint64_t ld, const dsp_exec *ex) {
-    (void)sr;
+
     if (B == 0) return invalid("block size B must be > 0");
     int st = check_stft_args(N, H, K, ld);
     if (st) return st;
@@ -661,11 +675,11 @@ int dsp_render_stft(const float *const *in, uint32_t in_channels, uint64_t L,
         for (uint32_t c = 0; c < C; ++c) { dout[c] = out[c]; dmag[c] = mag[c]; }
     }
     SampleMap map;
-    if ((st = plugin_map(plugin, B, g.dev, s, &map))) return st;
+    if ((st = plugin_map(plugin, B, g.dev, s, &map, sr))) return st;
     const uint64_t goff = goff_of(ex);
 
     bool fused = (N == 8192) && (H % 128 == 0) && (H <= N) && (goff % 2 == 0) && F > 0 &&
-                 map.kind != MapKind::Fir;
+                 map.kind != MapKind::Fir && map.kind != MapKind::Generic;
     for (uint32_t c = 0; c < C; ++c) fused = fused && aligned(dout[c], 8);
     for (uint32_t c = 0; c < in_channels; ++c) fused = fused && aligned(din[c], 8);
 
@@ -731,7 +745,6 @@ int dsp_render_stft(const float *const *in, uint32_t in_channels, uint64_t L,
 
 int dsp_ir_analysis(const dsp_plugin *plugin, uint32_t C, float sr, uint32_t ir_len,
                     float *const *ir_out, float *mag, const dsp_exec *ex) {
-    (void)sr;
     if (C == 0 || ir_len == 0) return invalid("C and ir_len must be > 0");
     if (!is_pow2(ir_len) || 4ull * ir_len > 8192) return invalid("4*ir_len must be a power of two <= 8192");
     if (!ir_out || !mag) return invalid("ir_out / mag is NULL");
@@ -759,9 +772,14 @@ int dsp_ir_analysis(const dsp_plugin *plugin, uint32_t C, float sr, uint32_t ir_
         DSPB_HIP(hipMemcpyAsync(dir[c], &one, sizeof(float), hipMemcpyHostToDevice, s));
     }
     SampleMap map;
-    if ((st = plugin_map(plugin, ir_len, g.dev, s, &map))) return st;
-    std::vector<const float *> cin(dir.begin(), dir.end());
-    if ((st = render_device(cin.data(), C, ir_len, dir.data(), C, ir_len, map, 0, 0, s))) return st;
+    if ((st = plugin_map(plugin, ir_len, g.dev, s, &map, sr))) return st;
+    if (map.kind == MapKind::Generic) {  // fresh scratch State, one callback in place
+        if ((st = module_ir((::dsp_module *)map.module, map.gparams, map.gparams_size, dir.data(), C, ir_len, sr, s)))
+            return st;
+    } else {
+        std::vector<const float *> cin(dir.begin(), dir.end());
+        if ((st = render_device(cin.data(), C, ir_len, dir.data(), C, ir_len, map, 0, 0, s))) return st;
+    }
 
     // fft_perform_and_get_magnitude (dsp.cpp:53-66): channel 0 only
     const v2f *tw = nullptr;

@@ -21,7 +21,7 @@ struct ChanOut {
 // Per-sample plugin maps that the render / fused kernels specialise on.
 // `table` is the IR_test ramp (B floats) computed on the device by
 // ramp_table_kernel; the others use the scalar `a`.
-enum class MapKind : int { Noop = 0, Gain = 1, Ramp = 3, Fir = 4 };
+enum class MapKind : int { Noop = 0, Gain = 1, Ramp = 3, Fir = 4, Generic = 5 };
 
 struct SampleMap {
     MapKind kind;
@@ -31,6 +31,10 @@ struct SampleMap {
     uint32_t b_mask;     // B - 1 when B is a power of two, else 0
     const float *taps;   // FIR taps, zero-padded to ntaps8 = ceil(T/16)*16 (Fir; not a per-sample map)
     uint32_t ntaps8;
+    void *module;        // Generic: the dsp_module running the plugin's own audio_callback
+    const void *gparams; // Generic: host Parameters blob
+    uint32_t gparams_size;
+    float sr;            // sample rate handed to the callback (Generic)
 };
 
 __device__ __forceinline__ uint32_t block_pos(const SampleMap &m, uint64_t gi) {

@@ -3,6 +3,8 @@
 #pragma once
 #include "common.hpp"
 
+struct dsp_module;  // include/dspbench/module.h
+
 namespace dspb {
 
 typedef float v2f __attribute__((ext_vector_type(2)));
@@ -67,6 +69,11 @@ int launch_stft8192_pair(const Stft8kArgs &A, uint32_t C, bool fused, hipStream_
 int launch_stft8192_soa(const Stft8kArgs &A, uint32_t C, bool fused, int opt, hipStream_t s);
 int launch_stft8192_pair_soa(const Stft8kArgs &A, uint32_t C, bool fused, hipStream_t s);
 int launch_stft8192_pair2(const Stft8kArgs &A, uint32_t C, bool fused, hipStream_t s);
+int module_render(::dsp_module *m, const void *params, uint32_t params_size, const float *const *in,
+                  uint32_t in_ch, uint64_t L, float *const *out, uint32_t C, uint32_t B, float sr,
+                  uint64_t goff, hipStream_t s);
+int module_ir(::dsp_module *m, const void *params, uint32_t params_size, float *const *bufs, uint32_t C,
+              uint32_t n, float sr, hipStream_t s);
 int launch_fir(const float *x, uint64_t L, float *y, uint64_t Ly, const float *h8, uint32_t T8,
                bool y_aligned16, hipStream_t s);
 int launch_minmax(const float *x, uint64_t n, uint32_t P, float *vmax, float *vmin, hipStream_t s);

@@ -1,0 +1,432 @@
+// module.cpp -- generic GPU dispatch: plugin source -> hiprtc -> gfx950 code
+// object -> kernels that call the plugin's own functions (module.h).
+//
+// The generated translation unit is, in order:
+//   plugin_device.h          (as "plugin_header.h": device services)
+//   #pragma clang force_cuda_host_device begin
+//   the plugin source         (unchanged; its #include of plugin_header.h
+//                              hits the include guard)
+//   #pragma clang force_cuda_host_device end
+//   kDriver                   (dspb_sizes / _defaults / _init / _render /
+//                              _callback kernels)
+// compiled with -ffp-contract=off so the plugin's float / double arithmetic
+// rounds as the CPU build of the same source does.
+#include <hip/hip_runtime.h>
+#include <hip/hiprtc.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "dspbench/module.h"
+#include "kernels.hpp"
+
+namespace {
+
+#include "plugin_device_src.inc"  // const char kPluginDeviceSrc[] (generated from plugin_device.h)
+
+// Host mirror of the driver's argument block (same layout on both sides).
+struct RenderArgsG {
+    void *P;
+    void *S;
+    float *in[dspb::kMaxChannels];
+    float *out[dspb::kMaxChannels];
+    unsigned long long L;
+    unsigned long long nblocks;
+    unsigned long long block0;
+    unsigned in_ch;
+    unsigned C;
+    unsigned B;
+    float sr;
+};
+
+const char *kDriver = R"DSPB(
+struct dspb_render_args {
+    void *P;
+    void *S;
+    float *in[16];
+    float *out[16];
+    unsigned long long L;
+    unsigned long long nblocks;
+    unsigned long long block0;
+    unsigned in_ch;
+    unsigned C;
+    unsigned B;
+    float sr;
+};
+extern "C" __global__ void dspb_sizes(unsigned *o) {
+    o[0] = sizeof(Parameters);
+    o[1] = sizeof(State);
+    o[2] = __is_empty(State) ? 1u : 0u;
+}
+extern "C" __global__ void dspb_defaults(Parameters *p) { *p = default_parameters(); }
+// non-const lvalues, as the reference's generated wrappers pass them
+// (compiler.cpp:1181-1203): plugins may take Parameters& or const Parameters&
+extern "C" __global__ void dspb_init(Parameters *p, State *s, unsigned C, float sr, dspb_arena *a) {
+    *s = initialize_state(*p, C, sr, (void *)a);
+}
+// one block: the render_audio body (audio.cpp:13-175), one-shot
+__device__ static void dspb_block(const dspb_render_args &A, unsigned long long b, State &st) {
+    float *ptrs[16];
+    const unsigned long long s0 = (A.block0 + b) * A.B;  // global sample of the block
+    for (unsigned c = 0; c < A.C; ++c) {
+        ptrs[c] = A.out[c] + b * A.B;
+        for (unsigned s = 0; s < A.B; ++s) {
+            const unsigned long long i = b * A.B + s;
+            ptrs[c][s] = (c < A.in_ch && i < A.L) ? A.in[c][i] : 0.0f;
+        }
+    }
+    (void)s0;
+    audio_callback(*(Parameters *)A.P, st, ptrs, A.C, A.B, A.sr);
+}
+extern "C" __global__ void dspb_render(dspb_render_args A) {
+    if (__is_empty(State)) {  // no state: every block on its own thread
+        State local = *(State *)A.S;
+        for (unsigned long long b = blockIdx.x * (unsigned long long)blockDim.x + threadIdx.x; b < A.nblocks;
+             b += (unsigned long long)gridDim.x * blockDim.x)
+            dspb_block(A, b, local);
+    } else if (blockIdx.x == 0 && threadIdx.x == 0) {  // stateful: in order, one thread
+        State &st = *(State *)A.S;
+        for (unsigned long long b = 0; b < A.nblocks; ++b) dspb_block(A, b, st);
+    }
+}
+// compute_IR (plugin.cpp:17-58): the callback once, on buffers as they are
+extern "C" __global__ void dspb_callback(dspb_render_args A) {
+    float *ptrs[16];
+    for (unsigned c = 0; c < A.C; ++c) ptrs[c] = A.out[c];
+    audio_callback(*(Parameters *)A.P, *(State *)A.S, ptrs, A.C, A.B, A.sr);
+}
+)DSPB";
+
+struct ArenaHost {  // mirror of dspb_arena
+    char *base;
+    unsigned long long capacity;
+    unsigned long long used;
+    float *fft_tmp;
+};
+
+}  // namespace
+
+struct dsp_module {
+    int device = -1;
+    hipModule_t mod = nullptr;
+    hipFunction_t f_sizes = nullptr, f_defaults = nullptr, f_init = nullptr, f_render = nullptr,
+                  f_callback = nullptr;
+    uint32_t params_size = 0, state_size = 0;
+    int stateless = 0;
+    void *d_params = nullptr;          // device Parameters
+    void *d_state[2] = {nullptr, nullptr};  // [0] live State, [1] compute_IR scratch State
+    ArenaHost *d_arena[2] = {nullptr, nullptr};
+    char *arena_mem[2] = {nullptr, nullptr};
+    bool initialized = false;
+    std::mutex mu;
+};
+
+namespace dspb {
+void set_last_error(const char *fmt, ...);
+int hip_fail(hipError_t e, const char *what);
+}  // namespace dspb
+using dspb::set_last_error;
+
+#define MOD_HIP(x)                                                   \
+    do {                                                             \
+        hipError_t e_ = (x);                                         \
+        if (e_ != hipSuccess) return dspb::hip_fail(e_, #x);         \
+    } while (0)
+
+namespace {
+
+int with_device(int device, int *prev) {
+    MOD_HIP(hipGetDevice(prev));
+    if (device >= 0 && device != *prev) MOD_HIP(hipSetDevice(device));
+    return DSP_OK;
+}
+
+int launch1(hipFunction_t f, void **args, hipStream_t s = nullptr) {
+    MOD_HIP(hipModuleLaunchKernel(f, 1, 1, 1, 1, 1, 1, 0, s, args, nullptr));
+    return DSP_OK;
+}
+
+int make_arena(dsp_module *m, int slot, uint64_t bytes) {
+    if (m->arena_mem[slot]) (void)hipFree(m->arena_mem[slot]);
+    m->arena_mem[slot] = nullptr;
+    if (!m->d_arena[slot]) MOD_HIP(hipMalloc(&m->d_arena[slot], sizeof(ArenaHost)));
+    if (bytes) MOD_HIP(hipMalloc(&m->arena_mem[slot], bytes));
+    if (bytes) MOD_HIP(hipMemset(m->arena_mem[slot], 0, bytes));
+    ArenaHost h{m->arena_mem[slot], bytes, 0, nullptr};
+    MOD_HIP(hipMemcpy(m->d_arena[slot], &h, sizeof h, hipMemcpyHostToDevice));
+    return DSP_OK;
+}
+
+int init_slot(dsp_module *m, int slot, const void *params, uint32_t C, float sr, uint64_t arena_bytes,
+              hipStream_t s) {
+    if (!params && m->params_size > 0) {
+        set_last_error("initialize_state: params blob is NULL");
+        return DSP_ERR_INVALID;
+    }
+    int st = make_arena(m, slot, arena_bytes);
+    if (st) return st;
+    MOD_HIP(hipMemcpy(m->d_params, params, m->params_size, hipMemcpyHostToDevice));
+    void *a_p = m->d_params, *a_s = m->d_state[slot], *a_a = m->d_arena[slot];
+    unsigned a_c = C;
+    float a_sr = sr;
+    void *args[] = {&a_p, &a_s, &a_c, &a_sr, &a_a};
+    if ((st = launch1(m->f_init, args, s))) return st;
+    ArenaHost h{};
+    MOD_HIP(hipMemcpyAsync(&h, m->d_arena[slot], sizeof h, hipMemcpyDeviceToHost, s));
+    MOD_HIP(hipStreamSynchronize(s));
+    if (h.used > h.capacity) {  // an allocator returned NULL: Runtime_Low_Memory (errors.inc:22-23)
+        set_last_error("initialize_state: arena of %llu bytes exhausted (%llu requested)",
+                       (unsigned long long)h.capacity, (unsigned long long)h.used);
+        return DSP_ERR_NOMEM;
+    }
+    return DSP_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dsp_module_compile(const char *source, const char *name, void **code, uint64_t *code_size, char *log,
+                       uint64_t log_cap) {
+    if (log && log_cap) log[0] = 0;
+    if (!source || !code || !code_size) {
+        set_last_error("dsp_module_compile: NULL argument");
+        return DSP_ERR_INVALID;
+    }
+    *code = nullptr;
+    *code_size = 0;
+    std::string tu;
+    tu += "#include \"plugin_header.h\"\n";
+    tu += "#pragma clang force_cuda_host_device begin\n";
+    tu += "#include \"dspb_plugin_source.cpp\"\n";
+    tu += "#pragma clang force_cuda_host_device end\n";
+    tu += kDriver;
+    const char *hdrs[2] = {kPluginDeviceSrc, source};
+    const char *hnames[2] = {"plugin_header.h", "dspb_plugin_source.cpp"};
+    hiprtcProgram prog;
+    if (hiprtcCreateProgram(&prog, tu.c_str(), name ? name : "plugin.cpp", 2, hdrs, hnames) != HIPRTC_SUCCESS) {
+        set_last_error("hiprtcCreateProgram failed");
+        return DSP_ERR_INVALID;
+    }
+    const char *opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++20", "-ffp-contract=off", "-w"};
+    const hiprtcResult rc = hiprtcCompileProgram(prog, (int)(sizeof opts / sizeof *opts), opts);
+    size_t ls = 0;
+    hiprtcGetProgramLogSize(prog, &ls);
+    std::vector<char> lg(ls + 1, 0);
+    if (ls) hiprtcGetProgramLog(prog, lg.data());
+    if (log && log_cap) {
+        std::strncpy(log, lg.data(), log_cap - 1);
+        log[log_cap - 1] = 0;
+    }
+    if (rc != HIPRTC_SUCCESS) {
+        hiprtcDestroyProgram(&prog);
+        set_last_error("plugin compile failed: %.400s", lg.data());
+        return DSP_ERR_INVALID;
+    }
+    size_t cs = 0;
+    hiprtcGetCodeSize(prog, &cs);
+    void *buf = std::malloc(cs ? cs : 1);
+    if (!buf) {
+        hiprtcDestroyProgram(&prog);
+        return DSP_ERR_NOMEM;
+    }
+    hiprtcGetCode(prog, (char *)buf);
+    hiprtcDestroyProgram(&prog);
+    *code = buf;
+    *code_size = cs;
+    return DSP_OK;
+}
+
+void dsp_module_free_code(void *code) { std::free(code); }
+
+int dsp_module_load(const void *code, uint64_t code_size, int device, dsp_module **out) {
+    if (!code || !code_size || !out) {
+        set_last_error("dsp_module_load: NULL argument");
+        return DSP_ERR_INVALID;
+    }
+    *out = nullptr;
+    int prev = -1;
+    int st = with_device(device, &prev);
+    if (st) return st;
+    dsp_module *m = new dsp_module();
+    (void)hipGetDevice(&m->device);
+    auto fail = [&](int s) {
+        dsp_module_destroy(m);
+        if (prev >= 0) (void)hipSetDevice(prev);
+        return s;
+    };
+    hipError_t e = hipModuleLoadData(&m->mod, code);
+    if (e != hipSuccess) return fail(dspb::hip_fail(e, "hipModuleLoadData"));
+    struct { hipFunction_t *f; const char *n; } fs[] = {{&m->f_sizes, "dspb_sizes"}, {&m->f_defaults, "dspb_defaults"},
+                                                        {&m->f_init, "dspb_init"}, {&m->f_render, "dspb_render"},
+                                                        {&m->f_callback, "dspb_callback"}};
+    for (auto &f : fs)
+        if ((e = hipModuleGetFunction(f.f, m->mod, f.n)) != hipSuccess) return fail(dspb::hip_fail(e, f.n));
+    unsigned *d_o = nullptr;
+    if ((e = hipMalloc(&d_o, 4 * sizeof(unsigned))) != hipSuccess) return fail(dspb::hip_fail(e, "hipMalloc"));
+    void *args[] = {&d_o};
+    st = launch1(m->f_sizes, args);
+    unsigned h[4] = {0, 0, 0, 0};
+    if (!st && (e = hipMemcpy(h, d_o, sizeof h, hipMemcpyDeviceToHost)) != hipSuccess) st = dspb::hip_fail(e, "sizes");
+    (void)hipFree(d_o);
+    if (st) return fail(st);
+    m->params_size = h[0];
+    m->state_size = h[1];
+    m->stateless = (int)h[2];
+    if ((e = hipMalloc(&m->d_params, m->params_size ? m->params_size : 1)) != hipSuccess ||
+        (e = hipMalloc(&m->d_state[0], m->state_size ? m->state_size : 1)) != hipSuccess ||
+        (e = hipMalloc(&m->d_state[1], m->state_size ? m->state_size : 1)) != hipSuccess)
+        return fail(dspb::hip_fail(e, "hipMalloc"));
+    (void)hipMemset(m->d_state[0], 0, m->state_size ? m->state_size : 1);
+    (void)hipMemset(m->d_state[1], 0, m->state_size ? m->state_size : 1);
+    if (prev >= 0 && prev != m->device) (void)hipSetDevice(prev);
+    *out = m;
+    return DSP_OK;
+}
+
+void dsp_module_destroy(dsp_module *m) {
+    if (!m) return;
+    int prev = -1;
+    if (with_device(m->device, &prev) == DSP_OK) {
+        for (int i = 0; i < 2; ++i) {
+            if (m->d_state[i]) (void)hipFree(m->d_state[i]);
+            if (m->d_arena[i]) (void)hipFree(m->d_arena[i]);
+            if (m->arena_mem[i]) (void)hipFree(m->arena_mem[i]);
+        }
+        if (m->d_params) (void)hipFree(m->d_params);
+        if (m->mod) (void)hipModuleUnload(m->mod);
+        if (prev >= 0 && prev != m->device) (void)hipSetDevice(prev);
+    }
+    delete m;
+}
+
+int dsp_module_sizes(const dsp_module *m, uint32_t *params_size, uint32_t *state_size, int *stateless) {
+    if (!m) return DSP_ERR_INVALID;
+    if (params_size) *params_size = m->params_size;
+    if (state_size) *state_size = m->state_size;
+    if (stateless) *stateless = m->stateless;
+    return DSP_OK;
+}
+
+int dsp_module_default_parameters(dsp_module *m, void *params) {
+    if (!m || (!params && m->params_size)) return DSP_ERR_INVALID;
+    std::lock_guard<std::mutex> lk(m->mu);
+    int prev = -1;
+    int st = with_device(m->device, &prev);
+    if (st) return st;
+    void *a_p = m->d_params;
+    void *args[] = {&a_p};
+    if ((st = launch1(m->f_defaults, args))) return st;
+    MOD_HIP(hipMemcpy(params, m->d_params, m->params_size, hipMemcpyDeviceToHost));
+    if (prev >= 0 && prev != m->device) (void)hipSetDevice(prev);
+    return DSP_OK;
+}
+
+int dsp_module_initialize_state(dsp_module *m, const void *params, uint32_t C, float sr, uint64_t arena_bytes) {
+    if (!m) return DSP_ERR_INVALID;
+    if (C == 0 || C > (uint32_t)dspb::kMaxChannels) {
+        set_last_error("channels must be 1..%d", dspb::kMaxChannels);
+        return DSP_ERR_INVALID;
+    }
+    std::lock_guard<std::mutex> lk(m->mu);
+    int prev = -1;
+    int st = with_device(m->device, &prev);
+    if (st) return st;
+    st = init_slot(m, 0, params, C, sr, arena_bytes, nullptr);
+    m->initialized = (st == DSP_OK);
+    if (prev >= 0 && prev != m->device) (void)hipSetDevice(prev);
+    return st;
+}
+
+int dsp_module_read_state(const dsp_module *m, void *state) {
+    if (!m || (!state && m->state_size)) return DSP_ERR_INVALID;
+    MOD_HIP(hipMemcpy(state, m->d_state[0], m->state_size, hipMemcpyDeviceToHost));
+    return DSP_OK;
+}
+
+}  // extern "C"
+
+namespace dspb {
+
+// dsp_render_offline / dsp_render_stft with DSP_PLUGIN_GENERIC (device buffers)
+int module_render(dsp_module *m, const void *params, uint32_t params_size, const float *const *in,
+                  uint32_t in_ch, uint64_t L, float *const *out, uint32_t C, uint32_t B, float sr,
+                  uint64_t goff, hipStream_t s) {
+    if (!m || !m->initialized) {
+        set_last_error("GENERIC plugin: module not loaded / initialize_state not run");
+        return DSP_ERR_INVALID;
+    }
+    if (params_size != m->params_size || (!params && params_size)) {
+        set_last_error("GENERIC plugin: params blob is %u bytes, the plugin's Parameters %u", params_size,
+                       m->params_size);
+        return DSP_ERR_INVALID;
+    }
+    if (C > (uint32_t)kMaxChannels || in_ch > (uint32_t)kMaxChannels) {
+        set_last_error("GENERIC plugin: at most %d channels", kMaxChannels);
+        return DSP_ERR_INVALID;
+    }
+    if (goff % B) {
+        set_last_error("sample_offset must be a multiple of B");
+        return DSP_ERR_INVALID;
+    }
+    if (!m->stateless && goff) {
+        set_last_error("GENERIC plugin with State: whole files only (sample_offset 0)");
+        return DSP_ERR_INVALID;
+    }
+    std::lock_guard<std::mutex> lk(m->mu);
+    if (params_size) MOD_HIP(hipMemcpyAsync(m->d_params, params, params_size, hipMemcpyHostToDevice, s));
+    RenderArgsG A{};
+    A.P = m->d_params;
+    A.S = m->d_state[0];
+    for (uint32_t c = 0; c < in_ch; ++c) A.in[c] = const_cast<float *>(in[c]);
+    for (uint32_t c = 0; c < C; ++c) A.out[c] = out[c];
+    A.L = L;
+    A.nblocks = (L + B - 1) / B;
+    A.block0 = goff / B;
+    A.in_ch = in_ch;
+    A.C = C;
+    A.B = B;
+    A.sr = sr;
+    if (A.nblocks == 0) return DSP_OK;
+    void *args[] = {&A};
+    unsigned grid = 1, block = 1;
+    if (m->stateless) {
+        block = 64;
+        const uint64_t g = (A.nblocks + 63) / 64;
+        grid = (unsigned)(g < 65535 ? g : 65535);
+    }
+    MOD_HIP(hipModuleLaunchKernel(m->f_render, grid, 1, 1, block, 1, 1, 0, s, args, nullptr));
+    MOD_HIP(hipStreamSynchronize(s));  // the params blob is the caller's
+    return DSP_OK;
+}
+
+// dsp_ir_analysis with DSP_PLUGIN_GENERIC: fresh scratch State (compute_IR,
+// plugin.cpp:33-49), then the callback once on the impulse buffers.
+int module_ir(dsp_module *m, const void *params, uint32_t params_size, float *const *bufs, uint32_t C,
+              uint32_t n, float sr, hipStream_t s) {
+    if (!m) return DSP_ERR_INVALID;
+    if (params_size != m->params_size || (!params && params_size)) {
+        set_last_error("GENERIC plugin: params blob is %u bytes, the plugin's Parameters %u", params_size,
+                       m->params_size);
+        return DSP_ERR_INVALID;
+    }
+    std::lock_guard<std::mutex> lk(m->mu);
+    int st = init_slot(m, 1, params, C, sr, 16ull << 20, s);
+    if (st) return st;
+    RenderArgsG A{};
+    A.P = m->d_params;
+    A.S = m->d_state[1];
+    for (uint32_t c = 0; c < C; ++c) A.out[c] = bufs[c];
+    A.C = C;
+    A.B = n;
+    A.sr = sr;
+    void *args[] = {&A};
+    MOD_HIP(hipModuleLaunchKernel(m->f_callback, 1, 1, 1, 1, 1, 1, 0, s, args, nullptr));
+    return DSP_OK;
+}
+
+}  // namespace dspb

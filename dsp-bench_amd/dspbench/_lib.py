@@ -1,4 +1,4 @@
-"""ctypes binding of libdspbench.so (include/dspbench/dspbench.h, host.h, wav.h).
+"""ctypes binding of libdspbench.so (include/dspbench/dspbench.h, host.h, wav.h, module.h).
 
 The library is the product: there is no Python or CPU fallback behind these
 functions.  If the shared object is missing the import fails loudly.
@@ -98,6 +98,16 @@ _SIGS = {
     "dsp_minmax_decimate": (C.c_int, [FP, C.c_uint64, C.c_uint32, FP, FP, C.POINTER(dsp_exec)]),
     "dsp_spectrogram_decimate": (C.c_int, [FP, C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint32, FP,
                                            C.POINTER(dsp_exec)]),
+    "dsp_module_compile": (C.c_int, [C.c_char_p, C.c_char_p, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64),
+                                     C.c_char_p, C.c_uint64]),
+    "dsp_module_free_code": (None, [C.c_void_p]),
+    "dsp_module_load": (C.c_int, [C.c_void_p, C.c_uint64, C.c_int, C.POINTER(C.c_void_p)]),
+    "dsp_module_destroy": (None, [C.c_void_p]),
+    "dsp_module_sizes": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
+                                   C.POINTER(C.c_int)]),
+    "dsp_module_default_parameters": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "dsp_module_initialize_state": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_float, C.c_uint64]),
+    "dsp_module_read_state": (C.c_int, [C.c_void_p, C.c_void_p]),
     "dsp_wav_parse": (C.c_int, [C.c_void_p, C.c_uint64, C.POINTER(dsp_wav_info)]),
     "dsp_wav_decode": (C.c_int, [C.c_void_p, C.POINTER(dsp_wav_info), C.c_uint64, C.c_uint64, FPP,
                                  C.POINTER(dsp_exec)]),

@@ -1,0 +1,232 @@
+/*
+ * plugin_device.h -- plugin_header.h for plugins compiled to gfx950 code
+ * (generic GPU dispatch, include/dspbench/module.h).
+ *
+ * The module compiler (csrc/module.cpp) hands this text to hiprtc under the
+ * name "plugin_header.h", so a stock plugin's `#include "plugin_header.h"`
+ * resolves here and the plugin compiles unchanged.  Everything below sits in
+ * a `#pragma clang force_cuda_host_device` region together with the plugin
+ * source: the services of build/plugin_header.h:27-111 get device
+ * definitions with the host library's semantics (host/host_services.cpp):
+ *
+ *   allocate_*      bump arena in device memory, 16-byte slices, NULL when
+ *                   full (the initialization_context is a dspb_arena*)
+ *   *_64 / *_32     device libm (ocml): not bit-identical to the host libm
+ *   array ops       loops; log2/log10/to_db = ln * constant (dsp.cpp:226-239)
+ *   fft_forward /   in-thread radix-2, split re/im, 1/sqrt(n) both ways
+ *   fft_reverse     (dsp.cpp:74-132), double-precision twiddles
+ *   random_uniform_32_array: no-op, as the reference (dsp.cpp:203-205)
+ */
+#ifndef DSPBENCH_PLUGIN_DEVICE_H
+#define DSPBENCH_PLUGIN_DEVICE_H
+#define DSPBENCH_PLUGIN_HEADER_H /* this file replaces plugin_header.h */
+
+#define INT_PARAM(lo, hi)       __attribute__((annotate("Int " #lo " " #hi))) int
+#define FLOAT_PARAM(lo, hi)     __attribute__((annotate("Float " #lo " " #hi))) float
+#define FLOAT_PARAM_LOG(lo, hi) __attribute__((annotate("Float " #lo " " #hi " " "log"))) float
+#define ENUM_PARAM(enum_type)   __attribute__((annotate("Enum"))) enum_type
+
+typedef float        real32;
+typedef unsigned int u32;
+typedef int          i32;
+
+const float pi            = 3.141593f;
+const float two_pi        = 6.283185f;
+const float half_pi       = 1.570796f;
+const float quarter_pi    = 0.7853982f;
+const float three_half_pi = 4.7123889f;
+const float inv_two_pi    = 0.1591549f;
+
+#pragma clang force_cuda_host_device begin
+
+struct dspb_arena {
+    char *base;
+    unsigned long long capacity;
+    unsigned long long used;
+    float *fft_tmp;  /* fft_reverse's imaginary work buffer (8192 floats), made on first use */
+};
+
+static inline void *dspb_arena_alloc(void *ctx, unsigned long long bytes) {
+    dspb_arena *a = (dspb_arena *)ctx;
+    if (!a) return 0;
+    const unsigned long long n = (bytes + 15ull) & ~15ull;
+    const unsigned long long off = atomicAdd(&a->used, n);
+    if (off + n > a->capacity) return 0;
+    return a->base + off;
+}
+
+static inline float *allocate_buffer(int num_sample, void *ctx) {
+    return num_sample < 0 ? 0 : (float *)dspb_arena_alloc(ctx, 4ull * (unsigned long long)num_sample);
+}
+static inline float **allocate_buffers(int num_samples, int num_channels, void *ctx) {
+    if (num_samples < 0 || num_channels < 0) return 0;
+    float **ch = (float **)dspb_arena_alloc(ctx, sizeof(float *) * (unsigned long long)num_channels);
+    if (!ch) return 0;
+    for (int i = 0; i < num_channels; ++i) {
+        ch[i] = allocate_buffer(num_samples, ctx);
+        if (!ch[i]) return 0;
+    }
+    return ch;
+}
+static inline void *allocate_bytes(int num_bytes, void *ctx) {
+    return num_bytes < 0 ? 0 : dspb_arena_alloc(ctx, (unsigned long long)num_bytes);
+}
+
+static inline double sin_64(double d) { return sin(d); }
+static inline double cos_64(double d) { return cos(d); }
+static inline double tan_64(double d) { return tan(d); }
+static inline double fabs_64(double d) { return fabs(d); }
+static inline double pow_64(double a, double b) { return pow(a, b); }
+static inline double fmod_64(double a, double b) { return fmod(a, b); }
+static inline double ceil_64(double d) { return ceil(d); }
+static inline double floor_64(double d) { return floor(d); }
+static inline double sqrt_64(double d) { return sqrt(d); }
+static inline double exp_64(double d) { return exp(d); }
+static inline double log10_64(double d) { return log10(d); }
+static inline double log_64(double d) { return log(d); }
+static inline double asin_64(double d) { return asin(d); }
+static inline double acos_64(double d) { return acos(d); }
+static inline double atan_64(double d) { return atan(d); }
+static inline double atan2_64(double a, double b) { return atan2(a, b); }
+static inline double sinh_64(double d) { return sinh(d); }
+static inline double cosh_64(double d) { return cosh(d); }
+static inline double tanh_64(double d) { return tanh(d); }
+
+static inline float sin_32(float d) { return sinf(d); }
+static inline float cos_32(float d) { return cosf(d); }
+static inline float tan_32(float d) { return tanf(d); }
+static inline float fabs_32(float d) { return fabsf(d); }
+static inline float pow_32(float a, float b) { return powf(a, b); }
+static inline float fmod_32(float a, float b) { return fmodf(a, b); }
+static inline float ceil_32(float d) { return ceilf(d); }
+static inline float floor_32(float d) { return floorf(d); }
+static inline float sqrt_32(float d) { return sqrtf(d); }
+static inline float exp_32(float d) { return expf(d); }
+static inline float log10_32(float d) { return log10f(d); }
+static inline float log_32(float d) { return logf(d); }
+static inline float asin_32(float d) { return asinf(d); }
+static inline float acos_32(float d) { return acosf(d); }
+static inline float atan_32(float d) { return atanf(d); }
+static inline float atan2_32(float a, float b) { return atan2f(a, b); }
+static inline float sinh_32(float d) { return sinhf(d); }
+static inline float cosh_32(float d) { return coshf(d); }
+static inline float tanh_32(float d) { return tanhf(d); }
+
+#define DSPB_TWO_PI 6.283185307179586476925286766559
+static inline void sin_32_array(real32 *out, real32 ampl, real32 freq, i32 n, real32 *phase) {
+    const double ph = phase ? *phase : 0.0;
+    for (i32 i = 0; i < n; ++i) out[i] = (float)(ampl * cos(DSPB_TWO_PI * freq * i + ph));
+    if (phase) *phase = (float)fmod(ph + DSPB_TWO_PI * freq * n, DSPB_TWO_PI);
+}
+static inline float dspb_triangle_at(double ph, double ampl, double h) {
+    ph = fmod(ph, DSPB_TWO_PI);
+    if (ph < 0) ph += DSPB_TWO_PI;
+    const double fall = DSPB_TWO_PI / 2 + h;
+    if (ph < fall) return (float)(ampl * (1.0 - 2.0 * ph / fall));
+    return (float)(ampl * (-1.0 + 2.0 * (ph - fall) / (DSPB_TWO_PI - fall)));
+}
+static inline void dspb_triangle(real32 *out, real32 ampl, real32 freq, i32 n, double h, real32 *phase) {
+    const double ph = phase ? *phase : 0.0;
+    for (i32 i = 0; i < n; ++i) out[i] = dspb_triangle_at(ph + DSPB_TWO_PI * freq * i, ampl, h);
+    if (phase) *phase = (float)fmod(ph + DSPB_TWO_PI * freq * n, DSPB_TWO_PI);
+}
+static inline void triangle_32_array(real32 *out, real32 ampl, real32 freq, i32 n, real32 *phase) {
+    dspb_triangle(out, ampl, freq, n, 0.0, phase);
+}
+static inline void phasor_32_array(real32 *out, real32 ampl, real32 freq, i32 n, real32 *phase) {
+    if (phase && *phase == 0.0f) *phase += 0.000005f;
+    dspb_triangle(out, ampl, freq, n, -DSPB_TWO_PI / 2 + 0.00000004f, phase);
+}
+static inline void random_uniform_32_array(real32 *out, i32 n, void *rng) { (void)out; (void)n; (void)rng; }
+
+static inline void copy_array(real32 *in, real32 *out, i32 n) {
+    if (out < in) for (i32 i = 0; i < n; ++i) out[i] = in[i];
+    else for (i32 i = n - 1; i >= 0; --i) out[i] = in[i];
+}
+static inline void set_array(real32 v, real32 *out, i32 n) { for (i32 i = 0; i < n; ++i) out[i] = v; }
+static inline void zero_array(real32 *out, i32 n) { for (i32 i = 0; i < n; ++i) out[i] = 0.0f; }
+static inline void add_array(real32 *a, real32 *b, real32 *out, i32 n) { for (i32 i = 0; i < n; ++i) out[i] = a[i] + b[i]; }
+static inline void product_array(real32 *a, real32 *b, real32 *out, i32 n) { for (i32 i = 0; i < n; ++i) out[i] = a[i] * b[i]; }
+
+#define DSPB_INV_LN2 (1.0f / 0.69314718055994530942f)
+#define DSPB_INV_LN10 (1.0f / 2.30258509299404568402f)
+#define DSPB_DB_PER_LN (20.0f / 2.30258509299404568402f)
+#define DSPB_LN_PER_DB (2.30258509299404568402f / 20.0f)
+static inline void gain_32_array(real32 *in, real32 *out, real32 g, i32 n) { for (i32 i = 0; i < n; ++i) out[i] = in[i] * g; }
+static inline void dc_offset_32_array(real32 *in, real32 *out, real32 o, i32 n) { for (i32 i = 0; i < n; ++i) out[i] = in[i] + o; }
+static inline void sqrt_32_array(real32 *in, real32 *out, i32 n) { for (i32 i = 0; i < n; ++i) out[i] = sqrtf(in[i]); }
+static inline void abs_32_array(real32 *in, real32 *out, i32 n) { for (i32 i = 0; i < n; ++i) out[i] = fabsf(in[i]); }
+static inline void ln_32_array(real32 *in, real32 *out, i32 n) { for (i32 i = 0; i < n; ++i) out[i] = logf(in[i]); }
+static inline void log2_32_array(real32 *in, real32 *out, i32 n) { for (i32 i = 0; i < n; ++i) out[i] = logf(in[i]) * DSPB_INV_LN2; }
+static inline void log10_32_array(real32 *in, real32 *out, i32 n) { for (i32 i = 0; i < n; ++i) out[i] = logf(in[i]) * DSPB_INV_LN10; }
+static inline void to_db_32_array(real32 *in, real32 *out, i32 n) { for (i32 i = 0; i < n; ++i) out[i] = logf(in[i]) * DSPB_DB_PER_LN; }
+static inline void from_db_32_array(real32 *in, real32 *out, i32 n) { for (i32 i = 0; i < n; ++i) out[i] = expf(in[i] * DSPB_LN_PER_DB); }
+static inline void gain_ip_32_array(real32 *io, real32 g, i32 n) { gain_32_array(io, io, g, n); }
+static inline void dc_offset_ip_32_array(real32 *io, real32 o, i32 n) { dc_offset_32_array(io, io, o, n); }
+static inline void sqrt_ip_32_array(real32 *io, i32 n) { sqrt_32_array(io, io, n); }
+static inline void abs_ip_32_array(real32 *io, i32 n) { abs_32_array(io, io, n); }
+static inline void ln_ip_32_array(real32 *io, i32 n) { ln_32_array(io, io, n); }
+static inline void log2_ip_32_array(real32 *io, i32 n) { log2_32_array(io, io, n); }
+static inline void log10_ip_32_array(real32 *io, i32 n) { log10_32_array(io, io, n); }
+static inline void pythagore_array(real32 *x, real32 *y, real32 *out, i32 n) {
+    for (i32 i = 0; i < n; ++i) out[i] = sqrtf(x[i] * x[i] + y[i] * y[i]);
+}
+
+static inline void *fft_initialize(void *ctx) { return ctx; }
+static inline void windowing_hamming(real32 *in, real32 *out, i32 n) {
+    if (n <= 0) return;
+    if (n == 1) { out[0] = in[0]; return; }
+    for (i32 i = 0; i < n; ++i) out[i] = in[i] * (float)(0.54 - 0.46 * cos(DSPB_TWO_PI * (double)i / (double)(n - 1)));
+}
+/* in-place radix-2 on (re, im), sign -1 forward / +1 inverse, scaled 1/sqrt(n) */
+static inline void dspb_fft_inplace(real32 *re, real32 *im, i32 n, int sign) {
+    for (i32 i = 1, j = 0; i < n; ++i) {  /* bit reversal */
+        i32 bit = n >> 1;
+        for (; j & bit; bit >>= 1) j ^= bit;
+        j ^= bit;
+        if (i < j) {
+            float t = re[i]; re[i] = re[j]; re[j] = t;
+            t = im[i]; im[i] = im[j]; im[j] = t;
+        }
+    }
+    for (i32 len = 2; len <= n; len <<= 1) {
+        const i32 h = len >> 1;
+        for (i32 k = 0; k < h; ++k) {
+            const double a = sign * DSPB_TWO_PI * (double)k / (double)len;
+            const float wr = (float)cos(a), wi = (float)sin(a);
+            for (i32 s = 0; s < n; s += len) {
+                const float xr = re[s + k + h] * wr - im[s + k + h] * wi;
+                const float xi = re[s + k + h] * wi + im[s + k + h] * wr;
+                re[s + k + h] = re[s + k] - xr;
+                im[s + k + h] = im[s + k] - xi;
+                re[s + k] += xr;
+                im[s + k] += xi;
+            }
+        }
+    }
+    const float sc = (float)(1.0 / sqrt((double)n));
+    for (i32 i = 0; i < n; ++i) { re[i] *= sc; im[i] *= sc; }
+}
+static inline int dspb_pow2_ok(i32 n) { return n > 0 && (n & (n - 1)) == 0 && n <= 8192; }
+static inline void fft_forward(real32 *in, real32 *re, real32 *im, i32 n, void *ctx) {
+    (void)ctx;
+    if (!dspb_pow2_ok(n)) return;  /* the reference aborts (dsp.cpp:79,86) */
+    for (i32 i = 0; i < n; ++i) { re[i] = in[i]; im[i] = 0.0f; }
+    dspb_fft_inplace(re, im, n, -1);
+}
+static inline void fft_reverse(real32 *re_in, real32 *im_in, real32 *out, i32 n, void *ctx) {
+    /* out = Re(IDFT(re + i im)) / sqrt(n); the imaginary part goes to a work
+       buffer of the context, as the reference's IPP temp (dsp.cpp:106-132):
+       like it, one context is not for concurrent callers */
+    if (!dspb_pow2_ok(n) || !ctx) return;
+    dspb_arena *a = (dspb_arena *)ctx;
+    if (!a->fft_tmp) a->fft_tmp = (float *)dspb_arena_alloc(ctx, 4ull * 8192ull);
+    real32 *tmp = a->fft_tmp;
+    if (!tmp) return;
+    for (i32 i = 0; i < n; ++i) { out[i] = re_in[i]; tmp[i] = im_in[i]; }
+    dspb_fft_inplace(out, tmp, n, +1);
+}
+
+#pragma clang force_cuda_host_device end
+
+#endif /* DSPBENCH_PLUGIN_DEVICE_H */

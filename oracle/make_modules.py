@@ -1,0 +1,41 @@
+#!/usr/bin/env python3
+"""make_modules.py -- TEST INFRASTRUCTURE ONLY.
+
+Compiles the reference's stock plugins, from their sources where they lie
+under /root/reference, with the PRODUCT's plugin compiler
+(dsp_module_compile, hiprtc -> gfx950) into oracle/_ref/mod_<name>.co, so
+the GPU tests can load and run the reference's own plugins on a box that
+has no /root/reference.  Outputs go only to oracle/_ref/ (git-ignored).
+
+Usage: python oracle/make_modules.py [REF_DIR]
+"""
+import ctypes as C
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(os.path.dirname(HERE), "dsp-bench_amd"))
+
+PLUGINS = ["build/gain_test", "build/IR_test", "build/sine_test", "build/buffer_test",
+           "build/handmade_test", "build/template_plugin", "test/static_gain_plugin", "test/no_op",
+           "test/plugin_with_parameters"]
+
+
+def main():
+    ref = sys.argv[1] if len(sys.argv) > 1 else "/root/reference"
+    import dspbench.module as m
+    out = os.path.join(HERE, "_ref")
+    os.makedirs(out, exist_ok=True)
+    for p in PLUGINS:
+        src = os.path.join(ref, p + ".cpp")
+        dst = os.path.join(out, f"mod_{os.path.basename(p)}.co")
+        if os.path.exists(dst) and os.path.getmtime(dst) >= os.path.getmtime(src):
+            continue
+        code = m.compile_source(open(src).read(), os.path.basename(p))
+        with open(dst, "wb") as f:
+            f.write(code)
+        print(f"make_modules: {dst} ({len(code)} bytes)")
+
+
+if __name__ == "__main__":
+    main()
