@@ -16,7 +16,10 @@ import dspbench as d
 from dspbench import _lib
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADERS = sorted(glob.glob(os.path.join(REPO, "include", "dspbench", "*.h")))
+# plugin_device.h defines the services inline for GPU-compiled plugins (it is
+# handed to hiprtc as text, module.h): it declares nothing the library exports
+HEADERS = sorted(h for h in glob.glob(os.path.join(REPO, "include", "dspbench", "*.h"))
+                 if not h.endswith("plugin_device.h"))
 
 
 def declared_functions(path):
