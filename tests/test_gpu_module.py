@@ -27,6 +27,7 @@ PLUGIN_DIR = os.path.join(os.path.dirname(HERE), "dsp-bench_amd", "plugins")
 EXACT = ["gain_test", "IR_test", "handmade_test", "static_gain_plugin", "no_op", "plugin_with_parameters",
          "template_plugin"]
 TOL = {"sine_test": 1e-6, "buffer_test": 1e-6}
+EMPTY_PARAMS = {"static_gain_plugin", "no_op", "template_plugin"}
 
 
 def have(name):
@@ -59,7 +60,8 @@ def test_reference_plugin_descriptor_and_defaults(torch_cuda, oracle, name):
     ref = oracle.RefPlugin(name, 2, 48000.0)
     assert mod.params_size == ref.lib.ref_sizeof_parameters()
     assert mod.state_size == ref.lib.ref_sizeof_state()
-    assert mod.default_parameters() == bytes(ref.params[:mod.params_size])
+    if name not in EMPTY_PARAMS:  # an empty struct's one byte is padding on both sides
+        assert mod.default_parameters() == bytes(ref.params[:mod.params_size])
 
 
 @pytest.mark.gpu
