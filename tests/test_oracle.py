@@ -196,3 +196,16 @@ def test_fft_roundtrip_and_scaling(oracle):
 def test_frame_count(oracle, L, N, H):
     assert oracle.stft_frames(L, N, H) == oracle.lib().oracle_stft_frames(L, N, H)
     assert oracle.stft_frames(L, N, H) == (0 if L < N else (L - N) // H + 1)
+
+
+@needs_ref
+@pytest.mark.parametrize("name", ["gain_test", "IR_test", "sine_test", "buffer_test", "handmade_test",
+                                  "template_plugin", "static_gain_plugin", "no_op", "plugin_with_parameters"])
+def test_reference_plugins_load_beside_the_product(oracle, name):
+    """The reference plugins bind their services to oracle/ref_services.c
+    even with libdspbench.so (same symbol names) loaded globally first."""
+    import dspbench
+    dspbench.lib()
+    r = oracle.RefPlugin(name, 2, 48000.0)
+    out = oracle.callback_once(r.as_oracle(), np.zeros((2, 64), np.float32), 48000.0)
+    assert np.all(np.isfinite(out))
