@@ -56,10 +56,11 @@ def parse():
                     help="8192-pt kernel (dsp_stft_kernel_variant): 2 = wave/frame scalar SoA, "
                          "5 = wave/frame packed even/odd pairs")
     ap.add_argument("--workload", default="headline",
-                    choices=["headline", "stft96k", "gain10min", "fir1024", "wav16", "wav24"],
+                    choices=["headline", "stft96k", "ch96k", "gain10min", "fir1024", "wav16", "wav24"],
                     help="headline = IR_test + STFT 48 kHz (the metric); stft96k = BASELINE cfg 4 "
                          "(STFT of 1 h stereo 96 kHz from HBM); gain10min = cfg 2 render; "
-                         "wav16 / wav24 = GPU decode of a 1 h stereo int16 / int24 WAV payload")
+                         "wav16 / wav24 = GPU decode of a 1 h stereo int16 / int24 WAV payload; "
+                         "ch96k = BASELINE cfg 5: one 96 kHz channel per GPU through IR_test + STFT")
     return ap.parse_args()
 
 
@@ -122,25 +123,30 @@ def main():
     d.lib().dsp_stft_kernel_variant(args.stft_variant)
 
     wl = args.workload
-    sr = 96_000 if wl == "stft96k" else SR
+    sr = 96_000 if wl in ("stft96k", "ch96k") else SR
+    # cfg 5 shards by channel (one 96 kHz channel per GPU), the rest by time
+    CH = 1 if wl == "ch96k" else globals()["CH"]
     minutes = args.minutes if wl not in ("gain10min", "fir1024") or args.minutes != 60.0 else 10.0
     L = int(round(minutes * 60 * sr))
     L -= L % HOP  # whole hops per rank (HOP is a multiple of B)
     # the file is world * L samples long; rank r owns [r L, (r+1) L) and
     # reads a halo of the next rank's first N - H samples (dspbench/shard.py)
-    sh = d.shard.plan(world * L, world, rank, B, N_FFT if wl in ("headline", "stft96k") else HOP, HOP,
-                      render=(wl == "headline"))
+    if wl == "ch96k":  # the whole file of this rank's own channel
+        sh = d.shard.plan(L, 1, 0, B, N_FFT, HOP, render=True)
+    else:
+        sh = d.shard.plan(world * L, world, rank, B, N_FFT if wl in ("headline", "stft96k") else HOP, HOP,
+                          render=(wl == "headline"))
     assert sh.owned == L, (sh, L)
     L_in = sh.read_len
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     x = (torch.rand((CH, L_in), device=dev, generator=g) * 2 - 1) * 0.1  # synthetic WAV
     nb = d.num_blocks(L_in, B)
-    F = d.stft_frames(nb * B if wl == "headline" else L_in, N_FFT, HOP)
-    out = torch.empty((CH, nb * B), device=dev) if wl in ("headline", "gain10min", "fir1024") else None
+    F = d.stft_frames(nb * B if wl in ("headline", "ch96k") else L_in, N_FFT, HOP)
+    out = torch.empty((CH, nb * B), device=dev) if wl in ("headline", "ch96k", "gain10min", "fir1024") else None
     # rows: the last rank owns one frame less (no halo); equal-sized rows keep
     # the optional gather a plain dist.gather
-    mag = torch.empty((CH, max(F, L // HOP), K_BINS), device=dev) if wl in ("headline", "stft96k") else None
-    plugin = d.Plugin.ir_test(0.9, 0.002) if wl == "headline" else d.Plugin.gain_test(0.2)
+    mag = torch.empty((CH, max(F, L // HOP), K_BINS), device=dev) if wl in ("headline", "stft96k", "ch96k") else None
+    plugin = d.Plugin.ir_test(0.9, 0.002) if wl in ("headline", "ch96k") else d.Plugin.gain_test(0.2)
     stream = torch.cuda.current_stream(dev)
     soff = sh.start
 
@@ -153,6 +159,13 @@ def main():
                           K=K_BINS, out=out, mag=mag, sample_offset=soff)
         workload = ("IR_test render (B=512) + 8192-pt Hann STFT, hop 4096, 4097 bins, "
                     f"{minutes:g} min of 48 kHz stereo per GPU")
+        kname = f"{KERNELS[args.stft_variant]}<render> (fused render + window + FFT + |X|)"
+    elif wl == "ch96k":
+        def step():
+            d.render_stft(x, CH, B, float(sr), plugin, N=N_FFT, H=HOP, window=d.DSP_WIN_HANN,
+                          K=K_BINS, out=out, mag=mag)
+        workload = ("BASELINE cfg 5: IR_test render (B=512) + 8192-pt Hann STFT of one 96 kHz channel "
+                    f"({minutes:g} min) per GPU; channels sharded one per GPU")
         kname = f"{KERNELS[args.stft_variant]}<render> (fused render + window + FFT + |X|)"
     elif wl == "stft96k":
         def step():
@@ -245,7 +258,7 @@ def main():
             bufs = [torch.empty_like(owned) for _ in range(world)] if rank == 0 else None
             dist.gather(owned, bufs, dst=0)
         if mag is not None:
-            fm = mag[:, : L // HOP].contiguous()
+            fm = mag[:, : (F if wl == "ch96k" else L // HOP)].contiguous()
             mbufs = [torch.empty_like(fm) for _ in range(world)] if rank == 0 else None
             dist.gather(fm, mbufs, dst=0)
         torch.cuda.synchronize()
@@ -279,7 +292,8 @@ def main():
                 "plugin": plugin.name,
                 "samples_per_gpu": samples_per_rank,
                 "frames_per_gpu": CH * F if mag is not None else 0,
-                "sharding": "time-chunk per GPU, 4096-sample halo, no data-path collective",
+                "sharding": ("one channel per GPU, no data-path collective" if wl == "ch96k" else
+                             "time-chunk per GPU, 4096-sample halo, no data-path collective"),
                 "gather_ms": None if gather_ms is None else round(gather_ms, 3),
             },
             "roofline": ({
