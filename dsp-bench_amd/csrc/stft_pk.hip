@@ -114,6 +114,58 @@ __global__ __launch_bounds__(256, 2) void stft8192_pk_kernel(Stft8kArgs A) {
     float4 wbase = float4{0.f, 0.f, 0.f, 0.f};
     if constexpr (WINC) wbase = A.wbase[lane];
 
+    cx2 P[32];
+    // SoA frame path (computed window, and a periodic ramp table or a full
+    // frame in memory): the frame is loaded straight into even/odd pairs --
+    // X[j] = ((x_e(2j), x_e(2j+1)), (x_o(2j), x_o(2j+1))), x_e(b) = sample
+    // 2 lane + 128 b, x_o(b) the next one -- so the window is two v_pk_mul
+    // per pair with no register shuffles.
+    constexpr bool SOA = WINC && ((MK == MapKind::Ramp && PER > 0) || SRC == kSrcMemory);
+    if constexpr (SOA) {
+        constexpr int NJ = (SRC == kSrcMemory) ? 32 : (PER >= 2 ? PER / 2 : 1);
+        cx2 X[NJ];
+        if constexpr (SRC == kSrcMemory) {
+            // the odd samples through an opaque +1: otherwise the load/store
+            // optimiser fuses x_e, x_o into one dwordx2 (AoS) and the pairs
+            // come back only through v_mov shuffles
+            uint32_t one = 1u;
+            asm volatile("" : "+s"(one));
+            const float *xb = x + fs + 2u * lane, *xo = xb + one;
+#pragma unroll
+            for (int jj = 0; jj < NJ; ++jj)
+                X[jj] = cx2{v2f{xb[256u * jj], xb[256u * jj + 128u]}, v2f{xo[256u * jj], xo[256u * jj + 128u]}};
+        } else {
+            const uint32_t p0 = (uint32_t)(A.goff + fs) + 2u * lane;
+            const float *T = A.map.table;
+#pragma unroll
+            for (int jj = 0; jj < NJ; ++jj) {
+                const uint32_t q0 = (p0 + 256u * jj) & A.map.b_mask;
+                const uint32_t q1 = (p0 + 256u * jj + (PER >= 2 ? 128u : 0u)) & A.map.b_mask;
+                X[jj] = cx2{v2f{T[q0], T[q1]}, v2f{T[q0 + 1], T[q1 + 1]}};
+            }
+            // the render output: sample pairs of column b repeat with period PER
+            float *o = A.out.p[ch] + fs;
+            v2f st[PER >= 2 ? PER : 1];
+#pragma unroll
+            for (int b = 0; b < (PER >= 2 ? PER : 1); ++b)
+                st[b] = v2f{X[b / 2].r[b & 1], X[b / 2].i[b & 1]};
+#pragma unroll
+            for (int b = 0; b < 64; ++b)
+                if (128u * (uint32_t)b < A.H)
+                    reinterpret_cast<v2f *>(o + 128u * (uint32_t)b)[lane] = st[b % (PER >= 2 ? PER : 1)];
+        }
+        // w(n) = wa - wb cos(theta n) = wa - u C_b + v S_b per parity, with
+        // u = wb cos(theta n0), v = wb sin(theta n0) of the lane's base angle
+        const float ue = A.wb * wbase.x, ve = A.wb * wbase.y, uo = A.wb * wbase.z, vo = A.wb * wbase.w;
+#pragma unroll
+        for (int j = 0; j < 32; ++j) {
+            const v2f C = v2f{kWinB_c[2 * j], kWinB_c[2 * j + 1]}, S = v2f{kWinB_s[2 * j], kWinB_s[2 * j + 1]};
+            const v2f we = (v2f{ve, ve} * S + v2f{A.wa, A.wa}) - v2f{ue, ue} * C;
+            const v2f wo = (v2f{vo, vo} * S + v2f{A.wa, A.wa}) - v2f{uo, uo} * C;
+            const cx2 xj = X[j % NJ];
+            P[j] = cx2{xj.r * we, xj.i * wo};
+        }
+    } else {
     // ---- 1. frame (+ fused render) -----------------------------------------
     cx v[64];
     if constexpr (SRC == kSrcMemory) {
@@ -133,16 +185,7 @@ __global__ __launch_bounds__(256, 2) void stft8192_pk_kernel(Stft8kArgs A) {
             }
         }
     } else {
-        if constexpr (MK == MapKind::Ramp && PER > 0) {
-            const uint32_t p0 = (uint32_t)(A.goff + fs) + 2u * lane;
-#pragma unroll
-            for (int b = 0; b < PER; ++b) {
-                const v2f t = *reinterpret_cast<const v2f *>(A.map.table + ((p0 + 128u * (uint32_t)b) & A.map.b_mask));
-                v[b] = cx{t.x, t.y};
-            }
-#pragma unroll
-            for (int b = PER; b < 64; ++b) v[b] = v[b % PER];
-        } else if constexpr (MK == MapKind::Ramp && POW2) {
+        if constexpr (MK == MapKind::Ramp && POW2) {
             if (A.map.B >= 4u && A.map.B <= 4096u) lds_table_frame(A, lds, fs, lane, v);
             else s_render_frame<MK, POW2>(A, x, fs, lane, v);
         } else {
@@ -156,7 +199,6 @@ __global__ __launch_bounds__(256, 2) void stft8192_pk_kernel(Stft8kArgs A) {
     }
 
     // ---- 2. window (pre-scaled by 0.5/sqrt N), packed into even/odd pairs ---
-    cx2 P[32];
     {
         const v2f bc = v2f{wbase.x, wbase.z}, bs = v2f{wbase.y, wbase.w};
 #pragma unroll
@@ -177,6 +219,7 @@ __global__ __launch_bounds__(256, 2) void stft8192_pk_kernel(Stft8kArgs A) {
                        v2f{v[2 * j].i * w[0].y, v[2 * j + 1].i * w[1].y}};
         }
     }
+    }  // !SOA
 
     // ---- 3. DFT64 over b: even/odd DFT32 in the halves, then combine --------
     x2dft32<!(OPT & kPkNoBarDft)>(P);
