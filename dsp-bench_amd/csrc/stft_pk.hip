@@ -120,21 +120,14 @@ __global__ __launch_bounds__(256, 2) void stft8192_pk_kernel(Stft8kArgs A) {
     // X[j] = ((x_e(2j), x_e(2j+1)), (x_o(2j), x_o(2j+1))), x_e(b) = sample
     // 2 lane + 128 b, x_o(b) the next one -- so the window is two v_pk_mul
     // per pair with no register shuffles.
-    constexpr bool SOA = WINC && ((MK == MapKind::Ramp && PER > 0) || SRC == kSrcMemory);
+    // (for a frame in memory the 128 dword loads this needs cost more than
+    // the shuffles they save: 0.75 vs 0.65 ms per stereo hour, so memory
+    // frames keep the dwordx2 path below)
+    constexpr bool SOA = WINC && MK == MapKind::Ramp && PER > 0 && SRC == kSrcRender;
     if constexpr (SOA) {
-        constexpr int NJ = (SRC == kSrcMemory) ? 32 : (PER >= 2 ? PER / 2 : 1);
+        constexpr int NJ = PER >= 2 ? PER / 2 : 1;
         cx2 X[NJ];
-        if constexpr (SRC == kSrcMemory) {
-            // the odd samples through an opaque +1: otherwise the load/store
-            // optimiser fuses x_e, x_o into one dwordx2 (AoS) and the pairs
-            // come back only through v_mov shuffles
-            uint32_t one = 1u;
-            asm volatile("" : "+s"(one));
-            const float *xb = x + fs + 2u * lane, *xo = xb + one;
-#pragma unroll
-            for (int jj = 0; jj < NJ; ++jj)
-                X[jj] = cx2{v2f{xb[256u * jj], xb[256u * jj + 128u]}, v2f{xo[256u * jj], xo[256u * jj + 128u]}};
-        } else {
+        {
             const uint32_t p0 = (uint32_t)(A.goff + fs) + 2u * lane;
             const float *T = A.map.table;
 #pragma unroll
@@ -200,7 +193,8 @@ __global__ __launch_bounds__(256, 2) void stft8192_pk_kernel(Stft8kArgs A) {
 
     // ---- 2. window (pre-scaled by 0.5/sqrt N), packed into even/odd pairs ---
     {
-        const v2f bc = v2f{wbase.x, wbase.z}, bs = v2f{wbase.y, wbase.w};
+        // w(n) = wa - wb cos(theta n) = wa - u C_b + v S_b, n = 2 lane + {0, 1} + 128 b
+        const v2f uu = v2f{A.wb * wbase.x, A.wb * wbase.z}, vv = v2f{A.wb * wbase.y, A.wb * wbase.w};
 #pragma unroll
         for (int j = 0; j < 32; ++j) {
             v2f w[2];
@@ -208,9 +202,7 @@ __global__ __launch_bounds__(256, 2) void stft8192_pk_kernel(Stft8kArgs A) {
             for (int h = 0; h < 2; ++h) {
                 const int b = 2 * j + h;
                 if constexpr (WINC) {
-                    // w(n) = wa - wb cos(theta n), n = 2 lane + {0, 1} + 128 b
-                    const v2f t = bc * kWinB_c[b] - bs * kWinB_s[b];
-                    w[h] = A.wa - A.wb * t;
+                    w[h] = (vv * kWinB_s[b] + v2f{A.wa, A.wa}) - uu * kWinB_c[b];
                 } else {
                     w[h] = (A.win2 + 64u * (uint32_t)b)[lane];
                 }
