@@ -31,7 +31,7 @@ if [[ $mode == tests || $mode == all ]]; then
     run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 fi
 if [[ $mode == bench || $mode == all || $mode == prof ]]; then
-    run bench 600 python bench.py --steps 20 --warmup 5
+    run bench 600 python bench.py
 fi
 if [[ $mode == prof || $mode == all ]]; then
     run rocprof_stats 600 rocprofv3 --kernel-trace --stats -d $out/prof_$tag -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline
