@@ -246,6 +246,50 @@ static bool aligned(const void *p, size_t a) { return ((uintptr_t)p % a) == 0; }
 // ---------------------------------------------------------------------------
 // plugin -> sample map
 // ---------------------------------------------------------------------------
+// FFT(taps zero-padded to 8192) / 16384 in double, laid out for
+// fir_fft.hip: for ka < 16 and lane l, 8 floats
+//   (Re H[k1], Re H[k2], Im H[k1], Im H[k2], Re H[M-k1], Re H[M-k2], Im H[M-k1], Im H[M-k2])
+// with k1 = l + 64 ka, k2 = k1 + 1024, M = 4096; then H[2048] (re, im).
+static void ols_table(const float *taps, uint32_t T, float *out) {
+    const int n = 8192;
+    std::vector<double> re(n, 0.0), im(n, 0.0);
+    for (uint32_t i = 0; i < T; ++i) re[i] = taps[i];
+    for (int i = 1, j = 0; i < n; ++i) {  // iterative radix-2, forward (e^-i)
+        int bit = n >> 1;
+        for (; j & bit; bit >>= 1) j ^= bit;
+        j ^= bit;
+        if (i < j) { std::swap(re[i], re[j]); std::swap(im[i], im[j]); }
+    }
+    for (int len = 2; len <= n; len <<= 1) {
+        const int hlen = len >> 1;
+        for (int k = 0; k < hlen; ++k) {
+            const double a = -2.0 * M_PI * k / len, wr = std::cos(a), wi = std::sin(a);
+            for (int s0 = 0; s0 < n; s0 += len) {
+                const double xr = re[s0 + k + hlen] * wr - im[s0 + k + hlen] * wi;
+                const double xi = re[s0 + k + hlen] * wi + im[s0 + k + hlen] * wr;
+                re[s0 + k + hlen] = re[s0 + k] - xr;
+                im[s0 + k + hlen] = im[s0 + k] - xi;
+                re[s0 + k] += xr;
+                im[s0 + k] += xi;
+            }
+        }
+    }
+    const double sc = 1.0 / 16384.0;
+    for (int ka = 0; ka < 16; ++ka)
+        for (int l = 0; l < 64; ++l) {
+            const int k1 = l + 64 * ka, k2 = k1 + 1024, m1 = 4096 - k1, m2 = 4096 - k2;
+            float *o = out + 8 * (64 * ka + l);
+            o[0] = (float)(re[k1] * sc); o[1] = (float)(re[k2] * sc);
+            o[2] = (float)(im[k1] * sc); o[3] = (float)(im[k2] * sc);
+            o[4] = (float)(re[m1] * sc); o[5] = (float)(re[m2] * sc);
+            o[6] = (float)(im[m1] * sc); o[7] = (float)(im[m2] * sc);
+        }
+    out[8192] = (float)(re[2048] * sc);
+    out[8193] = (float)(im[2048] * sc);
+}
+
+static int g_fir_method = 0;  // 0 auto (overlap-save when T <= 1025), 1 direct, 2 overlap-save
+
 static int plugin_map(const dsp_plugin *p, uint32_t B, int dev, hipStream_t s, SampleMap *m,
                       float sr = 48000.f) {
     m->kind = MapKind::Noop;
@@ -294,16 +338,22 @@ static int plugin_map(const dsp_plugin *p, uint32_t B, int dev, hipStream_t s, S
         if (!p->params || T == 0 || p->params_size % 4 || T > 2048)
             return invalid("FIR plugin needs 1..2048 float taps as its params blob");
         const uint32_t T8 = (T + 15) & ~15u;  // zero-padded to 16 (fir.hip)
-        std::vector<float> h(T8, 0.f);
+        // scratch: [taps, T8 floats][overlap-save H table, 8192 + 2 floats]
+        std::vector<float> h(T8 + 8192 + 2, 0.f);
         std::memcpy(h.data(), p->params, 4 * (size_t)T);
+        if (T <= 1025) ols_table(h.data(), T, h.data() + T8);
         float *taps = nullptr;
-        int st = get_scratch(dev, s, sizeof(float) * T8, &taps);
+        int st = get_scratch(dev, s, sizeof(float) * h.size(), &taps);
         if (st) return st;
-        DSPB_HIP(hipMemcpyAsync(taps, h.data(), sizeof(float) * T8, hipMemcpyHostToDevice, s));
-        DSPB_HIP(hipStreamSynchronize(s));  // h is a stack buffer
+        DSPB_HIP(hipMemcpyAsync(taps, h.data(), sizeof(float) * h.size(), hipMemcpyHostToDevice, s));
+        DSPB_HIP(hipStreamSynchronize(s));  // h is a host buffer on this frame
         m->kind = MapKind::Fir;
         m->taps = taps;
         m->ntaps8 = T8;
+        m->ntaps = T;
+        m->olsH = taps + T8;
+        m->olsH2048[0] = h[T8 + 8192];
+        m->olsH2048[1] = h[T8 + 8193];
         return DSP_OK;
     }
     case DSP_PLUGIN_GENERIC:  // the plugin's own audio_callback, compiled for gfx950 (module.h)
@@ -362,6 +412,32 @@ static int render_device(const float *const *in, uint32_t in_ch, uint64_t L, flo
     }
     if (map.kind == MapKind::Fir) {  // convolution from the start of the file
         if (start != 0 || goff != 0) return invalid("FIR render: whole files only (sample_offset 0)");
+        if (map.ntaps <= 1025 && g_fir_method != 1) {  // overlap-save, 8192-point frames
+            const v2f *tw = nullptr;
+            int dev = 0;
+            DSPB_HIP(hipGetDevice(&dev));
+            int st = get_tw(dev, &tw);
+            if (st) return st;
+            for (uint32_t c0 = 0; c0 < C; c0 += kMaxChannels) {
+                const uint32_t cn = (C - c0) < (uint32_t)kMaxChannels ? (C - c0) : kMaxChannels;
+                FirFftArgs A{};
+                for (uint32_t j = 0; j < cn; ++j) {
+                    A.out.p[j] = out[c0 + j];
+                    if (c0 + j < in_ch) {
+                        A.in.p[j] = in[c0 + j];
+                        A.in_ch = j + 1;
+                    }
+                }
+                A.L = L;
+                A.Ly = end;
+                A.F = (end + 7167) / 7168;
+                A.H = map.olsH;
+                A.h2048 = v2f{map.olsH2048[0], map.olsH2048[1]};
+                A.tw = tw;
+                if ((st = launch_fir_fft(A, cn, s))) return st;
+            }
+            return DSP_OK;
+        }
         for (uint32_t c = 0; c < C; ++c) {
             int st = launch_fir(c < in_ch ? in[c] : nullptr, L, out[c], end, map.taps, map.ntaps8,
                                 aligned(out[c], 16), s);
@@ -474,6 +550,12 @@ using namespace dspb;
 extern "C" {
 
 int dsp_abi_version(void) { return DSPBENCH_ABI_VERSION; }
+
+int dsp_fir_method(int m) {
+    const int old = g_fir_method;
+    if (m >= 0 && m <= 2) g_fir_method = m;
+    return old;
+}
 
 int dsp_stft_soa_options(int opt) {
     std::lock_guard<std::mutex> lk(g_mu);

@@ -31,6 +31,9 @@ struct SampleMap {
     uint32_t b_mask;     // B - 1 when B is a power of two, else 0
     const float *taps;   // FIR taps, zero-padded to ntaps8 = ceil(T/16)*16 (Fir; not a per-sample map)
     uint32_t ntaps8;
+    uint32_t ntaps;      // Fir: real tap count (<= 1025 runs overlap-save)
+    const float *olsH;   // Fir: FFT(taps)/16384 in fir_fft.hip's lane-major pair layout
+    float olsH2048[2];   // Fir: H[2048]/16384
     void *module;        // Generic: the dsp_module running the plugin's own audio_callback
     const void *gparams; // Generic: host Parameters blob
     uint32_t gparams_size;

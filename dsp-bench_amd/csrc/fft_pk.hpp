@@ -1,0 +1,150 @@
+// fft_pk.hpp -- packed (two independent sub-transforms per VGPR pair)
+// 4096-point complex FFT for one wavefront, forward or inverse, as used by
+// the 8192-point real STFT (stft_pk.hip) and the overlap-save FIR
+// (fir_fft.hip).  See stft_pk.hip for the derivation of the layout.
+#pragma once
+#include "fft_soa.hpp"
+#include "fft_x2.hpp"
+
+namespace dspb {
+
+// both halves: a * w
+__device__ __forceinline__ cx2 cmul2(cx2 a, cx2 w) {
+    return cx2{a.r * w.r - a.i * w.i, a.r * w.i + a.i * w.r};
+}
+// (c + i s) broadcast times both halves of w
+__device__ __forceinline__ cx2 cmulb(cx c, cx2 w) {
+    return cx2{c.r * w.r - c.i * w.i, c.r * w.i + c.i * w.r};
+}
+
+// radix-2 DIT combine of a transformed pair: halves (E[k], O[k]) at
+// a[perm32(k)] -> (Y[k], Y[k+32]) as scalars
+__device__ __forceinline__ void combine64(const cx2 (&a)[32], cx (&yp)[32], cx (&ym)[32]) {
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+        const cx2 p = a[perm32(k)];
+        const cx e = cx{p.r.x, p.i.x};
+        const cx t = stw64(cx{p.r.y, p.i.y}, k);
+        yp[k] = e + t;
+        ym[k] = e - t;
+    }
+}
+
+// the same combine, packed: y[k] = (Y[k], Y[k+32]) as one cx2.  The odd
+// half is twiddled in place (the even half rides along times 1), then each
+// butterfly is one v_pk_fma: (e, e) + (t, t) * (1, -1).
+template <int K>
+__device__ __forceinline__ cx2 combine1(cx2 p) {
+    const v2f pm = v2f{1.f, -1.f};
+    v2f tr, ti;  // (t, t) where t = O W64^K, as splats of one register half
+    if constexpr (K == 0) {
+        tr = v2f{p.r.y, p.r.y};
+        ti = v2f{p.i.y, p.i.y};
+    } else if constexpr (K == 16) {  // t = -i O = (O.i, -O.r)
+        tr = v2f{p.i.y, p.i.y};
+        ti = -v2f{p.r.y, p.r.y};
+    } else {
+        const v2f w = v2f{1.f, kW64_re[K]}, s = v2f{0.f, kW64_im[K]};
+        const v2f qr = p.r * w - p.i * s, qi = p.r * s + p.i * w;  // (e, t) per part
+        tr = v2f{qr.y, qr.y};
+        ti = v2f{qi.y, qi.y};
+    }
+    return cx2{tr * pm + v2f{p.r.x, p.r.x}, ti * pm + v2f{p.i.x, p.i.x}};
+}
+template <int K = 0>
+__device__ __forceinline__ void combine64p(const cx2 (&a)[32], cx2 (&y)[32]) {
+    if constexpr (K < 32) {
+        y[K] = combine1<K>(a[perm32(K)]);
+        combine64p<K + 1>(a, y);
+    }
+}
+
+template <bool INV>
+__device__ __forceinline__ cx2 conj2(cx2 a) {
+    if constexpr (INV) return cx2{a.r, -a.i};
+    return a;
+}
+template <bool INV>
+__device__ __forceinline__ cx conj1(cx a) {
+    if constexpr (INV) return cx{a.r, -a.i};
+    return a;
+}
+
+// DFT32 of both halves; INV: the unnormalised inverse, conj(DFT(conj(x)))
+template <bool BAR, bool INV>
+__device__ __forceinline__ void x2dft32_dir(cx2 (&v)[32]) {
+#pragma unroll
+    for (int j = 0; j < 32; ++j) v[j] = conj2<INV>(v[j]);
+    x2dft32<BAR>(v);
+#pragma unroll
+    for (int j = 0; j < 32; ++j) v[j] = conj2<INV>(v[j]);
+}
+
+// combine of the inverse: (E, O) -> (E + W64^-k O, E - W64^-k O), through
+// the same conjugation identity
+template <bool INV, int K = 0>
+__device__ __forceinline__ void combine64p_dir(const cx2 (&a)[32], cx2 (&y)[32]) {
+    if constexpr (K < 32) {
+        y[K] = conj2<INV>(combine1<K>(conj2<INV>(a[perm32(K)])));
+        combine64p_dir<INV, K + 1>(a, y);
+    }
+}
+template <bool INV>
+__device__ __forceinline__ void combine64_dir(const cx2 (&a)[32], cx (&yp)[32], cx (&ym)[32]) {
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+        const cx2 p = conj2<INV>(a[perm32(k)]);
+        const cx e = cx{p.r.x, p.i.x};
+        const cx t = stw64(cx{p.r.y, p.i.y}, k);
+        yp[k] = conj1<INV>(e + t);
+        ym[k] = conj1<INV>(e - t);
+    }
+}
+
+// 4096-point complex FFT of one wavefront.  In: P[j] = (u[2j], u[2j+1]),
+// u[r] = element l + 64 r of this lane l (r is the register index).  Out:
+// U[l + 64 q] = zp[q] (q < 32), zm[q - 32] -- forward: Z = DFT(u), inverse
+// (INV): the unnormalised inverse.  tlo[j] = W4096^(l j), thp[h] =
+// (W4096^(8 l h), W4096^(8 l (h + 4))); lds = this wave's 64 x 65 tile.
+template <bool INV, bool BAR_DFT = true, bool BAR_TW = true>
+__device__ __forceinline__ void fft4096_pk(cx2 (&P)[32], float *lds, const cx (&tlo)[8], const cx2 (&thp)[4],
+                                           uint32_t lane, cx (&zp)[32], cx (&zm)[32]) {
+    // DFT64 over the register index: even/odd DFT32 in the halves, combine
+    x2dft32_dir<BAR_DFT, INV>(P);
+    cx2 Q[32];  // Q[k] = (Y[k], Y[k+32]) * (W4096^(+-l k), W4096^(+-l (k+32)))
+    {
+        cx2 Y[32];
+        combine64p_dir<INV>(P, Y);
+#pragma unroll
+        for (int k = 0; k < 32; ++k) {
+            if (BAR_TW) __builtin_amdgcn_sched_barrier(0);
+            const int lo = k & 7, hi = k >> 3;
+            const cx2 w = lo ? cmulb(tlo[lo], thp[hi]) : thp[hi];
+            Q[k] = cmul2(Y[k], conj2<INV>(w));
+        }
+    }
+    // transpose through LDS: row l, column kb -> column l, row a
+    cx2 R[32];  // R[j] = (t[2j], t[2j+1]), t[a] = row a of column l
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+        lds[lane * 65u + k] = Q[k].r.x;
+        lds[lane * 65u + k + 32] = Q[k].r.y;
+    }
+    lds_fence();
+#pragma unroll
+    for (int j = 0; j < 32; ++j) R[j].r = v2f{lds[(2 * j) * 65 + lane], lds[(2 * j + 1) * 65 + lane]};
+    lds_fence();
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+        lds[lane * 65u + k] = Q[k].i.x;
+        lds[lane * 65u + k + 32] = Q[k].i.y;
+    }
+    lds_fence();
+#pragma unroll
+    for (int j = 0; j < 32; ++j) R[j].i = v2f{lds[(2 * j) * 65 + lane], lds[(2 * j + 1) * 65 + lane]};
+    // DFT64 over the other index
+    x2dft32_dir<BAR_DFT, INV>(R);
+    combine64_dir<INV>(R, zp, zm);
+}
+
+}  // namespace dspb

@@ -1,0 +1,205 @@
+// fir_fft.hip -- FIR render by FFT overlap-save, one wavefront per
+// 8192-sample frame (cfg 3b at the HBM roof instead of the FP32 roof).
+//
+// Frame f covers input samples [f H - 1024, f H + 7168), H = 7168; its
+// circular convolution with the taps (T <= 1025) equals the linear one at
+// frame positions n >= 1024, so it owns outputs [f H, (f + 1) H).  Per frame:
+//
+//   forward   the 8192-point real FFT of stft_pk.hip (packed 4096-point
+//             complex FFT + paired real split): X1 = 2 X[k], X2 = conj 2 X[M-k]
+//   multiply  Y = X * H, H = FFT(taps zero-padded) / 16384 (the inverse's
+//             1/4096, the two real-split halvings; a power of two: exact)
+//   inverse   the split run backwards on the same lane pairs --
+//             Z'[k] = E + i O, Z'[M-k] = conj E + i conj O with
+//             E = Y[k] + conj Y[M-k], O = (Y[k] - conj Y[M-k]) W8192^-k --
+//             the M-k half sent back to its owner lane with ds_bpermute,
+//             then the packed 4096-point inverse (fft4096_pk<true>)
+//   store     y[2m] = Re z'[m], y[2m+1] = Im z'[m] for m >= 512
+//
+// tools/olsave_model.py is the numpy model of exactly this index math.
+#include "fft_pk.hpp"
+
+namespace dspb {
+
+constexpr uint32_t kOlsHop = 7168;    // outputs per frame
+constexpr uint32_t kOlsHist = 1024;   // history samples per frame (T - 1 <= 1024)
+
+// twiddles for the 4096-point passes; `salt` is an opaque zero so that the
+// second load (for the inverse) is not merged with the first and the
+// compiler does not keep 30 VGPRs of twiddles live across the whole frame
+__device__ __forceinline__ void load_stage_tw(const v2f *tw, uint32_t lane, uint32_t salt, cx (&tlo)[8],
+                                              cx2 (&thp)[4]) {
+    const v2f *t = tw + salt;
+#pragma unroll
+    for (int j = 1; j < 8; ++j) {
+        const v2f a = (t + 8192u + 64u * (uint32_t)(j - 1))[lane];
+        tlo[j] = cx{a.x, a.y};
+    }
+    const float4 *tp4 = reinterpret_cast<const float4 *>(t + 8192u + 896u);
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+        const float4 q = tp4[64u * (uint32_t)h + lane];
+        thp[h] = cx2{v2f{q.x, q.y}, v2f{q.z, q.w}};
+    }
+}
+
+// EDGE: frames that reach before sample 0 or past L (bounds-checked loads);
+// interior frames run the EDGE = false instantiation
+template <bool EDGE>
+__global__ __launch_bounds__(256, 2) void fir_fft_kernel(FirFftArgs A, uint64_t f0, uint64_t nf) {
+    __shared__ __attribute__((aligned(16))) float lds_all[4][64 * 65];
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t ch = blockIdx.y;
+    const uint64_t fi = (uint64_t)xcd_remap(blockIdx.x, gridDim.x) * 4u + wave;
+    if (fi >= nf) return;
+    const uint64_t f = f0 + fi;
+    float *lds = lds_all[wave];
+    const int64_t fs = (int64_t)(f * kOlsHop) - (int64_t)kOlsHist;  // even
+    const float *x = (ch < A.in_ch) ? A.in.p[ch] : nullptr;
+
+    cx tlo[8];
+    cx2 thp[4];
+    load_stage_tw(A.tw, lane, 0u, tlo, thp);
+
+    // ---- frame: v[b] = (x[fs + 2l + 128b], x[fs + 2l + 128b + 1]), zero outside [0, L)
+    cx2 P[32];
+    {
+        cx v[64];
+        if constexpr (!EDGE) {
+            if (x != nullptr) {
+#pragma unroll
+                for (int b = 0; b < 64; ++b) {
+                    const v2f t = reinterpret_cast<const v2f *>(x + fs + 128 * b)[lane];
+                    v[b] = cx{t.x, t.y};
+                }
+            } else {  // a channel the file does not have: silence
+#pragma unroll
+                for (int b = 0; b < 64; ++b) v[b] = cx{0.f, 0.f};
+            }
+        } else {
+#pragma unroll
+            for (int b = 0; b < 64; ++b) {
+                const int64_t s = fs + 2 * (int64_t)lane + 128 * b;
+                v[b] = cx{(x && s >= 0 && (uint64_t)s < A.L) ? x[s] : 0.f,
+                          (x && s + 1 >= 0 && (uint64_t)(s + 1) < A.L) ? x[s + 1] : 0.f};
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 32; ++j)
+            P[j] = cx2{v2f{v[2 * j].r, v[2 * j + 1].r}, v2f{v[2 * j].i, v[2 * j + 1].i}};
+    }
+
+    cx zp[32], zm[32];
+    fft4096_pk<false>(P, lds, tlo, thp, lane, zp, zm);
+
+    // ---- split, H multiply, inverse split, paired over (ka, ka + 16) --------
+    const uint32_t src = ((64u - lane) & 63u) * 4u;
+    const bool l0 = lane == 0;
+    const v2f wl2 = A.tw[lane];  // W8192^l
+    const cx wl = cx{wl2.x, wl2.y};
+    // own Z'[l + 64 ka] (ka < 32) and, received from lane 64 - l, Z'[l + 64 ka']
+    // (ka' = 32 + q): lane 64 - l computes it as its Z'[M - k] at ka = 31 - q
+    // and it is sent in the same iteration; lane 0 (which pairs with itself,
+    // shifted by one register) is fixed up after the loop
+    cx zk[32], zr[32];
+#pragma unroll
+    for (int ka = 0; ka < 16; ++ka) {
+        __builtin_amdgcn_sched_barrier(0);
+        const cx a0 = ka == 0 ? zp[0] : zm[32 - ka], b0 = zm[31 - ka];
+        const cx a1 = zm[16 - ka], b1 = zm[15 - ka];
+        const cx s0 = cx{l0 ? a0.r : b0.r, l0 ? a0.i : b0.i};
+        const cx s1 = cx{l0 ? a1.r : b1.r, l0 ? a1.i : b1.i};
+        const cx2 Pp = cx2{v2f{bperm(src, s0.r), bperm(src, s1.r)}, v2f{bperm(src, s0.i), bperm(src, s1.i)}};
+        const cx2 Z = cx2{v2f{zp[ka].r, zp[ka + 16].r}, v2f{zp[ka].i, zp[ka + 16].i}};
+        const cx2 E = cx2{Z.r + Pp.r, Z.i - Pp.i};
+        const cx2 D = cx2{Z.r - Pp.r, Z.i + Pp.i};
+        const cx2 tw = cmulb(wl, cx2{v2f{kW128_re[ka], kW128_re[ka + 16]}, v2f{kW128_im[ka], kW128_im[ka + 16]}});
+        const cx2 T = cmul2(negi(D), tw);
+        const cx2 X1 = E + T;  // 2 X[k]
+        const cx2 X2 = E - T;  // conj 2 X[M - k]
+        const float4 *hp = reinterpret_cast<const float4 *>(A.H) + 2u * (64u * (uint32_t)ka + lane);
+        const float4 ha = hp[0], hb = hp[1];
+        const cx2 Hk = cx2{v2f{ha.x, ha.y}, v2f{ha.z, ha.w}};
+        const cx2 HMk = cx2{v2f{hb.x, hb.y}, v2f{hb.z, hb.w}};
+        const cx2 Yk = cmul2(X1, Hk);
+        const cx2 YMk = cmul2(cx2{X2.r, -X2.i}, HMk);
+        const cx2 E2 = cx2{Yk.r + YMk.r, Yk.i - YMk.i};                           // Y[k] + conj Y[M-k]
+        const cx2 O2 = cmul2(cx2{Yk.r - YMk.r, Yk.i + YMk.i}, cx2{tw.r, -tw.i});  // (..) W^-k
+        const cx2 Zk = cx2{E2.r - O2.i, E2.i + O2.r};                            // E + i O
+        const cx2 ZMk = cx2{E2.r + O2.i, O2.r - E2.i};                           // conj E + i conj O
+        zk[ka] = cx{Zk.r.x, Zk.i.x};
+        zk[ka + 16] = cx{Zk.r.y, Zk.i.y};
+        zr[31 - ka] = cx{bperm(src, ZMk.r.x), bperm(src, ZMk.i.x)};
+        zr[15 - ka] = cx{bperm(src, ZMk.r.y), bperm(src, ZMk.i.y)};
+    }
+    // lane 0 received its own Z'[M - k] of ka = 31 - q at q; it needs the one of
+    // ka = 32 - q, i.e. what landed at q - 1, and at q = 0 the self-paired
+    // bin k = 2048: Z[2048] = zm[0], 2 X[2048] = 2 conj Z, Z'[2048] = 2 conj Y
+    {
+        const cx Z = zm[0];
+        const cx Y = mulc(cx{2.f * Z.r, -2.f * Z.i}, A.h2048.x, A.h2048.y);
+#pragma unroll
+        for (int q = 31; q >= 1; --q) zr[q] = cx{l0 ? zr[q - 1].r : zr[q].r, l0 ? zr[q - 1].i : zr[q].i};
+        zr[0] = cx{l0 ? 2.f * Y.r : zr[0].r, l0 ? -2.f * Y.i : zr[0].i};
+    }
+
+    // ---- inverse 4096-point FFT over the register index ka -------------------
+    cx2 Q[32];
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+        const cx u0 = 2 * j < 32 ? zk[2 * j] : zr[2 * j - 32];
+        const cx u1 = 2 * j + 1 < 32 ? zk[2 * j + 1] : zr[2 * j + 1 - 32];
+        Q[j] = cx2{v2f{u0.r, u1.r}, v2f{u0.i, u1.i}};
+    }
+    cx yp[32], ym[32];
+    {
+        uint32_t salt = 0u;
+        asm volatile("" : "+s"(salt));
+        load_stage_tw(A.tw, lane, salt, tlo, thp);
+    }
+    fft4096_pk<true>(Q, lds, tlo, thp, lane, yp, ym);
+
+    // ---- outputs: m = l + 64 b, b >= 8 -> y[f H + 2l + 128 (b - 8)] ----------
+    float *o = A.out.p[ch];
+    const uint64_t ob = f * kOlsHop + 2u * lane;
+    if (f * kOlsHop + kOlsHop <= A.Ly) {
+#pragma unroll
+        for (int b = 8; b < 64; ++b) {
+            const cx z = b < 32 ? yp[b] : ym[b - 32];
+            *reinterpret_cast<v2f *>(o + ob + 128u * (uint32_t)(b - 8)) = v2f{z.r, z.i};
+        }
+    } else {
+#pragma unroll
+        for (int b = 8; b < 64; ++b) {
+            const cx z = b < 32 ? yp[b] : ym[b - 32];
+            const uint64_t i = ob + 128u * (uint32_t)(b - 8);
+            if (i < A.Ly) o[i] = z.r;
+            if (i + 1 < A.Ly) o[i + 1] = z.i;
+        }
+    }
+}
+
+int launch_fir_fft(const FirFftArgs &A, uint32_t C, hipStream_t s) {
+    if (A.F == 0 || C == 0) return DSP_OK;
+    // interior frames: [1, fe) with (f H - 1024) + 8192 <= L; the rest is edge
+    uint64_t fe = 1;
+    if (A.L + kOlsHist >= 8192u && A.in_ch > 0) fe = (A.L + kOlsHist - 8192u) / kOlsHop + 1;
+    if (fe > A.F) fe = A.F;
+    if (fe < 1) fe = 1;
+    auto run = [&](bool edge, uint64_t f0, uint64_t nf) -> int {
+        if (nf == 0) return DSP_OK;
+        const uint64_t groups = (nf + 3) / 4;
+        if (groups > 0x7fffffffull) return DSP_ERR_INVALID;
+        if (edge) hipLaunchKernelGGL(fir_fft_kernel<true>, dim3((uint32_t)groups, C), dim3(256), 0, s, A, f0, nf);
+        else hipLaunchKernelGGL(fir_fft_kernel<false>, dim3((uint32_t)groups, C), dim3(256), 0, s, A, f0, nf);
+        DSPB_HIP(hipGetLastError());
+        return DSP_OK;
+    };
+    int st = run(true, 0, 1);  // frame 0 reaches before sample 0
+    if (!st && fe > 1) st = run(false, 1, fe - 1);
+    if (!st) st = run(true, fe, A.F - fe);
+    return st;
+}
+
+}  // namespace dspb

@@ -74,6 +74,18 @@ int module_render(::dsp_module *m, const void *params, uint32_t params_size, con
                   uint64_t goff, hipStream_t s);
 int module_ir(::dsp_module *m, const void *params, uint32_t params_size, float *const *bufs, uint32_t C,
               uint32_t n, float sr, hipStream_t s);
+struct FirFftArgs {
+    ChanIn in;           // input channels
+    uint32_t in_ch;
+    uint64_t L;          // input samples (zero past)
+    ChanOut out;         // render rows, Ly samples
+    uint64_t Ly;
+    uint64_t F;          // frames = ceil(Ly / 7168)
+    const float *H;      // FFT(taps)/16384, lane-major pairs (fir_fft.hip)
+    v2f h2048;           // H[2048]
+    const v2f *tw;       // T8192 + lane-major stage twiddles (capi.cpp get_tw)
+};
+int launch_fir_fft(const FirFftArgs &A, uint32_t C, hipStream_t s);
 int launch_fir(const float *x, uint64_t L, float *y, uint64_t Ly, const float *h8, uint32_t T8,
                bool y_aligned16, hipStream_t s);
 int launch_minmax(const float *x, uint64_t n, uint32_t P, float *vmax, float *vmin, hipStream_t s);

@@ -18,61 +18,10 @@
 //
 // Loads, render, window and stores are those of stft_soa.hip with options
 // 14 (LDS ramp table, lane-major twiddles issued first, computed window).
-#include "fft_x2.hpp"
+#include "fft_pk.hpp"
 #include "frame_load.hpp"
 
 namespace dspb {
-
-// both halves: a * w
-__device__ __forceinline__ cx2 cmul2(cx2 a, cx2 w) {
-    return cx2{a.r * w.r - a.i * w.i, a.r * w.i + a.i * w.r};
-}
-// (c + i s) broadcast times both halves of w
-__device__ __forceinline__ cx2 cmulb(cx c, cx2 w) {
-    return cx2{c.r * w.r - c.i * w.i, c.r * w.i + c.i * w.r};
-}
-
-// radix-2 DIT combine of a transformed pair: halves (E[k], O[k]) at
-// a[perm32(k)] -> (Y[k], Y[k+32]) as scalars
-__device__ __forceinline__ void combine64(const cx2 (&a)[32], cx (&yp)[32], cx (&ym)[32]) {
-#pragma unroll
-    for (int k = 0; k < 32; ++k) {
-        const cx2 p = a[perm32(k)];
-        const cx e = cx{p.r.x, p.i.x};
-        const cx t = stw64(cx{p.r.y, p.i.y}, k);
-        yp[k] = e + t;
-        ym[k] = e - t;
-    }
-}
-
-// the same combine, packed: y[k] = (Y[k], Y[k+32]) as one cx2.  The odd
-// half is twiddled in place (the even half rides along times 1), then each
-// butterfly is one v_pk_fma: (e, e) + (t, t) * (1, -1).
-template <int K>
-__device__ __forceinline__ cx2 combine1(cx2 p) {
-    const v2f pm = v2f{1.f, -1.f};
-    v2f tr, ti;  // (t, t) where t = O W64^K, as splats of one register half
-    if constexpr (K == 0) {
-        tr = v2f{p.r.y, p.r.y};
-        ti = v2f{p.i.y, p.i.y};
-    } else if constexpr (K == 16) {  // t = -i O = (O.i, -O.r)
-        tr = v2f{p.i.y, p.i.y};
-        ti = -v2f{p.r.y, p.r.y};
-    } else {
-        const v2f w = v2f{1.f, kW64_re[K]}, s = v2f{0.f, kW64_im[K]};
-        const v2f qr = p.r * w - p.i * s, qi = p.r * s + p.i * w;  // (e, t) per part
-        tr = v2f{qr.y, qr.y};
-        ti = v2f{qi.y, qi.y};
-    }
-    return cx2{tr * pm + v2f{p.r.x, p.r.x}, ti * pm + v2f{p.i.x, p.i.x}};
-}
-template <int K = 0>
-__device__ __forceinline__ void combine64p(const cx2 (&a)[32], cx2 (&y)[32]) {
-    if constexpr (K < 32) {
-        y[K] = combine1<K>(a[perm32(K)]);
-        combine64p<K + 1>(a, y);
-    }
-}
 
 // OPT bits (A/B, dsp_stft_soa_options >> 4): 1 = no scheduling barriers in
 // the DFT32s, 2 = none in the twiddle loop, 4 = none in the split loop
@@ -213,46 +162,10 @@ __global__ __launch_bounds__(256, 2) void stft8192_pk_kernel(Stft8kArgs A) {
     }
     }  // !SOA
 
-    // ---- 3. DFT64 over b: even/odd DFT32 in the halves, then combine --------
-    x2dft32<!(OPT & kPkNoBarDft)>(P);
-    cx2 Q[32];  // Q[k] = (Y[k], Y[k+32]) * (W4096^(l k), W4096^(l (k+32)))
-    {
-        cx2 Y[32];
-        combine64p(P, Y);
-#pragma unroll
-        for (int k = 0; k < 32; ++k) {
-            if (!(OPT & kPkNoBarTw)) __builtin_amdgcn_sched_barrier(0);
-            const cx2 y = Y[k];
-            const int lo = k & 7, hi = k >> 3;
-            const cx2 w = lo ? cmulb(tlo[lo], thp[hi]) : thp[hi];
-            Q[k] = cmul2(y, w);
-        }
-    }
-
-    // ---- 4. transpose through LDS: row l, column kb -> column l, row a -----
-    cx2 R[32];  // R[j] = (u[2j], u[2j+1]), u[a] = row a of column l
-#pragma unroll
-    for (int k = 0; k < 32; ++k) {
-        lds[lane * 65u + k] = Q[k].r.x;
-        lds[lane * 65u + k + 32] = Q[k].r.y;
-    }
-    lds_fence();
-#pragma unroll
-    for (int j = 0; j < 32; ++j) R[j].r = v2f{lds[(2 * j) * 65 + lane], lds[(2 * j + 1) * 65 + lane]};
-    lds_fence();
-#pragma unroll
-    for (int k = 0; k < 32; ++k) {
-        lds[lane * 65u + k] = Q[k].i.x;
-        lds[lane * 65u + k + 32] = Q[k].i.y;
-    }
-    lds_fence();
-#pragma unroll
-    for (int j = 0; j < 32; ++j) R[j].i = v2f{lds[(2 * j) * 65 + lane], lds[(2 * j + 1) * 65 + lane]};
-
-    // ---- 5. DFT64 over a: Z[l + 64 ka] = zp[ka] (ka < 32), zm[ka - 32] ------
-    x2dft32<!(OPT & kPkNoBarDft)>(R);
+    // ---- 3-5. 4096-point complex FFT of the packed frame (fft_pk.hpp):
+    // Z[l + 64 ka] = zp[ka] (ka < 32), zm[ka - 32]
     cx zp[32], zm[32];
-    combine64(R, zp, zm);
+    fft4096_pk<false, !(OPT & kPkNoBarDft), !(OPT & kPkNoBarTw)>(P, lds, tlo, thp, lane, zp, zm);
 
     // ---- 6. paired real split over (ka, ka + 16), ka < 16 ------------------
     // X[k] = E + T and X[M-k] = conj(E - T), k = l + 64 ka, partner

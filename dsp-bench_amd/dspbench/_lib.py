@@ -89,6 +89,7 @@ _SIGS = {
     "dsp_kernel_timing_enable": (None, [C.c_int]),
     "dsp_stft_kernel_variant": (C.c_int, [C.c_int]),
     "dsp_stft_soa_options": (C.c_int, [C.c_int]),
+    "dsp_fir_method": (C.c_int, [C.c_int]),
     "dsp_kernel_timing": (C.c_int, [C.POINTER(C.c_double), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     "dsp_initializer_create": (C.c_void_p, [C.c_size_t, C.c_int]),
     "dsp_initializer_reset": (None, [C.c_void_p]),

@@ -184,6 +184,12 @@ int dsp_stft_kernel_variant(int variant);
  * outside 0..127 only query.  Returns the previous options. */
 int dsp_stft_soa_options(int options);
 
+/* FIR render method (DSP_PLUGIN_FIR): 0 = auto (FFT overlap-save with
+ * 8192-point frames when T <= 1025, else direct form), 1 = direct form,
+ * 2 = overlap-save (T <= 1025).  Other values only query.  Returns the
+ * previous method. */
+int dsp_fir_method(int method);
+
 /* Diagnostics. */
 int dsp_abi_version(void);
 const char *dsp_status_string(int status);
