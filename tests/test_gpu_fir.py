@@ -116,7 +116,12 @@ def test_gpu_fir_stft_and_ir(torch_cuda, oracle, fir_method):
     m = mag.cpu().numpy()[1]
     assert np.max(np.abs(m - mref)) <= 1e-6 * np.max(mref)
     ir, imag = d.ir_analysis(d.Plugin.fir(taps), C_out=2, device="cuda")    # IR of a FIR = its taps
-    assert np.array_equal(ir.cpu().numpy()[0, :1024], taps) and not ir.cpu().numpy()[0, 1024:].any()
+    irn = ir.cpu().numpy()[0]
+    want = np.concatenate([taps, np.zeros(1024, np.float32)])
+    if fir_method == 1:
+        assert np.array_equal(irn, want)
+    else:  # an impulse through the FFT path: within the overlap-save tolerance
+        assert np.max(np.abs(irn - want)) <= OLS_TOL * np.max(np.abs(taps))
     ref = oracle.np_ir_magnitude(np.concatenate([taps, np.zeros(1024, np.float32)]), 2048)
     assert np.max(np.abs(imag.cpu().numpy() - ref)) <= 1e-6 * np.max(ref)
 
