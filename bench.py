@@ -55,6 +55,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
     ap.add_argument("--gather", action="store_true", help="also time an RCCL gather to rank 0")
+    ap.add_argument("--fir-method", type=int, default=0, choices=[0, 1, 2],
+                    help="fir1024: 0 auto (overlap-save), 1 direct form, 2 overlap-save")
     ap.add_argument("--stft-variant", type=int, default=5, choices=[0, 1, 2, 3, 4, 5],
                     help="8192-pt kernel (dsp_stft_kernel_variant): 2 = wave/frame scalar SoA, "
                          "5 = wave/frame packed even/odd pairs")
@@ -124,6 +126,7 @@ def main():
 
     import dspbench as d
     d.lib().dsp_stft_kernel_variant(args.stft_variant)
+    d.lib().dsp_fir_method(args.fir_method)
 
     wl = args.workload
     sr = 96_000 if wl in ("stft96k", "ch96k") else SR
@@ -182,10 +185,14 @@ def main():
 
         def step():
             d.render_offline(x, CH, B, float(sr), fplug, out=out)
+        ols = d.lib().dsp_fir_method(-1) != 1
         workload = (f"FIR render, 1024 taps = compute_IR(IR_test)[0:1024], B=512, {minutes:g} min of "
-                    "48 kHz stereo per GPU (cfg 3b)")
-        kname = "fir_kernel (packed fp32 direct form)"
-        alg_flops = 2.0 * 1024 * CH * nb * B
+                    f"48 kHz stereo per GPU (cfg 3b), {'FFT overlap-save' if ols else 'direct form'}")
+        if ols:  # HBM-bound: the library times it with read + write bytes
+            kname = "fir_fft_kernel (8192-pt overlap-save, 7168 outputs / frame)"
+        else:
+            kname = "fir_kernel (packed fp32 direct form)"
+            alg_flops = 2.0 * 1024 * CH * nb * B
     elif wl == "gain10min":
         def step():
             d.render_offline(x, CH, B, float(sr), plugin, out=out)

@@ -49,11 +49,18 @@ static int invalid(const char *fmt, ...) {
 // ---------------------------------------------------------------------------
 // per-device resources
 // ---------------------------------------------------------------------------
+struct FirTaps {  // a FIR filter's device taps + overlap-save spectrum
+    std::vector<float> taps;
+    float *dev;
+    float h2048r, h2048i;
+};
+
 struct DeviceRes {
     v2f *tw8192 = nullptr;  // exp(-2 pi i k / 8192), then 896 lane-major stage twiddles
     float4 *wbase = nullptr;  // (cos, sin)(theta 2l), (cos, sin)(theta (2l+1)), theta = 2 pi / 8191
     std::map<std::tuple<int, uint32_t, uint32_t, float>, float *> windows;  // (kind, N, valid, scale)
     std::map<void *, std::pair<float *, size_t>> scratch;     // per stream
+    std::vector<FirTaps> fir;                                  // FIR filters seen (plugin_map)
 };
 
 static std::mutex g_mu;
@@ -338,22 +345,38 @@ static int plugin_map(const dsp_plugin *p, uint32_t B, int dev, hipStream_t s, S
         if (!p->params || T == 0 || p->params_size % 4 || T > 2048)
             return invalid("FIR plugin needs 1..2048 float taps as its params blob");
         const uint32_t T8 = (T + 15) & ~15u;  // zero-padded to 16 (fir.hip)
-        // scratch: [taps, T8 floats][overlap-save H table, 8192 + 2 floats]
-        std::vector<float> h(T8 + 8192 + 2, 0.f);
-        std::memcpy(h.data(), p->params, 4 * (size_t)T);
-        if (T <= 1025) ols_table(h.data(), T, h.data() + T8);
-        float *taps = nullptr;
-        int st = get_scratch(dev, s, sizeof(float) * h.size(), &taps);
-        if (st) return st;
-        DSPB_HIP(hipMemcpyAsync(taps, h.data(), sizeof(float) * h.size(), hipMemcpyHostToDevice, s));
-        DSPB_HIP(hipStreamSynchronize(s));  // h is a host buffer on this frame
+        // device copy: [taps, T8 floats][overlap-save H table, 8192 + 2 floats],
+        // cached per device by the taps' bytes (the host FFT and the upload
+        // happen once per filter, not once per render)
+        std::vector<float> key((const float *)p->params, (const float *)p->params + T);
+        FirTaps *ft = nullptr;
+        {
+            std::lock_guard<std::mutex> lk(g_mu);
+            DeviceRes &r = g_res[dev];
+            for (auto &e : r.fir)
+                if (e.taps == key) { ft = &e; break; }
+            if (!ft) {
+                std::vector<float> h(T8 + 8192 + 2, 0.f);
+                std::memcpy(h.data(), key.data(), 4 * (size_t)T);
+                if (T <= 1025) ols_table(h.data(), T, h.data() + T8);
+                float *d = nullptr;
+                DSPB_HIP(hipMalloc(&d, sizeof(float) * h.size()));
+                DSPB_HIP(hipMemcpy(d, h.data(), sizeof(float) * h.size(), hipMemcpyHostToDevice));
+                if (r.fir.size() >= 8) {  // small LRU-ish cap
+                    (void)hipFree(r.fir.front().dev);
+                    r.fir.erase(r.fir.begin());
+                }
+                r.fir.push_back(FirTaps{key, d, h[T8 + 8192], h[T8 + 8193]});
+                ft = &r.fir.back();
+            }
+        }
         m->kind = MapKind::Fir;
-        m->taps = taps;
+        m->taps = ft->dev;
         m->ntaps8 = T8;
         m->ntaps = T;
-        m->olsH = taps + T8;
-        m->olsH2048[0] = h[T8 + 8192];
-        m->olsH2048[1] = h[T8 + 8193];
+        m->olsH = ft->dev + T8;
+        m->olsH2048[0] = ft->h2048r;
+        m->olsH2048[1] = ft->h2048i;
         return DSP_OK;
     }
     case DSP_PLUGIN_GENERIC:  // the plugin's own audio_callback, compiled for gfx950 (module.h)
