@@ -159,6 +159,9 @@ def main():
     lib0 = d.lib()
     alg_bytes = None  # set where the library's own launch timing does not apply
     alg_flops = None  # FLOP-bound workloads (fir1024)
+    alg_desc = ("fused: C*F*(4H + 4K) B (render write + |X| write; IR_test reads no input); "
+                "memory: C*F*(4H + 4K) B (each sample read once + |X| write)")
+    plug_name = plugin.name
     if wl == "headline":
         def step():
             d.render_stft(x, CH, B, float(sr), plugin, N=N_FFT, H=HOP, window=d.DSP_WIN_HANN,
@@ -182,6 +185,8 @@ def main():
         # BASELINE configs[2] / SURVEY cfg 3b: 1024 taps = compute_IR(IR_test)[0:1024]
         ir, _ = d.ir_analysis(d.Plugin.ir_test(0.9, 0.002), C_out=1, sr=float(sr), device=dev)
         fplug = d.Plugin.fir(ir[0, :1024].cpu().numpy())
+        plug_name = "fir (1024 taps)"
+        alg_desc = "C*L*(4 + 4) B (each input sample read once + each output sample written once)"
 
         def step():
             d.render_offline(x, CH, B, float(sr), fplug, out=out)
@@ -199,6 +204,7 @@ def main():
         workload = f"gain_test render (B=512), {minutes:g} min of 48 kHz stereo per GPU (cfg 2)"
         kname = "render_vec_kernel<Gain>"
         alg_bytes = CH * L_in * 8  # read + write
+        alg_desc = "C*L*(4 + 4) B (read + write)"
     else:
         bits = 16 if wl == "wav16" else 24
         pay = torch.randint(0, 256, (CH * L_in * bits // 8,), dtype=torch.uint8, device=dev, generator=g)
@@ -215,6 +221,8 @@ def main():
         workload = f"WAV int{bits} stereo payload -> planar float (decode + deinterleave), {minutes:g} min of 48 kHz per GPU"
         kname = f"wav_decode_kernel<{bits}, PCM, 2 ch>"
         alg_bytes = CH * L_in * (bits // 8 + 4)
+        plug_name = None
+        alg_desc = f"C*L*({bits // 8} + 4) B (PCM payload read + planar float write)"
 
     for _ in range(args.warmup):
         step()
@@ -296,10 +304,11 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (uniform noise WAV in HBM; IR_test output is input-independent)",
+            "data": ("synthetic (uniform noise WAV in HBM; IR_test output is input-independent)"
+                     if wl in ("headline", "ch96k") else "synthetic (uniform noise in HBM)"),
             "config": {
                 "workload": workload,
-                "plugin": plugin.name,
+                "plugin": plug_name,
                 "samples_per_gpu": samples_per_rank,
                 "frames_per_gpu": CH * F if mag is not None else 0,
                 "sharding": ("one channel per GPU, no data-path collective" if wl == "ch96k" else
@@ -328,8 +337,7 @@ def main():
                 "traffic_source": traffic_src,
                 "kernel_avg_ms": round(kernel_avg_ms, 5),
                 "algorithmic_bytes_per_launch": int(bytes_per_launch),
-                "algorithmic": "fused: C*F*(4H + 4K) B (render write + |X| write; IR_test reads no input); "
-                               "memory: C*F*(4H + 4K) B (each sample read once + |X| write)",
+                "algorithmic": alg_desc,
             }),
             "cpu_baseline": cpu,
         }

@@ -46,15 +46,8 @@ __device__ __forceinline__ void load_stage_tw(const v2f *tw, uint32_t lane, uint
 // EDGE: frames that reach before sample 0 or past L (bounds-checked loads);
 // interior frames run the EDGE = false instantiation
 template <bool EDGE>
-__global__ __launch_bounds__(256, 2) void fir_fft_kernel(FirFftArgs A, uint64_t f0, uint64_t nf) {
-    __shared__ __attribute__((aligned(16))) float lds_all[4][64 * 65];
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t ch = blockIdx.y;
-    const uint64_t fi = (uint64_t)xcd_remap(blockIdx.x, gridDim.x) * 4u + wave;
-    if (fi >= nf) return;
-    const uint64_t f = f0 + fi;
-    float *lds = lds_all[wave];
+__device__ __forceinline__ void fir_fft_frame(const FirFftArgs &A, uint64_t f, uint32_t ch, float *lds,
+                                              uint32_t lane) {
     const int64_t fs = (int64_t)(f * kOlsHop) - (int64_t)kOlsHist;  // even
     const float *x = (ch < A.in_ch) ? A.in.p[ch] : nullptr;
 
@@ -180,6 +173,21 @@ __global__ __launch_bounds__(256, 2) void fir_fft_kernel(FirFftArgs A, uint64_t 
     }
 }
 
+// one launch for all frames: a wave takes the bounds-checked path only for
+// frame 0 and the frames at or past fe (a wave-uniform branch), so the few
+// edge frames overlap the interior ones instead of running as serial
+// single-wave launches
+__global__ __launch_bounds__(256, 2) void fir_fft_kernel(FirFftArgs A, uint64_t fe) {
+    __shared__ __attribute__((aligned(16))) float lds_all[4][64 * 65];
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t ch = blockIdx.y;
+    const uint64_t f = (uint64_t)xcd_remap(blockIdx.x, gridDim.x) * 4u + wave;
+    if (f >= A.F) return;
+    if (f == 0 || f >= fe) fir_fft_frame<true>(A, f, ch, lds_all[wave], lane);
+    else fir_fft_frame<false>(A, f, ch, lds_all[wave], lane);
+}
+
 int launch_fir_fft(const FirFftArgs &A, uint32_t C, hipStream_t s) {
     if (A.F == 0 || C == 0) return DSP_OK;
     // interior frames: [1, fe) with (f H - 1024) + 8192 <= L; the rest is edge
@@ -187,19 +195,11 @@ int launch_fir_fft(const FirFftArgs &A, uint32_t C, hipStream_t s) {
     if (A.L + kOlsHist >= 8192u && A.in_ch > 0) fe = (A.L + kOlsHist - 8192u) / kOlsHop + 1;
     if (fe > A.F) fe = A.F;
     if (fe < 1) fe = 1;
-    auto run = [&](bool edge, uint64_t f0, uint64_t nf) -> int {
-        if (nf == 0) return DSP_OK;
-        const uint64_t groups = (nf + 3) / 4;
-        if (groups > 0x7fffffffull) return DSP_ERR_INVALID;
-        if (edge) hipLaunchKernelGGL(fir_fft_kernel<true>, dim3((uint32_t)groups, C), dim3(256), 0, s, A, f0, nf);
-        else hipLaunchKernelGGL(fir_fft_kernel<false>, dim3((uint32_t)groups, C), dim3(256), 0, s, A, f0, nf);
-        DSPB_HIP(hipGetLastError());
-        return DSP_OK;
-    };
-    int st = run(true, 0, 1);  // frame 0 reaches before sample 0
-    if (!st && fe > 1) st = run(false, 1, fe - 1);
-    if (!st) st = run(true, fe, A.F - fe);
-    return st;
+    const uint64_t groups = (A.F + 3) / 4;
+    if (groups > 0x7fffffffull) return DSP_ERR_INVALID;
+    hipLaunchKernelGGL(fir_fft_kernel, dim3((uint32_t)groups, C), dim3(256), 0, s, A, fe);
+    DSPB_HIP(hipGetLastError());
+    return DSP_OK;
 }
 
 }  // namespace dspb
