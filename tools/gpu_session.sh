@@ -2,7 +2,8 @@
 # tools/gpu_session.sh -- one gpurun session: GPU tests, smoke, bench, profile.
 # Every GPU step has its own time limit; a crash / abort / timeout ends the
 # session (no further GPU work), a plain test failure (exit 1) does not.
-#   usage: bash tools/gpu_session.sh [tests|bench|prof|all] [tag]
+#   usage: bash tools/gpu_session.sh [tests|bench|prof|all|others|full] [tag]
+#   (others: one bench line per non-headline workload; full: all + others)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -26,6 +27,7 @@ run() {  # run <name> <seconds> <cmd...>
     return 0
 }
 
+[[ $mode == full ]] && mode=all && others=1 || others=0
 if [[ $mode == tests || $mode == all ]]; then
     run pytest_gpu 900 python -m pytest tests -m gpu -q -x --timeout=600
     run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
@@ -34,7 +36,14 @@ if [[ $mode == bench || $mode == all || $mode == prof ]]; then
     run bench 600 python bench.py
 fi
 if [[ $mode == prof || $mode == all ]]; then
-    run rocprof_stats 600 rocprofv3 --kernel-trace --stats -d $out/prof_$tag -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline
-    find $out/prof_$tag -name "*kernel_stats.csv" | head -5
+    # the bench's own launch count (100 warmup + 200 timed), so the trace's
+    # last-200 average is the number bench.py reports as kernel_avg_ms
+    run rocprof_stats 600 rocprofv3 --kernel-trace --stats -d $out/prof_$tag -o run --output-format csv -- python bench.py --no-cpu-baseline
+    python tools/trace_avg.py $out/prof_$tag/run_kernel_trace.csv stft8192_pk 200 | tee $out/prof_$tag/trace_avg.txt
+fi
+if [[ $mode == others || $others == 1 ]]; then
+    for wl in gain10min stft96k ch96k fir1024 wav16 wav24; do
+        run bench_$wl 300 python bench.py --workload $wl --no-cpu-baseline
+    done
 fi
 echo "=== done"
