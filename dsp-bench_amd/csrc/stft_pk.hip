@@ -25,8 +25,27 @@ namespace dspb {
 
 // OPT bits (A/B, dsp_stft_soa_options >> 4): 1 = no scheduling barriers in
 // the DFT32s, 2 = none in the twiddle loop, 4 = none in the split loop
-enum { kPkNoBarDft = 1, kPkNoBarTw = 2, kPkNoBarSplit = 4 };
+// 8 = cached render stores (default: non-temporal -- the render is written
+// once and never read back; 2% faster at the headline shape), 16 =
+// non-temporal magnitude stores (slower: 256-byte row pieces need the L2 to
+// merge them), 32 = 4097-bin rows staged through LDS and stored as 16-byte
+// segments (no gain)
+enum { kPkNoBarDft = 1, kPkNoBarTw = 2, kPkNoBarSplit = 4, kPkRenderCached = 8, kPkNtMag = 16, kPkMagLds = 32 };
 constexpr int kPkDefaultOpt = 0;
+
+typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));  // a row is only dword-aligned
+
+template <bool NT, typename T>
+__device__ __forceinline__ void st(T *p, T v) {
+    if constexpr (NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
+template <bool NT>
+__device__ __forceinline__ void st4u(float *p, f4u v) {  // p: dword-aligned
+    if constexpr (NT) __builtin_nontemporal_store(v, reinterpret_cast<f4u *>(p));
+    else *reinterpret_cast<f4u *>(p) = v;
+}
 
 // PER (Ramp, pow2 B <= 4096): the frame's sample pairs repeat every PER
 // values of b (PER = max(1, B / 128)), so only v[0 .. PER) are fetched from
@@ -91,10 +110,18 @@ __global__ __launch_bounds__(256, 2) void stft8192_pk_kernel(Stft8kArgs A) {
 #pragma unroll
             for (int b = 0; b < (PER >= 2 ? PER : 1); ++b)
                 st[b] = v2f{X[b / 2].r[b & 1], X[b / 2].i[b & 1]};
+            constexpr bool NT = !(OPT & kPkRenderCached);
+            if (A.H == 4096u) {  // the headline hop: 32 columns, no per-store branch
 #pragma unroll
-            for (int b = 0; b < 64; ++b)
-                if (128u * (uint32_t)b < A.H)
-                    reinterpret_cast<v2f *>(o + 128u * (uint32_t)b)[lane] = st[b % (PER >= 2 ? PER : 1)];
+                for (int b = 0; b < 32; ++b)
+                    dspb::st<NT>(reinterpret_cast<v2f *>(o + 128u * (uint32_t)b) + lane, st[b % (PER >= 2 ? PER : 1)]);
+            } else {
+#pragma unroll
+                for (int b = 0; b < 64; ++b)
+                    if (128u * (uint32_t)b < A.H)
+                        dspb::st<NT>(reinterpret_cast<v2f *>(o + 128u * (uint32_t)b) + lane,
+                                     st[b % (PER >= 2 ? PER : 1)]);
+            }
         }
         // w(n) = wa - wb cos(theta n) = wa - u C_b + v S_b per parity, with
         // u = wb cos(theta n0), v = wb sin(theta n0) of the lane's base angle
@@ -134,10 +161,17 @@ __global__ __launch_bounds__(256, 2) void stft8192_pk_kernel(Stft8kArgs A) {
             s_render_frame<MK, POW2>(A, x, fs, lane, v);
         }
         float *o = A.out.p[ch] + fs;
+        constexpr bool NT = !(OPT & kPkRenderCached);
+        if (A.H == 4096u) {
 #pragma unroll
-        for (int b = 0; b < 64; ++b)
-            if (128u * (uint32_t)b < A.H)
-                reinterpret_cast<v2f *>(o + 128u * (uint32_t)b)[lane] = v2f{v[b].r, v[b].i};
+            for (int b = 0; b < 32; ++b)
+                st<NT>(reinterpret_cast<v2f *>(o + 128u * (uint32_t)b) + lane, v2f{v[b].r, v[b].i});
+        } else {
+#pragma unroll
+            for (int b = 0; b < 64; ++b)
+                if (128u * (uint32_t)b < A.H)
+                    st<NT>(reinterpret_cast<v2f *>(o + 128u * (uint32_t)b) + lane, v2f{v[b].r, v[b].i});
+        }
     }
 
     // ---- 2. window (pre-scaled by 0.5/sqrt N), packed into even/odd pairs ---
@@ -202,18 +236,35 @@ __global__ __launch_bounds__(256, 2) void stft8192_pk_kernel(Stft8kArgs A) {
             const uint32_t kk = (uint32_t)(ka + 16 * h);
             const uint32_t k1 = lane + 64u * kk;  // < 2048
             const uint32_t k2 = 4096u - k1;        // > 2048 (4096 at k1 = 0)
-            if constexpr (KM == kKPartial) {
+            if constexpr (KM == kKHalf && (OPT & kPkMagLds)) {
+                lds[64u * kk + lane] = m1[h];
+                lds[4096u - 64u * kk - lane] = m2[h];
+            } else if constexpr (KM == kKPartial) {
                 if (k1 < A.K) mrow[k1] = m1[h];
                 if (k2 < A.K) mrow[k2] = m2[h];
             } else {
-                (mrow + 64u * kk)[lane] = m1[h];
-                (mrow + 4096u - 64u * kk)[-(int)lane] = m2[h];
+                st<(OPT & kPkNtMag) != 0>(mrow + 64u * kk + lane, m1[h]);
+                st<(OPT & kPkNtMag) != 0>(mrow + 4096u - 64u * kk - lane, m2[h]);
                 if constexpr (KM == kKMirror) {
                     mrow[k1 == 0 ? 0u : 8192u - k1] = m1[h];
                     (mrow + 4096u + 64u * kk)[lane] = m2[h];
                 }
             }
         }
+    }
+    if constexpr (KM == kKHalf && (OPT & kPkMagLds)) {
+        if (l0) {
+            const cx Z = zm[0];
+            lds[2048] = 2.f * __builtin_amdgcn_sqrtf(__builtin_fmaf(Z.r, Z.r, Z.i * Z.i));
+        }
+        lds_fence();
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const float4 q = reinterpret_cast<const float4 *>(lds)[64 * i + lane];
+            st4u<(OPT & kPkNtMag) != 0>(mrow + 256u * (uint32_t)i + 4u * lane, f4u{q.x, q.y, q.z, q.w});
+        }
+        if (l0) mrow[4096] = lds[4096];
+        return;
     }
     if (l0) {  // the self-paired bin k = 2048: |X| = 2 |Z[2048]| (scaled), Z[2048] = zm[0]
         const cx Z = zm[0];
@@ -236,7 +287,6 @@ static void launch_pk_km(int km, dim3 grid, hipStream_t s, const Stft8kArgs &A) 
 // A.win2: the window pre-scaled by 0.5 / sqrt(8192); the computed window
 // (A.wbase, A.wa, A.wb) serves the full-frame 4097-bin shapes.
 int launch_stft8192_pk(const Stft8kArgs &A, uint32_t C, bool fused, int opt, hipStream_t stream) {
-    (void)opt;
     if (A.F == 0 || C == 0) return DSP_OK;
     const uint64_t groups = (A.F + 3) / 4;
     if (groups > 0x7fffffffull) return DSP_ERR_INVALID;
@@ -255,6 +305,23 @@ int launch_stft8192_pk(const Stft8kArgs &A, uint32_t C, bool fused, int opt, hip
 #define DSPB_PK_PER(p) \
     hipLaunchKernelGGL((stft8192_pk_kernel<kSrcRender, kKHalf, MapKind::Ramp, true, true, p>), grid, dim3(256), \
                        0, stream, A)
+#define DSPB_PK_PER_OPT(p, o) \
+    hipLaunchKernelGGL((stft8192_pk_kernel<kSrcRender, kKHalf, MapKind::Ramp, true, true, p, o>), grid, dim3(256), \
+                       0, stream, A)
+                // A/B of the store kinds at the headline shape (B = 512)
+                if (per == 4 && (opt & (kPkRenderCached | kPkNtMag | kPkMagLds))) {
+                    switch (opt & (kPkRenderCached | kPkNtMag | kPkMagLds)) {
+                    case kPkRenderCached: DSPB_PK_PER_OPT(4, kPkRenderCached); break;
+                    case kPkNtMag: DSPB_PK_PER_OPT(4, kPkNtMag); break;
+                    case kPkRenderCached | kPkNtMag: DSPB_PK_PER_OPT(4, kPkRenderCached | kPkNtMag); break;
+                    case kPkMagLds: DSPB_PK_PER_OPT(4, kPkMagLds); break;
+                    case kPkMagLds | kPkRenderCached: DSPB_PK_PER_OPT(4, kPkMagLds | kPkRenderCached); break;
+                    case kPkMagLds | kPkNtMag: DSPB_PK_PER_OPT(4, kPkMagLds | kPkNtMag); break;
+                    default: DSPB_PK_PER_OPT(4, kPkMagLds | kPkRenderCached | kPkNtMag); break;
+                    }
+                    break;
+                }
+#undef DSPB_PK_PER_OPT
                 switch (per) {
                 case 1: DSPB_PK_PER(1); break;
                 case 2: DSPB_PK_PER(2); break;

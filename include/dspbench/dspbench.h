@@ -180,8 +180,13 @@ int dsp_stft_kernel_variant(int variant);
 /* Option bits of variant 2 (A/B): 1 = no scheduling barrier inside the
  * register DFTs, 2 = prefetch the stage twiddles (lane-major table) with the
  * frame load, 4 = compute the window (angle addition) instead of loading it,
- * 8 = stage the IR_RAMP block table through LDS.  Default 14.  Values
- * outside 0..127 only query.  Returns the previous options. */
+ * 8 = stage the IR_RAMP block table through LDS.  Bits 4..8 (options >> 4)
+ * are variant 5's: 1/2/4 = no scheduling barriers in the DFTs / twiddle
+ * loop / split loop, 8 = cached render stores (default non-temporal), 16 =
+ * non-temporal magnitude stores, 32 =
+ * magnitude rows staged through LDS (B = 512 shape).  Default 14.  Values
+ * outside 0..1023 only query.  Returns the
+ * previous options. */
 int dsp_stft_soa_options(int options);
 
 /* FIR render method (DSP_PLUGIN_FIR): 0 = auto (FFT overlap-save with

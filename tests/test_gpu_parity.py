@@ -299,3 +299,30 @@ def test_pk_ramp_table_periods(torch_cuda, oracle, B):
         assert peak_rel_err(mag.cpu().numpy()[1], mref) <= PEAK_REL_TOL
     finally:
         L.dsp_stft_kernel_variant(oldv)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("opt", [0, 8, 16, 24, 32, 40, 48, 56])
+def test_pk_store_options(torch_cuda, oracle, opt):
+    """Packed kernel store A/B bits (dsp_stft_soa_options >> 4: 8/16
+    non-temporal render/magnitude stores, 32 rows staged through LDS):
+    the same bits as the default path, rows of any alignment (ld = K)."""
+    L = d.lib()
+    oldv, oldo = L.dsp_stft_kernel_variant(5), L.dsp_stft_soa_options(14 | (opt << 4))
+    try:
+        n = 8192 * 5 + 301
+        x = rnd((2, n), 63)
+        out, mag = d.render_stft(to_dev(torch_cuda, x), 2, 512, 48000.0, d.Plugin.ir_test(0.9, 0.002),
+                                 window=d.DSP_WIN_HANN)
+        L.dsp_stft_soa_options(14)
+        out0, mag0 = d.render_stft(to_dev(torch_cuda, x), 2, 512, 48000.0, d.Plugin.ir_test(0.9, 0.002),
+                                   window=d.DSP_WIN_HANN)
+        assert np.array_equal(out.cpu().numpy(), out0.cpu().numpy())
+        assert np.array_equal(mag.cpu().numpy(), mag0.cpu().numpy())
+        ref = oracle.render_offline([x[0], x[1]], 2, 512, 48000.0, oracle.restated_plugin("IR_test", [0.9, 0.002]))
+        assert np.array_equal(out.cpu().numpy(), ref)
+        mref = oracle.np_stft_mag(ref[0], 8192, 4096, d.DSP_WIN_HANN, 4097)
+        assert peak_rel_err(mag.cpu().numpy()[0], mref) <= PEAK_REL_TOL
+    finally:
+        L.dsp_stft_kernel_variant(oldv)
+        L.dsp_stft_soa_options(oldo)
