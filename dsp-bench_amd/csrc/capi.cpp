@@ -218,7 +218,18 @@ static float window_prescale(uint32_t N) {
     return g_stft_variant >= 2 ? (float)(0.5 / std::sqrt((double)N)) : 1.0f;
 }
 
+// a closed-form IR ramp (plugin_map) leaves the block table unbuilt; every
+// fused kernel but stft_pk's PER path reads it
+static int ensure_ramp_table(const SampleMap &m, hipStream_t s) {
+    if (m.kind != MapKind::Ramp || !m.closed) return DSP_OK;
+    return launch_ramp_table(const_cast<float *>(m.table), m.B, (float)m.rg0, (float)m.rs, s);
+}
+
 static int launch_stft(const Stft8kArgs &A, uint32_t C, bool fused, bool full, hipStream_t s) {
+    if (fused && !(g_stft_variant == 5 && A.map.closed && stft8192_pk_per_path(A, fused))) {
+        const int st = ensure_ramp_table(A.map, s);
+        if (st) return st;
+    }
     if (g_stft_variant == 5) return launch_stft8192_pk(A, C, fused, g_soa_opt >> 4, s);
     if (g_stft_variant == 4) return launch_stft8192_pair2(A, C, fused, s);
     if (g_stft_variant == 3) return launch_stft8192_pair_soa(A, C, fused, s);
@@ -297,6 +308,32 @@ static void ols_table(const float *taps, uint32_t T, float *out) {
 
 static int g_fir_method = 0;  // 0 auto (overlap-save when T <= 1025), 1 direct, 2 overlap-save
 
+// IR_test (build/IR_test.cpp:47-58) runs `gain -= step` in double from the
+// float parameters.  The sequence is often exact -- every partial result a
+// double -- and then table[i] = (float)(gain - i step) is one f64 FMA, with
+// no sequential kernel.  This checks that bit for bit against the recurrence
+// itself (B host f64 subtractions, cached per parameter set).
+static bool ramp_closed_form(float gain, float step, uint32_t B) {
+    if (B > (1u << 16)) return false;
+    static std::mutex mu;
+    static struct { uint32_t g, s, B; bool ok; } last = {0, 0, 0, false};
+    uint32_t gb, sb;
+    std::memcpy(&gb, &gain, 4);
+    std::memcpy(&sb, &step, 4);
+    std::lock_guard<std::mutex> lk(mu);
+    if (last.B == B && last.g == gb && last.s == sb) return last.ok;
+    double g = gain;
+    const double s = step;
+    bool ok = true;
+    for (uint32_t i = 0; i < B && ok; ++i) {
+        const double c = std::fma(-(double)i, s, (double)gain);
+        ok = std::memcmp(&c, &g, sizeof(double)) == 0;
+        g -= s;
+    }
+    last = {gb, sb, B, ok};
+    return ok;
+}
+
 static int plugin_map(const dsp_plugin *p, uint32_t B, int dev, hipStream_t s, SampleMap *m,
                       float sr = 48000.f) {
     m->kind = MapKind::Noop;
@@ -310,6 +347,8 @@ static int plugin_map(const dsp_plugin *p, uint32_t B, int dev, hipStream_t s, S
     m->gparams = nullptr;
     m->gparams_size = 0;
     m->sr = sr;
+    m->closed = 0;
+    m->rg0 = m->rs = 0.0;
     if (!p) return DSP_OK;  // no plugin loaded: the file plays through (audio.cpp:144)
     float v0 = 0.f, v1 = 0.f;
     switch (p->kind) {
@@ -334,10 +373,14 @@ static int plugin_map(const dsp_plugin *p, uint32_t B, int dev, hipStream_t s, S
         float *table = nullptr;
         int st = get_scratch(dev, s, sizeof(float) * B, &table);
         if (st) return st;
-        st = launch_ramp_table(table, B, v0, v1, s);
-        if (st) return st;
         m->kind = MapKind::Ramp;
         m->table = table;
+        m->rg0 = (double)v0;
+        m->rs = (double)v1;
+        m->closed = ramp_closed_form(v0, v1, B) ? 1u : 0u;
+        // closed form: the table is built only by ensure_ramp_table, for the
+        // kernels that read it
+        if (!m->closed) return launch_ramp_table(table, B, v0, v1, s);
         return DSP_OK;
     }
     case DSP_PLUGIN_FIR: {  // build-defined cfg 3b: Parameters{float taps[T]}
@@ -798,6 +841,7 @@ int dsp_render_stft(const float *const *in, uint32_t in_channels, uint64_t L,
         const float *win = nullptr;
         if ((st = get_tw(g.dev, &tw))) return st;
         if ((st = get_window(g.dev, window, N, N, &win, window_prescale(N)))) return st;
+        bool tail_in_kernel = false;
         for (uint32_t c0 = 0; c0 < C; c0 += kMaxChannels) {
             const uint32_t cn = (C - c0) < (uint32_t)kMaxChannels ? (C - c0) : kMaxChannels;
             Stft8kArgs A{};
@@ -822,6 +866,8 @@ int dsp_render_stft(const float *const *in, uint32_t in_channels, uint64_t L,
             if ((st = set_wincomp(g.dev, window, &A))) return st;
             A.map = map;
             A.goff = goff;
+            // the PER kernel also renders the tail no frame owns
+            if (g_stft_variant == 5 && stft8192_pk_per_path(A, true)) A.tail_end = Lr, tail_in_kernel = true;
             TimedLaunch tl{};
             if ((st = timing_begin(s, &tl))) return st;
             if ((st = launch_stft(A, cn, true, true, s))) return st;
@@ -830,12 +876,14 @@ int dsp_render_stft(const float *const *in, uint32_t in_channels, uint64_t L,
             const uint64_t hop_samples = (uint64_t)cn * F * H;
             uint64_t bytes = hop_samples * 4 + (uint64_t)cn * F * K * 4;
             if (map.kind != MapKind::Ramp) bytes += (uint64_t)A.in_ch * F * H * 4;
+            if (A.tail_end) bytes += (uint64_t)cn * (A.tail_end - F * (uint64_t)H) * 4;
             if ((st = timing_end(s, &tl, bytes))) return st;
         }
         // the render tail no frame owns: [F*H, Lr)
-        st = render_device(din.data(), in_channels, L, dout.data(), C, B, map, F * (uint64_t)H,
-                           goff, s);
-        if (st) return st;
+        if (!tail_in_kernel) {
+            st = render_device(din.data(), in_channels, L, dout.data(), C, B, map, F * (uint64_t)H, goff, s);
+            if (st) return st;
+        }
     }
     if (host_mode(ex)) {
         for (uint32_t c = 0; c < C; ++c) {

@@ -38,7 +38,17 @@ struct SampleMap {
     const void *gparams; // Generic: host Parameters blob
     uint32_t gparams_size;
     float sr;            // sample rate handed to the callback (Generic)
+    // Ramp: table[i] = (float)(gain - i step) in closed form when the host
+    // verified that IR_test's sequential f64 recurrence is exact for these
+    // parameters and this B (capi.cpp ramp_closed_form); the table is then
+    // only built for kernels that still read it
+    uint32_t closed;
+    double rg0, rs;
 };
+
+__device__ __forceinline__ float ramp_value(const SampleMap &m, uint32_t q) {
+    return (float)__fma_rn(-(double)q, m.rs, m.rg0);
+}
 
 __device__ __forceinline__ uint32_t block_pos(const SampleMap &m, uint64_t gi) {
     return m.b_mask ? (uint32_t)(gi & m.b_mask) : (uint32_t)(gi % m.B);
@@ -51,7 +61,7 @@ __device__ __forceinline__ float apply_map(const SampleMap &m, float base, uint6
     case MapKind::Gain:
         return base * m.a;  // single fp32 multiply: bit-exact vs gain_test
     case MapKind::Ramp:
-        return m.table[block_pos(m, gi)];
+        return m.closed ? ramp_value(m, block_pos(m, gi)) : m.table[block_pos(m, gi)];
     default:
         return base;
     }

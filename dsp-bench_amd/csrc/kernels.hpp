@@ -39,6 +39,7 @@ struct Stft8kArgs {
     uint64_t *stamps;    // diagnostic builds only (-DDSPB_STAMPS): per-frame phase clocks
     const float4 *wbase; // computed-window variants: (cos, sin) of theta (2 lane), theta (2 lane + 1)
     float wa, wb;        // window w = wa - wb cos(theta n), pre-scaled
+    uint64_t tail_end;   // > F H: waves F .. render [F H, tail_end) too (stft_pk PER path), else 0
 };
 
 struct GenericFftArgs {
@@ -95,6 +96,7 @@ int launch_wav_decode(const uint8_t *payload, uint32_t C, uint16_t bits, bool is
                       uint64_t frames, const ChanOut &out, bool out_aligned16, hipStream_t s);
 int launch_wav_encode(uint8_t *payload, uint32_t C, uint16_t bits, bool is_float, uint64_t frames,
                       const ChanOut &in, hipStream_t s);
+bool stft8192_pk_per_path(const Stft8kArgs &A, bool fused);
 int launch_stft8192_pk(const Stft8kArgs &A, uint32_t C, bool fused, int opt, hipStream_t s);
 int launch_fft_generic(const GenericFftArgs &A, uint64_t transforms, uint32_t C, hipStream_t s);
 int launch_gain(const float *in, float *out, float g, uint64_t n, hipStream_t s);

@@ -58,9 +58,30 @@ __global__ __launch_bounds__(256, 2) void stft8192_pk_kernel(Stft8kArgs A) {
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t ch = blockIdx.y;
     const uint64_t f = (uint64_t)xcd_remap(blockIdx.x, gridDim.x) * 4u + wave;
-    if (f >= A.F) return;  // whole wave leaves; nothing below waits on other waves
-    float *lds = lds_all[wave];
+    constexpr bool SOA = WINC && MK == MapKind::Ramp && PER > 0 && SRC == kSrcRender;
     const uint64_t fs = f * (uint64_t)A.H;
+    if (f >= A.F) {  // whole wave leaves; nothing below waits on other waves
+        if constexpr (SOA) {
+            // the render tail no frame owns, [F H, tail_end): H samples per wave
+            if (fs < A.tail_end) {
+                const uint32_t p0 = (uint32_t)(A.goff + fs) + 2u * lane;
+                float *o = A.out.p[ch] + fs;
+                const uint64_t n = A.tail_end - fs;
+#pragma unroll 4
+                for (uint32_t b = 0; 128u * b < A.H; ++b) {
+                    const uint32_t e = 128u * b + 2u * lane;  // even: tail_end is a multiple of B >= 2
+                    if (e < n) {
+                        const uint32_t q = (p0 + 128u * b) & A.map.b_mask;
+                        const v2f t = A.map.closed ? v2f{ramp_value(A.map, q), ramp_value(A.map, q + 1)}
+                                                   : v2f{A.map.table[q], A.map.table[q + 1]};
+                        reinterpret_cast<v2f *>(o + 128u * b)[lane] = t;
+                    }
+                }
+            }
+        }
+        return;
+    }
+    float *lds = lds_all[wave];
     const float *x = (ch < A.in_ch) ? A.in.p[ch] : nullptr;
 
     // ---- 0. constants, issued before the frame -----------------------------
@@ -91,18 +112,27 @@ __global__ __launch_bounds__(256, 2) void stft8192_pk_kernel(Stft8kArgs A) {
     // (for a frame in memory the 128 dword loads this needs cost more than
     // the shuffles they save: 0.75 vs 0.65 ms per stereo hour, so memory
     // frames keep the dwordx2 path below)
-    constexpr bool SOA = WINC && MK == MapKind::Ramp && PER > 0 && SRC == kSrcRender;
     if constexpr (SOA) {
         constexpr int NJ = PER >= 2 ? PER / 2 : 1;
         cx2 X[NJ];
         {
             const uint32_t p0 = (uint32_t)(A.goff + fs) + 2u * lane;
             const float *T = A.map.table;
+            if (A.map.closed) {  // table values in closed form (common.hpp ramp_value)
 #pragma unroll
-            for (int jj = 0; jj < NJ; ++jj) {
-                const uint32_t q0 = (p0 + 256u * jj) & A.map.b_mask;
-                const uint32_t q1 = (p0 + 256u * jj + (PER >= 2 ? 128u : 0u)) & A.map.b_mask;
-                X[jj] = cx2{v2f{T[q0], T[q1]}, v2f{T[q0 + 1], T[q1 + 1]}};
+                for (int jj = 0; jj < NJ; ++jj) {
+                    const uint32_t q0 = (p0 + 256u * jj) & A.map.b_mask;
+                    const uint32_t q1 = (p0 + 256u * jj + (PER >= 2 ? 128u : 0u)) & A.map.b_mask;
+                    X[jj] = cx2{v2f{ramp_value(A.map, q0), ramp_value(A.map, q1)},
+                                v2f{ramp_value(A.map, q0 + 1), ramp_value(A.map, q1 + 1)}};
+                }
+            } else {
+#pragma unroll
+                for (int jj = 0; jj < NJ; ++jj) {
+                    const uint32_t q0 = (p0 + 256u * jj) & A.map.b_mask;
+                    const uint32_t q1 = (p0 + 256u * jj + (PER >= 2 ? 128u : 0u)) & A.map.b_mask;
+                    X[jj] = cx2{v2f{T[q0], T[q1]}, v2f{T[q0 + 1], T[q1 + 1]}};
+                }
             }
             // the render output: sample pairs of column b repeat with period PER
             float *o = A.out.p[ch] + fs;
@@ -284,11 +314,24 @@ static void launch_pk_km(int km, dim3 grid, hipStream_t s, const Stft8kArgs &A) 
         hipLaunchKernelGGL((stft8192_pk_kernel<SRC, kKPartial, MK, POW2, WINC>), grid, dim3(256), 0, s, A);
 }
 
+// true when launch_stft8192_pk runs the PER kernel for these arguments --
+// the fused path that evaluates a closed-form IR ramp itself and renders the
+// tail past the last frame's hop (A.tail_end)
+bool stft8192_pk_per_path(const Stft8kArgs &A, bool fused) {
+    const int km = A.K == 4097u ? kKHalf : (A.K == 8192u ? kKMirror : kKPartial);
+    const bool pow2 = A.map.b_mask != 0 && A.map.B >= 2;
+    const bool winc = A.valid >= 8192u && A.wbase != nullptr && km == kKHalf;
+    return fused && A.map.kind == MapKind::Ramp && pow2 && winc && A.map.B <= 2048u;
+}
+
 // A.win2: the window pre-scaled by 0.5 / sqrt(8192); the computed window
 // (A.wbase, A.wa, A.wb) serves the full-frame 4097-bin shapes.
 int launch_stft8192_pk(const Stft8kArgs &A, uint32_t C, bool fused, int opt, hipStream_t stream) {
     if (A.F == 0 || C == 0) return DSP_OK;
-    const uint64_t groups = (A.F + 3) / 4;
+    // PER path: extra waves for the render tail [F H, tail_end)
+    const uint64_t tail = A.tail_end > A.F * A.H ? (A.tail_end - A.F * A.H + A.H - 1) / A.H : 0;
+    if (tail && !stft8192_pk_per_path(A, fused)) return DSP_ERR_INVALID;
+    const uint64_t groups = (A.F + tail + 3) / 4;
     if (groups > 0x7fffffffull) return DSP_ERR_INVALID;
     dim3 grid((uint32_t)groups, C);
     const int km = A.K == 4097u ? kKHalf : (A.K == 8192u ? kKMirror : kKPartial);

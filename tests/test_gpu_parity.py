@@ -326,3 +326,26 @@ def test_pk_store_options(torch_cuda, oracle, opt):
     finally:
         L.dsp_stft_kernel_variant(oldv)
         L.dsp_stft_soa_options(oldo)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("gain,step,B", [(0.9, 0.002, 512),    # recurrence exact: closed form
+                                         (0.9, 1e-10, 512),    # not exact: block table kernel
+                                         (0.9, 1e-10, 4),      # exact for 4 steps
+                                         (0.5, 1 / 3, 2048),
+                                         (-0.25, 3e-9, 256),   # not exact
+                                         (0.9, 0.002, 384)])   # non-pow2 B: table path
+def test_ir_ramp_closed_form_and_table(torch_cuda, oracle, gain, step, B):
+    """capi.cpp ramp_closed_form: IR_test's block table is evaluated in
+    closed form only when the sequential f64 recurrence is exact; either
+    way the render is bit-identical to the reference callback."""
+    n = 8192 * 3 + 1000
+    x = rnd((2, n), 64)
+    plug = d.Plugin.ir_test(gain, step)
+    ref = oracle.render_offline([x[0], x[1]], 2, B, 48000.0, oracle.restated_plugin("IR_test", [gain, step]))
+    out, mag = d.render_stft(to_dev(torch_cuda, x), 2, B, 48000.0, plug, window=d.DSP_WIN_HANN)
+    assert np.array_equal(out.cpu().numpy(), ref)
+    mref = oracle.np_stft_mag(ref[1], 8192, 4096, d.DSP_WIN_HANN, 4097)
+    assert peak_rel_err(mag.cpu().numpy()[1], mref) <= PEAK_REL_TOL
+    out2 = d.render_offline(to_dev(torch_cuda, x), 2, B, 48000.0, plug)
+    assert np.array_equal(out2.cpu().numpy(), ref)
