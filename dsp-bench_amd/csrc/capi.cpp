@@ -626,7 +626,7 @@ int dsp_fir_method(int m) {
 int dsp_stft_soa_options(int opt) {
     std::lock_guard<std::mutex> lk(g_mu);
     const int old = g_soa_opt;
-    if (opt >= 0 && opt <= 1023) g_soa_opt = opt;
+    if (opt >= 0 && opt <= 0xffff) g_soa_opt = opt;
     return old;
 }
 

@@ -106,9 +106,11 @@ __device__ __forceinline__ void combine64_dir(const cx2 (&a)[32], cx (&yp)[32], 
 // U[l + 64 q] = zp[q] (q < 32), zm[q - 32] -- forward: Z = DFT(u), inverse
 // (INV): the unnormalised inverse.  tlo[j] = W4096^(l j), thp[h] =
 // (W4096^(8 l h), W4096^(8 l (h + 4))); lds = this wave's 64 x 65 tile.
-template <bool INV, bool BAR_DFT = true, bool BAR_TW = true>
-__device__ __forceinline__ void fft4096_pk(cx2 (&P)[32], float *lds, const cx (&tlo)[8], const cx2 (&thp)[4],
-                                           uint32_t lane, cx (&zp)[32], cx (&zm)[32]) {
+// Everything up to the last combine: R holds the second DFT64's even/odd
+// DFT32 halves (combine64p / combine64_dir finish it).
+template <bool INV, bool BAR_DFT, bool BAR_TW>
+__device__ __forceinline__ void fft4096_pk_front(cx2 (&P)[32], float *lds, const cx (&tlo)[8], const cx2 (&thp)[4],
+                                                 uint32_t lane, cx2 (&R)[32]) {
     // DFT64 over the register index: even/odd DFT32 in the halves, combine
     x2dft32_dir<BAR_DFT, INV>(P);
     cx2 Q[32];  // Q[k] = (Y[k], Y[k+32]) * (W4096^(+-l k), W4096^(+-l (k+32)))
@@ -124,7 +126,7 @@ __device__ __forceinline__ void fft4096_pk(cx2 (&P)[32], float *lds, const cx (&
         }
     }
     // transpose through LDS: row l, column kb -> column l, row a
-    cx2 R[32];  // R[j] = (t[2j], t[2j+1]), t[a] = row a of column l
+    // R[j] = (t[2j], t[2j+1]), t[a] = row a of column l
 #pragma unroll
     for (int k = 0; k < 32; ++k) {
         lds[lane * 65u + k] = Q[k].r.x;
@@ -142,9 +144,27 @@ __device__ __forceinline__ void fft4096_pk(cx2 (&P)[32], float *lds, const cx (&
     lds_fence();
 #pragma unroll
     for (int j = 0; j < 32; ++j) R[j].i = v2f{lds[(2 * j) * 65 + lane], lds[(2 * j + 1) * 65 + lane]};
-    // DFT64 over the other index
+    // DFT64 over the other index (its combine is the caller's)
     x2dft32_dir<BAR_DFT, INV>(R);
+}
+
+template <bool INV, bool BAR_DFT = true, bool BAR_TW = true>
+__device__ __forceinline__ void fft4096_pk(cx2 (&P)[32], float *lds, const cx (&tlo)[8], const cx2 (&thp)[4],
+                                           uint32_t lane, cx (&zp)[32], cx (&zm)[32]) {
+    cx2 R[32];
+    fft4096_pk_front<INV, BAR_DFT, BAR_TW>(P, lds, tlo, thp, lane, R);
     combine64_dir<INV>(R, zp, zm);
+}
+
+// The same transform with a packed last combine: Y2[q] = (U[l + 64 q],
+// U[l + 64 (q + 32)]) in the halves of one cx2 (forward only) -- 6 packed
+// instructions per pair instead of 8 scalar ones.
+template <bool BAR_DFT = true, bool BAR_TW = true>
+__device__ __forceinline__ void fft4096_pk_y2(cx2 (&P)[32], float *lds, const cx (&tlo)[8], const cx2 (&thp)[4],
+                                              uint32_t lane, cx2 (&Y2)[32]) {
+    cx2 R[32];
+    fft4096_pk_front<false, BAR_DFT, BAR_TW>(P, lds, tlo, thp, lane, R);
+    combine64p(R, Y2);
 }
 
 }  // namespace dspb

@@ -29,8 +29,13 @@ namespace dspb {
 // once and never read back; 2% faster at the headline shape), 16 =
 // non-temporal magnitude stores (slower: 256-byte row pieces need the L2 to
 // merge them), 32 = 4097-bin rows staged through LDS and stored as 16-byte
-// segments (no gain)
-enum { kPkNoBarDft = 1, kPkNoBarTw = 2, kPkNoBarSplit = 4, kPkRenderCached = 8, kPkNtMag = 16, kPkMagLds = 32 };
+// segments (no gain; implies 64), 64 = the older scalar last combine and
+// (ka, ka + 16) split (default: the packed combine + split_y2, 60 VALU
+// fewer per frame, the same bits)
+enum { kPkNoBarDft = 1, kPkNoBarTw = 2, kPkNoBarSplit = 4, kPkRenderCached = 8, kPkNtMag = 16, kPkMagLds = 32,
+       kPkOldSplit = 64, kPkAbNoRender = 128, kPkAbNoMag = 256 };
+// 128 / 256: ablation only (A/B of what the stores cost): skip the render
+// stores / the magnitude stores of split_y2 (results discarded)
 constexpr int kPkDefaultOpt = 0;
 
 typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));  // a row is only dword-aligned
@@ -45,6 +50,89 @@ template <bool NT>
 __device__ __forceinline__ void st4u(float *p, f4u v) {  // p: dword-aligned
     if constexpr (NT) __builtin_nontemporal_store(v, reinterpret_cast<f4u *>(p));
     else *reinterpret_cast<f4u *>(p) = v;
+}
+
+template <int KM>
+__device__ __forceinline__ void put_bin(float *mrow, uint32_t K, uint32_t k, float m) {
+    if constexpr (KM == kKPartial) {
+        if (k < K) mrow[k] = m;
+    } else {
+        mrow[k] = m;
+        if constexpr (KM == kKMirror) mrow[(8192u - k) & 8191u] = m;  // k = 0: itself
+    }
+}
+
+// Real split and |X| from the packed last combine (fft4096_pk_y2):
+// Y2[q] = (Z[l + 64 q], Z[l + 64 (q + 32)]), q < 32, Z = the 4096-point FFT
+// of z[m] = x[2m] + i x[2m+1] (window pre-scaled by 0.5/sqrt N).
+//   X[k] = E + T, X[M - k] = conj(E - T), E = Z[k] + conj Z[M - k],
+//   T = W8192^k (-i)(Z[k] - conj Z[M - k]), M = 4096.
+// Iteration q < 16 takes k = l + 64 q and k + 2048 in the two halves; the
+// twiddle of the upper half is -i times the lower one, so one complex
+// W8192^(l + 64 q) serves both.  The partners Z[M - k], Z[M - k - 2048]
+// are the two halves of Y2[31 - q], swapped, on lane 64 - l (lane 0: its
+// own Y2[32 - q], or Y2[0] unswapped at q = 0, which pairs bin 0 with 4096
+// and bin 2048 with itself).  Bins 1024 / 3072 (lane 0, Y2[16]) are left
+// over and done at the end.  Bins per iteration: l + 64 q, 2048 + l + 64 q,
+// 4096 - l - 64 q, 2048 - l - 64 q.
+template <int KM, bool BAR, bool NOSTORE = false>
+__device__ __forceinline__ void split_y2(const cx2 (&Y2)[32], float *mrow, uint32_t K, const v2f *tw,
+                                         uint32_t lane) {
+    float acc = 0.f;  // NOSTORE: keeps the magnitudes live
+    const uint32_t src = ((64u - lane) & 63u) * 4u;
+    const bool l0 = lane == 0;
+    const v2f wl = tw[lane];  // W8192^l
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        if (BAR) __builtin_amdgcn_sched_barrier(0);
+        const cx2 a = Y2[q == 0 ? 0 : 32 - q], b = Y2[31 - q];
+        // what this lane sends to lane 64 - l (select on values: keeps Y2 in VGPRs)
+        const float sxr = l0 ? (q == 0 ? a.r.x : a.r.y) : b.r.y;
+        const float sxi = l0 ? (q == 0 ? a.i.x : a.i.y) : b.i.y;
+        const float syr = l0 ? (q == 0 ? a.r.y : a.r.x) : b.r.x;
+        const float syi = l0 ? (q == 0 ? a.i.y : a.i.x) : b.i.x;
+        const cx2 Pp = cx2{v2f{bperm(src, sxr), bperm(src, syr)}, v2f{bperm(src, sxi), bperm(src, syi)}};
+        const cx2 Z = Y2[q];
+        const cx2 E = cx2{Z.r + Pp.r, Z.i - Pp.i};
+        const cx2 D = cx2{Z.r - Pp.r, Z.i + Pp.i};
+        // u = W8192^(l + 64 q); T = (-i D.x u, -i D.y (-i u)) with U1 = u, U2 = (u.i, -u.r)
+        v2f u = wl;
+        if (q) u = v2f{wl.x, wl.x} * v2f{kW128_re[q], kW128_im[q]} + v2f{wl.y, wl.y} * v2f{-kW128_im[q], kW128_re[q]};
+        const v2f U2 = v2f{u.y, -u.x};
+        const cx2 T = cx2{D.i * u + D.r * U2, D.i * U2 - D.r * u};
+        const cx2 X1 = E + T;  // 2 X[k], k = l + 64 q (+ 2048)
+        const cx2 X2 = E - T;  // 2 conj X[M - k]
+        const v2f q1 = X1.r * X1.r + X1.i * X1.i;
+        const v2f q2 = X2.r * X2.r + X2.i * X2.i;
+        const uint32_t k = lane + 64u * (uint32_t)q;
+        if constexpr (NOSTORE) {
+            acc += __builtin_amdgcn_sqrtf(q1.x) + __builtin_amdgcn_sqrtf(q1.y) + __builtin_amdgcn_sqrtf(q2.x) +
+                   __builtin_amdgcn_sqrtf(q2.y);
+        } else if constexpr (KM == kKHalf) {  // four lane-based row pointers, constant offsets
+            (mrow + lane)[64 * q] = __builtin_amdgcn_sqrtf(q1.x);
+            (mrow + 2048u + lane)[64 * q] = __builtin_amdgcn_sqrtf(q1.y);
+            (mrow + 4096u - lane)[-64 * q] = __builtin_amdgcn_sqrtf(q2.x);
+            (mrow + 2048u - lane)[-64 * q] = __builtin_amdgcn_sqrtf(q2.y);
+        } else {
+            put_bin<KM>(mrow, K, k, __builtin_amdgcn_sqrtf(q1.x));
+            put_bin<KM>(mrow, K, 2048u + k, __builtin_amdgcn_sqrtf(q1.y));
+            put_bin<KM>(mrow, K, 4096u - k, __builtin_amdgcn_sqrtf(q2.x));
+            put_bin<KM>(mrow, K, 2048u - k, __builtin_amdgcn_sqrtf(q2.y));
+        }
+    }
+    if constexpr (NOSTORE) {
+        if (acc == -1.f) mrow[lane] = acc;  // never true: |X| >= 0
+        return;
+    }
+    if (l0) {  // bins 1024 and 3072: Z[1024] = Y2[16].x, Z[3072] = Y2[16].y
+        const cx z1 = cx{Y2[16].r.x, Y2[16].i.x}, z2 = cx{Y2[16].r.y, Y2[16].i.y};
+        const cx E = cx{z1.r + z2.r, z1.i - z2.i}, D = cx{z1.r - z2.r, z1.i + z2.i};
+        const float c = 0x1.6a09e6p-1f;  // W8192^1024 = (c, -c)
+        const cx T = cx{c * (D.i - D.r), -c * (D.i + D.r)};
+        const cx X1 = E + T, X2 = E - T;
+        put_bin<KM>(mrow, K, 1024u, __builtin_amdgcn_sqrtf(__builtin_fmaf(X1.r, X1.r, X1.i * X1.i)));
+        put_bin<KM>(mrow, K, 3072u, __builtin_amdgcn_sqrtf(__builtin_fmaf(X2.r, X2.r, X2.i * X2.i)));
+    }
 }
 
 // PER (Ramp, pow2 B <= 4096): the frame's sample pairs repeat every PER
@@ -141,7 +229,8 @@ __global__ __launch_bounds__(256, 2) void stft8192_pk_kernel(Stft8kArgs A) {
             for (int b = 0; b < (PER >= 2 ? PER : 1); ++b)
                 st[b] = v2f{X[b / 2].r[b & 1], X[b / 2].i[b & 1]};
             constexpr bool NT = !(OPT & kPkRenderCached);
-            if (A.H == 4096u) {  // the headline hop: 32 columns, no per-store branch
+            if (OPT & kPkAbNoRender) {
+            } else if (A.H == 4096u) {  // the headline hop: 32 columns, no per-store branch
 #pragma unroll
                 for (int b = 0; b < 32; ++b)
                     dspb::st<NT>(reinterpret_cast<v2f *>(o + 128u * (uint32_t)b) + lane, st[b % (PER >= 2 ? PER : 1)]);
@@ -225,6 +314,15 @@ __global__ __launch_bounds__(256, 2) void stft8192_pk_kernel(Stft8kArgs A) {
         }
     }
     }  // !SOA
+
+    if constexpr (!(OPT & (kPkOldSplit | kPkMagLds))) {
+        // ---- 3-5. 4096-point FFT with a packed last combine:
+        // Y2[q] = (Z[l + 64 q], Z[l + 64 (q + 32)])
+        cx2 Y2[32];
+        fft4096_pk_y2<!(OPT & kPkNoBarDft), !(OPT & kPkNoBarTw)>(P, lds, tlo, thp, lane, Y2);
+        split_y2<KM, !(OPT & kPkNoBarSplit), (OPT & kPkAbNoMag) != 0>(Y2, A.mag.p[ch] + f * A.ld, A.K, A.tw, lane);
+        return;
+    }
 
     // ---- 3-5. 4096-point complex FFT of the packed frame (fft_pk.hpp):
     // Z[l + 64 ka] = zp[ka] (ka < 32), zm[ka - 32]
@@ -352,15 +450,25 @@ int launch_stft8192_pk(const Stft8kArgs &A, uint32_t C, bool fused, int opt, hip
     hipLaunchKernelGGL((stft8192_pk_kernel<kSrcRender, kKHalf, MapKind::Ramp, true, true, p, o>), grid, dim3(256), \
                        0, stream, A)
                 // A/B of the store kinds at the headline shape (B = 512)
-                if (per == 4 && (opt & (kPkRenderCached | kPkNtMag | kPkMagLds))) {
-                    switch (opt & (kPkRenderCached | kPkNtMag | kPkMagLds)) {
-                    case kPkRenderCached: DSPB_PK_PER_OPT(4, kPkRenderCached); break;
-                    case kPkNtMag: DSPB_PK_PER_OPT(4, kPkNtMag); break;
-                    case kPkRenderCached | kPkNtMag: DSPB_PK_PER_OPT(4, kPkRenderCached | kPkNtMag); break;
-                    case kPkMagLds: DSPB_PK_PER_OPT(4, kPkMagLds); break;
-                    case kPkMagLds | kPkRenderCached: DSPB_PK_PER_OPT(4, kPkMagLds | kPkRenderCached); break;
-                    case kPkMagLds | kPkNtMag: DSPB_PK_PER_OPT(4, kPkMagLds | kPkNtMag); break;
-                    default: DSPB_PK_PER_OPT(4, kPkMagLds | kPkRenderCached | kPkNtMag); break;
+                // A/B and ablation bits at the headline shape (B = 512)
+                if (per == 4 && (opt & ~(kPkNoBarDft | kPkNoBarTw | kPkNoBarSplit))) {
+                    switch (opt & ~(kPkNoBarDft | kPkNoBarTw | kPkNoBarSplit)) {
+#define DSPB_PK_CASE(o) \
+    case (o): DSPB_PK_PER_OPT(4, (o)); break
+                    DSPB_PK_CASE(kPkRenderCached);
+                    DSPB_PK_CASE(kPkOldSplit);
+                    DSPB_PK_CASE(kPkOldSplit | kPkRenderCached);
+                    DSPB_PK_CASE(kPkOldSplit | kPkNtMag);
+                    DSPB_PK_CASE(kPkOldSplit | kPkRenderCached | kPkNtMag);
+                    DSPB_PK_CASE(kPkMagLds);
+                    DSPB_PK_CASE(kPkMagLds | kPkRenderCached);
+                    DSPB_PK_CASE(kPkMagLds | kPkNtMag);
+                    DSPB_PK_CASE(kPkMagLds | kPkRenderCached | kPkNtMag);
+                    DSPB_PK_CASE(kPkAbNoRender);
+                    DSPB_PK_CASE(kPkAbNoMag);
+                    DSPB_PK_CASE(kPkAbNoRender | kPkAbNoMag);
+#undef DSPB_PK_CASE
+                    default: return DSP_ERR_INVALID;
                     }
                     break;
                 }

@@ -183,9 +183,10 @@ int dsp_stft_kernel_variant(int variant);
  * 8 = stage the IR_RAMP block table through LDS.  Bits 4..8 (options >> 4)
  * are variant 5's: 1/2/4 = no scheduling barriers in the DFTs / twiddle
  * loop / split loop, 8 = cached render stores (default non-temporal), 16 =
- * non-temporal magnitude stores, 32 =
- * magnitude rows staged through LDS (B = 512 shape).  Default 14.  Values
- * outside 0..1023 only query.  Returns the
+ * non-temporal magnitude stores (with 64), 32 = magnitude rows staged
+ * through LDS, 64 = the older scalar last combine and split, 128 / 256 =
+ * ablation: skip the render / magnitude stores (results discarded) (B = 512
+ * shape).  Default 14.  Values outside 0..0xffff only query.  Returns the
  * previous options. */
 int dsp_stft_soa_options(int options);
 

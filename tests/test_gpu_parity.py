@@ -302,11 +302,13 @@ def test_pk_ramp_table_periods(torch_cuda, oracle, B):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("opt", [0, 8, 16, 24, 32, 40, 48, 56])
+@pytest.mark.parametrize("opt", [0, 8, 32, 40, 48, 56, 64, 72, 80, 88])
 def test_pk_store_options(torch_cuda, oracle, opt):
-    """Packed kernel store A/B bits (dsp_stft_soa_options >> 4: 8/16
-    non-temporal render/magnitude stores, 32 rows staged through LDS):
-    the same bits as the default path, rows of any alignment (ld = K)."""
+    """Packed kernel A/B bits (dsp_stft_soa_options >> 4: 8 cached render
+    stores, 16 non-temporal magnitude stores, 32 rows staged through LDS, 64
+    the older scalar last combine and (ka, ka + 16) split): the same bits as
+    the default path (packed combine + split_y2; within 1e-7 of its peak for
+    64), rows of any alignment (ld = K)."""
     L = d.lib()
     oldv, oldo = L.dsp_stft_kernel_variant(5), L.dsp_stft_soa_options(14 | (opt << 4))
     try:
@@ -318,11 +320,15 @@ def test_pk_store_options(torch_cuda, oracle, opt):
         out0, mag0 = d.render_stft(to_dev(torch_cuda, x), 2, 512, 48000.0, d.Plugin.ir_test(0.9, 0.002),
                                    window=d.DSP_WIN_HANN)
         assert np.array_equal(out.cpu().numpy(), out0.cpu().numpy())
-        assert np.array_equal(mag.cpu().numpy(), mag0.cpu().numpy())
+        if opt & 64:  # the other split's operation order: the last bit may differ
+            assert peak_rel_err(mag.cpu().numpy()[0], mag0.cpu().numpy()[0]) <= 1e-7
+        else:
+            assert np.array_equal(mag.cpu().numpy(), mag0.cpu().numpy())
         ref = oracle.render_offline([x[0], x[1]], 2, 512, 48000.0, oracle.restated_plugin("IR_test", [0.9, 0.002]))
         assert np.array_equal(out.cpu().numpy(), ref)
-        mref = oracle.np_stft_mag(ref[0], 8192, 4096, d.DSP_WIN_HANN, 4097)
-        assert peak_rel_err(mag.cpu().numpy()[0], mref) <= PEAK_REL_TOL
+        for c in range(2):
+            mref = oracle.np_stft_mag(ref[c], 8192, 4096, d.DSP_WIN_HANN, 4097)
+            assert peak_rel_err(mag.cpu().numpy()[c], mref) <= PEAK_REL_TOL
     finally:
         L.dsp_stft_kernel_variant(oldv)
         L.dsp_stft_soa_options(oldo)

@@ -1,0 +1,60 @@
+"""Clock / power of the headline kernel per option bit set: each option runs
+back to back for ~2.5 s while rocm-smi samples sclk and socket power twice
+(read-only queries).  Tells a power-capped kernel (lower sclk) from a
+stalled one.
+
+    python tools/clock_probe.py OPT [OPT ...]   (stft_pk.hip kPk* bits)
+"""
+import os
+import re
+import statistics
+import subprocess
+import sys
+import threading
+import time
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "dsp-bench_amd"))
+import dspbench as d  # noqa: E402
+
+L_ = 48_000 * 3600
+x = torch.zeros((2, L_), device="cuda")
+nb = d.num_blocks(L_, 512)
+F = d.stft_frames(nb * 512, 8192, 4096)
+out = torch.empty((2, nb * 512), device="cuda")
+mag = torch.empty((2, F, 4097), device="cuda")
+lib = d.lib()
+
+
+def smi(samples):
+    for delay in (1.0, 0.7):
+        time.sleep(delay)
+        r = subprocess.run(["rocm-smi", "--showclocks", "--showpower"], capture_output=True, text=True)
+        samples.append(r.stdout)
+
+
+for o in [int(a) for a in sys.argv[1:]] or [64]:
+    lib.dsp_stft_soa_options(o << 4)
+    samples = []
+    th = threading.Thread(target=smi, args=(samples,))
+    t0 = time.time()
+    th.start()
+    n = 0
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    ts = []
+    while time.time() - t0 < 2.5:
+        e0.record()
+        for _ in range(20):
+            d.render_stft(x, 2, 512, 48000.0, d.Plugin.ir_test(), out=out, mag=mag)
+        e1.record()
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1) / 20)
+        n += 20
+    th.join()
+    sclk = [m for s in samples for m in re.findall(r"sclk.*?\((\d+)Mhz\)", s)]
+    pw = [m for s in samples for m in re.findall(r"Socket Graphics Package Power \(W\): ([\d.]+)", s)]
+    print(f"opt {o:4d}: {n} launches, {statistics.median(ts[2:]):.4f} ms/launch settled, sclk {sclk} MHz, "
+          f"power {pw} W", flush=True)
+lib.dsp_stft_soa_options(14)
