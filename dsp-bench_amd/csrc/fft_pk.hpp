@@ -167,4 +167,86 @@ __device__ __forceinline__ void fft4096_pk_y2(cx2 (&P)[32], float *lds, const cx
     combine64p(R, Y2);
 }
 
+// Low-footprint forward transform for 3 waves per SIMD.  The stage
+// twiddles are loaded after the first DFT32s (tw = get_tw's table: T8192,
+// then the lane-major rows) instead of living in 30 VGPRs from the kernel's
+// start, and the transpose goes through a 64 x 33 tile (8.4 KB) in four
+// passes of 32 floats per lane, so no pass holds more than 128 VGPRs of
+// frame and 12 waves per CU fit in the LDS:
+//   pass x: every lane writes its row's columns 0..31 (the .x halves);
+//           lane d reads column d & 31, rows 32 (d >= 32) + a, a < 32 -> X[a]
+//   pass y: the same with columns 32..63 (.y halves) -> Y[a]
+//   then v_permlane32_swap(X[a], Y[a]) trades the upper lanes' X for the
+//   lower lanes' Y: every lane holds its own column, rows 0..31 in X and
+//   rows 32..63 in Y (32 swaps per component).
+// Output as fft4096_pk_y2.
+template <bool BAR_DFT = true>
+__device__ __forceinline__ void fft4096_pk_y2_lo(cx2 (&P)[32], float *lds, const v2f *tw, uint32_t lane,
+                                                 cx2 (&Y2)[32]) {
+    x2dft32_dir<BAR_DFT, false>(P);
+    cx2 Q[32];
+    {
+        cx tlo[8];
+#pragma unroll
+        for (int j = 1; j < 8; ++j) {
+            const v2f a = (tw + 8192u + 64u * (uint32_t)(j - 1))[lane];
+            tlo[j] = cx{a.x, a.y};
+        }
+        const float4 *tp4 = reinterpret_cast<const float4 *>(tw + 8192u + 896u);
+        cx2 Y[32];
+        combine64p(P, Y);
+#pragma unroll
+        for (int hi = 0; hi < 4; ++hi) {
+            const float4 t = tp4[64u * (uint32_t)hi + lane];
+            const cx2 th = cx2{v2f{t.x, t.y}, v2f{t.z, t.w}};
+#pragma unroll
+            for (int lo = 0; lo < 8; ++lo) {
+                __builtin_amdgcn_sched_barrier(0);
+                const int k = lo + 8 * hi;
+                const cx2 w = lo ? cmulb(tlo[lo], th) : th;
+                Q[k] = cmul2(Y[k], w);
+            }
+        }
+    }
+    cx2 R[32];
+    const uint32_t wrow = lane * 33u;                           // this lane's row
+    const uint32_t rcol = (lane & 32u) * 33u + (lane & 31u);    // rows 32 (d >= 32) + a, column d & 31
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+        float X[32], Yv[32];
+#pragma unroll
+        for (int k = 0; k < 32; ++k) lds[wrow + k] = c ? Q[k].i.x : Q[k].r.x;
+        lds_fence();
+#pragma unroll
+        for (int a = 0; a < 32; ++a) X[a] = lds[rcol + 33u * a];
+        lds_fence();
+#pragma unroll
+        for (int k = 0; k < 32; ++k) lds[wrow + k] = c ? Q[k].i.y : Q[k].r.y;
+        lds_fence();
+#pragma unroll
+        for (int a = 0; a < 32; ++a) Yv[a] = lds[rcol + 33u * a];
+        lds_fence();
+#pragma unroll
+        for (int a = 0; a < 32; ++a) {
+            const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(X[a]), __float_as_uint(Yv[a]), false,
+                                                            false);
+            X[a] = __uint_as_float(r[0]);
+            Yv[a] = __uint_as_float(r[1]);
+        }
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const v2f lo2 = v2f{X[2 * j], X[2 * j + 1]}, hi2 = v2f{Yv[2 * j], Yv[2 * j + 1]};
+            if (c) {
+                R[j].i = lo2;
+                R[16 + j].i = hi2;
+            } else {
+                R[j].r = lo2;
+                R[16 + j].r = hi2;
+            }
+        }
+    }
+    x2dft32_dir<BAR_DFT, false>(R);
+    combine64p(R, Y2);
+}
+
 }  // namespace dspb

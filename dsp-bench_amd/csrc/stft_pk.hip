@@ -33,7 +33,11 @@ namespace dspb {
 // (ka, ka + 16) split (default: the packed combine + split_y2, 60 VALU
 // fewer per frame, the same bits)
 enum { kPkNoBarDft = 1, kPkNoBarTw = 2, kPkNoBarSplit = 4, kPkRenderCached = 8, kPkNtMag = 16, kPkMagLds = 32,
-       kPkOldSplit = 64, kPkAbNoRender = 128, kPkAbNoMag = 256 };
+       kPkOldSplit = 64, kPkAbNoRender = 128, kPkAbNoMag = 256, kPkMagStage = 512, kPkOcc3 = 1024 };
+// 1024 = 3 waves per SIMD (OCC template argument): fft4096_pk_y2_lo's
+// 64 x 33 transpose tile and just-in-time stage twiddles
+// 512 = split_y2 stages the row in LDS at the row's 16-byte phase and stores
+// it as aligned 16-byte pieces (16 dwordx4 + <= 7 dwords instead of 65 dwords)
 // 128 / 256: ablation only (A/B of what the stores cost): skip the render
 // stores / the magnitude stores of split_y2 (results discarded)
 constexpr int kPkDefaultOpt = 0;
@@ -75,10 +79,15 @@ __device__ __forceinline__ void put_bin(float *mrow, uint32_t K, uint32_t k, flo
 // and bin 2048 with itself).  Bins 1024 / 3072 (lane 0, Y2[16]) are left
 // over and done at the end.  Bins per iteration: l + 64 q, 2048 + l + 64 q,
 // 4096 - l - 64 q, 2048 - l - 64 q.
-template <int KM, bool BAR, bool NOSTORE = false>
+template <int KM, bool BAR, bool NOSTORE = false, bool STAGE = false>
 __device__ __forceinline__ void split_y2(const cx2 (&Y2)[32], float *mrow, uint32_t K, const v2f *tw,
-                                         uint32_t lane) {
+                                         uint32_t lane, float *lds) {
+    static_assert(!STAGE || KM == kKHalf, "staged rows: 4097 bins");
     float acc = 0.f;  // NOSTORE: keeps the magnitudes live
+    // STAGE: bin k goes to lds[k + a], a = the row's dword phase mod 4, so
+    // LDS float4 j is the 16-byte-aligned global piece at bins [4j - a, 4j - a + 4)
+    const uint32_t a = (uint32_t)(reinterpret_cast<uintptr_t>(mrow) >> 2) & 3u;
+    float *sl = lds + a;
     const uint32_t src = ((64u - lane) & 63u) * 4u;
     const bool l0 = lane == 0;
     const v2f wl = tw[lane];  // W8192^l
@@ -108,6 +117,11 @@ __device__ __forceinline__ void split_y2(const cx2 (&Y2)[32], float *mrow, uint3
         if constexpr (NOSTORE) {
             acc += __builtin_amdgcn_sqrtf(q1.x) + __builtin_amdgcn_sqrtf(q1.y) + __builtin_amdgcn_sqrtf(q2.x) +
                    __builtin_amdgcn_sqrtf(q2.y);
+        } else if constexpr (STAGE) {
+            (sl + lane)[64 * q] = __builtin_amdgcn_sqrtf(q1.x);
+            (sl + 2048u + lane)[64 * q] = __builtin_amdgcn_sqrtf(q1.y);
+            (sl + 4096u - lane)[-64 * q] = __builtin_amdgcn_sqrtf(q2.x);
+            (sl + 2048u - lane)[-64 * q] = __builtin_amdgcn_sqrtf(q2.y);
         } else if constexpr (KM == kKHalf) {  // four lane-based row pointers, constant offsets
             (mrow + lane)[64 * q] = __builtin_amdgcn_sqrtf(q1.x);
             (mrow + 2048u + lane)[64 * q] = __builtin_amdgcn_sqrtf(q1.y);
@@ -130,8 +144,31 @@ __device__ __forceinline__ void split_y2(const cx2 (&Y2)[32], float *mrow, uint3
         const float c = 0x1.6a09e6p-1f;  // W8192^1024 = (c, -c)
         const cx T = cx{c * (D.i - D.r), -c * (D.i + D.r)};
         const cx X1 = E + T, X2 = E - T;
-        put_bin<KM>(mrow, K, 1024u, __builtin_amdgcn_sqrtf(__builtin_fmaf(X1.r, X1.r, X1.i * X1.i)));
-        put_bin<KM>(mrow, K, 3072u, __builtin_amdgcn_sqrtf(__builtin_fmaf(X2.r, X2.r, X2.i * X2.i)));
+        const float m1 = __builtin_amdgcn_sqrtf(__builtin_fmaf(X1.r, X1.r, X1.i * X1.i));
+        const float m2 = __builtin_amdgcn_sqrtf(__builtin_fmaf(X2.r, X2.r, X2.i * X2.i));
+        if constexpr (STAGE) {
+            sl[1024] = m1;
+            sl[3072] = m2;
+        } else {
+            put_bin<KM>(mrow, K, 1024u, m1);
+            put_bin<KM>(mrow, K, 3072u, m2);
+        }
+    }
+    if constexpr (STAGE) {
+        lds_fence();
+        // aligned pieces j in [j0, j1]: bins [4j - a, 4j - a + 4) inside [0, 4097)
+        const uint32_t j0 = a ? 1u : 0u, j1 = (4093u + a) >> 2;
+        float *gb = mrow - a;  // 16-byte aligned
+#pragma unroll
+        for (int it = 0; it < 16; ++it) {
+            const uint32_t j = j0 + 64u * (uint32_t)it + lane;
+            if (it < 15 || j <= j1)
+                *reinterpret_cast<float4 *>(gb + 4u * j) = reinterpret_cast<const float4 *>(lds)[j];
+        }
+        // head bins [0, 4 j0 - a) and tail bins [4 j1 + 4 - a, 4097): at most 3 + 4
+        const uint32_t head = 4u * j0 - a, tail0 = 4u * j1 + 4u - a;
+        if (lane < head) mrow[lane] = sl[lane];
+        if (lane >= 8u && tail0 + (lane - 8u) < 4097u) mrow[tail0 + lane - 8u] = sl[tail0 + lane - 8u];
     }
 }
 
@@ -139,9 +176,9 @@ __device__ __forceinline__ void split_y2(const cx2 (&Y2)[32], float *mrow, uint3
 // values of b (PER = max(1, B / 128)), so only v[0 .. PER) are fetched from
 // the block table -- 4 gathers at B = 512 -- and v[b] = v[b mod PER] is a
 // register alias.  PER = 0: generic path.
-template <int SRC, int KM, MapKind MK, bool POW2, bool WINC, int PER = 0, int OPT = kPkDefaultOpt>
-__global__ __launch_bounds__(256, 2) void stft8192_pk_kernel(Stft8kArgs A) {
-    __shared__ __attribute__((aligned(16))) float lds_all[4][64 * 65];
+template <int SRC, int KM, MapKind MK, bool POW2, bool WINC, int PER = 0, int OPT = kPkDefaultOpt, int OCC = 2>
+__global__ __launch_bounds__(256, OCC) void stft8192_pk_kernel(Stft8kArgs A) {
+    __shared__ __attribute__((aligned(16))) float lds_all[4][OCC >= 3 ? 64 * 33 : 64 * 65];
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t ch = blockIdx.y;
@@ -175,18 +212,22 @@ __global__ __launch_bounds__(256, 2) void stft8192_pk_kernel(Stft8kArgs A) {
     // ---- 0. constants, issued before the frame -----------------------------
     // tlo[j] = W4096^(l j), thp[h] = (W4096^(8 l h), W4096^(8 l (h + 4)))
     // (capi.cpp get_tw: lane-major rows after T8192)
+    static_assert(OCC == 2 || (SOA && !(OPT & (kPkOldSplit | kPkMagLds | kPkMagStage))),
+                  "3 waves per SIMD: the PER path with split_y2");
     cx tlo[8];
-#pragma unroll
-    for (int j = 1; j < 8; ++j) {
-        const v2f a = (A.tw + 8192u + 64u * (uint32_t)(j - 1))[lane];
-        tlo[j] = cx{a.x, a.y};
-    }
     cx2 thp[4];
-    const float4 *tp4 = reinterpret_cast<const float4 *>(A.tw + 8192u + 896u);
+    if constexpr (OCC == 2) {  // (OCC 3 loads them inside fft4096_pk_y2_lo)
 #pragma unroll
-    for (int h = 0; h < 4; ++h) {
-        const float4 t = tp4[64u * (uint32_t)h + lane];
-        thp[h] = cx2{v2f{t.x, t.y}, v2f{t.z, t.w}};
+        for (int j = 1; j < 8; ++j) {
+            const v2f a = (A.tw + 8192u + 64u * (uint32_t)(j - 1))[lane];
+            tlo[j] = cx{a.x, a.y};
+        }
+        const float4 *tp4 = reinterpret_cast<const float4 *>(A.tw + 8192u + 896u);
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+            const float4 t = tp4[64u * (uint32_t)h + lane];
+            thp[h] = cx2{v2f{t.x, t.y}, v2f{t.z, t.w}};
+        }
     }
     float4 wbase = float4{0.f, 0.f, 0.f, 0.f};
     if constexpr (WINC) wbase = A.wbase[lane];
@@ -319,8 +360,10 @@ __global__ __launch_bounds__(256, 2) void stft8192_pk_kernel(Stft8kArgs A) {
         // ---- 3-5. 4096-point FFT with a packed last combine:
         // Y2[q] = (Z[l + 64 q], Z[l + 64 (q + 32)])
         cx2 Y2[32];
-        fft4096_pk_y2<!(OPT & kPkNoBarDft), !(OPT & kPkNoBarTw)>(P, lds, tlo, thp, lane, Y2);
-        split_y2<KM, !(OPT & kPkNoBarSplit), (OPT & kPkAbNoMag) != 0>(Y2, A.mag.p[ch] + f * A.ld, A.K, A.tw, lane);
+        if constexpr (OCC >= 3) fft4096_pk_y2_lo<!(OPT & kPkNoBarDft)>(P, lds, A.tw, lane, Y2);
+        else fft4096_pk_y2<!(OPT & kPkNoBarDft), !(OPT & kPkNoBarTw)>(P, lds, tlo, thp, lane, Y2);
+        split_y2<KM, !(OPT & kPkNoBarSplit), (OPT & kPkAbNoMag) != 0, KM == kKHalf && (OPT & kPkMagStage) != 0>(
+            Y2, A.mag.p[ch] + f * A.ld, A.K, A.tw, lane, lds);
         return;
     }
 
@@ -451,11 +494,37 @@ int launch_stft8192_pk(const Stft8kArgs &A, uint32_t C, bool fused, int opt, hip
                        0, stream, A)
                 // A/B of the store kinds at the headline shape (B = 512)
                 // A/B and ablation bits at the headline shape (B = 512)
-                if (per == 4 && (opt & ~(kPkNoBarDft | kPkNoBarTw | kPkNoBarSplit))) {
-                    switch (opt & ~(kPkNoBarDft | kPkNoBarTw | kPkNoBarSplit)) {
+                if (per == 4 && (opt & kPkOcc3)) {
+                    switch (opt & ~kPkOcc3) {
+                    case 0:
+                        hipLaunchKernelGGL((stft8192_pk_kernel<kSrcRender, kKHalf, MapKind::Ramp, true, true, 4, 0, 3>),
+                                           grid, dim3(256), 0, stream, A);
+                        break;
+                    case kPkRenderCached:
+                        hipLaunchKernelGGL(
+                            (stft8192_pk_kernel<kSrcRender, kKHalf, MapKind::Ramp, true, true, 4, kPkRenderCached, 3>),
+                            grid, dim3(256), 0, stream, A);
+                        break;
+                    case kPkAbNoRender | kPkAbNoMag:
+                        hipLaunchKernelGGL((stft8192_pk_kernel<kSrcRender, kKHalf, MapKind::Ramp, true, true, 4,
+                                                               kPkAbNoRender | kPkAbNoMag, 3>),
+                                           grid, dim3(256), 0, stream, A);
+                        break;
+                    default: return DSP_ERR_INVALID;
+                    }
+                    break;
+                }
+                if (per == 4 && opt) {
+                    switch (opt) {
 #define DSPB_PK_CASE(o) \
     case (o): DSPB_PK_PER_OPT(4, (o)); break
+                    DSPB_PK_CASE(kPkNoBarDft);
+                    DSPB_PK_CASE(kPkNoBarTw);
+                    DSPB_PK_CASE(kPkNoBarSplit);
+                    DSPB_PK_CASE(kPkNoBarDft | kPkNoBarTw | kPkNoBarSplit);
                     DSPB_PK_CASE(kPkRenderCached);
+                    DSPB_PK_CASE(kPkMagStage);
+                    DSPB_PK_CASE(kPkMagStage | kPkRenderCached);
                     DSPB_PK_CASE(kPkOldSplit);
                     DSPB_PK_CASE(kPkOldSplit | kPkRenderCached);
                     DSPB_PK_CASE(kPkOldSplit | kPkNtMag);

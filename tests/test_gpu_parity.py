@@ -302,11 +302,12 @@ def test_pk_ramp_table_periods(torch_cuda, oracle, B):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("opt", [0, 8, 32, 40, 48, 56, 64, 72, 80, 88])
+@pytest.mark.parametrize("opt", [0, 8, 32, 40, 48, 56, 64, 72, 80, 88, 512, 520, 1024, 1032])
 def test_pk_store_options(torch_cuda, oracle, opt):
     """Packed kernel A/B bits (dsp_stft_soa_options >> 4: 8 cached render
     stores, 16 non-temporal magnitude stores, 32 rows staged through LDS, 64
-    the older scalar last combine and (ka, ka + 16) split): the same bits as
+    the older scalar last combine and (ka, ka + 16) split, 512 rows staged in
+    LDS at their 16-byte phase): the same bits as
     the default path (packed combine + split_y2; within 1e-7 of its peak for
     64), rows of any alignment (ld = K)."""
     L = d.lib()
