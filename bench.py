@@ -338,6 +338,9 @@ def main():
                 "kernel_avg_ms": round(kernel_avg_ms, 5),
                 "algorithmic_bytes_per_launch": int(bytes_per_launch),
                 "algorithmic": alg_desc,
+                "limiter": ("package power: the settled kernel draws the 1400 W cap at sclk ~1.8 GHz "
+                            "(2.38 GHz without its stores); profiles/r01_power_ablation"
+                            if wl in ("headline", "ch96k") else None),
             }),
             "cpu_baseline": cpu,
         }
