@@ -96,8 +96,21 @@ __device__ __forceinline__ void fir_fft_frame(const FirFftArgs &A, uint64_t f, u
     // and it is sent in the same iteration; lane 0 (which pairs with itself,
     // shifted by one register) is fixed up after the loop
     cx zk[32], zr[32];
+    // the spectrum H comes from L2: issued four iterations at a time (one
+    // wait per four, not one per iteration -- 16 serial L2 round trips were
+    // the frame's longest stall)
+    float4 hq[8];
 #pragma unroll
     for (int ka = 0; ka < 16; ++ka) {
+        if ((ka & 3) == 0) {
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float4 *hp = reinterpret_cast<const float4 *>(A.H) + 2u * (64u * (uint32_t)(ka + i) + lane);
+                hq[2 * i] = hp[0];
+                hq[2 * i + 1] = hp[1];
+            }
+        }
         __builtin_amdgcn_sched_barrier(0);
         const cx a0 = ka == 0 ? zp[0] : zm[32 - ka], b0 = zm[31 - ka];
         const cx a1 = zm[16 - ka], b1 = zm[15 - ka];
@@ -111,8 +124,7 @@ __device__ __forceinline__ void fir_fft_frame(const FirFftArgs &A, uint64_t f, u
         const cx2 T = cmul2(negi(D), tw);
         const cx2 X1 = E + T;  // 2 X[k]
         const cx2 X2 = E - T;  // conj 2 X[M - k]
-        const float4 *hp = reinterpret_cast<const float4 *>(A.H) + 2u * (64u * (uint32_t)ka + lane);
-        const float4 ha = hp[0], hb = hp[1];
+        const float4 ha = hq[2 * (ka & 3)], hb = hq[2 * (ka & 3) + 1];
         const cx2 Hk = cx2{v2f{ha.x, ha.y}, v2f{ha.z, ha.w}};
         const cx2 HMk = cx2{v2f{hb.x, hb.y}, v2f{hb.z, hb.w}};
         const cx2 Yk = cmul2(X1, Hk);

@@ -4,6 +4,7 @@ back to back for ~2.5 s while rocm-smi samples sclk and socket power twice
 stalled one.
 
     python tools/clock_probe.py OPT [OPT ...]   (stft_pk.hip kPk* bits)
+    python tools/clock_probe.py fir             (the fir1024 workload instead)
 """
 import os
 import re
@@ -18,13 +19,25 @@ import torch
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "dsp-bench_amd"))
 import dspbench as d  # noqa: E402
 
-L_ = 48_000 * 3600
+FIR = sys.argv[1:2] == ["fir"]
+L_ = 48_000 * (600 if FIR else 3600)
 x = torch.zeros((2, L_), device="cuda")
 nb = d.num_blocks(L_, 512)
 F = d.stft_frames(nb * 512, 8192, 4096)
 out = torch.empty((2, nb * 512), device="cuda")
 mag = torch.empty((2, F, 4097), device="cuda")
 lib = d.lib()
+if FIR:
+    ir, _ = d.ir_analysis(d.Plugin.ir_test(0.9, 0.002), C_out=1, sr=48000.0, device=torch.device("cuda"))
+    fplug = d.Plugin.fir(ir[0, :1024].cpu().numpy())
+    x.uniform_(-0.1, 0.1)
+
+
+def step():
+    if FIR:
+        d.render_offline(x, 2, 512, 48000.0, fplug, out=out)
+    else:
+        d.render_stft(x, 2, 512, 48000.0, d.Plugin.ir_test(), out=out, mag=mag)
 
 
 def smi(samples):
@@ -34,7 +47,7 @@ def smi(samples):
         samples.append(r.stdout)
 
 
-for o in [int(a) for a in sys.argv[1:]] or [64]:
+for o in ([0] if FIR else [int(a) for a in sys.argv[1:]] or [0]):
     lib.dsp_stft_soa_options(o << 4)
     samples = []
     th = threading.Thread(target=smi, args=(samples,))
@@ -47,7 +60,7 @@ for o in [int(a) for a in sys.argv[1:]] or [64]:
     while time.time() - t0 < 2.5:
         e0.record()
         for _ in range(20):
-            d.render_stft(x, 2, 512, 48000.0, d.Plugin.ir_test(), out=out, mag=mag)
+            step()
         e1.record()
         torch.cuda.synchronize()
         ts.append(e0.elapsed_time(e1) / 20)
