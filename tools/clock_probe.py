@@ -5,6 +5,7 @@ stalled one.
 
     python tools/clock_probe.py OPT [OPT ...]   (stft_pk.hip kPk* bits)
     python tools/clock_probe.py fir             (the fir1024 workload instead)
+    python tools/clock_probe.py mem             (the stft96k workload: STFT from HBM)
 """
 import os
 import re
@@ -20,22 +21,27 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 import dspbench as d  # noqa: E402
 
 FIR = sys.argv[1:2] == ["fir"]
-L_ = 48_000 * (600 if FIR else 3600)
+MEM = sys.argv[1:2] == ["mem"]
+L_ = 48_000 * (600 if FIR else 7200 if MEM else 3600)
 x = torch.zeros((2, L_), device="cuda")
 nb = d.num_blocks(L_, 512)
 F = d.stft_frames(nb * 512, 8192, 4096)
 out = torch.empty((2, nb * 512), device="cuda")
-mag = torch.empty((2, F, 4097), device="cuda")
+mag = torch.empty((2, d.stft_frames(L_, 8192, 4096) if MEM else F, 4097), device="cuda")
 lib = d.lib()
 if FIR:
     ir, _ = d.ir_analysis(d.Plugin.ir_test(0.9, 0.002), C_out=1, sr=48000.0, device=torch.device("cuda"))
     fplug = d.Plugin.fir(ir[0, :1024].cpu().numpy())
+    x.uniform_(-0.1, 0.1)
+if MEM:
     x.uniform_(-0.1, 0.1)
 
 
 def step():
     if FIR:
         d.render_offline(x, 2, 512, 48000.0, fplug, out=out)
+    elif MEM:
+        d.stft_magnitude(x, N=8192, H=4096, window=d.DSP_WIN_HANN, K=4097, out=mag)
     else:
         d.render_stft(x, 2, 512, 48000.0, d.Plugin.ir_test(), out=out, mag=mag)
 
@@ -47,7 +53,7 @@ def smi(samples):
         samples.append(r.stdout)
 
 
-for o in ([0] if FIR else [int(a) for a in sys.argv[1:]] or [0]):
+for o in ([0] if FIR or MEM else [int(a) for a in sys.argv[1:]] or [0]):
     lib.dsp_stft_soa_options(o << 4)
     samples = []
     th = threading.Thread(target=smi, args=(samples,))
