@@ -33,7 +33,10 @@ namespace dspb {
 // (ka, ka + 16) split (default: the packed combine + split_y2, 60 VALU
 // fewer per frame, the same bits)
 enum { kPkNoBarDft = 1, kPkNoBarTw = 2, kPkNoBarSplit = 4, kPkRenderCached = 8, kPkNtMag = 16, kPkMagLds = 32,
-       kPkOldSplit = 64, kPkAbNoRender = 128, kPkAbNoMag = 256, kPkMagStage = 512, kPkOcc3 = 1024 };
+       kPkOldSplit = 64, kPkAbNoRender = 128, kPkAbNoMag = 256, kPkMagStage = 512, kPkOcc3 = 1024,
+       kPkMemAos = 2048 };
+// 2048 = memory frames (computed window) loaded as 64 pairs and regrouped
+// after the window multiply (the older path; default: regrouped at the load)
 // 1024 = 3 waves per SIMD (OCC template argument): fft4096_pk_y2_lo's
 // 64 x 33 transpose tile and just-in-time stage twiddles
 // 512 = split_y2 stages the row in LDS at the row's 16-byte phase and stores
@@ -184,6 +187,9 @@ __global__ __launch_bounds__(256, OCC) void stft8192_pk_kernel(Stft8kArgs A) {
     const uint32_t ch = blockIdx.y;
     const uint64_t f = (uint64_t)xcd_remap(blockIdx.x, gridDim.x) * 4u + wave;
     constexpr bool SOA = WINC && MK == MapKind::Ramp && PER > 0 && SRC == kSrcRender;
+    // memory frames with the computed window: two dwordx2 loads per pair
+    // (columns 2j, 2j+1) regrouped into even/odd halves
+    constexpr bool MSOA = WINC && SRC == kSrcMemory && !(OPT & kPkMemAos);
     const uint64_t fs = f * (uint64_t)A.H;
     if (f >= A.F) {  // whole wave leaves; nothing below waits on other waves
         if constexpr (SOA) {
@@ -241,10 +247,10 @@ __global__ __launch_bounds__(256, OCC) void stft8192_pk_kernel(Stft8kArgs A) {
     // (for a frame in memory the 128 dword loads this needs cost more than
     // the shuffles they save: 0.75 vs 0.65 ms per stereo hour, so memory
     // frames keep the dwordx2 path below)
-    if constexpr (SOA) {
+    if constexpr (SOA || MSOA) {
         constexpr int NJ = PER >= 2 ? PER / 2 : 1;
         cx2 X[NJ];
-        {
+        if constexpr (SOA) {
             const uint32_t p0 = (uint32_t)(A.goff + fs) + 2u * lane;
             const float *T = A.map.table;
             if (A.map.closed) {  // table values in closed form (common.hpp ramp_value)
@@ -291,7 +297,14 @@ __global__ __launch_bounds__(256, OCC) void stft8192_pk_kernel(Stft8kArgs A) {
             const v2f C = v2f{kWinB_c[2 * j], kWinB_c[2 * j + 1]}, S = v2f{kWinB_s[2 * j], kWinB_s[2 * j + 1]};
             const v2f we = (v2f{ve, ve} * S + v2f{A.wa, A.wa}) - v2f{ue, ue} * C;
             const v2f wo = (v2f{vo, vo} * S + v2f{A.wa, A.wa}) - v2f{uo, uo} * C;
-            const cx2 xj = X[j % NJ];
+            cx2 xj;
+            if constexpr (SOA) {
+                xj = X[j % NJ];
+            } else {  // (x[2l + 256 j], x[2l + 256 j + 1]) and 128 samples on
+                const v2f a = reinterpret_cast<const v2f *>(x + fs + 256u * (uint32_t)j)[lane];
+                const v2f b = reinterpret_cast<const v2f *>(x + fs + 256u * (uint32_t)j + 128u)[lane];
+                xj = cx2{v2f{a.x, b.x}, v2f{a.y, b.y}};
+            }
             P[j] = cx2{xj.r * we, xj.i * wo};
         }
     } else {
@@ -558,8 +571,12 @@ int launch_stft8192_pk(const Stft8kArgs &A, uint32_t C, bool fused, int opt, hip
         default: return DSP_ERR_INVALID;
         }
     } else if (winc) {
-        hipLaunchKernelGGL((stft8192_pk_kernel<kSrcMemory, kKHalf, MapKind::Noop, true, true>), grid, dim3(256),
-                           0, stream, A);
+        if (opt & kPkMemAos)
+            hipLaunchKernelGGL((stft8192_pk_kernel<kSrcMemory, kKHalf, MapKind::Noop, true, true, 0, kPkMemAos>),
+                               grid, dim3(256), 0, stream, A);
+        else
+            hipLaunchKernelGGL((stft8192_pk_kernel<kSrcMemory, kKHalf, MapKind::Noop, true, true>), grid, dim3(256),
+                               0, stream, A);
     } else {
         launch_pk_km<kSrcMemory, MapKind::Noop, true, false>(km, grid, stream, A);
     }

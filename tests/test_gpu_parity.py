@@ -107,6 +107,28 @@ def test_render_matches_reference_plugin_so(torch_cuda, oracle):
         assert np.array_equal(got, ref), name
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("opt", [0, 2048])
+@pytest.mark.parametrize("H", [4096, 1000])
+def test_pk_memory_load_options(torch_cuda, oracle, opt, H):
+    """Packed kernel, frames from memory with the computed window: pairs
+    regrouped at the load (default) or after the window multiply (2048),
+    against float64, on an offset (unaligned) signal view."""
+    L = d.lib()
+    oldv, oldo = L.dsp_stft_kernel_variant(5), L.dsp_stft_soa_options(14 | (opt << 4))
+    try:
+        n = 8192 * 6 + 555
+        x = rnd((2, n + 2), 64)
+        xd = to_dev(torch_cuda, x)[:, 2:]
+        mag = d.stft_magnitude(xd, N=8192, H=H, window=d.DSP_WIN_HANN, K=4097).cpu().numpy()
+        for c in range(2):
+            ref = oracle.np_stft_mag(x[c, 2:], 8192, H, d.DSP_WIN_HANN, 4097)
+            assert peak_rel_err(mag[c], ref) <= PEAK_REL_TOL
+    finally:
+        L.dsp_stft_kernel_variant(oldv)
+        L.dsp_stft_soa_options(oldo)
+
+
 @pytest.mark.parametrize("window", [d.DSP_WIN_HANN, d.DSP_WIN_HAMMING])
 @pytest.mark.parametrize("K", [4097, 8192, 1000])
 @pytest.mark.parametrize("H", [4096, 2048, 8192, 1000])

@@ -5,7 +5,7 @@ stalled one.
 
     python tools/clock_probe.py OPT [OPT ...]   (stft_pk.hip kPk* bits)
     python tools/clock_probe.py fir             (the fir1024 workload instead)
-    python tools/clock_probe.py mem             (the stft96k workload: STFT from HBM)
+    python tools/clock_probe.py mem [OPT ...]   (the stft96k workload: STFT from HBM)
 """
 import os
 import re
@@ -53,7 +53,7 @@ def smi(samples):
         samples.append(r.stdout)
 
 
-for o in ([0] if FIR or MEM else [int(a) for a in sys.argv[1:]] or [0]):
+for o in ([0] if FIR else [int(a) for a in sys.argv[2:]] or [0] if MEM else [int(a) for a in sys.argv[1:]] or [0]):
     lib.dsp_stft_soa_options(o << 4)
     samples = []
     th = threading.Thread(target=smi, args=(samples,))
