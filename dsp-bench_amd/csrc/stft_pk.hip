@@ -110,8 +110,13 @@ __device__ __forceinline__ void split_y2(const cx2 (&Y2)[32], float *mrow, uint3
         // u = W8192^(l + 64 q); T = (-i D.x u, -i D.y (-i u)) with U1 = u, U2 = (u.i, -u.r)
         v2f u = wl;
         if (q) u = v2f{wl.x, wl.x} * v2f{kW128_re[q], kW128_im[q]} + v2f{wl.y, wl.y} * v2f{-kW128_im[q], kW128_re[q]};
-        const v2f U2 = v2f{u.y, -u.x};
-        const cx2 T = cx2{D.i * u + D.r * U2, D.i * U2 - D.r * u};
+        // a (.) U2 with U2 = (u.y, -u.x) as one v_pk_mul: the swap and the
+        // negation ride on the operand's op_sel / neg_hi (the compiler builds
+        // U2 with a v_xor + v_mov otherwise)
+        v2f rU2, iU2;
+        asm("v_pk_mul_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(rU2) : "v"(D.r), "v"(u));
+        asm("v_pk_mul_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(iU2) : "v"(D.i), "v"(u));
+        const cx2 T = cx2{D.i * u + rU2, iU2 - D.r * u};
         const cx2 X1 = E + T;  // 2 X[k], k = l + 64 q (+ 2048)
         const cx2 X2 = E - T;  // 2 conj X[M - k]
         const v2f q1 = X1.r * X1.r + X1.i * X1.i;

@@ -1,0 +1,42 @@
+"""Interleaved A/B of two builds of libdspbench.so at the headline shape:
+each round runs every library in a fresh subprocess (settled: 60 warm + 200
+timed launches) and prints the median kernel time.
+
+    python tools/ab_lib.py ROUNDS LIB_A LIB_B ...
+"""
+import os
+import statistics
+import subprocess
+import sys
+
+CHILD = r'''
+import ctypes as C, os, sys, torch
+sys.path.insert(0, os.path.join(%r, "dsp-bench_amd"))
+os.environ["DSPBENCH_LIB"] = %r
+import dspbench as d
+lib = d.lib()
+L_ = 48_000 * 3600
+x = torch.zeros((2, L_), device="cuda")
+nb = d.num_blocks(L_, 512)
+F = d.stft_frames(nb * 512, 8192, 4096)
+out = torch.empty((2, nb * 512), device="cuda"); mag = torch.empty((2, F, 4097), device="cuda")
+for _ in range(60): d.render_stft(x, 2, 512, 48000.0, d.Plugin.ir_test(), out=out, mag=mag)
+torch.cuda.synchronize()
+lib.dsp_kernel_timing(None, None, None); lib.dsp_kernel_timing_enable(1)
+for _ in range(200): d.render_stft(x, 2, 512, 48000.0, d.Plugin.ir_test(), out=out, mag=mag)
+torch.cuda.synchronize(); lib.dsp_kernel_timing_enable(0)
+ms, n, b = C.c_double(), C.c_uint64(), C.c_uint64()
+lib.dsp_kernel_timing(C.byref(ms), C.byref(n), C.byref(b))
+print(ms.value / n.value)
+'''
+repo = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+rounds = int(sys.argv[1])
+libs = sys.argv[2:]
+res = {l: [] for l in libs}
+for r in range(rounds):
+    for l in libs:
+        o = subprocess.run([sys.executable, "-c", CHILD % (repo, os.path.abspath(l))], capture_output=True,
+                           text=True, timeout=120)
+        res[l].append(float(o.stdout.strip().splitlines()[-1]))
+for l, v in res.items():
+    print(f"{l}: median {statistics.median(v):.4f} ms  all {' '.join(f'{t:.4f}' for t in v)}")
