@@ -61,11 +61,12 @@ def parse():
                     help="8192-pt kernel (dsp_stft_kernel_variant): 2 = wave/frame scalar SoA, "
                          "5 = wave/frame packed even/odd pairs")
     ap.add_argument("--workload", default="headline",
-                    choices=["headline", "stft96k", "ch96k", "gain10min", "fir1024", "wav16", "wav24"],
+                    choices=["headline", "stft96k", "ch96k", "gain10min", "fir1024", "wav16", "wav24", "ir"],
                     help="headline = IR_test + STFT 48 kHz (the metric); stft96k = BASELINE cfg 4 "
                          "(STFT of 1 h stereo 96 kHz from HBM); gain10min = cfg 2 render; "
                          "wav16 / wav24 = GPU decode of a 1 h stereo int16 / int24 WAV payload; "
-                         "ch96k = BASELINE cfg 5: one 96 kHz channel per GPU through IR_test + STFT")
+                         "ch96k = BASELINE cfg 5: one 96 kHz channel per GPU through IR_test + STFT; "
+                         "ir = compute_IR + fft_perform_and_get_magnitude latency (one 8192-pt frame per call)")
     return ap.parse_args()
 
 
@@ -110,6 +111,62 @@ def cpu_baseline(seconds_budget: float):
                       f"1 thread) + fp32 radix-2 STFT ({threads} OpenMP threads), oracle/oracle.c"}
 
 
+def bench_ir(args, dev, world, rank):
+    """dsp_ir_analysis = compute_IR (plugin.cpp:17-58:
+    impulse, IR_test callback over 2048 samples, 2 channels) + the Hamming
+    window, 8192-point FFT and 8192 magnitudes of fft_perform_and_get_magnitude
+    (dsp.cpp:53-66).  It runs once per parameter change, so it is a latency
+    path: one step = one call, timed back to back."""
+    import numpy as np
+    import torch
+    import dspbench as d
+    ir_len, C_out = 2048, 2
+    plugin = d.Plugin.ir_test(0.9, 0.002)
+    for _ in range(args.warmup):
+        d.ir_analysis(plugin, C_out=C_out, sr=float(SR), ir_len=ir_len, device=dev)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        d.ir_analysis(plugin, C_out=C_out, sr=float(SR), ir_len=ir_len, device=dev)
+    torch.cuda.synchronize()
+    step_s = (time.perf_counter() - t0) / args.steps
+    cpu = None
+    if rank == 0 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import oracle as o
+        plug = o.restated_plugin("IR_test")
+        n = 0
+        t1 = time.perf_counter()
+        while time.perf_counter() - t1 < 2.0:
+            bufs = np.zeros((C_out, ir_len), np.float32)
+            bufs[:, 0] = 1.0
+            o.callback_once(plug, bufs, float(SR))
+            o.c_ir_magnitude(bufs[0], ir_len)
+            n += 1
+        cs = (time.perf_counter() - t1) / n
+        cpu = {"value": round(C_out * ir_len / cs / 1e6, 3), "unit": "Msamples/s", "cores": 1, "kind": "port",
+               "latency_us": round(cs * 1e6, 1),
+               "sample": f"{n} analyses: the restated IR_test callback + oracle/oracle.c's float64 "
+                         "Hamming window, 8192-point FFT and magnitudes (IPP is absent)"}
+    alg = C_out * ir_len * 4 + 4 * ir_len * 4  # impulse-response write + magnitudes
+    line = {
+        "metric": METRIC, "value": round(C_out * ir_len / step_s / 1e6, 3), "unit": "Msamples/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(step_s * 1e3, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "config": {"workload": "IR analysis (compute_IR + fft_perform_and_get_magnitude): IR_test, 2 ch x 2048 "
+                               "samples, Hamming, 8192-pt FFT, 8192 magnitudes; one call per step",
+                   "latency_us": round(step_s * 1e6, 1)},
+        "roofline": {"bound": "hbm", "kernel": "ramp/impulse render + stft8192_pk (one frame)",
+                     "achieved": round(alg / step_s / 1e9, 3), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": round(alg / step_s / 1e9 / HBM_PEAK_GBPS, 6), "traffic": None,
+                     "algorithmic_bytes_per_launch": alg,
+                     "limiter": "launch and host-call latency: one 8192-point frame per call"},
+        "cpu_baseline": cpu,
+    }
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+
+
 def main():
     args = parse()
     import torch
@@ -127,6 +184,11 @@ def main():
     import dspbench as d
     d.lib().dsp_stft_kernel_variant(args.stft_variant)
     d.lib().dsp_fir_method(args.fir_method)
+    if args.workload == "ir":
+        bench_ir(args, dev, world, rank)
+        if world > 1:
+            dist.destroy_process_group()
+        return
 
     wl = args.workload
     sr = 96_000 if wl in ("stft96k", "ch96k") else SR

@@ -919,10 +919,11 @@ int dsp_ir_analysis(const dsp_plugin *plugin, uint32_t C, float sr, uint32_t ir_
         for (uint32_t c = 0; c < C; ++c) dir[c] = ir_out[c];
     }
     // compute_IR (plugin.cpp:27-34): IR[c] = delta, then one callback of ir_len
-    static const float one = 1.0f;
-    for (uint32_t c = 0; c < C; ++c) {
-        DSPB_HIP(hipMemsetAsync(dir[c], 0, ir_len * sizeof(float), s));
-        DSPB_HIP(hipMemcpyAsync(dir[c], &one, sizeof(float), hipMemcpyHostToDevice, s));
+    for (uint32_t c0 = 0; c0 < C; c0 += kMaxChannels) {
+        const uint32_t cn = (C - c0) < (uint32_t)kMaxChannels ? (C - c0) : kMaxChannels;
+        ChanOut imp{};
+        for (uint32_t j = 0; j < cn; ++j) imp.p[j] = dir[c0 + j];
+        if ((st = launch_impulse(imp, cn, ir_len, s))) return st;
     }
     SampleMap map;
     if ((st = plugin_map(plugin, ir_len, g.dev, s, &map, sr))) return st;

@@ -173,6 +173,22 @@ int launch_set(float v, float *out, uint64_t n, hipStream_t s) {
     DSPB_HIP(hipGetLastError());
     return DSP_OK;
 }
+// compute_IR's impulse (plugin.cpp:27-34): buf[c][i] = (i == 0) for every
+// channel, one launch (was a memset + a pageable 4-byte copy per channel)
+__global__ void impulse_kernel(ChanOut buf, uint32_t C, uint32_t n) {
+    const uint32_t c = blockIdx.y;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+        buf.p[c][i] = i == 0 ? 1.f : 0.f;
+}
+int launch_impulse(const ChanOut &buf, uint32_t C, uint32_t n, hipStream_t s) {
+    if (!n || !C) return DSP_OK;
+    if (C > (uint32_t)kMaxChannels) return DSP_ERR_INVALID;
+    const uint32_t g = (n + 255) / 256 < 32 ? (n + 255) / 256 : 32;
+    hipLaunchKernelGGL(impulse_kernel, dim3(g, C), dim3(256), 0, s, buf, C, n);
+    DSPB_HIP(hipGetLastError());
+    return DSP_OK;
+}
+
 int launch_magnitude(const float *re, const float *im, float *out, uint64_t n,
                      hipStream_t s) {
     if (!n) return DSP_OK;
