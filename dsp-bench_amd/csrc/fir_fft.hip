@@ -111,7 +111,6 @@ __device__ __forceinline__ void fir_fft_frame(const FirFftArgs &A, uint64_t f, u
                 hq[2 * i + 1] = hp[1];
             }
         }
-        __builtin_amdgcn_sched_barrier(0);
         const cx a0 = ka == 0 ? zp[0] : zm[32 - ka], b0 = zm[31 - ka];
         const cx a1 = zm[16 - ka], b1 = zm[15 - ka];
         const cx s0 = cx{l0 ? a0.r : b0.r, l0 ? a0.i : b0.i};

@@ -2,7 +2,9 @@
 each round runs every library in a fresh subprocess (settled: 60 warm + 200
 timed launches) and prints the median kernel time.
 
-    python tools/ab_lib.py ROUNDS LIB_A LIB_B ...
+    python tools/ab_lib.py [--fir|--mem] ROUNDS LIB_A LIB_B ...
+(--fir: the fir1024 workload, 10 min stereo overlap-save; --mem: the stft96k
+memory-source STFT)
 """
 import os
 import statistics
@@ -15,27 +17,39 @@ sys.path.insert(0, os.path.join(%r, "dsp-bench_amd"))
 os.environ["DSPBENCH_LIB"] = %r
 import dspbench as d
 lib = d.lib()
-L_ = 48_000 * 3600
-x = torch.zeros((2, L_), device="cuda")
+MODE = %r
+L_ = 48_000 * (600 if MODE == "fir" else 7200 if MODE == "mem" else 3600)
+x = torch.rand((2, L_), device="cuda") - 0.5
 nb = d.num_blocks(L_, 512)
 F = d.stft_frames(nb * 512, 8192, 4096)
 out = torch.empty((2, nb * 512), device="cuda"); mag = torch.empty((2, F, 4097), device="cuda")
-for _ in range(60): d.render_stft(x, 2, 512, 48000.0, d.Plugin.ir_test(), out=out, mag=mag)
+if MODE == "fir":
+    ir, _ = d.ir_analysis(d.Plugin.ir_test(0.9, 0.002), C_out=1, sr=48000.0, device=torch.device("cuda"))
+    fplug = d.Plugin.fir(ir[0, :1024].cpu().numpy())
+def step():
+    if MODE == "fir": d.render_offline(x, 2, 512, 48000.0, fplug, out=out)
+    elif MODE == "mem": d.stft_magnitude(x, N=8192, H=4096, window=d.DSP_WIN_HANN, K=4097, out=mag)
+    else: d.render_stft(x, 2, 512, 48000.0, d.Plugin.ir_test(), out=out, mag=mag)
+for _ in range(60): step()
 torch.cuda.synchronize()
 lib.dsp_kernel_timing(None, None, None); lib.dsp_kernel_timing_enable(1)
-for _ in range(200): d.render_stft(x, 2, 512, 48000.0, d.Plugin.ir_test(), out=out, mag=mag)
+for _ in range(200): step()
 torch.cuda.synchronize(); lib.dsp_kernel_timing_enable(0)
 ms, n, b = C.c_double(), C.c_uint64(), C.c_uint64()
 lib.dsp_kernel_timing(C.byref(ms), C.byref(n), C.byref(b))
 print(ms.value / n.value)
 '''
 repo = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
-rounds = int(sys.argv[1])
-libs = sys.argv[2:]
+argv = sys.argv[1:]
+mode = "headline"
+if argv and argv[0] in ("--fir", "--mem"):
+    mode = argv.pop(0)[2:]
+rounds = int(argv[0])
+libs = argv[1:]
 res = {l: [] for l in libs}
 for r in range(rounds):
     for l in libs:
-        o = subprocess.run([sys.executable, "-c", CHILD % (repo, os.path.abspath(l))], capture_output=True,
+        o = subprocess.run([sys.executable, "-c", CHILD % (repo, os.path.abspath(l), mode)], capture_output=True,
                            text=True, timeout=120)
         res[l].append(float(o.stdout.strip().splitlines()[-1]))
 for l, v in res.items():

@@ -21,7 +21,7 @@ while read -r group; do
     [[ -z "$group" || "$group" == \#* ]] && continue
     i=$((i+1))
     echo "=== pass $i: $group"
-    timeout -k 10 300 rocprofv3 --pmc $group --kernel-include-regex 'stft8192|render_vec' \
+    timeout -k 10 300 rocprofv3 --pmc $group --kernel-include-regex "${KREGEX:-stft8192|render_vec}" \
         -d $out/p$i -o run --output-format csv -- python bench.py $args > $out/p$i.log 2>&1
     rc=$?
     echo "rc=$rc"; grep -h '"metric"' $out/p$i.log | cut -c1-120
