@@ -101,114 +101,16 @@ __device__ __forceinline__ void combine64_dir(const cx2 (&a)[32], cx (&yp)[32], 
     }
 }
 
-// 4096-point complex FFT of one wavefront.  In: P[j] = (u[2j], u[2j+1]),
-// u[r] = element l + 64 r of this lane l (r is the register index).  Out:
-// U[l + 64 q] = zp[q] (q < 32), zm[q - 32] -- forward: Z = DFT(u), inverse
-// (INV): the unnormalised inverse.  tlo[j] = W4096^(l j), thp[h] =
-// (W4096^(8 l h), W4096^(8 l (h + 4))); lds = this wave's 64 x 65 tile.
-// Everything up to the last combine: R holds the second DFT64's even/odd
-// DFT32 halves (combine64p / combine64_dir finish it).
-template <bool INV, bool BAR_DFT, bool BAR_TW>
-__device__ __forceinline__ void fft4096_pk_front(cx2 (&P)[32], float *lds, const cx (&tlo)[8], const cx2 (&thp)[4],
-                                                 uint32_t lane, cx2 (&R)[32]) {
-    // DFT64 over the register index: even/odd DFT32 in the halves, combine
-    x2dft32_dir<BAR_DFT, INV>(P);
-    cx2 Q[32];  // Q[k] = (Y[k], Y[k+32]) * (W4096^(+-l k), W4096^(+-l (k+32)))
-    {
-        cx2 Y[32];
-        combine64p_dir<INV>(P, Y);
-#pragma unroll
-        for (int k = 0; k < 32; ++k) {
-            if (BAR_TW) __builtin_amdgcn_sched_barrier(0);
-            const int lo = k & 7, hi = k >> 3;
-            const cx2 w = lo ? cmulb(tlo[lo], thp[hi]) : thp[hi];
-            Q[k] = cmul2(Y[k], conj2<INV>(w));
-        }
-    }
-    // transpose through LDS: row l, column kb -> column l, row a
-    // R[j] = (t[2j], t[2j+1]), t[a] = row a of column l
-#pragma unroll
-    for (int k = 0; k < 32; ++k) {
-        lds[lane * 65u + k] = Q[k].r.x;
-        lds[lane * 65u + k + 32] = Q[k].r.y;
-    }
-    lds_fence();
-#pragma unroll
-    for (int j = 0; j < 32; ++j) R[j].r = v2f{lds[(2 * j) * 65 + lane], lds[(2 * j + 1) * 65 + lane]};
-    lds_fence();
-#pragma unroll
-    for (int k = 0; k < 32; ++k) {
-        lds[lane * 65u + k] = Q[k].i.x;
-        lds[lane * 65u + k + 32] = Q[k].i.y;
-    }
-    lds_fence();
-#pragma unroll
-    for (int j = 0; j < 32; ++j) R[j].i = v2f{lds[(2 * j) * 65 + lane], lds[(2 * j + 1) * 65 + lane]};
-    // DFT64 over the other index (its combine is the caller's)
-    x2dft32_dir<BAR_DFT, INV>(R);
-}
-
-template <bool INV, bool BAR_DFT = true, bool BAR_TW = true>
-__device__ __forceinline__ void fft4096_pk(cx2 (&P)[32], float *lds, const cx (&tlo)[8], const cx2 (&thp)[4],
-                                           uint32_t lane, cx (&zp)[32], cx (&zm)[32]) {
-    cx2 R[32];
-    fft4096_pk_front<INV, BAR_DFT, BAR_TW>(P, lds, tlo, thp, lane, R);
-    combine64_dir<INV>(R, zp, zm);
-}
-
-// The same transform with a packed last combine: Y2[q] = (U[l + 64 q],
-// U[l + 64 (q + 32)]) in the halves of one cx2 (forward only) -- 6 packed
-// instructions per pair instead of 8 scalar ones.
-template <bool BAR_DFT = true, bool BAR_TW = true>
-__device__ __forceinline__ void fft4096_pk_y2(cx2 (&P)[32], float *lds, const cx (&tlo)[8], const cx2 (&thp)[4],
-                                              uint32_t lane, cx2 (&Y2)[32]) {
-    cx2 R[32];
-    fft4096_pk_front<false, BAR_DFT, BAR_TW>(P, lds, tlo, thp, lane, R);
-    combine64p(R, Y2);
-}
-
-// Low-footprint forward transform for 3 waves per SIMD.  The stage
-// twiddles are loaded after the first DFT32s (tw = get_tw's table: T8192,
-// then the lane-major rows) instead of living in 30 VGPRs from the kernel's
-// start, and the transpose goes through a 64 x 33 tile (8.4 KB) in four
-// passes of 32 floats per lane, so no pass holds more than 128 VGPRs of
-// frame and 12 waves per CU fit in the LDS:
+// The transpose of fft4096_pk_front through a 64 x 33 tile (8.4 KB per wave
+// instead of 16.6 KB) in four passes of 32 floats per lane:
 //   pass x: every lane writes its row's columns 0..31 (the .x halves);
 //           lane d reads column d & 31, rows 32 (d >= 32) + a, a < 32 -> X[a]
 //   pass y: the same with columns 32..63 (.y halves) -> Y[a]
 //   then v_permlane32_swap(X[a], Y[a]) trades the upper lanes' X for the
 //   lower lanes' Y: every lane holds its own column, rows 0..31 in X and
-//   rows 32..63 in Y (32 swaps per component).
-// Output as fft4096_pk_y2.
-template <bool BAR_DFT = true>
-__device__ __forceinline__ void fft4096_pk_y2_lo(cx2 (&P)[32], float *lds, const v2f *tw, uint32_t lane,
-                                                 cx2 (&Y2)[32]) {
-    x2dft32_dir<BAR_DFT, false>(P);
-    cx2 Q[32];
-    {
-        cx tlo[8];
-#pragma unroll
-        for (int j = 1; j < 8; ++j) {
-            const v2f a = (tw + 8192u + 64u * (uint32_t)(j - 1))[lane];
-            tlo[j] = cx{a.x, a.y};
-        }
-        const float4 *tp4 = reinterpret_cast<const float4 *>(tw + 8192u + 896u);
-        cx2 Y[32];
-        combine64p(P, Y);
-#pragma unroll
-        for (int hi = 0; hi < 4; ++hi) {
-            const float4 t = tp4[64u * (uint32_t)hi + lane];
-            const cx2 th = cx2{v2f{t.x, t.y}, v2f{t.z, t.w}};
-#pragma unroll
-            for (int lo = 0; lo < 8; ++lo) {
-                __builtin_amdgcn_sched_barrier(0);
-                const int k = lo + 8 * hi;
-                const cx2 w = lo ? cmulb(tlo[lo], th) : th;
-                Q[k] = cmul2(Y[k], w);
-            }
-        }
-    }
-    cx2 R[32];
+//   rows 32..63 in Y (32 swaps per component, no pass holds more than the
+//   frame's 128 VGPRs).
+__device__ __forceinline__ void transpose_pl(const cx2 (&Q)[32], float *lds, uint32_t lane, cx2 (&R)[32]) {
     const uint32_t wrow = lane * 33u;                           // this lane's row
     const uint32_t rcol = (lane & 32u) * 33u + (lane & 31u);    // rows 32 (d >= 32) + a, column d & 31
 #pragma unroll
@@ -245,6 +147,115 @@ __device__ __forceinline__ void fft4096_pk_y2_lo(cx2 (&P)[32], float *lds, const
             }
         }
     }
+}
+
+// 4096-point complex FFT of one wavefront.  In: P[j] = (u[2j], u[2j+1]),
+// u[r] = element l + 64 r of this lane l (r is the register index).  Out:
+// U[l + 64 q] = zp[q] (q < 32), zm[q - 32] -- forward: Z = DFT(u), inverse
+// (INV): the unnormalised inverse.  tlo[j] = W4096^(l j), thp[h] =
+// (W4096^(8 l h), W4096^(8 l (h + 4))); lds = this wave's 64 x 65 tile.
+// Everything up to the last combine: R holds the second DFT64's even/odd
+// DFT32 halves (combine64p / combine64_dir finish it).
+// PL: the transpose goes through transpose_pl's 64 x 33 tile.
+template <bool INV, bool BAR_DFT, bool BAR_TW, bool PL = false>
+__device__ __forceinline__ void fft4096_pk_front(cx2 (&P)[32], float *lds, const cx (&tlo)[8], const cx2 (&thp)[4],
+                                                 uint32_t lane, cx2 (&R)[32]) {
+    // DFT64 over the register index: even/odd DFT32 in the halves, combine
+    x2dft32_dir<BAR_DFT, INV>(P);
+    cx2 Q[32];  // Q[k] = (Y[k], Y[k+32]) * (W4096^(+-l k), W4096^(+-l (k+32)))
+    {
+        cx2 Y[32];
+        combine64p_dir<INV>(P, Y);
+#pragma unroll
+        for (int k = 0; k < 32; ++k) {
+            if (BAR_TW) __builtin_amdgcn_sched_barrier(0);
+            const int lo = k & 7, hi = k >> 3;
+            const cx2 w = lo ? cmulb(tlo[lo], thp[hi]) : thp[hi];
+            Q[k] = cmul2(Y[k], conj2<INV>(w));
+        }
+    }
+    // transpose through LDS: row l, column kb -> column l, row a
+    // R[j] = (t[2j], t[2j+1]), t[a] = row a of column l
+    if constexpr (PL) {
+        transpose_pl(Q, lds, lane, R);
+        x2dft32_dir<BAR_DFT, INV>(R);
+        return;
+    }
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+        lds[lane * 65u + k] = Q[k].r.x;
+        lds[lane * 65u + k + 32] = Q[k].r.y;
+    }
+    lds_fence();
+#pragma unroll
+    for (int j = 0; j < 32; ++j) R[j].r = v2f{lds[(2 * j) * 65 + lane], lds[(2 * j + 1) * 65 + lane]};
+    lds_fence();
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+        lds[lane * 65u + k] = Q[k].i.x;
+        lds[lane * 65u + k + 32] = Q[k].i.y;
+    }
+    lds_fence();
+#pragma unroll
+    for (int j = 0; j < 32; ++j) R[j].i = v2f{lds[(2 * j) * 65 + lane], lds[(2 * j + 1) * 65 + lane]};
+    // DFT64 over the other index (its combine is the caller's)
+    x2dft32_dir<BAR_DFT, INV>(R);
+}
+
+template <bool INV, bool BAR_DFT = true, bool BAR_TW = true, bool PL = false>
+__device__ __forceinline__ void fft4096_pk(cx2 (&P)[32], float *lds, const cx (&tlo)[8], const cx2 (&thp)[4],
+                                           uint32_t lane, cx (&zp)[32], cx (&zm)[32]) {
+    cx2 R[32];
+    fft4096_pk_front<INV, BAR_DFT, BAR_TW, PL>(P, lds, tlo, thp, lane, R);
+    combine64_dir<INV>(R, zp, zm);
+}
+
+// The same transform with a packed last combine: Y2[q] = (U[l + 64 q],
+// U[l + 64 (q + 32)]) in the halves of one cx2 (forward only) -- 6 packed
+// instructions per pair instead of 8 scalar ones.
+template <bool BAR_DFT = true, bool BAR_TW = true>
+__device__ __forceinline__ void fft4096_pk_y2(cx2 (&P)[32], float *lds, const cx (&tlo)[8], const cx2 (&thp)[4],
+                                              uint32_t lane, cx2 (&Y2)[32]) {
+    cx2 R[32];
+    fft4096_pk_front<false, BAR_DFT, BAR_TW>(P, lds, tlo, thp, lane, R);
+    combine64p(R, Y2);
+}
+
+// Low-footprint forward transform for 3 waves per SIMD.  The stage
+// twiddles are loaded after the first DFT32s (tw = get_tw's table: T8192,
+// then the lane-major rows) instead of living in 30 VGPRs from the kernel's
+// start, and the transpose is transpose_pl's, so 12 waves per CU fit in the
+// LDS.  Output as fft4096_pk_y2.
+template <bool BAR_DFT = true>
+__device__ __forceinline__ void fft4096_pk_y2_lo(cx2 (&P)[32], float *lds, const v2f *tw, uint32_t lane,
+                                                 cx2 (&Y2)[32]) {
+    x2dft32_dir<BAR_DFT, false>(P);
+    cx2 Q[32];
+    {
+        cx tlo[8];
+#pragma unroll
+        for (int j = 1; j < 8; ++j) {
+            const v2f a = (tw + 8192u + 64u * (uint32_t)(j - 1))[lane];
+            tlo[j] = cx{a.x, a.y};
+        }
+        const float4 *tp4 = reinterpret_cast<const float4 *>(tw + 8192u + 896u);
+        cx2 Y[32];
+        combine64p(P, Y);
+#pragma unroll
+        for (int hi = 0; hi < 4; ++hi) {
+            const float4 t = tp4[64u * (uint32_t)hi + lane];
+            const cx2 th = cx2{v2f{t.x, t.y}, v2f{t.z, t.w}};
+#pragma unroll
+            for (int lo = 0; lo < 8; ++lo) {
+                __builtin_amdgcn_sched_barrier(0);
+                const int k = lo + 8 * hi;
+                const cx2 w = lo ? cmulb(tlo[lo], th) : th;
+                Q[k] = cmul2(Y[k], w);
+            }
+        }
+    }
+    cx2 R[32];
+    transpose_pl(Q, lds, lane, R);
     x2dft32_dir<BAR_DFT, false>(R);
     combine64p(R, Y2);
 }

@@ -45,9 +45,10 @@ __device__ __forceinline__ void load_stage_tw(const v2f *tw, uint32_t lane, uint
 
 // EDGE: frames that reach before sample 0 or past L (bounds-checked loads);
 // interior frames run the EDGE = false instantiation
+// hs: the block's LDS copy of H, [2 ka + h][lane] float4 (kernel prologue)
 template <bool EDGE>
 __device__ __forceinline__ void fir_fft_frame(const FirFftArgs &A, uint64_t f, uint32_t ch, float *lds,
-                                              uint32_t lane) {
+                                              const float4 *hs, uint32_t lane) {
     const int64_t fs = (int64_t)(f * kOlsHop) - (int64_t)kOlsHist;  // even
     const float *x = (ch < A.in_ch) ? A.in.p[ch] : nullptr;
 
@@ -84,7 +85,7 @@ __device__ __forceinline__ void fir_fft_frame(const FirFftArgs &A, uint64_t f, u
     }
 
     cx zp[32], zm[32];
-    fft4096_pk<false>(P, lds, tlo, thp, lane, zp, zm);
+    fft4096_pk<false, true, true, true>(P, lds, tlo, thp, lane, zp, zm);
 
     // ---- split, H multiply, inverse split, paired over (ka, ka + 16) --------
     const uint32_t src = ((64u - lane) & 63u) * 4u;
@@ -96,21 +97,8 @@ __device__ __forceinline__ void fir_fft_frame(const FirFftArgs &A, uint64_t f, u
     // and it is sent in the same iteration; lane 0 (which pairs with itself,
     // shifted by one register) is fixed up after the loop
     cx zk[32], zr[32];
-    // the spectrum H comes from L2: issued four iterations at a time (one
-    // wait per four, not one per iteration -- 16 serial L2 round trips were
-    // the frame's longest stall)
-    float4 hq[8];
 #pragma unroll
     for (int ka = 0; ka < 16; ++ka) {
-        if ((ka & 3) == 0) {
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const float4 *hp = reinterpret_cast<const float4 *>(A.H) + 2u * (64u * (uint32_t)(ka + i) + lane);
-                hq[2 * i] = hp[0];
-                hq[2 * i + 1] = hp[1];
-            }
-        }
         const cx a0 = ka == 0 ? zp[0] : zm[32 - ka], b0 = zm[31 - ka];
         const cx a1 = zm[16 - ka], b1 = zm[15 - ka];
         const cx s0 = cx{l0 ? a0.r : b0.r, l0 ? a0.i : b0.i};
@@ -123,7 +111,7 @@ __device__ __forceinline__ void fir_fft_frame(const FirFftArgs &A, uint64_t f, u
         const cx2 T = cmul2(negi(D), tw);
         const cx2 X1 = E + T;  // 2 X[k]
         const cx2 X2 = E - T;  // conj 2 X[M - k]
-        const float4 ha = hq[2 * (ka & 3)], hb = hq[2 * (ka & 3) + 1];
+        const float4 ha = hs[(2u * ka) * 64u + lane], hb = hs[(2u * ka + 1u) * 64u + lane];
         const cx2 Hk = cx2{v2f{ha.x, ha.y}, v2f{ha.z, ha.w}};
         const cx2 HMk = cx2{v2f{hb.x, hb.y}, v2f{hb.z, hb.w}};
         const cx2 Yk = cmul2(X1, Hk);
@@ -162,7 +150,7 @@ __device__ __forceinline__ void fir_fft_frame(const FirFftArgs &A, uint64_t f, u
         asm volatile("" : "+s"(salt));
         load_stage_tw(A.tw, lane, salt, tlo, thp);
     }
-    fft4096_pk<true>(Q, lds, tlo, thp, lane, yp, ym);
+    fft4096_pk<true, true, true, true>(Q, lds, tlo, thp, lane, yp, ym);
 
     // ---- outputs: m = l + 64 b, b >= 8 -> y[f H + 2l + 128 (b - 8)] ----------
     float *o = A.out.p[ch];
@@ -188,15 +176,29 @@ __device__ __forceinline__ void fir_fft_frame(const FirFftArgs &A, uint64_t f, u
 // frame 0 and the frames at or past fe (a wave-uniform branch), so the few
 // edge frames overlap the interior ones instead of running as serial
 // single-wave launches
+// LDS per block: four 64 x 33 transpose tiles (transpose_pl) and the
+// filter's spectrum H (32 KB), staged once per block -- the split reads H
+// from LDS instead of waiting on L2 -- 66.5 KB, as with 64 x 65 tiles alone.
 __global__ __launch_bounds__(256, 2) void fir_fft_kernel(FirFftArgs A, uint64_t fe) {
-    __shared__ __attribute__((aligned(16))) float lds_all[4][64 * 65];
+    __shared__ __attribute__((aligned(16))) float lds_all[4][64 * 33];
+    __shared__ float4 hs[2048];
+    {  // global H: [ka][lane][h] float4 -> LDS [2 ka + h][lane]
+        const float4 *H4 = reinterpret_cast<const float4 *>(A.H);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const uint32_t g = threadIdx.x + 256u * (uint32_t)i;
+            const uint32_t ka = g >> 7, ln = (g & 127u) >> 1, h = g & 1u;
+            hs[(2u * ka + h) * 64u + ln] = H4[g];
+        }
+        __syncthreads();
+    }
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t ch = blockIdx.y;
     const uint64_t f = (uint64_t)xcd_remap(blockIdx.x, gridDim.x) * 4u + wave;
     if (f >= A.F) return;
-    if (f == 0 || f >= fe) fir_fft_frame<true>(A, f, ch, lds_all[wave], lane);
-    else fir_fft_frame<false>(A, f, ch, lds_all[wave], lane);
+    if (f == 0 || f >= fe) fir_fft_frame<true>(A, f, ch, lds_all[wave], hs, lane);
+    else fir_fft_frame<false>(A, f, ch, lds_all[wave], hs, lane);
 }
 
 int launch_fir_fft(const FirFftArgs &A, uint32_t C, hipStream_t s) {
