@@ -30,13 +30,16 @@ __device__ __forceinline__ void combine64(const cx2 (&a)[32], cx (&yp)[32], cx (
     }
 }
 
-// the same combine, packed: y[k] = (Y[k], Y[k+32]) as one cx2.  The odd
-// half is twiddled in place (the even half rides along times 1), then each
-// butterfly is one v_pk_fma: (e, e) + (t, t) * (1, -1).
+// the same combine, packed: y[k] = (Y[k], Y[k+32]) as one cx2.  W64^K is
+// factored as c (1 + i tan) or s (cot + i) (kW64_lf_*, |tan|, |cot| <= 1):
+// the odd half times the unit-free factor is two scalar FMAs, and the scale
+// rides in the butterfly, one v_pk_fma per part: (e, e) + (u, u) * (c, -c).
+// 4 instructions per nontrivial K instead of 6 (a full complex multiply
+// before the butterfly).
 template <int K>
 __device__ __forceinline__ cx2 combine1(cx2 p) {
-    const v2f pm = v2f{1.f, -1.f};
-    v2f tr, ti;  // (t, t) where t = O W64^K, as splats of one register half
+    v2f tr, ti;  // (u, u), splats of one scalar
+    v2f pm = v2f{1.f, -1.f};
     if constexpr (K == 0) {
         tr = v2f{p.r.y, p.r.y};
         ti = v2f{p.i.y, p.i.y};
@@ -44,10 +47,19 @@ __device__ __forceinline__ cx2 combine1(cx2 p) {
         tr = v2f{p.i.y, p.i.y};
         ti = -v2f{p.r.y, p.r.y};
     } else {
-        const v2f w = v2f{1.f, kW64_re[K]}, s = v2f{0.f, kW64_im[K]};
-        const v2f qr = p.r * w - p.i * s, qi = p.r * s + p.i * w;  // (e, t) per part
-        tr = v2f{qr.y, qr.y};
-        ti = v2f{qi.y, qi.y};
+        const float f = kW64_lf_f[K];
+        const float orr = p.r.y, oi = p.i.y;
+        float ur, ui;
+        if constexpr ((K + 8) % 32 <= 16) {  // W = c (1 + i tan)
+            ur = __builtin_fmaf(-f, oi, orr);
+            ui = __builtin_fmaf(f, orr, oi);
+        } else {  // W = s (cot + i)
+            ur = __builtin_fmaf(f, orr, -oi);
+            ui = __builtin_fmaf(f, oi, orr);
+        }
+        tr = v2f{ur, ur};
+        ti = v2f{ui, ui};
+        pm = v2f{kW64_lf_s[K], -kW64_lf_s[K]};
     }
     return cx2{tr * pm + v2f{p.r.x, p.r.x}, ti * pm + v2f{p.i.x, p.i.x}};
 }
