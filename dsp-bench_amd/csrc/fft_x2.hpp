@@ -55,6 +55,62 @@ __device__ __forceinline__ cx2 x2tw64(cx2 a, int m) {  // a * W64^m, m compile-t
     return mulc2(a, kW64_re[m], kW64_im[m]);
 }
 
+// (a + W64^M x, a - W64^M x) with W64^M factored as c (1 + i tan) or
+// s (cot + i) (twiddles.inc kW64_lf_*): two FMAs for x times the unit-free
+// factor, four for the butterfly with the scale folded in -- 6 instructions
+// instead of a complex multiply (4) and the add/sub (4).  M % 16 == 0: adds.
+template <int M>
+__device__ __forceinline__ void x2bfly(cx2 &a, cx2 &x) {
+    constexpr int m = M & 63;
+    if constexpr (m % 16 == 0) {
+        cx2 t = x;
+        if constexpr (m == 16) t = negi(x);
+        if constexpr (m == 32) t = cx2{-x.r, -x.i};
+        if constexpr (m == 48) t = cx2{-x.i, x.r};
+        const cx2 s = a;
+        a = s + t;
+        x = s - t;
+    } else {
+        const float f = kW64_lf_f[m], c = kW64_lf_s[m];
+        v2f ur, ui;
+        if constexpr ((m + 8) % 32 <= 16) {  // W = c (1 + i tan)
+            ur = x.r - v2f{f, f} * x.i;
+            ui = x.i + v2f{f, f} * x.r;
+        } else {  // W = s (cot + i)
+            ur = v2f{f, f} * x.r - x.i;
+            ui = v2f{f, f} * x.i + x.r;
+        }
+        const v2f cc = v2f{c, c};
+        const cx2 s = a;
+        a = cx2{s.r + cc * ur, s.i + cc * ui};
+        x = cx2{s.r - cc * ur, s.i - cc * ui};
+    }
+}
+
+// DFT4 of (a, W^{2K} b, W^{4K} c, W^{6K} d), W = W64, as four factored
+// butterflies: (t0, t1) = a +- W^{4K} c, (h2, h3) = b +- W^{4K} d, then
+// X0/X2 = t0 +- W^{2K} h2, X1/X3 = t1 +- W^{2K+16} h3 (W^16 = -i).
+// 24 instructions for K with nontrivial twiddles instead of 28.
+template <int K>
+__device__ __forceinline__ void x2dft4_tw(cx2 &a, cx2 &b, cx2 &c, cx2 &d) {
+    x2bfly<4 * K>(a, c);
+    x2bfly<4 * K>(b, d);
+    x2bfly<2 * K>(a, b);
+    x2bfly<2 * K + 16>(c, d);
+    const cx2 x1 = c, x2 = b;  // positions: a = X0, b = X1, c = X2, d = X3
+    b = x1;
+    c = x2;
+}
+
+template <int K1 = 0, bool BAR = true>
+__device__ __forceinline__ void x2dft32_stage2(cx2 (&v)[32]) {
+    if constexpr (K1 < 8) {
+        if (BAR) __builtin_amdgcn_sched_barrier(0);
+        x2dft4_tw<K1>(v[4 * K1], v[4 * K1 + 1], v[4 * K1 + 2], v[4 * K1 + 3]);
+        x2dft32_stage2<K1 + 1, BAR>(v);
+    }
+}
+
 // 32-point DFT, natural order in, X[k] at v[perm32(k)] out (8 x 4).
 // BAR: pin one DFT8 / DFT4 at a time (bounds register pressure, costs ILP).
 template <bool BAR = true>
@@ -65,15 +121,7 @@ __device__ __forceinline__ void x2dft32(cx2 (&v)[32]) {
         x2dft8(v[j2], v[4 + j2], v[8 + j2], v[12 + j2], v[16 + j2], v[20 + j2], v[24 + j2],
                v[28 + j2]);
     }
-#pragma unroll
-    for (int k1 = 1; k1 < 8; ++k1)
-#pragma unroll
-        for (int j2 = 1; j2 < 4; ++j2) v[4 * k1 + j2] = x2tw64(v[4 * k1 + j2], 2 * j2 * k1);
-#pragma unroll
-    for (int k1 = 0; k1 < 8; ++k1) {
-        if (BAR) __builtin_amdgcn_sched_barrier(0);
-        x2dft4(v[4 * k1], v[4 * k1 + 1], v[4 * k1 + 2], v[4 * k1 + 3]);
-    }
+    x2dft32_stage2<0, BAR>(v);
     __builtin_amdgcn_sched_barrier(0);
 }
 
