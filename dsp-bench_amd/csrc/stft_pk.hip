@@ -40,12 +40,14 @@ enum { kPkNoBarDft = 1, kPkNoBarTw = 2, kPkNoBarSplit = 4, kPkRenderCached = 8, 
 // 1024 = 3 waves per SIMD (OCC template argument): fft4096_pk_y2_lo's
 // 64 x 33 transpose tile and just-in-time stage twiddles
 // 512 = split_y2 stages the row in LDS at the row's 16-byte phase and stores
-// it as aligned 16-byte pieces (16 dwordx4 + <= 7 dwords instead of 65 dwords)
+// it as aligned 16-byte pieces (16 dwordx4 + <= 7 dwords instead of 65 dwords);
+// with 16, those pieces are non-temporal stores
 // 128 / 256: ablation only (A/B of what the stores cost): skip the render
 // stores / the magnitude stores of split_y2 (results discarded)
 constexpr int kPkDefaultOpt = 0;
 
 typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));  // a row is only dword-aligned
+typedef float f4a __attribute__((ext_vector_type(4)));               // 16-byte aligned
 
 template <bool NT, typename T>
 __device__ __forceinline__ void st(T *p, T v) {
@@ -82,7 +84,7 @@ __device__ __forceinline__ void put_bin(float *mrow, uint32_t K, uint32_t k, flo
 // and bin 2048 with itself).  Bins 1024 / 3072 (lane 0, Y2[16]) are left
 // over and done at the end.  Bins per iteration: l + 64 q, 2048 + l + 64 q,
 // 4096 - l - 64 q, 2048 - l - 64 q.
-template <int KM, bool BAR, bool NOSTORE = false, bool STAGE = false>
+template <int KM, bool BAR, bool NOSTORE = false, bool STAGE = false, bool STAGE_NT = false>
 __device__ __forceinline__ void split_y2(const cx2 (&Y2)[32], float *mrow, uint32_t K, const v2f *tw,
                                          uint32_t lane, float *lds) {
     static_assert(!STAGE || KM == kKHalf, "staged rows: 4097 bins");
@@ -171,7 +173,10 @@ __device__ __forceinline__ void split_y2(const cx2 (&Y2)[32], float *mrow, uint3
         for (int it = 0; it < 16; ++it) {
             const uint32_t j = j0 + 64u * (uint32_t)it + lane;
             if (it < 15 || j <= j1)
-                *reinterpret_cast<float4 *>(gb + 4u * j) = reinterpret_cast<const float4 *>(lds)[j];
+            {
+                const float4 q = reinterpret_cast<const float4 *>(lds)[j];
+                st<STAGE_NT>(reinterpret_cast<f4a *>(gb + 4u * j), f4a{q.x, q.y, q.z, q.w});
+            }
         }
         // head bins [0, 4 j0 - a) and tail bins [4 j1 + 4 - a, 4097): at most 3 + 4
         const uint32_t head = 4u * j0 - a, tail0 = 4u * j1 + 4u - a;
@@ -380,8 +385,8 @@ __global__ __launch_bounds__(256, OCC) void stft8192_pk_kernel(Stft8kArgs A) {
         cx2 Y2[32];
         if constexpr (OCC >= 3) fft4096_pk_y2_lo<!(OPT & kPkNoBarDft)>(P, lds, A.tw, lane, Y2);
         else fft4096_pk_y2<!(OPT & kPkNoBarDft), !(OPT & kPkNoBarTw)>(P, lds, tlo, thp, lane, Y2);
-        split_y2<KM, !(OPT & kPkNoBarSplit), (OPT & kPkAbNoMag) != 0, KM == kKHalf && (OPT & kPkMagStage) != 0>(
-            Y2, A.mag.p[ch] + f * A.ld, A.K, A.tw, lane, lds);
+        split_y2<KM, !(OPT & kPkNoBarSplit), (OPT & kPkAbNoMag) != 0, KM == kKHalf && (OPT & kPkMagStage) != 0,
+                 (OPT & kPkNtMag) != 0>(Y2, A.mag.p[ch] + f * A.ld, A.K, A.tw, lane, lds);
         return;
     }
 
@@ -543,6 +548,7 @@ int launch_stft8192_pk(const Stft8kArgs &A, uint32_t C, bool fused, int opt, hip
                     DSPB_PK_CASE(kPkRenderCached);
                     DSPB_PK_CASE(kPkMagStage);
                     DSPB_PK_CASE(kPkMagStage | kPkRenderCached);
+                    DSPB_PK_CASE(kPkMagStage | kPkNtMag);
                     DSPB_PK_CASE(kPkOldSplit);
                     DSPB_PK_CASE(kPkOldSplit | kPkRenderCached);
                     DSPB_PK_CASE(kPkOldSplit | kPkNtMag);
