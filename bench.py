@@ -208,6 +208,16 @@ def main():
     L_in = sh.read_len
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     x = (torch.rand((CH, L_in), device=dev, generator=g) * 2 - 1) * 0.1  # synthetic WAV
+    # the 10-minute files (230 MB per channel pair) would fit the 256 MiB
+    # Infinity Cache between steps; steps rotate over NX copies so that every
+    # step reads its input from HBM, as a one-pass offline render does
+    NX = 4 if wl in ("gain10min", "fir1024") else 1
+    xs = [x] + [x.clone() for _ in range(NX - 1)]
+    rot = [0]
+
+    def next_x():
+        rot[0] = (rot[0] + 1) % NX
+        return xs[rot[0]]
     nb = d.num_blocks(L_in, B)
     F = d.stft_frames(nb * B if wl in ("headline", "ch96k") else L_in, N_FFT, HOP)
     out = torch.empty((CH, nb * B), device=dev) if wl in ("headline", "ch96k", "gain10min", "fir1024") else None
@@ -251,7 +261,7 @@ def main():
         alg_desc = "C*L*(4 + 4) B (each input sample read once + each output sample written once)"
 
         def step():
-            d.render_offline(x, CH, B, float(sr), fplug, out=out)
+            d.render_offline(next_x(), CH, B, float(sr), fplug, out=out)
         ols = d.lib().dsp_fir_method(-1) != 1
         workload = (f"FIR render, 1024 taps = compute_IR(IR_test)[0:1024], B=512, {minutes:g} min of "
                     f"48 kHz stereo per GPU (cfg 3b), {'FFT overlap-save' if ols else 'direct form'}")
@@ -262,7 +272,7 @@ def main():
             alg_flops = 2.0 * 1024 * CH * nb * B
     elif wl == "gain10min":
         def step():
-            d.render_offline(x, CH, B, float(sr), plugin, out=out)
+            d.render_offline(next_x(), CH, B, float(sr), plugin, out=out)
         workload = f"gain_test render (B=512), {minutes:g} min of 48 kHz stereo per GPU (cfg 2)"
         kname = "render_vec_kernel<Gain>"
         alg_bytes = CH * L_in * 8  # read + write
@@ -367,7 +377,9 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": ("synthetic (uniform noise WAV in HBM; IR_test output is input-independent)"
-                     if wl in ("headline", "ch96k") else "synthetic (uniform noise in HBM)"),
+                     if wl in ("headline", "ch96k") else
+                     f"synthetic (uniform noise in HBM; {NX} input copies used in rotation, past the Infinity Cache)"
+                     if NX > 1 else "synthetic (uniform noise in HBM)"),
             "config": {
                 "workload": workload,
                 "plugin": plug_name,

@@ -13,8 +13,8 @@
 //     out[c][i]  = callback(base)[c][i]
 //
 // For the stock plugins whose callback is a per-sample map that rule is one
-// streaming kernel: 16-byte loads and stores, four float4 per thread in
-// flight, grid-stride over a capped grid (HBM-bound, no reuse to tile for).
+// streaming kernel: 16-byte loads and non-temporal stores, four float4 per
+// thread in flight, one tile per block (HBM-bound, no reuse to tile for).
 //
 // IR_test's callback is a sequential double recurrence that restarts at
 // every block (build/IR_test.cpp:47-58), so its output is input-independent
@@ -57,26 +57,34 @@ __device__ __forceinline__ float4 render4(const RenderArgs &A, const float *x, u
                        apply_map(m, b.z, g + 2), apply_map(m, b.w, g + 3));
 }
 
-// Vector path: start % 4 == 0 and every pointer 16-byte aligned.
+// Vector path: start % 4 == 0 and every pointer 16-byte aligned.  One tile
+// of 256 x kVecU float4 per block (no grid-stride loop: the tile's loads all
+// issue before its first store), non-temporal 16-byte stores (the render is
+// written once and not read back by this call).  tools/copy_probe.hip: this
+// shape streams y = g x at 5.6-5.8 TB/s where a grid-stride loop over a
+// capped grid reached 4.6-4.8 (inputs rotated past the Infinity Cache).
+constexpr int kVecU = 4;
+typedef float f4nt __attribute__((ext_vector_type(4)));
 template <MapKind K>
 __global__ __launch_bounds__(256) void render_vec_kernel(RenderArgs A) {
-    constexpr int U = 4;
     const uint32_t c = blockIdx.y;
     const float *x = (c < A.in_ch) ? A.in.p[c] : nullptr;
     float *o = A.out.p[c];
     const uint64_t n4 = (A.end - A.start) >> 2;
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    for (; q + (U - 1) * stride < n4; q += U * stride) {
-        float4 r[U];
+    const uint64_t q0 = (uint64_t)blockIdx.x * (256u * kVecU) + threadIdx.x;
+    float4 r[kVecU];
 #pragma unroll
-        for (int u = 0; u < U; ++u) r[u] = render4<K>(A, x, A.start + 4 * (q + u * stride));
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-            *reinterpret_cast<float4 *>(o + A.start + 4 * (q + u * stride)) = r[u];
+    for (int u = 0; u < kVecU; ++u) {
+        const uint64_t q = q0 + 256u * (uint32_t)u;
+        if (q < n4) r[u] = render4<K>(A, x, A.start + 4 * q);
     }
-    for (; q < n4; q += stride)
-        *reinterpret_cast<float4 *>(o + A.start + 4 * q) = render4<K>(A, x, A.start + 4 * q);
+#pragma unroll
+    for (int u = 0; u < kVecU; ++u) {
+        const uint64_t q = q0 + 256u * (uint32_t)u;
+        if (q < n4)
+            __builtin_nontemporal_store(f4nt{r[u].x, r[u].y, r[u].z, r[u].w},
+                                        reinterpret_cast<f4nt *>(o + A.start + 4 * q));
+    }
     // scalar tail (end - start not a multiple of 4)
     if (blockIdx.x == 0 && threadIdx.x < ((A.end - A.start) & 3)) {
         const uint64_t i = A.start + 4 * n4 + threadIdx.x;
@@ -137,10 +145,16 @@ int launch_ramp_table(float *table, uint32_t B, float gain, float step, hipStrea
 
 int launch_render(const RenderArgs &A, uint32_t C, bool vec, hipStream_t s) {
     if (A.end <= A.start || C == 0) return DSP_OK;
-    const uint64_t items = vec ? (A.end - A.start + 3) / 4 : (A.end - A.start);
-    uint32_t gx = stream_grid(items);
-    gx = (gx + C - 1) / C;  // keep ~2048 blocks in total across channels
-    if (gx == 0) gx = 1;
+    uint32_t gx;
+    if (vec) {  // one block per 256 x kVecU float4 of every channel
+        const uint64_t tiles = ((A.end - A.start) / 4 + 256u * kVecU - 1) / (256u * kVecU);
+        if (tiles > 0x7fffffffull) return DSP_ERR_INVALID;
+        gx = tiles ? (uint32_t)tiles : 1u;
+    } else {
+        gx = stream_grid(A.end - A.start);
+        gx = (gx + C - 1) / C;  // keep ~2048 blocks in total across channels
+        if (gx == 0) gx = 1;
+    }
     dim3 grid(gx, C), block(256);
 #define DSPB_RENDER_CASE(KIND)                                                            \
     case KIND:                                                                            \
