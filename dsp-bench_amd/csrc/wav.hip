@@ -13,8 +13,8 @@
 // HBM-bound byte work: each thread converts 4 whole frames, reading their
 // interleaved payload as dwords (4 frames x C x bytes is always a dword
 // multiple) and writing one float4 per channel; mono / stereo are
-// specialised, other channel counts and unaligned starts use per-sample
-// byte loads.
+// specialised (wav_decode_tile_kernel), other channel counts and unaligned
+// starts use per-sample byte loads.
 #include "kernels.hpp"
 
 namespace dspb {
@@ -95,6 +95,60 @@ __global__ __launch_bounds__(256) void wav_decode_kernel(WavArgs A) {
     }
 }
 
+// Mono / stereo fast path: one tile of 256 x kWavU groups of 4 frames per
+// block (all of a thread's payload loads issue before its first store), 16- or
+// 8-byte payload loads when the payload start allows (LDW dwords per load),
+// non-temporal float4 stores (the planar output is written once).
+constexpr int kWavU = 4;
+typedef float f4w __attribute__((ext_vector_type(4)));
+template <int BITS, bool FLT, int CH, int LDW>
+__global__ __launch_bounds__(256) void wav_decode_tile_kernel(WavArgs A) {
+    constexpr int BPS = BITS / 8;
+    constexpr int W = CH * BPS;  // dwords of 4 frames
+    static_assert(W % LDW == 0, "load width");
+    const uint64_t g0 = blockIdx.x * (256ull * kWavU) + threadIdx.x;
+    uint32_t w[kWavU][W + 1];
+#pragma unroll
+    for (int u = 0; u < kWavU; ++u) {
+        const uint64_t f = 4 * (g0 + 256u * (uint32_t)u);
+        w[u][W] = 0;
+        if (f + 4 <= A.frames) {
+            const uint8_t *src = A.payload + (A.frame0 + f) * (uint64_t)W;
+#pragma unroll
+            for (int i = 0; i < W; i += LDW) {
+                if constexpr (LDW == 4) {
+                    const uint4 q = *reinterpret_cast<const uint4 *>(src + 4 * i);
+                    w[u][i] = q.x, w[u][i + 1] = q.y, w[u][i + 2] = q.z, w[u][i + 3] = q.w;
+                } else if constexpr (LDW == 2) {
+                    const uint2 q = *reinterpret_cast<const uint2 *>(src + 4 * i);
+                    w[u][i] = q.x, w[u][i + 1] = q.y;
+                } else {
+                    w[u][i] = *reinterpret_cast<const uint32_t *>(src + 4 * i);
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < kWavU; ++u) {
+        const uint64_t f = 4 * (g0 + 256u * (uint32_t)u);
+        if (f + 4 <= A.frames) {
+#pragma unroll
+            for (int c = 0; c < CH; ++c) {
+                const f4w o = f4w{pcm_to_float<BITS, FLT>(extract<BITS>(w[u], 0 * CH + c)),
+                                  pcm_to_float<BITS, FLT>(extract<BITS>(w[u], 1 * CH + c)),
+                                  pcm_to_float<BITS, FLT>(extract<BITS>(w[u], 2 * CH + c)),
+                                  pcm_to_float<BITS, FLT>(extract<BITS>(w[u], 3 * CH + c))};
+                __builtin_nontemporal_store(o, reinterpret_cast<f4w *>(A.pl.p[c] + f));
+            }
+        } else if (f < A.frames) {  // the last, partial group
+            for (uint64_t ff = f; ff < A.frames; ++ff)
+                for (uint32_t c = 0; c < (uint32_t)CH; ++c)
+                    A.pl.p[c][ff] = pcm_to_float<BITS, FLT>(
+                        load_raw<BITS>(A.payload + ((A.frame0 + ff) * CH + c) * (uint64_t)BPS));
+        }
+    }
+}
+
 template <int BITS, bool FLT>
 __device__ __forceinline__ uint32_t float_to_pcm(float x) {
     if constexpr (FLT) {
@@ -138,12 +192,36 @@ static dim3 grid_for(uint64_t items) {
     return dim3((uint32_t)(g ? g : 1));
 }
 
+template <int BITS, bool FLT, int CH>
+static void dec_tile(const WavArgs &A, dim3 grid, hipStream_t s) {
+    constexpr int W = CH * BITS / 8;
+    const uintptr_t start = reinterpret_cast<uintptr_t>(A.payload) + A.frame0 * (uint64_t)W;
+    // every group starts W dwords after the previous one
+    if constexpr (W % 4 == 0) {
+        if (start % 16 == 0) {
+            hipLaunchKernelGGL((wav_decode_tile_kernel<BITS, FLT, CH, 4>), grid, dim3(256), 0, s, A);
+            return;
+        }
+    }
+    if constexpr (W % 2 == 0) {
+        if (start % 8 == 0) {
+            hipLaunchKernelGGL((wav_decode_tile_kernel<BITS, FLT, CH, 2>), grid, dim3(256), 0, s, A);
+            return;
+        }
+    }
+    hipLaunchKernelGGL((wav_decode_tile_kernel<BITS, FLT, CH, 1>), grid, dim3(256), 0, s, A);
+}
+
 template <int BITS, bool FLT>
 static void dec(const WavArgs &A, bool vec, hipStream_t s) {
-    const dim3 grid = grid_for((A.frames + 3) / 4);
-    if (vec && A.C == 1) hipLaunchKernelGGL((wav_decode_kernel<BITS, FLT, 1>), grid, dim3(256), 0, s, A);
-    else if (vec && A.C == 2) hipLaunchKernelGGL((wav_decode_kernel<BITS, FLT, 2>), grid, dim3(256), 0, s, A);
-    else hipLaunchKernelGGL((wav_decode_kernel<BITS, FLT, 0>), grid, dim3(256), 0, s, A);
+    if (vec && (A.C == 1 || A.C == 2)) {
+        const uint64_t tiles = ((A.frames + 3) / 4 + 256u * kWavU - 1) / (256u * kWavU);
+        const dim3 grid((uint32_t)(tiles ? tiles : 1));
+        if (A.C == 1) dec_tile<BITS, FLT, 1>(A, grid, s);
+        else dec_tile<BITS, FLT, 2>(A, grid, s);
+        return;
+    }
+    hipLaunchKernelGGL((wav_decode_kernel<BITS, FLT, 0>), grid_for((A.frames + 3) / 4), dim3(256), 0, s, A);
 }
 
 int launch_wav_decode(const uint8_t *payload, uint32_t C, uint16_t bits, bool is_float, uint64_t frame0,
