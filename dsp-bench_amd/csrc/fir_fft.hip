@@ -14,7 +14,8 @@
 //             E = Y[k] + conj Y[M-k], O = (Y[k] - conj Y[M-k]) W8192^-k --
 //             the M-k half sent back to its owner lane with ds_bpermute,
 //             then the packed 4096-point inverse (fft4096_pk<true>)
-//   store     y[2m] = Re z'[m], y[2m+1] = Im z'[m] for m >= 512
+//   store     y[2m] = Re z'[m], y[2m+1] = Im z'[m] for m >= 512 (non-temporal:
+//             the render is written once)
 //
 // tools/olsave_model.py is the numpy model of exactly this index math.
 #include "fft_pk.hpp"
@@ -159,7 +160,7 @@ __device__ __forceinline__ void fir_fft_frame(const FirFftArgs &A, uint64_t f, u
 #pragma unroll
         for (int b = 8; b < 64; ++b) {
             const cx z = b < 32 ? yp[b] : ym[b - 32];
-            *reinterpret_cast<v2f *>(o + ob + 128u * (uint32_t)(b - 8)) = v2f{z.r, z.i};
+            __builtin_nontemporal_store(v2f{z.r, z.i}, reinterpret_cast<v2f *>(o + ob + 128u * (uint32_t)(b - 8)));
         }
     } else {
 #pragma unroll
