@@ -41,7 +41,8 @@ enum { kPkNoBarDft = 1, kPkNoBarTw = 2, kPkNoBarSplit = 4, kPkRenderCached = 8, 
 // 64 x 33 transpose tile and just-in-time stage twiddles
 // 512 = split_y2 stages the row in LDS at the row's 16-byte phase and stores
 // it as aligned 16-byte pieces (16 dwordx4 + <= 7 dwords instead of 65 dwords);
-// with 16, those pieces are non-temporal stores
+// with 16, those pieces are non-temporal stores (16 alone: split_y2's
+// dword row stores non-temporal)
 // 128 / 256: ablation only (A/B of what the stores cost): skip the render
 // stores / the magnitude stores of split_y2 (results discarded)
 constexpr int kPkDefaultOpt = 0;
@@ -133,10 +134,10 @@ __device__ __forceinline__ void split_y2(const cx2 (&Y2)[32], float *mrow, uint3
             (sl + 4096u - lane)[-64 * q] = __builtin_amdgcn_sqrtf(q2.x);
             (sl + 2048u - lane)[-64 * q] = __builtin_amdgcn_sqrtf(q2.y);
         } else if constexpr (KM == kKHalf) {  // four lane-based row pointers, constant offsets
-            (mrow + lane)[64 * q] = __builtin_amdgcn_sqrtf(q1.x);
-            (mrow + 2048u + lane)[64 * q] = __builtin_amdgcn_sqrtf(q1.y);
-            (mrow + 4096u - lane)[-64 * q] = __builtin_amdgcn_sqrtf(q2.x);
-            (mrow + 2048u - lane)[-64 * q] = __builtin_amdgcn_sqrtf(q2.y);
+            st<STAGE_NT>(&(mrow + lane)[64 * q], __builtin_amdgcn_sqrtf(q1.x));
+            st<STAGE_NT>(&(mrow + 2048u + lane)[64 * q], __builtin_amdgcn_sqrtf(q1.y));
+            st<STAGE_NT>(&(mrow + 4096u - lane)[-64 * q], __builtin_amdgcn_sqrtf(q2.x));
+            st<STAGE_NT>(&(mrow + 2048u - lane)[-64 * q], __builtin_amdgcn_sqrtf(q2.y));
         } else {
             put_bin<KM>(mrow, K, k, __builtin_amdgcn_sqrtf(q1.x));
             put_bin<KM>(mrow, K, 2048u + k, __builtin_amdgcn_sqrtf(q1.y));
@@ -549,6 +550,7 @@ int launch_stft8192_pk(const Stft8kArgs &A, uint32_t C, bool fused, int opt, hip
                     DSPB_PK_CASE(kPkMagStage);
                     DSPB_PK_CASE(kPkMagStage | kPkRenderCached);
                     DSPB_PK_CASE(kPkMagStage | kPkNtMag);
+                    DSPB_PK_CASE(kPkNtMag);
                     DSPB_PK_CASE(kPkOldSplit);
                     DSPB_PK_CASE(kPkOldSplit | kPkRenderCached);
                     DSPB_PK_CASE(kPkOldSplit | kPkNtMag);
