@@ -28,6 +28,8 @@ namespace {
 
 #include "plugin_device_src.inc"  // const char kPluginDeviceSrc[] (generated from plugin_device.h)
 
+constexpr uint64_t kStagedLdsBytes = 64 * 1024;  // stateful render's LDS double-buffer limit
+
 // Host mirror of the driver's argument block (same layout on both sides).
 struct RenderArgsG {
     void *P;
@@ -41,6 +43,7 @@ struct RenderArgsG {
     unsigned C;
     unsigned B;
     float sr;
+    unsigned lds;  // stateful: the block double-buffer lives in LDS (2 C B floats)
 };
 
 const char *kDriver = R"DSPB(
@@ -56,6 +59,7 @@ struct dspb_render_args {
     unsigned C;
     unsigned B;
     float sr;
+    unsigned lds;
 };
 extern "C" __global__ void dspb_sizes(unsigned *o) {
     o[0] = sizeof(Parameters);
@@ -82,15 +86,60 @@ __device__ static void dspb_block(const dspb_render_args &A, unsigned long long 
     (void)s0;
     audio_callback(*(Parameters *)A.P, st, ptrs, A.C, A.B, A.sr);
 }
+// render_audio's copy of block b into a staging buffer (zero past EOF and
+// for the channels the file lacks), element j of every (n0 + k*nt) stride
+__device__ static void dspb_stage_in(const dspb_render_args &A, unsigned long long b, float *buf, unsigned j0,
+                                     unsigned nt) {
+    const unsigned CB = A.C * A.B;
+    for (unsigned j = j0; j < CB; j += nt) {
+        const unsigned c = j / A.B, s = j - c * A.B;
+        const unsigned long long i = b * A.B + s;
+        buf[j] = (c < A.in_ch && i < A.L) ? A.in[c][i] : 0.0f;
+    }
+}
+__device__ static void dspb_stage_out(const dspb_render_args &A, unsigned long long b, const float *buf,
+                                      unsigned j0, unsigned nt) {
+    const unsigned CB = A.C * A.B;
+    for (unsigned j = j0; j < CB; j += nt) {
+        const unsigned c = j / A.B, s = j - c * A.B;
+        A.out[c][b * A.B + s] = buf[j];
+    }
+}
 extern "C" __global__ void dspb_render(dspb_render_args A) {
+    extern __shared__ float dspb_lbuf[];
     if (__is_empty(State)) {  // no state: every block on its own thread
         State local = *(State *)A.S;
         for (unsigned long long b = blockIdx.x * (unsigned long long)blockDim.x + threadIdx.x; b < A.nblocks;
              b += (unsigned long long)gridDim.x * blockDim.x)
             dspb_block(A, b, local);
-    } else if (blockIdx.x == 0 && threadIdx.x == 0) {  // stateful: in order, one thread
+    } else if (!A.lds) {  // stateful, blocks too large for LDS: in order, one thread
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            State &st = *(State *)A.S;
+            for (unsigned long long b = 0; b < A.nblocks; ++b) dspb_block(A, b, st);
+        }
+    } else if (blockIdx.x == 0) {
+        // stateful, in order: thread 0 runs the callback on block b in LDS
+        // while waves 1.. write block b - 1 out and stage block b + 1 in the
+        // other half of the double buffer (the same elements per thread, so
+        // no element is overwritten before it is written out)
         State &st = *(State *)A.S;
-        for (unsigned long long b = 0; b < A.nblocks; ++b) dspb_block(A, b, st);
+        const unsigned CB = A.C * A.B, t = threadIdx.x, nt = blockDim.x;
+        float *buf0 = dspb_lbuf, *buf1 = dspb_lbuf + CB;
+        dspb_stage_in(A, 0, buf0, t, nt);
+        __syncthreads();
+        for (unsigned long long b = 0; b < A.nblocks; ++b) {
+            float *cur = (b & 1) ? buf1 : buf0, *oth = (b & 1) ? buf0 : buf1;
+            if (t == 0) {
+                float *ptrs[16];
+                for (unsigned c = 0; c < A.C; ++c) ptrs[c] = cur + c * A.B;
+                audio_callback(*(Parameters *)A.P, st, ptrs, A.C, A.B, A.sr);
+            } else if (t >= 64) {
+                if (b > 0) dspb_stage_out(A, b - 1, oth, t - 64, nt - 64);
+                if (b + 1 < A.nblocks) dspb_stage_in(A, b + 1, oth, t - 64, nt - 64);
+            }
+            __syncthreads();
+        }
+        dspb_stage_out(A, A.nblocks - 1, (A.nblocks - 1) & 1 ? buf1 : buf0, t, nt);
     }
 }
 // compute_IR (plugin.cpp:17-58): the callback once, on buffers as they are
@@ -393,13 +442,19 @@ int module_render(dsp_module *m, const void *params, uint32_t params_size, const
     A.sr = sr;
     if (A.nblocks == 0) return DSP_OK;
     void *args[] = {&A};
-    unsigned grid = 1, block = 1;
+    unsigned grid = 1, block = 1, lds_bytes = 0;
     if (m->stateless) {
         block = 64;
         const uint64_t g = (A.nblocks + 63) / 64;
         grid = (unsigned)(g < 65535 ? g : 65535);
+    } else if (2ull * C * B * sizeof(float) <= kStagedLdsBytes) {
+        // stateful: 4 waves, the block double-buffer in LDS (the callback's
+        // loads and stores hit LDS, the copies run on 192 lanes beside it)
+        A.lds = 1;
+        block = 256;
+        lds_bytes = (unsigned)(2ull * C * B * sizeof(float));
     }
-    MOD_HIP(hipModuleLaunchKernel(m->f_render, grid, 1, 1, block, 1, 1, 0, s, args, nullptr));
+    MOD_HIP(hipModuleLaunchKernel(m->f_render, grid, 1, 1, block, 1, 1, lds_bytes, s, args, nullptr));
     MOD_HIP(hipStreamSynchronize(s));  // the params blob is the caller's
     return DSP_OK;
 }

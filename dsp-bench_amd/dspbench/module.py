@@ -37,6 +37,8 @@ class Module:
 
     def __init__(self, code: bytes, device: int = -1):
         self.handle = C.c_void_p()
+        # bound now: at interpreter exit the module globals may already be gone
+        self._destroy = L.lib().dsp_module_destroy
         self._code = C.create_string_buffer(code, len(code))
         check(L.lib().dsp_module_load(self._code, len(code), device, C.byref(self.handle)), "dsp_module_load")
         ps, ss, sl = C.c_uint32(), C.c_uint32(), C.c_int()
@@ -45,8 +47,9 @@ class Module:
 
     def __del__(self):
         h = getattr(self, "handle", None)
-        if h:
-            L.lib().dsp_module_destroy(h)
+        destroy = getattr(self, "_destroy", None)
+        if h and destroy is not None:
+            destroy(h)
             self.handle = None
 
     def default_parameters(self) -> bytes:

@@ -21,6 +21,9 @@ PLUGINS = ["build/gain_test", "build/IR_test", "build/sine_test", "build/buffer_
            "test/plugin_with_parameters"]
 
 
+LIB = os.path.join(HERE, "..", "dsp-bench_amd", "libdspbench.so")
+
+
 def main():
     ref = sys.argv[1] if len(sys.argv) > 1 else "/root/reference"
     import dspbench.module as m
@@ -29,7 +32,10 @@ def main():
     for p in PLUGINS:
         src = os.path.join(ref, p + ".cpp")
         dst = os.path.join(out, f"mod_{os.path.basename(p)}.co")
-        if os.path.exists(dst) and os.path.getmtime(dst) >= os.path.getmtime(src):
+        # the driver kernels (csrc/module.cpp) are compiled into every module:
+        # rebuild when the library is newer too
+        newest = max(os.path.getmtime(src), os.path.getmtime(LIB)) if os.path.exists(LIB) else os.path.getmtime(src)
+        if os.path.exists(dst) and os.path.getmtime(dst) >= newest:
             continue
         code = m.compile_source(open(src).read(), os.path.basename(p))
         with open(dst, "wb") as f:
