@@ -34,7 +34,8 @@ namespace dspb {
 // fewer per frame, the same bits)
 enum { kPkNoBarDft = 1, kPkNoBarTw = 2, kPkNoBarSplit = 4, kPkRenderCached = 8, kPkNtMag = 16, kPkMagLds = 32,
        kPkOldSplit = 64, kPkAbNoRender = 128, kPkAbNoMag = 256, kPkMagStage = 512, kPkOcc3 = 1024,
-       kPkMemAos = 2048 };
+       kPkMemAos = 2048, kPkNoRemap = 4096 };
+// 4096 = frames in dispatch order (no XCD remap: all XCDs write one frontier)
 // 2048 = memory frames (computed window) loaded as 64 pairs and regrouped
 // after the window multiply (the older path; default: regrouped at the load)
 // 1024 = 3 waves per SIMD (OCC template argument): fft4096_pk_y2_lo's
@@ -196,7 +197,7 @@ __global__ __launch_bounds__(256, OCC) void stft8192_pk_kernel(Stft8kArgs A) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t ch = blockIdx.y;
-    const uint64_t f = (uint64_t)xcd_remap(blockIdx.x, gridDim.x) * 4u + wave;
+    const uint64_t f = (uint64_t)((OPT & kPkNoRemap) ? blockIdx.x : xcd_remap(blockIdx.x, gridDim.x)) * 4u + wave;
     constexpr bool SOA = WINC && MK == MapKind::Ramp && PER > 0 && SRC == kSrcRender;
     // memory frames with the computed window: two dwordx2 loads per pair
     // (columns 2j, 2j+1) regrouped into even/odd halves
@@ -551,6 +552,7 @@ int launch_stft8192_pk(const Stft8kArgs &A, uint32_t C, bool fused, int opt, hip
                     DSPB_PK_CASE(kPkMagStage | kPkRenderCached);
                     DSPB_PK_CASE(kPkMagStage | kPkNtMag);
                     DSPB_PK_CASE(kPkNtMag);
+                    DSPB_PK_CASE(kPkNoRemap);
                     DSPB_PK_CASE(kPkOldSplit);
                     DSPB_PK_CASE(kPkOldSplit | kPkRenderCached);
                     DSPB_PK_CASE(kPkOldSplit | kPkNtMag);
