@@ -322,6 +322,19 @@ def main():
     lib.dsp_kernel_timing(C.byref(k_ms), C.byref(k_n), C.byref(k_bytes))
     ev_ms = ev0.elapsed_time(ev1)
 
+    # the per-step distribution (median, p10 / p90), from a
+    # separate pass with an event after every step -- those events cost a few
+    # us per step, so they stay out of the timed region above
+    nd = min(args.steps, 50)
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(nd + 1)]
+    evs[0].record(stream)
+    for i in range(nd):
+        step()
+        evs[i + 1].record(stream)
+    torch.cuda.synchronize()
+    per_step = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(nd))
+    pct = lambda q: per_step[min(len(per_step) - 1, int(q * (len(per_step) - 1) + 0.5))]
+
     step_s = max(wall, ev_ms / 1e3) / args.steps
     t = torch.tensor([step_s], dtype=torch.float64, device=dev)
     if world > 1:
@@ -388,6 +401,8 @@ def main():
                 "sharding": ("one channel per GPU, no data-path collective" if wl == "ch96k" else
                              "time-chunk per GPU, 4096-sample halo, no data-path collective"),
                 "gather_ms": None if gather_ms is None else round(gather_ms, 3),
+                "step_ms_p10_p50_p90": [round(pct(0.1), 4), round(pct(0.5), 4), round(pct(0.9), 4)],
+                "step_ms_distribution": f"{nd} further steps, one event after each (outside the timed region)",
             },
             "roofline": ({
                 "bound": "fp32-vector",

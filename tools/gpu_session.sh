@@ -36,10 +36,11 @@ if [[ $mode == bench || $mode == all || $mode == prof ]]; then
     run bench 600 python bench.py
 fi
 if [[ $mode == prof || $mode == all ]]; then
-    # the bench's own launch count (100 warmup + 200 timed), so the trace's
-    # last-200 average is the number bench.py reports as kernel_avg_ms
+    # the bench's own launch count (100 warmup + 200 timed + 50 for the
+    # per-step distribution), so the trace's average over launches 100..299
+    # is the number bench.py reports as kernel_avg_ms
     run rocprof_stats 600 rocprofv3 --kernel-trace --stats -d $out/prof_$tag -o run --output-format csv -- python bench.py --no-cpu-baseline
-    python tools/trace_avg.py $out/prof_$tag/run_kernel_trace.csv stft8192_pk 200 | tee $out/prof_$tag/trace_avg.txt
+    python tools/trace_avg.py $out/prof_$tag/run_kernel_trace.csv stft8192_pk 200 100 | tee $out/prof_$tag/trace_avg.txt
 fi
 if [[ $mode == others || $others == 1 ]]; then
     for wl in gain10min stft96k ch96k fir1024 wav16 wav24; do
