@@ -175,9 +175,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal of the N > 1 path on a one-GPU box: every rank on cuda:0 and
+    # gloo for the barrier / max-reduce (DSPB_BENCH_REHEARSAL=1); the real
+    # multi-GPU run is one rank per GPU over RCCL
+    rehearsal = os.environ.get("DSPB_BENCH_REHEARSAL") == "1"
+    if rehearsal:
+        local = 0
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if rehearsal:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -336,7 +345,7 @@ def main():
     pct = lambda q: per_step[min(len(per_step) - 1, int(q * (len(per_step) - 1) + 0.5))]
 
     step_s = max(wall, ev_ms / 1e3) / args.steps
-    t = torch.tensor([step_s], dtype=torch.float64, device=dev)
+    t = torch.tensor([step_s], dtype=torch.float64, device="cpu" if rehearsal else dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     step_s = float(t.item())
