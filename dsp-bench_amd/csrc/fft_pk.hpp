@@ -169,7 +169,7 @@ __device__ __forceinline__ void transpose_pl(const cx2 (&Q)[32], float *lds, uin
 // Everything up to the last combine: R holds the second DFT64's even/odd
 // DFT32 halves (combine64p / combine64_dir finish it).
 // PL: the transpose goes through transpose_pl's 64 x 33 tile.
-template <bool INV, bool BAR_DFT, bool BAR_TW, bool PL = false>
+template <bool INV, bool BAR_DFT, bool BAR_TW, bool PL = false, bool AB_NOXP = false>
 __device__ __forceinline__ void fft4096_pk_front(cx2 (&P)[32], float *lds, const cx (&tlo)[8], const cx2 (&thp)[4],
                                                  uint32_t lane, cx2 (&R)[32]) {
     // DFT64 over the register index: even/odd DFT32 in the halves, combine
@@ -190,6 +190,12 @@ __device__ __forceinline__ void fft4096_pk_front(cx2 (&P)[32], float *lds, const
     // R[j] = (t[2j], t[2j+1]), t[a] = row a of column l
     if constexpr (PL) {
         transpose_pl(Q, lds, lane, R);
+        x2dft32_dir<BAR_DFT, INV>(R);
+        return;
+    }
+    if constexpr (AB_NOXP) {  // ablation only (wrong results): the transpose's cost
+#pragma unroll
+        for (int j = 0; j < 32; ++j) R[j] = Q[j];
         x2dft32_dir<BAR_DFT, INV>(R);
         return;
     }
@@ -225,11 +231,11 @@ __device__ __forceinline__ void fft4096_pk(cx2 (&P)[32], float *lds, const cx (&
 // The same transform with a packed last combine: Y2[q] = (U[l + 64 q],
 // U[l + 64 (q + 32)]) in the halves of one cx2 (forward only) -- 6 packed
 // instructions per pair instead of 8 scalar ones.
-template <bool BAR_DFT = true, bool BAR_TW = true>
+template <bool BAR_DFT = true, bool BAR_TW = true, bool AB_NOXP = false>
 __device__ __forceinline__ void fft4096_pk_y2(cx2 (&P)[32], float *lds, const cx (&tlo)[8], const cx2 (&thp)[4],
                                               uint32_t lane, cx2 (&Y2)[32]) {
     cx2 R[32];
-    fft4096_pk_front<false, BAR_DFT, BAR_TW>(P, lds, tlo, thp, lane, R);
+    fft4096_pk_front<false, BAR_DFT, BAR_TW, false, AB_NOXP>(P, lds, tlo, thp, lane, R);
     combine64p(R, Y2);
 }
 

@@ -34,7 +34,8 @@ namespace dspb {
 // fewer per frame, the same bits)
 enum { kPkNoBarDft = 1, kPkNoBarTw = 2, kPkNoBarSplit = 4, kPkRenderCached = 8, kPkNtMag = 16, kPkMagLds = 32,
        kPkOldSplit = 64, kPkAbNoRender = 128, kPkAbNoMag = 256, kPkMagStage = 512, kPkOcc3 = 1024,
-       kPkMemAos = 2048, kPkNoRemap = 4096 };
+       kPkMemAos = 2048, kPkNoRemap = 4096, kPkAbNoXpose = 8192 };
+// 8192: ablation only (results discarded): no LDS transpose
 // 4096 = frames in dispatch order (no XCD remap: all XCDs write one frontier)
 // 2048 = memory frames (computed window) loaded as 64 pairs and regrouped
 // after the window multiply (the older path; default: regrouped at the load)
@@ -386,7 +387,7 @@ __global__ __launch_bounds__(256, OCC) void stft8192_pk_kernel(Stft8kArgs A) {
         // Y2[q] = (Z[l + 64 q], Z[l + 64 (q + 32)])
         cx2 Y2[32];
         if constexpr (OCC >= 3) fft4096_pk_y2_lo<!(OPT & kPkNoBarDft)>(P, lds, A.tw, lane, Y2);
-        else fft4096_pk_y2<!(OPT & kPkNoBarDft), !(OPT & kPkNoBarTw)>(P, lds, tlo, thp, lane, Y2);
+        else fft4096_pk_y2<!(OPT & kPkNoBarDft), !(OPT & kPkNoBarTw), (OPT & kPkAbNoXpose) != 0>(P, lds, tlo, thp, lane, Y2);
         split_y2<KM, !(OPT & kPkNoBarSplit), (OPT & kPkAbNoMag) != 0, KM == kKHalf && (OPT & kPkMagStage) != 0,
                  (OPT & kPkNtMag) != 0>(Y2, A.mag.p[ch] + f * A.ld, A.K, A.tw, lane, lds);
         return;
@@ -553,6 +554,8 @@ int launch_stft8192_pk(const Stft8kArgs &A, uint32_t C, bool fused, int opt, hip
                     DSPB_PK_CASE(kPkMagStage | kPkNtMag);
                     DSPB_PK_CASE(kPkNtMag);
                     DSPB_PK_CASE(kPkNoRemap);
+                    DSPB_PK_CASE(kPkAbNoXpose);
+                    DSPB_PK_CASE(kPkAbNoXpose | kPkAbNoRender | kPkAbNoMag);
                     DSPB_PK_CASE(kPkOldSplit);
                     DSPB_PK_CASE(kPkOldSplit | kPkRenderCached);
                     DSPB_PK_CASE(kPkOldSplit | kPkNtMag);
