@@ -1,0 +1,280 @@
+// dspbench_render -- the offline-render command line: a C++ host that drives
+// the GPU path through the C ABI only (include/dspbench/*.h), the way the
+// reference's host would ("called from: the build's
+// offline-render CLI").
+//
+//   WAV file -> dsp_wav_parse -> payload to HBM -> dsp_wav_decode (planar)
+//   -> dsp_render_offline / dsp_render_stft through a plugin -> dsp_wav_encode
+//   -> output WAV (+ optional magnitude spectra as raw float32).
+//
+// It replaces the reference's load (wav_reader.h:57-205, audio.h:66-121),
+// render loop (audio.cpp:13-175, pumped by wasapi_audio.cpp:223-251) and the
+// analysis FFT (dsp.cpp:53-103) for a whole file, offline.
+//
+//   dspbench_render IN.wav OUT.wav [options]
+//     --plugin NAME     gain_test (default) | IR_test | no_op | static_gain |
+//                       PATH.cpp (any reference-style plugin source, compiled
+//                       for gfx950 at run time: DSP_PLUGIN_GENERIC)
+//     --gain G          gain_test / static_gain gain (0.2 / 0.1)
+//     --ir G,STEP       IR_test parameters (0.9,0.002)
+//     --block B         block size (512)
+//     --bits 16|24|32|float   output sample format (default: the input's)
+//     --stft FILE       also write the Hann 8192 / 4096 STFT magnitudes of the
+//                       render: header "DSPMAG1\0", u32 C, u32 K, u64 F, then
+//                       C x F x K float32
+//     --device N        GPU ordinal (0)
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "dspbench/dspbench.h"
+#include "dspbench/module.h"
+#include "dspbench/wav.h"
+
+namespace {
+
+int fail(const char *what, int st) {
+    std::fprintf(stderr, "dspbench_render: %s: %s (%s)\n", what, dsp_status_string(st), dsp_last_error());
+    return 1;
+}
+
+#define HIPCK(x)                                                                          \
+    do {                                                                                  \
+        hipError_t e_ = (x);                                                              \
+        if (e_ != hipSuccess) {                                                           \
+            std::fprintf(stderr, "dspbench_render: %s: %s\n", #x, hipGetErrorString(e_)); \
+            return 1;                                                                     \
+        }                                                                                 \
+    } while (0)
+
+bool read_file(const char *path, std::vector<unsigned char> &out) {
+    FILE *f = std::fopen(path, "rb");
+    if (!f) return false;
+    std::fseek(f, 0, SEEK_END);
+    const long n = std::ftell(f);
+    std::fseek(f, 0, SEEK_SET);
+    out.resize(n > 0 ? (size_t)n : 0);
+    const bool ok = n >= 0 && std::fread(out.data(), 1, out.size(), f) == out.size();
+    std::fclose(f);
+    return ok;
+}
+
+void usage() {
+    std::fprintf(stderr,
+                 "usage: dspbench_render IN.wav OUT.wav [--plugin gain_test|IR_test|no_op|static_gain|PATH.cpp]\n"
+                 "       [--gain G] [--ir G,STEP] [--block B] [--bits 16|24|32|float] [--stft MAG.f32]"
+                 " [--device N]\n");
+}
+
+double ms_since(std::chrono::steady_clock::time_point t0) {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
+}  // namespace
+
+int main(int argc, char **argv) {
+    if (argc < 3) {
+        usage();
+        return 2;
+    }
+    const char *in_path = argv[1], *out_path = argv[2];
+    std::string plugin = "gain_test", stft_path, bits_opt;
+    float gain = -1.f, ir_gain = 0.9f, ir_step = 0.002f;
+    uint32_t B = 512;
+    int device = 0;
+    for (int i = 3; i < argc; i += 2) {  // every option takes one value
+        const std::string a = argv[i];
+        const char *v = i + 1 < argc ? argv[i + 1] : nullptr;
+        if (!v) {
+            usage();
+            return 2;
+        }
+        if (a == "--plugin") plugin = v;
+        else if (a == "--gain") gain = std::strtof(v, nullptr);
+        else if (a == "--ir") {
+            if (std::sscanf(v, "%f,%f", &ir_gain, &ir_step) != 2) {
+                usage();
+                return 2;
+            }
+        } else if (a == "--block") B = (uint32_t)std::strtoul(v, nullptr, 10);
+        else if (a == "--bits") bits_opt = v;
+        else if (a == "--stft") stft_path = v;
+        else if (a == "--device") device = std::atoi(v);
+        else {
+            usage();
+            return 2;
+        }
+    }
+    if (B == 0) {
+        usage();
+        return 2;
+    }
+
+    // ---- load + parse (wav_reader.h:57-205) --------------------------------
+    std::vector<unsigned char> file;
+    if (!read_file(in_path, file)) {
+        std::fprintf(stderr, "dspbench_render: cannot read %s\n", in_path);
+        return 1;
+    }
+    dsp_wav_info info{};
+    int st = dsp_wav_parse(file.data(), file.size(), &info);
+    if (st) return fail("dsp_wav_parse", st);
+    const uint32_t C = info.channels;
+    const uint64_t L = info.frames;
+    if (C == 0 || C > 16) {
+        std::fprintf(stderr, "dspbench_render: %u channels (1..16 supported)\n", C);
+        return 1;
+    }
+    std::vector<unsigned char> payload(info.data_bytes);
+    for (uint64_t c = 0, o = 0; c < info.n_data_chunks; ++c) {  // the data chunks, concatenated
+        std::memcpy(payload.data() + o, file.data() + info.data_offset[c], info.data_size[c]);
+        o += info.data_size[c];
+    }
+    file.clear();
+    file.shrink_to_fit();
+
+    HIPCK(hipSetDevice(device));
+    hipStream_t s;
+    HIPCK(hipStreamCreate(&s));
+    dsp_exec ex{};
+    ex.device = device;
+    ex.stream = s;
+
+    // ---- payload -> HBM, decode to planar float (audio.h:66-121) ----------
+    const auto t0 = std::chrono::steady_clock::now();
+    void *d_pay = nullptr;
+    HIPCK(hipMalloc(&d_pay, payload.size() + 16));
+    HIPCK(hipMemcpyAsync(d_pay, payload.data(), payload.size(), hipMemcpyHostToDevice, s));
+    const uint64_t nblocks = (L + B - 1) / B, Lr = nblocks * B;
+    std::vector<float *> din(C), dout(C);
+    for (uint32_t c = 0; c < C; ++c) {
+        HIPCK(hipMalloc(&din[c], (L ? L : 1) * sizeof(float)));
+        HIPCK(hipMalloc(&dout[c], Lr * sizeof(float)));
+    }
+    if ((st = dsp_wav_decode(d_pay, &info, 0, L, din.data(), &ex))) return fail("dsp_wav_decode", st);
+
+    // ---- plugin ------------------------------------------------------------
+    dsp_plugin p{};
+    float pv[2] = {0.f, 0.f};
+    dsp_module *mod = nullptr;
+    std::vector<unsigned char> gparams;
+    if (plugin == "gain_test") {
+        pv[0] = gain >= 0.f ? gain : 0.2f;  // build/gain_test.cpp:23
+        p.kind = DSP_PLUGIN_GAIN, p.params = pv, p.params_size = 4;
+    } else if (plugin == "static_gain") {
+        pv[0] = gain >= 0.f ? gain : 0.1f;  // test/static_gain_plugin.cpp:22
+        p.kind = DSP_PLUGIN_STATIC_GAIN, p.state = pv, p.state_size = 4;
+    } else if (plugin == "IR_test") {
+        pv[0] = ir_gain, pv[1] = ir_step;  // build/IR_test.cpp:24
+        p.kind = DSP_PLUGIN_IR_RAMP, p.params = pv, p.params_size = 8;
+    } else if (plugin == "no_op") {
+        p.kind = DSP_PLUGIN_NOOP;
+    } else {  // a plugin source file: compile for gfx950, load, defaults, state
+        std::vector<unsigned char> src;
+        if (!read_file(plugin.c_str(), src)) {
+            std::fprintf(stderr, "dspbench_render: cannot read plugin %s\n", plugin.c_str());
+            return 1;
+        }
+        src.push_back(0);
+        void *code = nullptr;
+        uint64_t code_size = 0;
+        std::vector<char> log(1 << 16);
+        if ((st = dsp_module_compile((const char *)src.data(), plugin.c_str(), &code, &code_size, log.data(),
+                                     log.size()))) {
+            std::fprintf(stderr, "%s\n", log.data());
+            return fail("dsp_module_compile", st);
+        }
+        st = dsp_module_load(code, code_size, device, &mod);
+        dsp_module_free_code(code);
+        if (st) return fail("dsp_module_load", st);
+        uint32_t ps = 0, ss = 0;
+        int stateless = 0;
+        if ((st = dsp_module_sizes(mod, &ps, &ss, &stateless))) return fail("dsp_module_sizes", st);
+        gparams.resize(ps ? ps : 1);
+        if ((st = dsp_module_default_parameters(mod, gparams.data()))) return fail("dsp_module_default_parameters", st);
+        if ((st = dsp_module_initialize_state(mod, gparams.data(), C, (float)info.sample_rate, 16u << 20)))
+            return fail("dsp_module_initialize_state", st);
+        p.kind = DSP_PLUGIN_GENERIC, p.params = gparams.data(), p.params_size = ps, p.module = mod;
+    }
+
+    // ---- render (+ STFT) ---------------------------------------------------
+    const float sr = (float)info.sample_rate;
+    const uint32_t N = 8192, H = 4096, K = N / 2 + 1;
+    const uint64_t F = stft_path.empty() ? 0 : dsp_stft_frame_count(Lr, N, H);
+    std::vector<float *> dmag(C, nullptr);
+    hipEvent_t e0, e1;
+    HIPCK(hipEventCreate(&e0));
+    HIPCK(hipEventCreate(&e1));
+    HIPCK(hipEventRecord(e0, s));
+    if (!stft_path.empty() && F > 0) {
+        for (uint32_t c = 0; c < C; ++c) HIPCK(hipMalloc(&dmag[c], F * K * sizeof(float)));
+        st = dsp_render_stft(din.data(), C, L, dout.data(), C, B, sr, &p, N, H, DSP_WIN_HANN, K, dmag.data(), K,
+                             &ex);
+        if (st) return fail("dsp_render_stft", st);
+    } else {
+        if ((st = dsp_render_offline(din.data(), C, L, dout.data(), C, B, sr, &p, &ex)))
+            return fail("dsp_render_offline", st);
+    }
+    HIPCK(hipEventRecord(e1, s));
+
+    // ---- encode the render (audio.h:123-133 interleave) and write ----------
+    uint16_t fmt = info.format, bits = info.bits_per_sample;
+    if (bits_opt == "float") fmt = DSP_WAV_FORMAT_FLOAT, bits = 32;
+    else if (!bits_opt.empty()) fmt = DSP_WAV_FORMAT_PCM, bits = (uint16_t)std::atoi(bits_opt.c_str());
+    const uint64_t out_bytes = Lr * C * (bits / 8u);
+    void *d_opay = nullptr;
+    HIPCK(hipMalloc(&d_opay, out_bytes + 16));
+    if ((st = dsp_wav_encode(dout.data(), C, Lr, fmt, bits, d_opay, &ex))) return fail("dsp_wav_encode", st);
+    std::vector<unsigned char> out(64 + out_bytes);
+    const int hdr = dsp_wav_write_header(out.data(), out.size(), fmt, (uint16_t)C, info.sample_rate, bits, Lr);
+    if (hdr < 0) return fail("dsp_wav_write_header", hdr);
+    HIPCK(hipMemcpyAsync(out.data() + hdr, d_opay, out_bytes, hipMemcpyDeviceToHost, s));
+    std::vector<float> mag;
+    if (F > 0) {
+        mag.resize((size_t)C * F * K);
+        for (uint32_t c = 0; c < C; ++c)
+            HIPCK(hipMemcpyAsync(mag.data() + (size_t)c * F * K, dmag[c], F * K * sizeof(float),
+                                 hipMemcpyDeviceToHost, s));
+    }
+    HIPCK(hipStreamSynchronize(s));
+    float render_ms = 0.f;
+    HIPCK(hipEventElapsedTime(&render_ms, e0, e1));
+    FILE *f = std::fopen(out_path, "wb");
+    if (!f || std::fwrite(out.data(), 1, hdr + out_bytes, f) != hdr + out_bytes) {
+        std::fprintf(stderr, "dspbench_render: cannot write %s\n", out_path);
+        return 1;
+    }
+    std::fclose(f);
+    if (F > 0) {
+        f = std::fopen(stft_path.c_str(), "wb");
+        const uint32_t hk[2] = {C, K};
+        if (!f || std::fwrite("DSPMAG1", 1, 8, f) != 8 || std::fwrite(hk, 4, 2, f) != 2 ||
+            std::fwrite(&F, 8, 1, f) != 1 || std::fwrite(mag.data(), 4, mag.size(), f) != mag.size()) {
+            std::fprintf(stderr, "dspbench_render: cannot write %s\n", stft_path.c_str());
+            return 1;
+        }
+        std::fclose(f);
+    }
+    std::printf("dspbench_render: %s: %u ch x %llu frames @ %u Hz -> %s (%s %u-bit, %llu blocks of %u)%s; "
+                "render %.3f ms on the GPU, %.1f ms end to end\n",
+                in_path, C, (unsigned long long)L, info.sample_rate, out_path,
+                fmt == DSP_WAV_FORMAT_FLOAT ? "float" : "PCM", bits, (unsigned long long)nblocks, B,
+                F ? (" + STFT " + std::to_string(F) + " frames x " + std::to_string(K) + " bins").c_str() : "",
+                render_ms, ms_since(t0));
+
+    if (mod) dsp_module_destroy(mod);
+    for (uint32_t c = 0; c < C; ++c) {
+        (void)hipFree(din[c]);
+        (void)hipFree(dout[c]);
+        if (dmag[c]) (void)hipFree(dmag[c]);
+    }
+    (void)hipFree(d_pay);
+    (void)hipFree(d_opay);
+    (void)hipStreamDestroy(s);
+    return 0;
+}

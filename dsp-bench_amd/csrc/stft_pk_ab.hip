@@ -1,0 +1,73 @@
+// stft_pk_ab.hip -- the A/B and ablation instantiations of
+// stft8192_pk_kernel (stft_pk.hpp options, dsp_stft_soa_options >> 4): the
+// headline shape (IR_test, B = 512) and the memory-source kPkMemAos path.
+// Kept in their own code object: loaded only when an option is selected.
+#include "stft_pk.hpp"
+
+namespace dspb {
+
+int launch_pk_ab(const Stft8kArgs &A, bool fused, int opt, dim3 grid, hipStream_t stream) {
+    if (!fused) {  // kPkMemAos
+        hipLaunchKernelGGL((stft8192_pk_kernel<kSrcMemory, kKHalf, MapKind::Noop, true, true, 0, kPkMemAos>), grid,
+                           dim3(256), 0, stream, A);
+        DSPB_HIP(hipGetLastError());
+        return DSP_OK;
+    }
+    if (opt & kPkOcc3) {
+        switch (opt & ~kPkOcc3) {
+        case 0:
+            hipLaunchKernelGGL((stft8192_pk_kernel<kSrcRender, kKHalf, MapKind::Ramp, true, true, 4, 0, 3>), grid,
+                               dim3(256), 0, stream, A);
+            break;
+        case kPkRenderCached:
+            hipLaunchKernelGGL(
+                (stft8192_pk_kernel<kSrcRender, kKHalf, MapKind::Ramp, true, true, 4, kPkRenderCached, 3>), grid,
+                dim3(256), 0, stream, A);
+            break;
+        case kPkAbNoRender | kPkAbNoMag:
+            hipLaunchKernelGGL(
+                (stft8192_pk_kernel<kSrcRender, kKHalf, MapKind::Ramp, true, true, 4, kPkAbNoRender | kPkAbNoMag, 3>),
+                grid, dim3(256), 0, stream, A);
+            break;
+        default: return DSP_ERR_INVALID;
+        }
+        DSPB_HIP(hipGetLastError());
+        return DSP_OK;
+    }
+    switch (opt) {
+#define DSPB_PK_CASE(o)                                                                                     \
+    case (o):                                                                                               \
+        hipLaunchKernelGGL((stft8192_pk_kernel<kSrcRender, kKHalf, MapKind::Ramp, true, true, 4, (o)>), grid, \
+                           dim3(256), 0, stream, A);                                                        \
+        break
+        DSPB_PK_CASE(kPkNoBarDft);
+        DSPB_PK_CASE(kPkNoBarTw);
+        DSPB_PK_CASE(kPkNoBarSplit);
+        DSPB_PK_CASE(kPkNoBarDft | kPkNoBarTw | kPkNoBarSplit);
+        DSPB_PK_CASE(kPkRenderCached);
+        DSPB_PK_CASE(kPkMagStage);
+        DSPB_PK_CASE(kPkMagStage | kPkRenderCached);
+        DSPB_PK_CASE(kPkMagStage | kPkNtMag);
+        DSPB_PK_CASE(kPkNtMag);
+        DSPB_PK_CASE(kPkNoRemap);
+        DSPB_PK_CASE(kPkAbNoXpose);
+        DSPB_PK_CASE(kPkAbNoXpose | kPkAbNoRender | kPkAbNoMag);
+        DSPB_PK_CASE(kPkOldSplit);
+        DSPB_PK_CASE(kPkOldSplit | kPkRenderCached);
+        DSPB_PK_CASE(kPkOldSplit | kPkNtMag);
+        DSPB_PK_CASE(kPkOldSplit | kPkRenderCached | kPkNtMag);
+        DSPB_PK_CASE(kPkMagLds);
+        DSPB_PK_CASE(kPkMagLds | kPkRenderCached);
+        DSPB_PK_CASE(kPkMagLds | kPkNtMag);
+        DSPB_PK_CASE(kPkMagLds | kPkRenderCached | kPkNtMag);
+        DSPB_PK_CASE(kPkAbNoRender);
+        DSPB_PK_CASE(kPkAbNoMag);
+        DSPB_PK_CASE(kPkAbNoRender | kPkAbNoMag);
+#undef DSPB_PK_CASE
+    default: return DSP_ERR_INVALID;
+    }
+    DSPB_HIP(hipGetLastError());
+    return DSP_OK;
+}
+
+}  // namespace dspb

@@ -1,7 +1,7 @@
 """Interleaved in-process A/B of stft8192_pk_kernel store options at the
 headline shape (IR_test B = 512 fused render + Hann STFT, 1 h of 48 kHz stereo).
 
-    python tools/ab_pkopt.py ROUNDS OPT [OPT ...]     (OPT = stft_pk.hip kPk* bits)
+    python tools/ab_pkopt.py ROUNDS OPT [OPT ...]     (OPT = stft_pk.hpp kPk* bits)
 
 Each round runs every option for 20 back-to-back launches after 10 warm ones
 (the settled, power-capped state the bench measures) and records the average

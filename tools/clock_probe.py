@@ -3,7 +3,7 @@ back to back for ~2.5 s while rocm-smi samples sclk and socket power twice
 (read-only queries).  Tells a power-capped kernel (lower sclk) from a
 stalled one.
 
-    python tools/clock_probe.py OPT [OPT ...]   (stft_pk.hip kPk* bits)
+    python tools/clock_probe.py OPT [OPT ...]   (stft_pk.hpp kPk* bits)
     python tools/clock_probe.py fir             (the fir1024 workload instead)
     python tools/clock_probe.py mem [OPT ...]   (the stft96k workload: STFT from HBM)
 """
