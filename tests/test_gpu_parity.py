@@ -58,6 +58,7 @@ RENDER_SHAPES = [
     (2, 2, 100, 512),      # shorter than one block
     (3, 2, 4096, 4096),    # exact multiple
     (0, 2, 1000, 128),     # no file: silence through the plugin
+    (2, 2, 1_000_003, 512),  # ~245 tiles of the vector kernel, ragged last tile
 ]
 
 

@@ -38,7 +38,11 @@ def test_decode_every_code(torch_cuda, oracle, bits):
 
 @pytest.mark.parametrize("channels", [1, 2, 3])
 @pytest.mark.parametrize("bits,is_float", [(16, False), (24, False), (32, False), (32, True)])
-@pytest.mark.parametrize("frame0,frames", [(0, 10_007), (1, 5000), (3, 4), (0, 1)])
+# frame0 sets the payload start's alignment, so the tiled mono / stereo decode
+# takes its 16-, 8- and 4-byte load paths (e.g. int16 stereo: 0 and 4 -> 16 B,
+# 2 -> 8 B, 1 / 3 -> 4 B); 10_007 and 3001 end in a partial 4-frame group
+@pytest.mark.parametrize("frame0,frames", [(0, 10_007), (1, 5000), (3, 4), (0, 1), (2, 9_999), (4, 3001),
+                                           (0, 4 * 256 * 4 + 4)])
 def test_decode_interleaved(torch_cuda, oracle, channels, bits, is_float, frame0, frames):
     rng = np.random.default_rng(channels * 100 + bits)
     total = frame0 + frames + 5
