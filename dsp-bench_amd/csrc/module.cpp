@@ -14,9 +14,11 @@
 #include <hip/hip_runtime.h>
 #include <hip/hiprtc.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -105,41 +107,162 @@ __device__ static void dspb_stage_out(const dspb_render_args &A, unsigned long l
         A.out[c][b * A.B + s] = buf[j];
     }
 }
+typedef __attribute__((address_space(1))) float dspb_gfloat;
+// a generic pointer the compiler can prove is global memory (global_load /
+// global_store in the inlined callback, not flat ops that also wait on LDS)
+__device__ static inline float *dspb_global(float *p) { return (float *)(dspb_gfloat *)p; }
+// no state: one wavefront renders 64 consecutive blocks. render_audio's copy
+// (audio.cpp:13-175: the file at the cursor, zeros past EOF and for the
+// channels the file lacks) runs first for all 64 blocks at once, coalesced
+// per channel, four loads in flight per lane before their stores (in == out
+// is allowed: every element is stored where it was loaded). Then lane t runs
+// the callback in place on block t. CC > 0 makes the channel count a
+// constant, so the callback's channel loops unroll and its pointer table
+// lives in registers instead of scratch.
+template <unsigned CC>
+__device__ static void dspb_stateless(const dspb_render_args &A) {
+    State local = *(State *)A.S;
+    // a private copy: the callback's stores cannot alias it, so its fields
+    // stay in registers instead of being reloaded after every store
+    Parameters prm = *(const Parameters *)A.P;
+    const unsigned C = CC ? CC : A.C, t = threadIdx.x;
+    for (unsigned long long b0 = (unsigned long long)blockIdx.x * 64; b0 < A.nblocks;
+         b0 += (unsigned long long)gridDim.x * 64) {
+        const unsigned long long nb = A.nblocks - b0 < 64 ? A.nblocks - b0 : 64;
+        const unsigned long long i0 = b0 * A.B, n = nb * A.B;
+        const unsigned long long lim = A.L > i0 ? A.L - i0 : 0;  // file samples left at i0
+        for (unsigned c = 0; c < C; ++c) {
+            dspb_gfloat *o = (dspb_gfloat *)A.out[c] + i0;
+            const dspb_gfloat *x = (const dspb_gfloat *)A.in[c < A.in_ch ? c : 0] + i0;
+            const unsigned long long m = c < A.in_ch ? (lim < n ? lim : n) : 0;  // copied, the rest zeroed
+            unsigned long long j = t;
+            for (; j + 192 < m; j += 256) {
+                const float v0 = x[j], v1 = x[j + 64], v2 = x[j + 128], v3 = x[j + 192];
+                o[j] = v0;
+                o[j + 64] = v1;
+                o[j + 128] = v2;
+                o[j + 192] = v3;
+            }
+            for (; j < m; j += 64) o[j] = x[j];
+            for (j = m + ((t - m) & 63); j < n; j += 64) o[j] = 0.0f;
+        }
+        __syncthreads();  // the wave's copies are visible to every lane
+        if (t < nb) {
+            float *ptrs[CC ? CC : 16];
+            for (unsigned c = 0; c < C; ++c) ptrs[c] = dspb_global(A.out[c] + (i0 + (unsigned long long)t * A.B));
+            audio_callback(prm, local, ptrs, C, A.B, A.sr);
+        }
+        __syncthreads();
+    }
+}
+// stateful, in order: thread 0 runs the callback on block b in LDS while
+// waves 1.. write block b - 1 out and stage block b + 1 in the other half of
+// the double buffer (the same elements per thread, so no element is
+// overwritten before it is written out). Thread 0 keeps Parameters and a
+// small State in private copies (written back at the end): the callback's
+// LDS stores cannot alias them, so they stay in registers. CC as above.
+template <unsigned CC>
+__device__ static void dspb_stateful_lds(const dspb_render_args &A) {
+    extern __shared__ float dspb_lbuf[];
+    const unsigned C = CC ? CC : A.C, CB = C * A.B, t = threadIdx.x, nt = blockDim.x;
+    float *buf0 = dspb_lbuf, *buf1 = dspb_lbuf + CB;
+    dspb_stage_in(A, 0, buf0, t, nt);
+    __syncthreads();
+    constexpr bool kLocal = sizeof(State) <= 256;
+    State *gst = (State *)A.S;
+    // copies made by every thread (a few hundred bytes at most), used by
+    // thread 0; the blobs are plain bytes to the host, as in the reference
+    Parameters prm = *(const Parameters *)A.P;
+    State local = *gst;
+    for (unsigned long long b = 0; b < A.nblocks; ++b) {
+        float *cur = (b & 1) ? buf1 : buf0, *oth = (b & 1) ? buf0 : buf1;
+        if (t == 0) {
+            float *ptrs[CC ? CC : 16];
+            for (unsigned c = 0; c < C; ++c) ptrs[c] = cur + c * A.B;
+            if constexpr (kLocal) audio_callback(prm, local, ptrs, C, A.B, A.sr);
+            else audio_callback(prm, *gst, ptrs, C, A.B, A.sr);
+        } else if (t >= 64) {
+            if (b > 0) dspb_stage_out(A, b - 1, oth, t - 64, nt - 64);
+            if (b + 1 < A.nblocks) dspb_stage_in(A, b + 1, oth, t - 64, nt - 64);
+        }
+        __syncthreads();
+    }
+    if constexpr (kLocal) {
+        if (t == 0) __builtin_memcpy((void *)gst, (const void *)&local, sizeof(State));
+    }
+    dspb_stage_out(A, A.nblocks - 1, (A.nblocks - 1) & 1 ? buf1 : buf0, t, nt);
+}
+// no state, C B <= kPrivFloats: every lane renders its own block in a
+// private array. Scratch is lane-interleaved in hardware (dword k of every
+// lane of a wave is one 256-byte segment), so the callback's sample-by-sample
+// loads and stores are coalesced over the wave, where in place in HBM each
+// of them touches 64 different cache lines. The private copy also cannot
+// alias anything, so render_audio's copy in and the copy out pipeline freely
+// (float4 when B and the channel pointers allow).
+constexpr unsigned kPrivFloats = 1024;
+template <unsigned CC>
+__device__ static void dspb_stateless_private(const dspb_render_args &A) {
+    State local = *(State *)A.S;
+    Parameters prm = *(const Parameters *)A.P;
+    const unsigned B = A.B;
+    bool al = (B & 3) == 0;
+    for (unsigned c = 0; c < CC; ++c)
+        al = al && ((unsigned long long)A.out[c] & 15) == 0 &&
+             (c >= A.in_ch || ((unsigned long long)A.in[c] & 15) == 0);
+    float buf[kPrivFloats];
+    for (unsigned long long b = (unsigned long long)blockIdx.x * 64 + threadIdx.x; b < A.nblocks;
+         b += (unsigned long long)gridDim.x * 64) {
+        const unsigned long long i0 = b * B;
+        for (unsigned c = 0; c < CC; ++c) {
+            float *row = buf + c * B;
+            const dspb_gfloat *x = (const dspb_gfloat *)A.in[c < A.in_ch ? c : 0] + i0;
+            const unsigned long long left = A.L > i0 ? A.L - i0 : 0;
+            const unsigned m = c < A.in_ch ? (unsigned)(left < B ? left : B) : 0u;
+            if (al && m == B) {
+                for (unsigned s = 0; s < B; s += 4) {
+                    const float4 v = *(const __attribute__((address_space(1))) float4 *)(x + s);
+                    row[s] = v.x;
+                    row[s + 1] = v.y;
+                    row[s + 2] = v.z;
+                    row[s + 3] = v.w;
+                }
+            } else {
+                for (unsigned s = 0; s < B; ++s) row[s] = s < m ? x[s] : 0.0f;
+            }
+        }
+        float *ptrs[CC];
+        for (unsigned c = 0; c < CC; ++c) ptrs[c] = buf + c * B;
+        audio_callback(prm, local, ptrs, CC, B, A.sr);
+        for (unsigned c = 0; c < CC; ++c) {
+            const float *row = buf + c * B;
+            dspb_gfloat *o = (dspb_gfloat *)A.out[c] + i0;
+            if (al) {
+                for (unsigned s = 0; s < B; s += 4)
+                    *(__attribute__((address_space(1))) float4 *)(o + s) =
+                        make_float4(row[s], row[s + 1], row[s + 2], row[s + 3]);
+            } else {
+                for (unsigned s = 0; s < B; ++s) o[s] = row[s];
+            }
+        }
+    }
+}
 extern "C" __global__ void dspb_render(dspb_render_args A) {
     extern __shared__ float dspb_lbuf[];
-    if (__is_empty(State)) {  // no state: every block on its own thread
-        State local = *(State *)A.S;
-        for (unsigned long long b = blockIdx.x * (unsigned long long)blockDim.x + threadIdx.x; b < A.nblocks;
-             b += (unsigned long long)gridDim.x * blockDim.x)
-            dspb_block(A, b, local);
+    if (__is_empty(State)) {
+        if (A.lds == 1 && A.C == 1) dspb_stateless_private<1>(A);
+        else if (A.lds == 1 && A.C == 2) dspb_stateless_private<2>(A);
+        else if (A.C == 1) dspb_stateless<1>(A);
+        else if (A.C == 2) dspb_stateless<2>(A);
+        else dspb_stateless<0>(A);
     } else if (!A.lds) {  // stateful, blocks too large for LDS: in order, one thread
         if (blockIdx.x == 0 && threadIdx.x == 0) {
             State &st = *(State *)A.S;
             for (unsigned long long b = 0; b < A.nblocks; ++b) dspb_block(A, b, st);
         }
     } else if (blockIdx.x == 0) {
-        // stateful, in order: thread 0 runs the callback on block b in LDS
-        // while waves 1.. write block b - 1 out and stage block b + 1 in the
-        // other half of the double buffer (the same elements per thread, so
-        // no element is overwritten before it is written out)
-        State &st = *(State *)A.S;
-        const unsigned CB = A.C * A.B, t = threadIdx.x, nt = blockDim.x;
-        float *buf0 = dspb_lbuf, *buf1 = dspb_lbuf + CB;
-        dspb_stage_in(A, 0, buf0, t, nt);
-        __syncthreads();
-        for (unsigned long long b = 0; b < A.nblocks; ++b) {
-            float *cur = (b & 1) ? buf1 : buf0, *oth = (b & 1) ? buf0 : buf1;
-            if (t == 0) {
-                float *ptrs[16];
-                for (unsigned c = 0; c < A.C; ++c) ptrs[c] = cur + c * A.B;
-                audio_callback(*(Parameters *)A.P, st, ptrs, A.C, A.B, A.sr);
-            } else if (t >= 64) {
-                if (b > 0) dspb_stage_out(A, b - 1, oth, t - 64, nt - 64);
-                if (b + 1 < A.nblocks) dspb_stage_in(A, b + 1, oth, t - 64, nt - 64);
-            }
-            __syncthreads();
-        }
-        dspb_stage_out(A, A.nblocks - 1, (A.nblocks - 1) & 1 ? buf1 : buf0, t, nt);
+        if (A.C == 1) dspb_stateful_lds<1>(A);
+        else if (A.C == 2) dspb_stateful_lds<2>(A);
+        else dspb_stateful_lds<0>(A);
     }
 }
 // compute_IR (plugin.cpp:17-58): the callback once, on buffers as they are
@@ -166,6 +289,7 @@ struct dsp_module {
                   f_callback = nullptr;
     uint32_t params_size = 0, state_size = 0;
     int stateless = 0;
+    std::map<uint64_t, int> priv_choice;  // stateless (C << 32 | B) -> 1: private path faster
     void *d_params = nullptr;          // device Parameters
     void *d_state[2] = {nullptr, nullptr};  // [0] live State, [1] compute_IR scratch State
     ArenaHost *d_arena[2] = {nullptr, nullptr};
@@ -401,6 +525,28 @@ int dsp_module_read_state(const dsp_module *m, void *state) {
 
 namespace dspb {
 
+constexpr uint64_t kPrivMinBlocks = 32768;
+constexpr uint64_t kPrivFloatsHost = 1024;  // = kPrivFloats in kDriver
+// DSPB_STATELESS_PRIVATE=0 / 1 forces the in-place wave path / the private
+// path for eligible stateless renders (tools/generic_probe.py A/B); -1: timed
+static int stateless_private_forced() {
+    static const int v = [] {
+        const char *e = std::getenv("DSPB_STATELESS_PRIVATE");
+        return e && (e[0] == '0' || e[0] == '1') ? e[0] - '0' : -1;
+    }();
+    return v;
+}
+
+// does any input channel's [0, n) overlap any output channel's [0, n) floats
+static bool overlaps(const float *const *in, uint32_t in_ch, float *const *out, uint32_t C, uint64_t n) {
+    for (uint32_t a = 0; a < in_ch; ++a)
+        for (uint32_t b = 0; b < C; ++b) {
+            const uintptr_t i0 = (uintptr_t)in[a], o0 = (uintptr_t)out[b], len = n * sizeof(float);
+            if (i0 < o0 + len && o0 < i0 + len) return true;
+        }
+    return false;
+}
+
 // dsp_render_offline / dsp_render_stft with DSP_PLUGIN_GENERIC (device buffers)
 int module_render(dsp_module *m, const void *params, uint32_t params_size, const float *const *in,
                   uint32_t in_ch, uint64_t L, float *const *out, uint32_t C, uint32_t B, float sr,
@@ -443,10 +589,46 @@ int module_render(dsp_module *m, const void *params, uint32_t params_size, const
     if (A.nblocks == 0) return DSP_OK;
     void *args[] = {&A};
     unsigned grid = 1, block = 1, lds_bytes = 0;
-    if (m->stateless) {
+    if (m->stateless) {  // one wave per 64 blocks
         block = 64;
         const uint64_t g = (A.nblocks + 63) / 64;
         grid = (unsigned)(g < 65535 ? g : 65535);
+        // mono / stereo blocks of up to 1024 samples in long files may take
+        // the private path. Which one is faster depends on the callback: the
+        // private copies cost ~3x the traffic of the in-place copy (no_op,
+        // 1 h stereo: 2.6 vs 0.6 ms) while a callback that loads and stores
+        // runs 2.5x faster there (gain_test: 3.3 vs 8.2 ms). So the first
+        // eligible render of a (C, B) shape runs both (same bits by
+        // construction) and the module keeps the faster; an in-place render
+        // (in overlapping out) cannot run twice and takes the wave path until
+        // a decision exists. DSPB_STATELESS_PRIVATE=0/1 forces one.
+        if (C <= 2 && 1ull * C * B <= kPrivFloatsHost && A.nblocks >= kPrivMinBlocks) {
+            const int forced = stateless_private_forced();
+            const uint64_t key = (uint64_t)C << 32 | B;
+            auto it = m->priv_choice.find(key);
+            if (forced >= 0) {
+                A.lds = (unsigned)forced;
+            } else if (it != m->priv_choice.end()) {
+                A.lds = (unsigned)it->second;
+            } else if (!overlaps(in, in_ch, out, C, A.nblocks * B)) {
+                float ms[2];
+                for (unsigned mode = 0; mode < 2; ++mode) {
+                    A.lds = mode;
+                    hipEvent_t e0, e1;
+                    MOD_HIP(hipEventCreate(&e0));
+                    MOD_HIP(hipEventCreate(&e1));
+                    MOD_HIP(hipEventRecord(e0, s));
+                    MOD_HIP(hipModuleLaunchKernel(m->f_render, grid, 1, 1, block, 1, 1, 0, s, args, nullptr));
+                    MOD_HIP(hipEventRecord(e1, s));
+                    MOD_HIP(hipEventSynchronize(e1));
+                    MOD_HIP(hipEventElapsedTime(&ms[mode], e0, e1));
+                    (void)hipEventDestroy(e0);
+                    (void)hipEventDestroy(e1);
+                }
+                m->priv_choice[key] = ms[1] < ms[0] ? 1 : 0;
+                return DSP_OK;  // both wrote the same output
+            }
+        }
     } else if (2ull * C * B * sizeof(float) <= kStagedLdsBytes) {
         // stateful: 4 waves, the block double-buffer in LDS (the callback's
         // loads and stores hit LDS, the copies run on 192 lanes beside it)
