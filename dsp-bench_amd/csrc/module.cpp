@@ -611,20 +611,24 @@ int module_render(dsp_module *m, const void *params, uint32_t params_size, const
             } else if (it != m->priv_choice.end()) {
                 A.lds = (unsigned)it->second;
             } else if (!overlaps(in, in_ch, out, C, A.nblocks * B)) {
-                float ms[2];
+                struct Events {  // destroyed on every return
+                    hipEvent_t e[3] = {nullptr, nullptr, nullptr};
+                    ~Events() {
+                        for (hipEvent_t x : e)
+                            if (x) (void)hipEventDestroy(x);
+                    }
+                } ev;
+                for (hipEvent_t &x : ev.e) MOD_HIP(hipEventCreate(&x));
+                MOD_HIP(hipEventRecord(ev.e[0], s));
                 for (unsigned mode = 0; mode < 2; ++mode) {
                     A.lds = mode;
-                    hipEvent_t e0, e1;
-                    MOD_HIP(hipEventCreate(&e0));
-                    MOD_HIP(hipEventCreate(&e1));
-                    MOD_HIP(hipEventRecord(e0, s));
                     MOD_HIP(hipModuleLaunchKernel(m->f_render, grid, 1, 1, block, 1, 1, 0, s, args, nullptr));
-                    MOD_HIP(hipEventRecord(e1, s));
-                    MOD_HIP(hipEventSynchronize(e1));
-                    MOD_HIP(hipEventElapsedTime(&ms[mode], e0, e1));
-                    (void)hipEventDestroy(e0);
-                    (void)hipEventDestroy(e1);
+                    MOD_HIP(hipEventRecord(ev.e[mode + 1], s));
                 }
+                MOD_HIP(hipEventSynchronize(ev.e[2]));
+                float ms[2];
+                MOD_HIP(hipEventElapsedTime(&ms[0], ev.e[0], ev.e[1]));
+                MOD_HIP(hipEventElapsedTime(&ms[1], ev.e[1], ev.e[2]));
                 m->priv_choice[key] = ms[1] < ms[0] ? 1 : 0;
                 return DSP_OK;  // both wrote the same output
             }
