@@ -2,7 +2,7 @@
 
 The plan is checked two ways: exhaustively as arithmetic (chunks tile the
 file, frames tile the whole-file frame range, every owned frame's samples
-lie inside owned + halo), and end to end with world_size-2 gloo processes
+lie inside owned + halo), and end to end with world_size-2 and -4 gloo processes
 that each render + STFT their chunk with the oracle and gather to rank 0,
 which must reproduce the whole-file oracle result exactly.
 """
@@ -75,14 +75,14 @@ def _worker(rank, world, port, L, B, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("B", [512, 384])
-def test_gloo_two_ranks_match_whole_file(B):
+@pytest.mark.parametrize("B,world", [(512, 2), (384, 2), (512, 4)])
+def test_gloo_ranks_match_whole_file(B, world):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     L = 5 * 49152 + 1234
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, L, B, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, L, B, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = q.get(timeout=240)
