@@ -61,7 +61,8 @@ def parse():
                     help="8192-pt kernel (dsp_stft_kernel_variant): 2 = wave/frame scalar SoA, "
                          "5 = wave/frame packed even/odd pairs")
     ap.add_argument("--workload", default="headline",
-                    choices=["headline", "stft96k", "ch96k", "gain10min", "fir1024", "wav16", "wav24", "ir"],
+                    choices=["headline", "stft96k", "ch96k", "gain10min", "fir1024", "wav16", "wav24", "ir",
+                             "generic"],
                     help="headline = IR_test + STFT 48 kHz (the metric); stft96k = BASELINE cfg 4 "
                          "(STFT of 1 h stereo 96 kHz from HBM); gain10min = cfg 2 render; "
                          "wav16 / wav24 = GPU decode of a 1 h stereo int16 / int24 WAV payload; "
@@ -83,6 +84,30 @@ def pmc_traffic(workload: str, kernel: str, src: int):
         if f"{kernel}<{src}," in name and "hbm_bytes" in m:
             return float(m["hbm_bytes"]), os.path.relpath(paths[-1], REPO)
     return None, None
+
+
+def cpu_baseline_generic(seconds_budget: float):
+    """The reference's own gain_test.cpp, compiled from its source with the
+    JIT's flags (oracle/_ref/libref_gain_test.so), called block by block by
+    the oracle's render loop on one host core: chunks of 60 s stereo until
+    the budget."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import numpy as np
+    import oracle as o
+    ref = o.RefPlugin("gain_test", CH, float(SR))
+    chunk = SR * 60
+    x = np.random.default_rng(1).uniform(-1, 1, (CH, chunk)).astype(np.float32)
+    done = 0
+    t0 = time.perf_counter()
+    while True:
+        o.render_offline([x[c] for c in range(CH)], CH, B, float(SR), ref.as_oracle())
+        done += CH * chunk
+        el = time.perf_counter() - t0
+        if el >= seconds_budget:
+            break
+    return {"value": done / el / 1e6, "unit": "Msamples/s", "cores": 1, "kind": "reference",
+            "sample": f"{done // CH / SR:.0f} s of 48 kHz stereo through the reference's gain_test.cpp "
+                      "(compiled from source, -Ofast) and the oracle's render_audio loop, 1 thread"}
 
 
 def cpu_baseline(seconds_budget: float):
@@ -229,7 +254,8 @@ def main():
         return xs[rot[0]]
     nb = d.num_blocks(L_in, B)
     F = d.stft_frames(nb * B if wl in ("headline", "ch96k") else L_in, N_FFT, HOP)
-    out = torch.empty((CH, nb * B), device=dev) if wl in ("headline", "ch96k", "gain10min", "fir1024") else None
+    out = (torch.empty((CH, nb * B), device=dev) if wl in ("headline", "ch96k", "gain10min", "fir1024", "generic")
+           else None)
     # rows: the last rank owns one frame less (no halo); equal-sized rows keep
     # the optional gather a plain dist.gather
     mag = torch.empty((CH, max(F, L // HOP), K_BINS), device=dev) if wl in ("headline", "stft96k", "ch96k") else None
@@ -284,6 +310,24 @@ def main():
             d.render_offline(next_x(), CH, B, float(sr), plugin, out=out)
         workload = f"gain_test render (B=512), {minutes:g} min of 48 kHz stereo per GPU (cfg 2)"
         kname = "render_vec_kernel<Gain>"
+        alg_bytes = CH * L_in * 8  # read + write
+        alg_desc = "C*L*(4 + 4) B (read + write)"
+    elif wl == "generic":
+        # the reference's gain_test.cpp compiled by the
+        # product's plugin compiler (hiprtc -> gfx950, oracle/_ref/mod_*.co,
+        # built by oracle/make_modules.py) and run by the generic driver
+        with open(os.path.join(REPO, "oracle", "_ref", "mod_gain_test.co"), "rb") as f:
+            gmod = d.module.Module(f.read())
+        gparams = gmod.default_parameters()
+        gmod.initialize_state(gparams, CH, float(sr))
+        gplug = gmod.plugin(gparams, "gain_test")
+        plug_name = "gain_test.cpp (DSP_PLUGIN_GENERIC, compiled from the reference source)"
+
+        def step():
+            d.render_offline(x, CH, B, float(sr), gplug, out=out)
+        workload = (f"gain_test.cpp via the generic plugin driver (B=512), {minutes:g} min of 48 kHz "
+                    "stereo per GPU")
+        kname = "dspb_render (generic driver, hiprtc module; step time incl. the call's stream sync)"
         alg_bytes = CH * L_in * 8  # read + write
         alg_desc = "C*L*(4 + 4) B (read + write)"
     else:
@@ -384,6 +428,8 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and wl == "headline":
         cpu = cpu_baseline(args.cpu_seconds)
+    elif rank == 0 and world == 1 and not args.no_cpu_baseline and wl == "generic":
+        cpu = cpu_baseline_generic(min(args.cpu_seconds, 5.0))
 
     if rank == 0:
         line = {
@@ -438,7 +484,9 @@ def main():
                 "algorithmic": alg_desc,
                 "limiter": ("package power: the settled kernel draws the 1400 W cap at sclk ~1.8 GHz "
                             "(2.38 GHz without its stores); profiles/r01_power_ablation"
-                            if wl in ("headline", "ch96k") else None),
+                            if wl in ("headline", "ch96k") else
+                            "one lane per block: the plugin callback's 1024 dependent load -> store steps "
+                            "(DESIGN 4.6)" if wl == "generic" else None),
             }),
             "cpu_baseline": cpu,
         }
