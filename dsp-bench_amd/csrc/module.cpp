@@ -246,10 +246,61 @@ __device__ static void dspb_stateless_private(const dspb_render_args &A) {
         }
     }
 }
+// the private path with B a multiple of 64: the wave moves its 64 blocks
+// between HBM and the lanes' private arrays through a 64 x 65 LDS tile, so
+// every global load and store is one contiguous 256-byte row (a lane's own
+// block is 2 KB away from its neighbours': per-lane float4 copies touch 64
+// cache lines per instruction)
+template <unsigned CC>
+__device__ static void dspb_stateless_tiled(const dspb_render_args &A) {
+    extern __shared__ float dspb_lbuf[];
+    State local = *(State *)A.S;
+    Parameters prm = *(const Parameters *)A.P;
+    const unsigned B = A.B, t = threadIdx.x;
+    float buf[kPrivFloats];
+    for (unsigned long long b0 = (unsigned long long)blockIdx.x * 64; b0 < A.nblocks;
+         b0 += (unsigned long long)gridDim.x * 64) {
+        const unsigned nb = (unsigned)(A.nblocks - b0 < 64 ? A.nblocks - b0 : 64);
+        for (unsigned c = 0; c < CC; ++c) {
+            const bool has = c < A.in_ch;
+            const dspb_gfloat *x = (const dspb_gfloat *)A.in[has ? c : 0];
+            for (unsigned s0 = 0; s0 < B; s0 += 64) {
+#pragma unroll 16
+                for (unsigned bi = 0; bi < 64; ++bi) {
+                    const unsigned long long i = (b0 + bi) * B + s0 + t;
+                    dspb_lbuf[bi * 65 + t] = (has && bi < nb && i < A.L) ? x[i] : 0.0f;
+                }
+                __syncthreads();
+#pragma unroll
+                for (unsigned j = 0; j < 64; ++j) buf[c * B + s0 + j] = dspb_lbuf[t * 65 + j];
+                __syncthreads();
+            }
+        }
+        if (t < nb) {
+            float *ptrs[CC];
+            for (unsigned c = 0; c < CC; ++c) ptrs[c] = buf + c * B;
+            audio_callback(prm, local, ptrs, CC, B, A.sr);
+        }
+        for (unsigned c = 0; c < CC; ++c) {
+            dspb_gfloat *o = (dspb_gfloat *)A.out[c];
+            for (unsigned s0 = 0; s0 < B; s0 += 64) {
+#pragma unroll
+                for (unsigned j = 0; j < 64; ++j) dspb_lbuf[t * 65 + j] = buf[c * B + s0 + j];
+                __syncthreads();
+#pragma unroll 16
+                for (unsigned bi = 0; bi < 64; ++bi)
+                    if (bi < nb) o[(b0 + bi) * B + s0 + t] = dspb_lbuf[bi * 65 + t];
+                __syncthreads();
+            }
+        }
+    }
+}
 extern "C" __global__ void dspb_render(dspb_render_args A) {
     extern __shared__ float dspb_lbuf[];
     if (__is_empty(State)) {
-        if (A.lds == 1 && A.C == 1) dspb_stateless_private<1>(A);
+        if (A.lds == 2 && A.C == 1) dspb_stateless_tiled<1>(A);
+        else if (A.lds == 2 && A.C == 2) dspb_stateless_tiled<2>(A);
+        else if (A.lds == 1 && A.C == 1) dspb_stateless_private<1>(A);
         else if (A.lds == 1 && A.C == 2) dspb_stateless_private<2>(A);
         else if (A.C == 1) dspb_stateless<1>(A);
         else if (A.C == 2) dspb_stateless<2>(A);
@@ -537,6 +588,28 @@ static int stateless_private_forced() {
     return v;
 }
 
+// the private path's grid: DSPB_PRIV_WAVES=<waves per CU> caps it (the
+// lanes loop over blocks), bounding the scratch footprint in flight
+static unsigned priv_grid(unsigned grid) {
+    static const unsigned cap = [] {
+        const char *e = std::getenv("DSPB_PRIV_WAVES");
+        const unsigned long k = e ? std::strtoul(e, nullptr, 10) : 0;
+        return k ? (unsigned)(256 * k) : 0u;
+    }();
+    return cap && cap < grid ? cap : grid;
+}
+
+// the private path's driver mode: 2 (LDS-tiled copies) when B is a multiple
+// of 64, else 1 (per-lane copies); DSPB_PRIV_TILED=0 keeps mode 1
+constexpr unsigned kTileBytes = 64 * 65 * sizeof(float);
+static unsigned priv_mode(unsigned mode, uint32_t B) {
+    static const bool tiled = [] {
+        const char *e = std::getenv("DSPB_PRIV_TILED");
+        return !(e && e[0] == '0');
+    }();
+    return mode && tiled && B % 64 == 0 ? 2u : mode;
+}
+
 // does any input channel's [0, n) overlap any output channel's [0, n) floats
 static bool overlaps(const float *const *in, uint32_t in_ch, float *const *out, uint32_t C, uint64_t n) {
     for (uint32_t a = 0; a < in_ch; ++a)
@@ -598,8 +671,8 @@ int module_render(dsp_module *m, const void *params, uint32_t params_size, const
         // private copies cost ~3x the traffic of the in-place copy (no_op,
         // 1 h stereo: 2.6 vs 0.6 ms) while a callback that loads and stores
         // runs 2.5x faster there (gain_test: 3.3 vs 8.2 ms). So the first
-        // eligible render of a (C, B) shape runs both (same bits by
-        // construction) and the module keeps the faster; an in-place render
+        // eligible render of a (C, B) shape runs both, twice each (same bits
+        // by construction), and the module keeps the faster; an in-place render
         // (in overlapping out) cannot run twice and takes the wave path until
         // a decision exists. DSPB_STATELESS_PRIVATE=0/1 forces one.
         if (C <= 2 && 1ull * C * B <= kPrivFloatsHost && A.nblocks >= kPrivMinBlocks) {
@@ -611,8 +684,10 @@ int module_render(dsp_module *m, const void *params, uint32_t params_size, const
             } else if (it != m->priv_choice.end()) {
                 A.lds = (unsigned)it->second;
             } else if (!overlaps(in, in_ch, out, C, A.nblocks * B)) {
+                // the order 0, 1, 0, 1, each path's faster run: the first
+                // launch also pays the output's first touch
                 struct Events {  // destroyed on every return
-                    hipEvent_t e[3] = {nullptr, nullptr, nullptr};
+                    hipEvent_t e[5] = {};
                     ~Events() {
                         for (hipEvent_t x : e)
                             if (x) (void)hipEventDestroy(x);
@@ -620,17 +695,18 @@ int module_render(dsp_module *m, const void *params, uint32_t params_size, const
                 } ev;
                 for (hipEvent_t &x : ev.e) MOD_HIP(hipEventCreate(&x));
                 MOD_HIP(hipEventRecord(ev.e[0], s));
-                for (unsigned mode = 0; mode < 2; ++mode) {
-                    A.lds = mode;
-                    MOD_HIP(hipModuleLaunchKernel(m->f_render, grid, 1, 1, block, 1, 1, 0, s, args, nullptr));
-                    MOD_HIP(hipEventRecord(ev.e[mode + 1], s));
+                for (unsigned r = 0; r < 4; ++r) {
+                    const unsigned mode = r & 1;
+                    A.lds = priv_mode(mode, B);
+                    MOD_HIP(hipModuleLaunchKernel(m->f_render, mode ? priv_grid(grid) : grid, 1, 1, block, 1, 1,
+                                                  A.lds == 2 ? kTileBytes : 0, s, args, nullptr));
+                    MOD_HIP(hipEventRecord(ev.e[r + 1], s));
                 }
-                MOD_HIP(hipEventSynchronize(ev.e[2]));
-                float ms[2];
-                MOD_HIP(hipEventElapsedTime(&ms[0], ev.e[0], ev.e[1]));
-                MOD_HIP(hipEventElapsedTime(&ms[1], ev.e[1], ev.e[2]));
-                m->priv_choice[key] = ms[1] < ms[0] ? 1 : 0;
-                return DSP_OK;  // both wrote the same output
+                MOD_HIP(hipEventSynchronize(ev.e[4]));
+                float ms[4];
+                for (unsigned r = 0; r < 4; ++r) MOD_HIP(hipEventElapsedTime(&ms[r], ev.e[r], ev.e[r + 1]));
+                m->priv_choice[key] = std::min(ms[1], ms[3]) < std::min(ms[0], ms[2]) ? 1 : 0;
+                return DSP_OK;  // every run wrote the same output
             }
         }
     } else if (2ull * C * B * sizeof(float) <= kStagedLdsBytes) {
@@ -639,6 +715,11 @@ int module_render(dsp_module *m, const void *params, uint32_t params_size, const
         A.lds = 1;
         block = 256;
         lds_bytes = (unsigned)(2ull * C * B * sizeof(float));
+    }
+    if (m->stateless && A.lds) {
+        grid = priv_grid(grid);
+        A.lds = priv_mode(A.lds, B);
+        lds_bytes = A.lds == 2 ? kTileBytes : 0;
     }
     MOD_HIP(hipModuleLaunchKernel(m->f_render, grid, 1, 1, block, 1, 1, lds_bytes, s, args, nullptr));
     MOD_HIP(hipStreamSynchronize(s));  // the params blob is the caller's
