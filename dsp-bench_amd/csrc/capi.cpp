@@ -61,6 +61,7 @@ struct DeviceRes {
     std::map<std::tuple<int, uint32_t, uint32_t, float>, float *> windows;  // (kind, N, valid, scale)
     std::map<void *, std::pair<float *, size_t>> scratch;     // per stream
     std::vector<FirTaps> fir;                                  // FIR filters seen (plugin_map)
+    float *delta = nullptr;  // 2048 floats: 1, 0, 0, ... (compute_IR's impulse, read-only)
 };
 
 static std::mutex g_mu;
@@ -121,6 +122,22 @@ static int get_tw(int dev, const v2f **out) {
         DSPB_HIP(hipMemcpy(r.tw8192, h.data(), sizeof(v2f) * h.size(), hipMemcpyHostToDevice));
     }
     *out = r.tw8192;
+    return DSP_OK;
+}
+
+// compute_IR's impulse (plugin.cpp:27-34) as a read-only device buffer: the
+// IR render of a map plugin reads it as its file, so no impulse launch
+constexpr uint32_t kDeltaLen = 2048;  // the largest ir_len (4 ir_len <= 8192)
+static int get_delta(int dev, const float **out) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    DeviceRes &r = g_res[dev];
+    if (!r.delta) {
+        std::vector<float> h(kDeltaLen, 0.0f);
+        h[0] = 1.0f;
+        DSPB_HIP(hipMalloc(&r.delta, sizeof(float) * kDeltaLen));
+        DSPB_HIP(hipMemcpy(r.delta, h.data(), sizeof(float) * kDeltaLen, hipMemcpyHostToDevice));
+    }
+    *out = r.delta;
     return DSP_OK;
 }
 
@@ -919,19 +936,21 @@ int dsp_ir_analysis(const dsp_plugin *plugin, uint32_t C, float sr, uint32_t ir_
         for (uint32_t c = 0; c < C; ++c) dir[c] = ir_out[c];
     }
     // compute_IR (plugin.cpp:27-34): IR[c] = delta, then one callback of ir_len
-    for (uint32_t c0 = 0; c0 < C; c0 += kMaxChannels) {
-        const uint32_t cn = (C - c0) < (uint32_t)kMaxChannels ? (C - c0) : kMaxChannels;
-        ChanOut imp{};
-        for (uint32_t j = 0; j < cn; ++j) imp.p[j] = dir[c0 + j];
-        if ((st = launch_impulse(imp, cn, ir_len, s))) return st;
-    }
     SampleMap map;
     if ((st = plugin_map(plugin, ir_len, g.dev, s, &map, sr))) return st;
-    if (map.kind == MapKind::Generic) {  // fresh scratch State, one callback in place
+    if (map.kind == MapKind::Generic) {  // the impulse in place, a fresh scratch State, one callback
+        for (uint32_t c0 = 0; c0 < C; c0 += kMaxChannels) {
+            const uint32_t cn = (C - c0) < (uint32_t)kMaxChannels ? (C - c0) : kMaxChannels;
+            ChanOut imp{};
+            for (uint32_t j = 0; j < cn; ++j) imp.p[j] = dir[c0 + j];
+            if ((st = launch_impulse(imp, cn, ir_len, s))) return st;
+        }
         if ((st = module_ir((::dsp_module *)map.module, map.gparams, map.gparams_size, dir.data(), C, ir_len, sr, s)))
             return st;
-    } else {
-        std::vector<const float *> cin(dir.begin(), dir.end());
+    } else {  // map plugins: render the read-only impulse into IR[c], one launch
+        const float *delta;
+        if ((st = get_delta(g.dev, &delta))) return st;
+        std::vector<const float *> cin(C, delta);
         if ((st = render_device(cin.data(), C, ir_len, dir.data(), C, ir_len, map, 0, 0, s))) return st;
     }
 
