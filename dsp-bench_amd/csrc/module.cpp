@@ -671,8 +671,8 @@ int module_render(dsp_module *m, const void *params, uint32_t params_size, const
         // private copies cost ~3x the traffic of the in-place copy (no_op,
         // 1 h stereo: 2.6 vs 0.6 ms) while a callback that loads and stores
         // runs 2.5x faster there (gain_test: 3.3 vs 8.2 ms). So the first
-        // eligible render of a (C, B) shape runs both, twice each (same bits
-        // by construction), and the module keeps the faster; an in-place render
+        // eligible render of a (C, B) shape runs a warm-up and both paths
+        // twice each (same bits by construction), and keeps the faster; an in-place render
         // (in overlapping out) cannot run twice and takes the wave path until
         // a decision exists. DSPB_STATELESS_PRIVATE=0/1 forces one.
         if (C <= 2 && 1ull * C * B <= kPrivFloatsHost && A.nblocks >= kPrivMinBlocks) {
@@ -684,10 +684,13 @@ int module_render(dsp_module *m, const void *params, uint32_t params_size, const
             } else if (it != m->priv_choice.end()) {
                 A.lds = (unsigned)it->second;
             } else if (!overlaps(in, in_ch, out, C, A.nblocks * B)) {
-                // the order 0, 1, 0, 1, each path's faster run: the first
-                // launch also pays the output's first touch
+                // a warm-up run (it pays the output's first touch and the
+                // clock ramp), then the paths in the order 0, 1, 1, 0 (a
+                // drifting clock favours neither), each path's faster run
+                constexpr unsigned kRuns = 5;
+                static const unsigned kMode[kRuns] = {0, 0, 1, 1, 0};
                 struct Events {  // destroyed on every return
-                    hipEvent_t e[5] = {};
+                    hipEvent_t e[kRuns + 1] = {};
                     ~Events() {
                         for (hipEvent_t x : e)
                             if (x) (void)hipEventDestroy(x);
@@ -695,17 +698,21 @@ int module_render(dsp_module *m, const void *params, uint32_t params_size, const
                 } ev;
                 for (hipEvent_t &x : ev.e) MOD_HIP(hipEventCreate(&x));
                 MOD_HIP(hipEventRecord(ev.e[0], s));
-                for (unsigned r = 0; r < 4; ++r) {
-                    const unsigned mode = r & 1;
+                for (unsigned r = 0; r < kRuns; ++r) {
+                    const unsigned mode = kMode[r];
                     A.lds = priv_mode(mode, B);
                     MOD_HIP(hipModuleLaunchKernel(m->f_render, mode ? priv_grid(grid) : grid, 1, 1, block, 1, 1,
                                                   A.lds == 2 ? kTileBytes : 0, s, args, nullptr));
                     MOD_HIP(hipEventRecord(ev.e[r + 1], s));
                 }
-                MOD_HIP(hipEventSynchronize(ev.e[4]));
-                float ms[4];
-                for (unsigned r = 0; r < 4; ++r) MOD_HIP(hipEventElapsedTime(&ms[r], ev.e[r], ev.e[r + 1]));
-                m->priv_choice[key] = std::min(ms[1], ms[3]) < std::min(ms[0], ms[2]) ? 1 : 0;
+                MOD_HIP(hipEventSynchronize(ev.e[kRuns]));
+                float best[2] = {1e30f, 1e30f};
+                for (unsigned r = 1; r < kRuns; ++r) {
+                    float ms;
+                    MOD_HIP(hipEventElapsedTime(&ms, ev.e[r], ev.e[r + 1]));
+                    best[kMode[r]] = std::min(best[kMode[r]], ms);
+                }
+                m->priv_choice[key] = best[1] < best[0] ? 1 : 0;
                 return DSP_OK;  // every run wrote the same output
             }
         }
