@@ -161,10 +161,11 @@ __device__ static void dspb_stateless(const dspb_render_args &A) {
 // overwritten before it is written out). Thread 0 keeps Parameters and a
 // small State in private copies (written back at the end): the callback's
 // LDS stores cannot alias them, so they stay in registers. CC as above.
-template <unsigned CC>
+template <unsigned CC, unsigned NB = 0>
 __device__ static void dspb_stateful_lds(const dspb_render_args &A) {
     extern __shared__ float dspb_lbuf[];
-    const unsigned C = CC ? CC : A.C, CB = C * A.B, t = threadIdx.x, nt = blockDim.x;
+    const unsigned B = NB ? NB : A.B;
+    const unsigned C = CC ? CC : A.C, CB = C * B, t = threadIdx.x, nt = blockDim.x;
     float *buf0 = dspb_lbuf, *buf1 = dspb_lbuf + CB;
     dspb_stage_in(A, 0, buf0, t, nt);
     __syncthreads();
@@ -178,9 +179,9 @@ __device__ static void dspb_stateful_lds(const dspb_render_args &A) {
         float *cur = (b & 1) ? buf1 : buf0, *oth = (b & 1) ? buf0 : buf1;
         if (t == 0) {
             float *ptrs[CC ? CC : 16];
-            for (unsigned c = 0; c < C; ++c) ptrs[c] = cur + c * A.B;
-            if constexpr (kLocal) audio_callback(prm, local, ptrs, C, A.B, A.sr);
-            else audio_callback(prm, *gst, ptrs, C, A.B, A.sr);
+            for (unsigned c = 0; c < C; ++c) ptrs[c] = cur + c * B;
+            if constexpr (kLocal) audio_callback(prm, local, ptrs, C, B, A.sr);
+            else audio_callback(prm, *gst, ptrs, C, B, A.sr);
         } else if (t >= 64) {
             if (b > 0) dspb_stage_out(A, b - 1, oth, t - 64, nt - 64);
             if (b + 1 < A.nblocks) dspb_stage_in(A, b + 1, oth, t - 64, nt - 64);
@@ -311,7 +312,11 @@ extern "C" __global__ void dspb_render(dspb_render_args A) {
             for (unsigned long long b = 0; b < A.nblocks; ++b) dspb_block(A, b, st);
         }
     } else if (blockIdx.x == 0) {
-        if (A.C == 1) dspb_stateful_lds<1>(A);
+        // B = 512 stereo as constants too: the callback's sample loop then
+        // addresses one LDS base at constant offsets, so its loads can run
+        // ahead of its stores instead of waiting a round trip per sample
+        if (A.C == 2 && A.B == 512) dspb_stateful_lds<2, 512>(A);
+        else if (A.C == 1) dspb_stateful_lds<1>(A);
         else if (A.C == 2) dspb_stateful_lds<2>(A);
         else dspb_stateful_lds<0>(A);
     }
