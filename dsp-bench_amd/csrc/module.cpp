@@ -315,7 +315,10 @@ extern "C" __global__ void dspb_render(dspb_render_args A) {
         // B = 512 stereo as constants too: the callback's sample loop then
         // addresses one LDS base at constant offsets, so its loads can run
         // ahead of its stores instead of waiting a round trip per sample
+        // (512: the render configs; 256: BASELINE configs[0], the reference
+        // device's forced stereo)
         if (A.C == 2 && A.B == 512) dspb_stateful_lds<2, 512>(A);
+        else if (A.C == 2 && A.B == 256) dspb_stateful_lds<2, 256>(A);
         else if (A.C == 1) dspb_stateful_lds<1>(A);
         else if (A.C == 2) dspb_stateful_lds<2>(A);
         else dspb_stateful_lds<0>(A);

@@ -66,9 +66,10 @@ def test_reference_plugin_descriptor_and_defaults(torch_cuda, oracle, name):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", EXACT + list(TOL))
+# B = 512 and 256: the stateful driver's constant-B instantiations (stereo);
 # B = 16384: a stateful plugin's 2 x 2 x B floats no longer fit the driver's
 # 64 KB LDS double-buffer, so it takes the one-thread global-memory path
-@pytest.mark.parametrize("B", [512, 100, 16384])
+@pytest.mark.parametrize("B", [512, 256, 100, 16384])
 def test_reference_plugin_render(torch_cuda, oracle, name, B):
     if not have(name):
         pytest.skip("oracle/_ref not built")
