@@ -37,8 +37,7 @@ sys.path.insert(0, os.path.join(REPO, "dsp-bench_amd"))
 METRIC = "Msamples/s offline render+8192-pt FFT, 48kHz stereo, 1/2/4/8 GPU; %HBM roofline"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 FP32_PEAK_TFLOPS = 157.3  # MI355X FP32 vector (packed) peak, same table
-KERNELS = {0: "stft8192_kernel", 1: "stft8192_pair_kernel", 2: "stft8192_soa_kernel",
-           3: "stft8192_pair_soa_kernel", 4: "stft8192_pair2_kernel", 5: "stft8192_pk_kernel"}
+KERNEL = "stft8192_pk_kernel"
 SR, CH, B, N_FFT, HOP = 48_000, 2, 512, 8192, 4096
 K_BINS = N_FFT // 2 + 1
 
@@ -57,9 +56,6 @@ def parse():
     ap.add_argument("--gather", action="store_true", help="also time an RCCL gather to rank 0")
     ap.add_argument("--fir-method", type=int, default=0, choices=[0, 1, 2],
                     help="fir1024: 0 auto (overlap-save), 1 direct form, 2 overlap-save")
-    ap.add_argument("--stft-variant", type=int, default=5, choices=[0, 1, 2, 3, 4, 5],
-                    help="8192-pt kernel (dsp_stft_kernel_variant): 2 = wave/frame scalar SoA, "
-                         "5 = wave/frame packed even/odd pairs")
     ap.add_argument("--workload", default="headline",
                     choices=["headline", "stft96k", "ch96k", "gain10min", "fir1024", "wav16", "wav24", "ir",
                              "generic"],
@@ -216,7 +212,6 @@ def main():
     torch.cuda.set_device(dev)
 
     import dspbench as d
-    d.lib().dsp_stft_kernel_variant(args.stft_variant)
     d.lib().dsp_fir_method(args.fir_method)
     if args.workload == "ir":
         bench_ir(args, dev, world, rank)
@@ -275,19 +270,19 @@ def main():
                           K=K_BINS, out=out, mag=mag, sample_offset=soff)
         workload = ("IR_test render (B=512) + 8192-pt Hann STFT, hop 4096, 4097 bins, "
                     f"{minutes:g} min of 48 kHz stereo per GPU")
-        kname = f"{KERNELS[args.stft_variant]}<render> (fused render + window + FFT + |X|)"
+        kname = f"{KERNEL}<render> (fused render + window + FFT + |X|)"
     elif wl == "ch96k":
         def step():
             d.render_stft(x, CH, B, float(sr), plugin, N=N_FFT, H=HOP, window=d.DSP_WIN_HANN,
                           K=K_BINS, out=out, mag=mag)
         workload = ("BASELINE cfg 5: IR_test render (B=512) + 8192-pt Hann STFT of one 96 kHz channel "
                     f"({minutes:g} min) per GPU; channels sharded one per GPU")
-        kname = f"{KERNELS[args.stft_variant]}<render> (fused render + window + FFT + |X|)"
+        kname = f"{KERNEL}<render> (fused render + window + FFT + |X|)"
     elif wl == "stft96k":
         def step():
             d.stft_magnitude(x, N=N_FFT, H=HOP, window=d.DSP_WIN_HANN, K=K_BINS, out=mag)
         workload = f"8192-pt Hann STFT, hop 4096, 4097 bins, {minutes:g} min of 96 kHz stereo per GPU (cfg 4)"
-        kname = f"{KERNELS[args.stft_variant]}<memory> (window + FFT + |X|)"
+        kname = f"{KERNEL}<memory> (window + FFT + |X|)"
     elif wl == "fir1024":
         # BASELINE configs[2] / SURVEY cfg 3b: 1024 taps = compute_IR(IR_test)[0:1024]
         ir, _ = d.ir_analysis(d.Plugin.ir_test(0.9, 0.002), C_out=1, sr=float(sr), device=dev)
@@ -423,7 +418,7 @@ def main():
 
     traffic, traffic_src = (None, None)
     if wl in ("headline", "stft96k"):
-        traffic, traffic_src = pmc_traffic(wl, KERNELS[args.stft_variant], 1 if wl == "headline" else 0)
+        traffic, traffic_src = pmc_traffic(wl, KERNEL, 1 if wl == "headline" else 0)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and wl == "headline":

@@ -165,7 +165,9 @@ static int get_window(int dev, int kind, uint32_t N, uint32_t valid, const float
     return DSP_OK;
 }
 
-static float window_prescale(uint32_t N);
+// stft8192_pk_kernel folds DIV_BY_SQRTN and the 1/2 of the real split into
+// the window: 0.5 / sqrt(N)
+static float window_prescale(uint32_t N) { return (float)(0.5 / std::sqrt((double)N)); }
 
 // Inputs of the computed-window kernels (stft_soa.hip kOptWinComp): per-lane
 // base angles and the (pre-scaled) cosine-window coefficients.
@@ -222,37 +224,30 @@ struct TimedLaunch {
     uint64_t bytes;
 };
 static bool g_timing = false;
-// which 8192-point kernel: 0 = one wave per frame, packed (spectral.hip),
-// 1 = two waves per frame (stft_pair.hip), 2 = one wave per frame, scalar
-// SoA with a pre-scaled window (stft_soa.hip), 3 = two waves per frame,
-// scalar SoA (stft_pair_soa.hip), 4 = two frames packed per VGPR pair,
-// two waves per frame pair (stft_pair2.hip)
-static int g_stft_variant = 5;
-static int g_soa_opt = 14;  // stft_soa.hip OPT bits (A/B), default kSoaDefaultOpt
 
-// the SoA kernel folds 0.5/sqrt(N) into the window
-static float window_prescale(uint32_t N) {
-    return g_stft_variant >= 2 ? (float)(0.5 / std::sqrt((double)N)) : 1.0f;
-}
+#ifdef DSPB_AB_BUILD
+// A/B and ablation options of stft8192_pk_kernel (stft_pk.hpp kPk* bits),
+// only in the tools build (make ab -> build/ab/libdspbench_ab.so).  Thread
+// local: a thread's A/B switch never changes another thread's kernel.
+static thread_local int g_pk_ab_opt = 0;
+static int pk_options() { return g_pk_ab_opt; }
+#else
+static int pk_options() { return 0; }
+#endif
 
 // a closed-form IR ramp (plugin_map) leaves the block table unbuilt; every
-// fused kernel but stft_pk's PER path reads it
+// fused path but stft_pk's PER path reads it
 static int ensure_ramp_table(const SampleMap &m, hipStream_t s) {
     if (m.kind != MapKind::Ramp || !m.closed) return DSP_OK;
     return launch_ramp_table(const_cast<float *>(m.table), m.B, (float)m.rg0, (float)m.rs, s);
 }
 
-static int launch_stft(const Stft8kArgs &A, uint32_t C, bool fused, bool full, hipStream_t s) {
-    if (fused && !(g_stft_variant == 5 && A.map.closed && stft8192_pk_per_path(A, fused))) {
+static int launch_stft(const Stft8kArgs &A, uint32_t C, bool fused, hipStream_t s) {
+    if (fused && !(A.map.closed && stft8192_pk_per_path(A, fused))) {
         const int st = ensure_ramp_table(A.map, s);
         if (st) return st;
     }
-    if (g_stft_variant == 5) return launch_stft8192_pk(A, C, fused, g_soa_opt >> 4, s);
-    if (g_stft_variant == 4) return launch_stft8192_pair2(A, C, fused, s);
-    if (g_stft_variant == 3) return launch_stft8192_pair_soa(A, C, fused, s);
-    if (g_stft_variant == 2) return launch_stft8192_soa(A, C, fused, g_soa_opt, s);
-    if (g_stft_variant == 1) return launch_stft8192_pair(A, C, fused, s);
-    return launch_stft8192(A, C, fused, full, s);
+    return launch_stft8192_pk(A, C, fused, pk_options(), s);
 }
 
 static std::vector<TimedLaunch> g_timed;
@@ -595,7 +590,7 @@ static int stft_device(const float *const *in, uint32_t C, uint64_t L, uint32_t 
             if ((st = set_wincomp(dev, window, &A))) return st;
             TimedLaunch tl{};
             if ((st = timing_begin(s, &tl))) return st;
-            st = launch_stft(A, cn, false, true, s);
+            st = launch_stft(A, cn, false, s);
             if (st) return st;
             // algorithmic bytes: frame input read once per hop + magnitudes
             st = timing_end(s, &tl, (uint64_t)cn * F * ((uint64_t)H * 4 + (uint64_t)K * 4));
@@ -640,19 +635,13 @@ int dsp_fir_method(int m) {
     return old;
 }
 
-int dsp_stft_soa_options(int opt) {
-    std::lock_guard<std::mutex> lk(g_mu);
-    const int old = g_soa_opt;
-    if (opt >= 0 && opt <= 0xffff) g_soa_opt = opt;
+#ifdef DSPB_AB_BUILD
+int dsp_stft_pk_ab_options(int opt) {
+    const int old = g_pk_ab_opt;
+    if (opt >= 0 && opt <= 0xfff) g_pk_ab_opt = opt;
     return old;
 }
-
-int dsp_stft_kernel_variant(int v) {
-    std::lock_guard<std::mutex> lk(g_mu);
-    const int old = g_stft_variant;
-    if (v >= 0 && v <= 5) g_stft_variant = v;
-    return old;
-}
+#endif
 
 void dsp_kernel_timing_enable(int on) {
     std::lock_guard<std::mutex> lk(g_mu);
@@ -884,10 +873,10 @@ int dsp_render_stft(const float *const *in, uint32_t in_channels, uint64_t L,
             A.map = map;
             A.goff = goff;
             // the PER kernel also renders the tail no frame owns
-            if (g_stft_variant == 5 && stft8192_pk_per_path(A, true)) A.tail_end = Lr, tail_in_kernel = true;
+            if (stft8192_pk_per_path(A, true)) A.tail_end = Lr, tail_in_kernel = true;
             TimedLaunch tl{};
             if ((st = timing_begin(s, &tl))) return st;
-            if ((st = launch_stft(A, cn, true, true, s))) return st;
+            if ((st = launch_stft(A, cn, true, s))) return st;
             // algorithmic bytes: render write 4 B + magnitudes 4 K/H B
             // per hop sample, plus the file read when the map uses its input
             const uint64_t hop_samples = (uint64_t)cn * F * H;
@@ -920,6 +909,8 @@ int dsp_ir_analysis(const dsp_plugin *plugin, uint32_t C, float sr, uint32_t ir_
     if (!ir_out || !mag) return invalid("ir_out / mag is NULL");
     for (uint32_t c = 0; c < C; ++c)
         if (!ir_out[c]) return invalid("ir_out[%u] is NULL", c);
+    if (plugin && plugin->kind == DSP_PLUGIN_GENERIC && C > (uint32_t)kMaxChannels)
+        return invalid("GENERIC plugin: IR analysis of 1..%d channels", kMaxChannels);
     DeviceGuard g(ex);
     if (g.status) return g.status;
     hipStream_t s = stream_of(ex);
@@ -975,7 +966,7 @@ int dsp_ir_analysis(const dsp_plugin *plugin, uint32_t C, float sr, uint32_t ir_
         A.win2 = reinterpret_cast<const v2f *>(win);
         A.tw = tw;
         A.scale = (float)(1.0 / std::sqrt((double)n));
-        if ((st = launch_stft(A, 1, false, false, s))) return st;
+        if ((st = launch_stft(A, 1, false, s))) return st;
     } else {
         GenericFftArgs A{};
         A.sig.p[0] = dir[0];

@@ -65,11 +65,6 @@ struct GenericFftArgs {
 
 int launch_ramp_table(float *table, uint32_t B, float gain, float step, hipStream_t s);
 int launch_render(const RenderArgs &A, uint32_t C, bool vec, hipStream_t s);
-int launch_stft8192(const Stft8kArgs &A, uint32_t C, bool fused, bool full, hipStream_t s);
-int launch_stft8192_pair(const Stft8kArgs &A, uint32_t C, bool fused, hipStream_t s);
-int launch_stft8192_soa(const Stft8kArgs &A, uint32_t C, bool fused, int opt, hipStream_t s);
-int launch_stft8192_pair_soa(const Stft8kArgs &A, uint32_t C, bool fused, hipStream_t s);
-int launch_stft8192_pair2(const Stft8kArgs &A, uint32_t C, bool fused, hipStream_t s);
 int module_render(::dsp_module *m, const void *params, uint32_t params_size, const float *const *in,
                   uint32_t in_ch, uint64_t L, float *const *out, uint32_t C, uint32_t B, float sr,
                   uint64_t goff, hipStream_t s);

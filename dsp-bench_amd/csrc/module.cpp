@@ -337,6 +337,7 @@ struct ArenaHost {  // mirror of dspb_arena
     unsigned long long capacity;
     unsigned long long used;
     float *fft_tmp;
+    unsigned long long failed;
 };
 
 }  // namespace
@@ -388,7 +389,7 @@ int make_arena(dsp_module *m, int slot, uint64_t bytes) {
     if (!m->d_arena[slot]) MOD_HIP(hipMalloc(&m->d_arena[slot], sizeof(ArenaHost)));
     if (bytes) MOD_HIP(hipMalloc(&m->arena_mem[slot], bytes));
     if (bytes) MOD_HIP(hipMemset(m->arena_mem[slot], 0, bytes));
-    ArenaHost h{m->arena_mem[slot], bytes, 0, nullptr};
+    ArenaHost h{m->arena_mem[slot], bytes, 0, nullptr, 0};
     MOD_HIP(hipMemcpy(m->d_arena[slot], &h, sizeof h, hipMemcpyHostToDevice));
     return DSP_OK;
 }
@@ -410,9 +411,10 @@ int init_slot(dsp_module *m, int slot, const void *params, uint32_t C, float sr,
     ArenaHost h{};
     MOD_HIP(hipMemcpyAsync(&h, m->d_arena[slot], sizeof h, hipMemcpyDeviceToHost, s));
     MOD_HIP(hipStreamSynchronize(s));
-    if (h.used > h.capacity) {  // an allocator returned NULL: Runtime_Low_Memory (errors.inc:22-23)
-        set_last_error("initialize_state: arena of %llu bytes exhausted (%llu requested)",
-                       (unsigned long long)h.capacity, (unsigned long long)h.used);
+    if (h.failed) {  // an allocator returned NULL: Runtime_Low_Memory (errors.inc:22-23)
+        set_last_error("initialize_state: arena of %llu bytes exhausted (%llu used, a request of %llu failed)",
+                       (unsigned long long)h.capacity, (unsigned long long)h.used,
+                       (unsigned long long)h.failed);
         return DSP_ERR_NOMEM;
     }
     return DSP_OK;
@@ -618,6 +620,18 @@ static unsigned priv_mode(unsigned mode, uint32_t B) {
     return mode && tiled && B % 64 == 0 ? 2u : mode;
 }
 
+// the module's code object, Parameters and State live on m->device: a call
+// made on another device (e.g. a mis-wired shard rank) is refused
+static int check_device(const dsp_module *m) {
+    int dev = -1;
+    MOD_HIP(hipGetDevice(&dev));
+    if (dev != m->device) {
+        set_last_error("GENERIC plugin: module loaded on device %d, called on device %d", m->device, dev);
+        return DSP_ERR_INVALID;
+    }
+    return DSP_OK;
+}
+
 // does any input channel's [0, n) overlap any output channel's [0, n) floats
 static bool overlaps(const float *const *in, uint32_t in_ch, float *const *out, uint32_t C, uint64_t n) {
     for (uint32_t a = 0; a < in_ch; ++a)
@@ -636,6 +650,7 @@ int module_render(dsp_module *m, const void *params, uint32_t params_size, const
         set_last_error("GENERIC plugin: module not loaded / initialize_state not run");
         return DSP_ERR_INVALID;
     }
+    if (int st = check_device(m)) return st;
     if (params_size != m->params_size || (!params && params_size)) {
         set_last_error("GENERIC plugin: params blob is %u bytes, the plugin's Parameters %u", params_size,
                        m->params_size);
@@ -746,6 +761,11 @@ int module_render(dsp_module *m, const void *params, uint32_t params_size, const
 int module_ir(dsp_module *m, const void *params, uint32_t params_size, float *const *bufs, uint32_t C,
               uint32_t n, float sr, hipStream_t s) {
     if (!m) return DSP_ERR_INVALID;
+    if (C == 0 || C > (uint32_t)kMaxChannels) {  // the driver's channel table holds 16 pointers
+        set_last_error("GENERIC plugin: 1..%d channels", kMaxChannels);
+        return DSP_ERR_INVALID;
+    }
+    if (int st = check_device(m)) return st;
     if (params_size != m->params_size || (!params && params_size)) {
         set_last_error("GENERIC plugin: params blob is %u bytes, the plugin's Parameters %u", params_size,
                        m->params_size);

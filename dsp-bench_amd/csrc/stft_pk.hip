@@ -30,7 +30,9 @@ int launch_stft8192_pk(const Stft8kArgs &A, uint32_t C, bool fused, int opt, hip
     if (fused && A.map.kind == MapKind::Ramp && pow2 && winc) {
         // period of the block table in units of 128 samples
         const uint32_t per = A.map.B <= 128u ? 1u : A.map.B / 128u;
+#ifdef DSPB_AB_BUILD
         if (per == 4 && opt) return launch_pk_ab(A, fused, opt, grid, stream);  // A/B at the headline shape
+#endif
 #define DSPB_PK_PER(p) \
     hipLaunchKernelGGL((stft8192_pk_kernel<kSrcRender, kKHalf, MapKind::Ramp, true, true, p>), grid, dim3(256), \
                        0, stream, A)
@@ -46,7 +48,11 @@ int launch_stft8192_pk(const Stft8kArgs &A, uint32_t C, bool fused, int opt, hip
         DSPB_HIP(hipGetLastError());
         return DSP_OK;
     }
+#ifdef DSPB_AB_BUILD
     if (!fused && winc && (opt & kPkMemAos)) return launch_pk_ab(A, fused, opt, grid, stream);
+#else
+    (void)opt;  // the A/B options exist only in the tools build (make ab)
+#endif
     return launch_pk_paths(A, fused, km, pow2, winc, grid, stream);
 }
 

@@ -87,8 +87,6 @@ _SIGS = {
     "dsp_set": (C.c_int, [C.c_float, FP, C.c_uint64, C.POINTER(dsp_exec)]),
     "dsp_magnitude": (C.c_int, [FP, FP, FP, C.c_uint64, C.POINTER(dsp_exec)]),
     "dsp_kernel_timing_enable": (None, [C.c_int]),
-    "dsp_stft_kernel_variant": (C.c_int, [C.c_int]),
-    "dsp_stft_soa_options": (C.c_int, [C.c_int]),
     "dsp_fir_method": (C.c_int, [C.c_int]),
     "dsp_kernel_timing": (C.c_int, [C.POINTER(C.c_double), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     "dsp_initializer_create": (C.c_void_p, [C.c_size_t, C.c_int]),
@@ -118,6 +116,11 @@ _SIGS = {
                                        C.c_uint16, C.c_uint64]),
 }
 
+# exported only by the A/B tools build (build/ab/libdspbench_ab.so)
+_OPTIONAL_SIGS = {
+    "dsp_stft_pk_ab_options": (C.c_int, [C.c_int]),
+}
+
 _lib: C.CDLL | None = None
 
 
@@ -132,6 +135,11 @@ def lib() -> C.CDLL:
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
+        for name, (res, args) in _OPTIONAL_SIGS.items():  # tools build only (make ab)
+            fn = getattr(L, name, None)
+            if fn is not None:
+                fn.restype = res
+                fn.argtypes = args
         _lib = L
     return _lib
 

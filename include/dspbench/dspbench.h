@@ -25,9 +25,9 @@
  * specialised kernel that reads the plugin's own parameter / state blob at
  * the struct offsets the plugin declares (gain_test: Parameters{float gain},
  * IR_test: Parameters{float gain; float step}, static_gain_plugin:
- * State{float gain}).  DSP_PLUGIN_GENERIC (the plugin's own compiled
- * audio_callback run on the GPU) is reserved: this build returns
- * DSP_ERR_UNSUPPORTED for it ("next").
+ * State{float gain}).  DSP_PLUGIN_GENERIC runs the plugin's own
+ * audio_callback, compiled from its unchanged source to gfx950 code by the
+ * module compiler (module.h), through the generic block driver.
  *
  * Errors: every entry point returns DSP_OK (0) or a negative dsp_status.
  * Nothing aborts; HIP errors are mapped to DSP_ERR_HIP and the HIP error
@@ -168,27 +168,10 @@ int dsp_spectrogram_decimate(const float *mag, uint64_t F, uint32_t K, uint64_t 
 void dsp_kernel_timing_enable(int on);
 int dsp_kernel_timing(double *total_ms, uint64_t *launches, uint64_t *bytes);
 
-/* Select the 8192-point kernel (A/B and tests): 0 = one wavefront per frame,
- * packed float2 math; 1 = two wavefronts per frame; 2 = one wavefront per
- * frame, scalar structure-of-arrays math; 3 = variant 2 split over two
- * wavefronts; 4 = two frames per wavefront pair; 5 = one wavefront per
- * frame, even/odd halves in packed VGPR pairs (default).  Other values
- * only query.
- * Returns the previous selection. */
-int dsp_stft_kernel_variant(int variant);
-
-/* Option bits of variant 2 (A/B): 1 = no scheduling barrier inside the
- * register DFTs, 2 = prefetch the stage twiddles (lane-major table) with the
- * frame load, 4 = compute the window (angle addition) instead of loading it,
- * 8 = stage the IR_RAMP block table through LDS.  Bits 4..8 (options >> 4)
- * are variant 5's: 1/2/4 = no scheduling barriers in the DFTs / twiddle
- * loop / split loop, 8 = cached render stores (default non-temporal), 16 =
- * non-temporal magnitude stores (with 64), 32 = magnitude rows staged
- * through LDS, 64 = the older scalar last combine and split, 128 / 256 =
- * ablation: skip the render / magnitude stores (results discarded) (B = 512
- * shape).  Default 14.  Values outside 0..0xffff only query.  Returns the
- * previous options. */
-int dsp_stft_soa_options(int options);
+/* The 8192-point kernel and its options are fixed at build time.  The A/B
+ * and ablation instantiations live in a separate tools build (`make ab`:
+ * build/ab/libdspbench_ab.so, which adds dsp_stft_pk_ab_options()); this
+ * library has no process-wide kernel selection. */
 
 /* FIR render method (DSP_PLUGIN_FIR): 0 = auto (FFT overlap-save with
  * 8192-point frames when T <= 1025, else direct form), 1 = direct form,

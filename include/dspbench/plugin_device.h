@@ -44,15 +44,27 @@ struct dspb_arena {
     unsigned long long capacity;
     unsigned long long used;
     float *fft_tmp;  /* fft_reverse's imaginary work buffer (8192 floats), made on first use */
+    unsigned long long failed;  /* bytes of the first request that did not fit (0: none) */
 };
 
+/* Bump allocation, 16-byte slices.  The capacity is checked before the slice
+ * is claimed (compare-and-swap), so a request that does not fit leaves the
+ * arena as it was and later smaller requests still succeed; the failure is
+ * recorded for initialize_state's Runtime_Low_Memory (errors.inc:22-23). */
 static inline void *dspb_arena_alloc(void *ctx, unsigned long long bytes) {
     dspb_arena *a = (dspb_arena *)ctx;
     if (!a) return 0;
     const unsigned long long n = (bytes + 15ull) & ~15ull;
-    const unsigned long long off = atomicAdd(&a->used, n);
-    if (off + n > a->capacity) return 0;
-    return a->base + off;
+    unsigned long long off = a->used;
+    for (;;) {
+        if (n < bytes || n > a->capacity || off > a->capacity - n) {
+            atomicCAS(&a->failed, 0ull, bytes ? bytes : 1ull);
+            return 0;
+        }
+        const unsigned long long seen = atomicCAS(&a->used, off, off + n);
+        if (seen == off) return a->base + off;
+        off = seen;
+    }
 }
 
 static inline float *allocate_buffer(int num_sample, void *ctx) {

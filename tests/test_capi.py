@@ -89,6 +89,22 @@ def test_invalid_arguments_rejected_before_device_use():
     assert L.dsp_render_offline(rows, 1, 1024, rows, 0, 512, 48000.0, None, C.byref(ex)) == 0   # C = 0: no-op
 
 
+def test_generic_ir_analysis_rejects_more_than_16_channels():
+    """The generic driver's channel table holds 16 pointers: a GENERIC
+    plugin's IR analysis with C = 17 is refused before any device or module
+    use (the module handle here is never dereferenced)."""
+    L = d.lib()
+    bufs = np.zeros((17, 2048), np.float32)
+    mag = np.zeros(8192, np.float32)
+    rows = _lib.chan_table([bufs[c].ctypes.data for c in range(17)])
+    plug = _lib.dsp_plugin(_lib.DSP_PLUGIN_GENERIC, 0, None, 0, None, C.c_void_p(0x1000))
+    ex = _exec_host()
+    st = L.dsp_ir_analysis(C.byref(plug), 17, 48000.0, 2048, rows, mag.ctypes.data_as(_lib.FP), C.byref(ex))
+    assert st == -1
+    L.dsp_last_error.restype = C.c_char_p
+    assert b"1..16 channels" in L.dsp_last_error()
+
+
 @pytest.mark.skipif(d.lib().dsp_device_count() > 0, reason="a GPU is visible")
 def test_no_gpu_fails_loudly_no_cpu_fallback():
     """The product path has no CPU fallback: without a device every compute

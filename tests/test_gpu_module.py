@@ -209,3 +209,125 @@ def test_generic_without_module_is_rejected(torch_cuda):
     x = torch_cuda.zeros((1, 1024), device="cuda")
     with pytest.raises(d.DspError):
         d.render_offline(x, 1, 512, 48000.0, d.Plugin(d._lib.DSP_PLUGIN_GENERIC, b"", b"", "none"))
+
+
+# ---- stateful driver branches no stock plugin reaches ---------
+ONE_POLE_SRC = r'''
+#include "plugin_header.h"
+struct Parameters { FLOAT_PARAM(0.0f, 1.0f) a; };
+struct State { float z[16]; };
+Parameters default_parameters() { Parameters p = {0.25f}; return p; }
+State initialize_state(const Parameters& p, const unsigned C, const float sr, void* ctx) {
+    State s; for (int c = 0; c < 16; ++c) s.z[c] = 0.0f; return s;
+}
+void audio_callback(const Parameters& p, State& st, float** out, const u32 C, const u32 B, const real32 sr) {
+    for (u32 c = 0; c < C; ++c)
+        for (u32 s = 0; s < B; ++s) {
+            const float d = out[c][s] - st.z[c];
+            st.z[c] = st.z[c] + p.a * d;
+            out[c][s] = st.z[c];
+        }
+}
+'''
+
+# State of 1 KB + 4 B (> the driver's 256-byte private-copy limit): the
+# callback works on the global State directly
+DELAY_SRC = r'''
+#include "plugin_header.h"
+struct Parameters { FLOAT_PARAM(0.0f, 1.0f) mix; };
+struct State { float ring[2][128]; int pos; };
+Parameters default_parameters() { Parameters p = {0.5f}; return p; }
+State initialize_state(const Parameters& p, const unsigned C, const float sr, void* ctx) {
+    State s; for (int c = 0; c < 2; ++c) for (int i = 0; i < 128; ++i) s.ring[c][i] = 0.0f; s.pos = 0; return s;
+}
+void audio_callback(const Parameters& p, State& st, float** out, const u32 C, const u32 B, const real32 sr) {
+    for (u32 s = 0; s < B; ++s) {
+        const int w = (st.pos + (int)s) & 127, r = (st.pos + (int)s - 100) & 127;
+        for (u32 c = 0; c < C && c < 2; ++c) {
+            const float x = out[c][s];
+            const float y = x + p.mix * st.ring[c][r];
+            st.ring[c][w] = x;
+            out[c][s] = y;
+        }
+    }
+    st.pos = (st.pos + (int)B) & 127;
+}
+'''
+
+
+def _padded(x, C, B):
+    n = (x.shape[1] + B - 1) // B * B
+    xp = np.zeros((C, n), np.float32)
+    xp[:x.shape[0], :x.shape[1]] = x
+    return xp
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("C,B", [(1, 512), (1, 100), (4, 512), (4, 64)])
+def test_stateful_lds_driver_mono_and_multichannel(torch_cuda, C, B):
+    """dspb_stateful_lds<1> (mono) and <0> (C > 2) against a float32 numpy
+    restatement of the one-pole recurrence (bit-exact: no FMA contraction)."""
+    mod = d.module.Module(d.module.compile_source(ONE_POLE_SRC, "one_pole.cpp"))
+    assert not mod.stateless and mod.state_size == 64
+    params = mod.default_parameters()
+    mod.initialize_state(params, C, 48000.0)
+    x = np.random.default_rng(11).uniform(-1, 1, (C, 5000)).astype(np.float32)
+    got = d.render_offline(torch_cuda.from_numpy(x).cuda(), C, B, 48000.0, mod.plugin(params)).cpu().numpy()
+    xp = _padded(x, C, B)
+    a = np.float32(0.25)
+    want = np.zeros_like(xp)
+    for c in range(C):
+        z = np.float32(0)
+        for i in range(xp.shape[1]):
+            z = np.float32(z + np.float32(a * np.float32(xp[c, i] - z)))
+            want[c, i] = z
+    assert np.array_equal(got, want)
+    # the State carries the last sample of every channel
+    st = np.frombuffer(mod.read_state(), np.float32)
+    assert np.array_equal(st[:C], want[:, -1])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B", [512, 37])
+def test_stateful_large_state_in_global_memory(torch_cuda, B):
+    """A State larger than 256 bytes: the callback mutates the device State
+    in place (the non-private branch of dspb_stateful_lds)."""
+    mod = d.module.Module(d.module.compile_source(DELAY_SRC, "delay.cpp"))
+    assert mod.state_size == 2 * 128 * 4 + 4
+    params = mod.default_parameters()
+    mod.initialize_state(params, 2, 48000.0)
+    x = np.random.default_rng(12).uniform(-1, 1, (2, 7000)).astype(np.float32)
+    got = d.render_offline(torch_cuda.from_numpy(x).cuda(), 2, B, 48000.0, mod.plugin(params)).cpu().numpy()
+    xp = _padded(x, 2, B)
+    want = xp.copy()
+    want[:, 100:] = xp[:, 100:] + np.float32(0.5) * xp[:, :-100]
+    assert np.array_equal(got, want)
+
+
+ARENA_SRC = r'''
+#include "plugin_header.h"
+struct Parameters { FLOAT_PARAM(0.0f, 1.0f) g; };
+struct State { float *big; float *small; };
+Parameters default_parameters() { Parameters p = {1.0f}; return p; }
+State initialize_state(const Parameters& p, const unsigned C, const float sr, void* ctx) {
+    State s;
+    s.big = allocate_buffer(1 << 20, ctx);   // 4 MB: does not fit the arena
+    s.small = allocate_buffer(16, ctx);      // 64 B: still fits after the failure
+    return s;
+}
+void audio_callback(const Parameters& p, State& st, float** out, const u32 C, const u32 B, const real32 sr) {}
+'''
+
+
+@pytest.mark.gpu
+def test_arena_overflow_leaves_room_for_later_allocations(torch_cuda):
+    """allocate_*: a request that does not fit returns NULL without claiming
+    the arena (initialize_state then reports Runtime_Low_Memory = NOMEM), and
+    a later small request still succeeds."""
+    mod = d.module.Module(d.module.compile_source(ARENA_SRC, "arena.cpp"))
+    params = mod.default_parameters()
+    with pytest.raises(d.DspError) as e:
+        mod.initialize_state(params, 1, 48000.0, arena_bytes=64 << 10)
+    assert e.value.status == d._lib.DSP_ERR_NOMEM
+    big, small = struct.unpack("<QQ", mod.read_state())
+    assert big == 0 and small != 0

@@ -29,15 +29,6 @@ def rnd(shape, seed):
     return np.random.default_rng(seed).uniform(-1.0, 1.0, size=shape).astype(np.float32)
 
 
-@pytest.fixture(params=[0, 1, 2, 3, 4, 5], ids=["wave", "pair", "soa", "pairsoa", "pair2", "pk"])
-def variant(request):
-    """Run the test on every 8192-point kernel (dsp_stft_kernel_variant)."""
-    L = d.lib()
-    old = L.dsp_stft_kernel_variant(request.param)
-    yield request.param
-    L.dsp_stft_kernel_variant(old)
-
-
 def to_dev(torch, x):
     return torch.from_numpy(np.ascontiguousarray(x)).cuda()
 
@@ -108,32 +99,10 @@ def test_render_matches_reference_plugin_so(torch_cuda, oracle):
         assert np.array_equal(got, ref), name
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("opt", [0, 2048])
-@pytest.mark.parametrize("H", [4096, 1000])
-def test_pk_memory_load_options(torch_cuda, oracle, opt, H):
-    """Packed kernel, frames from memory with the computed window: pairs
-    regrouped at the load (default) or after the window multiply (2048),
-    against float64, on an offset (unaligned) signal view."""
-    L = d.lib()
-    oldv, oldo = L.dsp_stft_kernel_variant(5), L.dsp_stft_soa_options(14 | (opt << 4))
-    try:
-        n = 8192 * 6 + 555
-        x = rnd((2, n + 2), 64)
-        xd = to_dev(torch_cuda, x)[:, 2:]
-        mag = d.stft_magnitude(xd, N=8192, H=H, window=d.DSP_WIN_HANN, K=4097).cpu().numpy()
-        for c in range(2):
-            ref = oracle.np_stft_mag(x[c, 2:], 8192, H, d.DSP_WIN_HANN, 4097)
-            assert peak_rel_err(mag[c], ref) <= PEAK_REL_TOL
-    finally:
-        L.dsp_stft_kernel_variant(oldv)
-        L.dsp_stft_soa_options(oldo)
-
-
 @pytest.mark.parametrize("window", [d.DSP_WIN_HANN, d.DSP_WIN_HAMMING])
 @pytest.mark.parametrize("K", [4097, 8192, 1000])
 @pytest.mark.parametrize("H", [4096, 2048, 8192, 1000])
-def test_stft_8192_vs_f64(torch_cuda, oracle, window, K, H, variant):
+def test_stft_8192_vs_f64(torch_cuda, oracle, window, K, H):
     L = 8192 * 3 + 1234
     x = rnd((2, L), 21)
     mag = d.stft_magnitude(to_dev(torch_cuda, x), N=8192, H=H, window=window, K=K).cpu().numpy()
@@ -153,7 +122,7 @@ def test_stft_generic_sizes(torch_cuda, oracle, N):
     assert peak_rel_err(mag[0], ref) <= PEAK_REL_TOL
 
 
-def test_stft_sine_tone_peak(torch_cuda, oracle, variant):
+def test_stft_sine_tone_peak(torch_cuda, oracle):
     """A pure tone: peak bin, and sidelobes relative to the peak."""
     n = np.arange(8192 * 4)
     x = (0.5 * np.sin(2 * np.pi * 1000.25 / 48000 * n)).astype(np.float32)[None]
@@ -165,7 +134,7 @@ def test_stft_sine_tone_peak(torch_cuda, oracle, variant):
 
 @pytest.mark.parametrize("pname", ["IR_test", "gain_test", "static_gain_plugin", "no_op"])
 @pytest.mark.parametrize("B", [512, 384, 1, 4096])
-def test_render_stft_fused(torch_cuda, oracle, pname, B, variant):
+def test_render_stft_fused(torch_cuda, oracle, pname, B):
     L = 8192 * 6 + 777
     x = rnd((2, L), 31)
     out, mag = d.render_stft(to_dev(torch_cuda, x), 2, B, 48000.0, PLUGINS[pname][0](),
@@ -180,7 +149,7 @@ def test_render_stft_fused(torch_cuda, oracle, pname, B, variant):
         assert peak_rel_err(mag[c], mref) <= PEAK_REL_TOL
 
 
-def test_render_stft_shards_match_whole(torch_cuda, variant):
+def test_render_stft_shards_match_whole(torch_cuda):
     """Time-chunk sharding with a halo: each shard's frames and
     render equal the corresponding slice of the unsharded result."""
     torch = torch_cuda
@@ -200,7 +169,7 @@ def test_render_stft_shards_match_whole(torch_cuda, variant):
         assert torch.equal(mag_s, mag_all[:, f0:f0 + nf])
 
 
-def test_ir_analysis_gain_flat(torch_cuda, oracle, variant):
+def test_ir_analysis_gain_flat(torch_cuda, oracle):
     """K4: IR of gain_test(0.2) = 0.2 delta; w[0] = 0.08 -> flat 0.2*0.08/sqrt(8192)."""
     ir, mag = d.ir_analysis(d.Plugin.gain_test(0.2), 2, 48000.0)
     expect = np.zeros((2, 2048), np.float32)
@@ -211,7 +180,7 @@ def test_ir_analysis_gain_flat(torch_cuda, oracle, variant):
     assert np.max(np.abs(mag - flat)) <= 1e-6 * flat * 8
 
 
-def test_ir_analysis_ir_test_kat(torch_cuda, oracle, variant):
+def test_ir_analysis_ir_test_kat(torch_cuda, oracle):
     """K5: IR_test(0.9, 0.002) magnitudes at bins 0, 1, 2, 4096, 8191."""
     ir, mag = d.ir_analysis(d.Plugin.ir_test(0.9, 0.002), 1, 48000.0)
     ramp = oracle.ir_ramp_reference(0.9, 0.002, 2048)
@@ -260,7 +229,7 @@ def test_full_size_gain_render_10min(torch_cuda):
     assert torch.equal(out, x * torch.tensor(0.2, dtype=torch.float32, device="cuda"))
 
 
-def test_full_size_ir_test_stft_1h(torch_cuda, oracle, variant):
+def test_full_size_ir_test_stft_1h(torch_cuda, oracle):
     """Headline workload at full size: 1 h stereo 48 kHz through IR_test +
     8192-pt Hann STFT (hop 4096).  Properties: the render is the B-periodic
     ramp everywhere; every frame of a B-periodic signal with B | H is the same
@@ -281,81 +250,18 @@ def test_full_size_ir_test_stft_1h(torch_cuda, oracle, variant):
         assert spread <= 1e-6 * float(ref0.max())
 
 
-@pytest.mark.parametrize("B", [2, 64, 512, 4096, 8192])
-@pytest.mark.parametrize("opt", range(0, 16, 2))
-def test_soa_kernel_options(torch_cuda, oracle, opt, B):
-    """Every A/B option combination of the SoA kernel (dsp_stft_soa_options)
-    on the fused IR_test path (ramp table in LDS for 4 <= B <= 4096, global
-    gathers otherwise) and the memory path, 4097 bins."""
-    L = d.lib()
-    oldv, oldo = L.dsp_stft_kernel_variant(2), L.dsp_stft_soa_options(opt)
-    try:
-        n = 8192 * 5 + 99
-        x = rnd((2, n), 61)
-        for win in (d.DSP_WIN_HANN, d.DSP_WIN_HAMMING):
-            out, mag = d.render_stft(to_dev(torch_cuda, x), 2, B, 48000.0, d.Plugin.ir_test(), window=win)
-            ref = oracle.render_offline([x[0], x[1]], 2, B, 48000.0, oracle.restated_plugin("IR_test"))
-            assert np.array_equal(out.cpu().numpy(), ref)
-            mref = oracle.np_stft_mag(ref[0], 8192, 4096, win, 4097)
-            assert peak_rel_err(mag.cpu().numpy()[0], mref) <= PEAK_REL_TOL
-            m2 = d.stft_magnitude(to_dev(torch_cuda, x), window=win).cpu().numpy()
-            assert peak_rel_err(m2[1], oracle.np_stft_mag(x[1], 8192, 4096, win, 4097)) <= PEAK_REL_TOL
-    finally:
-        L.dsp_stft_kernel_variant(oldv)
-        L.dsp_stft_soa_options(oldo)
-
-
 @pytest.mark.parametrize("B", [2, 64, 128, 256, 1024, 2048, 4096, 8192])
 def test_pk_ramp_table_periods(torch_cuda, oracle, B):
-    """Packed kernel (variant 5): the IR_test block table is fetched once
-    per period of B / 128 columns and aliased (stft_pk.hip PER)."""
-    L = d.lib()
-    oldv = L.dsp_stft_kernel_variant(5)
-    try:
-        n = 8192 * 4 + 777
-        x = rnd((2, n), 62)
-        out, mag = d.render_stft(to_dev(torch_cuda, x), 2, B, 48000.0, d.Plugin.ir_test(0.7, 0.001),
-                                 window=d.DSP_WIN_HANN, sample_offset=B * 3)
-        ref = oracle.render_offline([x[0], x[1]], 2, B, 48000.0, oracle.restated_plugin("IR_test", [0.7, 0.001]))
-        assert np.array_equal(out.cpu().numpy(), ref)
-        mref = oracle.np_stft_mag(ref[1], 8192, 4096, d.DSP_WIN_HANN, 4097)
-        assert peak_rel_err(mag.cpu().numpy()[1], mref) <= PEAK_REL_TOL
-    finally:
-        L.dsp_stft_kernel_variant(oldv)
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("opt", [0, 8, 32, 40, 48, 56, 64, 72, 80, 88, 512, 520, 1024, 1032])
-def test_pk_store_options(torch_cuda, oracle, opt):
-    """Packed kernel A/B bits (dsp_stft_soa_options >> 4: 8 cached render
-    stores, 16 non-temporal magnitude stores, 32 rows staged through LDS, 64
-    the older scalar last combine and (ka, ka + 16) split, 512 rows staged in
-    LDS at their 16-byte phase): the same bits as
-    the default path (packed combine + split_y2; within 1e-7 of its peak for
-    64), rows of any alignment (ld = K)."""
-    L = d.lib()
-    oldv, oldo = L.dsp_stft_kernel_variant(5), L.dsp_stft_soa_options(14 | (opt << 4))
-    try:
-        n = 8192 * 5 + 301
-        x = rnd((2, n), 63)
-        out, mag = d.render_stft(to_dev(torch_cuda, x), 2, 512, 48000.0, d.Plugin.ir_test(0.9, 0.002),
-                                 window=d.DSP_WIN_HANN)
-        L.dsp_stft_soa_options(14)
-        out0, mag0 = d.render_stft(to_dev(torch_cuda, x), 2, 512, 48000.0, d.Plugin.ir_test(0.9, 0.002),
-                                   window=d.DSP_WIN_HANN)
-        assert np.array_equal(out.cpu().numpy(), out0.cpu().numpy())
-        if opt & 64:  # the other split's operation order: the last bit may differ
-            assert peak_rel_err(mag.cpu().numpy()[0], mag0.cpu().numpy()[0]) <= 1e-7
-        else:
-            assert np.array_equal(mag.cpu().numpy(), mag0.cpu().numpy())
-        ref = oracle.render_offline([x[0], x[1]], 2, 512, 48000.0, oracle.restated_plugin("IR_test", [0.9, 0.002]))
-        assert np.array_equal(out.cpu().numpy(), ref)
-        for c in range(2):
-            mref = oracle.np_stft_mag(ref[c], 8192, 4096, d.DSP_WIN_HANN, 4097)
-            assert peak_rel_err(mag.cpu().numpy()[c], mref) <= PEAK_REL_TOL
-    finally:
-        L.dsp_stft_kernel_variant(oldv)
-        L.dsp_stft_soa_options(oldo)
+    """Packed kernel: the IR_test block table is fetched once per period of
+    B / 128 columns and aliased (stft_pk.hip PER)."""
+    n = 8192 * 4 + 777
+    x = rnd((2, n), 62)
+    out, mag = d.render_stft(to_dev(torch_cuda, x), 2, B, 48000.0, d.Plugin.ir_test(0.7, 0.001),
+                             window=d.DSP_WIN_HANN, sample_offset=B * 3)
+    ref = oracle.render_offline([x[0], x[1]], 2, B, 48000.0, oracle.restated_plugin("IR_test", [0.7, 0.001]))
+    assert np.array_equal(out.cpu().numpy(), ref)
+    mref = oracle.np_stft_mag(ref[1], 8192, 4096, d.DSP_WIN_HANN, 4097)
+    assert peak_rel_err(mag.cpu().numpy()[1], mref) <= PEAK_REL_TOL
 
 
 @pytest.mark.gpu

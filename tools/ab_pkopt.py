@@ -14,6 +14,9 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "dsp-bench_amd"))
+# the A/B options live in the tools build only (make -C dsp-bench_amd ab)
+os.environ.setdefault("DSPBENCH_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)), "..",
+                                                   "dsp-bench_amd", "build", "ab", "libdspbench_ab.so"))
 import dspbench as d  # noqa: E402
 
 L_ = 48_000 * 3600
@@ -29,7 +32,7 @@ res = {o: [] for o in OPTS}
 ref = None
 for rnd in range(rounds):
     for o in OPTS:
-        lib.dsp_stft_soa_options(o << 4)
+        lib.dsp_stft_pk_ab_options(o)
         for _ in range(10):
             d.render_stft(x, 2, 512, 48000.0, d.Plugin.ir_test(), out=out, mag=mag)
         torch.cuda.synchronize()
@@ -51,7 +54,7 @@ for rnd in range(rounds):
         ms, n, b = C.c_double(), C.c_uint64(), C.c_uint64()
         lib.dsp_kernel_timing(C.byref(ms), C.byref(n), C.byref(b))
         res[o].append(ms.value / n.value)
-lib.dsp_stft_soa_options(0)
+lib.dsp_stft_pk_ab_options(0)
 byt = b.value / n.value
 for o, v in res.items():
     med = statistics.median(v)

@@ -18,6 +18,9 @@ import time
 import torch
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "dsp-bench_amd"))
+# the A/B options live in the tools build only (make -C dsp-bench_amd ab)
+os.environ.setdefault("DSPBENCH_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)), "..",
+                                                   "dsp-bench_amd", "build", "ab", "libdspbench_ab.so"))
 import dspbench as d  # noqa: E402
 
 FIR = sys.argv[1:2] == ["fir"]
@@ -54,7 +57,7 @@ def smi(samples):
 
 
 for o in ([0] if FIR else [int(a) for a in sys.argv[2:]] or [0] if MEM else [int(a) for a in sys.argv[1:]] or [0]):
-    lib.dsp_stft_soa_options(o << 4)
+    lib.dsp_stft_pk_ab_options(o)
     samples = []
     th = threading.Thread(target=smi, args=(samples,))
     t0 = time.time()
@@ -76,4 +79,4 @@ for o in ([0] if FIR else [int(a) for a in sys.argv[2:]] or [0] if MEM else [int
     pw = [m for s in samples for m in re.findall(r"Socket Graphics Package Power \(W\): ([\d.]+)", s)]
     print(f"opt {o:4d}: {n} launches, {statistics.median(ts[2:]):.4f} ms/launch settled, sclk {sclk} MHz, "
           f"power {pw} W", flush=True)
-lib.dsp_stft_soa_options(14)
+lib.dsp_stft_pk_ab_options(0)

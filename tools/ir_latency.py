@@ -50,15 +50,12 @@ for name, fn in (("python face", face), ("bare C call", bare)):
     ts = (time.perf_counter() - t) / n
     print(f"{name:12s}: back to back {tb * 1e6:7.2f} us/call, synchronised {ts * 1e6:7.2f} us/call", flush=True)
 
-# the one-frame STFT by kernel variant (dsp_stft_kernel_variant), bare call
-for v in (5, 0, 1, 2, 3, 4):
-    lib.dsp_stft_kernel_variant(v)
-    for _ in range(200):
-        bare()
-    torch.cuda.synchronize()
-    t = time.perf_counter()
-    for _ in range(n):
-        bare()
-    torch.cuda.synchronize()
-    print(f"variant {v}: back to back {(time.perf_counter() - t) / n * 1e6:7.2f} us/call", flush=True)
-lib.dsp_stft_kernel_variant(5)
+# the one-frame STFT, bare call
+for _ in range(200):
+    bare()
+torch.cuda.synchronize()
+t = time.perf_counter()
+for _ in range(n):
+    bare()
+torch.cuda.synchronize()
+print(f"one-frame STFT: back to back {(time.perf_counter() - t) / n * 1e6:7.2f} us/call", flush=True)
