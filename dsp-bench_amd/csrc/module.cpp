@@ -7,6 +7,7 @@
 //   the plugin source         (unchanged; its #include of plugin_header.h
 //                              hits the include guard)
 //   #pragma clang force_cuda_host_device end
+//   the descriptor            (dspb_desc_blob / dspb_desc_text, descriptor.cpp)
 //   kDriver                   (dspb_sizes / _defaults / _init / _render /
 //                              _callback kernels)
 // compiled with -ffp-contract=off so the plugin's float / double arithmetic
@@ -15,6 +16,7 @@
 #include <hip/hiprtc.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -23,6 +25,7 @@
 #include <string>
 #include <vector>
 
+#include "descriptor.hpp"
 #include "dspbench/module.h"
 #include "kernels.hpp"
 
@@ -342,7 +345,12 @@ struct ArenaHost {  // mirror of dspb_arena
 
 }  // namespace
 
+struct dsp_descriptor {
+    dspb::desc::Descriptor d;
+};
+
 struct dsp_module {
+    dsp_descriptor *desc = nullptr;  // from the code object (NULL for code without one)
     int device = -1;
     hipModule_t mod = nullptr;
     hipFunction_t f_sizes = nullptr, f_defaults = nullptr, f_init = nullptr, f_render = nullptr,
@@ -438,6 +446,8 @@ int dsp_module_compile(const char *source, const char *name, void **code, uint64
     tu += "#pragma clang force_cuda_host_device begin\n";
     tu += "#include \"dspb_plugin_source.cpp\"\n";
     tu += "#pragma clang force_cuda_host_device end\n";
+    std::string note;
+    tu += dspb::desc::generate(source, kPluginDeviceSrc, &note);
     tu += kDriver;
     const char *hdrs[2] = {kPluginDeviceSrc, source};
     const char *hnames[2] = {"plugin_header.h", "dspb_plugin_source.cpp"};
@@ -470,6 +480,26 @@ int dsp_module_compile(const char *source, const char *name, void **code, uint64
     }
     hiprtcGetCode(prog, (char *)buf);
     hiprtcDestroyProgram(&prog);
+    // the parameter descriptor, validated as the reference's JIT does
+    // (compiler.cpp:944-1164): an invalid annotation fails the compile
+    dspb::desc::Descriptor d;
+    std::string derr;
+    if (dspb::desc::read(buf, cs, &d, &derr) != 0) note += "descriptor: " + derr + "\n";
+    std::string bad;
+    for (const auto &p : d.params)
+        if (p.error != dspb::desc::kSuccess)
+            bad += "parameter '" + p.name + "' (annotate \"" + p.annotation + "\"): " +
+                   dspb::desc::error_name(p.error) + "\n";
+    if (log && log_cap) {
+        const std::string all = std::string(lg.data()) + note + bad;
+        std::strncpy(log, all.c_str(), log_cap - 1);
+        log[log_cap - 1] = 0;
+    }
+    if (!bad.empty()) {
+        std::free(buf);
+        set_last_error("plugin descriptor: %.400s", bad.c_str());
+        return DSP_ERR_INVALID;
+    }
     *code = buf;
     *code_size = cs;
     return DSP_OK;
@@ -488,6 +518,11 @@ int dsp_module_load(const void *code, uint64_t code_size, int device, dsp_module
     if (st) return st;
     dsp_module *m = new dsp_module();
     (void)hipGetDevice(&m->device);
+    {
+        dsp_descriptor *dd = new dsp_descriptor();
+        if (dspb::desc::read(code, code_size, &dd->d, nullptr) == 0) m->desc = dd;
+        else delete dd;
+    }
     auto fail = [&](int s) {
         dsp_module_destroy(m);
         if (prev >= 0) (void)hipSetDevice(prev);
@@ -535,6 +570,7 @@ void dsp_module_destroy(dsp_module *m) {
         if (m->mod) (void)hipModuleUnload(m->mod);
         if (prev >= 0 && prev != m->device) (void)hipSetDevice(prev);
     }
+    delete m->desc;
     delete m;
 }
 
@@ -574,6 +610,166 @@ int dsp_module_initialize_state(dsp_module *m, const void *params, uint32_t C, f
     m->initialized = (st == DSP_OK);
     if (prev >= 0 && prev != m->device) (void)hipSetDevice(prev);
     return st;
+}
+
+// ---- parameter descriptor (module.h) ----------------------------------------
+int dsp_descriptor_from_code(const void *code, uint64_t code_size, dsp_descriptor **out) {
+    if (!code || !code_size || !out) {
+        set_last_error("dsp_descriptor_from_code: NULL argument");
+        return DSP_ERR_INVALID;
+    }
+    *out = nullptr;
+    dsp_descriptor *d = new dsp_descriptor();
+    std::string err;
+    if (dspb::desc::read(code, code_size, &d->d, &err) != 0) {
+        delete d;
+        set_last_error("%s", err.c_str());
+        return DSP_ERR_INVALID;
+    }
+    *out = d;
+    return DSP_OK;
+}
+
+void dsp_descriptor_destroy(dsp_descriptor *d) { delete d; }
+
+const dsp_descriptor *dsp_module_descriptor(const dsp_module *m) { return m ? m->desc : nullptr; }
+
+int dsp_descriptor_info(const dsp_descriptor *d, dsp_plugin_descriptor *out) {
+    if (!d || !out) return DSP_ERR_INVALID;
+    out->params_size = d->d.params_size;
+    out->params_align = d->d.params_align;
+    out->state_size = d->d.state_size;
+    out->state_align = d->d.state_align;
+    out->num_parameters = (uint32_t)d->d.params.size();
+    out->error = d->d.error;
+    return DSP_OK;
+}
+
+int dsp_descriptor_param(const dsp_descriptor *d, uint32_t i, dsp_param_desc *out) {
+    if (!d || !out || i >= d->d.params.size()) return DSP_ERR_INVALID;
+    const dspb::desc::Param &p = d->d.params[i];
+    std::memset(out, 0, sizeof *out);
+    std::strncpy(out->name, p.name.c_str(), DSP_PARAM_NAME_MAX - 1);
+    out->offset = p.offset;
+    out->type = p.type;
+    out->error = p.error;
+    out->int_min = p.int_min;
+    out->int_max = p.int_max;
+    out->float_min = p.float_min;
+    out->float_max = p.float_max;
+    out->float_log = p.float_log ? 1 : 0;
+    out->num_entries = (uint32_t)p.entries.size();
+    return DSP_OK;
+}
+
+int dsp_descriptor_enum_entry(const dsp_descriptor *d, uint32_t i, uint32_t e, int64_t *value, char *name,
+                              uint32_t name_cap) {
+    if (!d || i >= d->d.params.size() || e >= d->d.params[i].entries.size()) return DSP_ERR_INVALID;
+    const dspb::desc::Entry &en = d->d.params[i].entries[e];
+    if (value) *value = en.value;
+    if (name && name_cap) {
+        std::strncpy(name, en.name.c_str(), name_cap - 1);
+        name[name_cap - 1] = 0;
+    }
+    return DSP_OK;
+}
+
+int dsp_params_from_values(const dsp_descriptor *d, const dsp_param_value *values, void *holder) {
+    if (!d || (!d->d.params.empty() && (!values || !holder))) return DSP_ERR_INVALID;
+    char *h = (char *)holder;
+    for (size_t i = 0; i < d->d.params.size(); ++i) {
+        const dspb::desc::Param &p = d->d.params[i];
+        if (p.offset + 4ull > d->d.params_size) return DSP_ERR_INVALID;
+        switch (p.type) {  // plugin.cpp:155-168: every kind is a 4-byte store
+        case dspb::desc::kInt: std::memcpy(h + p.offset, &values[i].int_value, 4); break;
+        case dspb::desc::kFloat: std::memcpy(h + p.offset, &values[i].float_value, 4); break;
+        default: std::memcpy(h + p.offset, &values[i].enum_value, 4); break;
+        }
+    }
+    return DSP_OK;
+}
+
+int dsp_params_to_values(const dsp_descriptor *d, const void *holder, dsp_param_value *values) {
+    if (!d || (!d->d.params.empty() && (!values || !holder))) return DSP_ERR_INVALID;
+    const char *h = (const char *)holder;
+    for (size_t i = 0; i < d->d.params.size(); ++i) {
+        const dspb::desc::Param &p = d->d.params[i];
+        if (p.offset + 4ull > d->d.params_size) return DSP_ERR_INVALID;
+        std::memcpy(&values[i], h + p.offset, 4);  // plugin.cpp:129-142
+    }
+    return DSP_OK;
+}
+
+int dsp_descriptor_equal(const dsp_descriptor *a, const dsp_descriptor *b) {
+    if (!a || !b) return 0;
+    const dspb::desc::Descriptor &x = a->d, &y = b->d;
+    if (x.params_size != y.params_size || x.params_align != y.params_align || x.state_size != y.state_size ||
+        x.state_align != y.state_align || x.params.size() != y.params.size())
+        return 0;
+    for (size_t i = 0; i < x.params.size(); ++i) {
+        const dspb::desc::Param &p = x.params[i], &q = y.params[i];
+        // (the reference compares a's name with itself, plugin.cpp:74; the
+        // names are compared here)
+        if (p.offset != q.offset || p.type != q.type || p.name != q.name) return 0;
+        if (p.type == dspb::desc::kInt && (p.int_min != q.int_min || p.int_max != q.int_max)) return 0;
+        if (p.type == dspb::desc::kFloat && (p.float_min != q.float_min || p.float_max != q.float_max)) return 0;
+        if (p.type == dspb::desc::kEnum) {
+            if (p.entries.size() != q.entries.size()) return 0;
+            for (size_t e = 0; e < p.entries.size(); ++e)
+                if (p.entries[e].value != q.entries[e].value || p.entries[e].name != q.entries[e].name) return 0;
+        }
+    }
+    return 1;
+}
+
+// plugin.h:173-233, in fp32 as the reference computes them (real32
+// arguments: the float overloads of log / exp)
+int dsp_param_normalize(const dsp_param_desc *p, const int64_t *enum_values, dsp_param_value v, float *out) {
+    if (!p || !out) return DSP_ERR_INVALID;
+    switch (p->type) {
+    case DSP_PARAM_INT:  // normalize_parameter_int_value
+        *out = (float)((float)v.int_value - (float)p->int_min) / (float)(p->int_max - p->int_min);
+        return DSP_OK;
+    case DSP_PARAM_FLOAT: {  // normalize_parameter_float_value
+        float x = v.float_value;
+        x = x < p->float_min ? p->float_min : (x > p->float_max ? p->float_max : x);
+        if (x == p->float_min) *out = 0.0f;
+        else if (p->float_log) *out = std::log(x / p->float_min) / std::log(p->float_max / p->float_min);
+        else *out = (x - p->float_min) / (p->float_max - p->float_min);
+        return DSP_OK;
+    }
+    case DSP_PARAM_ENUM: {  // enum_value_to_index + normalize_parameter_enum_index
+        if (!enum_values || p->num_entries == 0) return DSP_ERR_INVALID;
+        uint32_t idx = 0;
+        for (; idx < p->num_entries && enum_values[idx] != (int64_t)v.enum_value; ++idx) {
+        }
+        if (idx == p->num_entries) return DSP_ERR_INVALID;
+        *out = p->num_entries == 1 ? 0.0f : (float)idx / (float)(p->num_entries - 1);
+        return DSP_OK;
+    }
+    default: return DSP_ERR_INVALID;
+    }
+}
+
+int dsp_param_denormalize(const dsp_param_desc *p, const int64_t *enum_values, float x, dsp_param_value *out) {
+    if (!p || !out) return DSP_ERR_INVALID;
+    switch (p->type) {
+    case DSP_PARAM_INT:  // denormalize_int_value
+        out->int_value = (int32_t)(x * (float)(p->int_max - p->int_min) + (float)p->int_min);
+        return DSP_OK;
+    case DSP_PARAM_FLOAT:  // denormalize_float_value
+        out->float_value = p->float_log ? p->float_min * std::exp(x * std::log(p->float_max / p->float_min))
+                                        : x * (p->float_max - p->float_min) + p->float_min;
+        return DSP_OK;
+    case DSP_PARAM_ENUM: {  // denormalize_enum_index + enum_index_to_value
+        if (!enum_values || p->num_entries == 0) return DSP_ERR_INVALID;
+        const uint32_t idx = (uint32_t)(x * (float)(p->num_entries - 1));
+        if (idx >= p->num_entries) return DSP_ERR_INVALID;
+        out->enum_value = (int32_t)enum_values[idx];
+        return DSP_OK;
+    }
+    default: return DSP_ERR_INVALID;
+    }
 }
 
 int dsp_module_read_state(const dsp_module *m, void *state) {

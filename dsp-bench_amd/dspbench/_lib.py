@@ -64,6 +64,26 @@ class dsp_wav_info(C.Structure):
 FPP = C.POINTER(C.POINTER(C.c_float))
 FP = C.POINTER(C.c_float)
 
+DSP_PARAM_INT, DSP_PARAM_FLOAT, DSP_PARAM_ENUM = 0, 1, 2
+DSP_PARAM_NAME_MAX = 64
+
+
+class dsp_param_desc(C.Structure):
+    _fields_ = [("name", C.c_char * DSP_PARAM_NAME_MAX), ("offset", C.c_uint32), ("type", C.c_int32),
+                ("error", C.c_int32), ("int_min", C.c_int32), ("int_max", C.c_int32),
+                ("float_min", C.c_float), ("float_max", C.c_float), ("float_log", C.c_int32),
+                ("num_entries", C.c_uint32)]
+
+
+class dsp_plugin_descriptor(C.Structure):
+    _fields_ = [("params_size", C.c_uint64), ("params_align", C.c_uint64), ("state_size", C.c_uint64),
+                ("state_align", C.c_uint64), ("num_parameters", C.c_uint32), ("error", C.c_int32)]
+
+
+class dsp_param_value(C.Union):
+    _fields_ = [("int_value", C.c_int32), ("float_value", C.c_float), ("enum_value", C.c_int32)]
+
+
 # name -> (restype, argtypes)
 _SIGS = {
     "dsp_abi_version": (C.c_int, []),
@@ -107,6 +127,20 @@ _SIGS = {
     "dsp_module_default_parameters": (C.c_int, [C.c_void_p, C.c_void_p]),
     "dsp_module_initialize_state": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_float, C.c_uint64]),
     "dsp_module_read_state": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "dsp_descriptor_from_code": (C.c_int, [C.c_void_p, C.c_uint64, C.POINTER(C.c_void_p)]),
+    "dsp_descriptor_destroy": (None, [C.c_void_p]),
+    "dsp_module_descriptor": (C.c_void_p, [C.c_void_p]),
+    "dsp_descriptor_info": (C.c_int, [C.c_void_p, C.POINTER(dsp_plugin_descriptor)]),
+    "dsp_descriptor_param": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(dsp_param_desc)]),
+    "dsp_descriptor_enum_entry": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.POINTER(C.c_int64),
+                                            C.c_char_p, C.c_uint32]),
+    "dsp_params_from_values": (C.c_int, [C.c_void_p, C.POINTER(dsp_param_value), C.c_void_p]),
+    "dsp_params_to_values": (C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(dsp_param_value)]),
+    "dsp_descriptor_equal": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "dsp_param_normalize": (C.c_int, [C.POINTER(dsp_param_desc), C.POINTER(C.c_int64), dsp_param_value,
+                                      C.POINTER(C.c_float)]),
+    "dsp_param_denormalize": (C.c_int, [C.POINTER(dsp_param_desc), C.POINTER(C.c_int64), C.c_float,
+                                        C.POINTER(dsp_param_value)]),
     "dsp_wav_parse": (C.c_int, [C.c_void_p, C.c_uint64, C.POINTER(dsp_wav_info)]),
     "dsp_wav_decode": (C.c_int, [C.c_void_p, C.POINTER(dsp_wav_info), C.c_uint64, C.c_uint64, FPP,
                                  C.POINTER(dsp_exec)]),

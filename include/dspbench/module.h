@@ -67,6 +67,92 @@ int dsp_module_initialize_state(dsp_module *m, const void *params, uint32_t C, f
  * are device addresses). */
 int dsp_module_read_state(const dsp_module *m, void *state);
 
+/* ---- parameter descriptor -------------------------------------
+ * The reference's JIT parses the `annotate` attributes of struct Parameters
+ * into a Plugin_Descriptor (compiler.cpp:944-1164; plugin.h:15-82) and
+ * marshals parameter values into the Parameters blob at the fields' byte
+ * offsets (plugin_set_parameter_holder_from_values, plugin.cpp:147-171).
+ * dsp_module_compile builds the same descriptor -- names and annotations from
+ * the source text, offsets / sizes / types / enumerator values evaluated by
+ * the device compiler -- stores it in the code object, and fails (with the
+ * reference's error flag in the log) when an annotation is invalid.
+ * Reading it needs no GPU. */
+enum dsp_param_type { DSP_PARAM_INT = 0, DSP_PARAM_FLOAT = 1, DSP_PARAM_ENUM = 2 }; /* plugin.h:15-19 */
+
+enum dsp_desc_error { /* errors.inc:1-19 */
+    DSP_DESC_SUCCESS = 0,               /* Compiler_Success */
+    DSP_DESC_ERROR_RECURSE = 1,         /* Compiler_Error_Recurse: some parameter has an error */
+    DSP_DESC_EMPTY_ANNOTATION = 2,      /* Compiler_Empty_Annotation */
+    DSP_DESC_INVALID_ANNOTATION = 3,    /* Compiler_Invalid_Annotation */
+    DSP_DESC_MISSING_MIN_MAX = 4,       /* Compiler_Missing_Min_Max */
+    DSP_DESC_MIN_GREATER_THAN_MAX = 5,  /* Compiler_Min_Greater_Than_Max */
+    DSP_DESC_INVALID_MIN = 6,           /* Compiler_Invalid_Min_Value */
+    DSP_DESC_INVALID_MAX = 7,           /* Compiler_Invalid_Max_Value */
+    DSP_DESC_TYPE_MISMATCH = 8          /* Compiler_Annotation_Type_Mismatch */
+};
+
+#define DSP_PARAM_NAME_MAX 64
+
+typedef struct dsp_param_desc { /* Plugin_Descriptor_Parameter (plugin.h:47-55) */
+    char name[DSP_PARAM_NAME_MAX]; /* field name, NUL-terminated (truncated) */
+    uint32_t offset;               /* byte offset in the Parameters blob */
+    int32_t type;                  /* dsp_param_type */
+    int32_t error;                 /* dsp_desc_error */
+    int32_t int_min, int_max;      /* Int */
+    float float_min, float_max;    /* Float */
+    int32_t float_log;             /* Float: "log" annotation */
+    uint32_t num_entries;          /* Enum: enumerators (dsp_descriptor_enum_entry) */
+} dsp_param_desc;
+
+typedef struct dsp_plugin_descriptor { /* Plugin_Descriptor (plugin.h:57-74) */
+    uint64_t params_size, params_align;
+    uint64_t state_size, state_align;
+    uint32_t num_parameters; /* annotated fields of Parameters, in declaration order */
+    int32_t error;           /* dsp_desc_error */
+} dsp_plugin_descriptor;
+
+typedef union dsp_param_value { /* Plugin_Parameter_Value (plugin.h:76-82) */
+    int32_t int_value;
+    float float_value;
+    int32_t enum_value;
+} dsp_param_value;
+
+typedef struct dsp_descriptor dsp_descriptor;
+
+/* The descriptor stored in a code object (no GPU).  Free with
+ * dsp_descriptor_destroy.  DSP_ERR_INVALID when the code object has none. */
+int dsp_descriptor_from_code(const void *code, uint64_t code_size, dsp_descriptor **out);
+void dsp_descriptor_destroy(dsp_descriptor *d);
+/* The descriptor of a loaded module (owned by the module), or NULL. */
+const dsp_descriptor *dsp_module_descriptor(const dsp_module *m);
+
+int dsp_descriptor_info(const dsp_descriptor *d, dsp_plugin_descriptor *out);
+int dsp_descriptor_param(const dsp_descriptor *d, uint32_t index, dsp_param_desc *out);
+/* Enum parameter `index`, enumerator `entry`: value and name (NUL-terminated,
+ * truncated to name_cap; name may be NULL). */
+int dsp_descriptor_enum_entry(const dsp_descriptor *d, uint32_t index, uint32_t entry, int64_t *value,
+                              char *name, uint32_t name_cap);
+
+/* values[i] -> the holder at parameter i's offset: int / float / enum as a
+ * 4-byte int (plugin_set_parameter_holder_from_values, plugin.cpp:147-171).
+ * Bytes of the holder that are no parameter are left as they are. */
+int dsp_params_from_values(const dsp_descriptor *d, const dsp_param_value *values, void *holder);
+/* the reverse (plugin_set_parameter_values_from_holder, plugin.cpp:121-145) */
+int dsp_params_to_values(const dsp_descriptor *d, const void *holder, dsp_param_value *values);
+/* 1 when two descriptors describe the same layout and parameters
+ * (plugin_descriptor_compare, plugin.cpp:66-105: sizes, alignments, and per
+ * parameter offset, type, name, ranges, enumerators), else 0. */
+int dsp_descriptor_equal(const dsp_descriptor *a, const dsp_descriptor *b);
+
+/* Normalisation (plugin.h:173-233) of one parameter's value to [0, 1] and
+ * back.  Int: (v - min) / (max - min); Float: clamped, linear or log;
+ * Enum: the index of the enumerator whose value is v over num_entries - 1
+ * (enum_values = the parameter's enumerator values in declaration order).
+ * dsp_param_normalize returns DSP_ERR_INVALID for an enum value that is no
+ * enumerator (the reference asserts, plugin.h:222-231). */
+int dsp_param_normalize(const dsp_param_desc *p, const int64_t *enum_values, dsp_param_value v, float *out);
+int dsp_param_denormalize(const dsp_param_desc *p, const int64_t *enum_values, float x, dsp_param_value *out);
+
 /* Render with a loaded module: dsp_render_offline / dsp_render_stft /
  * dsp_ir_analysis with plugin->kind = DSP_PLUGIN_GENERIC and plugin->module
  * = the module (plugin->params = the Parameters blob).  dsp_ir_analysis
