@@ -752,6 +752,74 @@ int dsp_render_offline(const float *const *in, uint32_t in_channels, uint64_t L,
     return finish(ex);
 }
 
+int dsp_render_loop(const float *const *in, uint32_t in_channels, uint64_t L, uint64_t cursor,
+                    float *const *out, uint32_t C, uint32_t B, uint64_t nblocks, float sr,
+                    const dsp_plugin *plugin, uint64_t *cursor_out, const dsp_exec *ex) {
+    if (B == 0) return invalid("block size B must be > 0");
+    if (in_channels && L == 0) return invalid("loop mode over an empty file (the reference spins forever, audio.cpp:104)");
+    if (in_channels && cursor >= L) return invalid("cursor %llu past the file (L = %llu)", (unsigned long long)cursor,
+                                                   (unsigned long long)L);
+    if (cursor_out) *cursor_out = in_channels ? (uint64_t)((cursor + (unsigned __int128)nblocks * B) % L) : cursor;
+    if (C == 0 || nblocks == 0) return DSP_OK;
+    if (!out) return invalid("out is NULL");
+    for (uint32_t c = 0; c < C; ++c)
+        if (!out[c]) return invalid("out[%u] is NULL", c);
+    if (in_channels && !in) return invalid("in is NULL");
+    for (uint32_t c = 0; c < in_channels; ++c)
+        if (!in[c]) return invalid("in[%u] is NULL", c);
+    if (host_mode(ex)) return invalid("dsp_render_loop: device buffers only");
+    if (ex && ex->sample_offset % B) return invalid("sample_offset must be a multiple of B");
+    DeviceGuard g(ex);
+    if (g.status) return g.status;
+    hipStream_t s = stream_of(ex);
+    const uint64_t Lr = nblocks * B;
+    SampleMap map;
+    int st = plugin_map(plugin, B, g.dev, s, &map, sr);
+    if (st) return st;
+    if ((st = ensure_ramp_table(map, s))) return st;
+    const uint32_t in_ch = std::min(in_channels, C);  // channels_to_write (audio.cpp:66)
+    auto wrap = [&](const float *const *src, float *const *dst, uint32_t nc, const SampleMap &m) -> int {
+        for (uint32_t c0 = 0; c0 < nc; c0 += kMaxChannels) {
+            const uint32_t cn = (nc - c0) < (uint32_t)kMaxChannels ? (nc - c0) : kMaxChannels;
+            RenderArgs A{};
+            for (uint32_t j = 0; j < cn; ++j) {
+                A.out.p[j] = dst[c0 + j];
+                if (c0 + j < in_ch) {
+                    A.in.p[j] = src[c0 + j];
+                    A.in_ch = j + 1;
+                }
+            }
+            A.L = L;
+            A.start = 0;
+            A.end = Lr;
+            A.map = m;
+            A.goff = goff_of(ex);
+            if (int e = launch_render_wrap(A, cn, cursor, s)) return e;
+        }
+        return DSP_OK;
+    };
+    if (map.kind == MapKind::Noop || map.kind == MapKind::Gain || map.kind == MapKind::Ramp)
+        return (st = wrap(in, out, C, map)) ? st : finish(ex);
+    // FIR / GENERIC: the wrapped file is materialised (the plugin's block
+    // stream), then rendered as a one-shot file of nblocks B samples
+    float *tmp = nullptr;
+    if (in_ch) {
+        DSPB_HIP(hipMallocAsync((void **)&tmp, sizeof(float) * Lr * in_ch, s));
+        std::vector<float *> rows(in_ch);
+        for (uint32_t c = 0; c < in_ch; ++c) rows[c] = tmp + (uint64_t)c * Lr;
+        SampleMap id{};
+        id.kind = MapKind::Noop;
+        id.B = B;
+        if ((st = wrap(in, rows.data(), in_ch, id))) return st;
+        std::vector<const float *> crow(rows.begin(), rows.end());
+        st = render_device(crow.data(), in_ch, Lr, out, C, B, map, 0, goff_of(ex), s);
+    } else {
+        st = render_device(nullptr, 0, Lr, out, C, B, map, 0, goff_of(ex), s);
+    }
+    if (tmp) (void)hipFreeAsync(tmp, s);
+    return st ? st : finish(ex);
+}
+
 int dsp_stft_magnitude(const float *const *in, uint32_t C, uint64_t L, uint32_t N, uint32_t H,
                        int32_t window, uint32_t K, float *const *mag, uint64_t ld,
                        const dsp_exec *ex) {

@@ -127,7 +127,9 @@ __global__ __launch_bounds__(256) void magnitude_kernel(const float *re, const f
                                                         float *out, uint64_t n) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
          i += (uint64_t)gridDim.x * blockDim.x)
-        out[i] = __builtin_sqrtf(re[i] * re[i] + im[i] * im[i]);
+        // ippsMagnitude_32f (dsp.cpp:166-168) restated without contraction:
+        // two rounded products, a rounded sum, a correctly rounded root
+        out[i] = __builtin_sqrtf(__fadd_rn(__fmul_rn(re[i], re[i]), __fmul_rn(im[i], im[i])));
 }
 
 static uint32_t stream_grid(uint64_t work_items) {
@@ -135,6 +137,48 @@ static uint32_t stream_grid(uint64_t work_items) {
     uint64_t g = (work_items + 255) / 256;
     if (g > 2048) g = 2048;
     return g ? (uint32_t)g : 1u;
+}
+
+// Loop mode (audio.cpp:100-132): the file wraps, so output sample i of the
+// render reads file sample (cursor + i) mod L.  One float per lane and step,
+// the index advanced incrementally (one 64-bit modulo per thread): lanes
+// stay consecutive, so loads coalesce except at the wrap point.
+template <MapKind K>
+__global__ __launch_bounds__(256) void render_wrap_kernel(RenderArgs A, uint64_t cursor) {
+    const uint32_t c = blockIdx.y;
+    const float *x = (c < A.in_ch) ? A.in.p[c] : nullptr;
+    float *o = A.out.p[c];
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t i0 = A.start + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i0 >= A.end) return;
+    const uint64_t L = A.L;
+    uint64_t j = (K == MapKind::Ramp || x == nullptr) ? 0 : (cursor + i0) % L;
+    const uint64_t dj = (K == MapKind::Ramp || x == nullptr) ? 0 : stride % L;
+    SampleMap m = A.map;
+    m.kind = K;
+    for (uint64_t i = i0; i < A.end; i += stride) {
+        const float b = (K != MapKind::Ramp && x != nullptr) ? x[j] : 0.f;
+        o[i] = apply_map(m, b, A.goff + i);
+        j += dj;
+        if (j >= L) j -= L;
+    }
+}
+
+int launch_render_wrap(const RenderArgs &A, uint32_t C, uint64_t cursor, hipStream_t s) {
+    if (A.end <= A.start || C == 0) return DSP_OK;
+    if (A.in_ch && (A.L == 0 || cursor >= A.L)) return DSP_ERR_INVALID;
+    uint32_t gx = stream_grid(A.end - A.start);
+    gx = (gx + C - 1) / C;
+    if (gx == 0) gx = 1;
+    dim3 grid(gx, C), block(256);
+    switch (A.map.kind) {
+    case MapKind::Noop: hipLaunchKernelGGL(render_wrap_kernel<MapKind::Noop>, grid, block, 0, s, A, cursor); break;
+    case MapKind::Gain: hipLaunchKernelGGL(render_wrap_kernel<MapKind::Gain>, grid, block, 0, s, A, cursor); break;
+    case MapKind::Ramp: hipLaunchKernelGGL(render_wrap_kernel<MapKind::Ramp>, grid, block, 0, s, A, cursor); break;
+    default: return DSP_ERR_INVALID;
+    }
+    DSPB_HIP(hipGetLastError());
+    return DSP_OK;
 }
 
 int launch_ramp_table(float *table, uint32_t B, float gain, float step, hipStream_t s) {

@@ -93,6 +93,9 @@ _SIGS = {
     "dsp_stft_frame_count": (C.c_uint64, [C.c_uint64, C.c_uint32, C.c_uint32]),
     "dsp_render_offline": (C.c_int, [FPP, C.c_uint32, C.c_uint64, FPP, C.c_uint32, C.c_uint32,
                                      C.c_float, C.POINTER(dsp_plugin), C.POINTER(dsp_exec)]),
+    "dsp_render_loop": (C.c_int, [FPP, C.c_uint32, C.c_uint64, C.c_uint64, FPP, C.c_uint32, C.c_uint32,
+                                  C.c_uint64, C.c_float, C.POINTER(dsp_plugin), C.POINTER(C.c_uint64),
+                                  C.POINTER(dsp_exec)]),
     "dsp_stft_magnitude": (C.c_int, [FPP, C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint32,
                                      C.c_int32, C.c_uint32, FPP, C.c_uint64, C.POINTER(dsp_exec)]),
     "dsp_render_stft": (C.c_int, [FPP, C.c_uint32, C.c_uint64, FPP, C.c_uint32, C.c_uint32,

@@ -12,6 +12,7 @@ Interface mirror (reference odecaux/DSP-Bench):
       (build/gain_test.cpp:14-16, build/IR_test.cpp:14-17,
       test/static_gain_plugin.cpp:7-9)
   render_offline   render_audio pumped block by block (audio.cpp:13-175)
+  render_loop      the same with the file looping (audio.cpp:100-132)
   stft_magnitude   windowing -> fft_forward -> pythagore_array per frame
   render_stft      both, fused
   ir_analysis      compute_IR + fft_perform_and_get_magnitude
@@ -138,6 +139,25 @@ def render_offline(file, C_out: int, B: int, sr: float, plugin: Plugin | None,
                                     C.byref(ps) if ps is not None else None, C.byref(ex))
     check(st, "dsp_render_offline")
     return out[:, : nb * B]
+
+
+def render_loop(file, C_out: int, B: int, nblocks: int, sr: float, plugin: Plugin | None,
+                cursor: int = 0, out=None, sample_offset: int = 0, stream=None):
+    """Loop-mode render (audio.cpp:100-132): the file wraps from `cursor`.
+    Device tensors only.  Returns (out [C_out, nblocks*B], next cursor)."""
+    in_ptrs, ref = _rows(file)
+    L_ = file.shape[1] if file is not None else 0
+    if out is None:
+        out = _alloc_like(ref, (C_out, max(nblocks * B, 1)))
+    out_ptrs, oref = _rows(out)
+    ex = _exec(oref, sample_offset, stream)
+    ps = plugin.as_struct() if plugin is not None else None
+    cur = C.c_uint64()
+    st = L.lib().dsp_render_loop(chan_table(in_ptrs) if in_ptrs else None, len(in_ptrs), L_, cursor,
+                                 chan_table(out_ptrs), C_out, B, nblocks, sr,
+                                 C.byref(ps) if ps is not None else None, C.byref(cur), C.byref(ex))
+    check(st, "dsp_render_loop")
+    return out[:, : nblocks * B], cur.value
 
 
 def stft_magnitude(x, N: int = 8192, H: int = 4096, window: int = L.DSP_WIN_HANN,

@@ -106,6 +106,18 @@ int dsp_render_offline(const float *const *in, uint32_t in_channels, uint64_t L,
                        float *const *out, uint32_t C, uint32_t B, float sr,
                        const dsp_plugin *plugin, const dsp_exec *ex);
 
+/* Offline render, loop mode (render_audio with audio_file_loop set,
+ * audio.cpp:100-132): the file wraps -- block b, sample s reads file sample
+ * (cursor + b B + s) mod L for c < min(in_channels, C); other channels are
+ * zero (audio.cpp:138-141); then audio_callback in place.  Renders nblocks
+ * blocks into out[c] (nblocks B floats) and returns the next read cursor,
+ * (cursor + nblocks B) mod L, in *cursor_out (may be NULL).  L == 0 with a
+ * file is DSP_ERR_INVALID (the reference spins forever, audio.cpp:104).
+ * Device buffers only. */
+int dsp_render_loop(const float *const *in, uint32_t in_channels, uint64_t L, uint64_t cursor,
+                    float *const *out, uint32_t C, uint32_t B, uint64_t nblocks, float sr,
+                    const dsp_plugin *plugin, uint64_t *cursor_out, const dsp_exec *ex);
+
 /* STFT magnitude over C planar channels of L samples:
  *   F = dsp_stft_frame_count(L, N, H); mag[c][f * ld + k] = |X_f[k]| / sqrt(N)
  *   for k < K, X_f = DFT_N(w * in[c][f*H .. f*H + N)).

@@ -233,3 +233,19 @@ def test_library_has_no_unresolved_internal_symbols():
     bad = [l for l in out.splitlines() if "dspb" in l or " dsp_" in l]
     assert not bad, bad
     C.CDLL(_lib.LIB_PATH, mode=os.RTLD_NOW)
+
+
+def test_render_loop_rejects_empty_file_and_bad_cursor():
+    """Loop mode over an empty file would spin forever in the reference
+    (audio.cpp:104); here it is refused before any device use, as is a cursor
+    past the file."""
+    L = d.lib()
+    x = np.zeros((1, 100), np.float32)
+    rows = _lib.chan_table([x[0].ctypes.data])
+    ex = _lib.dsp_exec(-1, 0, None, 0)
+    cur = C.c_uint64()
+    assert L.dsp_render_loop(rows, 1, 0, 0, rows, 1, 64, 4, 48000.0, None, C.byref(cur), C.byref(ex)) == -1
+    assert L.dsp_render_loop(rows, 1, 100, 100, rows, 1, 64, 4, 48000.0, None, C.byref(cur), C.byref(ex)) == -1
+    # the next cursor is computed before anything runs
+    L.dsp_render_loop(rows, 1, 100, 30, rows, 1, 64, 0, 48000.0, None, C.byref(cur), C.byref(ex))
+    assert cur.value == 30

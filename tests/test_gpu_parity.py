@@ -285,3 +285,100 @@ def test_ir_ramp_closed_form_and_table(torch_cuda, oracle, gain, step, B):
     assert peak_rel_err(mag.cpu().numpy()[1], mref) <= PEAK_REL_TOL
     out2 = d.render_offline(to_dev(torch_cuda, x), 2, B, 48000.0, plug)
     assert np.array_equal(out2.cpu().numpy(), ref)
+
+
+# ---- device elementwise services (dsp.cpp:166-181, 208-210) ---------------
+
+def test_elementwise_services_bit_exact(torch_cuda):
+    """dsp_gain / dsp_copy / dsp_set / dsp_magnitude through the C ABI, bit for
+    bit against float32 numpy (gain_32_array = MulC, copy_array, set_array,
+    pythagore_array = sqrt(re^2 + im^2) with rounded products and sum)."""
+    import ctypes as C
+    torch = torch_cuda
+    L = d.lib()
+    n = 1_000_003
+    rng = np.random.default_rng(41)
+    a = rng.uniform(-3, 3, n).astype(np.float32)
+    b = rng.uniform(-3, 3, n).astype(np.float32)
+    ga, gb = to_dev(torch, a), to_dev(torch, b)
+    out = torch.empty(n, device="cuda")
+    ex = d._lib.dsp_exec(torch.cuda.current_device(), d._lib.DSP_EXEC_SYNC,
+                         C.c_void_p(torch.cuda.current_stream().cuda_stream), 0)
+    fp = lambda t: C.cast(C.c_void_p(t.data_ptr()), d._lib.FP)  # noqa: E731
+    assert L.dsp_gain(fp(ga), fp(out), 0.37, n, C.byref(ex)) == 0
+    assert np.array_equal(out.cpu().numpy(), a * np.float32(0.37))
+    assert L.dsp_copy(fp(gb), fp(out), n, C.byref(ex)) == 0
+    assert np.array_equal(out.cpu().numpy(), b)
+    assert L.dsp_set(-2.5, fp(out), n, C.byref(ex)) == 0
+    assert np.array_equal(out.cpu().numpy(), np.full(n, -2.5, np.float32))
+    assert L.dsp_magnitude(fp(ga), fp(gb), fp(out), n, C.byref(ex)) == 0
+    want = np.sqrt((a * a) + (b * b)).astype(np.float32)
+    assert np.array_equal(out.cpu().numpy(), want)
+    # in place (gain_ip_32_array) and n = 0
+    assert L.dsp_gain(fp(ga), fp(ga), 2.0, n, C.byref(ex)) == 0
+    assert np.array_equal(ga.cpu().numpy(), a * np.float32(2.0))
+    assert L.dsp_set(1.0, fp(out), 0, C.byref(ex)) == 0
+
+
+def test_full_size_cfg4_stft_1h_96k_from_hbm(torch_cuda, oracle):
+    """BASELINE cfg 4 at full size: the Hann 8192 / 4096 STFT of 1 h of 96 kHz
+    stereo (2 x 345.6 M samples) from HBM.  Frame count, and sampled frames
+    (first, last, and 12 seeded ones per channel) against float64."""
+    torch = torch_cuda
+    L_ = 96_000 * 3600
+    g = torch.Generator(device="cuda").manual_seed(4)
+    x = torch.rand((2, L_), device="cuda", generator=g) * 0.2 - 0.1
+    mag = d.stft_magnitude(x, N=8192, H=4096, window=d.DSP_WIN_HANN, K=4097)
+    F = mag.shape[1]
+    assert F == (L_ - 8192) // 4096 + 1 == 84_374
+    rng = np.random.default_rng(5)
+    for c in range(2):
+        for f in [0, F - 1] + list(rng.integers(0, F, 12)):
+            seg = x[c, f * 4096:f * 4096 + 8192].cpu().numpy()
+            ref = oracle.np_stft_mag(seg, 8192, 4096, d.DSP_WIN_HANN, 4097)[0]
+            assert peak_rel_err(mag[c, f].cpu().numpy(), ref) <= PEAK_REL_TOL, (c, f)
+
+
+# ---- loop mode (audio.cpp:100-132) ------------------------------------------
+
+@pytest.mark.parametrize("pname", list(PLUGINS))
+@pytest.mark.parametrize("cin,cout,L,B,nblocks,cursor", [
+    (2, 2, 10_007, 512, 60, 0),      # several wraps, ragged file
+    (1, 2, 300, 512, 9, 123),        # file shorter than a block: wraps inside every block
+    (2, 1, 4096, 4096, 5, 4095),     # cursor at the last sample
+    (3, 2, 50_000, 384, 200, 49_000),
+])
+def test_render_loop_bit_exact(torch_cuda, oracle, pname, cin, cout, L, B, nblocks, cursor):
+    x = rnd((cin, L), 71)
+    ref, ref_cur = oracle.render_loop([x[c] for c in range(cin)], cout, B, nblocks, 48000.0,
+                                      oracle_plugin(oracle, pname), cursor=cursor)
+    got, cur = d.render_loop(to_dev(torch_cuda, x), cout, B, nblocks, 48000.0, PLUGINS[pname][0](), cursor=cursor)
+    assert cur == ref_cur == (cursor + nblocks * B) % L
+    assert np.array_equal(got.cpu().numpy(), ref)
+
+
+def test_render_loop_generic_and_fir(torch_cuda, oracle):
+    """Non-map plugins loop over the materialised wrapped stream: the
+    reference's gain_test compiled by the module compiler (bit-exact) and the
+    cfg 3b FIR (the whole wrapped stream convolved, 2e-6 of the peak)."""
+    import os
+    torch = torch_cuda
+    L, B, nb, cursor = 7_777, 512, 40, 5_000
+    x = rnd((2, L), 72)
+    co = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle", "_ref",
+                      "mod_gain_test.co")
+    if os.path.exists(co):
+        mod = d.module.Module(open(co, "rb").read())
+        mod.initialize_state(mod.default_parameters(), 2, 48000.0)
+        got, _ = d.render_loop(to_dev(torch, x), 2, B, nb, 48000.0, mod.plugin_from_values({"gain": 0.45}),
+                               cursor=cursor)
+        ref, _ = oracle.render_loop([x[0], x[1]], 2, B, nb, 48000.0, oracle.restated_plugin("gain_test", [0.45]),
+                                    cursor=cursor)
+        assert np.array_equal(got.cpu().numpy(), ref)
+    taps = rnd((1, 300), 73)[0] * 0.05
+    got, _ = d.render_loop(to_dev(torch, x), 2, B, nb, 48000.0, d.Plugin.fir(taps), cursor=cursor)
+    idx = (cursor + np.arange(nb * B)) % L
+    for c in range(2):
+        want = oracle.fir_f64(x[c][idx], taps)
+        g = got[c].cpu().numpy().astype(np.float64)
+        assert np.max(np.abs(g - want[: nb * B])) <= 2e-6 * np.max(np.abs(want))
