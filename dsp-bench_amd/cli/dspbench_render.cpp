@@ -22,8 +22,26 @@
 //     --stft FILE       also write the Hann 8192 / 4096 STFT magnitudes of the
 //                       render: header "DSPMAG1\0", u32 C, u32 K, u64 F, then
 //                       C x F x K float32
-//     --device N        GPU ordinal (0)
+//     --device N        GPU ordinal (0; with --world: LOCAL_RANK if set, else the rank)
+//     --device-channels C   render into C device channels, as the reference's
+//                       device does (always 2, wasapi_audio.cpp:432-433): file
+//                       channels past C are dropped, missing ones render from
+//                       zeros (audio.cpp:65-81, 138-141).  Default: the file's.
+//     --device-rate R   the sample rate handed to the plugin and written to the
+//                       output header (the reference ignores the WAV's own rate,
+//                       wav_reader.h:7-14).  Default: the file's.
+//     --loop NBLOCKS    loop mode (audio.cpp:100-132): NBLOCKS blocks from a
+//                       file that wraps around (no --stft)
+//   multi-GPU (cfg 5, shard.h): one process per GPU, channels sharded one
+//   run per rank, the render + STFT gathered to rank 0 over RCCL (needs --stft)
+//     --world W --rank R    W processes, this one's rank (default: WORLD_SIZE /
+//                       RANK from the environment when --comm-id is given)
+//     --comm-id FILE    rendezvous file: rank 0 writes the RCCL id, the others
+//                       wait for it (a shared local path)
+//     --chunk S         pipeline chunk in samples (default 16 Mi)
 #include <hip/hip_runtime.h>
+
+#include <unistd.h>
 
 #include <chrono>
 #include <cstdio>
@@ -34,6 +52,7 @@
 
 #include "dspbench/dspbench.h"
 #include "dspbench/module.h"
+#include "dspbench/shard.h"
 #include "dspbench/wav.h"
 
 namespace {
@@ -68,7 +87,32 @@ void usage() {
     std::fprintf(stderr,
                  "usage: dspbench_render IN.wav OUT.wav [--plugin gain_test|IR_test|no_op|static_gain|PATH.cpp]\n"
                  "       [--gain G] [--ir G,STEP] [--block B] [--bits 16|24|32|float] [--stft MAG.f32]"
-                 " [--device N]\n");
+                 " [--device N]\n"
+                 "       [--device-channels C] [--device-rate R] [--loop NBLOCKS]\n"
+                 "       [--world W --rank R --comm-id FILE [--chunk SAMPLES]]\n");
+}
+
+// rank 0 writes the RCCL id to `path` (atomically: a temp file renamed),
+// the other ranks wait up to two minutes for it
+bool exchange_comm_id(const std::string &path, uint32_t rank, unsigned char *id) {
+    if (rank == 0) {
+        if (dsp_comm_unique_id(id)) return false;
+        const std::string tmp = path + ".tmp";
+        FILE *f = std::fopen(tmp.c_str(), "wb");
+        if (!f || std::fwrite(id, 1, DSP_COMM_ID_BYTES, f) != DSP_COMM_ID_BYTES) return false;
+        std::fclose(f);
+        return std::rename(tmp.c_str(), path.c_str()) == 0;
+    }
+    for (int i = 0; i < 1200; ++i) {
+        FILE *f = std::fopen(path.c_str(), "rb");
+        if (f) {
+            const size_t n = std::fread(id, 1, DSP_COMM_ID_BYTES, f);
+            std::fclose(f);
+            if (n == DSP_COMM_ID_BYTES) return true;
+        }
+        usleep(100000);
+    }
+    return false;
 }
 
 double ms_since(std::chrono::steady_clock::time_point t0) {
@@ -86,7 +130,11 @@ int main(int argc, char **argv) {
     std::string plugin = "gain_test", stft_path, bits_opt;
     float gain = -1.f, ir_gain = 0.9f, ir_step = 0.002f;
     uint32_t B = 512;
-    int device = 0;
+    int device = -1;
+    uint32_t dev_channels = 0, dev_rate = 0, world = 0, rank = 0;
+    uint64_t loop_blocks = 0, chunk = 16ull << 20;
+    bool have_rank = false;
+    std::string comm_path;
     for (int i = 3; i < argc; i += 2) {  // every option takes one value
         const std::string a = argv[i];
         const char *v = i + 1 < argc ? argv[i + 1] : nullptr;
@@ -105,6 +153,13 @@ int main(int argc, char **argv) {
         else if (a == "--bits") bits_opt = v;
         else if (a == "--stft") stft_path = v;
         else if (a == "--device") device = std::atoi(v);
+        else if (a == "--device-channels") dev_channels = (uint32_t)std::strtoul(v, nullptr, 10);
+        else if (a == "--device-rate") dev_rate = (uint32_t)std::strtoul(v, nullptr, 10);
+        else if (a == "--loop") loop_blocks = std::strtoull(v, nullptr, 10);
+        else if (a == "--world") world = (uint32_t)std::strtoul(v, nullptr, 10);
+        else if (a == "--rank") rank = (uint32_t)std::strtoul(v, nullptr, 10), have_rank = true;
+        else if (a == "--comm-id") comm_path = v;
+        else if (a == "--chunk") chunk = std::strtoull(v, nullptr, 10);
         else {
             usage();
             return 2;
@@ -114,6 +169,21 @@ int main(int argc, char **argv) {
         usage();
         return 2;
     }
+    const bool multi = !comm_path.empty();
+    if (multi) {  // torchrun-style environment when not given explicitly
+        const char *ew = std::getenv("WORLD_SIZE"), *er = std::getenv("RANK");
+        if (!world) world = ew ? (uint32_t)std::atoi(ew) : 1;
+        if (!have_rank) rank = er ? (uint32_t)std::atoi(er) : 0;
+        if (device < 0) {
+            const char *lr = std::getenv("LOCAL_RANK");
+            device = lr ? std::atoi(lr) : (int)rank;
+        }
+        if (world == 0 || rank >= world || stft_path.empty() || loop_blocks) {
+            std::fprintf(stderr, "dspbench_render: --comm-id needs --stft, rank < world and no --loop\n");
+            return 2;
+        }
+    }
+    if (device < 0) device = 0;
 
     // ---- load + parse (wav_reader.h:57-205) --------------------------------
     std::vector<unsigned char> file;
@@ -124,10 +194,13 @@ int main(int argc, char **argv) {
     dsp_wav_info info{};
     int st = dsp_wav_parse(file.data(), file.size(), &info);
     if (st) return fail("dsp_wav_parse", st);
-    const uint32_t C = info.channels;
+    const uint32_t Cf = info.channels;                // the file's channels
+    const uint32_t C = dev_channels ? dev_channels : Cf;  // the device's (the render's)
+    const uint32_t Cin = Cf < C ? Cf : C;             // channels_to_write (audio.cpp:66)
+    const uint32_t rate = dev_rate ? dev_rate : info.sample_rate;
     const uint64_t L = info.frames;
-    if (C == 0 || C > 16) {
-        std::fprintf(stderr, "dspbench_render: %u channels (1..16 supported)\n", C);
+    if (Cf == 0 || Cf > 16 || C == 0 || C > 16) {
+        std::fprintf(stderr, "dspbench_render: %u file / %u device channels (1..16 supported)\n", Cf, C);
         return 1;
     }
     std::vector<unsigned char> payload(info.data_bytes);
@@ -150,12 +223,10 @@ int main(int argc, char **argv) {
     void *d_pay = nullptr;
     HIPCK(hipMalloc(&d_pay, payload.size() + 16));
     HIPCK(hipMemcpyAsync(d_pay, payload.data(), payload.size(), hipMemcpyHostToDevice, s));
-    const uint64_t nblocks = (L + B - 1) / B, Lr = nblocks * B;
-    std::vector<float *> din(C), dout(C);
-    for (uint32_t c = 0; c < C; ++c) {
-        HIPCK(hipMalloc(&din[c], (L ? L : 1) * sizeof(float)));
-        HIPCK(hipMalloc(&dout[c], Lr * sizeof(float)));
-    }
+    const uint64_t nblocks = loop_blocks ? loop_blocks : (L + B - 1) / B, Lr = nblocks * B;
+    std::vector<float *> din(Cf), dout(C);
+    for (uint32_t c = 0; c < Cf; ++c) HIPCK(hipMalloc(&din[c], (L ? L : 1) * sizeof(float)));
+    for (uint32_t c = 0; c < C; ++c) HIPCK(hipMalloc(&dout[c], Lr * sizeof(float)));
     if ((st = dsp_wav_decode(d_pay, &info, 0, L, din.data(), &ex))) return fail("dsp_wav_decode", st);
 
     // ---- plugin ------------------------------------------------------------
@@ -197,30 +268,81 @@ int main(int argc, char **argv) {
         if ((st = dsp_module_sizes(mod, &ps, &ss, &stateless))) return fail("dsp_module_sizes", st);
         gparams.resize(ps ? ps : 1);
         if ((st = dsp_module_default_parameters(mod, gparams.data()))) return fail("dsp_module_default_parameters", st);
-        if ((st = dsp_module_initialize_state(mod, gparams.data(), C, (float)info.sample_rate, 16u << 20)))
+        if ((st = dsp_module_initialize_state(mod, gparams.data(), C, (float)rate, 16u << 20)))
             return fail("dsp_module_initialize_state", st);
         p.kind = DSP_PLUGIN_GENERIC, p.params = gparams.data(), p.params_size = ps, p.module = mod;
     }
 
     // ---- render (+ STFT) ---------------------------------------------------
-    const float sr = (float)info.sample_rate;
+    const float sr = (float)rate;
     const uint32_t N = 8192, H = 4096, K = N / 2 + 1;
     const uint64_t F = stft_path.empty() ? 0 : dsp_stft_frame_count(Lr, N, H);
     std::vector<float *> dmag(C, nullptr);
     hipEvent_t e0, e1;
     HIPCK(hipEventCreate(&e0));
     HIPCK(hipEventCreate(&e1));
+    dsp_comm *comm = nullptr;
+    if (multi) {
+        unsigned char id[DSP_COMM_ID_BYTES];
+        if (!exchange_comm_id(comm_path, rank, id)) {
+            std::fprintf(stderr, "dspbench_render: rank %u: no communicator id at %s\n", rank, comm_path.c_str());
+            return 1;
+        }
+        if ((st = dsp_comm_init(id, world, rank, device, &comm))) return fail("dsp_comm_init", st);
+    }
     HIPCK(hipEventRecord(e0, s));
-    if (!stft_path.empty() && F > 0) {
+    if (multi) {
+        // cfg 5: this rank renders + STFTs its run of channels, rank 0
+        // gathers every channel (dout / dmag hold the whole file there)
+        dsp_shard sh{};
+        if ((st = dsp_shard_plan(L, C, world, rank, B, N, H, DSP_SHARD_CHANNELS, 1, &sh)))
+            return fail("dsp_shard_plan", st);
+        std::vector<float *> lout(sh.channels), lmag(sh.channels);
+        std::vector<const float *> lin;
+        for (uint32_t j = 0; j < sh.channels; ++j) {
+            const uint32_t c = sh.chan0 + j;
+            if (c < Cin) lin.push_back(din[c]);
+            if (rank == 0) {
+                lout[j] = dout[c];
+            } else {
+                HIPCK(hipMalloc(&lout[j], Lr * sizeof(float)));
+            }
+            HIPCK(hipMalloc(&lmag[j], (F ? F : 1) * K * sizeof(float)));
+        }
+        if (rank == 0)
+            for (uint32_t c = 0; c < C; ++c) HIPCK(hipMalloc(&dmag[c], (F ? F : 1) * K * sizeof(float)));
+        st = dsp_render_stft_sharded(lin.data(), (uint32_t)lin.size(), L, lout.data(), lmag.data(), K, C, B, sr, &p,
+                                     N, H, DSP_WIN_HANN, K, &sh, chunk, comm, 0, rank == 0 ? dout.data() : nullptr,
+                                     rank == 0 ? dmag.data() : nullptr, &ex);
+        if (st) return fail("dsp_render_stft_sharded", st);
+        HIPCK(hipStreamSynchronize(s));
+        for (uint32_t j = 0; j < sh.channels; ++j) {
+            if (rank != 0) (void)hipFree(lout[j]);
+            (void)hipFree(lmag[j]);
+        }
+    } else if (loop_blocks) {
+        uint64_t cursor = 0;
+        if ((st = dsp_render_loop(din.data(), Cin, L, 0, dout.data(), C, B, nblocks, sr, &p, &cursor, &ex)))
+            return fail("dsp_render_loop", st);
+    } else if (!stft_path.empty() && F > 0) {
         for (uint32_t c = 0; c < C; ++c) HIPCK(hipMalloc(&dmag[c], F * K * sizeof(float)));
-        st = dsp_render_stft(din.data(), C, L, dout.data(), C, B, sr, &p, N, H, DSP_WIN_HANN, K, dmag.data(), K,
+        st = dsp_render_stft(din.data(), Cin, L, dout.data(), C, B, sr, &p, N, H, DSP_WIN_HANN, K, dmag.data(), K,
                              &ex);
         if (st) return fail("dsp_render_stft", st);
     } else {
-        if ((st = dsp_render_offline(din.data(), C, L, dout.data(), C, B, sr, &p, &ex)))
+        if ((st = dsp_render_offline(din.data(), Cin, L, dout.data(), C, B, sr, &p, &ex)))
             return fail("dsp_render_offline", st);
     }
     HIPCK(hipEventRecord(e1, s));
+    if (multi && rank != 0) {  // only the root writes
+        HIPCK(hipStreamSynchronize(s));
+        float ms = 0.f;
+        HIPCK(hipEventElapsedTime(&ms, e0, e1));
+        std::printf("dspbench_render: rank %u of %u: channels rendered and gathered to rank 0 in %.3f ms\n", rank,
+                    world, ms);
+        dsp_comm_destroy(comm);
+        return 0;
+    }
 
     // ---- encode the render (audio.h:123-133 interleave) and write ----------
     uint16_t fmt = info.format, bits = info.bits_per_sample;
@@ -231,7 +353,7 @@ int main(int argc, char **argv) {
     HIPCK(hipMalloc(&d_opay, out_bytes + 16));
     if ((st = dsp_wav_encode(dout.data(), C, Lr, fmt, bits, d_opay, &ex))) return fail("dsp_wav_encode", st);
     std::vector<unsigned char> out(64 + out_bytes);
-    const int hdr = dsp_wav_write_header(out.data(), out.size(), fmt, (uint16_t)C, info.sample_rate, bits, Lr);
+    const int hdr = dsp_wav_write_header(out.data(), out.size(), fmt, (uint16_t)C, rate, bits, Lr);
     if (hdr < 0) return fail("dsp_wav_write_header", hdr);
     HIPCK(hipMemcpyAsync(out.data() + hdr, d_opay, out_bytes, hipMemcpyDeviceToHost, s));
     std::vector<float> mag;
@@ -262,14 +384,15 @@ int main(int argc, char **argv) {
     }
     std::printf("dspbench_render: %s: %u ch x %llu frames @ %u Hz -> %s (%s %u-bit, %llu blocks of %u)%s; "
                 "render %.3f ms on the GPU, %.1f ms end to end\n",
-                in_path, C, (unsigned long long)L, info.sample_rate, out_path,
+                in_path, C, (unsigned long long)L, rate, out_path,
                 fmt == DSP_WAV_FORMAT_FLOAT ? "float" : "PCM", bits, (unsigned long long)nblocks, B,
                 F ? (" + STFT " + std::to_string(F) + " frames x " + std::to_string(K) + " bins").c_str() : "",
                 render_ms, ms_since(t0));
 
     if (mod) dsp_module_destroy(mod);
+    if (comm) dsp_comm_destroy(comm);
+    for (uint32_t c = 0; c < Cf; ++c) (void)hipFree(din[c]);
     for (uint32_t c = 0; c < C; ++c) {
-        (void)hipFree(din[c]);
         (void)hipFree(dout[c]);
         if (dmag[c]) (void)hipFree(dmag[c]);
     }

@@ -59,7 +59,7 @@ struct DeviceRes {
     v2f *tw8192 = nullptr;  // exp(-2 pi i k / 8192), then 896 lane-major stage twiddles
     float4 *wbase = nullptr;  // (cos, sin)(theta 2l), (cos, sin)(theta (2l+1)), theta = 2 pi / 8191
     std::map<std::tuple<int, uint32_t, uint32_t, float>, float *> windows;  // (kind, N, valid, scale)
-    std::map<void *, std::pair<float *, size_t>> scratch;     // per stream
+    std::map<std::pair<void *, int>, std::pair<float *, size_t>> scratch;  // per (stream, slot)
     std::vector<FirTaps> fir;                                  // FIR filters seen (plugin_map)
     float *delta = nullptr;  // 2048 floats: 1, 0, 0, ... (compute_IR's impulse, read-only)
 };
@@ -196,11 +196,12 @@ static int set_wincomp(int dev, int kind, Stft8kArgs *A) {
 }
 
 // Stream-ordered scratch: calls on one stream are serialised by the stream,
-// so one buffer per (device, stream) is enough.
-static int get_scratch(int dev, hipStream_t s, size_t bytes, float **out) {
+// so one buffer per (device, stream, slot) is enough.  Slots: 0 the IR_test
+// block table, 1 loop mode's wrapped file.
+static int get_scratch(int dev, hipStream_t s, size_t bytes, float **out, int slot_id = 0) {
     std::lock_guard<std::mutex> lk(g_mu);
     DeviceRes &r = g_res[dev];
-    auto &slot = r.scratch[(void *)s];
+    auto &slot = r.scratch[std::make_pair((void *)s, slot_id)];
     if (slot.second < bytes) {
         if (slot.first) {
             DSPB_HIP(hipStreamSynchronize(s));
@@ -804,7 +805,7 @@ int dsp_render_loop(const float *const *in, uint32_t in_channels, uint64_t L, ui
     // stream), then rendered as a one-shot file of nblocks B samples
     float *tmp = nullptr;
     if (in_ch) {
-        DSPB_HIP(hipMallocAsync((void **)&tmp, sizeof(float) * Lr * in_ch, s));
+        if ((st = get_scratch(g.dev, s, sizeof(float) * Lr * in_ch, &tmp, 1))) return st;
         std::vector<float *> rows(in_ch);
         for (uint32_t c = 0; c < in_ch; ++c) rows[c] = tmp + (uint64_t)c * Lr;
         SampleMap id{};
@@ -816,7 +817,6 @@ int dsp_render_loop(const float *const *in, uint32_t in_channels, uint64_t L, ui
     } else {
         st = render_device(nullptr, 0, Lr, out, C, B, map, 0, goff_of(ex), s);
     }
-    if (tmp) (void)hipFreeAsync(tmp, s);
     return st ? st : finish(ex);
 }
 

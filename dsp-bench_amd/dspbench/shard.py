@@ -248,9 +248,13 @@ def render_stft_sharded(x, L_total: int, C_total: int, B: int, sr: float, plugin
                     compute(c, xo, oo, mo, c.start)
                 else:
                     from .api import render_stft
+                    Fc = stft_frames(nb * B, N, H)
+                    if Fc > c.frames:
+                        raise ValueError(f"chunk computes {Fc} frames, owns {c.frames}")
+                    # (a chunk without frames still needs valid magnitude rows)
+                    mrows = mag[:, c.frame0 - s.frame0:] if c.frames else mag
                     render_stft(xo, s.channels, B, sr, plugin, N=N, H=H, window=window, K=K, ld=ld,
-                                out=oo, mag=mag[:, c.frame0 - s.frame0:], sample_offset=c.start, L_file=Lc,
-                                ref=out)
+                                out=oo, mag=mrows, sample_offset=c.start, L_file=Lc, ref=out)
                     if out.is_cuda:
                         torch.cuda.current_stream().synchronize()
             pieces = []

@@ -81,7 +81,7 @@ def test_render_file_matches_oracle(torch_cuda, oracle, tmp_path, plugin, B):
 
 @needs_cli
 @pytest.mark.gpu
-def test_render_stft_file(torch_cuda, tmp_path):
+def test_render_stft_file(torch_cuda, oracle, tmp_path):
     src, raw, L = _pcm16_stereo(tmp_path, L=48_000 * 2)
     out, mag = tmp_path / "out.wav", tmp_path / "mag.f32"
     r = run(str(src), str(out), "--plugin", "IR_test", "--stft", str(mag), "--bits", "float")
@@ -96,6 +96,15 @@ def test_render_stft_file(torch_cuda, tmp_path):
     assert (C_, F, K) == tuple(ref_mag.shape)
     assert np.array_equal(m, ref_mag.cpu().numpy())
     assert np.array_equal(_read_float_wav(out), ref_out.cpu().numpy())
+    # and against the oracle: the render bit for bit, the spectra within the
+    # STFT bar (1e-6 of each frame's peak, float64)
+    want = oracle.render_offline([], 2, 512, 48000.0,
+                                 oracle.restated_plugin("IR_test"), L=L)
+    assert np.array_equal(_read_float_wav(out), want)
+    for c in range(2):
+        mref = oracle.np_stft_mag(want[c], 8192, 4096, d.DSP_WIN_HANN, 4097)
+        err = np.max(np.abs(m[c] - mref).max(axis=1) / mref.max(axis=1))
+        assert err <= 1e-6
 
 
 def _read_float_wav_pcm(path):
@@ -117,3 +126,71 @@ def test_plugin_source_file(torch_cuda, tmp_path):
     x = torch_cuda.from_numpy(_read_float_wav_pcm(src)).cuda()
     want = d.render_offline(x, 2, 256, 48000.0, mod.plugin(params)).cpu().numpy()
     assert np.array_equal(got, want)
+
+
+@needs_cli
+def test_multi_rank_needs_stft(tmp_path):
+    src, _, _ = _pcm16_stereo(tmp_path, L=1000)
+    r = run(str(src), str(tmp_path / "o.wav"), "--comm-id", str(tmp_path / "id"), "--world", "2", "--rank", "0")
+    assert r.returncode == 2 and "--comm-id needs --stft" in r.stderr
+
+
+def _pcm16(tmp_path, C, L, sr, seed, name="in.wav"):
+    raw = np.random.default_rng(seed).integers(-32768, 32768, size=C * L, dtype=np.int64).astype("<i2")
+    p = tmp_path / name
+    p.write_bytes(wav_image(raw.tobytes(), fmt=1, channels=C, bits=16, sr=sr))
+    return p, raw
+
+
+@needs_cli
+@pytest.mark.gpu
+@pytest.mark.parametrize("Cf,Cd", [(1, 2), (3, 2)])
+def test_device_format_mode(torch_cuda, oracle, tmp_path, Cf, Cd):
+    """the reference renders at the device's format -- 2
+    channels, the device rate -- whatever the file's (wav_reader.h:7-14,
+    wasapi_audio.cpp:432-447): extra file channels are dropped, missing ones
+    render from zeros, the callback sees the device rate."""
+    L = 30_011
+    src, raw = _pcm16(tmp_path, Cf, L, 44100, 12)
+    out = tmp_path / "out.wav"
+    r = run(str(src), str(out), "--plugin", "gain_test", "--device-channels", str(Cd), "--device-rate", "48000",
+            "--bits", "float")
+    assert r.returncode == 0, r.stderr
+    got, info = d.wav.load(str(out))
+    assert info.sample_rate == 48000 and info.channels == Cd
+    x = oracle.deinterleave(oracle.pcm_to_float(raw.view(np.uint8), 16), Cf)
+    want = oracle.render_offline([x[c] for c in range(Cf)], Cd, 512, 48000.0, oracle.restated_plugin("gain_test", [0.2]))
+    assert np.array_equal(np.asarray(got), want)
+
+
+@needs_cli
+@pytest.mark.gpu
+def test_loop_mode_file(torch_cuda, oracle, tmp_path):
+    """--loop: render_audio with the file looping (audio.cpp:100-132)."""
+    src, raw, L = _pcm16_stereo(tmp_path, L=5_000)
+    out = tmp_path / "out.wav"
+    r = run(str(src), str(out), "--plugin", "gain_test", "--loop", "33", "--block", "512", "--bits", "float")
+    assert r.returncode == 0, r.stderr
+    x = oracle.deinterleave(oracle.pcm_to_float(raw.view(np.uint8), 16), 2)
+    want, _ = oracle.render_loop([x[0], x[1]], 2, 512, 33, 48000.0, oracle.restated_plugin("gain_test", [0.2]))
+    assert np.array_equal(_read_float_wav(out), want)
+
+
+@needs_cli
+@pytest.mark.gpu
+def test_multi_rank_cli_one_rank(torch_cuda, oracle, tmp_path):
+    """The CLI's multi-GPU mode (cfg 5 shape: 96 kHz, one channel run per rank,
+    RCCL gather to rank 0) with one rank: the RCCL rendezvous file, the
+    sharded pipelined driver and the root's output equal the single-process
+    render + STFT."""
+    L = 8192 * 10 + 321
+    src, raw = _pcm16(tmp_path, 4, L, 96000, 13)
+    a, am = tmp_path / "a.wav", tmp_path / "a.f32"
+    b, bm = tmp_path / "b.wav", tmp_path / "b.f32"
+    r = run(str(src), str(a), "--plugin", "IR_test", "--stft", str(am), "--bits", "float")
+    assert r.returncode == 0, r.stderr
+    r = run(str(src), str(b), "--plugin", "IR_test", "--stft", str(bm), "--bits", "float",
+            "--comm-id", str(tmp_path / "rccl.id"), "--world", "1", "--rank", "0", "--chunk", "30000")
+    assert r.returncode == 0, r.stderr
+    assert a.read_bytes() == b.read_bytes()
+    assert am.read_bytes() == bm.read_bytes()
