@@ -16,8 +16,9 @@ is already resident in HBM:
 Multi-GPU (launched by torch.distributed.run): the file is N hours long and
 every rank renders its own hour (time-chunk sharding with an N - H = 4096
 sample halo) -- no data-path collective, weak scaling.  With
---gather the outputs are additionally gathered to rank 0 over RCCL (xGMI)
-and that time is reported separately ("gather_ms"), outside `value`.
+--gather one more pass runs the product's pipelined sharded driver with the
+gather of every rank's render and spectra to rank 0 over RCCL (xGMI), timed
+separately ("render_gather_ms"), outside `value`.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--minutes M]
                        [--no-cpu-baseline] [--gather]
@@ -54,6 +55,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
     ap.add_argument("--gather", action="store_true", help="also time an RCCL gather to rank 0")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (host WAV -> host spectra) pass")
     ap.add_argument("--fir-method", type=int, default=0, choices=[0, 1, 2],
                     help="fir1024: 0 auto (overlap-save), 1 direct form, 2 overlap-save")
     ap.add_argument("--workload", default="headline",
@@ -106,30 +108,68 @@ def cpu_baseline_generic(seconds_budget: float):
                       "(compiled from source, -Ofast) and the oracle's render_audio loop, 1 thread"}
 
 
+def _cpu_threads():
+    """Host threads the all-core CPU baseline uses: the CPUs this process may
+    run on (sched_getaffinity), capped by OMP_NUM_THREADS when the
+    environment sets it (the GPU box sets 16 per GPU; nproc there counts the
+    whole machine)."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(aff, int(omp))) if omp and omp.isdigit() else aff, aff
+
+
 def cpu_baseline(seconds_budget: float):
-    """The oracle (C restatement, fp32 FFT) on the host cores: render IR_test
-    block by block through the restated callback + fp32 STFT, on a bounded
-    sample of the same workload (chunks of 60 s stereo until the budget)."""
+    """BASELINE.md section 2 on the GPU box's host cores, a bounded sample of
+    the same workload (48 kHz stereo, chunks of 60 s):
+
+      render  the reference's own IR_test.cpp, compiled from its source with
+              the JIT's flags (oracle/_ref/libref_IR_test.so), called block by
+              block by the oracle's render_audio loop (audio.cpp:13-175);
+      STFT    Hann 8192 / 4096, 4097 bins: the oracle's fp32 radix-4 Stockham
+              real FFT (a CPU restatement, not IPP: IPP is absent).
+
+    Timed on 1 thread, then on all available threads (render chunks in
+    parallel threads, OpenMP over STFT frames).  Falls back to the restated
+    callback when oracle/_ref is not built."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import numpy as np
     import oracle as o
-    threads = min(16, os.cpu_count() or 1)
+    from concurrent.futures import ThreadPoolExecutor
+    threads, aff = _cpu_threads()
     chunk = SR * 60
-    plug = o.restated_plugin("IR_test")
-    done = 0
-    t0 = time.perf_counter()
+    if o.ref_available():
+        ref = o.RefPlugin("IR_test", CH, float(SR))
+        plug, render_src = ref.as_oracle(), "the reference's IR_test.cpp (-Ofast JIT flags, oracle/_ref)"
+    else:
+        plug, render_src = o.restated_plugin("IR_test"), "the restated IR_test callback (oracle/_ref not built)"
     zero = np.zeros(chunk, np.float32)
-    while True:
-        out = o.render_offline([zero, zero], CH, B, float(SR), plug)
-        for c in range(CH):
-            o.c_stft_mag_f32(out[c], N_FFT, HOP, o.WIN_HANN, K_BINS, nthreads=threads)
-        done += CH * chunk
-        el = time.perf_counter() - t0
-        if el >= seconds_budget or done >= CH * SR * 3600:
-            break
-    return {"value": done / el / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port",
-            "sample": f"{done // CH / SR:.0f} s of 48 kHz stereo, IR_test render (restated callback, "
-                      f"1 thread) + fp32 radix-2 STFT ({threads} OpenMP threads), oracle/oracle.c"}
+    sub = chunk // threads // B * B
+
+    def render_part(i):  # blocks [i sub, (i + 1) sub) of the chunk (IR_test keeps no state)
+        n = sub if i < threads - 1 else chunk - sub * (threads - 1)
+        return o.render_offline([zero[:n], zero[:n]], CH, B, float(SR), plug, L=n)
+
+    def run(nt, budget):
+        done, t0 = 0, time.perf_counter()
+        with ThreadPoolExecutor(max_workers=nt) as ex:
+            while True:
+                if nt == 1:
+                    out = o.render_offline([zero, zero], CH, B, float(SR), plug)
+                else:
+                    out = np.concatenate(list(ex.map(render_part, range(threads))), axis=1)
+                for c in range(CH):
+                    o.c_stft_mag_f32_r4(out[c], N_FFT, HOP, o.WIN_HANN, K_BINS, nthreads=nt)
+                done += CH * chunk
+                el = time.perf_counter() - t0
+                if el >= budget:
+                    return done / el / 1e6, done
+    v1, d1 = run(1, seconds_budget / 2)
+    vn, dn = run(threads, seconds_budget / 2) if threads > 1 else (v1, d1)
+    return {"value": round(vn, 2), "unit": "Msamples/s", "cores": threads, "kind": "port",
+            "value_1_thread": round(v1, 2), "nproc": os.cpu_count(), "cpus_available": aff,
+            "sample": f"{dn // CH / SR:.0f} s ({threads} threads) and {d1 // CH / SR:.0f} s (1 thread) of 48 kHz "
+                      f"stereo: render through {render_src}, block by block; fp32 radix-4 Stockham real-FFT "
+                      "STFT (oracle/oracle.c, OpenMP over frames). CPU restatement, not IPP"}
 
 
 def bench_ir(args, dev, world, rank):
@@ -228,8 +268,9 @@ def main():
     L -= L % HOP  # whole hops per rank (HOP is a multiple of B)
     # the file is world * L samples long; rank r owns [r L, (r+1) L) and
     # reads a halo of the next rank's first N - H samples (dspbench/shard.py)
-    if wl == "ch96k":  # the whole file of this rank's own channel
-        sh = d.shard.plan(L, 1, 0, B, N_FFT, HOP, render=True)
+    if wl == "ch96k":  # cfg 5: a world-channel file, one channel run (here: one channel) per rank
+        sh = d.shard.plan(L, world, rank, B, N_FFT, HOP, True, world, d.shard.CHANNELS)
+        assert sh.channels == 1, sh
     else:
         sh = d.shard.plan(world * L, world, rank, B, N_FFT if wl in ("headline", "stft96k") else HOP, HOP,
                           render=(wl == "headline"))
@@ -251,9 +292,7 @@ def main():
     F = d.stft_frames(nb * B if wl in ("headline", "ch96k") else L_in, N_FFT, HOP)
     out = (torch.empty((CH, nb * B), device=dev) if wl in ("headline", "ch96k", "gain10min", "fir1024", "generic")
            else None)
-    # rows: the last rank owns one frame less (no halo); equal-sized rows keep
-    # the optional gather a plain dist.gather
-    mag = torch.empty((CH, max(F, L // HOP), K_BINS), device=dev) if wl in ("headline", "stft96k", "ch96k") else None
+    mag = torch.empty((CH, max(F, 1), K_BINS), device=dev) if wl in ("headline", "stft96k", "ch96k") else None
     plugin = d.Plugin.ir_test(0.9, 0.002) if wl in ("headline", "ch96k") else d.Plugin.gain_test(0.2)
     stream = torch.cuda.current_stream(dev)
     soff = sh.start
@@ -272,9 +311,11 @@ def main():
                     f"{minutes:g} min of 48 kHz stereo per GPU")
         kname = f"{KERNEL}<render> (fused render + window + FFT + |X|)"
     elif wl == "ch96k":
+        # the product's sharded driver (shard.h dsp_render_stft_sharded) for
+        # this rank's channel, no collective in the timed step
         def step():
-            d.render_stft(x, CH, B, float(sr), plugin, N=N_FFT, H=HOP, window=d.DSP_WIN_HANN,
-                          K=K_BINS, out=out, mag=mag)
+            d.shard.render_stft_sharded(x, L, world, B, float(sr), plugin, sh, out, mag, comm=None, gather=False,
+                                        chunk=0, N=N_FFT, H=HOP, window=d.DSP_WIN_HANN, K=K_BINS)
         workload = ("BASELINE cfg 5: IR_test render (B=512) + 8192-pt Hann STFT of one 96 kHz channel "
                     f"({minutes:g} min) per GPU; channels sharded one per GPU")
         kname = f"{KERNEL}<render> (fused render + window + FFT + |X|)"
@@ -344,7 +385,14 @@ def main():
         plug_name = None
         alg_desc = f"C*L*({bits // 8} + 4) B (PCM payload read + planar float write)"
 
-    for _ in range(args.warmup):
+    # the first call is cold (code objects load, the output's first touch,
+    # the clock leaves idle): what an offline user rendering one file sees
+    torch.cuda.synchronize()
+    tf = time.perf_counter()
+    step()
+    torch.cuda.synchronize()
+    first_call_ms = (time.perf_counter() - tf) * 1e3
+    for _ in range(max(0, args.warmup - 1)):
         step()
     torch.cuda.synchronize()
 
@@ -399,22 +447,58 @@ def main():
         bytes_per_launch = alg_bytes
     achieved = bytes_per_launch / (kernel_avg_ms / 1e3) / 1e9 if kernel_avg_ms > 0 else 0.0
 
+    # --gather: one more pass through the product's pipelined sharded driver
+    # with the gather to rank 0 (RCCL over xGMI inside libdspbench; the
+    # one-GPU rehearsal uses gloo), timed on its own, outside `value`
     gather_ms = None
-    if args.gather and world > 1:
+    if args.gather and world > 1 and wl in ("headline", "ch96k"):
+        comm = d.shard.TorchComm() if rehearsal else d.shard.RcclComm.from_torch(device=local)
+        Ctot = world if wl == "ch96k" else CH
+        Lfile = L if wl == "ch96k" else world * L
+        Lpad = d.num_blocks(Lfile, B) * B
+        Ftot = d.stft_frames(Lpad, N_FFT, HOP)
+        all_out = torch.empty((Ctot, Lpad), device=dev) if rank == 0 else None
+        all_mag = torch.empty((Ctot, Ftot, K_BINS), device=dev) if rank == 0 else None
         torch.cuda.synchronize()
         dist.barrier()
         tg = time.perf_counter()
-        if out is not None:
-            owned = out[:, :L].contiguous()
-            bufs = [torch.empty_like(owned) for _ in range(world)] if rank == 0 else None
-            dist.gather(owned, bufs, dst=0)
-        if mag is not None:
-            fm = mag[:, : (F if wl == "ch96k" else L // HOP)].contiguous()
-            mbufs = [torch.empty_like(fm) for _ in range(world)] if rank == 0 else None
-            dist.gather(fm, mbufs, dst=0)
+        d.shard.render_stft_sharded(x, Lfile, Ctot, B, float(sr), plugin, sh, out, mag, comm=comm, root=0,
+                                    all_out=all_out, all_mag=all_mag, chunk=1 << 24, N=N_FFT, H=HOP,
+                                    window=d.DSP_WIN_HANN, K=K_BINS)
         torch.cuda.synchronize()
         dist.barrier()
         gather_ms = (time.perf_counter() - tg) * 1e3
+        del all_out, all_mag
+
+    # end to end: the same hour as a 16-bit PCM WAV payload in
+    # pinned host memory -> chunked H2D -> GPU decode -> render + STFT -> D2H
+    # of the render and the spectra into pinned host rows
+    # (dsp_render_stft_wav); never `value`
+    e2e = None
+    if wl == "headline" and world == 1 and not args.no_e2e:
+        from dspbench import wav as dwav
+        frames = L_in
+        pay = torch.randint(-32768, 32768, (CH * frames,), dtype=torch.int16).view(torch.uint8).pin_memory()
+        info = d._lib.dsp_wav_info(format=1, channels=CH, sample_rate=sr, bits_per_sample=16, block_align=CH * 2,
+                                   frames=frames, data_bytes=pay.numel(), n_data_chunks=1)
+        h_out = torch.empty((CH, nb * B), pin_memory=True)
+        h_mag = torch.empty((CH, F, K_BINS), pin_memory=True)
+        ts = []
+        for i in range(3):  # the first call pays the slots' allocation
+            torch.cuda.synchronize()
+            te = time.perf_counter()
+            dwav.render_stft_wav(pay, info, CH, B, float(sr), plugin, out=h_out, mag=h_mag, chunk=1 << 23,
+                                 stream=stream.cuda_stream)
+            ts.append((time.perf_counter() - te) * 1e3)
+        e2e_ms = min(ts[1:])
+        pcie = (pay.numel() + (h_out.numel() + h_mag.numel()) * 4) / (e2e_ms / 1e3) / 1e9
+        e2e = {"end_to_end_ms": round(e2e_ms, 3), "first_call_ms": round(ts[0], 3),
+               "msamples_per_s": round(CH * L / (e2e_ms / 1e3) / 1e6, 1),
+               "host_link_gb_s": round(pcie, 1),
+               "path": "16-bit stereo WAV payload in pinned host memory -> dsp_render_stft_wav (8 Mi-sample "
+                       "chunks: H2D, GPU decode, fused IR_test render + STFT, D2H of render + 4097-bin spectra "
+                       "into pinned host rows), best of 2 after a first call"}
+        del pay, h_out, h_mag
 
     traffic, traffic_src = (None, None)
     if wl in ("headline", "stft96k"):
@@ -448,9 +532,16 @@ def main():
                 "plugin": plug_name,
                 "samples_per_gpu": samples_per_rank,
                 "frames_per_gpu": CH * F if mag is not None else 0,
-                "sharding": ("one channel per GPU, no data-path collective" if wl == "ch96k" else
+                "sharding": ("one 96 kHz channel per GPU (a world-channel file, dsp_shard_plan CHANNELS, "
+                             "dsp_render_stft_sharded), no data-path collective" if wl == "ch96k" else
                              "time-chunk per GPU, 4096-sample halo, no data-path collective"),
-                "gather_ms": None if gather_ms is None else round(gather_ms, 3),
+                "render_gather_ms": None if gather_ms is None else round(gather_ms, 3),
+                "render_gather": ("one pass of the product's pipelined sharded driver with the gather of every "
+                                  "rank's render and spectra to rank 0 (dsp_render_stft_sharded over RCCL)"
+                                  if gather_ms is not None else None),
+                "first_call_ms": round(first_call_ms, 4),
+                "end_to_end": e2e,
+                "settled_step_ms_p50": round(pct(0.5), 4),
                 "step_ms_p10_p50_p90": [round(pct(0.1), 4), round(pct(0.5), 4), round(pct(0.9), 4)],
                 "step_ms_distribution": f"{nd} further steps, one event after each (outside the timed region)",
             },

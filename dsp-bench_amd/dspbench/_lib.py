@@ -101,6 +101,9 @@ _SIGS = {
     "dsp_render_stft": (C.c_int, [FPP, C.c_uint32, C.c_uint64, FPP, C.c_uint32, C.c_uint32,
                                   C.c_float, C.POINTER(dsp_plugin), C.c_uint32, C.c_uint32,
                                   C.c_int32, C.c_uint32, FPP, C.c_uint64, C.POINTER(dsp_exec)]),
+    "dsp_render_stft_host": (C.c_int, [FPP, C.c_uint32, C.c_uint64, FPP, C.c_uint32, C.c_uint32, C.c_float,
+                                       C.POINTER(dsp_plugin), C.c_uint32, C.c_uint32, C.c_int32, C.c_uint32, FPP,
+                                       C.c_uint64, C.c_uint64, C.POINTER(dsp_exec)]),
     "dsp_ir_analysis": (C.c_int, [C.POINTER(dsp_plugin), C.c_uint32, C.c_float, C.c_uint32,
                                   FPP, FP, C.POINTER(dsp_exec)]),
     "dsp_fft_forward": (C.c_int, [FP, FP, FP, C.c_uint32, C.POINTER(dsp_exec)]),
@@ -149,6 +152,9 @@ _SIGS = {
                                  C.POINTER(dsp_exec)]),
     "dsp_wav_encode": (C.c_int, [FPP, C.c_uint32, C.c_uint64, C.c_uint16, C.c_uint16, C.c_void_p,
                                  C.POINTER(dsp_exec)]),
+    "dsp_render_stft_wav": (C.c_int, [C.c_void_p, C.POINTER(dsp_wav_info), C.c_uint32, C.c_uint32, C.c_float,
+                                      C.POINTER(dsp_plugin), C.c_uint32, C.c_uint32, C.c_int32, C.c_uint32, FPP, FPP,
+                                      C.c_uint64, C.c_uint64, C.POINTER(dsp_exec)]),
     "dsp_wav_write_header": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint16, C.c_uint16, C.c_uint32,
                                        C.c_uint16, C.c_uint64]),
 }

@@ -207,6 +207,33 @@ def render_stft(file, C_out: int, B: int, sr: float, plugin: Plugin | None,
     return out[:, : nb * B], mag[:, :F, :K]
 
 
+def render_stft_host(x, C_out: int, B: int, sr: float, plugin: Plugin | None, stft: bool = True,
+                     N: int = 8192, H: int = 4096, window: int = L.DSP_WIN_HANN, K: int | None = None,
+                     chunk: int = 1 << 22, out=None, mag=None, sample_offset: int = 0, device: int = -1,
+                     stream=None):
+    """Host rows in, host rows out, streamed through HBM in chunks
+    (dsp_render_stft_host).  x: numpy / pinned torch CPU [Cin, L] float32.
+    Returns (out [C_out, ceil(L/B)B], mag [C_out, F, K] | None)."""
+    K = K if K is not None else N // 2 + 1
+    L_ = int(x.shape[1]) if x is not None else 0
+    Lp = num_blocks(L_, B) * B
+    F = stft_frames(Lp, N, H) if stft else 0
+    out = np.empty((C_out, max(Lp, 1)), np.float32) if out is None else out
+    if stft and mag is None:
+        mag = np.empty((C_out, max(F, 1), K), np.float32)
+    ptr = lambda a, c: a[c].data_ptr() if _is_torch(a) else a[c].ctypes.data  # noqa: E731
+    in_ptrs = [ptr(x, c) for c in range(x.shape[0])] if x is not None else []
+    ex = dsp_exec(device, 0, C.c_void_p(stream) if stream else None, sample_offset)
+    ps = plugin.as_struct() if plugin is not None else None
+    st = L.lib().dsp_render_stft_host(chan_table(in_ptrs) if in_ptrs else None, len(in_ptrs), L_,
+                                      chan_table([ptr(out, c) for c in range(C_out)]), C_out, B, sr,
+                                      C.byref(ps) if ps is not None else None, N, H, window, K,
+                                      chan_table([ptr(mag, c) for c in range(C_out)]) if stft else None, K, chunk,
+                                      C.byref(ex))
+    check(st, "dsp_render_stft_host")
+    return out[:, :Lp], (mag[:, :F] if stft else None)
+
+
 def ir_analysis(plugin: Plugin | None, C_out: int = 2, sr: float = 48000.0,
                 ir_len: int = IR_BUFFER_LENGTH, device=None):
     """compute_IR + fft_perform_and_get_magnitude.  Returns (ir [C, ir_len],

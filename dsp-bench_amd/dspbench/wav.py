@@ -106,3 +106,30 @@ def save(path: str, x, sample_rate: int, fmt: int = L.DSP_WAV_FORMAT_FLOAT, bits
         f.write(memoryview(data))
         if data.size & 1:
             f.write(b"\0")
+
+
+def render_stft_wav(data, info: dsp_wav_info, C_out: int, B: int, sr: float, plugin, stft: bool = True,
+                    N: int = 8192, H: int = 4096, window: int = L.DSP_WIN_HANN, K: int | None = None,
+                    chunk: int = 1 << 22, out=None, mag=None, device: int = -1, stream=None):
+    """The end-to-end path (wav.h dsp_render_stft_wav): a WAV payload in host
+    memory -> per chunk H2D, GPU decode, render (+ STFT), D2H into host rows.
+    `out` / `mag` (host float32, [C_out, ceil(L/B)B] / [C_out, F, K]) may be
+    given pinned (torch.empty(..., pin_memory=True)) for direct DMA.
+    Returns (out, mag | None) as numpy / the given host tensors."""
+    from .api import Plugin  # noqa: F401
+    K = K if K is not None else N // 2 + 1
+    Lp = -(-info.frames // B) * B
+    F = (Lp - N) // H + 1 if stft and Lp >= N else 0
+    out = np.empty((C_out, max(Lp, 1)), np.float32) if out is None else out
+    if stft and mag is None:
+        mag = np.empty((C_out, max(F, 1), K), np.float32)
+    ptr = (lambda a, c: a[c].data_ptr()) if _is_torch(out) else (lambda a, c: a[c].ctypes.data)
+    optrs = chan_table([ptr(out, c) for c in range(C_out)])
+    mptrs = chan_table([ptr(mag, c) for c in range(C_out)]) if stft else None
+    src = data.data_ptr() if _is_torch(data) else np.ascontiguousarray(data).ctypes.data
+    ex = L.dsp_exec(device, 0, C.c_void_p(stream) if stream else None, 0)
+    ps = plugin.as_struct() if plugin is not None else None
+    check(L.lib().dsp_render_stft_wav(C.c_void_p(src), C.byref(info), C_out, B, sr,
+                                      C.byref(ps) if ps is not None else None, N, H, window, K, optrs, mptrs, K,
+                                      chunk, C.byref(ex)), "dsp_render_stft_wav")
+    return out, (mag if stft else None)

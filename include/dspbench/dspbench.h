@@ -138,6 +138,21 @@ int dsp_render_stft(const float *const *in, uint32_t in_channels, uint64_t L,
                     int32_t window, uint32_t K, float *const *mag, uint64_t ld,
                     const dsp_exec *ex);
 
+/* End to end from host memory: dsp_render_stft (mag != NULL) or
+ * dsp_render_offline (mag == NULL) of host rows in[c] (L samples) into host
+ * rows out[c] (ceil(L / B) B floats) and mag[c] (F rows of stride ld),
+ * streamed through HBM in time chunks of about `chunk` samples (0: one
+ * chunk): the upload of chunk t + 1 and the download of chunk t - 1 overlap
+ * chunk t's compute (three HIP streams, two device slots).  Pinned host
+ * buffers (hipHostMalloc / hipHostRegister) are DMA'd directly, pageable ones
+ * staged through pinned slots.  Results equal the device-buffer call bit for
+ * bit (lcm(B, H)-aligned chunks with an N - H halo); FIR and GENERIC plugins
+ * run as one chunk.  Returns when the host rows are written.  ex->stream is
+ * the compute stream. */
+int dsp_render_stft_host(const float *const *in, uint32_t in_channels, uint64_t L, float *const *out, uint32_t C,
+                         uint32_t B, float sr, const dsp_plugin *plugin, uint32_t N, uint32_t H, int32_t window,
+                         uint32_t K, float *const *mag, uint64_t ld, uint64_t chunk, const dsp_exec *ex);
+
 /* IR analysis: ir_out[c][0..ir_len) = audio_callback(delta) for every
  * channel (plugin.cpp:27-54), then mag[0 .. 4*ir_len) = |FFT_{4 ir_len}(
  * hamming(ir_len) * ir_out[0], zero padded)| / sqrt(4 ir_len) (dsp.cpp:53-66).

@@ -71,6 +71,17 @@ int dsp_wav_decode(const void *payload, const dsp_wav_info *info, uint64_t frame
 int dsp_wav_encode(const float *const *in, uint32_t channels, uint64_t frames,
                    uint16_t format, uint16_t bits, void *payload, const dsp_exec *ex);
 
+/* The offline render path end to end from a WAV payload in host memory
+ * (the reference's load + convert + render, wav_reader.h:57-205,
+ * audio.h:66-121, audio.cpp:13-175): per time chunk the payload bytes cross
+ * PCIe, are decoded on the GPU (dsp_wav_decode), rendered (+ the STFT when
+ * mag != NULL) with C device channels (file channels past C dropped,
+ * missing ones zero), and the render / magnitude rows are copied back into
+ * host rows out[c] / mag[c]; streamed as dsp_render_stft_host (dspbench.h). */
+int dsp_render_stft_wav(const void *payload, const dsp_wav_info *info, uint32_t C, uint32_t B, float sr,
+                        const dsp_plugin *plugin, uint32_t N, uint32_t H, int32_t window, uint32_t K,
+                        float *const *out, float *const *mag, uint64_t ld, uint64_t chunk, const dsp_exec *ex);
+
 /* Write the header for `frames` frames; returns the header size in bytes
  * (44 PCM, 46 float) or a negative dsp_status if cap is too small. */
 int dsp_wav_write_header(void *out, uint64_t cap, uint16_t format, uint16_t channels,

@@ -398,6 +398,178 @@ void oracle_stft_mag_f32(const float *x, uint64_t L, uint32_t N, uint32_t H,
 }
 
 /* ------------------------------------------------------------------------ */
+/* fp32 CPU BASELINE STFT (bench.py cpu_baseline).    */
+/* A competent restatement, not IPP: window pre-scaled by 1/sqrt(N), the    */
+/* real frame packed as N/2 complex points, a radix-4 Stockham autosort FFT */
+/* (structure of arrays, per-stage twiddle tables, no bit reversal; one     */
+/* radix-2 stage when log2(N/2) is odd), then the real split and |X|.       */
+/* Parity: tests/test_oracle.py checks it against float64 (1e-6 of the      */
+/* frame's peak).  The hot loops are built for AVX2+FMA and baseline x86-64 */
+/* (gcc target_clones) so the same .so runs on any host.                    */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+    uint32_t M, npass;
+    float *tw[16][6];     /* per radix-4 pass: W_m^p, W_m^2p, W_m^3p (re, im), p < m/4 */
+    float *sr, *si;       /* W_N^k, k <= M (the real split) */
+    float *win;           /* window * 1/sqrt(N) */
+} rfft4_plan;
+
+static void rfft4_init(rfft4_plan *p, uint32_t N, int win)
+{
+    p->M = N / 2;
+    p->npass = 0;
+    for (uint32_t m = p->M; m >= 4 && p->npass < 16; m /= 4, ++p->npass) {
+        const uint32_t m4 = m / 4;
+        for (int j = 0; j < 6; ++j) p->tw[p->npass][j] = (float *)aligned_alloc(64, sizeof(float) * (m4 + 16));
+        for (uint32_t q = 0; q < m4; ++q)
+            for (int e = 1; e <= 3; ++e) {
+                double a = -2.0 * M_PI * (double)(e * q) / (double)m;
+                p->tw[p->npass][2 * (e - 1)][q] = (float)cos(a);
+                p->tw[p->npass][2 * (e - 1) + 1][q] = (float)sin(a);
+            }
+    }
+    p->sr = (float *)malloc(sizeof(float) * (p->M + 1));
+    p->si = (float *)malloc(sizeof(float) * (p->M + 1));
+    for (uint32_t k = 0; k <= p->M; ++k) {
+        double a = -2.0 * M_PI * (double)k / (double)N;
+        p->sr[k] = (float)cos(a); p->si[k] = (float)sin(a);
+    }
+    double *wd = (double *)malloc(sizeof(double) * N);
+    oracle_window_f64(win, N, wd);
+    p->win = (float *)malloc(sizeof(float) * N);
+    for (uint32_t i = 0; i < N; ++i) p->win[i] = (float)(wd[i] / sqrt((double)N));
+    free(wd);
+}
+
+static void rfft4_free(rfft4_plan *p)
+{
+    for (uint32_t i = 0; i < p->npass; ++i)
+        for (int j = 0; j < 6; ++j) free(p->tw[i][j]);
+    free(p->sr); free(p->si); free(p->win);
+}
+
+/* the radix-4 butterfly of one (p, q): a, b, c, d in, four outputs twiddled */
+#define R4_BFLY(ar_, ai_, br_, bi_, cr_, ci_, dr_, di_, w1r, w1i, w2r, w2i, w3r, w3i, Y0R, Y0I, Y1R, Y1I, Y2R, Y2I, \
+                Y3R, Y3I)                                                                                         \
+    do {                                                                                                          \
+        const float apcr = (ar_) + (cr_), apci = (ai_) + (ci_);                                                   \
+        const float amcr = (ar_) - (cr_), amci = (ai_) - (ci_);                                                   \
+        const float bpdr = (br_) + (dr_), bpdi = (bi_) + (di_);                                                   \
+        const float jr = (bi_) - (di_), ji = (dr_) - (br_); /* -i (b - d) */                                      \
+        Y0R = apcr + bpdr;                                                                                        \
+        Y0I = apci + bpdi;                                                                                        \
+        const float t1r = amcr + jr, t1i = amci + ji;                                                             \
+        Y1R = t1r * (w1r) - t1i * (w1i);                                                                          \
+        Y1I = t1r * (w1i) + t1i * (w1r);                                                                          \
+        const float t2r = apcr - bpdr, t2i = apci - bpdi;                                                         \
+        Y2R = t2r * (w2r) - t2i * (w2i);                                                                          \
+        Y2I = t2r * (w2i) + t2i * (w2r);                                                                          \
+        const float t3r = amcr - jr, t3i = amci - ji;                                                             \
+        Y3R = t3r * (w3r) - t3i * (w3i);                                                                          \
+        Y3I = t3r * (w3i) + t3i * (w3r);                                                                          \
+    } while (0)
+
+/* the first pass (stride 1): vectorised over p, outputs interleaved by 4 */
+__attribute__((target_clones("avx2", "default")))
+static void r4_pass_s1(uint32_t m, const float *restrict xr, const float *restrict xi, float *restrict yr,
+                       float *restrict yi, float *const *tw)
+{
+    const uint32_t m4 = m / 4;
+    const float *w1r = tw[0], *w1i = tw[1], *w2r = tw[2], *w2i = tw[3], *w3r = tw[4], *w3i = tw[5];
+    for (uint32_t p = 0; p < m4; ++p) {
+        float y0r, y0i, y1r, y1i, y2r, y2i, y3r, y3i;
+        R4_BFLY(xr[p], xi[p], xr[p + m4], xi[p + m4], xr[p + 2 * m4], xi[p + 2 * m4], xr[p + 3 * m4],
+                xi[p + 3 * m4], w1r[p], w1i[p], w2r[p], w2i[p], w3r[p], w3i[p], y0r, y0i, y1r, y1i, y2r, y2i, y3r,
+                y3i);
+        yr[4 * p] = y0r; yr[4 * p + 1] = y1r; yr[4 * p + 2] = y2r; yr[4 * p + 3] = y3r;
+        yi[4 * p] = y0i; yi[4 * p + 1] = y1i; yi[4 * p + 2] = y2i; yi[4 * p + 3] = y3i;
+    }
+}
+
+/* a later pass (stride s >= 4): vectorised over q */
+__attribute__((target_clones("avx2", "default")))
+static void r4_pass(uint32_t m, uint32_t s, const float *restrict xr, const float *restrict xi,
+                    float *restrict yr, float *restrict yi, float *const *tw)
+{
+    const uint32_t m4 = m / 4;
+    for (uint32_t p = 0; p < m4; ++p) {
+        const float w1r = tw[0][p], w1i = tw[1][p], w2r = tw[2][p], w2i = tw[3][p], w3r = tw[4][p], w3i = tw[5][p];
+        const float *ar = xr + s * p, *ai = xi + s * p;
+        const float *br = xr + s * (p + m4), *bi = xi + s * (p + m4);
+        const float *cr = xr + s * (p + 2 * m4), *ci = xi + s * (p + 2 * m4);
+        const float *dr = xr + s * (p + 3 * m4), *di = xi + s * (p + 3 * m4);
+        float *y0r = yr + s * 4 * p, *y0i = yi + s * 4 * p;
+        for (uint32_t q = 0; q < s; ++q)
+            R4_BFLY(ar[q], ai[q], br[q], bi[q], cr[q], ci[q], dr[q], di[q], w1r, w1i, w2r, w2i, w3r, w3i, y0r[q],
+                    y0i[q], y0r[s + q], y0i[s + q], y0r[2 * s + q], y0i[2 * s + q], y0r[3 * s + q], y0i[3 * s + q]);
+    }
+}
+
+__attribute__((target_clones("avx2", "default")))
+static void r4_frame(const rfft4_plan *p, const float *fr, float *ar, float *ai, float *br, float *bi, uint32_t K,
+                     float *row)
+{
+    const uint32_t M = p->M;
+    for (uint32_t m = 0; m < M; ++m) {  /* window (pre-scaled) and pack */
+        ar[m] = fr[2 * m] * p->win[2 * m];
+        ai[m] = fr[2 * m + 1] * p->win[2 * m + 1];
+    }
+    float *xr = ar, *xi = ai, *yr = br, *yi = bi;
+    uint32_t m = M, s = 1;
+    for (uint32_t pass = 0; m >= 4; m /= 4, s *= 4, ++pass) {
+        if (s == 1) r4_pass_s1(m, xr, xi, yr, yi, (float *const *)p->tw[pass]);
+        else r4_pass(m, s, xr, xi, yr, yi, (float *const *)p->tw[pass]);
+        float *t = xr; xr = yr; yr = t;
+        t = xi; xi = yi; yi = t;
+    }
+    if (m == 2) {  /* a last radix-2 pass */
+        for (uint32_t q = 0; q < s; ++q) {
+            const float a0r = xr[q], a0i = xi[q], a1r = xr[q + s], a1i = xi[q + s];
+            yr[q] = a0r + a1r; yi[q] = a0i + a1i;
+            yr[q + s] = a0r - a1r; yi[q + s] = a0i - a1i;
+        }
+        float *t = xr; xr = yr; yr = t;
+        t = xi; xi = yi; yi = t;
+    }
+    /* split: X[k] = E + W_N^k O, E = (Z[k] + conj Z[M-k]) / 2,
+       O = (Z[k] - conj Z[M-k]) / (2i); Z[M] = Z[0] */
+    const uint32_t kend = K < M + 1 ? K : M + 1;
+    for (uint32_t k = 0; k < kend; ++k) {
+        const uint32_t kk = k == M ? 0 : k, km = (k == 0 || k == M) ? 0 : M - k;
+        const float zr = xr[kk], zi = xi[kk], cr = xr[km], ci = -xi[km];
+        const float er = 0.5f * (zr + cr), ei = 0.5f * (zi + ci);
+        const float orr = 0.5f * (zi - ci), oi = -0.5f * (zr - cr);
+        const float tr = p->sr[k], ti = p->si[k];
+        const float Xr = er + (orr * tr - oi * ti), Xi = ei + (orr * ti + oi * tr);
+        row[k] = sqrtf(Xr * Xr + Xi * Xi);
+    }
+}
+
+void oracle_stft_mag_f32_r4(const float *x, uint64_t L, uint32_t N, uint32_t H,
+                            int win, uint32_t K, uint64_t ld, float *mag, int nthreads)
+{
+    uint64_t F = oracle_stft_frames(L, N, H);
+    rfft4_plan p;
+    rfft4_init(&p, N, win);
+    const uint32_t M = p.M;
+#ifdef _OPENMP
+    if (nthreads <= 0) nthreads = omp_get_max_threads();
+#else
+    nthreads = 1;
+#endif
+#pragma omp parallel num_threads(nthreads)
+    {
+        float *buf = (float *)aligned_alloc(64, sizeof(float) * 4 * (M + 16));
+        float *ar = buf, *ai = buf + (M + 16), *br = buf + 2 * (M + 16), *bi = buf + 3 * (M + 16);
+#pragma omp for schedule(static)
+        for (int64_t f = 0; f < (int64_t)F; ++f)
+            r4_frame(&p, x + (uint64_t)f * H, ar, ai, br, bi, K, mag + (uint64_t)f * ld);
+        free(buf);
+    }
+    rfft4_free(&p);
+}
+
+/* ------------------------------------------------------------------------ */
 /* Parameter normalisation (ref plugin.h:173-233)                            */
 /* ------------------------------------------------------------------------ */
 

@@ -90,6 +90,9 @@ void oracle_stft_mag_f64(const float *x, uint64_t L, uint32_t N, uint32_t H,
 void oracle_stft_mag_f32(const float *x, uint64_t L, uint32_t N, uint32_t H,
                          int win, uint32_t K, uint64_t ld, float *mag,
                          int nthreads);
+/* The CPU baseline's STFT: radix-4 Stockham real FFT, fp32 (bench.py). */
+void oracle_stft_mag_f32_r4(const float *x, uint64_t L, uint32_t N, uint32_t H,
+                            int win, uint32_t K, uint64_t ld, float *mag, int nthreads);
 
 /* Parameter normalisation (ref plugin.h:173-233), used by the K6 KATs. */
 float    oracle_normalize_int(int32_t lo, int32_t hi, float value);

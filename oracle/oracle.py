@@ -57,6 +57,7 @@ def lib() -> C.CDLL:
         L.oracle_stft_frames.argtypes = [u64, u32, u32]
         L.oracle_stft_mag_f64.argtypes = [vp, u64, u32, u32, C.c_int, u32, u64, vp]
         L.oracle_stft_mag_f32.argtypes = [vp, u64, u32, u32, C.c_int, u32, u64, vp, C.c_int]
+        L.oracle_stft_mag_f32_r4.argtypes = [vp, u64, u32, u32, C.c_int, u32, u64, vp, C.c_int]
         L.oracle_normalize_int.restype = f32
         L.oracle_normalize_int.argtypes = [C.c_int32, C.c_int32, f32]
         L.oracle_denormalize_int.restype = C.c_int32
@@ -262,6 +263,15 @@ def c_stft_mag_f32(x: np.ndarray, N: int, H: int, win: int, K: int, nthreads: in
     F = stft_frames(len(x), N, H)
     m = np.empty((max(F, 1), K), np.float32)
     lib().oracle_stft_mag_f32(_ptr(x), len(x), N, H, win, K, K, _ptr(m), nthreads)
+    return m[:F]
+
+
+def c_stft_mag_f32_r4(x: np.ndarray, N: int, H: int, win: int, K: int, nthreads: int = 0) -> np.ndarray:
+    """The CPU baseline's fp32 STFT (radix-4 Stockham real FFT, OpenMP over frames)."""
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    F = stft_frames(len(x), N, H)
+    m = np.empty((max(F, 1), K), np.float32)
+    lib().oracle_stft_mag_f32_r4(_ptr(x), len(x), N, H, win, K, K, _ptr(m), nthreads)
     return m[:F]
 
 
