@@ -141,6 +141,10 @@ int run(const Source &src, uint32_t C, uint32_t B, float sr, const dsp_plugin *p
         max_pad = std::max(max_pad, (nin + B - 1) / B * B);
         max_fr = std::max(max_fr, c.frames);
     }
+    // row strides of the slots: whole 16-byte units, so every row is as
+    // aligned as a fresh allocation (the fused kernels need 8-byte rows)
+    max_in = (max_in + 3) & ~3ull;
+    max_pad = (max_pad + 3) & ~3ull;
     bool in_pinned = true, out_pinned = true;
     if (src.wav()) in_pinned = is_pinned(src.payload);
     else

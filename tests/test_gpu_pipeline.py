@@ -27,7 +27,12 @@ def test_host_pipeline_equals_device_call(torch_cuda, plugin, B, chunk, pin):
     torch = torch_cuda
     L = 8192 * 9 + 333
     x = rnd((2, L), 81)
-    want_out, want_mag = d.render_stft(torch.from_numpy(x).cuda(), 2, B, 48000.0, plugin(), window=d.DSP_WIN_HANN)
+    # the reference call on 16-byte aligned rows, so that it takes the fused
+    # kernel as every chunk does (an odd row stride would send it down the
+    # unfused path, whose window is the table's: last-bit differences)
+    xp = torch.zeros((2, L + 3), device="cuda")
+    xp[:, :L] = torch.from_numpy(x).cuda()
+    want_out, want_mag = d.render_stft(xp[:, :L], 2, B, 48000.0, plugin(), window=d.DSP_WIN_HANN, L_file=L)
     Lp = d.num_blocks(L, B) * B
     F = d.stft_frames(Lp, 8192, 4096)
     if pin:
@@ -68,6 +73,8 @@ def test_wav_pipeline_matches_decode_and_oracle(torch_cuda, oracle, Cf, C_out, b
     want = oracle.render_offline([x[c] for c in range(Cf)][:C_out], C_out, 512, 48000.0,
                                  oracle.restated_plugin("gain_test", [0.2]))
     assert np.array_equal(out, want)
-    xd = torch.from_numpy(np.ascontiguousarray(x[:C_out])).cuda()
-    _, dmag = d.render_stft(xd, C_out, 512, 48000.0, d.Plugin.gain_test(0.2), L_file=L)
+    nin = min(Cf, C_out)
+    xd = torch.zeros((nin, L + 1), device="cuda")  # 8-byte aligned rows: the fused kernel, as the pipeline's chunks
+    xd[:, :L] = torch.from_numpy(np.ascontiguousarray(x[:nin])).cuda()
+    _, dmag = d.render_stft(xd[:, :L], C_out, 512, 48000.0, d.Plugin.gain_test(0.2), L_file=L)
     assert np.array_equal(mag, dmag.cpu().numpy())
