@@ -48,7 +48,9 @@ struct RenderArgsG {
     unsigned C;
     unsigned B;
     float sr;
-    unsigned lds;  // stateful: the block double-buffer lives in LDS (2 C B floats)
+    unsigned lds;  // path: stateful 1 = LDS double buffer; stateless 1/2 private, 3 LDS blocks
+    unsigned lds_nb;      // stateless LDS path: blocks per workgroup round
+    unsigned lds_stride;  // stateless LDS path: floats per block in LDS (C B + 1)
 };
 
 const char *kDriver = R"DSPB(
@@ -65,6 +67,8 @@ struct dspb_render_args {
     unsigned B;
     float sr;
     unsigned lds;
+    unsigned lds_nb;
+    unsigned lds_stride;
 };
 extern "C" __global__ void dspb_sizes(unsigned *o) {
     o[0] = sizeof(Parameters);
@@ -299,9 +303,85 @@ __device__ static void dspb_stateless_tiled(const dspb_render_args &A) {
         }
     }
 }
+// no state, LDS blocks: a workgroup renders lds_nb consecutive blocks per
+// round.  render_audio's copy (audio.cpp:13-175: the file at the cursor,
+// zeros past EOF and for the channels the file lacks) stages them into LDS
+// with all 256 threads, coalesced per channel; then wave w's lanes run the
+// callback on blocks [w nb/4, (w + 1) nb/4), one block per lane, in LDS (a
+// block's rows at a stride of C B + 1 floats: the lanes of one ds_read hit
+// different banks); then all threads copy the blocks out, coalesced.  The
+// callback's sample loop addresses one LDS base at constant offsets when C
+// and B are constants (CC, BB), so its loads run ahead of its stores.  Two
+// workgroups per CU: one stages while the other runs callbacks.
+template <unsigned CC, unsigned BB>
+__device__ static void dspb_stateless_lds(const dspb_render_args &A) {
+    extern __shared__ float dspb_lbuf[];
+    State local = *(State *)A.S;
+    Parameters prm = *(const Parameters *)A.P;
+    const unsigned C = CC ? CC : A.C, B = BB ? BB : A.B, NB = A.lds_nb, SB = A.lds_stride;
+    const unsigned t = threadIdx.x, nt = blockDim.x, wave = t >> 6, lane = t & 63u;
+    const unsigned per = NB / 4;  // blocks per wave
+    for (unsigned long long b0 = (unsigned long long)blockIdx.x * NB; b0 < A.nblocks;
+         b0 += (unsigned long long)gridDim.x * NB) {
+        const unsigned nb = (unsigned)(A.nblocks - b0 < NB ? A.nblocks - b0 : NB);
+        const unsigned long long i0 = b0 * B;
+        const unsigned long long lim = A.L > i0 ? A.L - i0 : 0;  // file samples left at i0
+        for (unsigned c = 0; c < C; ++c) {
+            const dspb_gfloat *x = (const dspb_gfloat *)A.in[c < A.in_ch ? c : 0] + i0;
+            const unsigned long long m = c < A.in_ch ? lim : 0;
+            const unsigned n = nb * B;
+            unsigned j = t;
+            for (; j + 3 * nt < n; j += 4 * nt) {  // four loads in flight per thread
+                const float v0 = j < m ? x[j] : 0.0f, v1 = j + nt < m ? x[j + nt] : 0.0f;
+                const float v2 = j + 2 * nt < m ? x[j + 2 * nt] : 0.0f, v3 = j + 3 * nt < m ? x[j + 3 * nt] : 0.0f;
+                unsigned q;
+                q = j / B;
+                dspb_lbuf[q * SB + c * B + (j - q * B)] = v0;
+                q = (j + nt) / B;
+                dspb_lbuf[q * SB + c * B + (j + nt - q * B)] = v1;
+                q = (j + 2 * nt) / B;
+                dspb_lbuf[q * SB + c * B + (j + 2 * nt - q * B)] = v2;
+                q = (j + 3 * nt) / B;
+                dspb_lbuf[q * SB + c * B + (j + 3 * nt - q * B)] = v3;
+            }
+            for (; j < n; j += nt) {
+                const unsigned q = j / B;
+                dspb_lbuf[q * SB + c * B + (j - q * B)] = j < m ? x[j] : 0.0f;
+            }
+        }
+        __syncthreads();
+        const unsigned k = wave * per + lane;
+        if (lane < per && k < nb) {
+            float *blk = dspb_lbuf + k * SB;
+            float *ptrs[CC ? CC : 16];
+            for (unsigned c = 0; c < C; ++c) ptrs[c] = blk + c * B;
+            audio_callback(prm, local, ptrs, C, B, A.sr);
+        }
+        __syncthreads();
+        for (unsigned c = 0; c < C; ++c) {
+            dspb_gfloat *o = (dspb_gfloat *)A.out[c] + i0;
+            const unsigned n = nb * B;
+            for (unsigned j = t; j < n; j += nt) {
+                const unsigned q = j / B;
+                o[j] = dspb_lbuf[q * SB + c * B + (j - q * B)];
+            }
+        }
+        __syncthreads();
+    }
+}
 extern "C" __global__ void dspb_render(dspb_render_args A) {
     extern __shared__ float dspb_lbuf[];
     if (__is_empty(State)) {
+        if (A.lds == 3) {
+            if (A.C == 2 && A.B == 512) dspb_stateless_lds<2, 512>(A);
+            else if (A.C == 2 && A.B == 256) dspb_stateless_lds<2, 256>(A);
+            else if (A.C == 2 && A.B == 1024) dspb_stateless_lds<2, 1024>(A);
+            else if (A.C == 1 && A.B == 512) dspb_stateless_lds<1, 512>(A);
+            else if (A.C == 1) dspb_stateless_lds<1, 0>(A);
+            else if (A.C == 2) dspb_stateless_lds<2, 0>(A);
+            else dspb_stateless_lds<0, 0>(A);
+            return;
+        }
         if (A.lds == 2 && A.C == 1) dspb_stateless_tiled<1>(A);
         else if (A.lds == 2 && A.C == 2) dspb_stateless_tiled<2>(A);
         else if (A.lds == 1 && A.C == 1) dspb_stateless_private<1>(A);
@@ -357,7 +437,9 @@ struct dsp_module {
                   f_callback = nullptr;
     uint32_t params_size = 0, state_size = 0;
     int stateless = 0;
-    std::map<uint64_t, int> priv_choice;  // stateless (C << 32 | B) -> 1: private path faster
+    void *h_params = nullptr;          // pinned staging of the Parameters upload
+    hipEvent_t upload_ev = nullptr;    // the last upload from h_params
+    hipEvent_t use_ev = nullptr;       // the last render launched with d_params / d_state
     void *d_params = nullptr;          // device Parameters
     void *d_state[2] = {nullptr, nullptr};  // [0] live State, [1] compute_IR scratch State
     ArenaHost *d_arena[2] = {nullptr, nullptr};
@@ -402,8 +484,16 @@ int make_arena(dsp_module *m, int slot, uint64_t bytes) {
     return DSP_OK;
 }
 
+// host-side writers of the device Parameters / State wait for the renders
+// that use them
+int wait_uses(dsp_module *m) {
+    if (m->use_ev) MOD_HIP(hipEventSynchronize(m->use_ev));
+    return DSP_OK;
+}
+
 int init_slot(dsp_module *m, int slot, const void *params, uint32_t C, float sr, uint64_t arena_bytes,
               hipStream_t s) {
+    if (int st = wait_uses(m)) return st;
     if (!params && m->params_size > 0) {
         set_last_error("initialize_state: params blob is NULL");
         return DSP_ERR_INVALID;
@@ -567,6 +657,12 @@ void dsp_module_destroy(dsp_module *m) {
             if (m->arena_mem[i]) (void)hipFree(m->arena_mem[i]);
         }
         if (m->d_params) (void)hipFree(m->d_params);
+        for (hipEvent_t e : {m->upload_ev, m->use_ev})
+            if (e) {
+                (void)hipEventSynchronize(e);
+                (void)hipEventDestroy(e);
+            }
+        if (m->h_params) (void)hipHostFree(m->h_params);
         if (m->mod) (void)hipModuleUnload(m->mod);
         if (prev >= 0 && prev != m->device) (void)hipSetDevice(prev);
     }
@@ -585,6 +681,7 @@ int dsp_module_sizes(const dsp_module *m, uint32_t *params_size, uint32_t *state
 int dsp_module_default_parameters(dsp_module *m, void *params) {
     if (!m || (!params && m->params_size)) return DSP_ERR_INVALID;
     std::lock_guard<std::mutex> lk(m->mu);
+    if (int st = wait_uses(m)) return st;
     int prev = -1;
     int st = with_device(m->device, &prev);
     if (st) return st;
@@ -774,6 +871,7 @@ int dsp_param_denormalize(const dsp_param_desc *p, const int64_t *enum_values, f
 
 int dsp_module_read_state(const dsp_module *m, void *state) {
     if (!m || (!state && m->state_size)) return DSP_ERR_INVALID;
+    if (int st = wait_uses(const_cast<dsp_module *>(m))) return st;
     MOD_HIP(hipMemcpy(state, m->d_state[0], m->state_size, hipMemcpyDeviceToHost));
     return DSP_OK;
 }
@@ -782,17 +880,18 @@ int dsp_module_read_state(const dsp_module *m, void *state) {
 
 namespace dspb {
 
-constexpr uint64_t kPrivMinBlocks = 32768;
 constexpr uint64_t kPrivFloatsHost = 1024;  // = kPrivFloats in kDriver
 // DSPB_STATELESS_PRIVATE=0 / 1 forces the in-place wave path / the private
 // path for eligible stateless renders (tools/generic_probe.py A/B); -1: timed
-static int stateless_private_forced() {
+static int stateless_path_forced() {
     static const int v = [] {
-        const char *e = std::getenv("DSPB_STATELESS_PRIVATE");
-        return e && (e[0] == '0' || e[0] == '1') ? e[0] - '0' : -1;
+        const char *e = std::getenv("DSPB_STATELESS_PATH");
+        return e && (e[0] == '0' || e[0] == '1' || e[0] == '3') ? e[0] - '0' : -1;
     }();
     return v;
 }
+// the LDS-blocks path: LDS per workgroup round (two workgroups per CU)
+constexpr uint64_t kLdsRoundBytes = 76 * 1024;
 
 // the private path's grid: DSPB_PRIV_WAVES=<waves per CU> caps it (the
 // lanes loop over blocks), bounding the scratch footprint in flight
@@ -816,6 +915,27 @@ static unsigned priv_mode(unsigned mode, uint32_t B) {
     return mode && tiled && B % 64 == 0 ? 2u : mode;
 }
 
+// the caller's Parameters blob -> the module's device Parameters, stream
+// ordered: through a pinned staging copy (reused once the previous upload
+// from it has completed), behind every earlier render's use of the device
+// Parameters on any stream (use_ev), so the call returns without a sync
+static int upload_params(dsp_module *m, const void *params, uint32_t n, hipStream_t s) {
+    if (!m->upload_ev) {
+        MOD_HIP(hipEventCreateWithFlags(&m->upload_ev, hipEventDisableTiming));
+        MOD_HIP(hipEventCreateWithFlags(&m->use_ev, hipEventDisableTiming));
+        MOD_HIP(hipEventRecord(m->upload_ev, s));
+        MOD_HIP(hipEventRecord(m->use_ev, s));
+    }
+    MOD_HIP(hipStreamWaitEvent(s, m->use_ev, 0));
+    if (!n) return DSP_OK;
+    if (!m->h_params) MOD_HIP(hipHostMalloc(&m->h_params, n, hipHostMallocDefault));
+    MOD_HIP(hipEventSynchronize(m->upload_ev));
+    std::memcpy(m->h_params, params, n);
+    MOD_HIP(hipMemcpyAsync(m->d_params, m->h_params, n, hipMemcpyHostToDevice, s));
+    MOD_HIP(hipEventRecord(m->upload_ev, s));
+    return DSP_OK;
+}
+
 // the module's code object, Parameters and State live on m->device: a call
 // made on another device (e.g. a mis-wired shard rank) is refused
 static int check_device(const dsp_module *m) {
@@ -826,16 +946,6 @@ static int check_device(const dsp_module *m) {
         return DSP_ERR_INVALID;
     }
     return DSP_OK;
-}
-
-// does any input channel's [0, n) overlap any output channel's [0, n) floats
-static bool overlaps(const float *const *in, uint32_t in_ch, float *const *out, uint32_t C, uint64_t n) {
-    for (uint32_t a = 0; a < in_ch; ++a)
-        for (uint32_t b = 0; b < C; ++b) {
-            const uintptr_t i0 = (uintptr_t)in[a], o0 = (uintptr_t)out[b], len = n * sizeof(float);
-            if (i0 < o0 + len && o0 < i0 + len) return true;
-        }
-    return false;
 }
 
 // dsp_render_offline / dsp_render_stft with DSP_PLUGIN_GENERIC (device buffers)
@@ -865,7 +975,7 @@ int module_render(dsp_module *m, const void *params, uint32_t params_size, const
         return DSP_ERR_INVALID;
     }
     std::lock_guard<std::mutex> lk(m->mu);
-    if (params_size) MOD_HIP(hipMemcpyAsync(m->d_params, params, params_size, hipMemcpyHostToDevice, s));
+    if (int st = upload_params(m, params, params_size, s)) return st;
     RenderArgsG A{};
     A.P = m->d_params;
     A.S = m->d_state[0];
@@ -881,58 +991,33 @@ int module_render(dsp_module *m, const void *params, uint32_t params_size, const
     if (A.nblocks == 0) return DSP_OK;
     void *args[] = {&A};
     unsigned grid = 1, block = 1, lds_bytes = 0;
-    if (m->stateless) {  // one wave per 64 blocks
-        block = 64;
-        const uint64_t g = (A.nblocks + 63) / 64;
-        grid = (unsigned)(g < 65535 ? g : 65535);
-        // mono / stereo blocks of up to 1024 samples in long files may take
-        // the private path. Which one is faster depends on the callback: the
-        // private copies cost ~3x the traffic of the in-place copy (no_op,
-        // 1 h stereo: 2.6 vs 0.6 ms) while a callback that loads and stores
-        // runs 2.5x faster there (gain_test: 3.3 vs 8.2 ms). So the first
-        // eligible render of a (C, B) shape runs a warm-up and both paths
-        // twice each (same bits by construction), and keeps the faster; an in-place render
-        // (in overlapping out) cannot run twice and takes the wave path until
-        // a decision exists. DSPB_STATELESS_PRIVATE=0/1 forces one.
-        if (C <= 2 && 1ull * C * B <= kPrivFloatsHost && A.nblocks >= kPrivMinBlocks) {
-            const int forced = stateless_private_forced();
-            const uint64_t key = (uint64_t)C << 32 | B;
-            auto it = m->priv_choice.find(key);
-            if (forced >= 0) {
-                A.lds = (unsigned)forced;
-            } else if (it != m->priv_choice.end()) {
-                A.lds = (unsigned)it->second;
-            } else if (!overlaps(in, in_ch, out, C, A.nblocks * B)) {
-                // a warm-up run (it pays the output's first touch and the
-                // clock ramp), then the paths in the order 0, 1, 1, 0 (a
-                // drifting clock favours neither), each path's faster run
-                constexpr unsigned kRuns = 5;
-                static const unsigned kMode[kRuns] = {0, 0, 1, 1, 0};
-                struct Events {  // destroyed on every return
-                    hipEvent_t e[kRuns + 1] = {};
-                    ~Events() {
-                        for (hipEvent_t x : e)
-                            if (x) (void)hipEventDestroy(x);
-                    }
-                } ev;
-                for (hipEvent_t &x : ev.e) MOD_HIP(hipEventCreate(&x));
-                MOD_HIP(hipEventRecord(ev.e[0], s));
-                for (unsigned r = 0; r < kRuns; ++r) {
-                    const unsigned mode = kMode[r];
-                    A.lds = priv_mode(mode, B);
-                    MOD_HIP(hipModuleLaunchKernel(m->f_render, mode ? priv_grid(grid) : grid, 1, 1, block, 1, 1,
-                                                  A.lds == 2 ? kTileBytes : 0, s, args, nullptr));
-                    MOD_HIP(hipEventRecord(ev.e[r + 1], s));
-                }
-                MOD_HIP(hipEventSynchronize(ev.e[kRuns]));
-                float best[2] = {1e30f, 1e30f};
-                for (unsigned r = 1; r < kRuns; ++r) {
-                    float ms;
-                    MOD_HIP(hipEventElapsedTime(&ms, ev.e[r], ev.e[r + 1]));
-                    best[kMode[r]] = std::min(best[kMode[r]], ms);
-                }
-                m->priv_choice[key] = best[1] < best[0] ? 1 : 0;
-                return DSP_OK;  // every run wrote the same output
+    if (m->stateless) {
+        // default: the LDS-blocks path (mode 3) when a round of at least 4
+        // blocks fits the per-workgroup LDS budget, else the in-place wave
+        // path (mode 0); DSPB_STATELESS_PATH=0/1/3 forces one (A/B: 1 = the
+        // private-array path, tiled when B % 64 == 0)
+        const uint64_t stride = (uint64_t)C * B + 1;
+        const uint64_t nb = std::min<uint64_t>(64, kLdsRoundBytes / (stride * sizeof(float)) / 4 * 4);
+        int path = stateless_path_forced();
+        if (path < 0) path = nb >= 4 ? 3 : 0;
+        if (path == 3 && nb < 4) path = 0;
+        if (path == 1 && !(C <= 2 && 1ull * C * B <= kPrivFloatsHost)) path = 0;
+        if (path == 3) {
+            A.lds = 3;
+            A.lds_nb = (unsigned)nb;
+            A.lds_stride = (unsigned)stride;
+            block = 256;
+            const uint64_t g = (A.nblocks + nb - 1) / nb;
+            grid = (unsigned)(g < (1u << 20) ? g : (1u << 20));
+            lds_bytes = (unsigned)(nb * stride * sizeof(float));
+        } else {
+            block = 64;  // one wave per 64 blocks
+            const uint64_t g = (A.nblocks + 63) / 64;
+            grid = (unsigned)(g < 65535 ? g : 65535);
+            if (path == 1) {
+                A.lds = priv_mode(1, B);
+                grid = priv_grid(grid);
+                lds_bytes = A.lds == 2 ? kTileBytes : 0;
             }
         }
     } else if (2ull * C * B * sizeof(float) <= kStagedLdsBytes) {
@@ -942,13 +1027,8 @@ int module_render(dsp_module *m, const void *params, uint32_t params_size, const
         block = 256;
         lds_bytes = (unsigned)(2ull * C * B * sizeof(float));
     }
-    if (m->stateless && A.lds) {
-        grid = priv_grid(grid);
-        A.lds = priv_mode(A.lds, B);
-        lds_bytes = A.lds == 2 ? kTileBytes : 0;
-    }
     MOD_HIP(hipModuleLaunchKernel(m->f_render, grid, 1, 1, block, 1, 1, lds_bytes, s, args, nullptr));
-    MOD_HIP(hipStreamSynchronize(s));  // the params blob is the caller's
+    MOD_HIP(hipEventRecord(m->use_ev, s));
     return DSP_OK;
 }
 
@@ -979,6 +1059,8 @@ int module_ir(dsp_module *m, const void *params, uint32_t params_size, float *co
     A.sr = sr;
     void *args[] = {&A};
     MOD_HIP(hipModuleLaunchKernel(m->f_callback, 1, 1, 1, 1, 1, 1, 0, s, args, nullptr));
+    if (!m->use_ev) MOD_HIP(hipEventCreateWithFlags(&m->use_ev, hipEventDisableTiming));
+    MOD_HIP(hipEventRecord(m->use_ev, s));
     return DSP_OK;
 }
 
