@@ -4,6 +4,7 @@
 // The generated translation unit is, in order:
 //   plugin_device.h          (as "plugin_header.h": device services)
 //   #pragma clang force_cuda_host_device begin
+//   #define annotate(...)     (the annotations are read from the text)
 //   the plugin source         (unchanged; its #include of plugin_header.h
 //                              hits the include guard)
 //   #pragma clang force_cuda_host_device end
@@ -115,6 +116,14 @@ __device__ static void dspb_stage_out(const dspb_render_args &A, unsigned long l
     }
 }
 typedef __attribute__((address_space(1))) float dspb_gfloat;
+// the Parameters / State blobs, read through a global-address-space pointer:
+// a copy the compiler forwards to the source then reads global memory, which
+// the callback's LDS stores cannot alias -- so a field the callback reads
+// every sample (gain_test's gain, IR_test's step) stays in a register
+// instead of being reloaded through a flat pointer after every store
+template <class T> __device__ static inline T dspb_from_global(const void *p) {
+    return *(const __attribute__((address_space(1))) T *)p;
+}
 // a generic pointer the compiler can prove is global memory (global_load /
 // global_store in the inlined callback, not flat ops that also wait on LDS)
 __device__ static inline float *dspb_global(float *p) { return (float *)(dspb_gfloat *)p; }
@@ -128,10 +137,10 @@ __device__ static inline float *dspb_global(float *p) { return (float *)(dspb_gf
 // lives in registers instead of scratch.
 template <unsigned CC>
 __device__ static void dspb_stateless(const dspb_render_args &A) {
-    State local = *(State *)A.S;
+    State local = dspb_from_global<State>(A.S);
     // a private copy: the callback's stores cannot alias it, so its fields
     // stay in registers instead of being reloaded after every store
-    Parameters prm = *(const Parameters *)A.P;
+    Parameters prm = dspb_from_global<Parameters>(A.P);
     const unsigned C = CC ? CC : A.C, t = threadIdx.x;
     for (unsigned long long b0 = (unsigned long long)blockIdx.x * 64; b0 < A.nblocks;
          b0 += (unsigned long long)gridDim.x * 64) {
@@ -180,7 +189,7 @@ __device__ static void dspb_stateful_lds(const dspb_render_args &A) {
     State *gst = (State *)A.S;
     // copies made by every thread (a few hundred bytes at most), used by
     // thread 0; the blobs are plain bytes to the host, as in the reference
-    Parameters prm = *(const Parameters *)A.P;
+    Parameters prm = dspb_from_global<Parameters>(A.P);
     State local = *gst;
     for (unsigned long long b = 0; b < A.nblocks; ++b) {
         float *cur = (b & 1) ? buf1 : buf0, *oth = (b & 1) ? buf0 : buf1;
@@ -200,109 +209,6 @@ __device__ static void dspb_stateful_lds(const dspb_render_args &A) {
     }
     dspb_stage_out(A, A.nblocks - 1, (A.nblocks - 1) & 1 ? buf1 : buf0, t, nt);
 }
-// no state, C B <= kPrivFloats: every lane renders its own block in a
-// private array. Scratch is lane-interleaved in hardware (dword k of every
-// lane of a wave is one 256-byte segment), so the callback's sample-by-sample
-// loads and stores are coalesced over the wave, where in place in HBM each
-// of them touches 64 different cache lines. The private copy also cannot
-// alias anything, so render_audio's copy in and the copy out pipeline freely
-// (float4 when B and the channel pointers allow).
-constexpr unsigned kPrivFloats = 1024;
-template <unsigned CC>
-__device__ static void dspb_stateless_private(const dspb_render_args &A) {
-    State local = *(State *)A.S;
-    Parameters prm = *(const Parameters *)A.P;
-    const unsigned B = A.B;
-    bool al = (B & 3) == 0;
-    for (unsigned c = 0; c < CC; ++c)
-        al = al && ((unsigned long long)A.out[c] & 15) == 0 &&
-             (c >= A.in_ch || ((unsigned long long)A.in[c] & 15) == 0);
-    float buf[kPrivFloats];
-    for (unsigned long long b = (unsigned long long)blockIdx.x * 64 + threadIdx.x; b < A.nblocks;
-         b += (unsigned long long)gridDim.x * 64) {
-        const unsigned long long i0 = b * B;
-        for (unsigned c = 0; c < CC; ++c) {
-            float *row = buf + c * B;
-            const dspb_gfloat *x = (const dspb_gfloat *)A.in[c < A.in_ch ? c : 0] + i0;
-            const unsigned long long left = A.L > i0 ? A.L - i0 : 0;
-            const unsigned m = c < A.in_ch ? (unsigned)(left < B ? left : B) : 0u;
-            if (al && m == B) {
-                for (unsigned s = 0; s < B; s += 4) {
-                    const float4 v = *(const __attribute__((address_space(1))) float4 *)(x + s);
-                    row[s] = v.x;
-                    row[s + 1] = v.y;
-                    row[s + 2] = v.z;
-                    row[s + 3] = v.w;
-                }
-            } else {
-                for (unsigned s = 0; s < B; ++s) row[s] = s < m ? x[s] : 0.0f;
-            }
-        }
-        float *ptrs[CC];
-        for (unsigned c = 0; c < CC; ++c) ptrs[c] = buf + c * B;
-        audio_callback(prm, local, ptrs, CC, B, A.sr);
-        for (unsigned c = 0; c < CC; ++c) {
-            const float *row = buf + c * B;
-            dspb_gfloat *o = (dspb_gfloat *)A.out[c] + i0;
-            if (al) {
-                for (unsigned s = 0; s < B; s += 4)
-                    *(__attribute__((address_space(1))) float4 *)(o + s) =
-                        make_float4(row[s], row[s + 1], row[s + 2], row[s + 3]);
-            } else {
-                for (unsigned s = 0; s < B; ++s) o[s] = row[s];
-            }
-        }
-    }
-}
-// the private path with B a multiple of 64: the wave moves its 64 blocks
-// between HBM and the lanes' private arrays through a 64 x 65 LDS tile, so
-// every global load and store is one contiguous 256-byte row (a lane's own
-// block is 2 KB away from its neighbours': per-lane float4 copies touch 64
-// cache lines per instruction)
-template <unsigned CC>
-__device__ static void dspb_stateless_tiled(const dspb_render_args &A) {
-    extern __shared__ float dspb_lbuf[];
-    State local = *(State *)A.S;
-    Parameters prm = *(const Parameters *)A.P;
-    const unsigned B = A.B, t = threadIdx.x;
-    float buf[kPrivFloats];
-    for (unsigned long long b0 = (unsigned long long)blockIdx.x * 64; b0 < A.nblocks;
-         b0 += (unsigned long long)gridDim.x * 64) {
-        const unsigned nb = (unsigned)(A.nblocks - b0 < 64 ? A.nblocks - b0 : 64);
-        for (unsigned c = 0; c < CC; ++c) {
-            const bool has = c < A.in_ch;
-            const dspb_gfloat *x = (const dspb_gfloat *)A.in[has ? c : 0];
-            for (unsigned s0 = 0; s0 < B; s0 += 64) {
-#pragma unroll 16
-                for (unsigned bi = 0; bi < 64; ++bi) {
-                    const unsigned long long i = (b0 + bi) * B + s0 + t;
-                    dspb_lbuf[bi * 65 + t] = (has && bi < nb && i < A.L) ? x[i] : 0.0f;
-                }
-                __syncthreads();
-#pragma unroll
-                for (unsigned j = 0; j < 64; ++j) buf[c * B + s0 + j] = dspb_lbuf[t * 65 + j];
-                __syncthreads();
-            }
-        }
-        if (t < nb) {
-            float *ptrs[CC];
-            for (unsigned c = 0; c < CC; ++c) ptrs[c] = buf + c * B;
-            audio_callback(prm, local, ptrs, CC, B, A.sr);
-        }
-        for (unsigned c = 0; c < CC; ++c) {
-            dspb_gfloat *o = (dspb_gfloat *)A.out[c];
-            for (unsigned s0 = 0; s0 < B; s0 += 64) {
-#pragma unroll
-                for (unsigned j = 0; j < 64; ++j) dspb_lbuf[t * 65 + j] = buf[c * B + s0 + j];
-                __syncthreads();
-#pragma unroll 16
-                for (unsigned bi = 0; bi < 64; ++bi)
-                    if (bi < nb) o[(b0 + bi) * B + s0 + t] = dspb_lbuf[bi * 65 + t];
-                __syncthreads();
-            }
-        }
-    }
-}
 // no state, LDS blocks: a workgroup renders lds_nb consecutive blocks per
 // round.  render_audio's copy (audio.cpp:13-175: the file at the cursor,
 // zeros past EOF and for the channels the file lacks) stages them into LDS
@@ -316,8 +222,8 @@ __device__ static void dspb_stateless_tiled(const dspb_render_args &A) {
 template <unsigned CC, unsigned BB>
 __device__ static void dspb_stateless_lds(const dspb_render_args &A) {
     extern __shared__ float dspb_lbuf[];
-    State local = *(State *)A.S;
-    Parameters prm = *(const Parameters *)A.P;
+    State local = dspb_from_global<State>(A.S);
+    Parameters prm = dspb_from_global<Parameters>(A.P);
     const unsigned C = CC ? CC : A.C, B = BB ? BB : A.B, NB = A.lds_nb, SB = A.lds_stride;
     const unsigned t = threadIdx.x, nt = blockDim.x, wave = t >> 6, lane = t & 63u;
     const unsigned per = NB / 4;  // blocks per wave
@@ -326,27 +232,37 @@ __device__ static void dspb_stateless_lds(const dspb_render_args &A) {
         const unsigned nb = (unsigned)(A.nblocks - b0 < NB ? A.nblocks - b0 : NB);
         const unsigned long long i0 = b0 * B;
         const unsigned long long lim = A.L > i0 ? A.L - i0 : 0;  // file samples left at i0
+        const unsigned n = nb * B;
         for (unsigned c = 0; c < C; ++c) {
             const dspb_gfloat *x = (const dspb_gfloat *)A.in[c < A.in_ch ? c : 0] + i0;
             const unsigned long long m = c < A.in_ch ? lim : 0;
-            const unsigned n = nb * B;
-            unsigned j = t;
-            for (; j + 3 * nt < n; j += 4 * nt) {  // four loads in flight per thread
-                const float v0 = j < m ? x[j] : 0.0f, v1 = j + nt < m ? x[j + nt] : 0.0f;
-                const float v2 = j + 2 * nt < m ? x[j + 2 * nt] : 0.0f, v3 = j + 3 * nt < m ? x[j + 3 * nt] : 0.0f;
-                unsigned q;
-                q = j / B;
-                dspb_lbuf[q * SB + c * B + (j - q * B)] = v0;
-                q = (j + nt) / B;
-                dspb_lbuf[q * SB + c * B + (j + nt - q * B)] = v1;
-                q = (j + 2 * nt) / B;
-                dspb_lbuf[q * SB + c * B + (j + 2 * nt - q * B)] = v2;
-                q = (j + 3 * nt) / B;
-                dspb_lbuf[q * SB + c * B + (j + 3 * nt - q * B)] = v3;
-            }
-            for (; j < n; j += nt) {
-                const unsigned q = j / B;
-                dspb_lbuf[q * SB + c * B + (j - q * B)] = j < m ? x[j] : 0.0f;
+            float *row = dspb_lbuf + c * B;
+            if (m >= n && (B & 3) == 0 && (((unsigned long long)x) & 15) == 0) {
+                // the whole round is inside the file: 16-byte loads, two in
+                // flight per thread (a float4 never crosses a block: 4 | B)
+                const __attribute__((address_space(1))) float4 *x4 =
+                    (const __attribute__((address_space(1))) float4 *)x;
+                unsigned j = 4 * t;
+                for (; j + 4 * nt < n; j += 8 * nt) {
+                    const float4 v0 = x4[j / 4], v1 = x4[(j + 4 * nt) / 4];
+                    unsigned q = j / B;
+                    float *d = row + q * SB + (j - q * B);
+                    d[0] = v0.x, d[1] = v0.y, d[2] = v0.z, d[3] = v0.w;
+                    q = (j + 4 * nt) / B;
+                    d = row + q * SB + (j + 4 * nt - q * B);
+                    d[0] = v1.x, d[1] = v1.y, d[2] = v1.z, d[3] = v1.w;
+                }
+                for (; j < n; j += 4 * nt) {
+                    const float4 v0 = x4[j / 4];
+                    const unsigned q = j / B;
+                    float *d = row + q * SB + (j - q * B);
+                    d[0] = v0.x, d[1] = v0.y, d[2] = v0.z, d[3] = v0.w;
+                }
+            } else {  // EOF in the round, or no file channel: zeros past it
+                for (unsigned j = t; j < n; j += nt) {
+                    const unsigned q = j / B;
+                    row[q * SB + (j - q * B)] = j < m ? x[j] : 0.0f;
+                }
             }
         }
         __syncthreads();
@@ -360,33 +276,39 @@ __device__ static void dspb_stateless_lds(const dspb_render_args &A) {
         __syncthreads();
         for (unsigned c = 0; c < C; ++c) {
             dspb_gfloat *o = (dspb_gfloat *)A.out[c] + i0;
-            const unsigned n = nb * B;
-            for (unsigned j = t; j < n; j += nt) {
-                const unsigned q = j / B;
-                o[j] = dspb_lbuf[q * SB + c * B + (j - q * B)];
+            const float *row = dspb_lbuf + c * B;
+            if ((B & 3) == 0 && (((unsigned long long)o) & 15) == 0) {
+                __attribute__((address_space(1))) float4 *o4 = (__attribute__((address_space(1))) float4 *)o;
+                for (unsigned j = 4 * t; j < n; j += 4 * nt) {
+                    const unsigned q = j / B;
+                    const float *d = row + q * SB + (j - q * B);
+                    o4[j / 4] = make_float4(d[0], d[1], d[2], d[3]);
+                }
+            } else {
+                for (unsigned j = t; j < n; j += nt) {
+                    const unsigned q = j / B;
+                    o[j] = row[q * SB + (j - q * B)];
+                }
             }
         }
         __syncthreads();
     }
 }
+// the LDS-blocks path as its own kernel: four waves, two workgroups per CU
+extern "C" __global__ __launch_bounds__(256) void dspb_render_lds(dspb_render_args A) {
+    if (!__is_empty(State)) return;
+    if (A.C == 2 && A.B == 512) dspb_stateless_lds<2, 512>(A);
+    else if (A.C == 2 && A.B == 256) dspb_stateless_lds<2, 256>(A);
+    else if (A.C == 2 && A.B == 1024) dspb_stateless_lds<2, 1024>(A);
+    else if (A.C == 1 && A.B == 512) dspb_stateless_lds<1, 512>(A);
+    else if (A.C == 1) dspb_stateless_lds<1, 0>(A);
+    else if (A.C == 2) dspb_stateless_lds<2, 0>(A);
+    else dspb_stateless_lds<0, 0>(A);
+}
 extern "C" __global__ void dspb_render(dspb_render_args A) {
     extern __shared__ float dspb_lbuf[];
     if (__is_empty(State)) {
-        if (A.lds == 3) {
-            if (A.C == 2 && A.B == 512) dspb_stateless_lds<2, 512>(A);
-            else if (A.C == 2 && A.B == 256) dspb_stateless_lds<2, 256>(A);
-            else if (A.C == 2 && A.B == 1024) dspb_stateless_lds<2, 1024>(A);
-            else if (A.C == 1 && A.B == 512) dspb_stateless_lds<1, 512>(A);
-            else if (A.C == 1) dspb_stateless_lds<1, 0>(A);
-            else if (A.C == 2) dspb_stateless_lds<2, 0>(A);
-            else dspb_stateless_lds<0, 0>(A);
-            return;
-        }
-        if (A.lds == 2 && A.C == 1) dspb_stateless_tiled<1>(A);
-        else if (A.lds == 2 && A.C == 2) dspb_stateless_tiled<2>(A);
-        else if (A.lds == 1 && A.C == 1) dspb_stateless_private<1>(A);
-        else if (A.lds == 1 && A.C == 2) dspb_stateless_private<2>(A);
-        else if (A.C == 1) dspb_stateless<1>(A);
+        if (A.C == 1) dspb_stateless<1>(A);
         else if (A.C == 2) dspb_stateless<2>(A);
         else dspb_stateless<0>(A);
     } else if (!A.lds) {  // stateful, blocks too large for LDS: in order, one thread
@@ -433,6 +355,7 @@ struct dsp_module {
     dsp_descriptor *desc = nullptr;  // from the code object (NULL for code without one)
     int device = -1;
     hipModule_t mod = nullptr;
+    hipFunction_t f_render_lds = nullptr;  // NULL for code objects compiled before it existed
     hipFunction_t f_sizes = nullptr, f_defaults = nullptr, f_init = nullptr, f_render = nullptr,
                   f_callback = nullptr;
     uint32_t params_size = 0, state_size = 0;
@@ -534,7 +457,13 @@ int dsp_module_compile(const char *source, const char *name, void **code, uint64
     std::string tu;
     tu += "#include \"plugin_header.h\"\n";
     tu += "#pragma clang force_cuda_host_device begin\n";
+    // the parameter annotations are read from the source text (descriptor.cpp);
+    // compiled, each access to an annotated field would go through
+    // llvm.ptr.annotation, an opaque pointer that keeps the field in memory
+    // (a reload after every LDS store of the callback): drop the attribute
+    tu += "#define annotate(...)\n#define __annotate__(...)\n";
     tu += "#include \"dspb_plugin_source.cpp\"\n";
+    tu += "#undef annotate\n#undef __annotate__\n";
     tu += "#pragma clang force_cuda_host_device end\n";
     std::string note;
     tu += dspb::desc::generate(source, kPluginDeviceSrc, &note);
@@ -625,6 +554,10 @@ int dsp_module_load(const void *code, uint64_t code_size, int device, dsp_module
                                                         {&m->f_callback, "dspb_callback"}};
     for (auto &f : fs)
         if ((e = hipModuleGetFunction(f.f, m->mod, f.n)) != hipSuccess) return fail(dspb::hip_fail(e, f.n));
+    if (hipModuleGetFunction(&m->f_render_lds, m->mod, "dspb_render_lds") != hipSuccess) {
+        (void)hipGetLastError();
+        m->f_render_lds = nullptr;
+    }
     unsigned *d_o = nullptr;
     if ((e = hipMalloc(&d_o, 4 * sizeof(unsigned))) != hipSuccess) return fail(dspb::hip_fail(e, "hipMalloc"));
     void *args[] = {&d_o};
@@ -880,40 +813,17 @@ int dsp_module_read_state(const dsp_module *m, void *state) {
 
 namespace dspb {
 
-constexpr uint64_t kPrivFloatsHost = 1024;  // = kPrivFloats in kDriver
-// DSPB_STATELESS_PRIVATE=0 / 1 forces the in-place wave path / the private
-// path for eligible stateless renders (tools/generic_probe.py A/B); -1: timed
+// DSPB_STATELESS_PATH=0 / 3 forces the in-place wave path / the LDS-blocks
+// path for a stateless plugin (tools/generic_probe.py A/B); -1: by size
 static int stateless_path_forced() {
     static const int v = [] {
         const char *e = std::getenv("DSPB_STATELESS_PATH");
-        return e && (e[0] == '0' || e[0] == '1' || e[0] == '3') ? e[0] - '0' : -1;
+        return e && (e[0] == '0' || e[0] == '3') ? e[0] - '0' : -1;
     }();
     return v;
 }
 // the LDS-blocks path: LDS per workgroup round (two workgroups per CU)
 constexpr uint64_t kLdsRoundBytes = 76 * 1024;
-
-// the private path's grid: DSPB_PRIV_WAVES=<waves per CU> caps it (the
-// lanes loop over blocks), bounding the scratch footprint in flight
-static unsigned priv_grid(unsigned grid) {
-    static const unsigned cap = [] {
-        const char *e = std::getenv("DSPB_PRIV_WAVES");
-        const unsigned long k = e ? std::strtoul(e, nullptr, 10) : 0;
-        return k ? (unsigned)(256 * k) : 0u;
-    }();
-    return cap && cap < grid ? cap : grid;
-}
-
-// the private path's driver mode: 2 (LDS-tiled copies) when B is a multiple
-// of 64, else 1 (per-lane copies); DSPB_PRIV_TILED=0 keeps mode 1
-constexpr unsigned kTileBytes = 64 * 65 * sizeof(float);
-static unsigned priv_mode(unsigned mode, uint32_t B) {
-    static const bool tiled = [] {
-        const char *e = std::getenv("DSPB_PRIV_TILED");
-        return !(e && e[0] == '0');
-    }();
-    return mode && tiled && B % 64 == 0 ? 2u : mode;
-}
 
 // the caller's Parameters blob -> the module's device Parameters, stream
 // ordered: through a pinned staging copy (reused once the previous upload
@@ -992,34 +902,27 @@ int module_render(dsp_module *m, const void *params, uint32_t params_size, const
     void *args[] = {&A};
     unsigned grid = 1, block = 1, lds_bytes = 0;
     if (m->stateless) {
-        // default: the LDS-blocks path (mode 3) when a round of at least 4
-        // blocks fits the per-workgroup LDS budget, else the in-place wave
-        // path (mode 0); DSPB_STATELESS_PATH=0/1/3 forces one (A/B: 1 = the
-        // private-array path, tiled when B % 64 == 0)
+        // default: the LDS-blocks path (dspb_render_lds) when a round of at
+        // least 4 blocks fits the per-workgroup LDS budget, else the
+        // in-place wave path; DSPB_STATELESS_PATH=0/3 forces one
         const uint64_t stride = (uint64_t)C * B + 1;
         const uint64_t nb = std::min<uint64_t>(64, kLdsRoundBytes / (stride * sizeof(float)) / 4 * 4);
         int path = stateless_path_forced();
         if (path < 0) path = nb >= 4 ? 3 : 0;
-        if (path == 3 && nb < 4) path = 0;
-        if (path == 1 && !(C <= 2 && 1ull * C * B <= kPrivFloatsHost)) path = 0;
+        if (path == 3 && (nb < 4 || !m->f_render_lds)) path = 0;
         if (path == 3) {
             A.lds = 3;
             A.lds_nb = (unsigned)nb;
             A.lds_stride = (unsigned)stride;
-            block = 256;
             const uint64_t g = (A.nblocks + nb - 1) / nb;
-            grid = (unsigned)(g < (1u << 20) ? g : (1u << 20));
-            lds_bytes = (unsigned)(nb * stride * sizeof(float));
-        } else {
-            block = 64;  // one wave per 64 blocks
-            const uint64_t g = (A.nblocks + 63) / 64;
-            grid = (unsigned)(g < 65535 ? g : 65535);
-            if (path == 1) {
-                A.lds = priv_mode(1, B);
-                grid = priv_grid(grid);
-                lds_bytes = A.lds == 2 ? kTileBytes : 0;
-            }
+            MOD_HIP(hipModuleLaunchKernel(m->f_render_lds, (unsigned)(g < (1u << 20) ? g : (1u << 20)), 1, 1, 256, 1, 1,
+                                          (unsigned)(nb * stride * sizeof(float)), s, args, nullptr));
+            MOD_HIP(hipEventRecord(m->use_ev, s));
+            return DSP_OK;
         }
+        block = 64;  // one wave per 64 blocks
+        const uint64_t g = (A.nblocks + 63) / 64;
+        grid = (unsigned)(g < 65535 ? g : 65535);
     } else if (2ull * C * B * sizeof(float) <= kStagedLdsBytes) {
         // stateful: 4 waves, the block double-buffer in LDS (the callback's
         // loads and stores hit LDS, the copies run on 192 lanes beside it)

@@ -111,29 +111,28 @@ def test_stateless_plugin_staged_edges(torch_cuda, oracle, name, B):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", ["gain_test", "IR_test", "handmade_test"])
-# >= 32768 blocks of <= 1024 mono/stereo samples: the private-array path,
-# timed against the in-place wave path on the shape's first render.
-# (Cin, C, B): mono file into stereo with B = 100 (no float4: B % 4 != 0),
-# stereo B = 512 (float4 copies), mono B = 1024 (the largest block it takes)
-@pytest.mark.parametrize("cin,C,B", [(1, 2, 100), (2, 2, 512), (1, 1, 1024)])
-def test_stateless_plugin_private_path(torch_cuda, oracle, name, cin, C, B):
+# long files through the LDS-blocks path (dspb_render_lds): (Cin, C, B) =
+# mono file into stereo with B = 100 (scalar staging: B % 4 != 0), stereo
+# B = 512 and mono B = 1024 (constant-shape instantiations, float4 staging),
+# 4 channels of B = 384 (the generic-shape instantiation); ragged last block
+@pytest.mark.parametrize("cin,C,B", [(1, 2, 100), (2, 2, 512), (1, 1, 1024), (3, 4, 384)])
+def test_stateless_plugin_lds_path(torch_cuda, oracle, name, cin, C, B):
     if not have(name):
         pytest.skip("oracle/_ref not built")
     mod = load(name)
     params = mod.default_parameters()
     mod.initialize_state(params, C, 48000.0)
     ref = oracle.RefPlugin(name, C, 48000.0)
-    L = 32768 * B + 7 * B // 3  # a ragged last block
+    L = 3000 * B + 7 * B // 3  # a ragged last block
     x = np.random.default_rng(6).uniform(-1, 1, (cin, L)).astype(np.float32)
     want = oracle.render_offline([x[c] for c in range(cin)], C, B, 48000.0, ref.as_oracle())
     xg = torch_cuda.from_numpy(x).cuda()
-    # the first render of the shape runs both paths (the later one's output is
-    # returned), the second the one the module kept
     for _ in range(2):
         got = d.render_offline(xg, C, B, 48000.0, mod.plugin(params, name)).cpu().numpy()
         assert np.array_equal(got, want)
     if cin == C:
-        # in place (the file is the output buffer): never timed twice
+        # in place (the file is the output buffer): a round stages all its
+        # blocks into LDS before it stores any
         buf = torch_cuda.zeros((C, (L + B - 1) // B * B), dtype=torch_cuda.float32, device="cuda")
         buf[:, :L] = xg
         d.render_offline(buf, C, B, 48000.0, mod.plugin(params, name), out=buf, L_file=L)
