@@ -60,12 +60,16 @@ def parse():
                     help="fir1024: 0 auto (overlap-save), 1 direct form, 2 overlap-save")
     ap.add_argument("--workload", default="headline",
                     choices=["headline", "stft96k", "ch96k", "gain10min", "fir1024", "wav16", "wav24", "ir",
-                             "generic"],
+                             "generic", "generic_stft"],
                     help="headline = IR_test + STFT 48 kHz (the metric); stft96k = BASELINE cfg 4 "
                          "(STFT of 1 h stereo 96 kHz from HBM); gain10min = cfg 2 render; "
                          "wav16 / wav24 = GPU decode of a 1 h stereo int16 / int24 WAV payload; "
                          "ch96k = BASELINE cfg 5: one 96 kHz channel per GPU through IR_test + STFT; "
-                         "ir = compute_IR + fft_perform_and_get_magnitude latency (one 8192-pt frame per call)")
+                         "ir = compute_IR + fft_perform_and_get_magnitude latency (one 8192-pt frame per call); "
+                         "generic = a reference plugin source through the generic driver (render only); "
+                         "generic_stft = the same + the 8192-pt STFT (render and STFT pipelined)")
+    ap.add_argument("--plugin", default=None, choices=["gain_test", "IR_test"],
+                    help="generic / generic_stft: the reference plugin source (default gain_test / IR_test)")
     return ap.parse_args()
 
 
@@ -290,9 +294,12 @@ def main():
         return xs[rot[0]]
     nb = d.num_blocks(L_in, B)
     F = d.stft_frames(nb * B if wl in ("headline", "ch96k") else L_in, N_FFT, HOP)
-    out = (torch.empty((CH, nb * B), device=dev) if wl in ("headline", "ch96k", "gain10min", "fir1024", "generic")
-           else None)
-    mag = torch.empty((CH, max(F, 1), K_BINS), device=dev) if wl in ("headline", "stft96k", "ch96k") else None
+    out = (torch.empty((CH, nb * B), device=dev)
+           if wl in ("headline", "ch96k", "gain10min", "fir1024", "generic", "generic_stft") else None)
+    if wl == "generic_stft":
+        F = d.stft_frames(nb * B, N_FFT, HOP)
+    mag = (torch.empty((CH, max(F, 1), K_BINS), device=dev)
+           if wl in ("headline", "stft96k", "ch96k", "generic_stft") else None)
     plugin = d.Plugin.ir_test(0.9, 0.002) if wl in ("headline", "ch96k") else d.Plugin.gain_test(0.2)
     stream = torch.cuda.current_stream(dev)
     soff = sh.start
@@ -348,24 +355,35 @@ def main():
         kname = "render_vec_kernel<Gain>"
         alg_bytes = CH * L_in * 8  # read + write
         alg_desc = "C*L*(4 + 4) B (read + write)"
-    elif wl == "generic":
-        # the reference's gain_test.cpp compiled by the
-        # product's plugin compiler (hiprtc -> gfx950, oracle/_ref/mod_*.co,
-        # built by oracle/make_modules.py) and run by the generic driver
-        with open(os.path.join(REPO, "oracle", "_ref", "mod_gain_test.co"), "rb") as f:
+    elif wl in ("generic", "generic_stft"):
+        # a reference plugin source (gain_test.cpp /
+        # IR_test.cpp) compiled by the product's plugin compiler (hiprtc ->
+        # gfx950, dsp-bench_amd/modules/mod_*.co, built by
+        # tools/make_plugin_modules.py) and run by the generic driver
+        pname = args.plugin or ("gain_test" if wl == "generic" else "IR_test")
+        with open(os.path.join(REPO, "dsp-bench_amd", "modules", f"mod_{pname}.co"), "rb") as f:
             gmod = d.module.Module(f.read())
         gparams = gmod.default_parameters()
         gmod.initialize_state(gparams, CH, float(sr))
-        gplug = gmod.plugin(gparams, "gain_test")
-        plug_name = "gain_test.cpp (DSP_PLUGIN_GENERIC, compiled from the reference source)"
-
-        def step():
-            d.render_offline(x, CH, B, float(sr), gplug, out=out)
-        workload = (f"gain_test.cpp via the generic plugin driver (B=512), {minutes:g} min of 48 kHz "
-                    "stereo per GPU")
-        kname = "dspb_render (generic driver, hiprtc module; step time incl. the call's stream sync)"
-        alg_bytes = CH * L_in * 8  # read + write
-        alg_desc = "C*L*(4 + 4) B (read + write)"
+        gplug = gmod.plugin(gparams, pname)
+        plug_name = f"{pname}.cpp (DSP_PLUGIN_GENERIC, compiled unchanged from the reference source)"
+        if wl == "generic":
+            def step():
+                d.render_offline(x, CH, B, float(sr), gplug, out=out)
+            workload = (f"{pname}.cpp via the generic plugin driver (B=512), {minutes:g} min of 48 kHz "
+                        "stereo per GPU")
+            kname = "dspb_render_lds (generic driver, hiprtc module)"
+            alg_desc = "C*L*(4 + 4) B (read + write)"
+        else:
+            def step():
+                d.render_stft(x, CH, B, float(sr), gplug, N=N_FFT, H=HOP, window=d.DSP_WIN_HANN,
+                              K=K_BINS, out=out, mag=mag)
+            workload = (f"{pname}.cpp via the generic plugin driver (B=512) + 8192-pt Hann STFT, hop 4096, "
+                        f"4097 bins, {minutes:g} min of 48 kHz stereo per GPU")
+            kname = ("dspb_render_lds (generic driver) + stft8192_pk<memory>, pipelined in 32 MiB chunks "
+                     "on two streams (one region, dsp_render_stft)")
+            alg_desc = ("C*L*(4 + 4) + C*F*4K B (file read + render write + |X| write; the STFT's read of "
+                        "the render is served by the Infinity Cache)")
     else:
         bits = 16 if wl == "wav16" else 24
         pay = torch.randint(0, 256, (CH * L_in * bits // 8,), dtype=torch.uint8, device=dev, generator=g)
@@ -507,7 +525,7 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and wl == "headline":
         cpu = cpu_baseline(args.cpu_seconds)
-    elif rank == 0 and world == 1 and not args.no_cpu_baseline and wl == "generic":
+    elif rank == 0 and world == 1 and not args.no_cpu_baseline and wl == "generic" and not args.plugin:
         cpu = cpu_baseline_generic(min(args.cpu_seconds, 5.0))
 
     if rank == 0:
@@ -524,7 +542,7 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": ("synthetic (uniform noise WAV in HBM; IR_test output is input-independent)"
-                     if wl in ("headline", "ch96k") else
+                     if wl in ("headline", "ch96k") or (wl == "generic_stft" and "IR_test" in plug_name) else
                      f"synthetic (uniform noise in HBM; {NX} input copies used in rotation, past the Infinity Cache)"
                      if NX > 1 else "synthetic (uniform noise in HBM)"),
             "config": {
@@ -571,8 +589,10 @@ def main():
                 "limiter": ("package power: the settled kernel draws the 1400 W cap at sclk ~1.8 GHz "
                             "(2.38 GHz without its stores); profiles/r01_power_ablation"
                             if wl in ("headline", "ch96k") else
-                            "one lane per block: the plugin callback's 1024 dependent load -> store steps "
-                            "(DESIGN 4.6)" if wl == "generic" else None),
+                            "one lane per block: the plugin callback runs serially over its block in LDS, "
+                            "16 blocks per 64 KB workgroup round (DESIGN 4.6)" if wl == "generic" else
+                            "render (LDS-capacity-bound callbacks) overlapped with the power-capped FFT "
+                            "(DESIGN 4.6)" if wl == "generic_stft" else None),
             }),
             "cpu_baseline": cpu,
         }

@@ -10,6 +10,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <algorithm>
 #include <map>
@@ -62,6 +63,11 @@ struct DeviceRes {
     std::map<std::pair<void *, int>, std::pair<float *, size_t>> scratch;  // per (stream, slot)
     std::vector<FirTaps> fir;                                  // FIR filters seen (plugin_map)
     float *delta = nullptr;  // 2048 floats: 1, 0, 0, ... (compute_IR's impulse, read-only)
+    struct Aux {  // a second stream beside a caller's stream + the events that order them
+        hipStream_t s2 = nullptr;
+        hipEvent_t ev_chunk = nullptr, ev_join = nullptr;
+    };
+    std::map<void *, Aux> aux;  // per caller stream
 };
 
 static std::mutex g_mu;
@@ -216,6 +222,20 @@ static int get_scratch(int dev, hipStream_t s, size_t bytes, float **out, int sl
     return DSP_OK;
 }
 
+// The STFT stream of the pipelined GENERIC render + STFT: one per (device,
+// caller stream), non-blocking, with its two ordering events.
+static int get_aux(int dev, hipStream_t s, DeviceRes::Aux *out) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    DeviceRes::Aux &a = g_res[dev].aux[(void *)s];
+    if (!a.s2) {
+        DSPB_HIP(hipStreamCreateWithFlags(&a.s2, hipStreamNonBlocking));
+        DSPB_HIP(hipEventCreateWithFlags(&a.ev_chunk, hipEventDisableTiming));
+        DSPB_HIP(hipEventCreateWithFlags(&a.ev_join, hipEventDisableTiming));
+    }
+    *out = a;
+    return DSP_OK;
+}
+
 // ---------------------------------------------------------------------------
 // optional per-launch timing of the dominant kernel (HIP events on the
 // launch stream), read back by dsp_kernel_timing(); used by bench.py
@@ -253,8 +273,13 @@ static int launch_stft(const Stft8kArgs &A, uint32_t C, bool fused, hipStream_t 
 
 static std::vector<TimedLaunch> g_timed;
 
+// set while a call times its launches as one region (the pipelined GENERIC
+// render + STFT): the launches inside record nothing of their own
+static thread_local bool tl_timing_outer = false;
+
 static int timing_begin(hipStream_t s, TimedLaunch *t) {
-    if (!g_timing) return DSP_OK;
+    t->start = t->stop = nullptr;
+    if (!g_timing || tl_timing_outer) return DSP_OK;
     DSPB_HIP(hipEventCreate(&t->start));
     DSPB_HIP(hipEventCreate(&t->stop));
     DSPB_HIP(hipEventRecord(t->start, s));
@@ -262,7 +287,7 @@ static int timing_begin(hipStream_t s, TimedLaunch *t) {
 }
 
 static int timing_end(hipStream_t s, TimedLaunch *t, uint64_t bytes) {
-    if (!g_timing) return DSP_OK;
+    if (!t->start) return DSP_OK;
     DSPB_HIP(hipEventRecord(t->stop, s));
     t->bytes = bytes;
     std::lock_guard<std::mutex> lk(g_mu);
@@ -619,6 +644,75 @@ static int stft_device(const float *const *in, uint32_t C, uint64_t L, uint32_t 
     return DSP_OK;
 }
 
+// GENERIC render + STFT, pipelined through the Infinity Cache.  The plugin's
+// own callback (hiprtc module) renders the file in chunks of ~kPipeBytes on
+// the caller's stream; the STFT of the frames a chunk completes runs on a
+// second stream behind it, while the next chunk renders.  A chunk's render is
+// still resident in the 256 MiB last-level cache when its STFT reads it, so
+// the render is written to HBM once and not read back from it; the
+// memory-bound render and the VALU-bound FFT overlap on the CUs.  Stream
+// ordered on s: s2 starts behind everything queued on s, and s waits for the
+// last STFT before the call's later work.  Chunk boundaries are multiples of
+// B, so every callback sees whole blocks in order (a plugin with State
+// continues across chunks on s).
+constexpr uint64_t kPipeBytes = 32ull << 20;  // render bytes per chunk (all channels)
+
+// DSPB_PIPE_CHUNK_BYTES overrides the chunk size (tests: many chunks on a
+// short file; tuning)
+static uint64_t pipe_bytes() {
+    const char *e = std::getenv("DSPB_PIPE_CHUNK_BYTES");
+    const uint64_t v = e ? std::strtoull(e, nullptr, 10) : 0;
+    return v ? v : kPipeBytes;
+}
+
+static int generic_render_stft(const float *const *in, uint32_t in_ch, uint64_t L, float *const *out, uint32_t C,
+                               uint32_t B, const SampleMap &map, uint32_t N, uint32_t H, int window, uint32_t K,
+                               float *const *mag, uint64_t ld, uint64_t goff, int dev, hipStream_t s) {
+    const uint64_t nblocks = (L + B - 1) / B, Lr = nblocks * B;
+    const uint64_t F = dsp_stft_frame_count(Lr, N, H);
+    const uint64_t per = std::max<uint64_t>(1, pipe_bytes() / (4ull * C * B));  // blocks per chunk
+    ::dsp_module *mod = (::dsp_module *)map.module;
+    if (F == 0 || nblocks <= per) {  // one chunk: render, then the STFT, on s
+        int st = module_render(mod, map.gparams, map.gparams_size, in, in_ch, L, out, C, B, map.sr, goff, s);
+        return st ? st : stft_device(out, C, Lr, N, H, window, K, mag, ld, dev, s);
+    }
+    DeviceRes::Aux ax;
+    int st = get_aux(dev, s, &ax);
+    if (st) return st;
+    DSPB_HIP(hipEventRecord(ax.ev_chunk, s));  // s2 behind the caller's earlier work
+    DSPB_HIP(hipStreamWaitEvent(ax.s2, ax.ev_chunk, 0));
+    std::vector<const float *> ci(in_ch);
+    std::vector<float *> co(C), cm(C);
+    std::vector<const float *> ro(C);
+    uint64_t f0 = 0;  // frames done
+    for (uint64_t b0 = 0; b0 < nblocks; b0 += per) {
+        const uint64_t nb = std::min(per, nblocks - b0), i0 = b0 * B;
+        // the chunk's file samples (the last chunk holds the file's end: i0 < L)
+        const uint64_t Lc = std::min<uint64_t>(L - i0, nb * B);
+        for (uint32_t c = 0; c < in_ch; ++c) ci[c] = in[c] + i0;
+        for (uint32_t c = 0; c < C; ++c) co[c] = out[c] + i0;
+        if ((st = module_render(mod, map.gparams, map.gparams_size, ci.data(), in_ch, Lc, co.data(), C, B, map.sr,
+                                goff + i0, s, b0 > 0)))
+            return st;
+        DSPB_HIP(hipEventRecord(ax.ev_chunk, s));
+        // frames inside [0, rendered): f < frame_count(rendered)
+        const uint64_t done = i0 + nb * B;
+        const uint64_t f1 = b0 + nb == nblocks ? F : dsp_stft_frame_count(done, N, H);
+        if (f1 <= f0) continue;
+        DSPB_HIP(hipStreamWaitEvent(ax.s2, ax.ev_chunk, 0));
+        for (uint32_t c = 0; c < C; ++c) {
+            ro[c] = out[c] + f0 * H;
+            cm[c] = mag[c] + f0 * ld;
+        }
+        if ((st = stft_device(ro.data(), C, (f1 - f0 - 1) * H + N, N, H, window, K, cm.data(), ld, dev, ax.s2)))
+            return st;
+        f0 = f1;
+    }
+    DSPB_HIP(hipEventRecord(ax.ev_join, ax.s2));
+    DSPB_HIP(hipStreamWaitEvent(s, ax.ev_join, 0));
+    return DSP_OK;
+}
+
 }  // namespace dspb
 
 using namespace dspb;
@@ -905,7 +999,20 @@ int dsp_render_stft(const float *const *in, uint32_t in_channels, uint64_t L,
     for (uint32_t c = 0; c < C; ++c) fused = fused && aligned(dout[c], 8);
     for (uint32_t c = 0; c < in_channels; ++c) fused = fused && aligned(din[c], 8);
 
-    if (!fused) {
+    if (!fused && map.kind == MapKind::Generic) {
+        // the plugin's own callback, render and STFT pipelined (generic_render_stft),
+        // timed as one region: file read + render write + magnitude write
+        TimedLaunch tl{};
+        if ((st = timing_begin(s, &tl))) return st;
+        tl_timing_outer = true;
+        st = generic_render_stft(din.data(), in_channels, L, dout.data(), C, B, map, N, H, window, K, dmag.data(),
+                                 ld, goff, g.dev, s);
+        tl_timing_outer = false;
+        if (st) return st;
+        const uint64_t bytes = (uint64_t)std::min(in_channels, C) * L * 4 + (uint64_t)C * Lr * 4 +
+                               (uint64_t)C * F * K * 4;
+        if ((st = timing_end(s, &tl, bytes))) return st;
+    } else if (!fused) {
         st = render_device(din.data(), in_channels, L, dout.data(), C, B, map, 0, goff, s);
         if (st) return st;
         st = stft_device(dout.data(), C, Lr, N, H, window, K, dmag.data(), ld, g.dev, s);

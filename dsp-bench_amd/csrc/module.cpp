@@ -36,6 +36,19 @@ namespace {
 
 constexpr uint64_t kStagedLdsBytes = 64 * 1024;  // stateful render's LDS double-buffer limit
 
+// the LDS-blocks kernels of kDriver: (C, B) = 0 matches any value
+struct LdsShape {
+    const char *name;
+    uint32_t C, B;
+};
+constexpr LdsShape kLdsShapes[7] = {{"dspb_render_lds", 0, 0},         {"dspb_render_lds_c2b512", 2, 512},
+                                    {"dspb_render_lds_c2b256", 2, 256}, {"dspb_render_lds_c2b1024", 2, 1024},
+                                    {"dspb_render_lds_c1b512", 1, 512}, {"dspb_render_lds_c1", 1, 0},
+                                    {"dspb_render_lds_c2", 2, 0}};
+// the stateful LDS path's kernels: dspb_render covers every other shape
+constexpr LdsShape kStShapes[4] = {{"dspb_render_st_c2b512", 2, 512}, {"dspb_render_st_c2b256", 2, 256},
+                                   {"dspb_render_st_c1", 1, 0}, {"dspb_render_st_c2", 2, 0}};
+
 // Host mirror of the driver's argument block (same layout on both sides).
 struct RenderArgsG {
     void *P;
@@ -294,17 +307,139 @@ __device__ static void dspb_stateless_lds(const dspb_render_args &A) {
         __syncthreads();
     }
 }
-// the LDS-blocks path as its own kernel: four waves, two workgroups per CU
-extern "C" __global__ __launch_bounds__(256) void dspb_render_lds(dspb_render_args A) {
-    if (!__is_empty(State)) return;
-    if (A.C == 2 && A.B == 512) dspb_stateless_lds<2, 512>(A);
-    else if (A.C == 2 && A.B == 256) dspb_stateless_lds<2, 256>(A);
-    else if (A.C == 2 && A.B == 1024) dspb_stateless_lds<2, 1024>(A);
-    else if (A.C == 1 && A.B == 512) dspb_stateless_lds<1, 512>(A);
-    else if (A.C == 1) dspb_stateless_lds<1, 0>(A);
-    else if (A.C == 2) dspb_stateless_lds<2, 0>(A);
-    else dspb_stateless_lds<0, 0>(A);
+// blocks per round of the LDS-blocks path (the host computes the same:
+// module.cpp lds_round_blocks)
+constexpr unsigned dspb_lds_nb(unsigned C, unsigned B) {
+    const unsigned v = 76u * 1024u / ((C * B + 1u) * 4u) / 4u * 4u;
+    return v < 64u ? v : 64u;
 }
+// the LDS-blocks path for a constant shape (C, B, 4 | B), software
+// pipelined over the workgroup's rounds: a persistent grid of two
+// workgroups per CU walks the file, and while the lanes of round r run their
+// callbacks in LDS, the next round's file samples are already in flight into
+// registers (PT float4 per thread and channel, all loads issued at once), so
+// a round costs one copy out and the callbacks, not a chain of dependent HBM
+// loads.  Rounds the file does not cover completely (EOF, no file channel,
+// the ragged last round) take dspb_stateless_lds's copy instead.
+template <unsigned CC, unsigned BB>
+__device__ static void dspb_stateless_lds_pf(const dspb_render_args &A) {
+    extern __shared__ float dspb_lbuf[];
+    constexpr unsigned C = CC, B = BB, SB = C * B + 1u, NB = dspb_lds_nb(C, B);
+    constexpr unsigned N4 = NB * B / 4u, PT = (N4 + 255u) / 256u;  // float4 per channel / per thread
+    State local = dspb_from_global<State>(A.S);
+    Parameters prm = dspb_from_global<Parameters>(A.P);
+    const unsigned t = threadIdx.x, wave = t >> 6, lane = t & 63u;
+    constexpr unsigned per = NB / 4u;  // blocks per wave
+    bool aligned_in = true;
+    for (unsigned c = 0; c < C && c < A.in_ch; ++c) aligned_in = aligned_in && !(((unsigned long long)A.in[c]) & 15);
+    const unsigned long long stride = (unsigned long long)gridDim.x * NB;
+    auto full = [&](unsigned long long b0) {
+        return b0 + NB <= A.nblocks && (A.in_ch == 0 || ((b0 + NB) * B <= A.L && aligned_in));
+    };
+    float4 pf[C][PT];
+    auto load = [&](unsigned long long b0) {
+#pragma unroll
+        for (unsigned c = 0; c < C; ++c) {
+            const __attribute__((address_space(1))) float4 *x4 =
+                (const __attribute__((address_space(1))) float4 *)(A.in[c < A.in_ch ? c : 0] + b0 * B);
+#pragma unroll
+            for (unsigned k = 0; k < PT; ++k) {
+                const unsigned i = t + 256u * k;
+                if (c < A.in_ch && (N4 % 256u == 0 || i < N4)) {
+                    const float4 v = x4[i];
+                    pf[c][k] = v;
+                } else {
+                    pf[c][k] = make_float4(0.f, 0.f, 0.f, 0.f);
+                }
+            }
+        }
+    };
+    unsigned long long b0 = (unsigned long long)blockIdx.x * NB;
+    bool have = b0 < A.nblocks && full(b0);
+    if (have) load(b0);
+    for (; b0 < A.nblocks; b0 += stride) {
+        const unsigned nb = (unsigned)(A.nblocks - b0 < NB ? A.nblocks - b0 : NB);
+        const unsigned long long i0 = b0 * B;
+        const unsigned n = nb * B;
+        if (have) {
+#pragma unroll
+            for (unsigned c = 0; c < C; ++c) {
+                float *row = dspb_lbuf + c * B;
+#pragma unroll
+                for (unsigned k = 0; k < PT; ++k) {
+                    const unsigned j = 4u * (t + 256u * k);
+                    if (N4 % 256u == 0 || j < 4u * N4) {
+                        const unsigned q = j / B;
+                        float *d = row + q * SB + (j - q * B);
+                        d[0] = pf[c][k].x, d[1] = pf[c][k].y, d[2] = pf[c][k].z, d[3] = pf[c][k].w;
+                    }
+                }
+            }
+        } else {  // render_audio's copy with zeros past EOF and for missing channels
+            const unsigned long long lim = A.L > i0 ? A.L - i0 : 0;
+            for (unsigned c = 0; c < C; ++c) {
+                const dspb_gfloat *x = (const dspb_gfloat *)A.in[c < A.in_ch ? c : 0] + i0;
+                const unsigned long long m = c < A.in_ch ? lim : 0;
+                float *row = dspb_lbuf + c * B;
+                for (unsigned j = t; j < n; j += 256u) {
+                    const unsigned q = j / B;
+                    row[q * SB + (j - q * B)] = j < m ? x[j] : 0.0f;
+                }
+            }
+        }
+        __syncthreads();
+        // the next round's loads fly while this round's callbacks run
+        have = b0 + stride < A.nblocks && full(b0 + stride);
+        if (have) load(b0 + stride);
+        const unsigned k = wave * per + lane;
+        if (lane < per && k < nb) {
+            float *blk = dspb_lbuf + k * SB;
+            float *ptrs[C];
+            for (unsigned c = 0; c < C; ++c) ptrs[c] = blk + c * B;
+            audio_callback(prm, local, ptrs, C, B, A.sr);
+        }
+        __syncthreads();
+        for (unsigned c = 0; c < C; ++c) {
+            dspb_gfloat *o = (dspb_gfloat *)A.out[c] + i0;
+            const float *row = dspb_lbuf + c * B;
+            if ((((unsigned long long)o) & 15) == 0) {
+                __attribute__((address_space(1))) float4 *o4 = (__attribute__((address_space(1))) float4 *)o;
+                for (unsigned j = 4 * t; j < n; j += 1024u) {
+                    const unsigned q = j / B;
+                    const float *d = row + q * SB + (j - q * B);
+                    o4[j / 4] = make_float4(d[0], d[1], d[2], d[3]);
+                }
+            } else {
+                for (unsigned j = t; j < n; j += 256u) {
+                    const unsigned q = j / B;
+                    o[j] = row[q * SB + (j - q * B)];
+                }
+            }
+        }
+        __syncthreads();
+    }
+}
+// the LDS-blocks path: four waves, two workgroups per CU, one kernel per
+// (C, B) instantiation (the host picks it).  Kept apart, each kernel's
+// register budget is its own: with all instantiations behind one dispatch the
+// scheduler held the callback to one LDS round trip per sample pair (a ds_read
+// waited on the previous ds_write) to keep the whole kernel under 64 VGPRs.
+// Constant shapes with 4 | B take the pipelined rounds (dspb_stateless_lds_pf).
+#define DSPB_LDS_KERNEL(name, CC, BB)                                                  \
+    extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) void name(  \
+        dspb_render_args A) {                                                          \
+        if constexpr (__is_empty(State)) {                                             \
+            if constexpr (CC > 0 && BB > 0 && BB % 4 == 0) dspb_stateless_lds_pf<CC, BB>(A); \
+            else dspb_stateless_lds<CC, BB>(A);                                        \
+        }                                                                              \
+    }
+DSPB_LDS_KERNEL(dspb_render_lds_c2b512, 2, 512)
+DSPB_LDS_KERNEL(dspb_render_lds_c2b256, 2, 256)
+DSPB_LDS_KERNEL(dspb_render_lds_c2b1024, 2, 1024)
+DSPB_LDS_KERNEL(dspb_render_lds_c1b512, 1, 512)
+DSPB_LDS_KERNEL(dspb_render_lds_c1, 1, 0)
+DSPB_LDS_KERNEL(dspb_render_lds_c2, 2, 0)
+DSPB_LDS_KERNEL(dspb_render_lds, 0, 0)
 extern "C" __global__ void dspb_render(dspb_render_args A) {
     extern __shared__ float dspb_lbuf[];
     if (__is_empty(State)) {
@@ -329,6 +464,18 @@ extern "C" __global__ void dspb_render(dspb_render_args A) {
         else dspb_stateful_lds<0>(A);
     }
 }
+// the stateful LDS path's common shapes as kernels of their own (as the
+// LDS-blocks kernels above: a register budget of their own, so the callback's
+// LDS loads can run ahead of its stores)
+#define DSPB_ST_KERNEL(name, CC, BB)                                                   \
+    extern "C" __global__ void name(dspb_render_args A) {                              \
+        extern __shared__ float dspb_lbuf[];                                           \
+        if (!__is_empty(State) && blockIdx.x == 0) dspb_stateful_lds<CC, BB>(A);       \
+    }
+DSPB_ST_KERNEL(dspb_render_st_c2b512, 2, 512)
+DSPB_ST_KERNEL(dspb_render_st_c2b256, 2, 256)
+DSPB_ST_KERNEL(dspb_render_st_c1, 1, 0)
+DSPB_ST_KERNEL(dspb_render_st_c2, 2, 0)
 // compute_IR (plugin.cpp:17-58): the callback once, on buffers as they are
 extern "C" __global__ void dspb_callback(dspb_render_args A) {
     float *ptrs[16];
@@ -355,11 +502,15 @@ struct dsp_module {
     dsp_descriptor *desc = nullptr;  // from the code object (NULL for code without one)
     int device = -1;
     hipModule_t mod = nullptr;
-    hipFunction_t f_render_lds = nullptr;  // NULL for code objects compiled before it existed
+    // the LDS-blocks kernels (NULL for code objects compiled before they
+    // existed): [0] any (C, B), then the instantiations of kLdsShapes
+    hipFunction_t f_render_lds[7] = {};
+    hipFunction_t f_render_st[4] = {};  // kStShapes (NULL: dspb_render)
     hipFunction_t f_sizes = nullptr, f_defaults = nullptr, f_init = nullptr, f_render = nullptr,
                   f_callback = nullptr;
     uint32_t params_size = 0, state_size = 0;
     int stateless = 0;
+    int cus = 256;                     // compute units of the device (persistent grids)
     void *h_params = nullptr;          // pinned staging of the Parameters upload
     hipEvent_t upload_ev = nullptr;    // the last upload from h_params
     hipEvent_t use_ev = nullptr;       // the last render launched with d_params / d_state
@@ -537,6 +688,8 @@ int dsp_module_load(const void *code, uint64_t code_size, int device, dsp_module
     if (st) return st;
     dsp_module *m = new dsp_module();
     (void)hipGetDevice(&m->device);
+    if (hipDeviceGetAttribute(&m->cus, hipDeviceAttributeMultiprocessorCount, m->device) != hipSuccess || m->cus < 1)
+        m->cus = 256;
     {
         dsp_descriptor *dd = new dsp_descriptor();
         if (dspb::desc::read(code, code_size, &dd->d, nullptr) == 0) m->desc = dd;
@@ -554,9 +707,17 @@ int dsp_module_load(const void *code, uint64_t code_size, int device, dsp_module
                                                         {&m->f_callback, "dspb_callback"}};
     for (auto &f : fs)
         if ((e = hipModuleGetFunction(f.f, m->mod, f.n)) != hipSuccess) return fail(dspb::hip_fail(e, f.n));
-    if (hipModuleGetFunction(&m->f_render_lds, m->mod, "dspb_render_lds") != hipSuccess) {
-        (void)hipGetLastError();
-        m->f_render_lds = nullptr;
+    for (int i = 0; i < 7; ++i) {
+        if (hipModuleGetFunction(&m->f_render_lds[i], m->mod, kLdsShapes[i].name) != hipSuccess) {
+            (void)hipGetLastError();
+            m->f_render_lds[i] = nullptr;
+        }
+    }
+    for (int i = 0; i < 4; ++i) {
+        if (hipModuleGetFunction(&m->f_render_st[i], m->mod, kStShapes[i].name) != hipSuccess) {
+            (void)hipGetLastError();
+            m->f_render_st[i] = nullptr;
+        }
     }
     unsigned *d_o = nullptr;
     if ((e = hipMalloc(&d_o, 4 * sizeof(unsigned))) != hipSuccess) return fail(dspb::hip_fail(e, "hipMalloc"));
@@ -823,7 +984,7 @@ static int stateless_path_forced() {
     return v;
 }
 // the LDS-blocks path: LDS per workgroup round (two workgroups per CU)
-constexpr uint64_t kLdsRoundBytes = 76 * 1024;
+constexpr uint64_t kLdsRoundBytes = 76 * 1024;  // (kDriver dspb_lds_nb: the same formula)
 
 // the caller's Parameters blob -> the module's device Parameters, stream
 // ordered: through a pinned staging copy (reused once the previous upload
@@ -858,10 +1019,13 @@ static int check_device(const dsp_module *m) {
     return DSP_OK;
 }
 
-// dsp_render_offline / dsp_render_stft with DSP_PLUGIN_GENERIC (device buffers)
+// dsp_render_offline / dsp_render_stft with DSP_PLUGIN_GENERIC (device buffers).
+// cont: this call renders the next chunk of a file whose earlier chunks were
+// rendered by the previous calls on the same stream (the pipelined render +
+// STFT of capi.cpp), so a plugin with State may start at goff > 0
 int module_render(dsp_module *m, const void *params, uint32_t params_size, const float *const *in,
                   uint32_t in_ch, uint64_t L, float *const *out, uint32_t C, uint32_t B, float sr,
-                  uint64_t goff, hipStream_t s) {
+                  uint64_t goff, hipStream_t s, bool cont) {
     if (!m || !m->initialized) {
         set_last_error("GENERIC plugin: module not loaded / initialize_state not run");
         return DSP_ERR_INVALID;
@@ -880,12 +1044,14 @@ int module_render(dsp_module *m, const void *params, uint32_t params_size, const
         set_last_error("sample_offset must be a multiple of B");
         return DSP_ERR_INVALID;
     }
-    if (!m->stateless && goff) {
+    if (!m->stateless && goff && !cont) {
         set_last_error("GENERIC plugin with State: whole files only (sample_offset 0)");
         return DSP_ERR_INVALID;
     }
     std::lock_guard<std::mutex> lk(m->mu);
-    if (int st = upload_params(m, params, params_size, s)) return st;
+    // (a continuing chunk renders with the Parameters its first chunk uploaded)
+    if (!cont)
+        if (int st = upload_params(m, params, params_size, s)) return st;
     RenderArgsG A{};
     A.P = m->d_params;
     A.S = m->d_state[0];
@@ -907,15 +1073,29 @@ int module_render(dsp_module *m, const void *params, uint32_t params_size, const
         // in-place wave path; DSPB_STATELESS_PATH=0/3 forces one
         const uint64_t stride = (uint64_t)C * B + 1;
         const uint64_t nb = std::min<uint64_t>(64, kLdsRoundBytes / (stride * sizeof(float)) / 4 * 4);
+        // the most specific instantiation for (C, B): exact shapes first (the
+        // software-pipelined rounds of dspb_stateless_lds_pf, on a persistent
+        // grid of two workgroups per CU)
+        hipFunction_t f = nullptr;
+        bool persistent = false;
+        for (int i = 6; i >= 0 && !f; --i)
+            if (m->f_render_lds[i] && kLdsShapes[i].C == C && kLdsShapes[i].B == B) {
+                f = m->f_render_lds[i];
+                persistent = B % 4 == 0;
+            }
+        for (int i = 6; i >= 0 && !f; --i)
+            if (m->f_render_lds[i] && (!kLdsShapes[i].C || kLdsShapes[i].C == C) && !kLdsShapes[i].B)
+                f = m->f_render_lds[i];
         int path = stateless_path_forced();
         if (path < 0) path = nb >= 4 ? 3 : 0;
-        if (path == 3 && (nb < 4 || !m->f_render_lds)) path = 0;
+        if (path == 3 && (nb < 4 || !f)) path = 0;
         if (path == 3) {
             A.lds = 3;
             A.lds_nb = (unsigned)nb;
             A.lds_stride = (unsigned)stride;
-            const uint64_t g = (A.nblocks + nb - 1) / nb;
-            MOD_HIP(hipModuleLaunchKernel(m->f_render_lds, (unsigned)(g < (1u << 20) ? g : (1u << 20)), 1, 1, 256, 1, 1,
+            uint64_t g = (A.nblocks + nb - 1) / nb;
+            if (persistent) g = std::min<uint64_t>(g, 2ull * m->cus);
+            MOD_HIP(hipModuleLaunchKernel(f, (unsigned)(g < (1u << 20) ? g : (1u << 20)), 1, 1, 256, 1, 1,
                                           (unsigned)(nb * stride * sizeof(float)), s, args, nullptr));
             MOD_HIP(hipEventRecord(m->use_ev, s));
             return DSP_OK;
@@ -923,14 +1103,21 @@ int module_render(dsp_module *m, const void *params, uint32_t params_size, const
         block = 64;  // one wave per 64 blocks
         const uint64_t g = (A.nblocks + 63) / 64;
         grid = (unsigned)(g < 65535 ? g : 65535);
-    } else if (2ull * C * B * sizeof(float) <= kStagedLdsBytes) {
+    }
+    hipFunction_t f = m->f_render;
+    if (!m->stateless && 2ull * C * B * sizeof(float) <= kStagedLdsBytes) {
         // stateful: 4 waves, the block double-buffer in LDS (the callback's
         // loads and stores hit LDS, the copies run on 192 lanes beside it)
         A.lds = 1;
         block = 256;
         lds_bytes = (unsigned)(2ull * C * B * sizeof(float));
+        for (int i = 0; i < 4; ++i)
+            if (m->f_render_st[i] && kStShapes[i].C == C && (!kStShapes[i].B || kStShapes[i].B == B)) {
+                f = m->f_render_st[i];
+                break;
+            }
     }
-    MOD_HIP(hipModuleLaunchKernel(m->f_render, grid, 1, 1, block, 1, 1, lds_bytes, s, args, nullptr));
+    MOD_HIP(hipModuleLaunchKernel(f, grid, 1, 1, block, 1, 1, lds_bytes, s, args, nullptr));
     MOD_HIP(hipEventRecord(m->use_ev, s));
     return DSP_OK;
 }

@@ -20,13 +20,13 @@ import dspbench as d
 from dspbench.module import Descriptor, compile_source
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-REF = os.path.join(os.path.dirname(HERE), "oracle", "_ref")
+MODS = os.path.join(os.path.dirname(HERE), "dsp-bench_amd", "modules")
 
 
 def ref_code(name):
-    p = os.path.join(REF, f"mod_{name}.co")
+    p = os.path.join(MODS, f"mod_{name}.co")
     if not os.path.exists(p):
-        pytest.skip("oracle/_ref not built")
+        pytest.skip("dsp-bench_amd/modules not built (tools/make_plugin_modules.py)")
     return open(p, "rb").read()
 
 

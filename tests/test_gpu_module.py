@@ -1,7 +1,7 @@
 """Generic GPU dispatch: the reference's stock plugins,
 compiled from their own sources by the product's plugin compiler
-(dsp_module_compile: hiprtc -> gfx950, oracle/make_modules.py ->
-oracle/_ref/mod_*.co), run unchanged on the GPU and are compared with the
+(dsp_module_compile: hiprtc -> gfx950, tools/make_plugin_modules.py ->
+dsp-bench_amd/modules/mod_*.co), run unchanged on the GPU and are compared with the
 same sources compiled for the CPU with the JIT's flags (oracle/_ref/
 libref_*.so) through the oracle's render loop.
 
@@ -22,6 +22,7 @@ import dspbench as d
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 REF = os.path.join(os.path.dirname(HERE), "oracle", "_ref")
+MODS = os.path.join(os.path.dirname(HERE), "dsp-bench_amd", "modules")
 PLUGIN_DIR = os.path.join(os.path.dirname(HERE), "dsp-bench_amd", "plugins")
 
 EXACT = ["gain_test", "IR_test", "handmade_test", "static_gain_plugin", "no_op", "plugin_with_parameters",
@@ -31,12 +32,12 @@ EMPTY_PARAMS = {"static_gain_plugin", "no_op", "template_plugin"}
 
 
 def have(name):
-    return os.path.exists(os.path.join(REF, f"mod_{name}.co")) and os.path.exists(
+    return os.path.exists(os.path.join(MODS, f"mod_{name}.co")) and os.path.exists(
         os.path.join(REF, f"libref_{name}.so"))
 
 
 def load(name):
-    with open(os.path.join(REF, f"mod_{name}.co"), "rb") as f:
+    with open(os.path.join(MODS, f"mod_{name}.co"), "rb") as f:
         return d.module.Module(f.read())
 
 
@@ -114,8 +115,12 @@ def test_stateless_plugin_staged_edges(torch_cuda, oracle, name, B):
 # long files through the LDS-blocks path (dspb_render_lds): (Cin, C, B) =
 # mono file into stereo with B = 100 (scalar staging: B % 4 != 0), stereo
 # B = 512 and mono B = 1024 (constant-shape instantiations, float4 staging),
-# 4 channels of B = 384 (the generic-shape instantiation); ragged last block
-@pytest.mark.parametrize("cin,C,B", [(1, 2, 100), (2, 2, 512), (1, 1, 1024), (3, 4, 384)])
+# 4 channels of B = 384 (the generic-shape instantiation); ragged last block.
+# The constant shapes (2, 512), (2, 256), (2, 1024), (1, 512) take the
+# software-pipelined rounds on a persistent grid (dspb_stateless_lds_pf),
+# also with a mono file into stereo (the second channel's rounds are zeros)
+@pytest.mark.parametrize("cin,C,B", [(1, 2, 100), (2, 2, 512), (1, 1, 1024), (3, 4, 384), (1, 2, 512),
+                                     (2, 2, 256), (2, 2, 1024), (1, 1, 512)])
 def test_stateless_plugin_lds_path(torch_cuda, oracle, name, cin, C, B):
     if not have(name):
         pytest.skip("oracle/_ref not built")
@@ -137,6 +142,26 @@ def test_stateless_plugin_lds_path(torch_cuda, oracle, name, cin, C, B):
         buf[:, :L] = xg
         d.render_offline(buf, C, B, 48000.0, mod.plugin(params, name), out=buf, L_file=L)
         assert np.array_equal(buf.cpu().numpy(), want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["gain_test", "handmade_test"])
+def test_stateless_plugin_lds_pipelined_unaligned_file(torch_cuda, oracle, name):
+    """A file whose rows start 4 bytes past a 16-byte boundary: the pipelined
+    rounds cannot take 16-byte loads, every round takes the scalar copy."""
+    if not have(name):
+        pytest.skip("modules / oracle/_ref not built")
+    mod = load(name)
+    params = mod.default_parameters()
+    mod.initialize_state(params, 2, 48000.0)
+    ref = oracle.RefPlugin(name, 2, 48000.0)
+    L = 700 * 512 + 5
+    x = np.random.default_rng(8).uniform(-1, 1, (2, L + 1)).astype(np.float32)
+    xg = torch_cuda.from_numpy(x).cuda()[:, 1:]
+    assert xg.data_ptr() % 16 == 4
+    got = d.render_offline(xg, 2, 512, 48000.0, mod.plugin(params, name)).cpu().numpy()
+    want = oracle.render_offline([x[0, 1:], x[1, 1:]], 2, 512, 48000.0, ref.as_oracle())
+    assert np.array_equal(got, want)
 
 
 @pytest.mark.gpu
@@ -172,6 +197,82 @@ def test_generic_ir_analysis_and_stft(torch_cuda, oracle):
     out2, mg2 = d.render_stft(x, 2, 512, 48000.0, d.Plugin.ir_test())
     assert torch_cuda.equal(out, out2)
     assert float((mg - mg2).abs().max()) <= 1e-6 * float(mg2.max())
+
+
+@pytest.fixture
+def small_chunks(monkeypatch):
+    """The pipelined GENERIC render + STFT (capi.cpp generic_render_stft) in
+    1 MiB chunks, so a short file crosses many chunk boundaries."""
+    monkeypatch.setenv("DSPB_PIPE_CHUNK_BYTES", str(1 << 20))
+
+
+@pytest.mark.gpu
+# stateless (gain_test, IR_test, handmade_test) and stateful (sine_test: its
+# State continues across the chunks on the render stream); B = 512 divides
+# H, B = 384 does not (frames straddle chunk ends), B = 100 with a mono file
+# into stereo
+@pytest.mark.parametrize("name", ["gain_test", "IR_test", "handmade_test", "sine_test"])
+@pytest.mark.parametrize("cin,B", [(2, 512), (2, 384), (1, 100)])
+def test_generic_render_stft_pipelined(torch_cuda, oracle, small_chunks, name, cin, B):
+    if not have(name):
+        pytest.skip("modules / oracle/_ref not built")
+    torch = torch_cuda
+    mod = load(name)
+    params = mod.default_parameters()
+    ref = oracle.RefPlugin(name, 2, 48000.0)
+    L = 600_000 + 77  # 4.8 MB of stereo render: 5+ chunks of 1 MiB, ragged last block
+    x = np.random.default_rng(11).uniform(-1, 1, (cin, L)).astype(np.float32)
+    xg = torch.from_numpy(x).cuda()
+    mod.initialize_state(params, 2, 48000.0)
+    out, mag = d.render_stft(xg, 2, B, 48000.0, mod.plugin(params, name))
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()
+    want = oracle.render_offline([x[c] for c in range(cin)], 2, B, 48000.0, ref.as_oracle())
+    if name in TOL:
+        assert np.max(np.abs(got - want)) <= TOL[name]
+    else:
+        assert np.array_equal(got, want)
+    m = mag.cpu().numpy()
+    F = m.shape[1]
+    assert F == (got.shape[1] - 8192) // 4096 + 1
+    for c in range(2):  # every frame against float64, from the GPU's own render
+        mref = oracle.np_stft_mag(got[c], 8192, 4096, oracle.WIN_HANN, 4097)
+        assert mref.shape == m[c].shape
+        err = np.abs(m[c] - mref).max(axis=1) / np.maximum(mref.max(axis=1), 1e-30)
+        assert err.max() <= 1e-6, (c, err.argmax(), err.max())
+    # one chunk (no pipeline) gives the same bits
+    os.environ["DSPB_PIPE_CHUNK_BYTES"] = str(1 << 40)
+    mod.initialize_state(params, 2, 48000.0)
+    out1, mag1 = d.render_stft(xg, 2, B, 48000.0, mod.plugin(params, name))
+    assert torch.equal(out1, out) and torch.equal(mag1, mag)
+
+
+@pytest.mark.gpu
+def test_generic_render_stft_pipelined_full_hour(torch_cuda, oracle):
+    """1 h of 48 kHz stereo: IR_test.cpp compiled unchanged through the
+    pipelined generic path (43 chunks of 32 MiB) gives the specialised fused
+    kernel's render bit for bit and its spectra within 1e-6 of each frame's
+    peak (two FFT kernels: the fused PER path and the memory path)."""
+    if not have("IR_test"):
+        pytest.skip("modules / oracle/_ref not built")
+    torch = torch_cuda
+    mod = load("IR_test")
+    params = mod.default_parameters()
+    mod.initialize_state(params, 2, 48000.0)
+    L = 48_000 * 3600
+    x = torch.zeros((2, L), device="cuda")
+    out, mag = d.render_stft(x, 2, 512, 48000.0, mod.plugin(params, "IR_test"))
+    out2, mag2 = d.render_stft(x, 2, 512, 48000.0, d.Plugin.ir_test())
+    assert torch.equal(out, out2)
+    rel = ((mag - mag2).abs().amax(dim=2) / mag2.amax(dim=2)).max()
+    assert float(rel) <= 1e-6
+    del out, out2
+    # sampled frames against float64
+    ramp = oracle.ir_ramp_reference(0.9, 0.002, 512)
+    frame = np.tile(ramp, 8192 // 512)
+    mref = oracle.np_stft_mag(frame, 8192, 4096, oracle.WIN_HANN, 4097)[0]
+    for f in (0, 1, 20_000, mag.shape[1] - 1):
+        assert np.abs(mag[1, f].cpu().numpy() - mref).max() <= 1e-6 * mref.max()
 
 
 @pytest.mark.gpu

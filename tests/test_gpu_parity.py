@@ -365,7 +365,7 @@ def test_render_loop_generic_and_fir(torch_cuda, oracle):
     torch = torch_cuda
     L, B, nb, cursor = 7_777, 512, 40, 5_000
     x = rnd((2, L), 72)
-    co = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle", "_ref",
+    co = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "dsp-bench_amd", "modules",
                       "mod_gain_test.co")
     if os.path.exists(co):
         mod = d.module.Module(open(co, "rb").read())

@@ -24,7 +24,7 @@ sys.path.insert(0, ROOT)
 import dspbench as d  # noqa: E402
 from oracle import oracle  # noqa: E402
 
-REF = os.path.join(ROOT, "oracle", "_ref")
+MODS = os.path.join(ROOT, "dsp-bench_amd", "modules")
 secs = float(sys.argv[1]) if len(sys.argv) > 1 else 10.0
 names = sys.argv[2:] or ["sine_test", "handmade_test", "gain_test"]
 L = int(secs * 48000)
@@ -32,7 +32,7 @@ g = torch.Generator(device="cuda").manual_seed(1)
 xg = torch.rand((2, L), device="cuda", generator=g) * 2 - 1
 path = os.environ.get("DSPB_STATELESS_PATH", "3 (default)")
 for name in names:
-    with open(os.path.join(REF, f"mod_{name}.co"), "rb") as f:
+    with open(os.path.join(MODS, f"mod_{name}.co"), "rb") as f:
         mod = d.module.Module(f.read())
     params = mod.default_parameters()
     mod.initialize_state(params, 2, 48000.0)

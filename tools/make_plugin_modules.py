@@ -1,33 +1,37 @@
 #!/usr/bin/env python3
-"""make_modules.py -- TEST INFRASTRUCTURE ONLY.
+"""make_plugin_modules.py -- the reference's stock plugins as gfx950 modules.
 
 Compiles the reference's stock plugins, from their sources where they lie
-under /root/reference, with the PRODUCT's plugin compiler
-(dsp_module_compile, hiprtc -> gfx950) into oracle/_ref/mod_<name>.co, so
-the GPU tests can load and run the reference's own plugins on a box that
-has no /root/reference.  Outputs go only to oracle/_ref/ (git-ignored).
+under /root/reference, with the product's plugin compiler
+(dsp_module_compile, hiprtc -> gfx950) into
+dsp-bench_amd/modules/mod_<name>.co: what a user of the reference gets by
+pointing the product at those plugin sources.  The GPU tests and bench.py
+load these code objects on a box that has no /root/reference.  Outputs are
+git-ignored build products (they travel to the GPU box with the tree).
 
-Usage: python oracle/make_modules.py [REF_DIR]
+Usage: python tools/make_plugin_modules.py [REF_DIR]
 """
 import ctypes as C
 import os
 import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-sys.path.insert(0, os.path.join(os.path.dirname(HERE), "dsp-bench_amd"))
+ROOT = os.path.dirname(HERE)
+sys.path.insert(0, os.path.join(ROOT, "dsp-bench_amd"))
 
 PLUGINS = ["build/gain_test", "build/IR_test", "build/sine_test", "build/buffer_test",
            "build/handmade_test", "build/template_plugin", "test/static_gain_plugin", "test/no_op",
            "test/plugin_with_parameters"]
 
 
-LIB = os.path.join(HERE, "..", "dsp-bench_amd", "libdspbench.so")
+LIB = os.path.join(ROOT, "dsp-bench_amd", "libdspbench.so")
+OUT = os.path.join(ROOT, "dsp-bench_amd", "modules")
 
 
 def main():
     ref = sys.argv[1] if len(sys.argv) > 1 else "/root/reference"
     import dspbench.module as m
-    out = os.path.join(HERE, "_ref")
+    out = OUT
     os.makedirs(out, exist_ok=True)
     for p in PLUGINS:
         src = os.path.join(ref, p + ".cpp")
@@ -40,7 +44,7 @@ def main():
         code = m.compile_source(open(src).read(), os.path.basename(p))
         with open(dst, "wb") as f:
             f.write(code)
-        print(f"make_modules: {dst} ({len(code)} bytes)")
+        print(f"make_plugin_modules: {dst} ({len(code)} bytes)")
 
 
 if __name__ == "__main__":
