@@ -665,22 +665,57 @@ static uint64_t pipe_bytes() {
     return v ? v : kPipeBytes;
 }
 
+// does any row [a[i], a[i] + la) overlap any row [b[j], b[j] + lb)?
+static bool rows_overlap(const float *const *a, uint32_t na, uint64_t la, const float *const *b, uint32_t nb,
+                         uint64_t lb) {
+    for (uint32_t i = 0; i < na; ++i)
+        for (uint32_t j = 0; j < nb; ++j)
+            if (a[i] < b[j] + lb && b[j] < a[i] + la) return true;
+    return false;
+}
+
 static int generic_render_stft(const float *const *in, uint32_t in_ch, uint64_t L, float *const *out, uint32_t C,
                                uint32_t B, const SampleMap &map, uint32_t N, uint32_t H, int window, uint32_t K,
                                float *const *mag, uint64_t ld, uint64_t goff, int dev, hipStream_t s) {
     const uint64_t nblocks = (L + B - 1) / B, Lr = nblocks * B;
     const uint64_t F = dsp_stft_frame_count(Lr, N, H);
+    // the fused kernel of the plugin's module (module.cpp dspb_rstft): the
+    // headline STFT shape, a stateless plugin of a compiled (C, B), rows that
+    // do not overlap (the kernel reads its own render back)
+    // (DSPB_GENERIC_FUSED=0: always the pipeline -- tests, A/B)
+    const char *fe = std::getenv("DSPB_GENERIC_FUSED");
+    bool ok = N == 8192 && H == 4096 && K == 4097 && F > 0 && !rows_overlap(in, in_ch, L, out, C, Lr) &&
+              !(fe && fe[0] == '0');
+    for (uint32_t c = 0; c < C; ++c) ok = ok && aligned(out[c], 8);
+    if (ok) {
+        const v2f *tw = nullptr;
+        Stft8kArgs W{};
+        int st = get_tw(dev, &tw);
+        if (!st) st = set_wincomp(dev, window, &W);
+        if (st) return st;
+        bool done = false;
+        st = module_render_stft((::dsp_module *)map.module, map.gparams, map.gparams_size, in, in_ch, L, out, C, B,
+                                map.sr, mag, ld, tw, W.wbase, W.wa, W.wb, s, &done);
+        if (st || done) return st;
+    }
     const uint64_t per = std::max<uint64_t>(1, pipe_bytes() / (4ull * C * B));  // blocks per chunk
     ::dsp_module *mod = (::dsp_module *)map.module;
     if (F == 0 || nblocks <= per) {  // one chunk: render, then the STFT, on s
         int st = module_render(mod, map.gparams, map.gparams_size, in, in_ch, L, out, C, B, map.sr, goff, s);
         return st ? st : stft_device(out, C, Lr, N, H, window, K, mag, ld, dev, s);
     }
+    // DSPB_PIPE_STREAMS=1: the STFT chunks on the caller's stream too (A/B)
+    const char *se = std::getenv("DSPB_PIPE_STREAMS");
+    const bool one = se && se[0] == '1';
     DeviceRes::Aux ax;
-    int st = get_aux(dev, s, &ax);
-    if (st) return st;
-    DSPB_HIP(hipEventRecord(ax.ev_chunk, s));  // s2 behind the caller's earlier work
-    DSPB_HIP(hipStreamWaitEvent(ax.s2, ax.ev_chunk, 0));
+    int st = DSP_OK;
+    if (one) {
+        ax.s2 = s;
+    } else {
+        if ((st = get_aux(dev, s, &ax))) return st;
+        DSPB_HIP(hipEventRecord(ax.ev_chunk, s));  // s2 behind the caller's earlier work
+        DSPB_HIP(hipStreamWaitEvent(ax.s2, ax.ev_chunk, 0));
+    }
     std::vector<const float *> ci(in_ch);
     std::vector<float *> co(C), cm(C);
     std::vector<const float *> ro(C);
@@ -694,12 +729,12 @@ static int generic_render_stft(const float *const *in, uint32_t in_ch, uint64_t 
         if ((st = module_render(mod, map.gparams, map.gparams_size, ci.data(), in_ch, Lc, co.data(), C, B, map.sr,
                                 goff + i0, s, b0 > 0)))
             return st;
-        DSPB_HIP(hipEventRecord(ax.ev_chunk, s));
+        if (!one) DSPB_HIP(hipEventRecord(ax.ev_chunk, s));
         // frames inside [0, rendered): f < frame_count(rendered)
         const uint64_t done = i0 + nb * B;
         const uint64_t f1 = b0 + nb == nblocks ? F : dsp_stft_frame_count(done, N, H);
         if (f1 <= f0) continue;
-        DSPB_HIP(hipStreamWaitEvent(ax.s2, ax.ev_chunk, 0));
+        if (!one) DSPB_HIP(hipStreamWaitEvent(ax.s2, ax.ev_chunk, 0));
         for (uint32_t c = 0; c < C; ++c) {
             ro[c] = out[c] + f0 * H;
             cm[c] = mag[c] + f0 * ld;
@@ -708,8 +743,10 @@ static int generic_render_stft(const float *const *in, uint32_t in_ch, uint64_t 
             return st;
         f0 = f1;
     }
-    DSPB_HIP(hipEventRecord(ax.ev_join, ax.s2));
-    DSPB_HIP(hipStreamWaitEvent(s, ax.ev_join, 0));
+    if (!one) {
+        DSPB_HIP(hipEventRecord(ax.ev_join, ax.s2));
+        DSPB_HIP(hipStreamWaitEvent(s, ax.ev_join, 0));
+    }
     return DSP_OK;
 }
 

@@ -69,6 +69,10 @@ int launch_render_wrap(const RenderArgs &A, uint32_t C, uint64_t cursor, hipStre
 int module_render(::dsp_module *m, const void *params, uint32_t params_size, const float *const *in,
                   uint32_t in_ch, uint64_t L, float *const *out, uint32_t C, uint32_t B, float sr,
                   uint64_t goff, hipStream_t s, bool cont = false);
+int module_render_stft(::dsp_module *m, const void *params, uint32_t params_size, const float *const *in,
+                       uint32_t in_ch, uint64_t L, float *const *out, uint32_t C, uint32_t B, float sr,
+                       float *const *mag, uint64_t ld, const void *tw, const void *wbase, float wa, float wb,
+                       hipStream_t s, bool *done);
 int module_ir(::dsp_module *m, const void *params, uint32_t params_size, float *const *bufs, uint32_t C,
               uint32_t n, float sr, hipStream_t s);
 struct FirFftArgs {
