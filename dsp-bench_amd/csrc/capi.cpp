@@ -63,11 +63,6 @@ struct DeviceRes {
     std::map<std::pair<void *, int>, std::pair<float *, size_t>> scratch;  // per (stream, slot)
     std::vector<FirTaps> fir;                                  // FIR filters seen (plugin_map)
     float *delta = nullptr;  // 2048 floats: 1, 0, 0, ... (compute_IR's impulse, read-only)
-    struct Aux {  // a second stream beside a caller's stream + the events that order them
-        hipStream_t s2 = nullptr;
-        hipEvent_t ev_chunk = nullptr, ev_join = nullptr;
-    };
-    std::map<void *, Aux> aux;  // per caller stream
 };
 
 static std::mutex g_mu;
@@ -219,20 +214,6 @@ static int get_scratch(int dev, hipStream_t s, size_t bytes, float **out, int sl
         slot.second = bytes;
     }
     *out = slot.first;
-    return DSP_OK;
-}
-
-// The STFT stream of the pipelined GENERIC render + STFT: one per (device,
-// caller stream), non-blocking, with its two ordering events.
-static int get_aux(int dev, hipStream_t s, DeviceRes::Aux *out) {
-    std::lock_guard<std::mutex> lk(g_mu);
-    DeviceRes::Aux &a = g_res[dev].aux[(void *)s];
-    if (!a.s2) {
-        DSPB_HIP(hipStreamCreateWithFlags(&a.s2, hipStreamNonBlocking));
-        DSPB_HIP(hipEventCreateWithFlags(&a.ev_chunk, hipEventDisableTiming));
-        DSPB_HIP(hipEventCreateWithFlags(&a.ev_join, hipEventDisableTiming));
-    }
-    *out = a;
     return DSP_OK;
 }
 
@@ -644,110 +625,20 @@ static int stft_device(const float *const *in, uint32_t C, uint64_t L, uint32_t 
     return DSP_OK;
 }
 
-// GENERIC render + STFT, pipelined through the Infinity Cache.  The plugin's
-// own callback (hiprtc module) renders the file in chunks of ~kPipeBytes on
-// the caller's stream; the STFT of the frames a chunk completes runs on a
-// second stream behind it, while the next chunk renders.  A chunk's render is
-// still resident in the 256 MiB last-level cache when its STFT reads it, so
-// the render is written to HBM once and not read back from it; the
-// memory-bound render and the VALU-bound FFT overlap on the CUs.  Stream
-// ordered on s: s2 starts behind everything queued on s, and s waits for the
-// last STFT before the call's later work.  Chunk boundaries are multiples of
-// B, so every callback sees whole blocks in order (a plugin with State
-// continues across chunks on s).
-constexpr uint64_t kPipeBytes = 32ull << 20;  // render bytes per chunk (all channels)
-
-// DSPB_PIPE_CHUNK_BYTES overrides the chunk size (tests: many chunks on a
-// short file; tuning)
-static uint64_t pipe_bytes() {
-    const char *e = std::getenv("DSPB_PIPE_CHUNK_BYTES");
-    const uint64_t v = e ? std::strtoull(e, nullptr, 10) : 0;
-    return v ? v : kPipeBytes;
-}
-
-// does any row [a[i], a[i] + la) overlap any row [b[j], b[j] + lb)?
-static bool rows_overlap(const float *const *a, uint32_t na, uint64_t la, const float *const *b, uint32_t nb,
-                         uint64_t lb) {
-    for (uint32_t i = 0; i < na; ++i)
-        for (uint32_t j = 0; j < nb; ++j)
-            if (a[i] < b[j] + lb && b[j] < a[i] + la) return true;
-    return false;
-}
-
+// GENERIC render + STFT: the plugin's own callback renders the whole file
+// (module.cpp, the LDS-blocks driver), then the memory-source STFT reads the
+// render back, both on the caller's stream.  Measured against the
+// alternatives: chunks pipelined through the Infinity Cache on
+// two streams, and three kernels fusing the callback with the FFT, were all
+// slower -- a plugin callback runs serially over its block, and the LDS that
+// holds blocks in flight is the same LDS the FFT's transposes need.
 static int generic_render_stft(const float *const *in, uint32_t in_ch, uint64_t L, float *const *out, uint32_t C,
                                uint32_t B, const SampleMap &map, uint32_t N, uint32_t H, int window, uint32_t K,
                                float *const *mag, uint64_t ld, uint64_t goff, int dev, hipStream_t s) {
-    const uint64_t nblocks = (L + B - 1) / B, Lr = nblocks * B;
-    const uint64_t F = dsp_stft_frame_count(Lr, N, H);
-    // the fused kernel of the plugin's module (module.cpp dspb_rstft): the
-    // headline STFT shape, a stateless plugin of a compiled (C, B), rows that
-    // do not overlap (the kernel reads its own render back)
-    // (DSPB_GENERIC_FUSED=0: always the pipeline -- tests, A/B)
-    const char *fe = std::getenv("DSPB_GENERIC_FUSED");
-    bool ok = N == 8192 && H == 4096 && K == 4097 && F > 0 && !rows_overlap(in, in_ch, L, out, C, Lr) &&
-              !(fe && fe[0] == '0');
-    for (uint32_t c = 0; c < C; ++c) ok = ok && aligned(out[c], 8);
-    if (ok) {
-        const v2f *tw = nullptr;
-        Stft8kArgs W{};
-        int st = get_tw(dev, &tw);
-        if (!st) st = set_wincomp(dev, window, &W);
-        if (st) return st;
-        bool done = false;
-        st = module_render_stft((::dsp_module *)map.module, map.gparams, map.gparams_size, in, in_ch, L, out, C, B,
-                                map.sr, mag, ld, tw, W.wbase, W.wa, W.wb, s, &done);
-        if (st || done) return st;
-    }
-    const uint64_t per = std::max<uint64_t>(1, pipe_bytes() / (4ull * C * B));  // blocks per chunk
-    ::dsp_module *mod = (::dsp_module *)map.module;
-    if (F == 0 || nblocks <= per) {  // one chunk: render, then the STFT, on s
-        int st = module_render(mod, map.gparams, map.gparams_size, in, in_ch, L, out, C, B, map.sr, goff, s);
-        return st ? st : stft_device(out, C, Lr, N, H, window, K, mag, ld, dev, s);
-    }
-    // DSPB_PIPE_STREAMS=1: the STFT chunks on the caller's stream too (A/B)
-    const char *se = std::getenv("DSPB_PIPE_STREAMS");
-    const bool one = se && se[0] == '1';
-    DeviceRes::Aux ax;
-    int st = DSP_OK;
-    if (one) {
-        ax.s2 = s;
-    } else {
-        if ((st = get_aux(dev, s, &ax))) return st;
-        DSPB_HIP(hipEventRecord(ax.ev_chunk, s));  // s2 behind the caller's earlier work
-        DSPB_HIP(hipStreamWaitEvent(ax.s2, ax.ev_chunk, 0));
-    }
-    std::vector<const float *> ci(in_ch);
-    std::vector<float *> co(C), cm(C);
-    std::vector<const float *> ro(C);
-    uint64_t f0 = 0;  // frames done
-    for (uint64_t b0 = 0; b0 < nblocks; b0 += per) {
-        const uint64_t nb = std::min(per, nblocks - b0), i0 = b0 * B;
-        // the chunk's file samples (the last chunk holds the file's end: i0 < L)
-        const uint64_t Lc = std::min<uint64_t>(L - i0, nb * B);
-        for (uint32_t c = 0; c < in_ch; ++c) ci[c] = in[c] + i0;
-        for (uint32_t c = 0; c < C; ++c) co[c] = out[c] + i0;
-        if ((st = module_render(mod, map.gparams, map.gparams_size, ci.data(), in_ch, Lc, co.data(), C, B, map.sr,
-                                goff + i0, s, b0 > 0)))
-            return st;
-        if (!one) DSPB_HIP(hipEventRecord(ax.ev_chunk, s));
-        // frames inside [0, rendered): f < frame_count(rendered)
-        const uint64_t done = i0 + nb * B;
-        const uint64_t f1 = b0 + nb == nblocks ? F : dsp_stft_frame_count(done, N, H);
-        if (f1 <= f0) continue;
-        if (!one) DSPB_HIP(hipStreamWaitEvent(ax.s2, ax.ev_chunk, 0));
-        for (uint32_t c = 0; c < C; ++c) {
-            ro[c] = out[c] + f0 * H;
-            cm[c] = mag[c] + f0 * ld;
-        }
-        if ((st = stft_device(ro.data(), C, (f1 - f0 - 1) * H + N, N, H, window, K, cm.data(), ld, dev, ax.s2)))
-            return st;
-        f0 = f1;
-    }
-    if (!one) {
-        DSPB_HIP(hipEventRecord(ax.ev_join, ax.s2));
-        DSPB_HIP(hipStreamWaitEvent(s, ax.ev_join, 0));
-    }
-    return DSP_OK;
+    const uint64_t Lr = (L + B - 1) / B * B;
+    int st = module_render((::dsp_module *)map.module, map.gparams, map.gparams_size, in, in_ch, L, out, C, B,
+                           map.sr, goff, s);
+    return st ? st : stft_device(out, C, Lr, N, H, window, K, mag, ld, dev, s);
 }
 
 }  // namespace dspb
@@ -1037,8 +928,8 @@ int dsp_render_stft(const float *const *in, uint32_t in_channels, uint64_t L,
     for (uint32_t c = 0; c < in_channels; ++c) fused = fused && aligned(din[c], 8);
 
     if (!fused && map.kind == MapKind::Generic) {
-        // the plugin's own callback, render and STFT pipelined (generic_render_stft),
-        // timed as one region: file read + render write + magnitude write
+        // the plugin's own callback, then the STFT (generic_render_stft), timed
+        // as one region: file read + render write + magnitude write
         TimedLaunch tl{};
         if ((st = timing_begin(s, &tl))) return st;
         tl_timing_outer = true;

@@ -33,7 +33,6 @@
 namespace {
 
 #include "plugin_device_src.inc"  // const char kPluginDeviceSrc[] (generated from plugin_device.h)
-#include "stft_device_src.inc"    // kStftHdrNames / kStftHdrTexts: the packed-FFT headers (tools/embed_headers.py)
 
 constexpr uint64_t kStagedLdsBytes = 64 * 1024;  // stateful render's LDS double-buffer limit
 
@@ -46,25 +45,6 @@ constexpr LdsShape kLdsShapes[7] = {{"dspb_render_lds", 0, 0},         {"dspb_re
                                     {"dspb_render_lds_c2b256", 2, 256}, {"dspb_render_lds_c2b1024", 2, 1024},
                                     {"dspb_render_lds_c1b512", 1, 512}, {"dspb_render_lds_c1", 1, 0},
                                     {"dspb_render_lds_c2", 2, 0}};
-// the fused render + STFT kernels (C, B)
-constexpr LdsShape kRstftShapes[6] = {{"dspb_rstft_c2b512", 2, 512},  {"dspb_rstft_c2b256", 2, 256},
-                                      {"dspb_rstft_c2b1024", 2, 1024}, {"dspb_rstft_c1b512", 1, 512},
-                                      {"dspb_rstft_c1b256", 1, 256},  {"dspb_rstft_c1b1024", 1, 1024}};
-// Host mirror of kDriver's dspb_rstft_args (same layout on both sides).
-struct RstftArgsG {
-    void *P;
-    void *S;
-    float *in[dspb::kMaxChannels];
-    float *out[dspb::kMaxChannels];
-    float *mag[dspb::kMaxChannels];
-    unsigned long long L, nblocks, F, ld, NR;
-    float *halo;
-    const void *tw;
-    const void *wbase;
-    float wa, wb;
-    unsigned in_ch;
-    float sr;
-};
 // the stateful LDS path's kernels: dspb_render covers every other shape
 constexpr LdsShape kStShapes[4] = {{"dspb_render_st_c2b512", 2, 512}, {"dspb_render_st_c2b256", 2, 256},
                                    {"dspb_render_st_c1", 1, 0}, {"dspb_render_st_c2", 2, 0}};
@@ -472,193 +452,6 @@ DSPB_ST_KERNEL(dspb_render_st_c2b256, 2, 256)
 DSPB_ST_KERNEL(dspb_render_st_c1, 1, 0)
 DSPB_ST_KERNEL(dspb_render_st_c2, 2, 0)
 
-// ---- the plugin's own render fused with the 8192-point STFT --------------
-// (dsp_render_stft with DSP_PLUGIN_GENERIC: hop 4096, 4097 bins, a computed
-// cosine window).  One workgroup of eight waves per CU, persistent over a
-// contiguous range of frames [fa, fb), in two roles that run side by side
-// on every SIMD and hand hops to each other through an LDS ring:
-//   render waves (4-7): hop h of the file -> a ring slot (render_audio's
-//     copy, zeros past EOF), the callbacks on wave 4's lanes (one block
-//     each), publish the hop, the hop -> the render output;
-//   FFT waves (0-3): frame f (hops f, f + 1) from its two slots, windowed,
-//     into registers, release the slot, FFT and 4097 magnitudes out.
-// The render is memory- and LDS-bound, the FFT VALU-bound: on one SIMD they
-// overlap.  Each sample crosses HBM once in (the file) and once out (the
-// render), the spectra once out; no frame is read back from memory.  The
-// range's last frame ends in hop fb, which the next workgroup owns: it is
-// rendered here too (a halo) but not written out.  The hand-offs are
-// monotonic LDS counters: `ready` (hops published), prog[w] (the next frame
-// FFT wave w will take); a slot is reused once every FFT wave has moved past
-// the frames that read it.  Every wait is bounded (a hang-free exit on a
-// bug: the error word is set and the waves leave).
-struct dspb_rstft_args {
-    void *P;
-    void *S;
-    float *in[16];
-    float *out[16];
-    float *mag[16];
-    unsigned long long L;        // file samples
-    unsigned long long nblocks;  // blocks rendered: ceil(L / B)
-    unsigned long long F;        // frames per channel
-    unsigned long long ld;       // magnitude row stride
-    unsigned long long NR;       // (unused)
-    float *halo;                 // word 0: the error word (nonzero: a wait timed out)
-    const void *tw;              // capi.cpp get_tw's table
-    const float4 *wbase;         // per-lane window base angles
-    float wa, wb;                // w = wa - wb cos(theta n), pre-scaled
-    unsigned in_ch;
-    float sr;
-};
-#define DSPB_RING 3u
-__device__ static inline unsigned dspb_ld_acq(const unsigned *p) {
-    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ static inline void dspb_st_rel(unsigned *p, unsigned v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-// wait until *p >= v; false after ~2 s (a bug: never in a correct run)
-__device__ static bool dspb_wait_ge(const unsigned *p, unsigned v) {
-    for (unsigned n = 0; dspb_ld_acq(p) < v; ++n) {
-        if (n > (1u << 25)) return false;
-        __builtin_amdgcn_s_sleep(1);
-    }
-    return true;
-}
-// the windowed half h of channel c's frame from a hop in LDS (blocks at a
-// stride of SB floats, channel c at + c B)
-template <unsigned B, unsigned SB>
-__device__ __forceinline__ void dspb_half_from_lds(dspb::cx2 *P, const float *hop, unsigned c, unsigned h,
-                                                   unsigned lane, float4 wq, float wa, float wb) {
-    lane &= 63u;  // (the range: each pair's block index is a constant per jj, one base + offsets)
-#pragma unroll
-    for (unsigned jj = 0; jj < 16; ++jj) {
-        dspb::v2f we, wo;
-        dspb::win_pair((int)(16 * h + jj), wq, wa, wb, we, wo);
-        const unsigned s0 = 256u * jj + 2u * lane, s1 = s0 + 128u;  // even: a pair never crosses a block
-        const float *x0 = hop + (s0 / B) * SB + c * B + s0 % B, *x1 = hop + (s1 / B) * SB + c * B + s1 % B;
-        P[jj] = dspb::cx2{dspb::v2f{x0[0], x1[0]} * we, dspb::v2f{x0[1], x1[1]} * wo};
-    }
-}
-template <unsigned CC, unsigned BB>
-__device__ static void dspb_rstft(const dspb_rstft_args &A) {
-    extern __shared__ float dspb_lbuf[];
-    constexpr unsigned C = CC, B = BB, SB = C * B + 1u, NBH = 4096u / B, HS = NBH * SB, PT = 4096u / 256u;
-    static_assert(NBH <= 64 && 4096u % B == 0 && B % 2 == 0, "a hop's blocks on one wave's lanes");
-    float *ring = dspb_lbuf;                        // DSPB_RING slots of HS floats
-    float *tiles = dspb_lbuf + DSPB_RING * HS;      // the FFT waves' 64 x 33 transpose tiles
-    unsigned *ctl = (unsigned *)(tiles + 4u * 64u * 33u);  // [0] ready, [1..4] prog, [5] render barrier
-    const unsigned t = threadIdx.x, lane = t & 63u, wave = __builtin_amdgcn_readfirstlane(t >> 6);
-    const unsigned long long g = blockIdx.x, G = gridDim.x;
-    const unsigned long long fa = g * A.F / G, fb = (g + 1) * A.F / G;
-    const unsigned long long Htot = (A.nblocks + NBH - 1) / NBH;  // hops of the render (the last may be partial)
-    const bool last = g + 1 == G;
-    const unsigned long long hend = last ? Htot : fb + 1;  // hops rendered here
-    unsigned *err = (unsigned *)A.halo;
-    if (t < 8) ctl[t] = 0u;
-    __syncthreads();
-    if (wave >= 4) {  // ---------------- render waves ----------------
-        State local = dspb_from_global<State>(A.S);
-        Parameters prm = dspb_from_global<Parameters>(A.P);
-        const unsigned rt = t - 256u;  // 0 .. 255
-        unsigned gen = 0;
-        auto rbar = [&]() {  // barrier of the four render waves
-            ++gen;
-            if (lane == 0) __hip_atomic_fetch_add(&ctl[5], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-            return dspb_wait_ge(&ctl[5], 4u * gen);
-        };
-        for (unsigned long long h = fa; h < hend; ++h) {
-            float *slot = ring + (unsigned)(h % DSPB_RING) * HS;
-            // the slot held hop h - 3: every FFT wave past frame h - 3
-            if (h >= fa + DSPB_RING) {
-                bool ok = true;
-                for (unsigned w = 0; w < 4 && ok; ++w) ok = dspb_wait_ge(&ctl[1 + w], (unsigned)(h - 2 - fa));
-                if (!ok) { if (rt == 0) err[0] = 1u; return; }
-            }
-            const unsigned long long b0 = h * NBH;
-            const unsigned nb = (unsigned)(A.nblocks - b0 < NBH ? A.nblocks - b0 : NBH);
-            const unsigned long long i0 = b0 * B;
-            const unsigned long long lim = A.L > i0 ? A.L - i0 : 0;  // file samples left at i0
-            const unsigned n = nb * B;
-            {
-                float v[C][PT];  // every load in flight, then the LDS writes
-#pragma unroll
-                for (unsigned c = 0; c < C; ++c) {
-                    const dspb_gfloat *x = (const dspb_gfloat *)A.in[c < A.in_ch ? c : 0] + i0;
-                    const unsigned long long m = c < A.in_ch ? (lim < n ? lim : n) : 0;
-#pragma unroll
-                    for (unsigned k = 0; k < PT; ++k) {
-                        const unsigned j = rt + 256u * k;
-                        v[c][k] = j < m ? x[j] : 0.0f;
-                    }
-                }
-#pragma unroll
-                for (unsigned c = 0; c < C; ++c)
-#pragma unroll
-                    for (unsigned k = 0; k < PT; ++k) {
-                        const unsigned j = rt + 256u * k;
-                        if (j < n) slot[(j / B) * SB + c * B + j % B] = v[c][k];
-                    }
-            }
-            if (!rbar()) { if (rt == 0) err[0] = 2u; return; }
-            if (wave == 4 && lane < nb) {  // one wave, one block per lane
-                float *blk = slot + lane * SB;
-                float *ptrs[C];
-                for (unsigned c = 0; c < C; ++c) ptrs[c] = blk + c * B;
-                audio_callback(prm, local, ptrs, C, B, A.sr);
-            }
-            if (!rbar()) { if (rt == 0) err[0] = 3u; return; }
-            if (rt == 0) dspb_st_rel(&ctl[0], (unsigned)(h + 1 - fa));  // hop h is in its slot
-            if (h < fb || last) {  // the hop -> the render output (not the halo)
-                for (unsigned c = 0; c < C; ++c) {
-                    dspb_gfloat *o = (dspb_gfloat *)A.out[c] + i0;
-#pragma unroll 4
-                    for (unsigned j = rt; j < n; j += 256u) o[j] = slot[(j / B) * SB + c * B + j % B];
-                }
-            }
-            // (the stage-out reads the slot beside the FFT waves; it is
-            // rewritten three hops on, after two more render barriers)
-        }
-    } else {  // ---------------- FFT waves ----------------
-        const float4 wbl = A.wbase[lane];
-        // wave w's frames: C = 2: frame fa + 2k + (w >> 1) of channel w & 1;
-        // C = 1: frame fa + 4k + w
-        const unsigned fc = C == 2 ? (wave & 1u) : 0u;
-        const unsigned step = C == 2 ? 2u : 4u;
-        unsigned long long f = fa + (C == 2 ? (wave >> 1) : wave);
-        if (lane == 0) dspb_st_rel(&ctl[1 + wave], (unsigned)(f - fa));
-        for (; f < fb; f += step) {
-            if (!dspb_wait_ge(&ctl[0], (unsigned)(f + 2 - fa))) { if (lane == 0) err[0] = 5u; return; }
-            // (the twiddle table's address, the window's base angles and the
-            // lane opaque per frame: the 64 window pairs, the twiddle loads and
-            // the frame's LDS offsets are loop invariants that would otherwise
-            // be hoisted out of the frame loop into live VGPRs)
-            float4 wq = wbl;
-            const void *tw = A.tw;
-            unsigned ln = lane;
-            asm volatile("" : "+s"(tw), "+v"(wq.x), "+v"(wq.y), "+v"(wq.z), "+v"(wq.w), "+v"(ln));
-            dspb::cx2 P[32];
-            dspb_half_from_lds<B, SB>(P, ring + (unsigned)(f % DSPB_RING) * HS, fc, 0u, ln, wq, A.wa, A.wb);
-            dspb_half_from_lds<B, SB>(P + 16, ring + (unsigned)((f + 1) % DSPB_RING) * HS, fc, 1u, ln, wq, A.wa,
-                                      A.wb);
-            // the frame is in registers: past it (the LDS reads are complete
-            // before the release store)
-            if (lane == 0) dspb_st_rel(&ctl[1 + wave], (unsigned)(f + step - fa));
-            dspb::stft_frame_fft<true>(P, A.mag[fc] + f * A.ld, (const dspb::v2f *)tw, ln, tiles + wave * (64u * 33u));
-        }
-        if (lane == 0) dspb_st_rel(&ctl[1 + wave], 0x7fffffffu);  // done: never holds a slot again
-    }
-}
-#define DSPB_RSTFT_KERNEL(name, CC, BB)                                                 \
-    extern "C" __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void name( \
-        dspb_rstft_args A) {                                                            \
-        if constexpr (__is_empty(State)) dspb_rstft<CC, BB>(A);                          \
-    }
-DSPB_RSTFT_KERNEL(dspb_rstft_c2b512, 2, 512)
-DSPB_RSTFT_KERNEL(dspb_rstft_c2b256, 2, 256)
-DSPB_RSTFT_KERNEL(dspb_rstft_c2b1024, 2, 1024)
-DSPB_RSTFT_KERNEL(dspb_rstft_c1b512, 1, 512)
-DSPB_RSTFT_KERNEL(dspb_rstft_c1b256, 1, 256)
-DSPB_RSTFT_KERNEL(dspb_rstft_c1b1024, 1, 1024)
 // compute_IR (plugin.cpp:17-58): the callback once, on buffers as they are
 extern "C" __global__ void dspb_callback(dspb_render_args A) {
     float *ptrs[16];
@@ -689,9 +482,6 @@ struct dsp_module {
     // existed): [0] any (C, B), then the instantiations of kLdsShapes
     hipFunction_t f_render_lds[7] = {};
     hipFunction_t f_render_st[4] = {};  // kStShapes (NULL: dspb_render)
-    hipFunction_t f_rstft[6] = {};      // kRstftShapes (NULL: code compiled before them)
-    float *d_halo = nullptr;            // the fused kernel's halo hops
-    uint64_t halo_floats = 0;
     hipFunction_t f_sizes = nullptr, f_defaults = nullptr, f_init = nullptr, f_render = nullptr,
                   f_callback = nullptr;
     uint32_t params_size = 0, state_size = 0;
@@ -804,15 +594,8 @@ int dsp_module_compile(const char *source, const char *name, void **code, uint64
     tu += "#pragma clang force_cuda_host_device end\n";
     std::string note;
     tu += dspb::desc::generate(source, kPluginDeviceSrc, &note);
-    // the packed FFT of the fused render + STFT kernels, contracted into FMAs
-    // as libdspbench builds it (the plugin above keeps -ffp-contract=off)
-    tu += "#pragma clang fp contract(fast)\n#include \"stft_pk.hpp\"\n#pragma clang fp contract(off)\n";
     tu += kDriver;
     std::vector<const char *> hdrs = {kPluginDeviceSrc, source}, hnames = {"plugin_header.h", "dspb_plugin_source.cpp"};
-    for (int i = 0; i < kStftHdrCount; ++i) {
-        hdrs.push_back(kStftHdrTexts[i]);
-        hnames.push_back(kStftHdrNames[i]);
-    }
     hiprtcProgram prog;
     if (hiprtcCreateProgram(&prog, tu.c_str(), name ? name : "plugin.cpp", (int)hdrs.size(), hdrs.data(),
                             hnames.data()) != HIPRTC_SUCCESS) {
@@ -906,12 +689,6 @@ int dsp_module_load(const void *code, uint64_t code_size, int device, dsp_module
             m->f_render_lds[i] = nullptr;
         }
     }
-    for (int i = 0; i < 6; ++i) {
-        if (hipModuleGetFunction(&m->f_rstft[i], m->mod, kRstftShapes[i].name) != hipSuccess) {
-            (void)hipGetLastError();
-            m->f_rstft[i] = nullptr;
-        }
-    }
     for (int i = 0; i < 4; ++i) {
         if (hipModuleGetFunction(&m->f_render_st[i], m->mod, kStShapes[i].name) != hipSuccess) {
             (void)hipGetLastError();
@@ -950,7 +727,6 @@ void dsp_module_destroy(dsp_module *m) {
             if (m->arena_mem[i]) (void)hipFree(m->arena_mem[i]);
         }
         if (m->d_params) (void)hipFree(m->d_params);
-        if (m->d_halo) (void)hipFree(m->d_halo);
         for (hipEvent_t e : {m->upload_ev, m->use_ev})
             if (e) {
                 (void)hipEventSynchronize(e);
@@ -1219,13 +995,10 @@ static int check_device(const dsp_module *m) {
     return DSP_OK;
 }
 
-// dsp_render_offline / dsp_render_stft with DSP_PLUGIN_GENERIC (device buffers).
-// cont: this call renders the next chunk of a file whose earlier chunks were
-// rendered by the previous calls on the same stream (the pipelined render +
-// STFT of capi.cpp), so a plugin with State may start at goff > 0
+// dsp_render_offline / dsp_render_stft with DSP_PLUGIN_GENERIC (device buffers)
 int module_render(dsp_module *m, const void *params, uint32_t params_size, const float *const *in,
                   uint32_t in_ch, uint64_t L, float *const *out, uint32_t C, uint32_t B, float sr,
-                  uint64_t goff, hipStream_t s, bool cont) {
+                  uint64_t goff, hipStream_t s) {
     if (!m || !m->initialized) {
         set_last_error("GENERIC plugin: module not loaded / initialize_state not run");
         return DSP_ERR_INVALID;
@@ -1244,14 +1017,12 @@ int module_render(dsp_module *m, const void *params, uint32_t params_size, const
         set_last_error("sample_offset must be a multiple of B");
         return DSP_ERR_INVALID;
     }
-    if (!m->stateless && goff && !cont) {
+    if (!m->stateless && goff) {
         set_last_error("GENERIC plugin with State: whole files only (sample_offset 0)");
         return DSP_ERR_INVALID;
     }
     std::lock_guard<std::mutex> lk(m->mu);
-    // (a continuing chunk renders with the Parameters its first chunk uploaded)
-    if (!cont)
-        if (int st = upload_params(m, params, params_size, s)) return st;
+    if (int st = upload_params(m, params, params_size, s)) return st;
     RenderArgsG A{};
     A.P = m->d_params;
     A.S = m->d_state[0];
@@ -1319,73 +1090,6 @@ int module_render(dsp_module *m, const void *params, uint32_t params_size, const
     }
     MOD_HIP(hipModuleLaunchKernel(f, grid, 1, 1, block, 1, 1, lds_bytes, s, args, nullptr));
     MOD_HIP(hipEventRecord(m->use_ev, s));
-    return DSP_OK;
-}
-
-// dsp_render_stft with DSP_PLUGIN_GENERIC, fused (kDriver dspb_rstft): a
-// stateless plugin of a compiled shape (C, B), hop 4096, 4097 bins, the
-// computed cosine window (wbase, wa, wb: capi.cpp set_wincomp), device rows
-// that do not overlap.  *done = false (and nothing launched) when the module
-// has no fused kernel for the call; the caller pipelines render and STFT.
-int module_render_stft(dsp_module *m, const void *params, uint32_t params_size, const float *const *in,
-                       uint32_t in_ch, uint64_t L, float *const *out, uint32_t C, uint32_t B, float sr,
-                       float *const *mag, uint64_t ld, const void *tw, const void *wbase, float wa, float wb,
-                       hipStream_t s, bool *done) {
-    *done = false;
-    if (!m || !m->initialized || !m->stateless) return DSP_OK;
-    if (params_size != m->params_size || (!params && params_size) || in_ch > C) return DSP_OK;
-    int idx = -1;
-    for (int i = 0; i < 6; ++i)
-        if (m->f_rstft[i] && kRstftShapes[i].C == C && kRstftShapes[i].B == B) idx = i;
-    if (idx < 0) return DSP_OK;
-    if (int st = check_device(m)) return st;
-    const uint64_t nblocks = (L + B - 1) / B, Lr = nblocks * B;
-    if (Lr < 8192) return DSP_OK;
-    const uint64_t F = (Lr - 8192) / 4096 + 1;
-    const uint64_t G = std::min<uint64_t>(F, (uint64_t)m->cus);  // one workgroup of 8 waves per CU
-    std::lock_guard<std::mutex> lk(m->mu);
-    if (!m->d_halo) {  // the kernel's error word
-        MOD_HIP(hipMalloc(&m->d_halo, 64));
-        m->halo_floats = 16;
-    }
-    if (int st = upload_params(m, params, params_size, s)) return st;
-    MOD_HIP(hipMemsetAsync(m->d_halo, 0, 4, s));
-    RstftArgsG A{};
-    A.P = m->d_params;
-    A.S = m->d_state[0];
-    for (uint32_t c = 0; c < in_ch; ++c) A.in[c] = const_cast<float *>(in[c]);
-    for (uint32_t c = 0; c < C; ++c) {
-        A.out[c] = out[c];
-        A.mag[c] = mag[c];
-    }
-    A.L = L;
-    A.nblocks = nblocks;
-    A.F = F;
-    A.ld = ld;
-    A.halo = m->d_halo;
-    A.tw = tw;
-    A.wbase = wbase;
-    A.wa = wa;
-    A.wb = wb;
-    A.in_ch = in_ch;
-    A.sr = sr;
-    void *args[] = {&A};
-    // LDS (kDriver dspb_rstft): the 3-slot hop ring (4096 / B blocks of C B + 1
-    // floats each), the four FFT waves' 64 x 33 tiles, 8 control words
-    const uint64_t hs = (4096ull / B) * (C * B + 1);
-    const unsigned lds = (unsigned)(4 * (3 * hs + 4ull * 64 * 33 + 8));
-    MOD_HIP(hipModuleLaunchKernel(m->f_rstft[idx], (unsigned)G, 1, 1, 512, 1, 1, lds, s, args, nullptr));
-    if (const char *e = std::getenv("DSPB_RSTFT_CHECK"); e && e[0] == '1') {  // tests: the bounded waits held
-        unsigned w = 0;
-        MOD_HIP(hipMemcpyAsync(&w, m->d_halo, 4, hipMemcpyDeviceToHost, s));
-        MOD_HIP(hipStreamSynchronize(s));
-        if (w) {
-            set_last_error("dspb_rstft: a hand-off wait timed out (code %u)", w);
-            return DSP_ERR_HIP;
-        }
-    }
-    MOD_HIP(hipEventRecord(m->use_ev, s));
-    *done = true;
     return DSP_OK;
 }
 

@@ -479,68 +479,6 @@ __global__ __launch_bounds__(256, OCC) void stft8192_pk_kernel(Stft8kArgs A) {
     }
 }
 
-// The computed cosine window (stft8192_pk_kernel's WINC path) for pair j of
-// a frame: w = wa - wb cos(theta n), pre-scaled by 0.5 / sqrt N, from the
-// lane's base angles wbase = (cos, sin) of theta 2l, theta (2l + 1).  we / wo
-// weigh the even / odd samples of (x[2l + 256 j], x[2l + 256 j + 128]).
-__device__ __forceinline__ void win_pair(int j, float4 wbase, float wa, float wb, v2f &we, v2f &wo) {
-    const float ue = wb * wbase.x, ve = wb * wbase.y, uo = wb * wbase.z, vo = wb * wbase.w;
-    const v2f C = v2f{kWinB_c[2 * j], kWinB_c[2 * j + 1]}, S = v2f{kWinB_s[2 * j], kWinB_s[2 * j + 1]};
-    we = (v2f{ve, ve} * S + v2f{wa, wa}) - v2f{ue, ue} * C;
-    wo = (v2f{vo, vo} * S + v2f{wa, wa}) - v2f{uo, uo} * C;
-}
-
-// FFT and 4097 magnitudes of a windowed frame P (P[j] = the even / odd
-// samples of (x[2l + 256 j], x[2l + 256 j + 128]) times the window).  LO: the
-// low-footprint transform (fft4096_pk_y2_lo: twiddles loaded just in time,
-// the 64 x 33 transpose tile), for kernels that run frames in a loop beside
-// other live state; else the stage twiddles are loaded first and the tile is
-// 64 x 65.  tw: capi.cpp get_tw's table.
-template <bool LO>
-__device__ __forceinline__ void stft_frame_fft(cx2 (&P)[32], float *mrow, const v2f *tw, uint32_t lane, float *lds) {
-    cx2 Y2[32];
-    if constexpr (LO) {
-        fft4096_pk_y2_lo<true>(P, lds, tw, lane, Y2);
-    } else {
-        cx tlo[8];
-        cx2 thp[4];
-#pragma unroll
-        for (int j = 1; j < 8; ++j) {
-            const v2f a = (tw + 8192u + 64u * (uint32_t)(j - 1))[lane];
-            tlo[j] = cx{a.x, a.y};
-        }
-        const float4 *tp4 = reinterpret_cast<const float4 *>(tw + 8192u + 896u);
-#pragma unroll
-        for (int h = 0; h < 4; ++h) {
-            const float4 t = tp4[64u * (uint32_t)h + lane];
-            thp[h] = cx2{v2f{t.x, t.y}, v2f{t.z, t.w}};
-        }
-        fft4096_pk_y2<true, true>(P, lds, tlo, thp, lane, Y2);
-    }
-    split_y2<kKHalf, true>(Y2, mrow, 4097u, tw, lane, lds);
-}
-
-// One 8192-point frame of a signal in memory (4097 magnitudes into mrow):
-// the memory-source path of stft8192_pk_kernel as a device function.  The
-// frame's first and second 4096 samples start at lo and hi (hi = lo + 4096
-// for a contiguous frame; 8-byte aligned), so a frame can be assembled from
-// two buffers.  lds: this wave's 64 x 65 float tile.
-template <bool LO = false>
-__device__ __forceinline__ void stft_frame_split(const float *lo, const float *hi, float *mrow, const v2f *tw,
-                                                 float4 wbase, float wa, float wb, uint32_t lane, float *lds) {
-    cx2 P[32];
-#pragma unroll
-    for (int j = 0; j < 32; ++j) {
-        v2f we, wo;
-        win_pair(j, wbase, wa, wb, we, wo);
-        const float *x = j < 16 ? lo + 256u * (uint32_t)j : hi + 256u * (uint32_t)(j - 16);
-        const v2f a = reinterpret_cast<const v2f *>(x)[lane];
-        const v2f b = reinterpret_cast<const v2f *>(x + 128u)[lane];
-        P[j] = cx2{v2f{a.x, b.x} * we, v2f{a.y, b.y} * wo};
-    }
-    stft_frame_fft<LO>(P, mrow, tw, lane, lds);
-}
-
 // the launches of stft_pk_paths.hip / stft_pk_ab.hip (DSP_OK or a status)
 int launch_pk_paths(const Stft8kArgs &A, bool fused, int km, bool pow2, bool winc, dim3 grid, hipStream_t s);
 int launch_pk_ab(const Stft8kArgs &A, bool fused, int opt, dim3 grid, hipStream_t s);

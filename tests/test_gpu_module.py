@@ -199,15 +199,6 @@ def test_generic_ir_analysis_and_stft(torch_cuda, oracle):
     assert float((mg - mg2).abs().max()) <= 1e-6 * float(mg2.max())
 
 
-@pytest.fixture
-def small_chunks(monkeypatch):
-    """The pipelined GENERIC render + STFT (capi.cpp generic_render_stft) in
-    1 MiB chunks, so a short file crosses many chunk boundaries; the fused
-    kernel off (DSPB_GENERIC_FUSED=0)."""
-    monkeypatch.setenv("DSPB_PIPE_CHUNK_BYTES", str(1 << 20))
-    monkeypatch.setenv("DSPB_GENERIC_FUSED", "0")
-
-
 def _check_stft(oracle, got, m, tol=1e-6):
     """every frame's 4097 magnitudes against float64, from the GPU's own render"""
     F = m.shape[1]
@@ -220,93 +211,39 @@ def _check_stft(oracle, got, m, tol=1e-6):
 
 
 @pytest.mark.gpu
-# the fused kernel (module.cpp dspb_rstft) for every compiled shape (C, B):
-# lengths of 1 frame (one workgroup), a few frames (one frame per workgroup:
-# every range but the last ends in a halo hop), and more frames than the
-# persistent grid (ranges of 2+ frames, the LDS ring wrapping); ragged files
-# (zero past EOF, a partial last hop), a mono file into stereo
-@pytest.mark.parametrize("name", ["gain_test", "IR_test", "handmade_test"])
-@pytest.mark.parametrize("cin,C,B", [(2, 2, 512), (1, 2, 256), (2, 2, 1024), (1, 1, 512), (1, 1, 256),
-                                     (1, 1, 1024)])
-@pytest.mark.parametrize("L", [8192, 5 * 8192 + 1000, 600 * 8192 + 77])
-def test_generic_render_stft_fused(torch_cuda, oracle, monkeypatch, name, cin, C, B, L):
+# dsp_render_stft with a plugin compiled from source (render, then the STFT
+# of the render): stateless (gain_test, IR_test, handmade_test) and stateful
+# (sine_test) plugins; the LDS-blocks kernels' constant shapes (2, 512),
+# (2, 256), (1, 512) and generic ones (2, 384; 2, 100 from a mono file);
+# one frame, a few frames, and a ragged file past the persistent grid
+@pytest.mark.parametrize("name", ["gain_test", "IR_test", "handmade_test", "sine_test"])
+@pytest.mark.parametrize("cin,C,B", [(2, 2, 512), (1, 2, 256), (1, 1, 512), (2, 2, 384), (1, 2, 100)])
+@pytest.mark.parametrize("L", [8192, 5 * 8192 + 1000, 600_077])
+def test_generic_render_stft(torch_cuda, oracle, name, cin, C, B, L):
     if not have(name):
         pytest.skip("modules / oracle/_ref not built")
-    monkeypatch.setenv("DSPB_RSTFT_CHECK", "1")  # the kernel's bounded hand-off waits all held
     torch = torch_cuda
     mod = load(name)
     params = mod.default_parameters()
     mod.initialize_state(params, C, 48000.0)
     ref = oracle.RefPlugin(name, C, 48000.0)
     x = np.random.default_rng(L + B).uniform(-1, 1, (cin, L)).astype(np.float32)
-    xg = torch.from_numpy(x).cuda()
-    d.lib().dsp_kernel_timing(None, None, None)
-    out, mag = d.render_stft(xg, C, B, 48000.0, mod.plugin(params, name))
+    out, mag = d.render_stft(torch.from_numpy(x).cuda(), C, B, 48000.0, mod.plugin(params, name))
     got = out.cpu().numpy()
     want = oracle.render_offline([x[c] for c in range(cin)], C, B, 48000.0, ref.as_oracle())
-    assert np.array_equal(got, want)
-    m = mag.cpu().numpy()
-    if L > 1_000_000:  # the float64 STFT of every frame: sampled channels' frames on the long file
-        for c in range(C):
-            idx = np.r_[0:3, m.shape[1] // 2, m.shape[1] - 3:m.shape[1]]
-            mref = oracle.np_stft_mag(got[c], 8192, 4096, oracle.WIN_HANN, 4097)[idx]
-            err = np.abs(m[c][idx] - mref).max(axis=1) / np.maximum(mref.max(axis=1), 1e-30)
-            assert err.max() <= 1e-6  # (a silent channel: exact zeros on both sides)
-        # every frame against the pipelined path (render bits equal, spectra
-        # within 1e-6 of each frame's peak: two builds of the same FFT)
-        import os as _os
-        _os.environ["DSPB_GENERIC_FUSED"] = "0"
-        try:
-            out2, mag2 = d.render_stft(xg, C, B, 48000.0, mod.plugin(params, name))
-        finally:
-            del _os.environ["DSPB_GENERIC_FUSED"]
-        assert torch.equal(out2, out)
-        rel = ((mag - mag2).abs().amax(dim=2) / mag2.amax(dim=2).clamp_min(1e-30)).max()
-        assert float(rel) <= 1e-6
-    else:
-        _check_stft(oracle, got, m)
-
-
-@pytest.mark.gpu
-# stateless (gain_test, IR_test, handmade_test) and stateful (sine_test: its
-# State continues across the chunks on the render stream); B = 512 divides
-# H, B = 384 does not (frames straddle chunk ends), B = 100 with a mono file
-# into stereo
-@pytest.mark.parametrize("name", ["gain_test", "IR_test", "handmade_test", "sine_test"])
-@pytest.mark.parametrize("cin,B", [(2, 512), (2, 384), (1, 100)])
-def test_generic_render_stft_pipelined(torch_cuda, oracle, small_chunks, name, cin, B):
-    if not have(name):
-        pytest.skip("modules / oracle/_ref not built")
-    torch = torch_cuda
-    mod = load(name)
-    params = mod.default_parameters()
-    ref = oracle.RefPlugin(name, 2, 48000.0)
-    L = 600_000 + 77  # 4.8 MB of stereo render: 5+ chunks of 1 MiB, ragged last block
-    x = np.random.default_rng(11).uniform(-1, 1, (cin, L)).astype(np.float32)
-    xg = torch.from_numpy(x).cuda()
-    mod.initialize_state(params, 2, 48000.0)
-    out, mag = d.render_stft(xg, 2, B, 48000.0, mod.plugin(params, name))
-    torch.cuda.synchronize()
-    got = out.cpu().numpy()
-    want = oracle.render_offline([x[c] for c in range(cin)], 2, B, 48000.0, ref.as_oracle())
     if name in TOL:
         assert np.max(np.abs(got - want)) <= TOL[name]
     else:
         assert np.array_equal(got, want)
     _check_stft(oracle, got, mag.cpu().numpy())
-    # one chunk (no pipeline) gives the same bits
-    os.environ["DSPB_PIPE_CHUNK_BYTES"] = str(1 << 40)
-    mod.initialize_state(params, 2, 48000.0)
-    out1, mag1 = d.render_stft(xg, 2, B, 48000.0, mod.plugin(params, name))
-    assert torch.equal(out1, out) and torch.equal(mag1, mag)
 
 
 @pytest.mark.gpu
-def test_generic_render_stft_pipelined_full_hour(torch_cuda, oracle):
+def test_generic_render_stft_full_hour(torch_cuda, oracle):
     """1 h of 48 kHz stereo: IR_test.cpp compiled unchanged through the
-    pipelined generic path (43 chunks of 32 MiB) gives the specialised fused
-    kernel's render bit for bit and its spectra within 1e-6 of each frame's
-    peak (two FFT kernels: the fused PER path and the memory path)."""
+    generic path gives the specialised fused kernel's render bit for bit and
+    its spectra within 1e-6 of each frame's peak (two FFT kernels: the fused
+    PER path and the memory path)."""
     if not have("IR_test"):
         pytest.skip("modules / oracle/_ref not built")
     torch = torch_cuda

@@ -1,5 +1,5 @@
 # GPU session: generic-driver module tests + generic benches (render only,
-# render + STFT pipelined, a chunk-size sweep of the pipeline)
+# render + STFT)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
@@ -11,4 +11,3 @@ run b_generic --workload generic
 run b_generic_ir --workload generic --plugin IR_test
 run b_gstft_ir --workload generic_stft
 run b_gstft_gain --workload generic_stft --plugin gain_test
-DSPB_GENERIC_FUSED=0 DSPB_PIPE_CHUNK_BYTES=67108864 run b_gstft_ir_pipe --workload generic_stft
