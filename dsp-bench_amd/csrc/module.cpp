@@ -307,42 +307,53 @@ __device__ static void dspb_stateless_lds(const dspb_render_args &A) {
         __syncthreads();
     }
 }
-// blocks per round of the LDS-blocks path (the host computes the same:
-// module.cpp lds_round_blocks)
-constexpr unsigned dspb_lds_nb(unsigned C, unsigned B) {
-    const unsigned v = 76u * 1024u / ((C * B + 1u) * 4u) / 4u * 4u;
+// blocks per round of the LDS-blocks path at a block stride of SB floats
+// (the host computes the same: module.cpp lds_round)
+constexpr unsigned dspb_lds_nb(unsigned SB) {
+    const unsigned v = 76u * 1024u / (SB * 4u) / 4u * 4u;
     return v < 64u ? v : 64u;
 }
-// the LDS-blocks path for a constant shape (C, B), software pipelined over
-// the workgroup's rounds: a persistent grid of two workgroups per CU walks
-// the file, and while round r's callbacks run in LDS, the next round's file
-// samples are already in flight into registers (PT floats per thread and
-// channel, every load issued at once), so a round costs its callbacks and one
-// copy out, not a chain of dependent HBM loads.  Rounds the file does not
-// cover completely (EOF, the ragged last round) take render_audio's copy
-// with zeros instead.  The copies move one dword per lane at consecutive
-// addresses (LDS conflict-free; a block's row stride C B + 1 is odd, so the
-// callback lanes' accesses are conflict-free too).
+// the LDS-blocks path for a constant shape (C, B, 4 | B), software
+// pipelined over the workgroup's rounds: a persistent grid of two
+// workgroups per CU walks the file, and while round r's callbacks run in LDS,
+// the next round's file samples are already in flight into registers (16-byte
+// loads, all issued at once), so a round costs its callbacks and one copy
+// out, not a chain of dependent HBM loads.  Rounds the file does not cover
+// completely (EOF, the ragged last round) or an unaligned file take
+// render_audio's copy with zeros instead.  Block rows at a stride of C B + 2
+// floats: 8-byte aligned (the copies move float2 pairs through LDS, 16-byte
+// rows to and from HBM) and conflict-free for the 16 callback lanes of a
+// stereo B = 512 round.
 template <unsigned CC, unsigned BB>
 __device__ static void dspb_stateless_lds_pf(const dspb_render_args &A) {
     extern __shared__ float dspb_lbuf[];
-    constexpr unsigned C = CC, B = BB, SB = C * B + 1u, NB = dspb_lds_nb(C, B);
-    constexpr unsigned N1 = NB * B, PT = (N1 + 255u) / 256u;  // floats per channel per round / per thread
-    static_assert(NB <= 64, "one wave runs a round's callbacks");
+    constexpr unsigned C = CC, B = BB, SB = C * B + 2u, NB = dspb_lds_nb(SB);
+    constexpr unsigned N4 = NB * B / 4u, PT = (N4 + 255u) / 256u;  // float4 per channel per round / per thread
+    static_assert(NB <= 64 && B % 4 == 0, "one wave runs a round's callbacks");
+    typedef __attribute__((address_space(1))) float4 gfloat4;
     State local = dspb_from_global<State>(A.S);
     Parameters prm = dspb_from_global<Parameters>(A.P);
     const unsigned t = threadIdx.x, lane = t & 63u;
     const unsigned long long stride = (unsigned long long)gridDim.x * NB;
-    auto full = [&](unsigned long long b0) { return b0 + NB <= A.nblocks && (b0 + NB) * B <= A.L; };
-    float pf[C][PT];
+    bool aligned_in = true;
+    for (unsigned c = 0; c < C && c < A.in_ch; ++c) aligned_in = aligned_in && !(((unsigned long long)A.in[c]) & 15);
+    auto full = [&](unsigned long long b0) {
+        return b0 + NB <= A.nblocks && (A.in_ch == 0 || ((b0 + NB) * B <= A.L && aligned_in));
+    };
+    float4 pf[C][PT];
     auto load = [&](unsigned long long b0) {
 #pragma unroll
         for (unsigned c = 0; c < C; ++c) {
-            const dspb_gfloat *x = (const dspb_gfloat *)A.in[c < A.in_ch ? c : 0] + b0 * B;
+            const gfloat4 *x4 = (const gfloat4 *)(A.in[c < A.in_ch ? c : 0] + b0 * B);
 #pragma unroll
             for (unsigned k = 0; k < PT; ++k) {
                 const unsigned i = t + 256u * k;
-                pf[c][k] = (c < A.in_ch && (N1 % 256u == 0 || i < N1)) ? x[i] : 0.0f;
+                if (c < A.in_ch && (N4 % 256u == 0 || i < N4)) {
+                    const float4 v = x4[i];
+                    pf[c][k] = v;
+                } else {
+                    pf[c][k] = make_float4(0.f, 0.f, 0.f, 0.f);
+                }
             }
         }
     };
@@ -356,11 +367,14 @@ __device__ static void dspb_stateless_lds_pf(const dspb_render_args &A) {
         if (have) {
 #pragma unroll
             for (unsigned c = 0; c < C; ++c) {
-                float *row = dspb_lbuf + c * B;
 #pragma unroll
                 for (unsigned k = 0; k < PT; ++k) {
-                    const unsigned j = t + 256u * k;
-                    if (N1 % 256u == 0 || j < N1) row[(j / B) * SB + j % B] = pf[c][k];
+                    const unsigned j = 4u * (t + 256u * k);
+                    if (N4 % 256u == 0 || j < 4u * N4) {
+                        float2 *d = (float2 *)(dspb_lbuf + (j / B) * SB + c * B + j % B);
+                        d[0] = make_float2(pf[c][k].x, pf[c][k].y);
+                        d[1] = make_float2(pf[c][k].z, pf[c][k].w);
+                    }
                 }
             }
         } else {  // render_audio's copy with zeros past EOF and for missing channels
@@ -368,8 +382,7 @@ __device__ static void dspb_stateless_lds_pf(const dspb_render_args &A) {
             for (unsigned c = 0; c < C; ++c) {
                 const dspb_gfloat *x = (const dspb_gfloat *)A.in[c < A.in_ch ? c : 0] + i0;
                 const unsigned long long m = c < A.in_ch ? lim : 0;
-                float *row = dspb_lbuf + c * B;
-                for (unsigned j = t; j < n; j += 256u) row[(j / B) * SB + j % B] = j < m ? x[j] : 0.0f;
+                for (unsigned j = t; j < n; j += 256u) dspb_lbuf[(j / B) * SB + c * B + j % B] = j < m ? x[j] : 0.0f;
             }
         }
         __syncthreads();
@@ -386,10 +399,18 @@ __device__ static void dspb_stateless_lds_pf(const dspb_render_args &A) {
         }
         __syncthreads();
         for (unsigned c = 0; c < C; ++c) {
-            dspb_gfloat *o = (dspb_gfloat *)A.out[c] + i0;
-            const float *row = dspb_lbuf + c * B;
-#pragma unroll 8
-            for (unsigned j = t; j < n; j += 256u) o[j] = row[(j / B) * SB + j % B];
+            if ((((unsigned long long)A.out[c]) & 15) == 0) {
+                gfloat4 *o4 = (gfloat4 *)(A.out[c] + i0);
+#pragma unroll 4
+                for (unsigned j = 4u * t; j < n; j += 1024u) {
+                    const float2 *d = (const float2 *)(dspb_lbuf + (j / B) * SB + c * B + j % B);
+                    const float2 lo = d[0], hi = d[1];
+                    o4[j / 4u] = make_float4(lo.x, lo.y, hi.x, hi.y);
+                }
+            } else {
+                dspb_gfloat *o = (dspb_gfloat *)A.out[c] + i0;
+                for (unsigned j = t; j < n; j += 256u) o[j] = dspb_lbuf[(j / B) * SB + c * B + j % B];
+            }
         }
         __syncthreads();
     }
@@ -1042,8 +1063,7 @@ int module_render(dsp_module *m, const void *params, uint32_t params_size, const
         // default: the LDS-blocks path (dspb_render_lds) when a round of at
         // least 4 blocks fits the per-workgroup LDS budget, else the
         // in-place wave path; DSPB_STATELESS_PATH=0/3 forces one
-        const uint64_t stride = (uint64_t)C * B + 1;
-        const uint64_t nb = std::min<uint64_t>(64, kLdsRoundBytes / (stride * sizeof(float)) / 4 * 4);
+        uint64_t stride = (uint64_t)C * B + 1;
         // the most specific instantiation for (C, B): exact shapes first (the
         // software-pipelined rounds of dspb_stateless_lds_pf, on a persistent
         // grid of two workgroups per CU)
@@ -1057,6 +1077,10 @@ int module_render(dsp_module *m, const void *params, uint32_t params_size, const
         for (int i = 6; i >= 0 && !f; --i)
             if (m->f_render_lds[i] && (!kLdsShapes[i].C || kLdsShapes[i].C == C) && !kLdsShapes[i].B)
                 f = m->f_render_lds[i];
+        // rounds of nb blocks at a block stride of C B + 1 floats, C B + 2 for
+        // the pipelined kernels (kDriver dspb_lds_nb: the same formula)
+        if (persistent) stride = (uint64_t)C * B + 2;
+        const uint64_t nb = std::min<uint64_t>(64, kLdsRoundBytes / (stride * sizeof(float)) / 4 * 4);
         int path = stateless_path_forced();
         if (path < 0) path = nb >= 4 ? 3 : 0;
         if (path == 3 && (nb < 4 || !f)) path = 0;
