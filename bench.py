@@ -380,10 +380,10 @@ def main():
                               K=K_BINS, out=out, mag=mag)
             workload = (f"{pname}.cpp via the generic plugin driver (B=512) + 8192-pt Hann STFT, hop 4096, "
                         f"4097 bins, {minutes:g} min of 48 kHz stereo per GPU")
-            kname = ("dspb_render_lds (generic driver) + stft8192_pk<memory>, pipelined in 32 MiB chunks "
-                     "on two streams (one region, dsp_render_stft)")
-            alg_desc = ("C*L*(4 + 4) + C*F*4K B (file read + render write + |X| write; the STFT's read of "
-                        "the render is served by the Infinity Cache)")
+            kname = ("dspb_render_lds (generic driver) then stft8192_pk<memory> on one stream (one timed "
+                     "region, dsp_render_stft)")
+            alg_desc = ("C*L*(4 + 4) + C*F*4K B (file read + render write + |X| write; the STFT's re-read of "
+                        "the render is extra traffic, not counted)")
     else:
         bits = 16 if wl == "wav16" else 24
         pay = torch.randint(0, 256, (CH * L_in * bits // 8,), dtype=torch.uint8, device=dev, generator=g)
@@ -591,8 +591,9 @@ def main():
                             if wl in ("headline", "ch96k") else
                             "one lane per block: the plugin callback runs serially over its block in LDS, "
                             "16 blocks per 64 KB workgroup round (DESIGN 4.6)" if wl == "generic" else
-                            "render (LDS-capacity-bound callbacks) overlapped with the power-capped FFT "
-                            "(DESIGN 4.6)" if wl == "generic_stft" else None),
+                            "the render (LDS-capacity-bound callbacks) then the power-capped memory STFT, "
+                            "serial: DESIGN 4.6, profiles/r02_generic_stft_schedules.txt"
+                            if wl == "generic_stft" else None),
             }),
             "cpu_baseline": cpu,
         }

@@ -8,7 +8,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mode=${1:-all}
-tag=${2:-r01}
+tag=${2:-r02}
 out=gpurun_out
 mkdir -p $out
 
@@ -43,8 +43,9 @@ if [[ $mode == prof || $mode == all ]]; then
     python tools/trace_avg.py $out/prof_$tag/run_kernel_trace.csv stft8192_pk 200 100 | tee $out/prof_$tag/trace_avg.txt
 fi
 if [[ $mode == others || $others == 1 ]]; then
-    for wl in gain10min stft96k ch96k fir1024 wav16 wav24 generic; do
+    for wl in gain10min stft96k ch96k fir1024 wav16 wav24 ir generic generic_stft; do
         run bench_$wl 300 python bench.py --workload $wl --no-cpu-baseline
     done
+    run bench_generic_stft_gain 300 python bench.py --workload generic_stft --plugin gain_test --no-cpu-baseline
 fi
 echo "=== done"
