@@ -361,7 +361,9 @@ def main():
         # gfx950, dsp-bench_amd/modules/mod_*.co, built by
         # tools/make_plugin_modules.py) and run by the generic driver
         pname = args.plugin or ("gain_test" if wl == "generic" else "IR_test")
-        with open(os.path.join(REPO, "dsp-bench_amd", "modules", f"mod_{pname}.co"), "rb") as f:
+        # (DSPB_MODULES_DIR: A/B builds of the driver, tools/build_lds_variants.sh)
+        mdir = os.environ.get("DSPB_MODULES_DIR", os.path.join(REPO, "dsp-bench_amd", "modules"))
+        with open(os.path.join(mdir, f"mod_{pname}.co"), "rb") as f:
             gmod = d.module.Module(f.read())
         gparams = gmod.default_parameters()
         gmod.initialize_state(gparams, CH, float(sr))

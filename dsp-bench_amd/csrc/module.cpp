@@ -35,6 +35,15 @@ namespace {
 #include "plugin_device_src.inc"  // const char kPluginDeviceSrc[] (generated from plugin_device.h)
 
 constexpr uint64_t kStagedLdsBytes = 64 * 1024;  // stateful render's LDS double-buffer limit
+#ifndef DSPB_LDS_ROUND
+#define DSPB_LDS_ROUND (76 * 1024)
+#define DSPB_LDS_WGS 2
+#endif
+// LDS per workgroup round of the stateless LDS-blocks path (kDriver
+// dspb_lds_nb: the same formula, handed to hiprtc as DSPB_LDS_ROUND_BYTES),
+// and the persistent grid's workgroups per CU
+constexpr uint64_t kLdsRoundBytes = DSPB_LDS_ROUND;
+constexpr uint64_t kLdsWgPerCu = DSPB_LDS_WGS;
 
 // the LDS-blocks kernels of kDriver: (C, B) = 0 matches any value
 struct LdsShape {
@@ -310,7 +319,7 @@ __device__ static void dspb_stateless_lds(const dspb_render_args &A) {
 // blocks per round of the LDS-blocks path at a block stride of SB floats
 // (the host computes the same: module.cpp lds_round)
 constexpr unsigned dspb_lds_nb(unsigned SB) {
-    const unsigned v = 76u * 1024u / (SB * 4u) / 4u * 4u;
+    const unsigned v = DSPB_LDS_ROUND_BYTES / (SB * 4u) / 4u * 4u;
     return v < 64u ? v : 64u;
 }
 // the LDS-blocks path for a constant shape (C, B, 4 | B), software
@@ -623,7 +632,8 @@ int dsp_module_compile(const char *source, const char *name, void **code, uint64
         set_last_error("hiprtcCreateProgram failed");
         return DSP_ERR_INVALID;
     }
-    const char *opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++20", "-ffp-contract=off", "-w"};
+    const std::string round = "-DDSPB_LDS_ROUND_BYTES=" + std::to_string(kLdsRoundBytes) + "u";
+    const char *opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++20", "-ffp-contract=off", "-w", round.c_str()};
     const hiprtcResult rc = hiprtcCompileProgram(prog, (int)(sizeof opts / sizeof *opts), opts);
     size_t ls = 0;
     hiprtcGetProgramLogSize(prog, &ls);
@@ -981,7 +991,7 @@ static int stateless_path_forced() {
     return v;
 }
 // the LDS-blocks path: LDS per workgroup round (two workgroups per CU)
-constexpr uint64_t kLdsRoundBytes = 76 * 1024;  // (kDriver dspb_lds_nb: the same formula)
+
 
 // the caller's Parameters blob -> the module's device Parameters, stream
 // ordered: through a pinned staging copy (reused once the previous upload
@@ -1089,7 +1099,7 @@ int module_render(dsp_module *m, const void *params, uint32_t params_size, const
             A.lds_nb = (unsigned)nb;
             A.lds_stride = (unsigned)stride;
             uint64_t g = (A.nblocks + nb - 1) / nb;
-            if (persistent) g = std::min<uint64_t>(g, 2ull * m->cus);
+            if (persistent) g = std::min<uint64_t>(g, kLdsWgPerCu * m->cus);
             MOD_HIP(hipModuleLaunchKernel(f, (unsigned)(g < (1u << 20) ? g : (1u << 20)), 1, 1, 256, 1, 1,
                                           (unsigned)(nb * stride * sizeof(float)), s, args, nullptr));
             MOD_HIP(hipEventRecord(m->use_ev, s));

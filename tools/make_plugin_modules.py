@@ -24,8 +24,8 @@ PLUGINS = ["build/gain_test", "build/IR_test", "build/sine_test", "build/buffer_
            "test/plugin_with_parameters"]
 
 
-LIB = os.path.join(ROOT, "dsp-bench_amd", "libdspbench.so")
-OUT = os.path.join(ROOT, "dsp-bench_amd", "modules")
+LIB = os.environ.get("DSPBENCH_LIB", os.path.join(ROOT, "dsp-bench_amd", "libdspbench.so"))
+OUT = os.environ.get("DSPB_MODULES_DIR", os.path.join(ROOT, "dsp-bench_amd", "modules"))
 
 
 def main():
