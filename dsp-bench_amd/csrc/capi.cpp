@@ -93,6 +93,15 @@ struct DeviceGuard {
     }
 };
 
+// Synchronous upload of a constant table (launch_upload: kernel arguments,
+// not a copy -- see render.hip); the tables are shared by every stream of the
+// device, so the upload completes before the first use.
+static int upload_table(void *dst, const void *src, size_t bytes) {
+    if (int st = launch_upload((float *)dst, (const float *)src, bytes / sizeof(float), nullptr)) return st;
+    DSPB_HIP(hipStreamSynchronize(nullptr));
+    return DSP_OK;
+}
+
 static int get_tw(int dev, const v2f **out) {
     std::lock_guard<std::mutex> lk(g_mu);
     DeviceRes &r = g_res[dev];
@@ -119,8 +128,13 @@ static int get_tw(int dev, const v2f **out) {
                 h.push_back(v2f{a.x, b.x});
                 h.push_back(v2f{a.y, b.y});
             }
-        DSPB_HIP(hipMalloc(&r.tw8192, sizeof(v2f) * h.size()));
-        DSPB_HIP(hipMemcpy(r.tw8192, h.data(), sizeof(v2f) * h.size(), hipMemcpyHostToDevice));
+        v2f *d = nullptr;
+        DSPB_HIP(hipMalloc(&d, sizeof(v2f) * h.size()));
+        if (int st = upload_table(d, h.data(), sizeof(v2f) * h.size())) {
+            (void)hipFree(d);
+            return st;
+        }
+        r.tw8192 = d;
     }
     *out = r.tw8192;
     return DSP_OK;
@@ -135,8 +149,13 @@ static int get_delta(int dev, const float **out) {
     if (!r.delta) {
         std::vector<float> h(kDeltaLen, 0.0f);
         h[0] = 1.0f;
-        DSPB_HIP(hipMalloc(&r.delta, sizeof(float) * kDeltaLen));
-        DSPB_HIP(hipMemcpy(r.delta, h.data(), sizeof(float) * kDeltaLen, hipMemcpyHostToDevice));
+        float *d = nullptr;
+        DSPB_HIP(hipMalloc(&d, sizeof(float) * kDeltaLen));
+        if (int st = upload_table(d, h.data(), sizeof(float) * kDeltaLen)) {
+            (void)hipFree(d);
+            return st;
+        }
+        r.delta = d;
     }
     *out = r.delta;
     return DSP_OK;
@@ -160,7 +179,7 @@ static int get_window(int dev, int kind, uint32_t N, uint32_t valid, const float
                           : (float)(scale * (a - b * std::cos(2.0 * M_PI * (double)n / (double)(valid - 1))));
     float *d = nullptr;
     DSPB_HIP(hipMalloc(&d, sizeof(float) * N));
-    DSPB_HIP(hipMemcpy(d, h.data(), sizeof(float) * N, hipMemcpyHostToDevice));
+    if (int st = upload_table(d, h.data(), sizeof(float) * N)) return st;
     r.windows[key] = d;
     *out = d;
     return DSP_OK;
@@ -182,8 +201,13 @@ static int set_wincomp(int dev, int kind, Stft8kArgs *A) {
             for (int l = 0; l < 64; ++l)
                 h[l] = float4{(float)std::cos(th * 2 * l), (float)std::sin(th * 2 * l),
                               (float)std::cos(th * (2 * l + 1)), (float)std::sin(th * (2 * l + 1))};
-            DSPB_HIP(hipMalloc(&r.wbase, sizeof(float4) * 64));
-            DSPB_HIP(hipMemcpy(r.wbase, h.data(), sizeof(float4) * 64, hipMemcpyHostToDevice));
+            float4 *d = nullptr;
+            DSPB_HIP(hipMalloc(&d, sizeof(float4) * 64));
+            if (int st = upload_table(d, h.data(), sizeof(float4) * 64)) {
+                (void)hipFree(d);
+                return st;
+            }
+            r.wbase = d;
         }
         A->wbase = r.wbase;
     }
@@ -423,7 +447,7 @@ static int plugin_map(const dsp_plugin *p, uint32_t B, int dev, hipStream_t s, S
                 if (T <= 1025) ols_table(h.data(), T, h.data() + T8);
                 float *d = nullptr;
                 DSPB_HIP(hipMalloc(&d, sizeof(float) * h.size()));
-                DSPB_HIP(hipMemcpy(d, h.data(), sizeof(float) * h.size(), hipMemcpyHostToDevice));
+                if (int st = upload_table(d, h.data(), sizeof(float) * h.size())) return st;
                 if (r.fir.size() >= 8) {  // small LRU-ish cap
                     (void)hipFree(r.fir.front().dev);
                     r.fir.erase(r.fir.begin());

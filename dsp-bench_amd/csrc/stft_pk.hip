@@ -4,6 +4,32 @@
 
 namespace dspb {
 
+// Host -> device upload of the library's small constant tables through
+// kernel arguments.  The first hipMemcpy of more than a few KB in a process,
+// pageable or pinned, costs 7-8 ms (copy-engine start-up,
+// tools/copy_init_probe.cpp; 0.02 ms afterwards) and was most of a cold
+// call; ~4 KB of kernel arguments per launch costs microseconds.  Here, in
+// the headline's translation unit, so that a cold headline call loads one
+// code object.
+constexpr uint32_t kUploadFloats = 960;
+struct UploadChunk {
+    uint32_t n;
+    float v[kUploadFloats];
+};
+__global__ void upload_kernel(float *dst, UploadChunk c) {
+    for (uint32_t i = threadIdx.x; i < c.n; i += blockDim.x) dst[i] = c.v[i];
+}
+int launch_upload(float *dst, const float *src, uint64_t n, hipStream_t s) {
+    UploadChunk c;
+    for (uint64_t off = 0; off < n; off += kUploadFloats) {
+        c.n = (uint32_t)(n - off < kUploadFloats ? n - off : kUploadFloats);
+        for (uint32_t i = 0; i < c.n; ++i) c.v[i] = src[off + i];
+        hipLaunchKernelGGL(upload_kernel, dim3(1), dim3(256), 0, s, dst + off, c);
+        DSPB_HIP(hipGetLastError());
+    }
+    return DSP_OK;
+}
+
 // true when launch_stft8192_pk runs the PER kernel for these arguments --
 // the fused path that evaluates a closed-form IR ramp itself and renders the
 // tail past the last frame's hop (A.tail_end)
