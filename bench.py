@@ -60,14 +60,16 @@ def parse():
                     help="fir1024: 0 auto (overlap-save), 1 direct form, 2 overlap-save")
     ap.add_argument("--workload", default="headline",
                     choices=["headline", "stft96k", "ch96k", "gain10min", "fir1024", "wav16", "wav24", "ir",
-                             "generic", "generic_stft"],
+                             "generic", "generic_stft", "gain_stft"],
                     help="headline = IR_test + STFT 48 kHz (the metric); stft96k = BASELINE cfg 4 "
                          "(STFT of 1 h stereo 96 kHz from HBM); gain10min = cfg 2 render; "
                          "wav16 / wav24 = GPU decode of a 1 h stereo int16 / int24 WAV payload; "
                          "ch96k = BASELINE cfg 5: one 96 kHz channel per GPU through IR_test + STFT; "
                          "ir = compute_IR + fft_perform_and_get_magnitude latency (one 8192-pt frame per call); "
                          "generic = a reference plugin source through the generic driver (render only); "
-                         "generic_stft = the same + the 8192-pt STFT (render and STFT pipelined)")
+                         "generic_stft = the same + the 8192-pt STFT (render, then the STFT, one stream); "
+                         "gain_stft = gain_test render fused with the STFT (the input is read: the headline "
+                         "shape with an input-dependent plugin)")
     ap.add_argument("--plugin", default=None, choices=["gain_test", "IR_test"],
                     help="generic / generic_stft: the reference plugin source (default gain_test / IR_test)")
     return ap.parse_args()
@@ -276,8 +278,8 @@ def main():
         sh = d.shard.plan(L, world, rank, B, N_FFT, HOP, True, world, d.shard.CHANNELS)
         assert sh.channels == 1, sh
     else:
-        sh = d.shard.plan(world * L, world, rank, B, N_FFT if wl in ("headline", "stft96k") else HOP, HOP,
-                          render=(wl == "headline"))
+        sh = d.shard.plan(world * L, world, rank, B, N_FFT if wl in ("headline", "stft96k", "gain_stft") else HOP,
+                          HOP, render=(wl in ("headline", "gain_stft")))
     assert sh.owned == L, (sh, L)
     L_in = sh.read_len
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
@@ -293,13 +295,13 @@ def main():
         rot[0] = (rot[0] + 1) % NX
         return xs[rot[0]]
     nb = d.num_blocks(L_in, B)
-    F = d.stft_frames(nb * B if wl in ("headline", "ch96k") else L_in, N_FFT, HOP)
+    F = d.stft_frames(nb * B if wl in ("headline", "ch96k", "gain_stft") else L_in, N_FFT, HOP)
     out = (torch.empty((CH, nb * B), device=dev)
-           if wl in ("headline", "ch96k", "gain10min", "fir1024", "generic", "generic_stft") else None)
+           if wl in ("headline", "ch96k", "gain10min", "fir1024", "generic", "generic_stft", "gain_stft") else None)
     if wl == "generic_stft":
         F = d.stft_frames(nb * B, N_FFT, HOP)
     mag = (torch.empty((CH, max(F, 1), K_BINS), device=dev)
-           if wl in ("headline", "stft96k", "ch96k", "generic_stft") else None)
+           if wl in ("headline", "stft96k", "ch96k", "generic_stft", "gain_stft") else None)
     plugin = d.Plugin.ir_test(0.9, 0.002) if wl in ("headline", "ch96k") else d.Plugin.gain_test(0.2)
     stream = torch.cuda.current_stream(dev)
     soff = sh.start
@@ -317,6 +319,17 @@ def main():
         workload = ("IR_test render (B=512) + 8192-pt Hann STFT, hop 4096, 4097 bins, "
                     f"{minutes:g} min of 48 kHz stereo per GPU")
         kname = f"{KERNEL}<render> (fused render + window + FFT + |X|)"
+    elif wl == "gain_stft":
+        # the headline's shape with an input-dependent plugin: gain_test
+        # (DSP_PLUGIN_GAIN) fused into the STFT wave, so every frame's hop is
+        # read from HBM, rendered and written, and its spectrum written
+        def step():
+            d.render_stft(x, CH, B, float(sr), plugin, N=N_FFT, H=HOP, window=d.DSP_WIN_HANN,
+                          K=K_BINS, out=out, mag=mag, sample_offset=soff)
+        workload = ("gain_test render (B=512) fused with the 8192-pt Hann STFT, hop 4096, 4097 bins, "
+                    f"{minutes:g} min of 48 kHz stereo per GPU")
+        kname = f"{KERNEL}<render> (fused file read + gain + window + FFT + |X|)"
+        alg_desc = "fused gain: C*F*(4H + 4H + 4K) B (file read + render write + |X| write)"
     elif wl == "ch96k":
         # the product's sharded driver (shard.h dsp_render_stft_sharded) for
         # this rank's channel, no collective in the timed step
@@ -590,7 +603,7 @@ def main():
                 "algorithmic": alg_desc,
                 "limiter": ("package power: the settled kernel draws the 1400 W cap at sclk ~1.8 GHz "
                             "(2.38 GHz without its stores); profiles/r01_power_ablation"
-                            if wl in ("headline", "ch96k") else
+                            if wl in ("headline", "ch96k", "gain_stft") else
                             "one lane per block: the plugin callback runs serially over its block in LDS, "
                             "16 blocks per 64 KB workgroup round (DESIGN 4.6)" if wl == "generic" else
                             "the render (LDS-capacity-bound callbacks) then the power-capped memory STFT, "
