@@ -534,8 +534,8 @@ def main():
         del pay, h_out, h_mag
 
     traffic, traffic_src = (None, None)
-    if wl in ("headline", "stft96k"):
-        traffic, traffic_src = pmc_traffic(wl, KERNEL, 1 if wl == "headline" else 0)
+    if wl in ("headline", "stft96k", "gain_stft"):
+        traffic, traffic_src = pmc_traffic(wl, KERNEL, 0 if wl == "stft96k" else 1)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and wl == "headline":
