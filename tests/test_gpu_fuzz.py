@@ -1,0 +1,135 @@
+"""Seeded random cases of the fused render + STFT (dsp_render_stft) against
+the oracle: the parametrized parity tests pin chosen shapes, these draw the
+shape, the plugin and its parameters, the block size, the window, the hop and
+the stored bins at random, so combinations nobody listed are covered too.
+
+Bars as in test_gpu_parity.py: the render bit-exact against the oracle's
+block loop (audio.cpp:13-175 restated, oracle/oracle.c), the magnitudes within
+1e-6 of each frame's peak against the float64 STFT of the oracle's render.
+"""
+import numpy as np
+import pytest
+
+import dspbench as d
+
+pytestmark = pytest.mark.gpu
+
+PEAK_REL_TOL = 1e-6
+N_CASES = 40
+
+
+def peak_rel_err(m, ref):
+    m = np.asarray(m, np.float64)
+    ref = np.asarray(ref, np.float64)
+    assert m.shape == ref.shape, (m.shape, ref.shape)
+    peak = np.maximum(ref.max(axis=-1), 1e-30)
+    return float(np.max(np.abs(m - ref).max(axis=-1) / peak))
+
+
+def draw(seed):
+    """One case: (plugin name, params, C_out, C_in, L, B, window, H, K)."""
+    r = np.random.default_rng(seed)
+    name = ["IR_test", "gain_test", "static_gain_plugin", "no_op"][int(r.integers(4))]
+    if name == "IR_test":
+        params = [float(np.float32(r.uniform(-1.0, 1.0))), float(np.float32(r.uniform(-0.01, 0.01)))]
+    elif name == "gain_test":
+        params = [float(np.float32(r.uniform(0.0, 2.0)))]
+    elif name == "static_gain_plugin":
+        params = [float(np.float32(r.uniform(0.0, 1.0)))]
+    else:
+        params = []
+    C_out = int(r.integers(1, 4))
+    C_in = int(r.integers(0, C_out + 2))
+    B = int(r.choice([1, 3, 64, 100, 128, 256, 384, 512, 640, 1000, 1024, 2048, 4096]))
+    L = int(r.integers(1, 60_000))
+    window = int(r.choice([d.DSP_WIN_HANN, d.DSP_WIN_HAMMING, d.DSP_WIN_RECT]))
+    H = int(r.choice([4096, 4096, 2048, 1000, 8192]))
+    K = int(r.choice([4097, 4097, 8192, int(r.integers(1, 4097))]))
+    return name, params, C_out, C_in, L, B, window, H, K
+
+
+def device_plugin(name, params):
+    if name == "IR_test":
+        return d.Plugin.ir_test(*params)
+    if name == "gain_test":
+        return d.Plugin.gain_test(*params)
+    if name == "static_gain_plugin":
+        return d.Plugin.static_gain(*params)
+    return d.Plugin.no_op()
+
+
+def oracle_plugin(oracle, name, params):
+    if name == "static_gain_plugin":
+        return oracle.restated_plugin(name, state=params)
+    return oracle.restated_plugin(name, params=params if params else None)
+
+
+@pytest.mark.parametrize("seed", range(N_CASES))
+def test_render_stft_random_case(torch_cuda, oracle, seed):
+    torch = torch_cuda
+    name, params, C_out, C_in, L, B, window, H, K = draw(1000 + seed)
+    x = np.random.default_rng(seed).uniform(-1.0, 1.0, (max(C_in, 1), L)).astype(np.float32)[:C_in]
+    ref = oracle.render_offline([x[c] for c in range(C_in)], C_out, B, 48000.0,
+                                oracle_plugin(oracle, name, params), L=L)
+    file = torch.from_numpy(np.ascontiguousarray(x)).cuda() if C_in else None
+    out, mag = d.render_stft(file, C_out, B, 48000.0, device_plugin(name, params), N=8192, H=H,
+                             window=window, K=K, L_file=L, ref=torch.empty(1, device="cuda"))
+    out = out.cpu().numpy()
+    mag = mag.cpu().numpy()
+    case = (name, params, C_out, C_in, L, B, window, H, K)
+    assert out.shape == ref.shape, case
+    assert np.array_equal(out.view(np.uint32), ref.view(np.uint32)), case
+    Kref = K if K <= 4097 else 8192
+    for c in range(C_out):
+        mref = oracle.np_stft_mag(ref[c], 8192, H, window, Kref)
+        if mref.shape[0] == 0:
+            assert mag.shape[1] <= 1, case  # no whole frame: nothing (or a placeholder row) stored
+            continue
+        assert mag.shape[1] == mref.shape[0], case
+        assert peak_rel_err(mag[c], mref) <= PEAK_REL_TOL, case
+
+
+# ---- plugins compiled from the reference sources (DSP_PLUGIN_GENERIC) ------
+# The same draw for the generic driver: a stock plugin compiled unchanged by
+# the product's plugin compiler (dsp-bench_amd/modules/mod_*.co) against the
+# same source compiled for the CPU with the JIT flags (oracle/_ref), whose
+# default parameters and state both sides start from.
+from test_gpu_module import EXACT, TOL, have, load  # noqa: E402
+
+GENERIC = EXACT + sorted(TOL)
+
+
+@pytest.mark.parametrize("seed", range(N_CASES))
+def test_generic_render_stft_random_case(torch_cuda, oracle, seed):
+    torch = torch_cuda
+    _, _, C_out, C_in, L, B, window, H, K = draw(2000 + seed)
+    name = GENERIC[seed % len(GENERIC)]
+    if not have(name):
+        pytest.skip("modules / oracle/_ref not built")
+    mod = load(name)
+    params = mod.default_parameters()
+    mod.initialize_state(params, C_out, 48000.0)
+    refp = oracle.RefPlugin(name, C_out, 48000.0)
+    x = np.random.default_rng(seed).uniform(-1.0, 1.0, (max(C_in, 1), L)).astype(np.float32)[:C_in]
+    want = oracle.render_offline([x[c] for c in range(C_in)], C_out, B, 48000.0, refp.as_oracle(), L=L)
+    file = torch.from_numpy(np.ascontiguousarray(x)).cuda() if C_in else None
+    out, mag = d.render_stft(file, C_out, B, 48000.0, mod.plugin(params, name), N=8192, H=H,
+                             window=window, K=K, L_file=L, ref=torch.empty(1, device="cuda"))
+    got = out.cpu().numpy()
+    mag = mag.cpu().numpy()
+    case = (name, C_out, C_in, L, B, window, H, K)
+    assert got.shape == want.shape, case
+    if name in TOL:
+        assert np.max(np.abs(got - want)) <= TOL[name], case
+    else:
+        assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), case
+    Kref = K if K <= 4097 else 8192
+    for c in range(C_out):
+        # the spectra of the GPU's own render (for the TOL plugins the render
+        # itself differs from the CPU's in the last ulp)
+        mref = oracle.np_stft_mag(got[c], 8192, H, window, Kref)
+        if mref.shape[0] == 0:
+            assert mag.shape[1] <= 1, case
+            continue
+        assert mag.shape[1] == mref.shape[0], case
+        assert peak_rel_err(mag[c], mref) <= PEAK_REL_TOL, case
