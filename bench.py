@@ -56,8 +56,10 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
     ap.add_argument("--gather", action="store_true", help="also time an RCCL gather to rank 0")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (host WAV -> host spectra) pass")
-    ap.add_argument("--no-launch-events", action="store_true",
-                    help="A/B: no per-launch library events in the timed region (kernel_avg = region / steps)")
+    ap.add_argument("--launch-events", action="store_true",
+                    help="one-kernel workloads: bracket every launch with the library's HIP events inside the "
+                         "timed region (costs 0.7-1%% of a step, profiles/r02_launch_events_ab.txt); default: "
+                         "kernel_avg_ms = the timed region's stream events / steps")
     ap.add_argument("--fir-method", type=int, default=0, choices=[0, 1, 2],
                     help="fir1024: 0 auto (overlap-save), 1 direct form, 2 overlap-save")
     ap.add_argument("--workload", default="headline",
@@ -423,15 +425,18 @@ def main():
     # the first call is cold (code objects load, the output's first touch,
     # the clock leaves idle): what an offline user rendering one file sees
     torch.cuda.synchronize()
+    # one kernel per step: the timed region's own stream events give its
+    # average launch duration, and no per-launch events sit between launches
+    region_timed = wl in ("headline", "ch96k", "gain_stft", "stft96k") and not args.launch_events
     bytes_probe = 0
-    if args.no_launch_events:  # the library's byte count of one launch, from the first call
+    if region_timed:  # the library's byte count of one launch, from the first call
         d.lib().dsp_kernel_timing(None, None, None)
         d.lib().dsp_kernel_timing_enable(1)
     tf = time.perf_counter()
     step()
     torch.cuda.synchronize()
     first_call_ms = (time.perf_counter() - tf) * 1e3
-    if args.no_launch_events:
+    if region_timed:
         d.lib().dsp_kernel_timing_enable(0)
         pm, pn, pb = C.c_double(), C.c_uint64(), C.c_uint64()
         d.lib().dsp_kernel_timing(C.byref(pm), C.byref(pn), C.byref(pb))
@@ -442,7 +447,7 @@ def main():
 
     lib = d.lib()
     lib.dsp_kernel_timing(None, None, None)  # clear
-    lib.dsp_kernel_timing_enable(0 if args.no_launch_events else 1)
+    lib.dsp_kernel_timing_enable(0 if region_timed else 1)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -486,7 +491,7 @@ def main():
 
     kernel_avg_ms = k_ms.value / max(1, k_n.value)
     bytes_per_launch = k_bytes.value / max(1, k_n.value)
-    if args.no_launch_events and wl in ("headline", "ch96k", "gain_stft", "stft96k"):  # one kernel per step
+    if region_timed:
         kernel_avg_ms = ev_ms / args.steps
         bytes_per_launch = bytes_probe
     if k_n.value == 0 and alg_bytes is not None:  # one kernel per step, timed by the step events
@@ -613,6 +618,10 @@ def main():
                 "traffic_unit": "GB per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
                 "traffic_source": traffic_src,
                 "kernel_avg_ms": round(kernel_avg_ms, 5),
+                "kernel_avg_source": ("HIP events on the launch stream around the timed region / steps (one "
+                                      "kernel launch per step)" if region_timed or (k_n.value == 0 and alg_bytes)
+                                      else "HIP events around every launch in the timed region (libdspbench "
+                                      "dsp_kernel_timing)"),
                 "algorithmic_bytes_per_launch": int(bytes_per_launch),
                 "algorithmic": alg_desc,
                 "limiter": ("package power: the settled kernel draws the 1400 W cap at sclk ~1.8 GHz "

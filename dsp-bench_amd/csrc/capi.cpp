@@ -248,8 +248,12 @@ static int get_scratch(int dev, hipStream_t s, size_t bytes, float **out, int sl
 struct TimedLaunch {
     hipEvent_t start, stop;
     uint64_t bytes;
+    int dev;
 };
 static bool g_timing = false;
+// recycled timing events per device (g_mu): a hipEventCreate pair per timed
+// launch cost more than the records themselves
+static std::map<int, std::vector<hipEvent_t>> g_event_pool;
 
 #ifdef DSPB_AB_BUILD
 // A/B and ablation options of stft8192_pk_kernel (stft_pk.hpp kPk* bits),
@@ -285,8 +289,21 @@ static thread_local bool tl_timing_outer = false;
 static int timing_begin(hipStream_t s, TimedLaunch *t) {
     t->start = t->stop = nullptr;
     if (!g_timing || tl_timing_outer) return DSP_OK;
-    DSPB_HIP(hipEventCreate(&t->start));
-    DSPB_HIP(hipEventCreate(&t->stop));
+    DSPB_HIP(hipGetDevice(&t->dev));
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        auto &pool = g_event_pool[t->dev];
+        if (pool.size() >= 2) {
+            t->start = pool.back();
+            pool.pop_back();
+            t->stop = pool.back();
+            pool.pop_back();
+        }
+    }
+    if (!t->start) {
+        DSPB_HIP(hipEventCreate(&t->start));
+        DSPB_HIP(hipEventCreate(&t->stop));
+    }
     DSPB_HIP(hipEventRecord(t->start, s));
     return DSP_OK;
 }
@@ -693,6 +710,17 @@ int dsp_stft_pk_ab_options(int opt) {
 void dsp_kernel_timing_enable(int on) {
     std::lock_guard<std::mutex> lk(g_mu);
     g_timing = on != 0;
+    // a stock of events for the current device, created here rather than
+    // between the launches being timed
+    int dev = 0;
+    if (g_timing && hipGetDevice(&dev) == hipSuccess) {
+        auto &pool = g_event_pool[dev];
+        while (pool.size() < 1024) {
+            hipEvent_t e = nullptr;
+            if (hipEventCreate(&e) != hipSuccess) break;
+            pool.push_back(e);
+        }
+    }
 }
 
 int dsp_kernel_timing(double *total_ms, uint64_t *launches, uint64_t *bytes) {
@@ -709,8 +737,13 @@ int dsp_kernel_timing(double *total_ms, uint64_t *launches, uint64_t *bytes) {
         DSPB_HIP(hipEventElapsedTime(&e, t.start, t.stop));
         ms += e;
         b += t.bytes;
-        (void)hipEventDestroy(t.start);
-        (void)hipEventDestroy(t.stop);
+    }
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        for (auto &t : v) {
+            g_event_pool[t.dev].push_back(t.stop);
+            g_event_pool[t.dev].push_back(t.start);
+        }
     }
     if (total_ms) *total_ms = ms;
     if (launches) *launches = v.size();

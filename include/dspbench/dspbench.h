@@ -191,7 +191,9 @@ int dsp_spectrogram_decimate(const float *mag, uint64_t F, uint32_t K, uint64_t 
  * dsp_render_stft / dsp_stft_magnitude (the 8192-point wave-per-frame kernel)
  * is bracketed by HIP events on its stream.  dsp_kernel_timing() waits for
  * them, returns the summed duration, the launch count and the algorithmic
- * bytes of those launches, and clears the record. */
+ * bytes of those launches, and clears the record.  Enabling
+ * creates a stock of events for the current device, and read-out events are
+ * reused, so the timed launches do not pay for event creation. */
 void dsp_kernel_timing_enable(int on);
 int dsp_kernel_timing(double *total_ms, uint64_t *launches, uint64_t *bytes);
 
