@@ -228,6 +228,14 @@ static int get_scratch(int dev, hipStream_t s, size_t bytes, float **out, int sl
     DeviceRes &r = g_res[dev];
     auto &slot = r.scratch[std::make_pair((void *)s, slot_id)];
     if (slot.second < bytes) {
+        // a stream being captured into a graph cannot allocate or wait: its
+        // scratch must exist from an eager call of the same shape first
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        if (hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) {
+            set_last_error("stream capture: make one eager call of this shape on the capturing stream first "
+                           "(its scratch buffer is allocated then)");
+            return DSP_ERR_INVALID;
+        }
         if (slot.first) {
             DSPB_HIP(hipStreamSynchronize(s));
             DSPB_HIP(hipFree(slot.first));
