@@ -133,3 +133,46 @@ def test_generic_render_stft_random_case(torch_cuda, oracle, seed):
             continue
         assert mag.shape[1] == mref.shape[0], case
         assert peak_rel_err(mag[c], mref) <= PEAK_REL_TOL, case
+
+
+# ---- the memory-source STFT and loop mode ----------------------------------
+@pytest.mark.parametrize("seed", range(24))
+def test_stft_magnitude_random_case(torch_cuda, oracle, seed):
+    """dsp_stft_magnitude (fft_perform_and_get_magnitude per frame,
+    dsp.cpp:208-271 restated): a random power-of-two size (the 8192-point
+    kernel and the generic one), hop, window and stored bins."""
+    torch = torch_cuda
+    r = np.random.default_rng(3000 + seed)
+    N = int(2 ** r.integers(4, 14))
+    H = int(r.choice([N // 2, N, max(1, N // 4), int(r.integers(1, 2 * N))]))
+    window = int(r.choice([d.DSP_WIN_HANN, d.DSP_WIN_HAMMING, d.DSP_WIN_RECT]))
+    K = int(r.choice([N // 2 + 1, int(r.integers(1, N // 2 + 2))]))
+    C = int(r.integers(1, 4))
+    L = int(r.integers(N, N * 6 + 1))
+    x = np.random.default_rng(seed).uniform(-1.0, 1.0, (C, L)).astype(np.float32)
+    mag = d.stft_magnitude(torch.from_numpy(x).cuda(), N=N, H=H, window=window, K=K).cpu().numpy()
+    case = (N, H, window, K, C, L)
+    for c in range(C):
+        mref = oracle.np_stft_mag(x[c], N, H, window, K)
+        assert mag.shape[1] == mref.shape[0], case
+        assert peak_rel_err(mag[c], mref) <= PEAK_REL_TOL, case
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_render_loop_random_case(torch_cuda, oracle, seed):
+    """Loop mode (audio.cpp:100-132): the file wraps from a random cursor;
+    bit-exact against oracle_render_loop, and the next cursor agrees."""
+    torch = torch_cuda
+    name, params, C_out, C_in, L, B, _, _, _ = draw(4000 + seed)
+    C_in = max(C_in, 1)  # loop mode wraps a file: at least one channel
+    nblocks = int(np.random.default_rng(seed).integers(1, 200))
+    cursor = int(np.random.default_rng(seed + 1).integers(0, L))
+    x = np.random.default_rng(seed).uniform(-1.0, 1.0, (C_in, L)).astype(np.float32)
+    want, wcur = oracle.render_loop([x[c] for c in range(C_in)], C_out, B, nblocks, 48000.0,
+                                    oracle_plugin(oracle, name, params), cursor=cursor)
+    got, gcur = d.render_loop(torch.from_numpy(x).cuda(), C_out, B, nblocks, 48000.0, device_plugin(name, params),
+                              cursor=cursor)
+    case = (name, params, C_out, C_in, L, B, nblocks, cursor)
+    assert gcur == wcur, case
+    got = got.cpu().numpy()
+    assert np.array_equal(got.view(np.uint32), np.asarray(want, np.float32).view(np.uint32)), case
