@@ -295,6 +295,7 @@ std::string expand(std::string s, const std::map<std::string, Macro> &macros) {
 // body text between the braces of `struct|class NAME {` (or of
 // `typedef struct ... { } NAME;`), "" when absent
 std::string find_record_body(const std::string &s, const std::string &name) {
+    if (name.empty()) return "";  // find("") matches everywhere: the loop would not advance
     for (size_t pos = 0; (pos = s.find(name, pos)) != std::string::npos; pos += name.size()) {
         if ((pos > 0 && ident_char(s[pos - 1])) || (pos + name.size() < s.size() && ident_char(s[pos + name.size()])))
             continue;
@@ -350,6 +351,7 @@ bool find_enumerators(const std::string &s, const std::string &name, std::vector
         }
         return true;
     };
+    if (name.empty()) return false;  // an ENUM_PARAM without a type name (tests/sanitize/host_fuzz.cpp)
     for (size_t pos = 0; (pos = s.find(name, pos)) != std::string::npos; pos += name.size()) {
         if ((pos > 0 && ident_char(s[pos - 1])) || (pos + name.size() < s.size() && ident_char(s[pos + name.size()])))
             continue;
@@ -414,7 +416,11 @@ std::string strip_attributes(const std::string &decl) {
     std::string o;
     for (size_t i = 0; i < decl.size();) {
         if (decl.compare(i, 13, "__attribute__") == 0) {
-            size_t p = decl.find('(', i);
+            const size_t p = decl.find('(', i);
+            if (p == std::string::npos) {  // no group follows: i would wrap to 0 (tests/sanitize/host_fuzz.cpp)
+                o += ' ';
+                break;
+            }
             int depth = 0;
             size_t e = p;
             for (; e < decl.size(); ++e) {
@@ -614,14 +620,19 @@ bool elf_symbol(const unsigned char *img, size_t size, const char *want, std::st
     if (size < sizeof(Elf64Ehdr) || std::memcmp(img, "\x7f" "ELF", 4) != 0 || img[4] != 2) return false;
     Elf64Ehdr eh;
     std::memcpy(&eh, img, sizeof eh);
-    if (eh.shentsize != sizeof(Elf64Shdr) || eh.shoff + (uint64_t)eh.shnum * sizeof(Elf64Shdr) > size) return false;
+    // every range check below is written so that no sum can wrap
+    // (a corrupted header must not pass them: tests/sanitize/host_fuzz.cpp)
+    auto in_image = [size](uint64_t off, uint64_t len) { return off <= size && len <= size - off; };
+    if (eh.shentsize != sizeof(Elf64Shdr) || eh.shnum == 0 ||
+        !in_image(eh.shoff, (uint64_t)eh.shnum * sizeof(Elf64Shdr)))
+        return false;
     std::vector<Elf64Shdr> sh(eh.shnum);
     std::memcpy(sh.data(), img + eh.shoff, sh.size() * sizeof(Elf64Shdr));
     for (const Elf64Shdr &s : sh) {
         if (s.type != 2 && s.type != 11) continue;  // SHT_SYMTAB / SHT_DYNSYM
-        if (s.link >= sh.size() || s.offset + s.size > size || s.entsize != sizeof(Elf64Sym)) continue;
+        if (s.link >= sh.size() || !in_image(s.offset, s.size) || s.entsize != sizeof(Elf64Sym)) continue;
         const Elf64Shdr &strs = sh[s.link];
-        if (strs.offset + strs.size > size) continue;
+        if (!in_image(strs.offset, strs.size)) continue;
         for (uint64_t k = 0; k < s.size / sizeof(Elf64Sym); ++k) {
             Elf64Sym sym;
             std::memcpy(&sym, img + s.offset + k * sizeof(Elf64Sym), sizeof sym);
@@ -630,9 +641,10 @@ bool elf_symbol(const unsigned char *img, size_t size, const char *want, std::st
             if (std::strncmp(nm, want, strs.size - sym.name) != 0) continue;
             const Elf64Shdr &sec = sh[sym.shndx];
             if (sec.type == 8) return false;  // NOBITS: no initialiser in the file
-            if (sym.value < sec.addr || sym.value - sec.addr + sym.size > sec.size) return false;
-            const uint64_t off = sec.offset + (sym.value - sec.addr);
-            if (off + sym.size > size) return false;
+            if (sym.value < sec.addr || sym.value - sec.addr > sec.size || sym.size > sec.size - (sym.value - sec.addr))
+                return false;
+            if (!in_image(sec.offset, sec.size)) return false;
+            const uint64_t off = sec.offset + (sym.value - sec.addr);  // within [sec.offset, sec.offset + sec.size]
             out->assign((const char *)img + off, sym.size);
             return true;
         }
@@ -665,7 +677,7 @@ int read(const void *code, size_t size, Descriptor *d, std::string *err) {
         return -1;
     }
     std::vector<unsigned long long> v(blob.size() / 8);
-    std::memcpy(v.data(), blob.data(), v.size() * 8);
+    if (!v.empty()) std::memcpy(v.data(), blob.data(), v.size() * 8);
     if (v.size() < 9 || v[0] != kMagic || v[1] != 1) {
         if (err) *err = "descriptor blob: bad magic / version";
         return -1;
@@ -677,6 +689,12 @@ int read(const void *code, size_t size, Descriptor *d, std::string *err) {
     d->state_empty = v[6] != 0;
     const uint64_t n = v[7];
     d->source_parsed = v[8] != 0;
+    auto pow2 = [](uint64_t a) { return a && a <= 4096 && !(a & (a - 1)); };
+    if (d->params_size > (1u << 24) || d->state_size > (1ull << 32) || !pow2(d->params_align) ||
+        !pow2(d->state_align) || n > 4096) {
+        if (err) *err = "descriptor blob: implausible layout";
+        return -1;
+    }
     // text records: name \x1f annotation [\x1f enumerator ...] \x1e
     std::vector<std::vector<std::string>> recs;
     {
@@ -711,6 +729,10 @@ int read(const void *code, size_t size, Descriptor *d, std::string *err) {
         Param p;
         p.name = recs[i][0];
         p.annotation = recs[i].size() > 1 ? recs[i][1] : "";
+        if (v[at] > d->params_size || d->params_size - v[at] < 4) {  // int, float and enum fields: 4 bytes
+            if (err) *err = "descriptor blob: a field lies outside Parameters";
+            return -1;
+        }
         p.offset = (uint32_t)v[at];
         const unsigned long long tc = v[at + 1];
         const uint64_t ne = v[at + 2];

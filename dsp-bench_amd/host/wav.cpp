@@ -78,6 +78,9 @@ extern "C" int dsp_wav_parse(const void *file, uint64_t n, dsp_wav_info *info) {
     const bool ok = (fmt == DSP_WAV_FORMAT_PCM && (bits == 16 || bits == 24 || bits == 32)) ||
                     (fmt == DSP_WAV_FORMAT_FLOAT && bits == 32);
     if (!ok) return DSP_ERR_UNSUPPORTED;  // Wav_Invalid_Format (wav_reader.h:191-195)
+    // a frame must fit the 16-bit nBlockAlign field (found by
+    // tests/sanitize/host_fuzz.cpp: 16384 channels x 4 bytes wrapped to 0)
+    if ((uint32_t)info->channels * (bits / 8u) > 0xffffu) return DSP_ERR_INVALID;
     info->format = fmt;
     info->block_align = (uint16_t)(info->channels * (bits / 8));
     info->frames = info->data_bytes / info->block_align;
