@@ -43,7 +43,7 @@ if [[ $mode == prof || $mode == all ]]; then
     python tools/trace_avg.py $out/prof_$tag/run_kernel_trace.csv stft8192_pk 200 100 | tee $out/prof_$tag/trace_avg.txt
 fi
 if [[ $mode == others || $others == 1 ]]; then
-    for wl in gain10min stft96k ch96k fir1024 wav16 wav24 ir generic generic_stft; do
+    for wl in gain10min stft96k ch96k fir1024 wav16 wav24 ir generic generic_stft gain_stft; do
         run bench_$wl 300 python bench.py --workload $wl --no-cpu-baseline
     done
     run bench_generic_stft_gain 300 python bench.py --workload generic_stft --plugin gain_test --no-cpu-baseline
