@@ -604,7 +604,9 @@ static int render_device(const float *const *in, uint32_t in_ch, uint64_t L, flo
     return DSP_OK;
 }
 
-static int check_stft_args(uint32_t N, uint32_t H, uint32_t K, uint64_t ld) {
+static int check_stft_args(uint32_t N, uint32_t H, uint32_t K, uint64_t ld, int32_t window) {
+    if (window != DSP_WIN_HAMMING && window != DSP_WIN_HANN && window != DSP_WIN_RECT)
+        return invalid("window=%d is not a DSP_WIN_* kind", window);
     if (!is_pow2(N) || N < 4 || N > 8192) return invalid("N=%u must be a power of two in [4, 8192]", N);
     if (H == 0) return invalid("hop H must be > 0");
     if (K == 0 || (K > N / 2 + 1 && K != N)) return invalid("K=%u must be <= N/2+1 or == N", K);
@@ -910,7 +912,7 @@ int dsp_render_loop(const float *const *in, uint32_t in_channels, uint64_t L, ui
 int dsp_stft_magnitude(const float *const *in, uint32_t C, uint64_t L, uint32_t N, uint32_t H,
                        int32_t window, uint32_t K, float *const *mag, uint64_t ld,
                        const dsp_exec *ex) {
-    int st = check_stft_args(N, H, K, ld);
+    int st = check_stft_args(N, H, K, ld, window);
     if (st) return st;
     if (C == 0) return DSP_OK;
     if (!in || !mag) return invalid("in / mag is NULL");
@@ -948,7 +950,7 @@ int dsp_render_stft(const float *const *in, uint32_t in_channels, uint64_t L,
                     uint32_t K, float *const *mag, uint64_t ld, const dsp_exec *ex) {
 
     if (B == 0) return invalid("block size B must be > 0");
-    int st = check_stft_args(N, H, K, ld);
+    int st = check_stft_args(N, H, K, ld, window);
     if (st) return st;
     if (C == 0) return DSP_OK;
     if (!out || !mag) return invalid("out / mag is NULL");

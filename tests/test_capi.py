@@ -89,6 +89,32 @@ def test_invalid_arguments_rejected_before_device_use():
     assert L.dsp_render_offline(rows, 1, 1024, rows, 0, 512, 48000.0, None, C.byref(ex)) == 0   # C = 0: no-op
 
 
+@pytest.mark.parametrize("N,H,window,K,ld,what", [
+    (8192, 4096, 7, 4097, 4097, b"window"),        # not a DSP_WIN_* kind
+    (8192, 4096, -1, 4097, 4097, b"window"),
+    (6000, 3000, 1, 3001, 3001, b"N="),            # not a power of two
+    (16384, 4096, 1, 8193, 8193, b"N="),           # above 8192
+    (8192, 0, 1, 4097, 4097, b"hop"),
+    (8192, 4096, 1, 0, 4097, b"K="),
+    (8192, 4096, 1, 5000, 5000, b"K="),            # neither <= N/2+1 nor N
+    (8192, 4096, 1, 4097, 4096, b"ld="),           # rows overlap
+])
+def test_stft_arguments_rejected_before_device_use(N, H, window, K, ld, what):
+    """dsp_stft_magnitude and dsp_render_stft refuse a bad shape before they
+    touch a device (so this runs without one) and name the argument."""
+    L = d.lib()
+    L.dsp_last_error.restype = C.c_char_p
+    x = np.zeros((1, 16384), np.float32)
+    m = np.zeros((1, 8 * 8193), np.float32)
+    rows, mrows = _lib.chan_table([x[0].ctypes.data]), _lib.chan_table([m[0].ctypes.data])
+    ex = _exec_host()
+    assert L.dsp_stft_magnitude(rows, 1, 16384, N, H, window, K, mrows, C.c_uint64(ld), C.byref(ex)) == -1
+    assert what in L.dsp_last_error()
+    assert L.dsp_render_stft(rows, 1, 16384, rows, 1, 512, C.c_float(48000.0), None, N, H, window, K, mrows,
+                             C.c_uint64(ld), C.byref(ex)) == -1
+    assert what in L.dsp_last_error()
+
+
 def test_generic_ir_analysis_rejects_more_than_16_channels():
     """The generic driver's channel table holds 16 pointers: a GENERIC
     plugin's IR analysis with C = 17 is refused before any device or module
