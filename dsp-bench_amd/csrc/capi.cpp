@@ -1229,7 +1229,12 @@ int dsp_copy(const float *in, float *out, uint64_t n, const dsp_exec *ex) {
     if (!in || !out) return invalid("NULL buffer");
     DeviceGuard g(ex);
     if (g.status) return g.status;
-    DSPB_HIP(hipMemcpyAsync(out, in, n * sizeof(float), hipMemcpyDeviceToDevice, stream_of(ex)));
+    bool done = false;
+    if (!host_mode(ex)) {
+        const int st = launch_copy(in, out, n, stream_of(ex), &done);
+        if (st) return st;
+    }
+    if (!done) DSPB_HIP(hipMemcpyAsync(out, in, n * sizeof(float), hipMemcpyDeviceToDevice, stream_of(ex)));
     return finish(ex);
 }
 

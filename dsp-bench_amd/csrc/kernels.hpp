@@ -97,6 +97,7 @@ int launch_stft8192_pk(const Stft8kArgs &A, uint32_t C, bool fused, int opt, hip
 int launch_fft_generic(const GenericFftArgs &A, uint64_t transforms, uint32_t C, hipStream_t s);
 int launch_gain(const float *in, float *out, float g, uint64_t n, hipStream_t s);
 int launch_set(float v, float *out, uint64_t n, hipStream_t s);
+int launch_copy(const float *in, float *out, uint64_t n, hipStream_t s, bool *done);
 int launch_upload(float *dst, const float *src, uint64_t n, hipStream_t s);
 int launch_impulse(const ChanOut &buf, uint32_t C, uint32_t n, hipStream_t s);
 int launch_magnitude(const float *re, const float *im, float *out, uint64_t n, hipStream_t s);

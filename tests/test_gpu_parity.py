@@ -320,6 +320,38 @@ def test_elementwise_services_bit_exact(torch_cuda):
     assert L.dsp_set(1.0, fp(out), 0, C.byref(ex)) == 0
 
 
+@pytest.mark.parametrize("n", [1, 3, 4, 5, 4095, 4096, 4097, 70_001])
+@pytest.mark.parametrize("off", [0, 1])
+def test_elementwise_services_shapes(torch_cuda, n, off):
+    """The services' vector path (16-byte aligned rows, one float4 tile per
+    block, the n % 4 tail) and scalar path (a row offset by one float), bit
+    for bit against float32 numpy."""
+    import ctypes as C
+    torch = torch_cuda
+    L = d.lib()
+    rng = np.random.default_rng(n + off)
+    a = rng.uniform(-3, 3, n).astype(np.float32)
+    b = rng.uniform(-3, 3, n).astype(np.float32)
+    ga = torch.zeros(n + 1, device="cuda")[off:off + n]
+    gb = torch.zeros(n + 1, device="cuda")[off:off + n]
+    ga.copy_(torch.from_numpy(a))
+    gb.copy_(torch.from_numpy(b))
+    base = torch.full((n + 2,), 7.0, device="cuda")
+    out = base[off:off + n]
+    ex = d._lib.dsp_exec(torch.cuda.current_device(), d._lib.DSP_EXEC_SYNC,
+                         C.c_void_p(torch.cuda.current_stream().cuda_stream), 0)
+    fp = lambda t: C.cast(C.c_void_p(t.data_ptr()), d._lib.FP)  # noqa: E731
+    assert L.dsp_gain(fp(ga), fp(out), 0.37, n, C.byref(ex)) == 0
+    assert np.array_equal(out.cpu().numpy(), a * np.float32(0.37))
+    assert L.dsp_copy(fp(gb), fp(out), n, C.byref(ex)) == 0
+    assert np.array_equal(out.cpu().numpy(), b)
+    assert L.dsp_set(-2.5, fp(out), n, C.byref(ex)) == 0
+    assert np.array_equal(out.cpu().numpy(), np.full(n, -2.5, np.float32))
+    assert L.dsp_magnitude(fp(ga), fp(gb), fp(out), n, C.byref(ex)) == 0
+    assert np.array_equal(out.cpu().numpy(), np.sqrt((a * a) + (b * b)).astype(np.float32))
+    assert float(base[off + n]) == 7.0  # nothing written past the row
+
+
 def test_full_size_cfg4_stft_1h_96k_from_hbm(torch_cuda, oracle):
     """BASELINE cfg 4 at full size: the Hann 8192 / 4096 STFT of 1 h of 96 kHz
     stereo (2 x 345.6 M samples) from HBM.  Frame count, and sampled frames

@@ -32,8 +32,10 @@ pa, pb = C.cast(C.c_void_p(a.data_ptr()), FP), C.cast(C.c_void_p(b.data_ptr()), 
 res = {
     "torch fill (write)": (t(lambda: b.fill_(1.0)), n * 4),
     "dsp_set (write)": (t(lambda: lib.dsp_set(1.0, pb, n, C.byref(ex))), n * 4),
-    "torch copy (r+w)": (t(lambda: b.copy_(a)), 2 * n * 4),
+    "torch copy (r+w; a device memcpy)": (t(lambda: b.copy_(a)), 2 * n * 4),
     "dsp_gain (r+w)": (t(lambda: lib.dsp_gain(pa, pb, 0.5, n, C.byref(ex))), 2 * n * 4),
+    "dsp_copy (r+w)": (t(lambda: lib.dsp_copy(pa, pb, n, C.byref(ex))), 2 * n * 4),
+    "dsp_magnitude (2r+w)": (t(lambda: lib.dsp_magnitude(pa, pa, pb, n, C.byref(ex))), 3 * n * 4),
     "torch sum (read)": (t(lambda: a.sum()), n * 4),
 }
 for k, (ms, byt) in res.items():
