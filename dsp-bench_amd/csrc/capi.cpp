@@ -1242,6 +1242,14 @@ int dsp_set(float value, float *out, uint64_t n, const dsp_exec *ex) {
     if (!out) return invalid("NULL buffer");
     DeviceGuard g(ex);
     if (g.status) return g.status;
+    // the runtime's 32-bit memset with the value's bit pattern: 6.5 TB/s
+    // against 6.0 for the float4 kernel (profiles/r02_elementwise_bw.txt)
+    if (!host_mode(ex) && n) {
+        uint32_t bits;
+        std::memcpy(&bits, &value, 4);
+        DSPB_HIP(hipMemsetD32Async((hipDeviceptr_t)out, (int)bits, n, stream_of(ex)));
+        return finish(ex);
+    }
     int st = launch_set(value, out, n, stream_of(ex));
     return st ? st : finish(ex);
 }
