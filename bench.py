@@ -64,7 +64,7 @@ def parse():
                     help="fir1024: 0 auto (overlap-save), 1 direct form, 2 overlap-save")
     ap.add_argument("--workload", default="headline",
                     choices=["headline", "stft96k", "ch96k", "gain10min", "fir1024", "wav16", "wav24", "ir",
-                             "generic", "generic_stft", "gain_stft"],
+                             "generic", "generic_stft", "gain_stft", "wav16enc", "wav24enc"],
                     help="headline = IR_test + STFT 48 kHz (the metric); stft96k = BASELINE cfg 4 "
                          "(STFT of 1 h stereo 96 kHz from HBM); gain10min = cfg 2 render; "
                          "wav16 / wav24 = GPU decode of a 1 h stereo int16 / int24 WAV payload; "
@@ -73,7 +73,8 @@ def parse():
                          "generic = a reference plugin source through the generic driver (render only); "
                          "generic_stft = the same + the 8192-pt STFT (render, then the STFT, one stream); "
                          "gain_stft = gain_test render fused with the STFT (the input is read: the headline "
-                         "shape with an input-dependent plugin)")
+                         "shape with an input-dependent plugin); wav16enc / wav24enc = GPU encode of 1 h of "
+                         "planar stereo into an interleaved int16 / int24 WAV payload")
     ap.add_argument("--plugin", default=None, choices=["gain_test", "IR_test"],
                     help="generic / generic_stft: the reference plugin source (default gain_test / IR_test)")
     return ap.parse_args()
@@ -403,6 +404,22 @@ def main():
                      "region, dsp_render_stft)")
             alg_desc = ("C*L*(4 + 4) + C*F*4K B (file read + render write + |X| write; the STFT's re-read of "
                         "the render is extra traffic, not counted)")
+    elif wl in ("wav16enc", "wav24enc"):
+        # SURVEY 8(f) row 1, the writer: planar float -> interleaved PCM
+        # (interleave + convert, audio.h:123-133; round half to even, clip)
+        bits = 16 if wl == "wav16enc" else 24
+        epay = torch.empty((CH * L_in * bits // 8,), dtype=torch.uint8, device=dev)
+        eptrs = d._lib.chan_table([x[c].data_ptr() for c in range(CH)])
+        eex = d.api._exec(x)
+
+        def step():
+            d._lib.check(lib0.dsp_wav_encode(eptrs, CH, L_in, 1, bits, C.c_void_p(epay.data_ptr()),
+                                             C.byref(eex)), "dsp_wav_encode")
+        workload = f"planar float stereo -> WAV int{bits} payload (convert + interleave), {minutes:g} min of 48 kHz per GPU"
+        kname = f"wav_encode_tile_kernel<{bits}, PCM, 2 ch>"
+        alg_bytes = CH * L_in * (4 + bits // 8)
+        plug_name = None
+        alg_desc = f"C*L*(4 + {bits // 8}) B (planar float read + PCM payload write)"
     else:
         bits = 16 if wl == "wav16" else 24
         pay = torch.randint(0, 256, (CH * L_in * bits // 8,), dtype=torch.uint8, device=dev, generator=g)

@@ -186,6 +186,96 @@ __global__ __launch_bounds__(256) void wav_encode_kernel(WavArgs A) {
     }
 }
 
+// Mono / stereo encode, the decode tile run backwards: each thread reads one
+// float4 per channel for each of kWavU groups of 4 frames (planar rows
+// 16-byte aligned), packs the group's W = CH * BITS / 8 dwords of
+// interleaved payload and stores them LDW dwords at a time (LDW from the
+// payload's alignment); the last partial group byte by byte.
+template <int BITS>
+__device__ __forceinline__ void pack(uint32_t *w, int j, uint32_t raw) {
+    if constexpr (BITS == 32) {
+        w[j] = raw;
+    } else if constexpr (BITS == 16) {
+        w[j >> 1] |= raw << (16 * (j & 1));
+    } else {
+        const int byte = 3 * j, q = byte >> 2, sh = (byte & 3) * 8;
+        w[q] |= raw << sh;
+        if (sh > 8) w[q + 1] |= raw >> (32 - sh);
+    }
+}
+template <int BITS, bool FLT, int CH, int LDW>
+__global__ __launch_bounds__(256) void wav_encode_tile_kernel(WavArgs A) {
+    constexpr int BPS = BITS / 8;
+    constexpr int W = CH * BPS;  // dwords of 4 frames
+    static_assert(W % LDW == 0, "store width");
+    const uint64_t g0 = blockIdx.x * (256ull * kWavU) + threadIdx.x;
+    float4 v[kWavU][CH];
+#pragma unroll
+    for (int u = 0; u < kWavU; ++u) {
+        const uint64_t f = 4 * (g0 + 256u * (uint32_t)u);
+        if (f + 4 <= A.frames) {
+#pragma unroll
+            for (int c = 0; c < CH; ++c) v[u][c] = *reinterpret_cast<const float4 *>(A.pl.p[c] + f);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < kWavU; ++u) {
+        const uint64_t f = 4 * (g0 + 256u * (uint32_t)u);
+        if (f + 4 <= A.frames) {
+            uint32_t w[W];
+#pragma unroll
+            for (int i = 0; i < W; ++i) w[i] = 0;
+#pragma unroll
+            for (int c = 0; c < CH; ++c) {
+                pack<BITS>(w, 0 * CH + c, float_to_pcm<BITS, FLT>(v[u][c].x));
+                pack<BITS>(w, 1 * CH + c, float_to_pcm<BITS, FLT>(v[u][c].y));
+                pack<BITS>(w, 2 * CH + c, float_to_pcm<BITS, FLT>(v[u][c].z));
+                pack<BITS>(w, 3 * CH + c, float_to_pcm<BITS, FLT>(v[u][c].w));
+            }
+            uint8_t *dst = const_cast<uint8_t *>(A.payload) + f * (uint64_t)W;  // W bytes per frame
+#pragma unroll
+            for (int i = 0; i < W; i += LDW) {
+                if constexpr (LDW == 4)
+                    *reinterpret_cast<uint4 *>(dst + 4 * i) = make_uint4(w[i], w[i + 1], w[i + 2], w[i + 3]);
+                else if constexpr (LDW == 2)
+                    *reinterpret_cast<uint2 *>(dst + 4 * i) = make_uint2(w[i], w[i + 1]);
+                else
+                    *reinterpret_cast<uint32_t *>(dst + 4 * i) = w[i];
+            }
+        } else if (f < A.frames) {  // the last, partial group
+            for (uint64_t ff = f; ff < A.frames; ++ff)
+                for (int c = 0; c < CH; ++c) {
+                    const uint32_t raw = float_to_pcm<BITS, FLT>(A.pl.p[c][ff]);
+                    uint8_t *d = const_cast<uint8_t *>(A.payload) + (ff * CH + c) * (uint64_t)BPS;
+#pragma unroll
+                    for (int b = 0; b < BPS; ++b) d[b] = (uint8_t)(raw >> (8 * b));
+                }
+        }
+    }
+}
+
+template <int BITS, bool FLT, int CH>
+static void enc_tile(const WavArgs &A, dim3 grid, hipStream_t s) {
+    constexpr int W = CH * BITS / 8;
+    const uintptr_t start = reinterpret_cast<uintptr_t>(A.payload);
+    if constexpr (W % 4 == 0) {
+        if (start % 16 == 0) {
+            hipLaunchKernelGGL((wav_encode_tile_kernel<BITS, FLT, CH, 4>), grid, dim3(256), 0, s, A);
+            return;
+        }
+    }
+    if constexpr (W % 2 == 0) {
+        if (start % 8 == 0) {
+            hipLaunchKernelGGL((wav_encode_tile_kernel<BITS, FLT, CH, 2>), grid, dim3(256), 0, s, A);
+            return;
+        }
+    }
+    hipLaunchKernelGGL((wav_encode_tile_kernel<BITS, FLT, CH, 1>), grid, dim3(256), 0, s, A);
+}
+
+template <int BITS, bool FLT>
+static void enc(const WavArgs &A, bool vec, hipStream_t s);
+
 static dim3 grid_for(uint64_t items) {
     uint64_t g = (items + 255) / 256;
     if (g > 4096) g = 4096;
@@ -239,15 +329,29 @@ int launch_wav_decode(const uint8_t *payload, uint32_t C, uint16_t bits, bool is
     return DSP_OK;
 }
 
+template <int BITS, bool FLT>
+static void enc(const WavArgs &A, bool vec, hipStream_t s) {
+    if (vec && (A.C == 1 || A.C == 2)) {
+        const uint64_t tiles = ((A.frames + 3) / 4 + 256u * kWavU - 1) / (256u * kWavU);
+        const dim3 grid((uint32_t)(tiles ? tiles : 1));
+        if (A.C == 1) enc_tile<BITS, FLT, 1>(A, grid, s);
+        else enc_tile<BITS, FLT, 2>(A, grid, s);
+        return;
+    }
+    hipLaunchKernelGGL((wav_encode_kernel<BITS, FLT>), grid_for(A.frames * A.C), dim3(256), 0, s, A);
+}
+
 int launch_wav_encode(uint8_t *payload, uint32_t C, uint16_t bits, bool is_float, uint64_t frames,
                       const ChanOut &in, hipStream_t s) {
     if (frames == 0) return DSP_OK;
     WavArgs A{payload, 0, frames, C, in};
-    const dim3 grid = grid_for(frames * C);
-    if (is_float) hipLaunchKernelGGL((wav_encode_kernel<32, true>), grid, dim3(256), 0, s, A);
-    else if (bits == 16) hipLaunchKernelGGL((wav_encode_kernel<16, false>), grid, dim3(256), 0, s, A);
-    else if (bits == 24) hipLaunchKernelGGL((wav_encode_kernel<24, false>), grid, dim3(256), 0, s, A);
-    else if (bits == 32) hipLaunchKernelGGL((wav_encode_kernel<32, false>), grid, dim3(256), 0, s, A);
+    bool vec = ((uintptr_t)payload % 4 == 0) && (C == 1 || C == 2);
+    for (uint32_t c = 0; c < C && vec; ++c) vec = ((uintptr_t)in.p[c] % 16) == 0;
+    if ((frames + 3) / 4 / (256u * kWavU) > 0x7fffffffull) vec = false;
+    if (is_float) enc<32, true>(A, vec, s);
+    else if (bits == 16) enc<16, false>(A, vec, s);
+    else if (bits == 24) enc<24, false>(A, vec, s);
+    else if (bits == 32) enc<32, false>(A, vec, s);
     else return DSP_ERR_UNSUPPORTED;
     DSPB_HIP(hipGetLastError());
     return DSP_OK;

@@ -99,3 +99,32 @@ def test_save_load_render_pipeline(torch_cuda, oracle, tmp_path):
     d.wav.save(str(q), out, info.sample_rate)
     y, info2 = d.wav.load(str(q))
     assert info2.format == 3 and np.array_equal(y, ref)
+
+
+@pytest.mark.parametrize("bits,is_float", [(16, False), (24, False), (32, False), (32, True)])
+@pytest.mark.parametrize("channels", [1, 2])
+@pytest.mark.parametrize("frames", [4, 4099, 70_000])
+@pytest.mark.parametrize("poff", [0, 4, 8])
+def test_encode_tile_path(torch_cuda, oracle, bits, is_float, channels, frames, poff):
+    """The mono / stereo encode tile (16-byte aligned planar rows; payload
+    stores 16, 8 or 4 bytes wide from its alignment; the last partial group
+    byte by byte), through the C ABI, against the oracle's converters."""
+    import ctypes as C
+    torch = torch_cuda
+    rng = np.random.default_rng(bits * 7 + channels + frames + poff)
+    x = (rng.random((channels, frames), dtype=np.float32) * 2.2 - 1.1).astype(np.float32)
+    rows = torch.zeros((channels, frames + 64), device="cuda")[:, :frames]   # 16-byte aligned rows
+    rows.copy_(torch.from_numpy(x))
+    nbytes = frames * channels * bits // 8
+    buf = torch.full((nbytes + 32,), 0xA5, dtype=torch.uint8, device="cuda")
+    ex = d._lib.dsp_exec(torch.cuda.current_device(), d._lib.DSP_EXEC_SYNC,
+                         C.c_void_p(torch.cuda.current_stream().cuda_stream), 0)
+    ptrs = d._lib.chan_table([rows[c].data_ptr() for c in range(channels)])
+    st = d.lib().dsp_wav_encode(ptrs, channels, frames, 3 if is_float else 1, bits,
+                                C.c_void_p(buf.data_ptr() + poff), C.byref(ex))
+    assert st == 0
+    got = buf.cpu().numpy()
+    inter = np.ascontiguousarray(x.T).ravel()
+    want = np.asarray(oracle.float_to_pcm(inter, bits, is_float)).view(np.uint8).ravel()
+    assert np.array_equal(got[poff:poff + nbytes], want)
+    assert np.all(got[:poff] == 0xA5) and np.all(got[poff + nbytes:] == 0xA5)   # nothing outside the payload
