@@ -231,9 +231,96 @@ __global__ __launch_bounds__(256) void render_wrap_kernel(RenderArgs A, uint64_t
     }
 }
 
+// Loop mode, vector path (output rows 16-byte aligned, start % 4 == 0): the
+// tile of render_vec_kernel -- kVecU float4 outputs per thread, all loads
+// before the first non-temporal store -- with the file index advanced per
+// sample and wrapped by compare (one wave-uniform 64-bit modulo per block).
+// tools/loop_probe.py: the scalar kernel rendered a stereo hour from a 10 s
+// file in 0.359 ms (3.9 TB/s of writes).
+template <MapKind K>
+__global__ __launch_bounds__(256) void render_wrap_vec_kernel(RenderArgs A, uint64_t cursor) {
+    const uint32_t c = blockIdx.y;
+    const float *x = (c < A.in_ch) ? A.in.p[c] : nullptr;
+    float *o = A.out.p[c];
+    const uint64_t n4 = (A.end - A.start) >> 2;
+    const uint64_t q0 = (uint64_t)blockIdx.x * (256u * kVecU) + threadIdx.x;
+    const uint64_t L = A.L;
+    const bool rd = K != MapKind::Ramp && x != nullptr;
+    SampleMap m = A.map;
+    m.kind = K;
+    // the block's first file index is wave-uniform (one scalar modulo per
+    // wave); lanes add 4 t < 1024 and wrap by compare when L > 1024
+    uint64_t j = 0;
+    if (rd) {
+        const uint64_t jb = (cursor + A.start + (uint64_t)blockIdx.x * (4u * 256u * kVecU)) % L;
+        j = jb + 4u * threadIdx.x;
+        if (L > 1024u) j = j >= L ? j - L : j;
+        else j %= L;
+    }
+    float4 r[kVecU];
+#pragma unroll
+    for (int u = 0; u < kVecU; ++u) {
+        const uint64_t q = q0 + 256u * (uint32_t)u;
+        if (q >= n4) continue;
+        float b[4] = {0.f, 0.f, 0.f, 0.f};
+        if (rd) {
+            const uint32_t ra = (uint32_t)(j & 3);  // the same on every lane until a wrap
+            if (ra == 0 && j + 4 <= L) {  // aligned, no wrap inside: one 16-byte load
+                const float4 t = *reinterpret_cast<const float4 *>(x + j);
+                b[0] = t.x, b[1] = t.y, b[2] = t.z, b[3] = t.w;
+            } else if (j - ra + 8 <= L) {  // two aligned 16-byte loads, shifted by ra
+                const float4 t0 = *reinterpret_cast<const float4 *>(x + (j - ra));
+                const float4 t1 = *reinterpret_cast<const float4 *>(x + (j - ra) + 4);
+                if (ra == 1) b[0] = t0.y, b[1] = t0.z, b[2] = t0.w, b[3] = t1.x;
+                else if (ra == 2) b[0] = t0.z, b[1] = t0.w, b[2] = t1.x, b[3] = t1.y;
+                else b[0] = t0.w, b[1] = t1.x, b[2] = t1.y, b[3] = t1.z;
+            } else {
+                uint64_t jj = j;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    b[k] = x[jj];
+                    jj = jj + 1 == L ? 0 : jj + 1;
+                }
+            }
+            j += 4u * 256u;  // the next float4 of this thread
+            if (L > 1024u) j = j >= L ? j - L : j;
+            else j %= L;
+        }
+        const uint64_t g = A.goff + A.start + 4 * q;
+        r[u] = make_float4(apply_map(m, b[0], g), apply_map(m, b[1], g + 1), apply_map(m, b[2], g + 2),
+                           apply_map(m, b[3], g + 3));
+    }
+#pragma unroll
+    for (int u = 0; u < kVecU; ++u) {
+        const uint64_t q = q0 + 256u * (uint32_t)u;
+        if (q < n4)
+            __builtin_nontemporal_store(f4nt{r[u].x, r[u].y, r[u].z, r[u].w},
+                                        reinterpret_cast<f4nt *>(o + A.start + 4 * q));
+    }
+    if (blockIdx.x == 0 && threadIdx.x < ((A.end - A.start) & 3)) {
+        const uint64_t i = A.start + 4 * n4 + threadIdx.x;
+        const float b = rd ? x[(cursor + i) % L] : 0.f;
+        o[i] = apply_map(m, b, A.goff + i);
+    }
+}
+
 int launch_render_wrap(const RenderArgs &A, uint32_t C, uint64_t cursor, hipStream_t s) {
     if (A.end <= A.start || C == 0) return DSP_OK;
     if (A.in_ch && (A.L == 0 || cursor >= A.L)) return DSP_ERR_INVALID;
+    bool vec = (A.start & 3) == 0;
+    for (uint32_t c = 0; c < C && vec; ++c) vec = ((uintptr_t)A.out.p[c] & 15u) == 0;
+    const uint64_t tiles = (((A.end - A.start) >> 2) + 256u * kVecU - 1) / (256u * kVecU);
+    if (vec && tiles <= 0x7fffffffull) {
+        const dim3 vgrid(tiles ? (uint32_t)tiles : 1u, C);
+        switch (A.map.kind) {
+        case MapKind::Noop: hipLaunchKernelGGL(render_wrap_vec_kernel<MapKind::Noop>, vgrid, dim3(256), 0, s, A, cursor); break;
+        case MapKind::Gain: hipLaunchKernelGGL(render_wrap_vec_kernel<MapKind::Gain>, vgrid, dim3(256), 0, s, A, cursor); break;
+        case MapKind::Ramp: hipLaunchKernelGGL(render_wrap_vec_kernel<MapKind::Ramp>, vgrid, dim3(256), 0, s, A, cursor); break;
+        default: return DSP_ERR_INVALID;
+        }
+        DSPB_HIP(hipGetLastError());
+        return DSP_OK;
+    }
     uint32_t gx = stream_grid(A.end - A.start);
     gx = (gx + C - 1) / C;
     if (gx == 0) gx = 1;
