@@ -169,9 +169,14 @@ __device__ __forceinline__ void transpose_pl(const cx2 (&Q)[32], float *lds, uin
 // Everything up to the last combine: R holds the second DFT64's even/odd
 // DFT32 halves (combine64p / combine64_dir finish it).
 // PL: the transpose goes through transpose_pl's 64 x 33 tile.
-template <bool INV, bool BAR_DFT, bool BAR_TW, bool PL = false, bool AB_NOXP = false>
+// HOOK: called once the transpose's last LDS read has completed (the tile
+// is free from there on; stft8192_mem_pf_kernel prefetches into it).
+struct NoHook {
+    __device__ void operator()() const {}
+};
+template <bool INV, bool BAR_DFT, bool BAR_TW, bool PL = false, bool AB_NOXP = false, typename HOOK = NoHook>
 __device__ __forceinline__ void fft4096_pk_front(cx2 (&P)[32], float *lds, const cx (&tlo)[8], const cx2 (&thp)[4],
-                                                 uint32_t lane, cx2 (&R)[32]) {
+                                                 uint32_t lane, cx2 (&R)[32], const HOOK &hook = HOOK{}) {
     // DFT64 over the register index: even/odd DFT32 in the halves, combine
     x2dft32_dir<BAR_DFT, INV>(P);
     cx2 Q[32];  // Q[k] = (Y[k], Y[k+32]) * (W4096^(+-l k), W4096^(+-l (k+32)))
@@ -216,6 +221,10 @@ __device__ __forceinline__ void fft4096_pk_front(cx2 (&P)[32], float *lds, const
     lds_fence();
 #pragma unroll
     for (int j = 0; j < 32; ++j) R[j].i = v2f{lds[(2 * j) * 65 + lane], lds[(2 * j + 1) * 65 + lane]};
+    if constexpr (!__is_same(HOOK, NoHook)) {
+        lds_fence();
+        hook();
+    }
     // DFT64 over the other index (its combine is the caller's)
     x2dft32_dir<BAR_DFT, INV>(R);
 }
@@ -231,11 +240,11 @@ __device__ __forceinline__ void fft4096_pk(cx2 (&P)[32], float *lds, const cx (&
 // The same transform with a packed last combine: Y2[q] = (U[l + 64 q],
 // U[l + 64 (q + 32)]) in the halves of one cx2 (forward only) -- 6 packed
 // instructions per pair instead of 8 scalar ones.
-template <bool BAR_DFT = true, bool BAR_TW = true, bool AB_NOXP = false>
+template <bool BAR_DFT = true, bool BAR_TW = true, bool AB_NOXP = false, typename HOOK = NoHook>
 __device__ __forceinline__ void fft4096_pk_y2(cx2 (&P)[32], float *lds, const cx (&tlo)[8], const cx2 (&thp)[4],
-                                              uint32_t lane, cx2 (&Y2)[32]) {
+                                              uint32_t lane, cx2 (&Y2)[32], const HOOK &hook = HOOK{}) {
     cx2 R[32];
-    fft4096_pk_front<false, BAR_DFT, BAR_TW, false, AB_NOXP>(P, lds, tlo, thp, lane, R);
+    fft4096_pk_front<false, BAR_DFT, BAR_TW, false, AB_NOXP, HOOK>(P, lds, tlo, thp, lane, R, hook);
     combine64p(R, Y2);
 }
 

@@ -6,6 +6,19 @@
 
 namespace dspb {
 
+int launch_mem_pf(const Stft8kArgs &A, uint32_t C, hipStream_t stream) {
+    // H = 4096 and whole frames only (the kernel's addressing)
+    if (A.H != 4096u || A.valid < 8192u || A.K != 4097u || !A.wbase) return DSP_ERR_INVALID;
+    int dev = 0, cus = 0;
+    DSPB_HIP(hipGetDevice(&dev));
+    DSPB_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    const uint64_t units = A.F * C, groups = (units + 3) / 4;
+    const uint32_t g = (uint32_t)(groups < 2ull * (uint64_t)cus ? groups : 2ull * (uint64_t)cus);
+    hipLaunchKernelGGL(stft8192_mem_pf_kernel<0>, dim3(g), dim3(256), 0, stream, A, C);
+    DSPB_HIP(hipGetLastError());
+    return DSP_OK;
+}
+
 int launch_pk_ab(const Stft8kArgs &A, bool fused, int opt, dim3 grid, hipStream_t stream) {
     if (!fused) {  // kPkMemAos
         hipLaunchKernelGGL((stft8192_pk_kernel<kSrcMemory, kKHalf, MapKind::Noop, true, true, 0, kPkMemAos>), grid,

@@ -1,0 +1,67 @@
+"""Interleaved in-process A/B of the memory-source STFT: stft8192_pk_kernel's
+MSOA path (opt 0) against stft8192_mem_pf_kernel (opt 16384, persistent grid,
+next frame's first hop prefetched into LDS), on 1 h of stereo at SR (default
+96 kHz: BASELINE cfg 4; 48000 gives the second half of the generic
+render + STFT).
+
+    python tools/ab_mem_pf.py ROUNDS [SR]
+
+Each round runs each option for 20 launches after 10 warm ones and records
+the average launch time from libdspbench's own HIP events; round 0 checks
+that both produce the same bits."""
+import ctypes as C
+import os
+import statistics
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "dsp-bench_amd"))
+os.environ.setdefault("DSPBENCH_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)), "..",
+                                                   "dsp-bench_amd", "build", "ab", "libdspbench_ab.so"))
+import dspbench as d  # noqa: E402
+
+rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 6
+SR = int(sys.argv[2]) if len(sys.argv) > 2 else 96_000
+L_ = SR * 3600
+g = torch.Generator(device="cuda").manual_seed(7)
+x = torch.rand((2, L_), device="cuda", generator=g) * 2 - 1
+F = d.stft_frames(L_, 8192, 4096)
+mag = torch.empty((2, F, 4097), device="cuda")
+lib = d.lib()
+OPTS = (0, 16384)
+res = {o: [] for o in OPTS}
+ref = None
+for rnd in range(rounds):
+    for o in OPTS:
+        lib.dsp_stft_pk_ab_options(o)
+        for _ in range(10):
+            d.stft_magnitude(x, out=mag)
+        torch.cuda.synchronize()
+        if rnd == 0:
+            if ref is None:
+                ref = mag.clone()
+            else:
+                same = torch.equal(mag, ref)
+                print(f"opt {o}: bit-identical to opt {OPTS[0]}: {same}", flush=True)
+                assert same, f"option {o} changed the output"
+                mag.zero_()
+                d.stft_magnitude(x, out=mag)
+                torch.cuda.synchronize()
+                assert torch.equal(mag, ref), "a rerun into a zeroed output differs"
+        lib.dsp_kernel_timing(None, None, None)
+        lib.dsp_kernel_timing_enable(1)
+        for _ in range(20):
+            d.stft_magnitude(x, out=mag)
+        torch.cuda.synchronize()
+        lib.dsp_kernel_timing_enable(0)
+        ms, n, b = C.c_double(), C.c_uint64(), C.c_uint64()
+        lib.dsp_kernel_timing(C.byref(ms), C.byref(n), C.byref(b))
+        res[o].append(ms.value / n.value)
+    print(f"round {rnd}: " + "  ".join(f"{o}: {res[o][-1]:.4f} ms" for o in OPTS), flush=True)
+lib.dsp_stft_pk_ab_options(0)
+byt = b.value / n.value
+for o, v in res.items():
+    med = statistics.median(v)
+    print(f"opt {o:5d}: median {med:.4f} ms  min {min(v):.4f} ms  ({byt / med / 1e6:.1f} GB/s, "
+          f"{byt / med / 8e9 * 1e3 / 1e3:.3f} of 8 TB/s)")
