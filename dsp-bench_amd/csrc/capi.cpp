@@ -374,7 +374,7 @@ static void ols_table(const float *taps, uint32_t T, float *out) {
     out[8193] = (float)(im[2048] * sc);
 }
 
-static int g_fir_method = 0;  // 0 auto (overlap-save when T <= 1025), 1 direct, 2 overlap-save, 3 overlap-save at 3 waves per SIMD
+static int g_fir_method = 0;  // 0 auto (overlap-save when T <= 1025), 1 direct, 2 overlap-save
 
 // IR_test (build/IR_test.cpp:47-58) runs `gain -= step` in double from the
 // float parameters.  The sequence is often exact -- every partial result a
@@ -568,7 +568,7 @@ static int render_device(const float *const *in, uint32_t in_ch, uint64_t L, flo
                 A.H = map.olsH;
                 A.h2048 = v2f{map.olsH2048[0], map.olsH2048[1]};
                 A.tw = tw;
-                if ((st = launch_fir_fft(A, cn, s, g_fir_method == 3))) return st;
+                if ((st = launch_fir_fft(A, cn, s))) return st;
             }
             return DSP_OK;
         }
@@ -705,7 +705,7 @@ int dsp_abi_version(void) { return DSPBENCH_ABI_VERSION; }
 
 int dsp_fir_method(int m) {
     const int old = g_fir_method;
-    if (m >= 0 && m <= 3) g_fir_method = m;
+    if (m >= 0 && m <= 2) g_fir_method = m;
     return old;
 }
 
