@@ -80,7 +80,16 @@ struct Slot {
 struct Resources {
     std::vector<Slot> slots;
     hipStream_t up = nullptr, down = nullptr;
+    hipStream_t compute = nullptr;  // the caller's stream (not owned)
+    bool compute_used = false;
+    int prev_device = -1;           // restored on exit
     ~Resources() {
+        // an early return leaves copies and kernels in flight on the slots'
+        // buffers: drain them before the buffers go
+        if (up) (void)hipStreamSynchronize(up);
+        if (compute_used) (void)hipStreamSynchronize(compute);
+        if (down) (void)hipStreamSynchronize(down);
+        (void)hipGetLastError();
         for (Slot &s : slots) {
             if (s.d_up) (void)hipFree(s.d_up);
             if (s.d_in) (void)hipFree(s.d_in);
@@ -94,6 +103,7 @@ struct Resources {
         }
         if (up) (void)hipStreamDestroy(up);
         if (down) (void)hipStreamDestroy(down);
+        if (prev_device >= 0) (void)hipSetDevice(prev_device);
     }
 };
 
@@ -111,10 +121,15 @@ int run(const Source &src, uint32_t C, uint32_t B, float sr, const dsp_plugin *p
         if (!out[c] || (stft && (!mag || !mag[c]))) return invalid("out / mag row is NULL");
     const uint64_t L = src.wav() ? src.info.frames : src.L;
     const uint32_t Cin = std::min<uint32_t>(src.wav() ? src.info.channels : src.in_channels, C);
+    Resources R;  // declared first: restores the caller's device on every return
     int dev = -1;
     PL_HIP(hipGetDevice(&dev));
-    if (ex && ex->device >= 0 && ex->device != dev) PL_HIP(hipSetDevice(ex->device));
+    if (ex && ex->device >= 0 && ex->device != dev) {
+        PL_HIP(hipSetDevice(ex->device));
+        R.prev_device = dev;
+    }
     const hipStream_t cs = ex ? (hipStream_t)ex->stream : nullptr;
+    R.compute = cs;
     const uint64_t goff = ex ? ex->sample_offset : 0;
     if (goff % B) return invalid("sample_offset must be a multiple of B");
     // render-only: chunks of whole blocks without a halo (N = H = B)
@@ -151,7 +166,6 @@ int run(const Source &src, uint32_t C, uint32_t B, float sr, const dsp_plugin *p
         for (uint32_t c = 0; c < Cin; ++c) in_pinned = in_pinned && is_pinned(src.rows[c]);
     for (uint32_t c = 0; c < C; ++c) out_pinned = out_pinned && is_pinned(out[c]) && (!stft || is_pinned(mag[c]));
 
-    Resources R;
     R.slots.resize(std::min<int64_t>(n, 2));
     PL_HIP(hipStreamCreateWithFlags(&R.up, hipStreamNonBlocking));
     PL_HIP(hipStreamCreateWithFlags(&R.down, hipStreamNonBlocking));
@@ -218,6 +232,7 @@ int run(const Source &src, uint32_t C, uint32_t B, float sr, const dsp_plugin *p
         }
         PL_HIP(hipEventRecord(s.up_done, R.up));
         // ---- compute (decode + render [+ STFT]) on the caller's stream
+        R.compute_used = true;
         PL_HIP(hipStreamWaitEvent(cs, s.up_done, 0));
         dsp_exec e{};
         e.device = -1;
