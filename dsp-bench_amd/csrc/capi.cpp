@@ -128,15 +128,6 @@ static int get_tw(int dev, const v2f **out) {
                 h.push_back(v2f{a.x, b.x});
                 h.push_back(v2f{a.y, b.y});
             }
-        // the full stage-twiddle table (stft_pk.hpp kPkTwTab, at kTwTabOff):
-        // float4 [64 k + l] = (re W4096^(l k), re W4096^(l (k + 32)), im .., im ..),
-        // W4096^m = T8192[2 m]
-        for (int k = 0; k < 32; ++k)
-            for (int l = 0; l < 64; ++l) {
-                const v2f a = h[(2 * l * k) & 8191], b = h[(2 * l * (k + 32)) & 8191];
-                h.push_back(v2f{a.x, b.x});
-                h.push_back(v2f{a.y, b.y});
-            }
         v2f *d = nullptr;
         DSPB_HIP(hipMalloc(&d, sizeof(v2f) * h.size()));
         if (int st = upload_table(d, h.data(), sizeof(v2f) * h.size())) {
@@ -721,7 +712,7 @@ int dsp_fir_method(int m) {
 #ifdef DSPB_AB_BUILD
 int dsp_stft_pk_ab_options(int opt) {
     const int old = g_pk_ab_opt;
-    if (opt >= 0 && opt <= 0xfffff) g_pk_ab_opt = opt;
+    if (opt >= 0 && opt <= 0xffff) g_pk_ab_opt = opt;
     return old;
 }
 #endif

@@ -174,38 +174,20 @@ __device__ __forceinline__ void transpose_pl(const cx2 (&Q)[32], float *lds, uin
 struct NoHook {
     __device__ void operator()() const {}
 };
-// TWT (A/B): the stage twiddles (W4096^(l k), W4096^(l (k + 32))) read from
-// a lane-major table twt[64 k + l] (get_tw, float64-rounded) eight
-// iterations ahead, instead of formed as tlo x thp products (4 VALU each)
-template <bool INV, bool BAR_DFT, bool BAR_TW, bool PL = false, bool AB_NOXP = false, bool TWT = false,
-          typename HOOK = NoHook>
+template <bool INV, bool BAR_DFT, bool BAR_TW, bool PL = false, bool AB_NOXP = false, typename HOOK = NoHook>
 __device__ __forceinline__ void fft4096_pk_front(cx2 (&P)[32], float *lds, const cx (&tlo)[8], const cx2 (&thp)[4],
-                                                 uint32_t lane, cx2 (&R)[32], const float4 *twt = nullptr,
-                                                 const HOOK &hook = HOOK{}) {
-    constexpr int kD = 8;  // TWT: loads in flight
-    float4 wq[32];
+                                                 uint32_t lane, cx2 (&R)[32], const HOOK &hook = HOOK{}) {
     // DFT64 over the register index: even/odd DFT32 in the halves, combine
     x2dft32_dir<BAR_DFT, INV>(P);
     cx2 Q[32];  // Q[k] = (Y[k], Y[k+32]) * (W4096^(+-l k), W4096^(+-l (k+32)))
     {
         cx2 Y[32];
         combine64p_dir<INV>(P, Y);
-        if constexpr (TWT) {
-            if (BAR_TW) __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int k = 0; k < kD; ++k) wq[k] = twt[64u * (uint32_t)k + lane];
-        }
 #pragma unroll
         for (int k = 0; k < 32; ++k) {
             if (BAR_TW) __builtin_amdgcn_sched_barrier(0);
-            cx2 w;
-            if constexpr (TWT) {
-                if (k + kD < 32) wq[k + kD] = twt[64u * (uint32_t)(k + kD) + lane];
-                w = cx2{v2f{wq[k].x, wq[k].y}, v2f{wq[k].z, wq[k].w}};
-            } else {
-                const int lo = k & 7, hi = k >> 3;
-                w = lo ? cmulb(tlo[lo], thp[hi]) : thp[hi];
-            }
+            const int lo = k & 7, hi = k >> 3;
+            const cx2 w = lo ? cmulb(tlo[lo], thp[hi]) : thp[hi];
             Q[k] = cmul2(Y[k], conj2<INV>(w));
         }
     }
@@ -258,12 +240,11 @@ __device__ __forceinline__ void fft4096_pk(cx2 (&P)[32], float *lds, const cx (&
 // The same transform with a packed last combine: Y2[q] = (U[l + 64 q],
 // U[l + 64 (q + 32)]) in the halves of one cx2 (forward only) -- 6 packed
 // instructions per pair instead of 8 scalar ones.
-template <bool BAR_DFT = true, bool BAR_TW = true, bool AB_NOXP = false, bool TWT = false, typename HOOK = NoHook>
+template <bool BAR_DFT = true, bool BAR_TW = true, bool AB_NOXP = false, typename HOOK = NoHook>
 __device__ __forceinline__ void fft4096_pk_y2(cx2 (&P)[32], float *lds, const cx (&tlo)[8], const cx2 (&thp)[4],
-                                              uint32_t lane, cx2 (&Y2)[32], const float4 *twt = nullptr,
-                                              const HOOK &hook = HOOK{}) {
+                                              uint32_t lane, cx2 (&Y2)[32], const HOOK &hook = HOOK{}) {
     cx2 R[32];
-    fft4096_pk_front<false, BAR_DFT, BAR_TW, false, AB_NOXP, TWT, HOOK>(P, lds, tlo, thp, lane, R, twt, hook);
+    fft4096_pk_front<false, BAR_DFT, BAR_TW, false, AB_NOXP, HOOK>(P, lds, tlo, thp, lane, R, hook);
     combine64p(R, Y2);
 }
 

@@ -42,8 +42,7 @@ namespace dspb {
 // fewer per frame, the same bits)
 enum { kPkNoBarDft = 1, kPkNoBarTw = 2, kPkNoBarSplit = 4, kPkRenderCached = 8, kPkNtMag = 16, kPkMagLds = 32,
        kPkOldSplit = 64, kPkAbNoRender = 128, kPkAbNoMag = 256, kPkMagStage = 512, kPkOcc3 = 1024,
-       kPkMemAos = 2048, kPkNoRemap = 4096, kPkAbNoXpose = 8192, kPkMemPf = 16384, kPkTwTab = 32768 };
-// 32768 = stage twiddles from get_tw's lane-major table (fft_pk.hpp TWT)
+       kPkMemAos = 2048, kPkNoRemap = 4096, kPkAbNoXpose = 8192, kPkMemPf = 16384 };
 // 16384 = memory frames on stft8192_mem_pf_kernel (persistent, LDS hop prefetch)
 // 8192: ablation only (results discarded): no LDS transpose
 // 4096 = frames in dispatch order (no XCD remap: all XCDs write one frontier)
@@ -58,9 +57,6 @@ enum { kPkNoBarDft = 1, kPkNoBarTw = 2, kPkNoBarSplit = 4, kPkRenderCached = 8, 
 // 128 / 256: ablation only (A/B of what the stores cost): skip the render
 // stores / the magnitude stores of split_y2 (results discarded)
 constexpr int kPkDefaultOpt = 0;
-// get_tw (capi.cpp): T8192, the lane-major tlo rows, the thp pairs, then the
-// full stage-twiddle table of kPkTwTab at this v2f offset
-constexpr uint32_t kTwTabOff = 8192u + 896u + 512u;
 
 typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));  // a row is only dword-aligned
 typedef float f4a __attribute__((ext_vector_type(4)));               // 16-byte aligned
@@ -248,7 +244,7 @@ __global__ __launch_bounds__(256, OCC) void stft8192_pk_kernel(Stft8kArgs A) {
                   "3 waves per SIMD: the PER path with split_y2");
     cx tlo[8];
     cx2 thp[4];
-    if constexpr (OCC == 2 && !(OPT & kPkTwTab)) {  // (OCC 3 loads them inside fft4096_pk_y2_lo)
+    if constexpr (OCC == 2) {  // (OCC 3 loads them inside fft4096_pk_y2_lo)
 #pragma unroll
         for (int j = 1; j < 8; ++j) {
             const v2f a = (A.tw + 8192u + 64u * (uint32_t)(j - 1))[lane];
@@ -400,8 +396,7 @@ __global__ __launch_bounds__(256, OCC) void stft8192_pk_kernel(Stft8kArgs A) {
         // Y2[q] = (Z[l + 64 q], Z[l + 64 (q + 32)])
         cx2 Y2[32];
         if constexpr (OCC >= 3) fft4096_pk_y2_lo<!(OPT & kPkNoBarDft)>(P, lds, A.tw, lane, Y2);
-        else fft4096_pk_y2<!(OPT & kPkNoBarDft), !(OPT & kPkNoBarTw), (OPT & kPkAbNoXpose) != 0, (OPT & kPkTwTab) != 0>(
-            P, lds, tlo, thp, lane, Y2, reinterpret_cast<const float4 *>(A.tw + kTwTabOff));
+        else fft4096_pk_y2<!(OPT & kPkNoBarDft), !(OPT & kPkNoBarTw), (OPT & kPkAbNoXpose) != 0>(P, lds, tlo, thp, lane, Y2);
         split_y2<KM, !(OPT & kPkNoBarSplit), (OPT & kPkAbNoMag) != 0, KM == kKHalf && (OPT & kPkMagStage) != 0,
                  (OPT & kPkNtMag) != 0>(Y2, A.mag.p[ch] + f * A.ld, A.K, A.tw, lane, lds);
         return;
@@ -586,7 +581,7 @@ __global__ __launch_bounds__(256, 2) void stft8192_mem_pf_kernel(Stft8kArgs A, u
         const uint64_t un = u + W;
         const bool more = un < U;
         cx2 Y2[32];
-        fft4096_pk_y2<true, true>(P, lds, tlo, thp, lane, Y2, nullptr, [&]() {
+        fft4096_pk_y2<true, true>(P, lds, tlo, thp, lane, Y2, [&]() {
             if (more) pf_hop(A.in.p[cn] + (uint64_t)fn * 4096u, lds, lane);
         });
         // the prefetch lands before the split's stores are issued, so the

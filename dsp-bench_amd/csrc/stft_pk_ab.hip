@@ -76,8 +76,6 @@ int launch_pk_ab(const Stft8kArgs &A, bool fused, int opt, dim3 grid, hipStream_
         DSPB_PK_CASE(kPkAbNoRender);
         DSPB_PK_CASE(kPkAbNoMag);
         DSPB_PK_CASE(kPkAbNoRender | kPkAbNoMag);
-        DSPB_PK_CASE(kPkTwTab);
-        DSPB_PK_CASE(kPkTwTab | kPkNoBarTw);
 #undef DSPB_PK_CASE
     default: return DSP_ERR_INVALID;
     }
