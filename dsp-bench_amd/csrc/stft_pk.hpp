@@ -56,7 +56,10 @@ enum { kPkNoBarDft = 1, kPkNoBarTw = 2, kPkNoBarSplit = 4, kPkRenderCached = 8, 
 // dword row stores non-temporal)
 // 128 / 256: ablation only (A/B of what the stores cost): skip the render
 // stores / the magnitude stores of split_y2 (results discarded)
-constexpr int kPkDefaultOpt = 0;
+// default: no scheduling barriers (round 2: 1.0-1.7% faster on the headline,
+// 0.1-0.5% on the memory and gain STFTs, the same VGPRs and spills;
+// profiles/r02_default_opt_ab.txt)
+constexpr int kPkDefaultOpt = kPkNoBarDft | kPkNoBarTw | kPkNoBarSplit;
 
 typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));  // a row is only dword-aligned
 typedef float f4a __attribute__((ext_vector_type(4)));               // 16-byte aligned
