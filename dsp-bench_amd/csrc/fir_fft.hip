@@ -86,7 +86,7 @@ __device__ __forceinline__ void fir_fft_frame(const FirFftArgs &A, uint64_t f, u
     }
 
     cx zp[32], zm[32];
-    fft4096_pk<false, true, true, true>(P, lds, tlo, thp, lane, zp, zm);
+    fft4096_pk<false, false, false, true>(P, lds, tlo, thp, lane, zp, zm);
 
     // ---- split, H multiply, inverse split, paired over (ka, ka + 16) --------
     const uint32_t src = ((64u - lane) & 63u) * 4u;
@@ -151,7 +151,7 @@ __device__ __forceinline__ void fir_fft_frame(const FirFftArgs &A, uint64_t f, u
         asm volatile("" : "+s"(salt));
         load_stage_tw(A.tw, lane, salt, tlo, thp);
     }
-    fft4096_pk<true, true, true, true>(Q, lds, tlo, thp, lane, yp, ym);
+    fft4096_pk<true, false, false, true>(Q, lds, tlo, thp, lane, yp, ym);
 
     // ---- outputs: m = l + 64 b, b >= 8 -> y[f H + 2l + 128 (b - 8)] ----------
     float *o = A.out.p[ch];
