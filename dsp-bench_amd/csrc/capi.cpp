@@ -712,7 +712,7 @@ int dsp_fir_method(int m) {
 #ifdef DSPB_AB_BUILD
 int dsp_stft_pk_ab_options(int opt) {
     const int old = g_pk_ab_opt;
-    if (opt >= 0 && opt <= 0xffff) g_pk_ab_opt = opt;
+    if (opt >= 0 && opt <= 0xfffff) g_pk_ab_opt = opt;
     return old;
 }
 #endif

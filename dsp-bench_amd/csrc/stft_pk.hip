@@ -47,7 +47,7 @@ int launch_stft8192_pk(const Stft8kArgs &A, uint32_t C, bool fused, int opt, hip
     // PER path: extra waves for the render tail [F H, tail_end)
     const uint64_t tail = A.tail_end > A.F * A.H ? (A.tail_end - A.F * A.H + A.H - 1) / A.H : 0;
     if (tail && !stft8192_pk_per_path(A, fused)) return DSP_ERR_INVALID;
-    const uint64_t groups = (A.F + tail + 3) / 4;
+    const uint64_t groups = (A.F + tail + kPkWpb - 1) / kPkWpb;  // workgroups of the default kernels
     if (groups > 0x7fffffffull) return DSP_ERR_INVALID;
     dim3 grid((uint32_t)groups, C);
     const int km = A.K == 4097u ? kKHalf : (A.K == 8192u ? kKMirror : kKPartial);
@@ -60,8 +60,11 @@ int launch_stft8192_pk(const Stft8kArgs &A, uint32_t C, bool fused, int opt, hip
         if (per == 4 && opt) return launch_pk_ab(A, fused, opt, grid, stream);  // A/B at the headline shape
 #endif
 #define DSPB_PK_PER(p) \
-    hipLaunchKernelGGL((stft8192_pk_kernel<kSrcRender, kKHalf, MapKind::Ramp, true, true, p>), grid, dim3(256), \
-                       0, stream, A)
+    hipLaunchKernelGGL((stft8192_pk_kernel<kSrcRender, kKHalf, MapKind::Ramp, true, true, p, kPkPerOpt>), grid_per, \
+                       dim3(64 * kPkPerWpb), 0, stream, A)
+        const uint64_t groups_per = (A.F + tail + kPkPerWpb - 1) / kPkPerWpb;
+        if (groups_per > 0x7fffffffull) return DSP_ERR_INVALID;
+        const dim3 grid_per((uint32_t)groups_per, C);
         switch (per) {
         case 1: DSPB_PK_PER(1); break;
         case 2: DSPB_PK_PER(2); break;

@@ -42,7 +42,8 @@ namespace dspb {
 // fewer per frame, the same bits)
 enum { kPkNoBarDft = 1, kPkNoBarTw = 2, kPkNoBarSplit = 4, kPkRenderCached = 8, kPkNtMag = 16, kPkMagLds = 32,
        kPkOldSplit = 64, kPkAbNoRender = 128, kPkAbNoMag = 256, kPkMagStage = 512, kPkOcc3 = 1024,
-       kPkMemAos = 2048, kPkNoRemap = 4096, kPkAbNoXpose = 8192, kPkMemPf = 16384 };
+       kPkMemAos = 2048, kPkNoRemap = 4096, kPkAbNoXpose = 8192, kPkMemPf = 16384, kPkW1 = 65536 };
+// 65536 = one wave per workgroup (64 threads, one 64 x 65 tile): a slot frees as its frame ends
 // 16384 = memory frames on stft8192_mem_pf_kernel (persistent, LDS hop prefetch)
 // 8192: ablation only (results discarded): no LDS transpose
 // 4096 = frames in dispatch order (no XCD remap: all XCDs write one frontier)
@@ -60,6 +61,11 @@ enum { kPkNoBarDft = 1, kPkNoBarTw = 2, kPkNoBarSplit = 4, kPkRenderCached = 8, 
 // 0.1-0.5% on the memory and gain STFTs, the same VGPRs and spills;
 // profiles/r02_default_opt_ab.txt)
 constexpr int kPkDefaultOpt = kPkNoBarDft | kPkNoBarTw | kPkNoBarSplit;
+// the fused IR_test (PER) kernels of the headline add one wave per workgroup:
+// 0.8-2.2% faster there, but 1-2% slower for the paths that read a signal
+// (memory, gain), whose four-frame workgroups share their hops in L2
+// (profiles/r02_w1_ab.txt)
+constexpr int kPkPerOpt = kPkDefaultOpt | kPkW1;
 
 typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));  // a row is only dword-aligned
 typedef float f4a __attribute__((ext_vector_type(4)));               // 16-byte aligned
@@ -204,13 +210,24 @@ __device__ __forceinline__ void split_y2(const cx2 (&Y2)[32], float *mrow, uint3
 // values of b (PER = max(1, B / 128)), so only v[0 .. PER) are fetched from
 // the block table -- 4 gathers at B = 512 -- and v[b] = v[b mod PER] is a
 // register alias.  PER = 0: generic path.
+template <int OPT>
+constexpr uint32_t pk_waves_per_block() { return (OPT & kPkW1) ? 1u : 4u; }
+// waves per workgroup of the default and the PER kernels (the launches size
+// their grids by them)
+constexpr uint32_t kPkWpb = pk_waves_per_block<kPkDefaultOpt>();
+constexpr uint32_t kPkPerWpb = pk_waves_per_block<kPkPerOpt>();
+
 template <int SRC, int KM, MapKind MK, bool POW2, bool WINC, int PER = 0, int OPT = kPkDefaultOpt, int OCC = 2>
-__global__ __launch_bounds__(256, OCC) void stft8192_pk_kernel(Stft8kArgs A) {
-    __shared__ __attribute__((aligned(16))) float lds_all[4][OCC >= 3 ? 64 * 33 : 64 * 65];
+// (OCC waves per SIMD whatever the workgroup size: stated as waves per EU,
+// which __launch_bounds__' workgroup count does not pin for one-wave groups)
+__global__ __launch_bounds__(64 * pk_waves_per_block<OPT>()) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
+void stft8192_pk_kernel(Stft8kArgs A) {
+    constexpr uint32_t WPB = pk_waves_per_block<OPT>();
+    __shared__ __attribute__((aligned(16))) float lds_all[WPB][OCC >= 3 ? 64 * 33 : 64 * 65];
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t ch = blockIdx.y;
-    const uint64_t f = (uint64_t)((OPT & kPkNoRemap) ? blockIdx.x : xcd_remap(blockIdx.x, gridDim.x)) * 4u + wave;
+    const uint64_t f = (uint64_t)((OPT & kPkNoRemap) ? blockIdx.x : xcd_remap(blockIdx.x, gridDim.x)) * WPB + wave;
     constexpr bool SOA = WINC && MK == MapKind::Ramp && PER > 0 && SRC == kSrcRender;
     // memory frames with the computed window: two dwordx2 loads per pair
     // (columns 2j, 2j+1) regrouped into even/odd halves

@@ -19,7 +19,9 @@ int launch_mem_pf(const Stft8kArgs &A, uint32_t C, hipStream_t stream) {
     return DSP_OK;
 }
 
-int launch_pk_ab(const Stft8kArgs &A, bool fused, int opt, dim3 grid, hipStream_t stream) {
+int launch_pk_ab(const Stft8kArgs &A, bool fused, int opt, dim3 grid_default, hipStream_t stream) {
+    // the variants below are four-wave workgroups; grid_default is sized for kPkWpb
+    const dim3 grid((grid_default.x * kPkWpb + 3) / 4, grid_default.y);
     if (!fused) {  // kPkMemAos
         hipLaunchKernelGGL((stft8192_pk_kernel<kSrcMemory, kKHalf, MapKind::Noop, true, true, 0, kPkMemAos>), grid,
                            dim3(256), 0, stream, A);

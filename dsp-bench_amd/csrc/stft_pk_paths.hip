@@ -7,11 +7,11 @@ namespace dspb {
 template <int SRC, MapKind MK, bool POW2, bool WINC>
 static void launch_pk_km(int km, dim3 grid, hipStream_t s, const Stft8kArgs &A) {
     if (km == kKHalf)
-        hipLaunchKernelGGL((stft8192_pk_kernel<SRC, kKHalf, MK, POW2, WINC>), grid, dim3(256), 0, s, A);
+        hipLaunchKernelGGL((stft8192_pk_kernel<SRC, kKHalf, MK, POW2, WINC>), grid, dim3(64 * kPkWpb), 0, s, A);
     else if (km == kKMirror)
-        hipLaunchKernelGGL((stft8192_pk_kernel<SRC, kKMirror, MK, POW2, WINC>), grid, dim3(256), 0, s, A);
+        hipLaunchKernelGGL((stft8192_pk_kernel<SRC, kKMirror, MK, POW2, WINC>), grid, dim3(64 * kPkWpb), 0, s, A);
     else
-        hipLaunchKernelGGL((stft8192_pk_kernel<SRC, kKPartial, MK, POW2, WINC>), grid, dim3(256), 0, s, A);
+        hipLaunchKernelGGL((stft8192_pk_kernel<SRC, kKPartial, MK, POW2, WINC>), grid, dim3(64 * kPkWpb), 0, s, A);
 }
 
 int launch_pk_paths(const Stft8kArgs &A, bool fused, int km, bool pow2, bool winc, dim3 grid, hipStream_t stream) {
@@ -26,7 +26,7 @@ int launch_pk_paths(const Stft8kArgs &A, bool fused, int km, bool pow2, bool win
         default: return DSP_ERR_INVALID;
         }
     } else if (winc) {
-        hipLaunchKernelGGL((stft8192_pk_kernel<kSrcMemory, kKHalf, MapKind::Noop, true, true>), grid, dim3(256), 0,
+        hipLaunchKernelGGL((stft8192_pk_kernel<kSrcMemory, kKHalf, MapKind::Noop, true, true>), grid, dim3(64 * kPkWpb), 0,
                            stream, A);
     } else {
         launch_pk_km<kSrcMemory, MapKind::Noop, true, false>(km, grid, stream, A);
