@@ -60,7 +60,7 @@ def parse():
                     help="one-kernel workloads: bracket every launch with the library's HIP events inside the "
                          "timed region (costs 0.7-1%% of a step, profiles/r02_launch_events_ab.txt); default: "
                          "kernel_avg_ms = the timed region's stream events / steps")
-    ap.add_argument("--fir-method", type=int, default=0, choices=[0, 1, 2, 3],
+    ap.add_argument("--fir-method", type=int, default=0, choices=[0, 1, 2],
                     help="fir1024: 0 auto (overlap-save), 1 direct form, 2 overlap-save")
     ap.add_argument("--workload", default="headline",
                     choices=["headline", "stft96k", "ch96k", "gain10min", "fir1024", "wav16", "wav24", "ir",

@@ -568,7 +568,7 @@ static int render_device(const float *const *in, uint32_t in_ch, uint64_t L, flo
                 A.H = map.olsH;
                 A.h2048 = v2f{map.olsH2048[0], map.olsH2048[1]};
                 A.tw = tw;
-                if ((st = launch_fir_fft(A, cn, s, g_fir_method == 3))) return st;
+                if ((st = launch_fir_fft(A, cn, s))) return st;
             }
             return DSP_OK;
         }
@@ -705,7 +705,7 @@ int dsp_abi_version(void) { return DSPBENCH_ABI_VERSION; }
 
 int dsp_fir_method(int m) {
     const int old = g_fir_method;
-    if (m >= 0 && m <= 3) g_fir_method = m;
+    if (m >= 0 && m <= 2) g_fir_method = m;
     return old;
 }
 

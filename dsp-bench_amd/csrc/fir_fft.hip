@@ -47,9 +47,7 @@ __device__ __forceinline__ void load_stage_tw(const v2f *tw, uint32_t lane, uint
 // EDGE: frames that reach before sample 0 or past L (bounds-checked loads);
 // interior frames run the EDGE = false instantiation
 // hs: the block's LDS copy of H, [2 ka + h][lane] float4 (kernel prologue)
-// HG: H read from global memory (A.H's [ka][lane][h] float4 layout,
-// L2-resident) instead of the block's LDS copy (the one-wave workgroups)
-template <bool EDGE, bool HG = false>
+template <bool EDGE>
 __device__ __forceinline__ void fir_fft_frame(const FirFftArgs &A, uint64_t f, uint32_t ch, float *lds,
                                               const float4 *hs, uint32_t lane) {
     const int64_t fs = (int64_t)(f * kOlsHop) - (int64_t)kOlsHist;  // even
@@ -114,14 +112,7 @@ __device__ __forceinline__ void fir_fft_frame(const FirFftArgs &A, uint64_t f, u
         const cx2 T = cmul2(negi(D), tw);
         const cx2 X1 = E + T;  // 2 X[k]
         const cx2 X2 = E - T;  // conj 2 X[M - k]
-        float4 ha, hb;
-        if constexpr (HG) {
-            ha = hs[128u * ka + 2u * lane];
-            hb = hs[128u * ka + 2u * lane + 1u];
-        } else {
-            ha = hs[(2u * ka) * 64u + lane];
-            hb = hs[(2u * ka + 1u) * 64u + lane];
-        }
+        const float4 ha = hs[(2u * ka) * 64u + lane], hb = hs[(2u * ka + 1u) * 64u + lane];
         const cx2 Hk = cx2{v2f{ha.x, ha.y}, v2f{ha.z, ha.w}};
         const cx2 HMk = cx2{v2f{hb.x, hb.y}, v2f{hb.z, hb.w}};
         const cx2 Yk = cmul2(X1, Hk);
@@ -211,20 +202,7 @@ __global__ __launch_bounds__(256, 2) void fir_fft_kernel(FirFftArgs A, uint64_t 
     else fir_fft_frame<false>(A, f, ch, lds_all[wave], hs, lane);
 }
 
-// one wave per workgroup (A/B, FIR method 3): a 64 x 33 tile, H from L2
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void fir_fft_w1_kernel(FirFftArgs A,
-                                                                                                  uint64_t fe) {
-    __shared__ __attribute__((aligned(16))) float lds[64 * 33];
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t ch = blockIdx.y;
-    const uint64_t f = (uint64_t)xcd_remap(blockIdx.x, gridDim.x);
-    if (f >= A.F) return;
-    const float4 *H4 = reinterpret_cast<const float4 *>(A.H);
-    if (f == 0 || f >= fe) fir_fft_frame<true, true>(A, f, ch, lds, H4, lane);
-    else fir_fft_frame<false, true>(A, f, ch, lds, H4, lane);
-}
-
-int launch_fir_fft(const FirFftArgs &A, uint32_t C, hipStream_t s, bool w1) {
+int launch_fir_fft(const FirFftArgs &A, uint32_t C, hipStream_t s) {
     if (A.F == 0 || C == 0) return DSP_OK;
     // interior frames: [1, fe) with (f H - 1024) + 8192 <= L; the rest is edge
     uint64_t fe = 1;
@@ -233,12 +211,7 @@ int launch_fir_fft(const FirFftArgs &A, uint32_t C, hipStream_t s, bool w1) {
     if (fe < 1) fe = 1;
     const uint64_t groups = (A.F + 3) / 4;
     if (groups > 0x7fffffffull) return DSP_ERR_INVALID;
-    if (w1) {
-        if (A.F > 0x7fffffffull) return DSP_ERR_INVALID;
-        hipLaunchKernelGGL(fir_fft_w1_kernel, dim3((uint32_t)A.F, C), dim3(64), 0, s, A, fe);
-    } else {
-        hipLaunchKernelGGL(fir_fft_kernel, dim3((uint32_t)groups, C), dim3(256), 0, s, A, fe);
-    }
+    hipLaunchKernelGGL(fir_fft_kernel, dim3((uint32_t)groups, C), dim3(256), 0, s, A, fe);
     DSPB_HIP(hipGetLastError());
     return DSP_OK;
 }

@@ -82,7 +82,7 @@ struct FirFftArgs {
     v2f h2048;           // H[2048]
     const v2f *tw;       // T8192 + lane-major stage twiddles (capi.cpp get_tw)
 };
-int launch_fir_fft(const FirFftArgs &A, uint32_t C, hipStream_t s, bool w1 = false);
+int launch_fir_fft(const FirFftArgs &A, uint32_t C, hipStream_t s);
 int launch_fir(const float *x, uint64_t L, float *y, uint64_t Ly, const float *h8, uint32_t T8,
                bool y_aligned16, hipStream_t s);
 int launch_minmax(const float *x, uint64_t n, uint32_t P, float *vmax, float *vmin, hipStream_t s);
