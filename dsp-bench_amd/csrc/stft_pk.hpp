@@ -42,8 +42,7 @@ namespace dspb {
 // fewer per frame, the same bits)
 enum { kPkNoBarDft = 1, kPkNoBarTw = 2, kPkNoBarSplit = 4, kPkRenderCached = 8, kPkNtMag = 16, kPkMagLds = 32,
        kPkOldSplit = 64, kPkAbNoRender = 128, kPkAbNoMag = 256, kPkMagStage = 512, kPkOcc3 = 1024,
-       kPkMemAos = 2048, kPkNoRemap = 4096, kPkAbNoXpose = 8192, kPkMemPf = 16384, kPkW1 = 65536, kPkPrio = 131072 };
-// 131072 = s_setprio 3 while the frame is loaded and windowed, 0 for the FFT
+       kPkMemAos = 2048, kPkNoRemap = 4096, kPkAbNoXpose = 8192, kPkMemPf = 16384, kPkW1 = 65536 };
 // 65536 = one wave per workgroup (64 threads, one 64 x 65 tile): a slot frees as its frame ends
 // 16384 = memory frames on stft8192_mem_pf_kernel (persistent, LDS hop prefetch)
 // 8192: ablation only (results discarded): no LDS transpose
@@ -257,7 +256,6 @@ void stft8192_pk_kernel(Stft8kArgs A) {
     }
     float *lds = lds_all[wave];
     const float *x = (ch < A.in_ch) ? A.in.p[ch] : nullptr;
-    if constexpr ((OPT & kPkPrio) != 0) __builtin_amdgcn_s_setprio(3);
 
     // ---- 0. constants, issued before the frame -----------------------------
     // tlo[j] = W4096^(l j), thp[h] = (W4096^(8 l h), W4096^(8 l (h + 4)))
@@ -412,7 +410,6 @@ void stft8192_pk_kernel(Stft8kArgs A) {
         }
     }
     }  // !SOA
-    if constexpr ((OPT & kPkPrio) != 0) __builtin_amdgcn_s_setprio(0);
 
     if constexpr (!(OPT & (kPkOldSplit | kPkMagLds))) {
         // ---- 3-5. 4096-point FFT with a packed last combine:

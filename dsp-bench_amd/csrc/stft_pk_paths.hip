@@ -2,10 +2,6 @@
 // NOOP / GAIN / non-PER IR_test renders and for the STFT of a signal in HBM.
 #include "stft_pk.hpp"
 
-#ifndef DSPB_MEM_PRIO
-#define DSPB_MEM_PRIO 0
-#endif
-
 namespace dspb {
 
 template <int SRC, MapKind MK, bool POW2, bool WINC>
@@ -30,7 +26,7 @@ int launch_pk_paths(const Stft8kArgs &A, bool fused, int km, bool pow2, bool win
         default: return DSP_ERR_INVALID;
         }
     } else if (winc) {
-        hipLaunchKernelGGL((stft8192_pk_kernel<kSrcMemory, kKHalf, MapKind::Noop, true, true, 0, kPkDefaultOpt | DSPB_MEM_PRIO>), grid, dim3(64 * kPkWpb), 0,
+        hipLaunchKernelGGL((stft8192_pk_kernel<kSrcMemory, kKHalf, MapKind::Noop, true, true>), grid, dim3(64 * kPkWpb), 0,
                            stream, A);
     } else {
         launch_pk_km<kSrcMemory, MapKind::Noop, true, false>(km, grid, stream, A);
