@@ -42,8 +42,7 @@ namespace dspb {
 // fewer per frame, the same bits)
 enum { kPkNoBarDft = 1, kPkNoBarTw = 2, kPkNoBarSplit = 4, kPkRenderCached = 8, kPkNtMag = 16, kPkMagLds = 32,
        kPkOldSplit = 64, kPkAbNoRender = 128, kPkAbNoMag = 256, kPkMagStage = 512, kPkOcc3 = 1024,
-       kPkMemAos = 2048, kPkNoRemap = 4096, kPkAbNoXpose = 8192, kPkMemPf = 16384, kPkW1 = 65536, kPkW2 = 262144 };
-// 262144 = two waves per workgroup
+       kPkMemAos = 2048, kPkNoRemap = 4096, kPkAbNoXpose = 8192, kPkMemPf = 16384, kPkW1 = 65536 };
 // 65536 = one wave per workgroup (64 threads, one 64 x 65 tile): a slot frees as its frame ends
 // 16384 = memory frames on stft8192_mem_pf_kernel (persistent, LDS hop prefetch)
 // 8192: ablation only (results discarded): no LDS transpose
@@ -61,10 +60,7 @@ enum { kPkNoBarDft = 1, kPkNoBarTw = 2, kPkNoBarSplit = 4, kPkRenderCached = 8, 
 // default: no scheduling barriers (round 2: 1.0-1.7% faster on the headline,
 // 0.1-0.5% on the memory and gain STFTs, the same VGPRs and spills;
 // profiles/r02_default_opt_ab.txt)
-#ifndef DSPB_PATH_OPT_EXTRA
-#define DSPB_PATH_OPT_EXTRA 0
-#endif
-constexpr int kPkDefaultOpt = kPkNoBarDft | kPkNoBarTw | kPkNoBarSplit | DSPB_PATH_OPT_EXTRA;
+constexpr int kPkDefaultOpt = kPkNoBarDft | kPkNoBarTw | kPkNoBarSplit;
 // the fused IR_test (PER) kernels of the headline add one wave per workgroup:
 // 0.8-2.2% faster there, but 1-2% slower for the paths that read a signal
 // (memory, gain), whose four-frame workgroups share their hops in L2
@@ -215,7 +211,7 @@ __device__ __forceinline__ void split_y2(const cx2 (&Y2)[32], float *mrow, uint3
 // the block table -- 4 gathers at B = 512 -- and v[b] = v[b mod PER] is a
 // register alias.  PER = 0: generic path.
 template <int OPT>
-constexpr uint32_t pk_waves_per_block() { return (OPT & kPkW1) ? 1u : (OPT & kPkW2) ? 2u : 4u; }
+constexpr uint32_t pk_waves_per_block() { return (OPT & kPkW1) ? 1u : 4u; }
 // waves per workgroup of the default and the PER kernels (the launches size
 // their grids by them)
 constexpr uint32_t kPkWpb = pk_waves_per_block<kPkDefaultOpt>();
