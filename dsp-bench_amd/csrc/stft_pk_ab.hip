@@ -28,14 +28,6 @@ int launch_pk_ab(const Stft8kArgs &A, bool fused, int opt, dim3 grid_default, hi
         DSPB_HIP(hipGetLastError());
         return DSP_OK;
     }
-    if (opt == (kPkOcc3 | kPkW1)) {  // 3 waves per SIMD as one-wave workgroups
-        const uint64_t tail = A.tail_end > A.F * A.H ? (A.tail_end - A.F * A.H + A.H - 1) / A.H : 0;
-        const dim3 g1((uint32_t)(A.F + tail), grid.y);
-        hipLaunchKernelGGL((stft8192_pk_kernel<kSrcRender, kKHalf, MapKind::Ramp, true, true, 4, kPkDefaultOpt | kPkW1, 3>),
-                           g1, dim3(64), 0, stream, A);
-        DSPB_HIP(hipGetLastError());
-        return DSP_OK;
-    }
     if (opt & kPkOcc3) {
         switch (opt & ~kPkOcc3) {
         case 0:
