@@ -15,7 +15,30 @@ static void launch_pk_km(int km, dim3 grid, hipStream_t s, const Stft8kArgs &A) 
 }
 
 int launch_pk_paths(const Stft8kArgs &A, bool fused, int km, bool pow2, bool winc, dim3 grid, hipStream_t stream) {
-    if (fused) {
+    if (fused && winc) {
+        // full frames, 4097 bins: the window computed by angle addition
+        // instead of 64 float2 loads per frame (the fused gain STFT: 0.807 ->
+        // 0.756 ms per stereo hour, profiles/r02_gain_winc_ab.txt)
+        switch (A.map.kind) {
+        case MapKind::Noop:
+            hipLaunchKernelGGL((stft8192_pk_kernel<kSrcRender, kKHalf, MapKind::Noop, true, true>), grid,
+                               dim3(64 * kPkWpb), 0, stream, A);
+            break;
+        case MapKind::Gain:
+            hipLaunchKernelGGL((stft8192_pk_kernel<kSrcRender, kKHalf, MapKind::Gain, true, true>), grid,
+                               dim3(64 * kPkWpb), 0, stream, A);
+            break;
+        case MapKind::Ramp:
+            if (pow2)
+                hipLaunchKernelGGL((stft8192_pk_kernel<kSrcRender, kKHalf, MapKind::Ramp, true, true>), grid,
+                                   dim3(64 * kPkWpb), 0, stream, A);
+            else
+                hipLaunchKernelGGL((stft8192_pk_kernel<kSrcRender, kKHalf, MapKind::Ramp, false, true>), grid,
+                                   dim3(64 * kPkWpb), 0, stream, A);
+            break;
+        default: return DSP_ERR_INVALID;
+        }
+    } else if (fused) {
         switch (A.map.kind) {
         case MapKind::Noop: launch_pk_km<kSrcRender, MapKind::Noop, true, false>(km, grid, stream, A); break;
         case MapKind::Gain: launch_pk_km<kSrcRender, MapKind::Gain, true, false>(km, grid, stream, A); break;
