@@ -263,7 +263,6 @@ def main():
     torch.cuda.set_device(dev)
 
     import dspbench as d
-    d.lib().dsp_fir_method(args.fir_method)
     if args.workload == "ir":
         bench_ir(args, dev, world, rank)
         if world > 1:
@@ -352,13 +351,13 @@ def main():
     elif wl == "fir1024":
         # BASELINE configs[2] / SURVEY cfg 3b: 1024 taps = compute_IR(IR_test)[0:1024]
         ir, _ = d.ir_analysis(d.Plugin.ir_test(0.9, 0.002), C_out=1, sr=float(sr), device=dev)
-        fplug = d.Plugin.fir(ir[0, :1024].cpu().numpy())
+        fplug = d.Plugin.fir(ir[0, :1024].cpu().numpy(), direct=(args.fir_method == 1))
         plug_name = "fir (1024 taps)"
         alg_desc = "C*L*(4 + 4) B (each input sample read once + each output sample written once)"
 
         def step():
             d.render_offline(next_x(), CH, B, float(sr), fplug, out=out)
-        ols = d.lib().dsp_fir_method(-1) != 1
+        ols = args.fir_method != 1
         workload = (f"FIR render, 1024 taps = compute_IR(IR_test)[0:1024], B=512, {minutes:g} min of "
                     f"48 kHz stereo per GPU (cfg 3b), {'FFT overlap-save' if ols else 'direct form'}")
         if ols:  # HBM-bound: the library times it with read + write bytes

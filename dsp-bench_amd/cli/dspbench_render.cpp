@@ -36,12 +36,19 @@
 //   run per rank, the render + STFT gathered to rank 0 over RCCL (needs --stft)
 //     --world W --rank R    W processes, this one's rank (default: WORLD_SIZE /
 //                       RANK from the environment when --comm-id is given)
-//     --comm-id FILE    rendezvous file: rank 0 writes the RCCL id, the others
-//                       wait for it (a shared local path)
+//     --comm-id FILE    rendezvous file: rank 0 writes the RCCL id and the run
+//                       id, the others wait for a file carrying their run id;
+//                       rank 0 removes it once every rank has joined
+//     --run-id STR      this launch's id (default: DSPB_RUN_ID, else
+//                       TORCHELASTIC_RUN_ID, else none: then a file older than
+//                       this process's start is taken as stale and ignored)
 //     --chunk S         pipeline chunk in samples (default 16 Mi)
 #include <hip/hip_runtime.h>
 
+#include <sys/stat.h>
 #include <unistd.h>
+
+#include <ctime>
 
 #include <chrono>
 #include <cstdio>
@@ -89,28 +96,38 @@ void usage() {
                  "       [--gain G] [--ir G,STEP] [--block B] [--bits 16|24|32|float] [--stft MAG.f32]"
                  " [--device N]\n"
                  "       [--device-channels C] [--device-rate R] [--loop NBLOCKS]\n"
-                 "       [--world W --rank R --comm-id FILE [--chunk SAMPLES]]\n");
+                 "       [--world W --rank R --comm-id FILE [--run-id STR] [--chunk SAMPLES]]\n");
 }
 
-// rank 0 writes the RCCL id to `path` (atomically: a temp file renamed),
-// the other ranks wait up to two minutes for it
-bool exchange_comm_id(const std::string &path, uint32_t rank, unsigned char *id) {
+// rank 0 writes the RCCL id and the run id to `path` (atomically: a temp
+// file renamed); the other ranks wait up to two minutes for a file carrying
+// their run id -- or, without one, a file written after they started -- so a
+// file a previous launch left behind is never read
+bool exchange_comm_id(const std::string &path, uint32_t rank, const std::string &run_id, time_t started,
+                      unsigned char *id) {
     if (rank == 0) {
         if (dsp_comm_unique_id(id)) return false;
         const std::string tmp = path + ".tmp";
         FILE *f = std::fopen(tmp.c_str(), "wb");
-        if (!f || std::fwrite(id, 1, DSP_COMM_ID_BYTES, f) != DSP_COMM_ID_BYTES) return false;
+        if (!f) return false;
+        const bool ok = std::fwrite(id, 1, DSP_COMM_ID_BYTES, f) == DSP_COMM_ID_BYTES &&
+                        std::fwrite(run_id.data(), 1, run_id.size(), f) == run_id.size();
         std::fclose(f);
-        return std::rename(tmp.c_str(), path.c_str()) == 0;
+        return ok && std::rename(tmp.c_str(), path.c_str()) == 0;
     }
-    for (int i = 0; i < 1200; ++i) {
+    std::vector<unsigned char> buf(DSP_COMM_ID_BYTES + run_id.size() + 1);
+    for (int i = 0; i < 1200; ++i, usleep(100000)) {
+        struct stat sb;
+        if (stat(path.c_str(), &sb) != 0) continue;
+        if (run_id.empty() && sb.st_mtime < started) continue;  // stale: before this launch
         FILE *f = std::fopen(path.c_str(), "rb");
-        if (f) {
-            const size_t n = std::fread(id, 1, DSP_COMM_ID_BYTES, f);
-            std::fclose(f);
-            if (n == DSP_COMM_ID_BYTES) return true;
-        }
-        usleep(100000);
+        if (!f) continue;
+        const size_t n = std::fread(buf.data(), 1, buf.size(), f);
+        std::fclose(f);
+        if (n != DSP_COMM_ID_BYTES + run_id.size()) continue;  // another launch's run id (or a partial file)
+        if (std::memcmp(buf.data() + DSP_COMM_ID_BYTES, run_id.data(), run_id.size()) != 0) continue;
+        std::memcpy(id, buf.data(), DSP_COMM_ID_BYTES);
+        return true;
     }
     return false;
 }
@@ -134,7 +151,10 @@ int main(int argc, char **argv) {
     uint32_t dev_channels = 0, dev_rate = 0, world = 0, rank = 0;
     uint64_t loop_blocks = 0, chunk = 16ull << 20;
     bool have_rank = false;
-    std::string comm_path;
+    std::string comm_path, run_id;
+    const time_t started = std::time(nullptr) - 2;  // (mtime has one-second resolution)
+    if (const char *e = std::getenv("DSPB_RUN_ID")) run_id = e;
+    else if (const char *e2 = std::getenv("TORCHELASTIC_RUN_ID")) run_id = e2;
     for (int i = 3; i < argc; i += 2) {  // every option takes one value
         const std::string a = argv[i];
         const char *v = i + 1 < argc ? argv[i + 1] : nullptr;
@@ -159,6 +179,7 @@ int main(int argc, char **argv) {
         else if (a == "--world") world = (uint32_t)std::strtoul(v, nullptr, 10);
         else if (a == "--rank") rank = (uint32_t)std::strtoul(v, nullptr, 10), have_rank = true;
         else if (a == "--comm-id") comm_path = v;
+        else if (a == "--run-id") run_id = v;
         else if (a == "--chunk") chunk = std::strtoull(v, nullptr, 10);
         else {
             usage();
@@ -284,11 +305,13 @@ int main(int argc, char **argv) {
     dsp_comm *comm = nullptr;
     if (multi) {
         unsigned char id[DSP_COMM_ID_BYTES];
-        if (!exchange_comm_id(comm_path, rank, id)) {
+        if (!exchange_comm_id(comm_path, rank, run_id, started, id)) {
             std::fprintf(stderr, "dspbench_render: rank %u: no communicator id at %s\n", rank, comm_path.c_str());
             return 1;
         }
         if ((st = dsp_comm_init(id, world, rank, device, &comm))) return fail("dsp_comm_init", st);
+        // every rank has joined (the init is collective): the id is spent
+        if (rank == 0) (void)std::remove(comm_path.c_str());
     }
     HIPCK(hipEventRecord(e0, s));
     if (multi) {

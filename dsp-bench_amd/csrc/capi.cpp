@@ -93,19 +93,35 @@ struct DeviceGuard {
     }
 };
 
+// A call on a stream that is being captured into a graph cannot make a
+// first-use table or scratch allocation (an allocation, a legacy-stream
+// launch and a sync would invalidate the capture): it is refused instead, and
+// one eager call of the same shape beforehand creates what it needs.
+static int refuse_capture(hipStream_t s, const char *what) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) {
+        set_last_error("stream capture: %s is created on first use; make one eager call of this shape on the "
+                       "capturing stream first", what);
+        return DSP_ERR_INVALID;
+    }
+    return DSP_OK;
+}
+
 // Synchronous upload of a constant table (launch_upload: kernel arguments,
 // not a copy -- see render.hip); the tables are shared by every stream of the
-// device, so the upload completes before the first use.
+// device, so the upload completes before the first use.  (Callers check the
+// caller's stream for capture first: refuse_capture.)
 static int upload_table(void *dst, const void *src, size_t bytes) {
     if (int st = launch_upload((float *)dst, (const float *)src, bytes / sizeof(float), nullptr)) return st;
     DSPB_HIP(hipStreamSynchronize(nullptr));
     return DSP_OK;
 }
 
-static int get_tw(int dev, const v2f **out) {
+static int get_tw(int dev, hipStream_t s, const v2f **out) {
     std::lock_guard<std::mutex> lk(g_mu);
     DeviceRes &r = g_res[dev];
     if (!r.tw8192) {
+        if (int st = refuse_capture(s, "the FFT twiddle table")) return st;
         std::vector<v2f> h(8192);
         for (int k = 0; k < 8192; ++k) {
             const double a = -2.0 * M_PI * (double)k / 8192.0;
@@ -143,10 +159,11 @@ static int get_tw(int dev, const v2f **out) {
 // compute_IR's impulse (plugin.cpp:27-34) as a read-only device buffer: the
 // IR render of a map plugin reads it as its file, so no impulse launch
 constexpr uint32_t kDeltaLen = 2048;  // the largest ir_len (4 ir_len <= 8192)
-static int get_delta(int dev, const float **out) {
+static int get_delta(int dev, hipStream_t s, const float **out) {
     std::lock_guard<std::mutex> lk(g_mu);
     DeviceRes &r = g_res[dev];
     if (!r.delta) {
+        if (int st = refuse_capture(s, "the impulse buffer")) return st;
         std::vector<float> h(kDeltaLen, 0.0f);
         h[0] = 1.0f;
         float *d = nullptr;
@@ -163,13 +180,14 @@ static int get_delta(int dev, const float **out) {
 
 // Window of length `valid` (symmetric, ref ippsWinHamming_32f convention)
 // zero-padded to N.  Computed in double, rounded once to float.
-static int get_window(int dev, int kind, uint32_t N, uint32_t valid, const float **out,
+static int get_window(int dev, hipStream_t s, int kind, uint32_t N, uint32_t valid, const float **out,
                       double scale = 1.0) {
     std::lock_guard<std::mutex> lk(g_mu);
     DeviceRes &r = g_res[dev];
     auto key = std::make_tuple(kind, N, valid, (float)scale);
     auto it = r.windows.find(key);
     if (it != r.windows.end()) { *out = it->second; return DSP_OK; }
+    if (int st = refuse_capture(s, "a window table")) return st;
     double a = 0.54, b = 0.46;
     if (kind == DSP_WIN_HANN) { a = 0.5; b = 0.5; }
     else if (kind == DSP_WIN_RECT) { a = 1.0; b = 0.0; }
@@ -179,7 +197,10 @@ static int get_window(int dev, int kind, uint32_t N, uint32_t valid, const float
                           : (float)(scale * (a - b * std::cos(2.0 * M_PI * (double)n / (double)(valid - 1))));
     float *d = nullptr;
     DSPB_HIP(hipMalloc(&d, sizeof(float) * N));
-    if (int st = upload_table(d, h.data(), sizeof(float) * N)) return st;
+    if (int st = upload_table(d, h.data(), sizeof(float) * N)) {
+        (void)hipFree(d);
+        return st;
+    }
     r.windows[key] = d;
     *out = d;
     return DSP_OK;
@@ -191,11 +212,12 @@ static float window_prescale(uint32_t N) { return (float)(0.5 / std::sqrt((doubl
 
 // Inputs of the computed-window kernels (stft_soa.hip kOptWinComp): per-lane
 // base angles and the (pre-scaled) cosine-window coefficients.
-static int set_wincomp(int dev, int kind, Stft8kArgs *A) {
+static int set_wincomp(int dev, hipStream_t s, int kind, Stft8kArgs *A) {
     {
         std::lock_guard<std::mutex> lk(g_mu);
         DeviceRes &r = g_res[dev];
         if (!r.wbase) {
+            if (int st = refuse_capture(s, "the window base angles")) return st;
             std::vector<float4> h(64);
             const double th = 2.0 * M_PI / 8191.0;
             for (int l = 0; l < 64; ++l)
@@ -230,12 +252,7 @@ static int get_scratch(int dev, hipStream_t s, size_t bytes, float **out, int sl
     if (slot.second < bytes) {
         // a stream being captured into a graph cannot allocate or wait: its
         // scratch must exist from an eager call of the same shape first
-        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-        if (hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) {
-            set_last_error("stream capture: make one eager call of this shape on the capturing stream first "
-                           "(its scratch buffer is allocated then)");
-            return DSP_ERR_INVALID;
-        }
+        if (int st = refuse_capture(s, "the stream's scratch buffer")) return st;
         if (slot.first) {
             DSPB_HIP(hipStreamSynchronize(s));
             DSPB_HIP(hipFree(slot.first));
@@ -374,8 +391,6 @@ static void ols_table(const float *taps, uint32_t T, float *out) {
     out[8193] = (float)(im[2048] * sc);
 }
 
-static int g_fir_method = 0;  // 0 auto (overlap-save when T <= 1025), 1 direct, 2 overlap-save
-
 // IR_test (build/IR_test.cpp:47-58) runs `gain -= step` in double from the
 // float parameters.  The sequence is often exact -- every partial result a
 // double -- and then table[i] = (float)(gain - i step) is one f64 FMA, with
@@ -403,8 +418,9 @@ static bool ramp_closed_form(float gain, float step, uint32_t B) {
 }
 
 static int plugin_map(const dsp_plugin *p, uint32_t B, int dev, hipStream_t s, SampleMap *m,
-                      float sr = 48000.f) {
+                      float sr = 48000.f, uint32_t flags = 0) {
     m->kind = MapKind::Noop;
+    m->fir_direct = (flags & DSP_EXEC_FIR_DIRECT) ? 1u : 0u;
     m->a = 1.f;
     m->table = nullptr;
     m->B = B;
@@ -467,12 +483,16 @@ static int plugin_map(const dsp_plugin *p, uint32_t B, int dev, hipStream_t s, S
             for (auto &e : r.fir)
                 if (e.taps == key) { ft = &e; break; }
             if (!ft) {
+                if (int st = refuse_capture(s, "a FIR filter's device taps")) return st;
                 std::vector<float> h(T8 + 8192 + 2, 0.f);
                 std::memcpy(h.data(), key.data(), 4 * (size_t)T);
                 if (T <= 1025) ols_table(h.data(), T, h.data() + T8);
                 float *d = nullptr;
                 DSPB_HIP(hipMalloc(&d, sizeof(float) * h.size()));
-                if (int st = upload_table(d, h.data(), sizeof(float) * h.size())) return st;
+                if (int st = upload_table(d, h.data(), sizeof(float) * h.size())) {
+                    (void)hipFree(d);
+                    return st;
+                }
                 if (r.fir.size() >= 8) {  // small LRU-ish cap
                     (void)hipFree(r.fir.front().dev);
                     r.fir.erase(r.fir.begin());
@@ -546,11 +566,11 @@ static int render_device(const float *const *in, uint32_t in_ch, uint64_t L, flo
     }
     if (map.kind == MapKind::Fir) {  // convolution from the start of the file
         if (start != 0 || goff != 0) return invalid("FIR render: whole files only (sample_offset 0)");
-        if (map.ntaps <= 1025 && g_fir_method != 1) {  // overlap-save, 8192-point frames
+        if (map.ntaps <= 1025 && !map.fir_direct) {  // overlap-save, 8192-point frames
             const v2f *tw = nullptr;
             int dev = 0;
             DSPB_HIP(hipGetDevice(&dev));
-            int st = get_tw(dev, &tw);
+            int st = get_tw(dev, s, &tw);
             if (st) return st;
             for (uint32_t c0 = 0; c0 < C; c0 += kMaxChannels) {
                 const uint32_t cn = (C - c0) < (uint32_t)kMaxChannels ? (C - c0) : kMaxChannels;
@@ -621,11 +641,11 @@ static int stft_device(const float *const *in, uint32_t C, uint64_t L, uint32_t 
     if (F == 0) return DSP_OK;
     const v2f *tw = nullptr;
     const float *win = nullptr;
-    int st = get_tw(dev, &tw);
+    int st = get_tw(dev, s, &tw);
     if (st) return st;
     bool fast = (N == 8192) && (H % 2 == 0);
     for (uint32_t c = 0; c < C; ++c) fast = fast && aligned(in[c], 8);
-    st = get_window(dev, window, N, N, &win, fast ? window_prescale(N) : 1.0);
+    st = get_window(dev, s, window, N, N, &win, fast ? window_prescale(N) : 1.0);
     if (st) return st;
     for (uint32_t c0 = 0; c0 < C; c0 += kMaxChannels) {
         const uint32_t cn = (C - c0) < (uint32_t)kMaxChannels ? (C - c0) : kMaxChannels;
@@ -645,7 +665,7 @@ static int stft_device(const float *const *in, uint32_t C, uint64_t L, uint32_t 
             A.win2 = reinterpret_cast<const v2f *>(win);
             A.tw = tw;
             A.scale = (float)(1.0 / std::sqrt((double)N));
-            if ((st = set_wincomp(dev, window, &A))) return st;
+            if ((st = set_wincomp(dev, s, window, &A))) return st;
             TimedLaunch tl{};
             if ((st = timing_begin(s, &tl))) return st;
             st = launch_stft(A, cn, false, s);
@@ -703,11 +723,6 @@ extern "C" {
 
 int dsp_abi_version(void) { return DSPBENCH_ABI_VERSION; }
 
-int dsp_fir_method(int m) {
-    const int old = g_fir_method;
-    if (m >= 0 && m <= 2) g_fir_method = m;
-    return old;
-}
 
 #ifdef DSPB_AB_BUILD
 int dsp_stft_pk_ab_options(int opt) {
@@ -825,7 +840,7 @@ int dsp_render_offline(const float *const *in, uint32_t in_channels, uint64_t L,
         for (uint32_t c = 0; c < C; ++c) dout[c] = out[c];
     }
     SampleMap map;
-    int st = plugin_map(plugin, B, g.dev, s, &map, sr);
+    int st = plugin_map(plugin, B, g.dev, s, &map, sr, ex ? ex->flags : 0);
     if (st) return st;
     TimedLaunch tl{};
     if ((st = timing_begin(s, &tl))) return st;
@@ -864,7 +879,7 @@ int dsp_render_loop(const float *const *in, uint32_t in_channels, uint64_t L, ui
     hipStream_t s = stream_of(ex);
     const uint64_t Lr = nblocks * B;
     SampleMap map;
-    int st = plugin_map(plugin, B, g.dev, s, &map, sr);
+    int st = plugin_map(plugin, B, g.dev, s, &map, sr, ex ? ex->flags : 0);
     if (st) return st;
     if ((st = ensure_ramp_table(map, s))) return st;
     const uint32_t in_ch = std::min(in_channels, C);  // channels_to_write (audio.cpp:66)
@@ -986,7 +1001,7 @@ int dsp_render_stft(const float *const *in, uint32_t in_channels, uint64_t L,
         for (uint32_t c = 0; c < C; ++c) { dout[c] = out[c]; dmag[c] = mag[c]; }
     }
     SampleMap map;
-    if ((st = plugin_map(plugin, B, g.dev, s, &map, sr))) return st;
+    if ((st = plugin_map(plugin, B, g.dev, s, &map, sr, ex ? ex->flags : 0))) return st;
     const uint64_t goff = goff_of(ex);
 
     bool fused = (N == 8192) && (H % 128 == 0) && (H <= N) && (goff % 2 == 0) && F > 0 &&
@@ -1015,8 +1030,8 @@ int dsp_render_stft(const float *const *in, uint32_t in_channels, uint64_t L,
     } else {
         const v2f *tw = nullptr;
         const float *win = nullptr;
-        if ((st = get_tw(g.dev, &tw))) return st;
-        if ((st = get_window(g.dev, window, N, N, &win, window_prescale(N)))) return st;
+        if ((st = get_tw(g.dev, s, &tw))) return st;
+        if ((st = get_window(g.dev, s, window, N, N, &win, window_prescale(N)))) return st;
         bool tail_in_kernel = false;
         for (uint32_t c0 = 0; c0 < C; c0 += kMaxChannels) {
             const uint32_t cn = (C - c0) < (uint32_t)kMaxChannels ? (C - c0) : kMaxChannels;
@@ -1039,7 +1054,7 @@ int dsp_render_stft(const float *const *in, uint32_t in_channels, uint64_t L,
             A.win2 = reinterpret_cast<const v2f *>(win);
             A.tw = tw;
             A.scale = (float)(1.0 / std::sqrt((double)N));
-            if ((st = set_wincomp(g.dev, window, &A))) return st;
+            if ((st = set_wincomp(g.dev, s, window, &A))) return st;
             A.map = map;
             A.goff = goff;
             // the PER kernel also renders the tail no frame owns
@@ -1098,7 +1113,7 @@ int dsp_ir_analysis(const dsp_plugin *plugin, uint32_t C, float sr, uint32_t ir_
     }
     // compute_IR (plugin.cpp:27-34): IR[c] = delta, then one callback of ir_len
     SampleMap map;
-    if ((st = plugin_map(plugin, ir_len, g.dev, s, &map, sr))) return st;
+    if ((st = plugin_map(plugin, ir_len, g.dev, s, &map, sr, ex ? ex->flags : 0))) return st;
     if (map.kind == MapKind::Generic) {  // the impulse in place, a fresh scratch State, one callback
         for (uint32_t c0 = 0; c0 < C; c0 += kMaxChannels) {
             const uint32_t cn = (C - c0) < (uint32_t)kMaxChannels ? (C - c0) : kMaxChannels;
@@ -1110,7 +1125,7 @@ int dsp_ir_analysis(const dsp_plugin *plugin, uint32_t C, float sr, uint32_t ir_
             return st;
     } else {  // map plugins: render the read-only impulse into IR[c], one launch
         const float *delta;
-        if ((st = get_delta(g.dev, &delta))) return st;
+        if ((st = get_delta(g.dev, s, &delta))) return st;
         std::vector<const float *> cin(C, delta);
         if ((st = render_device(cin.data(), C, ir_len, dir.data(), C, ir_len, map, 0, 0, s))) return st;
     }
@@ -1118,9 +1133,9 @@ int dsp_ir_analysis(const dsp_plugin *plugin, uint32_t C, float sr, uint32_t ir_
     // fft_perform_and_get_magnitude (dsp.cpp:53-66): channel 0 only
     const v2f *tw = nullptr;
     const float *win = nullptr;
-    if ((st = get_tw(g.dev, &tw))) return st;
+    if ((st = get_tw(g.dev, s, &tw))) return st;
     const bool fast_ir = n == 8192 && aligned(dir[0], 8);
-    if ((st = get_window(g.dev, DSP_WIN_HAMMING, n, ir_len, &win, fast_ir ? window_prescale(n) : 1.0)))
+    if ((st = get_window(g.dev, s, DSP_WIN_HAMMING, n, ir_len, &win, fast_ir ? window_prescale(n) : 1.0)))
         return st;
     if (fast_ir) {
         Stft8kArgs A{};
@@ -1169,7 +1184,7 @@ static int fft_service(const float *re_in, const float *im_in, float *re_out, fl
     if (g.status) return g.status;
     hipStream_t s = stream_of(ex);
     const v2f *tw = nullptr;
-    int st = get_tw(g.dev, &tw);
+    int st = get_tw(g.dev, s, &tw);
     if (st) return st;
     Staged stage;
     const float *dre = re_in, *dim = im_in;

@@ -32,6 +32,7 @@ struct SampleMap {
     const float *taps;   // FIR taps, zero-padded to ntaps8 = ceil(T/16)*16 (Fir; not a per-sample map)
     uint32_t ntaps8;
     uint32_t ntaps;      // Fir: real tap count (<= 1025 runs overlap-save)
+    uint32_t fir_direct; // Fir: the caller asked for the direct form (DSP_EXEC_FIR_DIRECT)
     const float *olsH;   // Fir: FFT(taps)/16384 in fir_fft.hip's lane-major pair layout
     float olsH2048[2];   // Fir: H[2048]/16384
     void *module;        // Generic: the dsp_module running the plugin's own audio_callback

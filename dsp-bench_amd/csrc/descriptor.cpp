@@ -637,8 +637,10 @@ bool elf_symbol(const unsigned char *img, size_t size, const char *want, std::st
             Elf64Sym sym;
             std::memcpy(&sym, img + s.offset + k * sizeof(Elf64Sym), sizeof sym);
             if (sym.name >= strs.size || sym.shndx == 0 || sym.shndx >= sh.size()) continue;
+            // the name and its terminator must both lie inside the string table
             const char *nm = (const char *)img + strs.offset + sym.name;
-            if (std::strncmp(nm, want, strs.size - sym.name) != 0) continue;
+            const size_t wl = std::strlen(want);
+            if (strs.size - sym.name < wl + 1 || std::memcmp(nm, want, wl) != 0 || nm[wl] != 0) continue;
             const Elf64Shdr &sec = sh[sym.shndx];
             if (sec.type == 8) return false;  // NOBITS: no initialiser in the file
             if (sym.value < sec.addr || sym.value - sec.addr > sec.size || sym.size > sec.size - (sym.value - sec.addr))

@@ -1014,6 +1014,19 @@ static int upload_params(dsp_module *m, const void *params, uint32_t n, hipStrea
     return DSP_OK;
 }
 
+// A GENERIC render cannot be captured into a graph: its Parameters upload
+// waits on the host for the pinned staging buffer and copies from it, so a
+// replay would upload whatever a later call left there.  Refused instead.
+static int refuse_capture(hipStream_t s) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) {
+        set_last_error("GENERIC plugin: calls cannot be captured into a graph (the Parameters upload is "
+                       "host-staged); call it eagerly");
+        return DSP_ERR_INVALID;
+    }
+    return DSP_OK;
+}
+
 // the module's code object, Parameters and State live on m->device: a call
 // made on another device (e.g. a mis-wired shard rank) is refused
 static int check_device(const dsp_module *m) {
@@ -1035,6 +1048,7 @@ int module_render(dsp_module *m, const void *params, uint32_t params_size, const
         return DSP_ERR_INVALID;
     }
     if (int st = check_device(m)) return st;
+    if (int st = refuse_capture(s)) return st;
     if (params_size != m->params_size || (!params && params_size)) {
         set_last_error("GENERIC plugin: params blob is %u bytes, the plugin's Parameters %u", params_size,
                        m->params_size);
@@ -1137,6 +1151,7 @@ int module_ir(dsp_module *m, const void *params, uint32_t params_size, float *co
         return DSP_ERR_INVALID;
     }
     if (int st = check_device(m)) return st;
+    if (int st = refuse_capture(s)) return st;
     if (params_size != m->params_size || (!params && params_size)) {
         set_last_error("GENERIC plugin: params blob is %u bytes, the plugin's Parameters %u", params_size,
                        m->params_size);

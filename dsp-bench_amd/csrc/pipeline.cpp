@@ -236,6 +236,7 @@ int run(const Source &src, uint32_t C, uint32_t B, float sr, const dsp_plugin *p
         PL_HIP(hipStreamWaitEvent(cs, s.up_done, 0));
         dsp_exec e{};
         e.device = -1;
+        e.flags = ex ? (ex->flags & DSP_EXEC_FIR_DIRECT) : 0;
         e.stream = cs;
         e.sample_offset = goff + c.start;
         std::vector<const float *> rin(Cin);

@@ -1,8 +1,9 @@
 // shard.cpp -- multi-GPU sharding of the render + STFT path (shard.h,
-// SURVEY 8(e)): the shard / chunk planners, an RCCL communicator, the gather
-// and the pipelined per-rank driver.
+// SURVEY 8(e)): the shard / chunk planners, the gather schedule, the
+// communicators (a transport table: RCCL, an in-process loopback, or the
+// caller's) and the pipelined per-rank driver.
 //
-// RCCL is loaded on first use (dlopen "librccl.so.1", the NCCL API of
+// RCCL is loaded on first use (dlopen "librccl.so.1"; the types come from
 // /opt/rocm/include/rccl/rccl.h), so the library, its planners and its CPU
 // tests do not depend on it.  When torch has already loaded its own copy the
 // same object is reused (dlopen by soname).
@@ -13,10 +14,16 @@
 #include <cstdarg>
 #include <cstdio>
 #include <algorithm>
+#include <chrono>
+#include <condition_variable>
 #include <cstring>
+#include <deque>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
+
+#include <rccl/rccl.h>
 
 #include "dspbench/shard.h"
 
@@ -72,24 +79,20 @@ void time_range(uint64_t L, uint64_t lo, uint64_t hi, uint32_t B, uint32_t N, ui
 }
 
 // ---- RCCL, loaded on first use -------------------------------------------
-typedef int ncclResult_t;
-typedef void *ncclComm_t;
-struct ncclUniqueId {
-    char internal[DSP_COMM_ID_BYTES];
-};
-constexpr int kNcclFloat32 = 7;
+// (types from rccl.h; the entry points resolved by dlsym)
+static_assert(NCCL_UNIQUE_ID_BYTES == DSP_COMM_ID_BYTES, "communicator id size");
 
 struct Rccl {
     bool ok = false;
     std::string err;
-    ncclResult_t (*GetUniqueId)(ncclUniqueId *);
-    ncclResult_t (*CommInitRank)(ncclComm_t *, int, ncclUniqueId, int);
-    ncclResult_t (*CommDestroy)(ncclComm_t);
-    ncclResult_t (*Send)(const void *, size_t, int, int, ncclComm_t, hipStream_t);
-    ncclResult_t (*Recv)(void *, size_t, int, int, ncclComm_t, hipStream_t);
-    ncclResult_t (*GroupStart)();
-    ncclResult_t (*GroupEnd)();
-    const char *(*GetErrorString)(ncclResult_t);
+    decltype(&ncclGetUniqueId) GetUniqueId;
+    decltype(&ncclCommInitRank) CommInitRank;
+    decltype(&ncclCommDestroy) CommDestroy;
+    decltype(&ncclSend) Send;
+    decltype(&ncclRecv) Recv;
+    decltype(&ncclGroupStart) GroupStart;
+    decltype(&ncclGroupEnd) GroupEnd;
+    decltype(&ncclGetErrorString) GetErrorString;
 };
 
 Rccl &rccl() {
@@ -123,24 +126,223 @@ Rccl &rccl() {
 }
 
 int nccl_fail(ncclResult_t e, const char *what) {
-    set_last_error("%s: RCCL error %d (%s)", what, e, rccl().GetErrorString ? rccl().GetErrorString(e) : "?");
+    set_last_error("%s: RCCL error %d (%s)", what, (int)e, rccl().GetErrorString ? rccl().GetErrorString(e) : "?");
     return DSP_ERR_HIP;
 }
 
 #define NCCL_CK(x)                                   \
     do {                                             \
         ncclResult_t e_ = (x);                       \
-        if (e_ != 0) return nccl_fail(e_, #x);       \
+        if (e_ != ncclSuccess) return nccl_fail(e_, #x); \
     } while (0)
+
+// the RCCL transport: user = the ncclComm_t
+int rccl_group_start(void *) {
+    NCCL_CK(rccl().GroupStart());
+    return DSP_OK;
+}
+int rccl_group_end(void *) {
+    NCCL_CK(rccl().GroupEnd());
+    return DSP_OK;
+}
+int rccl_send(void *u, const float *buf, uint64_t count, uint32_t peer, void *stream) {
+    NCCL_CK(rccl().Send(buf, count, ncclFloat32, (int)peer, (ncclComm_t)u, (hipStream_t)stream));
+    return DSP_OK;
+}
+int rccl_recv(void *u, float *buf, uint64_t count, uint32_t peer, void *stream) {
+    NCCL_CK(rccl().Recv(buf, count, ncclFloat32, (int)peer, (ncclComm_t)u, (hipStream_t)stream));
+    return DSP_OK;
+}
+void rccl_destroy(void *u) {
+    if (u) (void)rccl().CommDestroy((ncclComm_t)u);
+}
+const dsp_comm_transport kRcclTransport = {rccl_group_start, rccl_group_end, rccl_send, rccl_recv, rccl_destroy};
+
+// ---- the in-process loopback transport -------------------------------------
+// Ranks are host threads of one process on one device.  A send posts
+// (pointer, count, an event recorded on the sender's stream) to the
+// (src, dst) mailbox; the matching recv makes its stream wait for that event,
+// copies device to device, records `done` and hands it back; the sender's
+// stream waits for `done`.  Inside a group, recvs and the sends' completion
+// are deferred to group_end (sends post at once), so a group never blocks on
+// its peers' issue order.
+constexpr int kLoopWaitSeconds = 120;
+
+struct LoopMsg {
+    const float *ptr = nullptr;
+    uint64_t count = 0;
+    hipEvent_t ready = nullptr, done = nullptr;
+    bool taken = false;   // a recv has it
+    bool copied = false;  // the copy and `done` are enqueued (or failed)
+    int status = DSP_OK;
+};
+
+struct LoopHub {
+    std::mutex mu;
+    std::condition_variable cv;
+    uint32_t world = 0;
+    std::vector<std::deque<std::shared_ptr<LoopMsg>>> box;  // [src * world + dst]
+};
+
+struct LoopRank {
+    std::shared_ptr<LoopHub> hub;
+    uint32_t rank = 0;
+    int depth = 0;
+    struct Sent {
+        std::shared_ptr<LoopMsg> m;
+        hipStream_t s;
+    };
+    struct Recv {
+        float *buf;
+        uint64_t count;
+        uint32_t peer;
+        hipStream_t s;
+    };
+    std::vector<Sent> sent;
+    std::vector<Recv> recvs;
+};
+
+int loop_flush(LoopRank *lr);
+
+int loop_group_start(void *u) {
+    ++((LoopRank *)u)->depth;
+    return DSP_OK;
+}
+
+int loop_group_end(void *u) {
+    LoopRank *lr = (LoopRank *)u;
+    if (lr->depth <= 0) return invalid("loopback: group_end without group_start");
+    return --lr->depth == 0 ? loop_flush(lr) : DSP_OK;
+}
+
+int loop_send(void *u, const float *buf, uint64_t count, uint32_t peer, void *stream) {
+    LoopRank *lr = (LoopRank *)u;
+    LoopHub &h = *lr->hub;
+    if (peer >= h.world || peer == lr->rank) return invalid("loopback: bad peer %u (rank %u)", peer, lr->rank);
+    auto m = std::make_shared<LoopMsg>();
+    m->ptr = buf;
+    m->count = count;
+    SH_HIP(hipEventCreateWithFlags(&m->ready, hipEventDisableTiming));
+    SH_HIP(hipEventCreateWithFlags(&m->done, hipEventDisableTiming));
+    SH_HIP(hipEventRecord(m->ready, (hipStream_t)stream));
+    {
+        std::lock_guard<std::mutex> g(h.mu);
+        h.box[(size_t)lr->rank * h.world + peer].push_back(m);
+    }
+    h.cv.notify_all();
+    lr->sent.push_back({m, (hipStream_t)stream});
+    return lr->depth ? DSP_OK : loop_flush(lr);
+}
+
+int loop_recv(void *u, float *buf, uint64_t count, uint32_t peer, void *stream) {
+    LoopRank *lr = (LoopRank *)u;
+    if (peer >= lr->hub->world || peer == lr->rank) return invalid("loopback: bad peer %u (rank %u)", peer, lr->rank);
+    lr->recvs.push_back({buf, count, peer, (hipStream_t)stream});
+    return lr->depth ? DSP_OK : loop_flush(lr);
+}
+
+int loop_flush(LoopRank *lr) {
+    LoopHub &h = *lr->hub;
+    const auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(kLoopWaitSeconds);
+    int st = DSP_OK;
+    std::vector<LoopRank::Recv> recvs;
+    recvs.swap(lr->recvs);
+    for (const LoopRank::Recv &r : recvs) {
+        std::shared_ptr<LoopMsg> m;
+        {
+            std::unique_lock<std::mutex> g(h.mu);
+            auto &q = h.box[(size_t)r.peer * h.world + lr->rank];
+            if (!h.cv.wait_until(g, deadline, [&] { return !q.empty(); }))
+                return invalid("loopback: rank %u waited %d s for a send from rank %u", lr->rank, kLoopWaitSeconds,
+                               r.peer);
+            m = q.front();
+            q.pop_front();
+            m->taken = true;
+        }
+        int ms = DSP_OK;
+        if (m->count != r.count)
+            ms = invalid("loopback: rank %u receives %llu floats, rank %u sent %llu", lr->rank,
+                         (unsigned long long)r.count, r.peer, (unsigned long long)m->count);
+        hipError_t e = hipSuccess;
+        if (ms == DSP_OK) e = hipStreamWaitEvent(r.s, m->ready, 0);
+        if (ms == DSP_OK && e == hipSuccess && r.count)
+            e = hipMemcpyAsync(r.buf, m->ptr, r.count * sizeof(float), hipMemcpyDeviceToDevice, r.s);
+        if (ms == DSP_OK && e == hipSuccess) e = hipEventRecord(m->done, r.s);
+        if (ms == DSP_OK && e != hipSuccess) ms = dspb::hip_fail(e, "loopback copy");
+        {
+            std::lock_guard<std::mutex> g(h.mu);
+            m->status = ms;
+            m->copied = true;
+        }
+        h.cv.notify_all();
+        if (ms && !st) st = ms;
+    }
+    std::vector<LoopRank::Sent> sent;
+    sent.swap(lr->sent);
+    for (const LoopRank::Sent &s : sent) {
+        {
+            std::unique_lock<std::mutex> g(h.mu);
+            if (!h.cv.wait_until(g, deadline, [&] { return s.m->copied; })) {
+                if (!st) st = invalid("loopback: rank %u waited %d s for its send to be received", lr->rank,
+                                      kLoopWaitSeconds);
+                continue;  // the message stays in the mailbox; its events leak with it
+            }
+        }
+        if (s.m->status == DSP_OK) {
+            const hipError_t e = hipStreamWaitEvent(s.s, s.m->done, 0);
+            if (e != hipSuccess && !st) st = dspb::hip_fail(e, "loopback: wait for the copy");
+        } else if (!st) {
+            st = s.m->status;
+        }
+        // a recorded event may be destroyed while pending: the waits above
+        // hold what they need
+        (void)hipEventDestroy(s.m->ready);
+        (void)hipEventDestroy(s.m->done);
+    }
+    return st;
+}
+
+void loop_destroy(void *u) { delete (LoopRank *)u; }
+
+const dsp_comm_transport kLoopTransport = {loop_group_start, loop_group_end, loop_send, loop_recv, loop_destroy};
 
 }  // namespace
 
 struct dsp_comm {
-    ncclComm_t comm = nullptr;
+    dsp_comm_transport t{};
+    void *user = nullptr;
     uint32_t world = 0, rank = 0;
     int device = -1;
     hipStream_t stream = nullptr;  // the pipeline's gather stream
 };
+
+namespace {
+
+// a communicator on `device` with its gather stream; takes `user` (released
+// through t.destroy when this fails)
+int make_comm(const dsp_comm_transport &t, void *user, uint32_t world, uint32_t rank, int32_t device,
+              dsp_comm **out) {
+    int prev = -1;
+    hipError_t e = hipGetDevice(&prev);
+    if (e == hipSuccess && device >= 0 && device != prev) e = hipSetDevice(device);
+    dsp_comm *c = new dsp_comm();
+    c->t = t;
+    c->user = user;
+    c->world = world;
+    c->rank = rank;
+    if (e == hipSuccess) e = hipGetDevice(&c->device);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (prev >= 0 && prev != c->device) (void)hipSetDevice(prev);
+    if (e != hipSuccess) {
+        if (t.destroy) t.destroy(user);
+        delete c;
+        return dspb::hip_fail(e, "dsp_comm: device / stream");
+    }
+    *out = c;
+    return DSP_OK;
+}
+
+}  // namespace
 
 extern "C" {
 
@@ -189,6 +391,105 @@ int64_t dsp_shard_chunks(const dsp_shard *s, uint64_t L, uint32_t B, uint32_t N,
     return n;
 }
 
+}  // extern "C"
+
+namespace {
+
+// every rank's plan and chunks, and the pieces of the gather in schedule order
+struct GatherPlan {
+    std::vector<dsp_shard> plans;
+    std::vector<std::vector<dsp_shard>> chunks;
+    std::vector<dsp_gather_piece> pieces;
+    uint64_t steps = 0;
+};
+
+int gather_plan(uint64_t L, uint32_t C, uint32_t world, uint32_t B, uint32_t N, uint32_t H, uint32_t mode,
+                uint64_t chunk, uint64_t ld, GatherPlan *g) {
+    if (world == 0) return invalid("gather plan: world 0");
+    g->plans.assign(world, dsp_shard{});
+    g->chunks.assign(world, {});
+    g->pieces.clear();
+    g->steps = 0;
+    for (uint32_t r = 0; r < world; ++r) {
+        int st = dsp_shard_plan(L, C, world, r, B, N, H, mode, 1, &g->plans[r]);
+        if (st) return st;
+        const int64_t n = dsp_shard_chunks(&g->plans[r], L, B, N, H, 1, chunk, nullptr, 0);
+        if (n < 0) return (int)n;
+        g->chunks[r].resize((size_t)n);
+        dsp_shard_chunks(&g->plans[r], L, B, N, H, 1, chunk, g->chunks[r].data(), g->chunks[r].size());
+        g->steps = std::max<uint64_t>(g->steps, (uint64_t)n);
+    }
+    const uint64_t Lpad = (L + B - 1) / B * B;
+    for (uint64_t t = 0; t < g->steps; ++t)
+        for (uint32_t r = 0; r < world; ++r) {
+            const dsp_shard &p = g->plans[r];
+            if (t >= g->chunks[r].size()) continue;
+            const dsp_shard &c = g->chunks[r][t];
+            // the render samples a chunk contributes: its owned samples, and
+            // the block padding past EOF for the chunk that reaches it
+            const uint64_t rlen = (c.start + c.owned >= L) ? Lpad - c.start : c.owned;
+            for (uint32_t j = 0; j < p.channels; ++j) {
+                const uint32_t gc = p.chan0 + j;
+                if (rlen) g->pieces.push_back({(uint32_t)t, r, gc, DSP_PIECE_RENDER, c.start - p.start, c.start, rlen});
+                if (c.frames)
+                    g->pieces.push_back({(uint32_t)t, r, gc, DSP_PIECE_MAG, (c.frame0 - p.frame0) * ld, c.frame0 * ld,
+                                         c.frames * ld});
+            }
+        }
+    return DSP_OK;
+}
+
+// one gather step through the communicator's transport: rank src's pieces
+// into the root's rows (the root's own pieces are device copies)
+struct Move {
+    uint32_t src;
+    const float *send;  // on src
+    float *dst;         // on the root
+    uint64_t count;
+};
+
+int run_moves(dsp_comm *c, uint32_t root, const std::vector<Move> &moves, hipStream_t s) {
+    bool any_p2p = false;
+    for (const Move &m : moves) any_p2p = any_p2p || (m.src != root && m.count && (c->rank == root || c->rank == m.src));
+    int st = DSP_OK;
+    if (any_p2p && (st = c->t.group_start(c->user))) return st;
+    for (const Move &m : moves) {
+        if (!m.count || st) continue;
+        if (m.src == root) {
+            if (c->rank == root && m.dst != m.send) {
+                const hipError_t e = hipMemcpyAsync(m.dst, m.send, m.count * sizeof(float), hipMemcpyDeviceToDevice, s);
+                if (e != hipSuccess) st = dspb::hip_fail(e, "gather: root copy");
+            }
+        } else if (c->rank == root) {
+            st = c->t.recv(c->user, m.dst, m.count, m.src, s);
+        } else if (c->rank == m.src) {
+            st = c->t.send(c->user, m.send, m.count, root, s);
+        }
+    }
+    if (any_p2p) {  // close the group even after a failed call
+        const int ge = c->t.group_end(c->user);
+        if (!st) st = ge;
+    }
+    return st;
+}
+
+}  // namespace
+
+extern "C" {
+
+int64_t dsp_shard_gather_plan(uint64_t L, uint32_t C, uint32_t world, uint32_t B, uint32_t N, uint32_t H,
+                              uint32_t mode, uint64_t chunk, uint64_t ld, dsp_gather_piece *out, uint64_t cap,
+                              uint64_t *steps) {
+    if (B == 0 || H == 0 || N < H) return invalid("dsp_shard_gather_plan: bad B / N / H");
+    GatherPlan g;
+    int st = gather_plan(L, C, world, B, N, H, mode, chunk, ld, &g);
+    if (st) return st;
+    if (out)
+        for (size_t i = 0; i < g.pieces.size() && i < cap; ++i) out[i] = g.pieces[i];
+    if (steps) *steps = g.steps;
+    return (int64_t)g.pieces.size();
+}
+
 int dsp_comm_unique_id(void *id) {
     if (!id) return invalid("dsp_comm_unique_id: NULL");
     Rccl &r = rccl();
@@ -207,83 +508,71 @@ int dsp_comm_init(const void *id, uint32_t world, uint32_t rank, int32_t device,
     int prev = -1;
     SH_HIP(hipGetDevice(&prev));
     if (device >= 0 && device != prev) SH_HIP(hipSetDevice(device));
-    dsp_comm *c = new dsp_comm();
-    (void)hipGetDevice(&c->device);
-    c->world = world;
-    c->rank = rank;
     ncclUniqueId u;
     std::memcpy(u.internal, id, DSP_COMM_ID_BYTES);
-    ncclResult_t e = r.CommInitRank(&c->comm, (int)world, u, (int)rank);
-    hipError_t he = e == 0 ? hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) : hipSuccess;
-    if (prev >= 0 && prev != c->device) (void)hipSetDevice(prev);
-    if (e != 0) {
-        delete c;
-        return nccl_fail(e, "ncclCommInitRank");
+    ncclComm_t nc = nullptr;
+    const ncclResult_t e = r.CommInitRank(&nc, (int)world, u, (int)rank);
+    if (prev >= 0 && device >= 0 && device != prev) (void)hipSetDevice(prev);
+    if (e != ncclSuccess) return nccl_fail(e, "ncclCommInitRank");
+    return make_comm(kRcclTransport, nc, world, rank, device, out);
+}
+
+int dsp_comm_init_transport(const dsp_comm_transport *t, void *user, uint32_t world, uint32_t rank,
+                            int32_t device, dsp_comm **out) {
+    if (!t || !out || world == 0 || rank >= world || !t->group_start || !t->group_end || !t->send || !t->recv)
+        return invalid("dsp_comm_init_transport: bad arguments");
+    *out = nullptr;
+    return make_comm(*t, user, world, rank, device, out);
+}
+
+int dsp_comm_init_loopback(uint32_t world, int32_t device, dsp_comm **out) {
+    if (!out || world == 0) return invalid("dsp_comm_init_loopback: bad arguments");
+    auto hub = std::make_shared<LoopHub>();
+    hub->world = world;
+    hub->box.resize((size_t)world * world);
+    for (uint32_t r = 0; r < world; ++r) out[r] = nullptr;
+    for (uint32_t r = 0; r < world; ++r) {
+        LoopRank *lr = new LoopRank();
+        lr->hub = hub;
+        lr->rank = r;
+        int st = make_comm(kLoopTransport, lr, world, r, device, &out[r]);
+        if (st) {
+            for (uint32_t q = 0; q < r; ++q) dsp_comm_destroy(out[q]), out[q] = nullptr;
+            return st;
+        }
     }
-    if (he != hipSuccess) {
-        (void)r.CommDestroy(c->comm);
-        delete c;
-        return dspb::hip_fail(he, "hipStreamCreate");
-    }
-    *out = c;
     return DSP_OK;
 }
 
 void dsp_comm_destroy(dsp_comm *c) {
     if (!c) return;
-    if (c->stream) (void)hipStreamDestroy(c->stream);
-    if (c->comm) (void)rccl().CommDestroy(c->comm);
+    if (c->stream) {
+        (void)hipStreamSynchronize(c->stream);
+        (void)hipStreamDestroy(c->stream);
+    }
+    if (c->t.destroy) c->t.destroy(c->user);
     delete c;
 }
 
-}  // extern "C"
-
-namespace {
-
-// one gather step: rank `src` sends `count` floats to the root's `dst`
-struct Piece {
-    uint32_t src;
-    const float *send;  // on src
-    float *dst;         // on the root
-    uint64_t count;
-};
-
-int run_pieces(dsp_comm *c, uint32_t root, const std::vector<Piece> &pieces, hipStream_t s) {
-    Rccl &r = rccl();
-    bool any_p2p = false;
-    for (const Piece &p : pieces) any_p2p = any_p2p || (p.src != root && p.count);
-    if (any_p2p) NCCL_CK(r.GroupStart());
-    for (const Piece &p : pieces) {
-        if (!p.count) continue;
-        if (p.src == root) {
-            if (c->rank == root && p.dst != p.send)
-                SH_HIP(hipMemcpyAsync(p.dst, p.send, p.count * sizeof(float), hipMemcpyDeviceToDevice, s));
-        } else if (c->rank == root) {
-            NCCL_CK(r.Recv(p.dst, p.count, kNcclFloat32, (int)p.src, c->comm, s));
-        } else if (c->rank == p.src) {
-            NCCL_CK(r.Send(p.send, p.count, kNcclFloat32, (int)root, c->comm, s));
-        }
-    }
-    if (any_p2p) NCCL_CK(r.GroupEnd());
+int dsp_comm_info(const dsp_comm *c, uint32_t *rank, uint32_t *world) {
+    if (!c) return invalid("dsp_comm_info: NULL");
+    if (rank) *rank = c->rank;
+    if (world) *world = c->world;
     return DSP_OK;
 }
-
-}  // namespace
-
-extern "C" {
 
 int dsp_comm_gather(dsp_comm *c, const float *send, uint64_t count, float *const *recv, uint32_t root,
                     void *stream) {
     if (!c || root >= c->world) return invalid("dsp_comm_gather: bad communicator / root");
     if (count && !send) return invalid("dsp_comm_gather: send is NULL");
     if (c->rank == root && count && !recv) return invalid("dsp_comm_gather: recv is NULL on the root");
-    std::vector<Piece> pieces;
+    std::vector<Move> moves;
     for (uint32_t r = 0; r < c->world; ++r) {
         float *dst = (c->rank == root) ? recv[r] : nullptr;
         if (c->rank == root && count && !dst) return invalid("dsp_comm_gather: recv[%u] is NULL", r);
-        pieces.push_back(Piece{r, r == c->rank ? send : nullptr, dst, count});
+        moves.push_back(Move{r, r == c->rank ? send : nullptr, dst, count});
     }
-    return run_pieces(c, root, pieces, (hipStream_t)stream);
+    return run_moves(c, root, moves, (hipStream_t)stream);
 }
 
 int dsp_render_stft_sharded(const float *const *in, uint32_t in_channels, uint64_t L, float *const *out,
@@ -326,30 +615,21 @@ int dsp_render_stft_sharded(const float *const *in, uint32_t in_channels, uint64
     // this rank's chunks (a GENERIC plugin is rendered as one call: its
     // State, if any, carries through the whole channel)
     const bool one_chunk = (plugin && plugin->kind == DSP_PLUGIN_GENERIC) || !halo_fits;
-    const int64_t nch = dsp_shard_chunks(sh, L, B, N, H, 1, one_chunk ? 0 : chunk, nullptr, 0);
+    const uint64_t eff_chunk = one_chunk ? 0 : chunk;
+    const int64_t nch = dsp_shard_chunks(sh, L, B, N, H, 1, eff_chunk, nullptr, 0);
     if (nch < 0) return (int)nch;
     std::vector<dsp_shard> chunks((size_t)nch);
-    dsp_shard_chunks(sh, L, B, N, H, 1, one_chunk ? 0 : chunk, chunks.data(), chunks.size());
-    // the root's view of every rank's plan and chunks
-    std::vector<dsp_shard> plans(world);
-    std::vector<std::vector<dsp_shard>> rchunks(world);
-    int64_t steps = nch;
-    if (gather && comm) {
-        for (uint32_t r = 0; r < world; ++r) {
-            int st = dsp_shard_plan(L, C, world, r, B, N, H, sh->mode, 1, &plans[r]);
-            if (st) return st;
-        }
-        if (plans[rank].chan0 != sh->chan0 || plans[rank].channels != sh->channels || plans[rank].start != sh->start ||
-            plans[rank].owned != sh->owned)
+    dsp_shard_chunks(sh, L, B, N, H, 1, eff_chunk, chunks.data(), chunks.size());
+    // the gather schedule: every rank's plan, chunks and pieces
+    GatherPlan gp;
+    if (gather) {
+        int st = gather_plan(L, C, world, B, N, H, sh->mode, eff_chunk, ld, &gp);
+        if (st) return st;
+        const dsp_shard &p = gp.plans[rank];
+        if (p.chan0 != sh->chan0 || p.channels != sh->channels || p.start != sh->start || p.owned != sh->owned)
             return invalid("the shard does not match dsp_shard_plan(L, C = %u, world %u, rank %u)", C, world, rank);
-        for (uint32_t r = 0; r < world; ++r) {
-            const int64_t n = dsp_shard_chunks(&plans[r], L, B, N, H, 1, one_chunk ? 0 : chunk, nullptr, 0);
-            rchunks[r].resize((size_t)std::max<int64_t>(n, 0));
-            dsp_shard_chunks(&plans[r], L, B, N, H, 1, one_chunk ? 0 : chunk, rchunks[r].data(), rchunks[r].size());
-            steps = std::max<int64_t>(steps, n);
-        }
     }
-    const uint64_t Lpad = (L + B - 1) / B * B;
+    const int64_t steps = gather ? std::max<int64_t>(nch, (int64_t)gp.steps) : nch;
     const uint32_t nrow = sh->channels;
     hipEvent_t ev_done = nullptr;
     std::vector<hipEvent_t> evs;
@@ -361,6 +641,7 @@ int dsp_render_stft_sharded(const float *const *in, uint32_t in_channels, uint64
             if (*e) (void)hipEventDestroy(*e);
         }
     } evg{&evs, &ev_done};
+    size_t pi = 0;  // the next gather piece
     for (int64_t t = 0; t < steps; ++t) {
         // compute chunk t on the caller's stream
         if (t < nch && nrow) {
@@ -377,7 +658,7 @@ int dsp_render_stft_sharded(const float *const *in, uint32_t in_channels, uint64
             }
             dsp_exec e{};
             e.device = dev;
-            e.flags = 0;
+            e.flags = ex ? (ex->flags & DSP_EXEC_FIR_DIRECT) : 0;
             e.stream = s;
             e.sample_offset = goff0 + c.start;
             const uint64_t Fc = frames_of((Lc + B - 1) / B * B, N, H);
@@ -388,38 +669,33 @@ int dsp_render_stft_sharded(const float *const *in, uint32_t in_channels, uint64
             if (st) return st;
         }
         if (!gather) continue;
-        // gather chunk t to the root on the comm stream, behind its compute
-        hipEvent_t ev;
-        SH_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-        evs.push_back(ev);
-        SH_HIP(hipEventRecord(ev, s));
-        hipStream_t gs = comm ? comm->stream : s;
-        if (comm) SH_HIP(hipStreamWaitEvent(gs, ev, 0));
-        std::vector<Piece> pieces;
-        for (uint32_t r = 0; r < world; ++r) {
-            const dsp_shard &pr = comm ? plans[r] : *sh;
-            const std::vector<dsp_shard> &rc = comm ? rchunks[r] : chunks;
-            if (t >= (int64_t)rc.size()) continue;
-            const dsp_shard &c = rc[(size_t)t];
-            // the render rows a chunk contributes: its owned samples, and the
-            // block padding past EOF for the chunk that reaches it
-            const uint64_t rlen = (c.start + c.owned >= L) ? Lpad - c.start : c.owned;
-            for (uint32_t j = 0; j < pr.channels; ++j) {
-                const uint32_t gc = pr.chan0 + j;
-                const bool mine = r == rank;
-                const uint64_t o = c.start - pr.start;
-                pieces.push_back(Piece{r, mine ? out[j] + o : nullptr, rank == root ? all_out[gc] + c.start : nullptr, rlen});
-                pieces.push_back(Piece{r, mine ? mag[j] + (c.frame0 - pr.frame0) * ld : nullptr,
-                                       rank == root ? all_mag[gc] + c.frame0 * ld : nullptr, c.frames * ld});
-            }
+        // gather step t to the root on the comm stream, behind its compute
+        std::vector<Move> moves;
+        for (; pi < gp.pieces.size() && gp.pieces[pi].step == (uint32_t)t; ++pi) {
+            const dsp_gather_piece &p = gp.pieces[pi];
+            const dsp_shard &pr = gp.plans[p.src];
+            const uint32_t j = p.channel - pr.chan0;
+            const float *send = nullptr;
+            float *dst = nullptr;
+            if (p.src == rank) send = (p.what == DSP_PIECE_RENDER ? out[j] : mag[j]) + p.src_off;
+            if (rank == root) dst = (p.what == DSP_PIECE_RENDER ? all_out[p.channel] : all_mag[p.channel]) + p.dst_off;
+            moves.push_back(Move{p.src, send, dst, p.count});
         }
+        if (moves.empty()) continue;
+        hipStream_t gs = s;
         if (comm) {
-            int st = run_pieces(comm, root, pieces, gs);
+            hipEvent_t ev;
+            SH_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+            evs.push_back(ev);
+            SH_HIP(hipEventRecord(ev, s));
+            gs = comm->stream;
+            SH_HIP(hipStreamWaitEvent(gs, ev, 0));
+            int st = run_moves(comm, root, moves, gs);
             if (st) return st;
         } else {  // world 1 without a communicator: device copies
-            for (const Piece &p : pieces)
-                if (p.count && p.dst != p.send)
-                    SH_HIP(hipMemcpyAsync(p.dst, p.send, p.count * sizeof(float), hipMemcpyDeviceToDevice, s));
+            for (const Move &m : moves)
+                if (m.count && m.dst != m.send)
+                    SH_HIP(hipMemcpyAsync(m.dst, m.send, m.count * sizeof(float), hipMemcpyDeviceToDevice, s));
         }
     }
     if (gather && comm) {  // the caller's stream sees the gathered rows

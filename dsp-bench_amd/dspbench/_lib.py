@@ -30,6 +30,7 @@ DSP_PLUGIN_GENERIC = 16
 
 DSP_EXEC_HOST_BUFFERS = 0x1
 DSP_EXEC_SYNC = 0x2
+DSP_EXEC_FIR_DIRECT = 0x4
 
 
 class DspError(RuntimeError):
@@ -113,7 +114,6 @@ _SIGS = {
     "dsp_set": (C.c_int, [C.c_float, FP, C.c_uint64, C.POINTER(dsp_exec)]),
     "dsp_magnitude": (C.c_int, [FP, FP, FP, C.c_uint64, C.POINTER(dsp_exec)]),
     "dsp_kernel_timing_enable": (None, [C.c_int]),
-    "dsp_fir_method": (C.c_int, [C.c_int]),
     "dsp_kernel_timing": (C.c_int, [C.POINTER(C.c_double), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     "dsp_initializer_create": (C.c_void_p, [C.c_size_t, C.c_int]),
     "dsp_initializer_reset": (None, [C.c_void_p]),

@@ -41,6 +41,7 @@ class Plugin:
     state: bytes = b""
     name: str = ""
     module: object = None
+    exec_flags: int = 0  # DSP_EXEC_* bits every call with this plugin adds (per call, no global)
     _keep: list = field(default_factory=list, repr=False)
 
     @staticmethod
@@ -60,10 +61,13 @@ class Plugin:
         return Plugin(L.DSP_PLUGIN_NOOP, b"", b"", "no_op")
 
     @staticmethod
-    def fir(taps) -> "Plugin":
-        """Build-defined FIR (cfg 3b): y[n] = sum_k taps[k] x[n - k]."""
+    def fir(taps, direct: bool = False) -> "Plugin":
+        """Build-defined FIR (cfg 3b): y[n] = sum_k taps[k] x[n - k].  The
+        render uses FFT overlap-save for T <= 1025 taps unless `direct`
+        (DSP_EXEC_FIR_DIRECT on every call with this plugin)."""
         t = np.ascontiguousarray(np.asarray(taps, dtype=np.float32))
-        return Plugin(L.DSP_PLUGIN_FIR, t.tobytes(), b"", f"fir{t.size}")
+        return Plugin(L.DSP_PLUGIN_FIR, t.tobytes(), b"", f"fir{t.size}",
+                      exec_flags=L.DSP_EXEC_FIR_DIRECT if direct else 0)
 
     def as_struct(self) -> dsp_plugin:
         p = C.create_string_buffer(self.params, max(1, len(self.params)))
@@ -134,6 +138,7 @@ def render_offline(file, C_out: int, B: int, sr: float, plugin: Plugin | None,
     out_ptrs, oref = _rows(out)
     ex = _exec(oref, sample_offset, stream)
     ps = plugin.as_struct() if plugin is not None else None
+    ex.flags |= plugin.exec_flags if plugin is not None else 0
     st = L.lib().dsp_render_offline(chan_table(in_ptrs) if in_ptrs else None, len(in_ptrs), L_,
                                     chan_table(out_ptrs), C_out, B, sr,
                                     C.byref(ps) if ps is not None else None, C.byref(ex))
@@ -152,6 +157,7 @@ def render_loop(file, C_out: int, B: int, nblocks: int, sr: float, plugin: Plugi
     out_ptrs, oref = _rows(out)
     ex = _exec(oref, sample_offset, stream)
     ps = plugin.as_struct() if plugin is not None else None
+    ex.flags |= plugin.exec_flags if plugin is not None else 0
     cur = C.c_uint64()
     st = L.lib().dsp_render_loop(chan_table(in_ptrs) if in_ptrs else None, len(in_ptrs), L_, cursor,
                                  chan_table(out_ptrs), C_out, B, nblocks, sr,
@@ -199,6 +205,7 @@ def render_stft(file, C_out: int, B: int, sr: float, plugin: Plugin | None,
     mag_ptrs = [mag[c].data_ptr() if _is_torch(mag) else mag[c].ctypes.data for c in range(C_out)]
     ex = _exec(oref, sample_offset, stream)
     ps = plugin.as_struct() if plugin is not None else None
+    ex.flags |= plugin.exec_flags if plugin is not None else 0
     st = L.lib().dsp_render_stft(chan_table(in_ptrs) if in_ptrs else None, len(in_ptrs), L_,
                                  chan_table(out_ptrs), C_out, B, sr,
                                  C.byref(ps) if ps is not None else None, N, H, window, K,
@@ -225,6 +232,7 @@ def render_stft_host(x, C_out: int, B: int, sr: float, plugin: Plugin | None, st
     in_ptrs = [ptr(x, c) for c in range(x.shape[0])] if x is not None else []
     ex = dsp_exec(device, 0, C.c_void_p(stream) if stream else None, sample_offset)
     ps = plugin.as_struct() if plugin is not None else None
+    ex.flags |= plugin.exec_flags if plugin is not None else 0
     st = L.lib().dsp_render_stft_host(chan_table(in_ptrs) if in_ptrs else None, len(in_ptrs), L_,
                                       chan_table([ptr(out, c) for c in range(C_out)]), C_out, B, sr,
                                       C.byref(ps) if ps is not None else None, N, H, window, K,
@@ -252,6 +260,7 @@ def ir_analysis(plugin: Plugin | None, C_out: int = 2, sr: float = 48000.0,
         mptr = mag.ctypes.data
         ex = _exec(None)
     ps = plugin.as_struct() if plugin is not None else None
+    ex.flags |= plugin.exec_flags if plugin is not None else 0
     st = L.lib().dsp_ir_analysis(C.byref(ps) if ps is not None else None, C_out, sr, ir_len,
                                  chan_table(ir_ptrs), C.cast(C.c_void_p(mptr), L.FP), C.byref(ex))
     check(st, "dsp_ir_analysis")

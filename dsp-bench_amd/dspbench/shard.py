@@ -19,10 +19,16 @@ and the pipelined C driver use:
 
 Concatenating the ranks' owned render samples and owned frames reproduces the
 whole-file result exactly.  ``render_stft_sharded`` runs a rank's share in
-chunks and gathers every chunk's rows to the root behind the next chunk's
-compute: over RCCL inside libdspbench (``RcclComm``, dsp_render_stft_sharded),
-or over a torch.distributed group (``TorchComm``: gloo on CPU, the one-GPU
-rehearsal of the N > 1 path).
+chunks through the C++ driver (dsp_render_stft_sharded), which gathers every
+chunk's rows to the root behind the next chunk's compute following the
+library's gather schedule (``gather_plan``, dsp_shard_gather_plan), over a
+communicator's transport:
+
+  * ``RcclComm``      RCCL over xGMI, one process per GPU (the product);
+  * ``loopback``      ranks as host threads of one process on one GPU (the
+                      world > 1 driver exercised without a second GPU);
+  * ``TorchComm``     a torch.distributed group (gloo) as the transport, for
+                      the one-GPU multi-process rehearsal.
 """
 from __future__ import annotations
 
@@ -33,6 +39,25 @@ from . import _lib as L
 from ._lib import check
 
 TIME, CHANNELS = 0, 1
+
+
+PIECE_RENDER, PIECE_MAG = 0, 1
+
+
+class dsp_gather_piece(C.Structure):
+    _fields_ = [("step", C.c_uint32), ("src", C.c_uint32), ("channel", C.c_uint32), ("what", C.c_uint32),
+                ("src_off", C.c_uint64), ("dst_off", C.c_uint64), ("count", C.c_uint64)]
+
+
+_GROUP = C.CFUNCTYPE(C.c_int, C.c_void_p)
+_SEND = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p)
+_RECV = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p)
+_DESTROY = C.CFUNCTYPE(None, C.c_void_p)
+
+
+class dsp_comm_transport(C.Structure):
+    _fields_ = [("group_start", _GROUP), ("group_end", _GROUP), ("send", _SEND), ("recv", _RECV),
+                ("destroy", _DESTROY)]
 
 
 class dsp_shard(C.Structure):
@@ -50,6 +75,13 @@ _SIGS = {
     "dsp_comm_init": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_int32, C.POINTER(C.c_void_p)]),
     "dsp_comm_destroy": (None, [C.c_void_p]),
     "dsp_comm_gather": (C.c_int, [C.c_void_p, L.FP, C.c_uint64, L.FPP, C.c_uint32, C.c_void_p]),
+    "dsp_shard_gather_plan": (C.c_int64, [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
+                                          C.c_uint32, C.c_uint64, C.c_uint64, C.c_void_p, C.c_uint64,
+                                          C.POINTER(C.c_uint64)]),
+    "dsp_comm_init_loopback": (C.c_int, [C.c_uint32, C.c_int32, C.POINTER(C.c_void_p)]),
+    "dsp_comm_init_transport": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_int32,
+                                          C.POINTER(C.c_void_p)]),
+    "dsp_comm_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
     "dsp_render_stft_sharded": (C.c_int, [L.FPP, C.c_uint32, C.c_uint64, L.FPP, L.FPP, C.c_uint64, C.c_uint32,
                                           C.c_uint32, C.c_float, C.POINTER(L.dsp_plugin), C.c_uint32, C.c_uint32,
                                           C.c_int32, C.c_uint32, C.POINTER(dsp_shard), C.c_uint64, C.c_void_p,
@@ -133,18 +165,70 @@ def chunks(s: Shard, L_total: int, B: int, N: int = 8192, H: int = 4096, render:
 
 
 # --------------------------------------------------------------------------
+# the gather schedule
+# --------------------------------------------------------------------------
+
+@dataclass(frozen=True)
+class Piece:
+    step: int
+    src: int
+    channel: int
+    what: int       # PIECE_RENDER / PIECE_MAG
+    src_off: int    # floats into the sender's local row
+    dst_off: int    # floats into the root's whole-file row
+    count: int
+
+
+def gather_plan(L_total: int, C_total: int, world: int, B: int, N: int = 8192, H: int = 4096,
+                mode: int = TIME, chunk: int = 0, ld: int = 4097):
+    """(pieces, steps): the gather schedule dsp_render_stft_sharded follows
+    (dsp_shard_gather_plan), every rank's chunk t moved to the root at step t."""
+    lib = _lib()
+    steps = C.c_uint64()
+    n = lib.dsp_shard_gather_plan(L_total, C_total, world, B, N, H, mode, chunk, ld, None, 0, C.byref(steps))
+    if n < 0:
+        check(int(n), "dsp_shard_gather_plan")
+    arr = (dsp_gather_piece * max(1, n))()
+    lib.dsp_shard_gather_plan(L_total, C_total, world, B, N, H, mode, chunk, ld, arr, n, None)
+    return [Piece(a.step, a.src, a.channel, a.what, a.src_off, a.dst_off, a.count) for a in arr[:n]], steps.value
+
+
+# --------------------------------------------------------------------------
 # communicators
 # --------------------------------------------------------------------------
 
-class RcclComm:
-    """dsp_comm: an RCCL communicator inside libdspbench (xGMI)."""
+class _Comm:
+    handle = None
+
+    def _info(self):
+        r, w = C.c_uint32(), C.c_uint32()
+        check(_lib().dsp_comm_info(self.handle, C.byref(r), C.byref(w)), "dsp_comm_info")
+        self.rank, self.world = r.value, w.value
+
+    def gather(self, send, recv_rows, root: int = 0, stream=None):
+        """Every rank's `send` (device, count floats) into the root's recv_rows[r]."""
+        rows = L.chan_table([r.data_ptr() for r in recv_rows]) if recv_rows is not None else None
+        check(_lib().dsp_comm_gather(self.handle, C.cast(C.c_void_p(send.data_ptr()), L.FP), send.numel(), rows,
+                                     root, C.c_void_p(stream) if stream else None), "dsp_comm_gather")
+
+    def close(self):
+        h = getattr(self, "handle", None)
+        if h:
+            _lib().dsp_comm_destroy(h)
+            self.handle = None
+
+    def __del__(self):
+        self.close()
+
+
+class RcclComm(_Comm):
+    """dsp_comm over RCCL inside libdspbench (xGMI), one process per GPU."""
 
     def __init__(self, uid: bytes, world: int, rank: int, device: int = -1):
-        self.world, self.rank = world, rank
         self.handle = C.c_void_p()
-        self._destroy = _lib().dsp_comm_destroy
         buf = C.create_string_buffer(bytes(uid), 128)
         check(_lib().dsp_comm_init(buf, world, rank, device, C.byref(self.handle)), "dsp_comm_init")
+        self._info()
 
     @staticmethod
     def unique_id() -> bytes:
@@ -161,43 +245,89 @@ class RcclComm:
         dist.broadcast_object_list(obj, src=0, group=group)
         return RcclComm(obj[0], world, rank, device)
 
-    def gather(self, send, recv_rows, root: int = 0, stream=None):
-        """Every rank's `send` (device, count floats) into the root's recv_rows[r]."""
-        rows = L.chan_table([r.data_ptr() for r in recv_rows]) if recv_rows is not None else None
-        check(_lib().dsp_comm_gather(self.handle, C.cast(C.c_void_p(send.data_ptr()), L.FP), send.numel(), rows,
-                                     root, C.c_void_p(stream) if stream else None), "dsp_comm_gather")
 
-    def __del__(self):
-        h = getattr(self, "handle", None)
-        if h:
-            self._destroy(h)
-            self.handle = None
+class _Handle(_Comm):
+    def __init__(self, handle):
+        self.handle = handle
+        self._info()
 
 
-class TorchComm:
-    """A torch.distributed group as the gather transport (gloo: CPU tensors).
-    The CPU tests and the one-GPU rehearsal of the N > 1 path use it; the
-    product's multi-GPU path is RcclComm."""
+def loopback(world: int, device: int = -1) -> list:
+    """dsp_comm_init_loopback: `world` communicators of one process, ranks as
+    host threads sharing one GPU (each thread drives its own rank)."""
+    arr = (C.c_void_p * world)()
+    check(_lib().dsp_comm_init_loopback(world, device, arr), "dsp_comm_init_loopback")
+    return [_Handle(C.c_void_p(arr[r])) for r in range(world)]
 
-    def __init__(self, group=None):
+
+class TorchComm(_Comm):
+    """A torch.distributed group (gloo) as a dsp_comm transport
+    (dsp_comm_init_transport): the C++ driver's sends and recvs of device rows
+    move through host tensors.  For the one-GPU multi-process rehearsal of the
+    N > 1 path; the product's multi-GPU transport is RcclComm."""
+
+    def __init__(self, group=None, device: int = -1):
         import torch.distributed as dist
         self.group = group
-        self.world, self.rank = dist.get_world_size(group), dist.get_rank(group)
+        rank, world = dist.get_rank(group), dist.get_world_size(group)
+        self._hip = C.CDLL("libamdhip64.so")
+        self._hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+        self._hip.hipStreamSynchronize.argtypes = [C.c_void_p]
+        self._depth, self._ops = 0, []
 
-    def run(self, pieces, root: int):
-        """pieces: (src rank, send tensor on src | None, recv view on root | None)."""
+        def guard(fn):
+            def run(*a):
+                try:
+                    return fn(*a)
+                except Exception as e:  # a raising callback must not unwind through C
+                    print(f"TorchComm transport: {e!r}", flush=True)
+                    return L.DSP_ERR_INVALID
+            return run
+
+        def group_start(_u):
+            self._depth += 1
+            return 0
+
+        def group_end(_u):
+            self._depth -= 1
+            return self._flush() if self._depth == 0 else 0
+
+        def send(_u, buf, count, peer, stream):
+            self._ops.append(("send", buf, count, peer, stream))
+            return 0 if self._depth else self._flush()
+
+        def recv(_u, buf, count, peer, stream):
+            self._ops.append(("recv", buf, count, peer, stream))
+            return 0 if self._depth else self._flush()
+
+        self._fns = (_GROUP(guard(group_start)), _GROUP(guard(group_end)), _SEND(guard(send)),
+                     _RECV(guard(recv)), _DESTROY(0))
+        self._t = dsp_comm_transport(*self._fns)
+        self.handle = C.c_void_p()
+        check(_lib().dsp_comm_init_transport(C.byref(self._t), None, world, rank, device, C.byref(self.handle)),
+              "dsp_comm_init_transport")
+        self._info()
+
+    def _flush(self):
         import torch
         import torch.distributed as dist
-        for src, send, dst in pieces:
-            if src == root:
-                if self.rank == root and send is not None and dst is not None and dst.data_ptr() != send.data_ptr():
-                    dst.copy_(send)
-            elif self.rank == root:
-                buf = torch.empty(dst.shape, dtype=dst.dtype)
-                dist.recv(buf, src=src, group=self.group)
-                dst.copy_(buf)
-            elif self.rank == src:
-                dist.send(send.detach().to("cpu").contiguous(), dst=root, group=self.group)
+        ops, self._ops = self._ops, []
+        works, recvs = [], []
+        for kind, buf, count, peer, stream in ops:
+            host = torch.empty(int(count), dtype=torch.float32)
+            if kind == "send":  # the rows are final once the stream has passed them
+                if self._hip.hipStreamSynchronize(stream) or self._hip.hipMemcpy(host.data_ptr(), buf, count * 4, 2):
+                    return L.DSP_ERR_HIP
+                works.append(dist.isend(host, dst=peer, group=self.group))
+            else:
+                works.append(dist.irecv(host, src=peer, group=self.group))
+                recvs.append((host, buf, stream))
+        for w in works:
+            w.wait()
+        for host, buf, stream in recvs:  # into the root's rows, ordered after its earlier work
+            if self._hip.hipStreamSynchronize(stream) or self._hip.hipMemcpy(buf, host.data_ptr(), host.numel() * 4, 1):
+                return L.DSP_ERR_HIP
+        return 0
 
 
 # --------------------------------------------------------------------------
@@ -207,8 +337,9 @@ class TorchComm:
 def render_stft_sharded(x, L_total: int, C_total: int, B: int, sr: float, plugin, s: Shard,
                         out, mag, comm=None, root: int = 0, all_out=None, all_mag=None,
                         N: int = 8192, H: int = 4096, window: int = L.DSP_WIN_HANN, K: int | None = None,
-                        chunk: int = 1 << 24, compute=None, gather: bool = True):
-    """This rank's share of a sharded render + STFT, gathered to the root.
+                        chunk: int = 1 << 24, gather: bool = True, stream=None):
+    """This rank's share of a sharded render + STFT, gathered to the root
+    (dsp_render_stft_sharded).
 
     x:        this rank's file rows, local (x[c][0] = global sample s.start;
               time mode: owned + halo samples; channel mode: the file's rows
@@ -216,71 +347,24 @@ def render_stft_sharded(x, L_total: int, C_total: int, B: int, sr: float, plugin
     out, mag: this rank's rows: [channels, >= ceil((owned + halo) / B) B] and
               [channels, >= frames, ld]
     all_out / all_mag: root only, [C_total, ceil(L / B) B] / [C_total, F, ld]
-    comm:     RcclComm (or None with world 1): the pipelined C++ driver
-              (dsp_render_stft_sharded); TorchComm: the same chunk schedule and
-              gather pieces, driven from Python (compute: a function
-              (chunk, x_view, out_view, mag_view, sample_offset) standing in for
-              the GPU render, for the CPU tests).
+    comm:     a communicator (RcclComm, a loopback() entry, TorchComm), or None
+              (no collective; at world 1 the rows are copied to all_out /
+              all_mag)
+    stream:   the HIP stream to compute on (default: the current torch stream)
     """
-    import torch
-    from .api import _exec, _rows
     K = K if K is not None else N // 2 + 1
-    ld = mag.shape[-1] if hasattr(mag, "shape") else K
+    ld = mag.shape[-1]
     if gather and (comm is None or comm.rank == root) and (all_out is None or all_mag is None):
         raise ValueError("the root needs all_out and all_mag to gather into (gather=False to skip)")
+    from .api import _exec, _rows
     in_ch = 0 if x is None else int(x.shape[0])
-    if isinstance(comm, TorchComm):
-        world, rank = comm.world, comm.rank
-        plans = [plan(L_total, world, r, B, N, H, True, C_total, s.mode) for r in range(world)]
-        assert plans[rank] == s, (plans[rank], s)
-        rch = [chunks(p, L_total, B, N, H, True, chunk) for p in plans]
-        Lpad = -(-L_total // B) * B
-        for t in range(max(len(c) for c in rch)):
-            if t < len(rch[rank]) and s.channels:
-                c = rch[rank][t]
-                o = c.start - s.start
-                Lc = min(max(L_total - c.start, 0), c.owned + c.halo)
-                xo = x[:, o:o + Lc] if in_ch else None
-                nb = -(-Lc // B)
-                oo = out[:, o:o + nb * B]
-                mo = mag[:, c.frame0 - s.frame0:c.frame0 - s.frame0 + c.frames]
-                if compute is not None:
-                    compute(c, xo, oo, mo, c.start)
-                else:
-                    from .api import render_stft
-                    Fc = stft_frames(nb * B, N, H)
-                    if Fc > c.frames:
-                        raise ValueError(f"chunk computes {Fc} frames, owns {c.frames}")
-                    # (a chunk without frames still needs valid magnitude rows)
-                    mrows = mag[:, c.frame0 - s.frame0:] if c.frames else mag
-                    render_stft(xo, s.channels, B, sr, plugin, N=N, H=H, window=window, K=K, ld=ld,
-                                out=oo, mag=mrows, sample_offset=c.start, L_file=Lc, ref=out)
-                    if out.is_cuda:
-                        torch.cuda.current_stream().synchronize()
-            pieces = []
-            for r in range(world):
-                if t >= len(rch[r]):
-                    continue
-                c, pr = rch[r][t], plans[r]
-                rlen = Lpad - c.start if c.start + c.owned >= L_total else c.owned
-                o = c.start - pr.start
-                for j in range(pr.channels):
-                    gc = pr.chan0 + j
-                    mine, onroot = r == rank, rank == root
-                    pieces.append((r, out[j, o:o + rlen] if mine else None,
-                                   all_out[gc, c.start:c.start + rlen] if onroot else None))
-                    pieces.append((r, mag[j, c.frame0 - pr.frame0:c.frame0 - pr.frame0 + c.frames] if mine else None,
-                                   all_mag[gc, c.frame0:c.frame0 + c.frames] if onroot else None))
-            if gather:
-                comm.run(pieces, root)
-        return
-    # RCCL / world 1: the pipelined C++ driver
     lib = _lib()
     in_ptrs, _ = _rows(x) if in_ch else ([], None)
     out_ptrs, oref = _rows(out)
     mag_ptrs = [mag[c].data_ptr() for c in range(mag.shape[0])]
-    ex = _exec(oref)
+    ex = _exec(oref, stream=stream)
     ps = plugin.as_struct() if plugin is not None else None
+    ex.flags |= plugin.exec_flags if plugin is not None else 0
     cs = s._c()
     ao = am = None
     if gather and all_out is not None:

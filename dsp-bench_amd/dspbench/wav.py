@@ -129,6 +129,7 @@ def render_stft_wav(data, info: dsp_wav_info, C_out: int, B: int, sr: float, plu
     src = data.data_ptr() if _is_torch(data) else np.ascontiguousarray(data).ctypes.data
     ex = L.dsp_exec(device, 0, C.c_void_p(stream) if stream else None, 0)
     ps = plugin.as_struct() if plugin is not None else None
+    ex.flags |= plugin.exec_flags if plugin is not None else 0
     check(L.lib().dsp_render_stft_wav(C.c_void_p(src), C.byref(info), C_out, B, sr,
                                       C.byref(ps) if ps is not None else None, N, H, window, K, optrs, mptrs, K,
                                       chunk, C.byref(ex)), "dsp_render_stft_wav")

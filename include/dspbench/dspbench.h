@@ -85,6 +85,9 @@ typedef struct dsp_plugin {
 /* Execution context (ref has none: single-threaded per audio thread). */
 #define DSP_EXEC_HOST_BUFFERS 0x1u /* in/out/mag are host pointers: stage via HBM */
 #define DSP_EXEC_SYNC 0x2u         /* synchronise the stream before returning */
+#define DSP_EXEC_FIR_DIRECT 0x4u   /* DSP_PLUGIN_FIR: the direct form even when T <= 1025 (default:
+                                      FFT overlap-save with 8192-point frames for T <= 1025, the
+                                      direct form above) */
 
 typedef struct dsp_exec {
     int32_t device;         /* HIP device ordinal; -1 = current device */
@@ -202,11 +205,6 @@ int dsp_kernel_timing(double *total_ms, uint64_t *launches, uint64_t *bytes);
  * build/ab/libdspbench_ab.so, which adds dsp_stft_pk_ab_options()); this
  * library has no process-wide kernel selection. */
 
-/* FIR render method (DSP_PLUGIN_FIR): 0 = auto (FFT overlap-save with
- * 8192-point frames when T <= 1025, else direct form), 1 = direct form,
- * 2 = overlap-save (T <= 1025).  Other values only query.  Returns the
- * previous method. */
-int dsp_fir_method(int method);
 
 /* Diagnostics. */
 int dsp_abi_version(void);

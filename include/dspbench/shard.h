@@ -21,7 +21,10 @@
  *
  * Within a rank the owned range is processed in chunks (dsp_shard_chunks)
  * and each chunk's render rows and magnitude rows are gathered to the root
- * on a separate HIP stream while the next chunk computes.
+ * on a separate HIP stream while the next chunk computes, following
+ * dsp_shard_gather_plan, over a communicator's transport: RCCL between
+ * processes (the product), or an in-process loopback (ranks as threads on
+ * one GPU) that runs the same driver at world > 1 without a second GPU.
  *
  * The reference has no multi-GPU path (single audio thread, audio.cpp:13-175);
  * everything here is new, built around its single-GPU semantics.
@@ -66,16 +69,74 @@ int dsp_shard_plan(uint64_t L, uint32_t C, uint32_t world, uint32_t rank, uint32
 int64_t dsp_shard_chunks(const dsp_shard *s, uint64_t L, uint32_t B, uint32_t N, uint32_t H, int render,
                          uint64_t chunk, dsp_shard *out, uint64_t cap);
 
-/* ---- RCCL communicator (one per rank; xGMI between the GPUs of a node) ---- */
+/* ---- the gather schedule ---------------------------------------------------
+ * Every rank's chunk t is gathered to the root as one step: for each of the
+ * rank's channels, its owned render samples (plus the block padding past EOF
+ * for the chunk that reaches it) and its owned magnitude rows.  One entry per
+ * non-empty move, ordered by (step, src, channel, what). */
+enum dsp_piece_what { DSP_PIECE_RENDER = 0, DSP_PIECE_MAG = 1 };
+
+typedef struct dsp_gather_piece {
+    uint32_t step;     /* pipeline step (the sender's chunk index) */
+    uint32_t src;      /* sending rank */
+    uint32_t channel;  /* global device channel; the sender's row is channel - its chan0 */
+    uint32_t what;     /* dsp_piece_what */
+    uint64_t src_off;  /* floats into the sender's local row (out[j] / mag[j]) */
+    uint64_t dst_off;  /* floats into the root's whole-file row (all_out[channel] / all_mag[channel]) */
+    uint64_t count;    /* floats */
+} dsp_gather_piece;
+
+/* The gather schedule of a `world`-rank sharded render + STFT (the plans of
+ * dsp_shard_plan(..., render = 1), chunks of dsp_shard_chunks(..., chunk);
+ * chunk 0 = one chunk per rank), magnitude rows of stride ld.  Writes
+ * min(n, cap) pieces to out (may be NULL), returns n (or a negative status);
+ * *steps (may be NULL) receives the number of pipeline steps.
+ * dsp_render_stft_sharded moves exactly these pieces. */
+int64_t dsp_shard_gather_plan(uint64_t L, uint32_t C, uint32_t world, uint32_t B, uint32_t N, uint32_t H,
+                              uint32_t mode, uint64_t chunk, uint64_t ld, dsp_gather_piece *out, uint64_t cap,
+                              uint64_t *steps);
+
+/* ---- communicators (one per rank) -------------------------------------------
+ * A communicator moves floats between ranks through a transport with NCCL
+ * point-to-point semantics.  The product transport is RCCL over xGMI
+ * (dsp_comm_init); others plug in through dsp_comm_init_transport. */
 #define DSP_COMM_ID_BYTES 128
 typedef struct dsp_comm dsp_comm;
 
-/* A fresh communicator id (ncclGetUniqueId), made on one rank and handed
- * to the others out of band (torch.distributed, a file, a socket). */
+/* A transport: every call is enqueued on a HIP stream and returns 0 or a
+ * negative dsp_status.  A send and its matching recv carry the same count;
+ * between group_start and group_end (which nest) the sends and recvs of one
+ * gather step are issued in schedule order by every rank and must complete
+ * without deadlock whatever the peers' order; a send's buffer may be reused
+ * once `stream` has passed the send. */
+typedef struct dsp_comm_transport {
+    int (*group_start)(void *user);
+    int (*group_end)(void *user);
+    int (*send)(void *user, const float *buf, uint64_t count, uint32_t peer, void *stream);
+    int (*recv)(void *user, float *buf, uint64_t count, uint32_t peer, void *stream);
+    void (*destroy)(void *user); /* NULL: nothing to release */
+} dsp_comm_transport;
+
+/* A fresh RCCL communicator id (ncclGetUniqueId), made on one rank and
+ * handed to the others out of band (torch.distributed, a file, a socket). */
 int dsp_comm_unique_id(void *id);
-/* Join the communicator of `world` ranks on `device` (-1: current). */
+/* Join the RCCL communicator of `world` ranks on `device` (-1: current). */
 int dsp_comm_init(const void *id, uint32_t world, uint32_t rank, int32_t device, dsp_comm **out);
+/* Rank `rank` of `world` over a caller's transport (copied; `user` is passed
+ * to every call and to destroy when the communicator goes). */
+int dsp_comm_init_transport(const dsp_comm_transport *t, void *user, uint32_t world, uint32_t rank,
+                            int32_t device, dsp_comm **out);
+/* In-process loopback: `world` communicators (out[0 .. world)) whose ranks
+ * are host threads of this process sharing `device` (-1: current), one
+ * thread per rank.  A send records an event on the sender's stream; the
+ * matching recv makes the receiver's stream wait for it and copies device to
+ * device; the sender's stream then waits for that copy.  A peer that never
+ * posts its side fails the wait after 120 s (DSP_ERR_INVALID).  Each
+ * communicator is destroyed on its own. */
+int dsp_comm_init_loopback(uint32_t world, int32_t device, dsp_comm **out);
 void dsp_comm_destroy(dsp_comm *c);
+/* The rank and world of a communicator (either may be NULL). */
+int dsp_comm_info(const dsp_comm *c, uint32_t *rank, uint32_t *world);
 
 /* Gather: every rank sends `count` floats from `send` (device memory); the
  * root receives rank r's into recv[r] (device memory, world entries; its own

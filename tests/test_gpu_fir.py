@@ -28,10 +28,13 @@ OLS_TOL = 2e-6  # overlap-save: max |y - y64| <= OLS_TOL * max |y64| (fp32 FFT r
 
 @pytest.fixture(params=[1, 2], ids=["direct", "ols"])
 def fir_method(request):
-    """Both FIR kernels: 1 = direct form, 2 = FFT overlap-save (T <= 1025)."""
-    old = d.lib().dsp_fir_method(request.param)
-    yield request.param
-    d.lib().dsp_fir_method(old)
+    """Both FIR kernels: 1 = direct form (DSP_EXEC_FIR_DIRECT), 2 = FFT
+    overlap-save (the default for T <= 1025)."""
+    return request.param
+
+
+def fplug(taps, method):
+    return d.Plugin.fir(taps, direct=(method == 1))
 
 
 def check_fir(oracle, y, x, taps, Ly, method=1):
@@ -60,12 +63,12 @@ def test_gpu_fir_render(torch_cuda, oracle, fir_method, T, L, B):
     rng = np.random.default_rng(T * 7 + L)
     x = rng.uniform(-1, 1, (2, L)).astype(np.float32)
     taps = (rng.standard_normal(T) / np.sqrt(T)).astype(np.float32)
-    out = d.render_offline(torch_cuda.from_numpy(x).cuda(), 2, B, 48000.0, d.Plugin.fir(taps)).cpu().numpy()
+    out = d.render_offline(torch_cuda.from_numpy(x).cuda(), 2, B, 48000.0, fplug(taps, fir_method)).cpu().numpy()
     Ly = -(-L // B) * B
     assert out.shape == (2, Ly)
     for c in range(2):
         check_fir(oracle, out[c], x[c], taps, Ly, fir_method)
-    host = d.render_offline(x, 2, B, 48000.0, d.Plugin.fir(taps))          # host buffers
+    host = d.render_offline(x, 2, B, 48000.0, fplug(taps, fir_method))          # host buffers
     assert np.array_equal(host, out)
 
 
@@ -73,7 +76,7 @@ def test_gpu_fir_render(torch_cuda, oracle, fir_method, T, L, B):
 def test_gpu_fir_channels_and_missing_input(torch_cuda, oracle, fir_method):
     x = np.random.default_rng(5).uniform(-1, 1, (1, 9000)).astype(np.float32)
     taps = cfg3b_taps()
-    out = d.render_offline(torch_cuda.from_numpy(x).cuda(), 3, 512, 48000.0, d.Plugin.fir(taps)).cpu().numpy()
+    out = d.render_offline(torch_cuda.from_numpy(x).cuda(), 3, 512, 48000.0, fplug(taps, fir_method)).cpu().numpy()
     check_fir(oracle, out[0], x[0], taps, out.shape[1], fir_method)
     assert not out[1:].any()   # extra channels: zero input through the FIR
 
@@ -87,7 +90,7 @@ def test_gpu_fir_cfg3b_full_size(torch_cuda, oracle, fir_method):
     g = torch.Generator(device="cuda").manual_seed(2)
     x = torch.rand((2, L), device="cuda", generator=g) * 2 - 1
     taps = cfg3b_taps()
-    out = d.render_offline(x, 2, 512, 48000.0, d.Plugin.fir(taps))
+    out = d.render_offline(x, 2, 512, 48000.0, fplug(taps, fir_method))
     rng = np.random.default_rng(1)
     idx = np.concatenate([np.arange(2048), np.arange(L - 2048, L), rng.integers(0, L, 4000)])
     peak = float(np.sum(np.abs(taps)))  # |y| <= sum |h| for |x| <= 1
@@ -109,13 +112,13 @@ def test_gpu_fir_stft_and_ir(torch_cuda, oracle, fir_method):
     torch = torch_cuda
     taps = cfg3b_taps()
     x = np.random.default_rng(8).uniform(-1, 1, (2, 8192 * 3)).astype(np.float32)
-    out, mag = d.render_stft(torch.from_numpy(x).cuda(), 2, 512, 48000.0, d.Plugin.fir(taps))
+    out, mag = d.render_stft(torch.from_numpy(x).cuda(), 2, 512, 48000.0, fplug(taps, fir_method))
     o = out.cpu().numpy()
     check_fir(oracle, o[1], x[1], taps, o.shape[1], fir_method)
     mref = oracle.np_stft_mag(o[1], 8192, 4096, d.DSP_WIN_HANN, 4097)
     m = mag.cpu().numpy()[1]
     assert np.max(np.abs(m - mref)) <= 1e-6 * np.max(mref)
-    ir, imag = d.ir_analysis(d.Plugin.fir(taps), C_out=2, device="cuda")    # IR of a FIR = its taps
+    ir, imag = d.ir_analysis(fplug(taps, fir_method), C_out=2, device="cuda")    # IR of a FIR = its taps
     irn = ir.cpu().numpy()[0]
     want = np.concatenate([taps, np.zeros(1024, np.float32)])
     if fir_method == 1:
@@ -131,3 +134,20 @@ def test_gpu_fir_rejects_too_many_taps(torch_cuda):
     x = torch_cuda.zeros((1, 4096), device="cuda")
     with pytest.raises(d.DspError):
         d.render_offline(x, 1, 512, 48000.0, d.Plugin.fir(np.ones(2049, np.float32)))
+
+
+@pytest.mark.gpu
+def test_fir_method_is_per_call(torch_cuda):
+    """The FIR method travels with each call (dsp_exec flags): interleaved
+    direct-form and overlap-save renders each reproduce their own result."""
+    torch = torch_cuda
+    rng = np.random.default_rng(77)
+    taps = rng.uniform(-0.2, 0.2, 300).astype(np.float32)
+    x = torch.from_numpy(rng.uniform(-1, 1, (2, 48_000)).astype(np.float32)).cuda()
+    pd, po = d.Plugin.fir(taps, direct=True), d.Plugin.fir(taps)
+    ref_d = d.render_offline(x, 2, 512, 48000.0, pd).clone()
+    ref_o = d.render_offline(x, 2, 512, 48000.0, po).clone()
+    assert not torch.equal(ref_d, ref_o)  # two different kernels (rounding differs)
+    for _ in range(3):
+        assert torch.equal(d.render_offline(x, 2, 512, 48000.0, po), ref_o)
+        assert torch.equal(d.render_offline(x, 2, 512, 48000.0, pd), ref_d)

@@ -5,12 +5,35 @@ the current stream) and replay the whole render + STFT of a file with one
 launch -- what an application rendering many short files repeatedly wants.
 Replays must give the eager call's bits, and follow new input contents.
 """
+import gc
+
 import numpy as np
 import pytest
 
 import dspbench as d
 
 pytestmark = pytest.mark.gpu
+
+
+def _refused_capture(torch, fn):
+    """Capture fn() on a fresh stream, expecting the library to refuse it;
+    returns the error text.  The failed graph is destroyed and collected here,
+    outside any capture (a graph object collected during a later capture
+    would free its pool mid-capture)."""
+    gc.collect()
+    side = torch.cuda.Stream()
+    g = torch.cuda.CUDAGraph()
+    msg = None
+    try:
+        with torch.cuda.graph(g, stream=side):
+            fn()
+    except Exception as e:  # noqa: BLE001
+        msg = str(e)
+    torch.cuda.synchronize()
+    del g
+    gc.collect()
+    assert msg is not None, "the capture was not refused"
+    return msg
 
 
 def _eager_and_graph(torch, fn, x):
@@ -84,10 +107,48 @@ def test_capture_on_a_cold_stream_is_refused_cleanly(torch_cuda):
     p = d.Plugin.ir_test(0.8, 0.0013)
     d.render_stft(x, 2, 384, 48000.0, p)      # device tables exist
     torch.cuda.synchronize()
-    side = torch.cuda.Stream()
-    g = torch.cuda.CUDAGraph()
-    with pytest.raises(Exception) as e:
-        with torch.cuda.graph(g, stream=side):
-            d.render_stft(x, 2, 384, 48000.0, p)
-    assert "eager call" in str(e.value) or "capture" in str(e.value)
+    msg = _refused_capture(torch, lambda: d.render_stft(x, 2, 384, 48000.0, p))
+    assert "eager call" in msg or "capture" in msg
+
+
+def test_generic_plugin_capture_is_refused(torch_cuda):
+    """A GENERIC plugin's Parameters go up through a host-staged copy, which a
+    graph replay would not repeat: capturing its render is refused with a
+    clear error, and the eager call still works afterwards."""
+    import os
+    torch = torch_cuda
+    mods = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "dsp-bench_amd", "modules")
+    with open(os.path.join(mods, "mod_gain_test.co"), "rb") as f:
+        mod = d.module.Module(f.read())
+    params = mod.default_parameters()
+    mod.initialize_state(params, 2, 48000.0)
+    p = mod.plugin(params, "gain_test")
+    x = torch.rand((2, 4096), device="cuda")
+    want = d.render_offline(x, 2, 512, 48000.0, p).clone()
     torch.cuda.synchronize()
+    msg = _refused_capture(torch, lambda: d.render_offline(x, 2, 512, 48000.0, p))
+    assert "captured" in msg, msg
+    assert torch.equal(d.render_offline(x, 2, 512, 48000.0, p), want)
+
+
+def test_first_use_table_under_capture_is_refused(torch_cuda):
+    """A window table first needed inside a capture (a kind / N no eager call
+    used) is refused with the 'eager call first' error instead of uploading
+    on the legacy stream mid-capture; after one eager call the capture works."""
+    torch = torch_cuda
+    x = torch.rand((1, 3 * 2048), device="cuda")
+    msg = _refused_capture(torch, lambda: d.stft_magnitude(x, N=2048, H=777, window=d.DSP_WIN_RECT, K=1025))
+    assert "eager call" in msg, msg
+    side = torch.cuda.Stream()
+    want = d.stft_magnitude(x, N=2048, H=777, window=d.DSP_WIN_RECT, K=1025).clone()
+    out = torch.empty_like(want)
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        d.stft_magnitude(x, N=2048, H=777, window=d.DSP_WIN_RECT, K=1025, out=out)
+    torch.cuda.synchronize()
+    g2 = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g2, stream=side):
+        d.stft_magnitude(x, N=2048, H=777, window=d.DSP_WIN_RECT, K=1025, out=out)
+    g2.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(out, want)

@@ -2,10 +2,13 @@
 FFT, one channel per GPU, RCCL gather) through the product's shard path on
 one GPU: the per-GPU unit (C = 1, 96 kHz, IR_test + fused STFT) against the
 oracle, the pipelined C++ driver (dsp_render_stft_sharded) with an RCCL
-communicator of one rank, and a two-rank rehearsal of the N > 1 path (both
-ranks on cuda:0, gloo as the transport) that must reassemble the whole-file
-result.  The 8-GPU run itself is the driver's (unmeasured on hardware here).
+communicator of one rank, the same driver at world 2 and 4 with the ranks as
+threads on one GPU (the in-process loopback transport: the C++ chunk and
+gather schedule, every rank's pieces), and a two-process rehearsal with gloo
+as the transport; each must reassemble the whole-file result bit for bit.
+The 8-GPU run itself is the driver's.
 """
+import threading
 import os
 import socket
 
@@ -102,6 +105,124 @@ def test_rccl_gather_one_rank(torch_cuda):
     assert torch.equal(src, dst)
 
 
+def _run_ranks(torch, world, fn):
+    """fn(rank) on `world` host threads at once; re-raise the first failure."""
+    errs = [None] * world
+
+    def body(r):
+        try:
+            torch.cuda.set_device(0)
+            fn(r)
+        except BaseException as e:  # noqa: BLE001
+            errs[r] = e
+    ts = [threading.Thread(target=body, args=(r,)) for r in range(world)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=240)
+        assert not t.is_alive(), "a rank thread hung"
+    for e in errs:
+        if e is not None:
+            raise e
+
+
+@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("mode,C_total,C_file,chunk,root", [
+    (sh.CHANNELS, 8, 6, 1 << 16, 0),   # cfg 5 in small: 8 device channels, a 6-channel file
+    (sh.CHANNELS, 8, 8, 0, 1),         # one chunk per rank, root 1
+    (sh.TIME, 2, 2, 3 * 4096, 0),      # time shards with halos, chunked inside each rank
+])
+def test_loopback_sharded_driver_equals_whole_file(torch_cuda, world, mode, C_total, C_file, chunk, root):
+    """dsp_render_stft_sharded at world 2 / 4 over the loopback transport:
+    every rank a host thread with its own stream, its own file rows and
+    render / magnitude rows; the root's gathered rows equal dsp_render_stft
+    of the whole file bit for bit (the reference's per-channel rule for the
+    channels the file lacks, audio.cpp:65-81,138-141)."""
+    torch = torch_cuda
+    L, B, K = 8192 * 14 + 2345, 512, 4097
+    g = torch.Generator(device="cuda").manual_seed(5 + world)
+    # rows 8-byte aligned (an even row stride), so the whole-file call and
+    # every rank take the fused kernel: the two-pass path (render, then the
+    # memory STFT) that misaligned rows take agrees with it to ~1e-8 of the
+    # peak, not bit for bit
+    x = (torch.rand((C_file, L + 1), device="cuda", generator=g) * 2 - 1)[:, :L]
+    plugin = d.Plugin.ir_test(0.8, 0.001) if mode == sh.CHANNELS else d.Plugin.gain_test(0.3)
+    ref_out, ref_mag = _whole(torch, x, C_total, B, plugin, L)
+    nb = -(-L // B)
+    F = ref_mag.shape[1]
+    all_out = torch.full((C_total, nb * B), -7.0, device="cuda")
+    all_mag = torch.full((C_total, F, K), -7.0, device="cuda")
+    comms = sh.loopback(world, 0)
+    assert [c.rank for c in comms] == list(range(world)) and all(c.world == world for c in comms)
+
+    def rank_fn(r):
+        s = sh.plan(L, world, r, B, 8192, 4096, True, C_total, mode)
+        nf = max(0, min(s.chan0 + s.channels, C_file) - s.chan0)  # the file rows this rank reads
+        xl = x[s.chan0:s.chan0 + nf, s.start:s.start + s.read_len] if nf else None  # views: no copy
+        out = torch.empty((max(s.channels, 1), -(-s.read_len // B) * B), device="cuda")
+        mag = torch.empty((max(s.channels, 1), max(s.frames, 1), K), device="cuda")
+        st = torch.cuda.Stream()
+        with torch.cuda.stream(st):
+            sh.render_stft_sharded(xl, L, C_total, B, 96000.0, plugin, s, out, mag, comm=comms[r], root=root,
+                                   all_out=all_out if r == root else None, all_mag=all_mag if r == root else None,
+                                   chunk=chunk, stream=st.cuda_stream)
+        st.synchronize()
+    _run_ranks(torch, world, rank_fn)
+    torch.cuda.synchronize()
+    for c in comms:
+        c.close()
+    assert torch.equal(all_out, ref_out), _where(torch, all_out, ref_out)
+    assert torch.equal(all_mag, ref_mag), _where(torch, all_mag, ref_mag)
+
+
+def _where(torch, got, ref):
+    """Which channels / rows differ, by how much, and whether unwritten (-7)."""
+    bad = (got != ref).reshape(got.shape[0], got.shape[1], -1).any(dim=-1)
+    lines = []
+    for c in range(got.shape[0]):
+        rows = torch.nonzero(bad[c]).flatten().tolist()
+        if rows:
+            d = (got[c] - ref[c]).abs().max().item()
+            unwritten = bool((got[c][rows[0]] == -7.0).any().item())
+            lines.append(f"ch {c}: {len(rows)} rows differ, first {rows[:6]}, max |diff| {d:.3g}, "
+                         f"unwritten {unwritten}")
+    return "; ".join(lines)
+
+
+def test_loopback_gather_and_errors(torch_cuda):
+    """dsp_comm_gather over the loopback (3 ranks, root 2); a count mismatch
+    between a send and its recv fails both sides instead of copying."""
+    torch = torch_cuda
+    world, n = 3, 50_001
+    comms = sh.loopback(world, 0)
+    srcs = [torch.arange(n, dtype=torch.float32, device="cuda") + 1000 * r for r in range(world)]
+    dst = [torch.zeros(n, device="cuda") for _ in range(world)]
+
+    def rank_fn(r):
+        st = torch.cuda.Stream()
+        comms[r].gather(srcs[r], dst if r == 2 else None, root=2, stream=st.cuda_stream)
+        st.synchronize()
+    _run_ranks(torch, world, rank_fn)
+    for r in range(world):
+        assert torch.equal(dst[r], srcs[r])
+
+    def bad_fn(r):
+        st = torch.cuda.Stream()
+        src = srcs[r][: n - (1 if r == 1 else 0)]
+        comms[r].gather(src, dst if r == 2 else None, root=2, stream=st.cuda_stream)
+    errs = []
+
+    def wrapped(r):
+        try:
+            bad_fn(r)
+        except d.DspError as e:
+            errs.append((r, str(e)))
+    _run_ranks(torch, world, wrapped)
+    assert sorted(r for r, _ in errs) == [1, 2], errs
+    for c in comms:
+        c.close()
+
+
 def _free_port():
     with socket.socket() as so:
         so.bind(("127.0.0.1", 0))
@@ -109,8 +230,9 @@ def _free_port():
 
 
 def _rehearsal_worker(rank, world, port, q):
-    """One rank of the N > 1 cfg 5 path on cuda:0: the product's plan, its GPU
-    render + fused STFT per chunk, the gather over gloo."""
+    """One rank of the N > 1 cfg 5 path on cuda:0, one process per rank: the
+    C++ sharded driver (plan, chunks, GPU render + fused STFT, gather
+    schedule) with gloo as its transport (dsp_comm_init_transport)."""
     import torch
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -128,8 +250,11 @@ def _rehearsal_worker(rank, world, port, q):
         mag = torch.empty((s.channels, s.frames, 4097), device="cuda")
         all_out = torch.zeros((C_total, nb * B), device="cuda") if rank == 0 else None
         all_mag = torch.zeros((C_total, s.frames, 4097), device="cuda") if rank == 0 else None
-        sh.render_stft_sharded(xl, L, C_total, B, 96000.0, plugin, s, out, mag, comm=sh.TorchComm(), root=0,
+        comm = sh.TorchComm(device=0)  # gloo as the transport of the C++ driver
+        sh.render_stft_sharded(xl, L, C_total, B, 96000.0, plugin, s, out, mag, comm=comm, root=0,
                                all_out=all_out, all_mag=all_mag, chunk=1 << 15)
+        torch.cuda.synchronize()
+        comm.close()
         if rank == 0:
             torch.cuda.synchronize()
             ref_out, ref_mag = d.render_stft(x, C_total, B, 96000.0, plugin, window=d.DSP_WIN_HANN)

@@ -94,12 +94,13 @@ def test_gloo_ranks_match_whole_file(B, world):
     assert ok_m, f"sharded STFT differs from the whole-file STFT {shape} vs {rshape}"
 
 
-# ---- the product's sharded driver with a torch.distributed transport -------
+# ---- the product's gather schedule, executed over gloo ----------------------
 
 def _sharded_worker(rank, world, port, mode, C_total, C_file, L, B, chunk, q):
-    """dspbench.shard.render_stft_sharded over gloo (TorchComm): the product's
-    plan (dsp_shard_plan), chunk schedule (dsp_shard_chunks) and gather
-    pieces, with the oracle standing in for the GPU render of each chunk."""
+    """The product's plan (dsp_shard_plan), chunk schedule (dsp_shard_chunks)
+    and gather schedule (dsp_shard_gather_plan, the pieces
+    dsp_render_stft_sharded moves) executed over gloo, with the oracle
+    standing in for the GPU render of each chunk."""
     import torch
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -110,36 +111,44 @@ def _sharded_worker(rank, world, port, mode, C_total, C_file, L, B, chunk, q):
         rng = np.random.default_rng(21)
         x = (rng.random((C_file, L), dtype=np.float32) * 2 - 1).astype(np.float32)
         s = sh.plan(L, world, rank, B, N, H, True, C_total, mode)
-        # this rank's file rows, local to the shard
-        rows = [c for c in range(s.chan0, s.chan0 + s.channels) if c < C_file]
-        xl = torch.from_numpy(np.ascontiguousarray(x[rows, s.start:s.start + s.read_len]))
         nb = -(-s.read_len // B)
-        out = torch.zeros((s.channels, nb * B))
-        mag = torch.zeros((s.channels, max(s.frames, 1), K))
+        out = np.zeros((s.channels, nb * B), np.float32)
+        mag = np.zeros((s.channels, max(s.frames, 1), K), np.float32)
         plug = o.restated_plugin("IR_test", [0.7, 0.003])
-
-        def compute(c, xo, oo, mo, goff):
-            fc = [xo[j].numpy() for j in range(xo.shape[0])] if xo is not None else []
-            Lc = oo.shape[1] if xo is None else xo.shape[1]
-            ren = o.render_offline(fc, s.channels, B, 48000.0, plug, L=Lc)
-            oo.copy_(torch.from_numpy(ren[:, :oo.shape[1]]))
+        for c in sh.chunks(s, L, B, N, H, True, chunk):  # this rank's compute, chunk by chunk
+            o_ = c.start - s.start
+            Lc = min(max(L - c.start, 0), c.owned + c.halo)
+            rows = [x[g, c.start:c.start + Lc] for g in range(s.chan0, s.chan0 + s.channels) if g < C_file]
+            ren = o.render_offline(rows, s.channels, B, 48000.0, plug, L=Lc)
+            out[:, o_:o_ + ren.shape[1]] = ren
             for j in range(s.channels):
-                m = o.np_stft_mag(ren[j], N, H, o.WIN_HANN, K)
-                mo[j].copy_(torch.from_numpy(m[: mo.shape[1]].astype(np.float32)))
-
+                m = o.np_stft_mag(ren[j], N, H, o.WIN_HANN, K)[: c.frames]
+                mag[j, c.frame0 - s.frame0:c.frame0 - s.frame0 + m.shape[0]] = m
+        pieces, steps = sh.gather_plan(L, C_total, world, B, N, H, mode, chunk, K)
         Lpad = -(-L // B) * B
         F = sh.stft_frames(Lpad, N, H)
-        all_out = torch.zeros((C_total, Lpad)) if rank == 0 else None
-        all_mag = torch.zeros((C_total, F, K)) if rank == 0 else None
-        sh.render_stft_sharded(xl if rows else None, L, C_total, B, 48000.0, None, s, out, mag,
-                               comm=sh.TorchComm(), root=0, all_out=all_out, all_mag=all_mag, chunk=chunk,
-                               compute=compute)
+        all_out = np.zeros((C_total, Lpad), np.float32)
+        all_mag = np.zeros((C_total, F * K), np.float32)
+        for p in pieces:  # in schedule order, as the driver moves them
+            if p.src == rank:
+                j = p.channel - s.chan0
+                row = out[j] if p.what == sh.PIECE_RENDER else mag[j].reshape(-1)
+                buf = torch.from_numpy(np.ascontiguousarray(row[p.src_off:p.src_off + p.count]))
+            dst = (all_out if p.what == sh.PIECE_RENDER else all_mag)[p.channel]
+            if p.src == 0 and rank == 0:
+                dst[p.dst_off:p.dst_off + p.count] = buf.numpy()
+            elif rank == 0:
+                t = torch.empty(p.count)
+                dist.recv(t, src=p.src)
+                dst[p.dst_off:p.dst_off + p.count] = t.numpy()
+            elif p.src == rank:
+                dist.send(buf, dst=0)
         if rank == 0:
             ref = o.render_offline([x[c] for c in range(C_file)], C_total, B, 48000.0, plug)
-            ok_r = np.array_equal(all_out.numpy(), ref)
+            ok_r = np.array_equal(all_out, ref)
             mref = np.stack([o.np_stft_mag(ref[c], N, H, o.WIN_HANN, K) for c in range(C_total)]).astype(np.float32)
-            ok_m = np.array_equal(all_mag.numpy(), mref)
-            q.put((ok_r, ok_m))
+            ok_m = np.array_equal(all_mag.reshape(C_total, F, K), mref)
+            q.put((ok_r, ok_m, steps))
     finally:
         dist.destroy_process_group()
 
@@ -159,12 +168,42 @@ def test_gloo_sharded_driver_reassembles_the_whole_file(mode, C_total, C_file, B
              for r in range(world)]
     for p in procs:
         p.start()
-    ok_r, ok_m = q.get(timeout=300)
+    ok_r, ok_m, steps = q.get(timeout=300)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
     assert ok_r, "gathered render differs from the whole-file render"
     assert ok_m, "gathered STFT differs from the whole-file STFT"
+
+
+@pytest.mark.parametrize("mode,C_total,world,B,chunk", [
+    (sh.CHANNELS, 8, 8, 512, 1 << 16), (sh.CHANNELS, 8, 3, 512, 0), (sh.CHANNELS, 3, 4, 384, 49152),
+    (sh.TIME, 2, 4, 512, 36864), (sh.TIME, 2, 3, 384, 0), (sh.TIME, 1, 2, 1, 12288), (sh.TIME, 2, 1, 512, 20000),
+])
+def test_gather_plan_covers_every_row_once(mode, C_total, world, B, chunk):
+    """dsp_shard_gather_plan: the pieces cover every render sample of the
+    block-padded file and every magnitude row of every channel exactly once,
+    read inside each sender's local rows, in (step, src) order."""
+    N, H, K = 8192, 4096, 4097
+    for L in [0, 8191, 8192 * 3 + 5, 4 * 49152 + 777, 300_000]:
+        pieces, steps = sh.gather_plan(L, C_total, world, B, N, H, mode, chunk, K)
+        Lpad = -(-L // B) * B
+        F = sh.stft_frames(Lpad, N, H)
+        ren = np.zeros((C_total, Lpad), np.int32)
+        mg = np.zeros((C_total, F * K), np.int32)
+        plans = [sh.plan(L, world, r, B, N, H, True, C_total, mode) for r in range(world)]
+        assert [(p.step, p.src) for p in pieces] == sorted((p.step, p.src) for p in pieces)
+        for p in pieces:
+            assert p.step < steps and p.count > 0
+            s = plans[p.src]
+            assert s.chan0 <= p.channel < s.chan0 + s.channels
+            if p.what == sh.PIECE_RENDER:
+                assert p.src_off + p.count <= -(-s.read_len // B) * B
+                ren[p.channel, p.dst_off:p.dst_off + p.count] += 1
+            else:
+                assert p.src_off + p.count <= s.frames * K and p.count % K == 0
+                mg[p.channel, p.dst_off:p.dst_off + p.count] += 1
+        assert (ren == 1).all() and (mg == 1).all(), (L, ren.min(), ren.max(), mg.min() if mg.size else None)
 
 
 def test_channel_plan_and_chunks():
