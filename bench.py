@@ -15,13 +15,14 @@ is already resident in HBM:
 
 Multi-GPU (launched by torch.distributed.run): the file is N hours long and
 every rank renders its own hour (time-chunk sharding with an N - H = 4096
-sample halo) -- no data-path collective, weak scaling.  With
---gather one more pass runs the product's pipelined sharded driver with the
-gather of every rank's render and spectra to rank 0 over RCCL (xGMI), timed
-separately ("render_gather_ms"), outside `value`.
+sample halo) -- no data-path collective, weak scaling.  At
+N > 1 one more pass then runs the product's pipelined sharded driver
+(dsp_render_stft_sharded) with the gather of every rank's render and spectra
+to rank 0 over RCCL (xGMI), timed separately ("render_gather_ms", the
+north_star's "final RCCL gather"), outside `value` (--no-gather skips it).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--minutes M]
-                       [--no-cpu-baseline] [--gather]
+                       [--no-cpu-baseline] [--no-gather]
 """
 from __future__ import annotations
 
@@ -54,7 +55,8 @@ def parse():
     ap.add_argument("--minutes", type=float, default=60.0, help="audio per GPU (default 1 h)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
-    ap.add_argument("--gather", action="store_true", help="also time an RCCL gather to rank 0")
+    ap.add_argument("--no-gather", action="store_true",
+                    help="N > 1: skip the timed pass of the sharded driver with the RCCL gather to rank 0")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (host WAV -> host spectra) pass")
     ap.add_argument("--launch-events", action="store_true",
                     help="one-kernel workloads: bracket every launch with the library's HIP events inside the "
@@ -80,19 +82,32 @@ def parse():
     return ap.parse_args()
 
 
-def pmc_traffic(workload: str, kernel: str, src: int):
-    """HBM bytes per launch of `kernel` from the committed PMC summary of the
-    same bench command (tools/pmc.sh + tools/pmc_summary.py --json, FETCH_SIZE
-    x2 + WRITE_SIZE per MI355X_MICROARCH.md), or (None, None)."""
+# the instantiation each workload's dominant launch runs (stft_pk.hip /
+# stft_pk_paths.hip: <SRC, KM, MapKind, POW2, WINC, PER, OPT, OCC>); a PMC
+# summary counts only when it profiled this exact kernel
+PK_INST = {
+    "headline": "stft8192_pk_kernel<1, 0, (dspb::MapKind)3, true, true, 4, 65543, 2>",
+    "ch96k": "stft8192_pk_kernel<1, 0, (dspb::MapKind)3, true, true, 4, 65543, 2>",
+    "gain_stft": "stft8192_pk_kernel<1, 0, (dspb::MapKind)1, true, true, 0, 7, 2>",
+    "stft96k": "stft8192_pk_kernel<0, 0, (dspb::MapKind)0, true, true, 0, 7, 2>",
+}
+
+
+def pmc_traffic(workload: str):
+    """HBM bytes per launch of the workload's kernel instantiation from the
+    newest committed PMC summary of the same bench command (rocprofv3 --pmc
+    FETCH_SIZE / WRITE_SIZE in separate passes, tools/pmc_summary.py --json:
+    FETCH_SIZE x2 + WRITE_SIZE per MI355X_MICROARCH.md), or (None, None, None)."""
     import glob
-    paths = sorted(glob.glob(os.path.join(REPO, "profiles", f"r*_pmc_{workload}.json")))
-    if not paths:
-        return None, None
-    doc = json.load(open(paths[-1]))
-    for name, m in doc.get("kernels", {}).items():
-        if f"{kernel}<{src}," in name and "hbm_bytes" in m:
-            return float(m["hbm_bytes"]), os.path.relpath(paths[-1], REPO)
-    return None, None
+    inst = PK_INST.get(workload)
+    if inst is None:
+        return None, None, None
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", f"r*_pmc_{workload}.json")), reverse=True):
+        doc = json.load(open(path))
+        for name, m in doc.get("kernels", {}).items():
+            if name.endswith(inst) and "hbm_bytes" in m:
+                return float(m["hbm_bytes"]), os.path.relpath(path, REPO), inst
+    return None, None, inst
 
 
 def cpu_baseline_generic(seconds_budget: float):
@@ -515,12 +530,13 @@ def main():
         bytes_per_launch = alg_bytes
     achieved = bytes_per_launch / (kernel_avg_ms / 1e3) / 1e9 if kernel_avg_ms > 0 else 0.0
 
-    # --gather: one more pass through the product's pipelined sharded driver
+    # N > 1: one more pass through the product's pipelined sharded driver
     # with the gather to rank 0 (RCCL over xGMI inside libdspbench; the
-    # one-GPU rehearsal uses gloo), timed on its own, outside `value`
+    # one-GPU rehearsal uses gloo as the transport), timed on its own,
+    # outside `value`
     gather_ms = None
-    if args.gather and world > 1 and wl in ("headline", "ch96k"):
-        comm = d.shard.TorchComm() if rehearsal else d.shard.RcclComm.from_torch(device=local)
+    if not args.no_gather and world > 1 and wl in ("headline", "ch96k"):
+        comm = d.shard.TorchComm(device=local) if rehearsal else d.shard.RcclComm.from_torch(device=local)
         Ctot = world if wl == "ch96k" else CH
         Lfile = L if wl == "ch96k" else world * L
         Lpad = d.num_blocks(Lfile, B) * B
@@ -536,6 +552,7 @@ def main():
         torch.cuda.synchronize()
         dist.barrier()
         gather_ms = (time.perf_counter() - tg) * 1e3
+        comm.close()
         del all_out, all_mag
 
     # end to end: the same hour as a 16-bit PCM WAV payload in
@@ -565,12 +582,13 @@ def main():
                "host_link_gb_s": round(pcie, 1),
                "path": "16-bit stereo WAV payload in pinned host memory -> dsp_render_stft_wav (8 Mi-sample "
                        "chunks: H2D, GPU decode, fused IR_test render + STFT, D2H of render + 4097-bin spectra "
-                       "into pinned host rows), best of 2 after a first call"}
+                       "into pinned host rows on an SDMA engine), best of 2 after a first call",
+            "d2h_bound_ms": round((h_out.numel() + h_mag.numel()) * 4 / 57e9 * 1e3, 1),
+            "d2h_bound": "the downloads alone at the 57 GB/s one SDMA engine moves device -> host "
+                         "(profiles/r03_d2h_probe.txt)"}
         del pay, h_out, h_mag
 
-    traffic, traffic_src = (None, None)
-    if wl in ("headline", "stft96k", "gain_stft"):
-        traffic, traffic_src = pmc_traffic(wl, KERNEL, 0 if wl == "stft96k" else 1)
+    traffic, traffic_src, traffic_inst = pmc_traffic(wl)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and wl == "headline":
@@ -605,7 +623,8 @@ def main():
                              "time-chunk per GPU, 4096-sample halo, no data-path collective"),
                 "render_gather_ms": None if gather_ms is None else round(gather_ms, 3),
                 "render_gather": ("one pass of the product's pipelined sharded driver with the gather of every "
-                                  "rank's render and spectra to rank 0 (dsp_render_stft_sharded over RCCL)"
+                                  "rank's render and spectra to rank 0 (dsp_render_stft_sharded over "
+                                  + ("gloo, the one-GPU rehearsal)" if rehearsal else "RCCL / xGMI)")
                                   if gather_ms is not None else None),
                 "first_call_ms": round(first_call_ms, 4),
                 "end_to_end": e2e,
@@ -633,6 +652,9 @@ def main():
                 "traffic": None if traffic is None else round(traffic / 1e9, 4),
                 "traffic_unit": "GB per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
                 "traffic_source": traffic_src,
+                "traffic_kernel": traffic_inst if traffic is not None else None,
+                "traffic_over_algorithmic": (round(traffic / bytes_per_launch, 5)
+                                             if traffic is not None and bytes_per_launch else None),
                 "kernel_avg_ms": round(kernel_avg_ms, 5),
                 "kernel_avg_source": ("HIP events on the launch stream around the timed region / steps (one "
                                       "kernel launch per step)" if region_timed or (k_n.value == 0 and alg_bytes)

@@ -18,7 +18,11 @@
 // whole-file call bit for bit.  Plugins with state, and the FIR, run as one
 // chunk.  Host buffers that are pinned (hipHostMalloc / hipHostRegister) are
 // DMA'd directly; pageable ones go through pinned staging slots, copied by
-// the calling thread while the GPU works on the other slot.
+// the calling thread while the GPU works on the other slot.  Downloads into
+// HSA-allocated pinned memory run on an SDMA engine (sdma.hpp: the HIP
+// runtime a PyTorch process uses would run them as blit kernels on the CUs,
+// stalling the next chunk's kernel behind them); others go through
+// hipMemcpyAsync on the down stream.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -27,6 +31,7 @@
 
 #include "dspbench/shard.h"
 #include "dspbench/wav.h"
+#include "sdma.hpp"
 
 namespace dspb {
 void set_last_error(const char *fmt, ...);
@@ -78,6 +83,8 @@ struct Slot {
 };
 
 struct Resources {
+    dspb::SdmaDownloader dl;        // SDMA downloads (when used): stopped first
+    bool use_sdma = false;
     std::vector<Slot> slots;
     hipStream_t up = nullptr, down = nullptr;
     hipStream_t compute = nullptr;  // the caller's stream (not owned)
@@ -86,6 +93,7 @@ struct Resources {
     ~Resources() {
         // an early return leaves copies and kernels in flight on the slots'
         // buffers: drain them before the buffers go
+        (void)dl.finish();
         if (up) (void)hipStreamSynchronize(up);
         if (compute_used) (void)hipStreamSynchronize(compute);
         if (down) (void)hipStreamSynchronize(down);
@@ -186,10 +194,31 @@ int run(const Source &src, uint32_t C, uint32_t B, float sr, const dsp_plugin *p
         PL_HIP(hipEventCreateWithFlags(&s.comp_done, hipEventDisableTiming));
         PL_HIP(hipEventCreateWithFlags(&s.down_done, hipEventDisableTiming));
     }
+    // downloads on an SDMA engine when every destination allows it
+    {
+        int cur = -1;
+        PL_HIP(hipGetDevice(&cur));
+        bool ok = true;
+        for (uint32_t c = 0; c < C && ok; ++c) {
+            ok = dspb::SdmaDownloader::usable(cur, out_pinned ? (const void *)out[c] : R.slots[0].h_out);
+            if (ok && stft) ok = dspb::SdmaDownloader::usable(cur, out_pinned ? (const void *)mag[c] : R.slots[0].h_mag);
+        }
+        if (ok && !out_pinned)
+            for (const Slot &sl : R.slots)
+                ok = ok && dspb::SdmaDownloader::usable(cur, sl.h_out) && (!stft || dspb::SdmaDownloader::usable(cur, sl.h_mag));
+        R.use_sdma = ok;
+        if (ok && (st = R.dl.start(cur, (int)R.slots.size()))) return st;
+    }
+    // a slot's downloads have landed
+    auto landed = [&](Slot &s) -> int {
+        if (R.use_sdma) return R.dl.wait_slot((int)(&s - R.slots.data()));
+        PL_HIP(hipEventSynchronize(s.down_done));
+        return DSP_OK;
+    };
     // copy a finished download out of the pinned staging slot
     auto drain = [&](Slot &s) -> int {
         if (!s.pending_down) return DSP_OK;
-        PL_HIP(hipEventSynchronize(s.down_done));
+        if (int e = landed(s)) return e;
         for (uint32_t c = 0; c < C; ++c) {
             std::memcpy(out[c] + s.t_start, s.h_out + (uint64_t)c * max_pad, s.t_rlen * sizeof(float));
             if (stft && s.t_frames)
@@ -206,7 +235,7 @@ int run(const Source &src, uint32_t C, uint32_t B, float sr, const dsp_plugin *p
         // the slot's previous chunk: its upload buffer and device rows are
         // free once its download finished
         if ((st = drain(s))) return st;
-        PL_HIP(hipEventSynchronize(s.down_done));
+        if ((st = landed(s))) return st;
         // ---- upload
         if (Cin) {
             if (src.wav()) {
@@ -266,25 +295,33 @@ int run(const Source &src, uint32_t C, uint32_t B, float sr, const dsp_plugin *p
         if (st) return st;
         PL_HIP(hipEventRecord(s.comp_done, cs));
         // ---- download the owned rows
-        PL_HIP(hipStreamWaitEvent(R.down, s.comp_done, 0));
         const uint64_t rlen = (c.start + c.owned >= L) ? Lpad - c.start : c.owned;
         s.t_start = c.start;
         s.t_rlen = rlen;
         s.t_frame0 = c.frame0;
         s.t_frames = stft ? c.frames : 0;
+        std::vector<dspb::HostCopy> copies;
         for (uint32_t j = 0; j < C; ++j) {
             float *dst = out_pinned ? out[j] + c.start : s.h_out + (uint64_t)j * max_pad;
-            PL_HIP(hipMemcpyAsync(dst, rout[j], rlen * sizeof(float), hipMemcpyDeviceToHost, R.down));
+            copies.push_back({dst, rout[j], rlen * sizeof(float)});
             if (stft && c.frames) {
                 float *md = out_pinned ? mag[j] + c.frame0 * ld : s.h_mag + (uint64_t)j * max_fr * ld;
-                PL_HIP(hipMemcpyAsync(md, rmag[j], c.frames * ld * sizeof(float), hipMemcpyDeviceToHost, R.down));
+                copies.push_back({md, rmag[j], c.frames * ld * sizeof(float)});
             }
         }
-        PL_HIP(hipEventRecord(s.down_done, R.down));
+        if (R.use_sdma) {
+            if ((st = R.dl.submit((int)(t % (int64_t)R.slots.size()), s.comp_done, std::move(copies)))) return st;
+        } else {
+            PL_HIP(hipStreamWaitEvent(R.down, s.comp_done, 0));
+            for (const dspb::HostCopy &hc : copies)
+                PL_HIP(hipMemcpyAsync(hc.dst, hc.src, hc.bytes, hipMemcpyDeviceToHost, R.down));
+            PL_HIP(hipEventRecord(s.down_done, R.down));
+        }
         s.pending_down = !out_pinned;
     }
     for (Slot &s : R.slots)
-        if ((st = drain(s))) return st;
+        if ((st = drain(s)) || (st = landed(s))) return st;
+    if ((st = R.dl.finish())) return st;
     PL_HIP(hipStreamSynchronize(R.down));
     PL_HIP(hipStreamSynchronize(cs));
     return DSP_OK;

@@ -99,6 +99,11 @@ int main(int argc, char **argv) {
     uint32_t pref = 0;
     (void)hsa_amd_memory_get_preferred_copy_engine(g_cpu, g_gpu, &pref);
     printf("SDMA engines free for D2H: mask 0x%x, preferred 0x%x\n", mask, pref);
+    uint32_t mask_up = 0, pref_up = 0;
+    (void)hsa_amd_memory_copy_engine_status(g_gpu, g_cpu, &mask_up);
+    (void)hsa_amd_memory_get_preferred_copy_engine(g_gpu, g_cpu, &pref_up);
+    printf("SDMA engines free for H2D: mask 0x%x, preferred 0x%x\n", mask_up, pref_up);
+    if (argc > 2) return 0;  // masks only
     hsa_amd_sdma_engine_id_t eng = (hsa_amd_sdma_engine_id_t)(pref & mask ? (pref & mask & -(pref & mask)) : (mask & -mask));
     hsa_signal_t sig;
     HK(hsa_signal_create(1, 0, nullptr, &sig));

@@ -13,10 +13,25 @@ import sys
 root = sys.argv[1]
 js = sys.argv[sys.argv.index("--json") + 1] if "--json" in sys.argv else None
 summary = {}
+
+
+def kname(n):
+    """The kernel's name with its full template argument list (the
+    instantiation), without the parameter list."""
+    n = n.strip()
+    if n.endswith(")"):
+        depth = 0
+        for i in range(len(n) - 1, -1, -1):
+            depth += n[i] == ")"
+            depth -= n[i] == "("
+            if depth == 0:
+                return n[:i]
+    return n
+
 agg = collections.defaultdict(lambda: collections.defaultdict(list))
 for p in sorted(glob.glob(f"{root}/p*/run_counter_collection.csv")):
     for r in csv.DictReader(open(p)):
-        agg[r["Kernel_Name"][:70]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        agg[kname(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, d in agg.items():
     m = {c: sum(v) / len(v) for c, v in d.items()}
     print(k)
