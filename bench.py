@@ -79,6 +79,9 @@ def parse():
                          "planar stereo into an interleaved int16 / int24 WAV payload")
     ap.add_argument("--plugin", default=None, choices=["gain_test", "IR_test"],
                     help="generic / generic_stft: the reference plugin source (default gain_test / IR_test)")
+    ap.add_argument("--no-specialize", action="store_true",
+                    help="generic / generic_stft: run the plugin's callback on every block "
+                         "(DSP_EXEC_NO_SPECIALIZE) instead of its probed block class")
     return ap.parse_args()
 
 
@@ -331,6 +334,7 @@ def main():
     alg_desc = ("fused: C*F*(4H + 4K) B (render write + |X| write; IR_test reads no input); "
                 "memory: C*F*(4H + 4K) B (each sample read once + |X| write)")
     plug_name = plugin.name
+    block_class = None
     if wl == "headline":
         def step():
             d.render_stft(x, CH, B, float(sr), plugin, N=N_FFT, H=HOP, window=d.DSP_WIN_HANN,
@@ -399,25 +403,37 @@ def main():
             gmod = d.module.Module(f.read())
         gparams = gmod.default_parameters()
         gmod.initialize_state(gparams, CH, float(sr))
-        gplug = gmod.plugin(gparams, pname)
-        plug_name = f"{pname}.cpp (DSP_PLUGIN_GENERIC, compiled unchanged from the reference source)"
+        gplug = gmod.plugin(gparams, pname, specialize=not args.no_specialize)
+        block_class = "callback" if args.no_specialize else gmod.block_class(gparams, CH, B, float(sr))[0]
+        plug_name = (f"{pname}.cpp (DSP_PLUGIN_GENERIC, compiled unchanged from the reference source; block class "
+                     f"{block_class}: " + {"table": "its own callback's block, tiled, in the fused kernel",
+                                           "gain": "the gain its callback gives, in the gain map",
+                                           "callback": "the callback on every block"}[block_class] + ")")
         if wl == "generic":
             def step():
                 d.render_offline(x, CH, B, float(sr), gplug, out=out)
             workload = (f"{pname}.cpp via the generic plugin driver (B=512), {minutes:g} min of 48 kHz "
                         "stereo per GPU")
-            kname = "dspb_render_lds (generic driver, hiprtc module)"
-            alg_desc = "C*L*(4 + 4) B (read + write)"
+            kname = ("dspb_render_lds (generic driver, hiprtc module)" if block_class == "callback" else
+                     "render_vec_kernel (the plugin's block class)")
+            alg_desc = "C*L*(4 + 4) B (read + write)" if block_class != "table" else "C*L*4 B (write)"
         else:
             def step():
                 d.render_stft(x, CH, B, float(sr), gplug, N=N_FFT, H=HOP, window=d.DSP_WIN_HANN,
                               K=K_BINS, out=out, mag=mag)
             workload = (f"{pname}.cpp via the generic plugin driver (B=512) + 8192-pt Hann STFT, hop 4096, "
                         f"4097 bins, {minutes:g} min of 48 kHz stereo per GPU")
-            kname = ("dspb_render_lds (generic driver) then stft8192_pk<memory> on one stream (one timed "
-                     "region, dsp_render_stft)")
-            alg_desc = ("C*L*(4 + 4) + C*F*4K B (file read + render write + |X| write; the STFT's re-read of "
-                        "the render is extra traffic, not counted)")
+            if block_class == "callback":
+                kname = ("dspb_render_lds (generic driver) then stft8192_pk<memory> on one stream (one timed "
+                         "region, dsp_render_stft)")
+                alg_desc = ("C*L*(4 + 4) + C*F*4K B (file read + render write + |X| write; the STFT's re-read of "
+                            "the render is extra traffic, not counted)")
+            else:
+                kname = (f"{KERNEL}<render> (fused render + window + FFT + |X|; the render is the plugin's own "
+                         f"{'callback block, tiled' if block_class == 'table' else 'gain'})")
+                alg_desc = ("fused: C*F*(4H + 4K) B (render write + |X| write; the plugin ignores its input)"
+                            if block_class == "table" else
+                            "fused gain: C*F*(4H + 4H + 4K) B (file read + render write + |X| write)")
     elif wl in ("wav16enc", "wav24enc"):
         # SURVEY 8(f) row 1, the writer: planar float -> interleaved PCM
         # (interleave + convert, audio.h:123-133; round half to even, clip)
@@ -458,7 +474,8 @@ def main():
     torch.cuda.synchronize()
     # one kernel per step: the timed region's own stream events give its
     # average launch duration, and no per-launch events sit between launches
-    region_timed = wl in ("headline", "ch96k", "gain_stft", "stft96k") and not args.launch_events
+    region_timed = (wl in ("headline", "ch96k", "gain_stft", "stft96k") or
+                    (wl == "generic_stft" and block_class != "callback")) and not args.launch_events
     bytes_probe = 0
     if region_timed:  # the library's byte count of one launch, from the first call
         d.lib().dsp_kernel_timing(None, None, None)
@@ -616,6 +633,7 @@ def main():
             "config": {
                 "workload": workload,
                 "plugin": plug_name,
+                "block_class": block_class,
                 "samples_per_gpu": samples_per_rank,
                 "frames_per_gpu": CH * F if mag is not None else 0,
                 "sharding": ("one 96 kHz channel per GPU (a world-channel file, dsp_shard_plan CHANNELS, "
@@ -666,10 +684,14 @@ def main():
                             "(2.38 GHz without its stores); profiles/r01_power_ablation"
                             if wl in ("headline", "ch96k", "gain_stft") else
                             "one lane per block: the plugin callback runs serially over its block in LDS, "
-                            "16 blocks per 64 KB workgroup round (DESIGN 4.6)" if wl == "generic" else
+                            "16 blocks per 64 KB workgroup round (DESIGN 4.6)"
+                            if wl == "generic" and block_class == "callback" else
+                            "the read + write stream (render_vec_kernel)" if wl == "generic" else
                             "the render (LDS-capacity-bound callbacks) then the power-capped memory STFT, "
                             "serial: DESIGN 4.6, profiles/r02_generic_stft_schedules.txt"
-                            if wl == "generic_stft" else None),
+                            if wl == "generic_stft" and block_class == "callback" else
+                            "package power, as the headline (the same fused kernel)" if wl == "generic_stft"
+                            else None),
             }),
             "cpu_baseline": cpu,
         }

@@ -522,6 +522,24 @@ static int plugin_map(const dsp_plugin *p, uint32_t B, int dev, hipStream_t s, S
     }
 }
 
+// A GENERIC plugin with a known block class (module.h dsp_module_block_class)
+// runs as that map: its own callback's block as a table, or its gain
+static int specialize_generic(SampleMap *m, uint32_t C, uint32_t B, hipStream_t s, const dsp_exec *ex) {
+    if (m->kind != MapKind::Generic || (ex && (ex->flags & DSP_EXEC_NO_SPECIALIZE))) return DSP_OK;
+    ModuleSpec sp;
+    int st = module_specialize((::dsp_module *)m->module, m->gparams, m->gparams_size, C, B, m->sr, s, &sp);
+    if (st) return st;
+    if (sp.kind == kSpecTable) {
+        m->kind = MapKind::Ramp;  // value = table[(global sample) mod B]
+        m->table = sp.table;
+        m->closed = 0;
+    } else if (sp.kind == kSpecGain) {
+        m->kind = MapKind::Gain;
+        m->a = sp.gain;
+    }
+    return DSP_OK;
+}
+
 // ---------------------------------------------------------------------------
 // host-buffer staging (DSP_EXEC_HOST_BUFFERS)
 // ---------------------------------------------------------------------------
@@ -842,6 +860,7 @@ int dsp_render_offline(const float *const *in, uint32_t in_channels, uint64_t L,
     SampleMap map;
     int st = plugin_map(plugin, B, g.dev, s, &map, sr, ex ? ex->flags : 0);
     if (st) return st;
+    if ((st = specialize_generic(&map, C, B, s, ex))) return st;
     TimedLaunch tl{};
     if ((st = timing_begin(s, &tl))) return st;
     st = render_device(din.data(), in_channels, L, dout.data(), C, B, map, 0, goff_of(ex), s);
@@ -1002,6 +1021,7 @@ int dsp_render_stft(const float *const *in, uint32_t in_channels, uint64_t L,
     }
     SampleMap map;
     if ((st = plugin_map(plugin, B, g.dev, s, &map, sr, ex ? ex->flags : 0))) return st;
+    if ((st = specialize_generic(&map, C, B, s, ex))) return st;
     const uint64_t goff = goff_of(ex);
 
     bool fused = (N == 8192) && (H % 128 == 0) && (H <= N) && (goff % 2 == 0) && F > 0 &&

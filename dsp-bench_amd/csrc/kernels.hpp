@@ -71,6 +71,16 @@ int module_render(::dsp_module *m, const void *params, uint32_t params_size, con
                   uint64_t goff, hipStream_t s);
 int module_ir(::dsp_module *m, const void *params, uint32_t params_size, float *const *bufs, uint32_t C,
               uint32_t n, float sr, hipStream_t s);
+// a stateless plugin's block class for (Parameters, C, B, sr), probed once
+// through its own callback and cached in the module (module.cpp)
+enum { kSpecNone = 0, kSpecTable = 1, kSpecGain = 2 };
+struct ModuleSpec {
+    int kind = kSpecNone;
+    float gain = 1.f;             // kSpecGain: y = gain x
+    const float *table = nullptr; // kSpecTable: the block every block renders (B floats, every channel)
+};
+int module_specialize(::dsp_module *m, const void *params, uint32_t params_size, uint32_t C, uint32_t B, float sr,
+                      hipStream_t s, ModuleSpec *out);
 struct FirFftArgs {
     ChanIn in;           // input channels
     uint32_t in_ch;

@@ -525,6 +525,15 @@ struct dsp_module {
     ArenaHost *d_arena[2] = {nullptr, nullptr};
     char *arena_mem[2] = {nullptr, nullptr};
     bool initialized = false;
+    // block classes found by module_specialize, per (Parameters, C, B, sr);
+    // newest last, at most kSpecCache
+    struct Spec {
+        std::vector<unsigned char> params;
+        uint32_t C, B;
+        float sr;
+        dspb::ModuleSpec r;
+    };
+    std::vector<Spec> spec;
     std::mutex mu;
 };
 
@@ -758,6 +767,8 @@ void dsp_module_destroy(dsp_module *m) {
             if (m->arena_mem[i]) (void)hipFree(m->arena_mem[i]);
         }
         if (m->d_params) (void)hipFree(m->d_params);
+        for (auto &e : m->spec)
+            if (e.r.table) (void)hipFree(const_cast<float *>(e.r.table));
         for (hipEvent_t e : {m->upload_ev, m->use_ev})
             if (e) {
                 (void)hipEventSynchronize(e);
@@ -769,6 +780,25 @@ void dsp_module_destroy(dsp_module *m) {
     }
     delete m->desc;
     delete m;
+}
+
+int dsp_module_block_class(dsp_module *m, const void *params, uint32_t params_size, uint32_t C, uint32_t B,
+                           float sr, int32_t *block_class, float *gain, const dsp_exec *ex) {
+    if (!m || !block_class) {
+        set_last_error("dsp_module_block_class: NULL argument");
+        return DSP_ERR_INVALID;
+    }
+    int prev = -1;
+    if (int st = with_device(ex && ex->device >= 0 ? ex->device : m->device, &prev)) return st;
+    dspb::ModuleSpec r;
+    const int st = dspb::module_specialize(m, params, params_size, C, B, sr, ex ? (hipStream_t)ex->stream : nullptr, &r);
+    int cur = -1;
+    if (hipGetDevice(&cur) == hipSuccess && prev >= 0 && prev != cur) (void)hipSetDevice(prev);
+    if (st) return st;
+    *block_class = r.kind == dspb::kSpecTable ? DSP_BLOCK_TABLE : r.kind == dspb::kSpecGain ? DSP_BLOCK_GAIN
+                                                                                              : DSP_BLOCK_CALLBACK;
+    if (gain) *gain = r.gain;
+    return DSP_OK;
 }
 
 int dsp_module_sizes(const dsp_module *m, uint32_t *params_size, uint32_t *state_size, int *stateless) {
@@ -1171,6 +1201,113 @@ int module_ir(dsp_module *m, const void *params, uint32_t params_size, float *co
     MOD_HIP(hipModuleLaunchKernel(m->f_callback, 1, 1, 1, 1, 1, 1, 0, s, args, nullptr));
     if (!m->use_ev) MOD_HIP(hipEventCreateWithFlags(&m->use_ev, hipEventDisableTiming));
     MOD_HIP(hipEventRecord(m->use_ev, s));
+    return DSP_OK;
+}
+
+
+// ---------------------------------------------------------------------------
+// Block classes of a stateless plugin (kernels.hpp ModuleSpec).  A plugin
+// with an empty State computes each block as f(Parameters, block, C, B, sr):
+// it cannot see the block's position, so if f ignores the block's samples
+// every block renders the same output, and if f is y = g x per sample it is
+// the gain map.  The plugin's own callback is run on kProbes probe blocks
+// (zeros; uniform in [-1, 1] with x = 1 at each channel's first sample;
+// uniform in [-1000, 1000]; small signed steps with a -0) and the outputs
+// are compared bit for bit:
+//   TABLE  every probe renders the same block, the same on every channel:
+//          the render is that block (computed by the callback) tiled, and the
+//          fused kernels read it as a block table (MapKind::Ramp);
+//   GAIN   every output is fl(g x) for the g the callback gives x = 1
+//          (MapKind::Gain, a = g).
+// This is probing, not proof: a plugin whose input dependence none of the
+// probes exposes would be misclassified; DSP_EXEC_NO_SPECIALIZE runs the
+// callback on every block instead.
+constexpr int kProbes = 4;
+constexpr uint32_t kSpecMaxB = 1u << 16;
+constexpr size_t kSpecCache = 4;
+
+static uint32_t xorshift(uint32_t &x) {
+    x ^= x << 13;
+    x ^= x >> 17;
+    x ^= x << 5;
+    return x;
+}
+
+static bool same_bits(float a, float b) { return std::memcmp(&a, &b, 4) == 0; }
+
+int module_specialize(dsp_module *m, const void *params, uint32_t params_size, uint32_t C, uint32_t B, float sr,
+                      hipStream_t s, ModuleSpec *out) {
+    *out = ModuleSpec{};
+    if (!m || !m->initialized || !m->stateless || C == 0 || C > (uint32_t)kMaxChannels || B == 0 || B > kSpecMaxB)
+        return DSP_OK;
+    if (params_size != m->params_size || (!params && params_size)) return DSP_OK;  // module_render reports it
+    if (int st = check_device(m)) return st;
+    std::lock_guard<std::mutex> lk(m->mu);
+    for (const auto &e : m->spec)
+        if (e.C == C && e.B == B && same_bits(e.sr, sr) && e.params.size() == params_size &&
+            (!params_size || std::memcmp(e.params.data(), params, params_size) == 0)) {
+            *out = e.r;
+            return DSP_OK;
+        }
+    if (int st = refuse_capture(s)) return st;  // probing allocates and synchronises
+    if (int st = upload_params(m, params, params_size, s)) return st;
+    const uint64_t n = (uint64_t)C * B;
+    std::vector<float> h((size_t)(kProbes * n), 0.f);
+    uint32_t seed = 0x9e3779b9u;
+    for (uint64_t i = 0; i < n; ++i) {
+        h[n + i] = (float)((int32_t)xorshift(seed)) * (1.0f / 2147483648.0f);
+        h[2 * n + i] = (float)((int32_t)xorshift(seed)) * (1000.0f / 2147483648.0f);
+        h[3 * n + i] = (float)((int)(i % 13) - 6) * 0.125f;
+    }
+    for (uint32_t c = 0; c < C; ++c) h[n + (uint64_t)c * B] = 1.0f;
+    h[3 * n + (B > 1 ? 1 : 0)] = -0.0f;
+    float *d = nullptr;
+    MOD_HIP(hipMalloc(&d, sizeof(float) * h.size()));
+    struct Free {
+        float **p;
+        ~Free() { if (*p) (void)hipFree(*p); }
+    } fr{&d};
+    MOD_HIP(hipMemcpyAsync(d, h.data(), sizeof(float) * h.size(), hipMemcpyHostToDevice, s));
+    for (int p = 0; p < kProbes; ++p) {
+        RenderArgsG A{};
+        A.P = m->d_params;
+        A.S = m->d_state[0];
+        for (uint32_t c = 0; c < C; ++c) A.out[c] = d + (uint64_t)(p * C + c) * B;
+        A.C = C;
+        A.B = B;
+        A.sr = sr;
+        void *args[] = {&A};
+        MOD_HIP(hipModuleLaunchKernel(m->f_callback, 1, 1, 1, 1, 1, 1, 0, s, args, nullptr));
+    }
+    MOD_HIP(hipEventRecord(m->use_ev, s));
+    std::vector<float> r(h.size());
+    MOD_HIP(hipMemcpyAsync(r.data(), d, sizeof(float) * r.size(), hipMemcpyDeviceToHost, s));
+    MOD_HIP(hipStreamSynchronize(s));
+    ModuleSpec res{};
+    bool table = true;
+    for (uint64_t i = 0; i < kProbes * n && table; ++i) table = same_bits(r[i], r[i % B]);
+    const float g = r[n];  // the callback's output for x = 1
+    bool gain = !table && std::isfinite(g);
+    for (uint64_t i = 0; i < kProbes * n && gain; ++i) gain = same_bits(r[i], h[i] * g);
+    if (table) {
+        float *t = nullptr;
+        MOD_HIP(hipMalloc(&t, sizeof(float) * B));
+        MOD_HIP(hipMemcpyAsync(t, d, sizeof(float) * B, hipMemcpyDeviceToDevice, s));
+        res.kind = kSpecTable;
+        res.table = t;
+    } else if (gain) {
+        res.kind = kSpecGain;
+        res.gain = g;
+    }
+    if (m->spec.size() >= kSpecCache) {  // the oldest goes (its table after the stream's last use)
+        MOD_HIP(hipStreamSynchronize(s));
+        if (m->spec.front().r.table) (void)hipFree(const_cast<float *>(m->spec.front().r.table));
+        m->spec.erase(m->spec.begin());
+    }
+    m->spec.push_back({std::vector<unsigned char>((const unsigned char *)params,
+                                                  (const unsigned char *)params + params_size),
+                       C, B, sr, res});
+    *out = res;
     return DSP_OK;
 }
 

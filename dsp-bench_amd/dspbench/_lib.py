@@ -31,6 +31,8 @@ DSP_PLUGIN_GENERIC = 16
 DSP_EXEC_HOST_BUFFERS = 0x1
 DSP_EXEC_SYNC = 0x2
 DSP_EXEC_FIR_DIRECT = 0x4
+DSP_EXEC_NO_SPECIALIZE = 0x8
+DSP_BLOCK_CALLBACK, DSP_BLOCK_TABLE, DSP_BLOCK_GAIN = 0, 1, 2
 
 
 class DspError(RuntimeError):
@@ -133,6 +135,8 @@ _SIGS = {
     "dsp_module_default_parameters": (C.c_int, [C.c_void_p, C.c_void_p]),
     "dsp_module_initialize_state": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_float, C.c_uint64]),
     "dsp_module_read_state": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "dsp_module_block_class": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_float,
+                                         C.POINTER(C.c_int32), C.POINTER(C.c_float), C.POINTER(dsp_exec)]),
     "dsp_descriptor_from_code": (C.c_int, [C.c_void_p, C.c_uint64, C.POINTER(C.c_void_p)]),
     "dsp_descriptor_destroy": (None, [C.c_void_p]),
     "dsp_module_descriptor": (C.c_void_p, [C.c_void_p]),

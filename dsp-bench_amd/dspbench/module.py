@@ -206,6 +206,23 @@ class Module:
         check(L.lib().dsp_module_read_state(self.handle, buf), "dsp_module_read_state")
         return buf.raw[:self.state_size]
 
-    def plugin(self, params: bytes, name: str = "generic"):
+    def plugin(self, params: bytes, name: str = "generic", specialize: bool = True):
+        """A GENERIC plugin over this module.  specialize=False runs the
+        plugin's callback on every block (DSP_EXEC_NO_SPECIALIZE); by default
+        a stateless plugin of a known block class runs as that class
+        (block_class)."""
         from .api import Plugin
-        return Plugin(L.DSP_PLUGIN_GENERIC, bytes(params), b"", name, self)
+        return Plugin(L.DSP_PLUGIN_GENERIC, bytes(params), b"", name, self,
+                      exec_flags=0 if specialize else L.DSP_EXEC_NO_SPECIALIZE)
+
+    def block_class(self, params: bytes, channels: int, block: int, sample_rate: float, stream=None):
+        """(class, gain): "table" | "gain" | "callback" (dsp_module_block_class),
+        probing the plugin's callback on the current device if not known yet."""
+        import torch
+        buf = C.create_string_buffer(bytes(params), max(1, len(params)))
+        cls, g = C.c_int32(), C.c_float()
+        st = stream if stream is not None else torch.cuda.current_stream().cuda_stream
+        ex = L.dsp_exec(-1, 0, C.c_void_p(st), 0)
+        check(L.lib().dsp_module_block_class(self.handle, buf, len(params), channels, block, sample_rate,
+                                             C.byref(cls), C.byref(g), C.byref(ex)), "dsp_module_block_class")
+        return {L.DSP_BLOCK_TABLE: "table", L.DSP_BLOCK_GAIN: "gain"}.get(cls.value, "callback"), g.value

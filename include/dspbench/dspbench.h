@@ -88,6 +88,12 @@ typedef struct dsp_plugin {
 #define DSP_EXEC_FIR_DIRECT 0x4u   /* DSP_PLUGIN_FIR: the direct form even when T <= 1025 (default:
                                       FFT overlap-save with 8192-point frames for T <= 1025, the
                                       direct form above) */
+#define DSP_EXEC_NO_SPECIALIZE 0x8u /* DSP_PLUGIN_GENERIC: run the plugin's callback on every block.
+                                      Default: a stateless plugin whose callback, probed once per
+                                      (Parameters, C, B, sample rate), ignores its input (renders
+                                      the same block whatever it is given, on every channel) or
+                                      scales it by one factor runs as that block tiled / that gain
+                                      in the fused kernels (module.h) */
 
 typedef struct dsp_exec {
     int32_t device;         /* HIP device ordinal; -1 = current device */

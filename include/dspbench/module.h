@@ -157,7 +157,31 @@ int dsp_param_denormalize(const dsp_param_desc *p, const int64_t *enum_values, f
  * dsp_ir_analysis with plugin->kind = DSP_PLUGIN_GENERIC and plugin->module
  * = the module (plugin->params = the Parameters blob).  dsp_ir_analysis
  * initialises a separate scratch State per call (compute_IR,
- * plugin.cpp:17-58). */
+ * plugin.cpp:17-58).
+ *
+ * Block classes.  A plugin with an empty State computes each block from the
+ * block alone (it cannot tell where the block lies in the file), so:
+ *   DSP_BLOCK_TABLE  a callback that ignores the samples it is given renders
+ *                    the same block everywhere (IR_test.cpp,
+ *                    build/IR_test.cpp:40-60): the render is that block --
+ *                    computed once by the plugin's own callback -- tiled, and
+ *                    dsp_render_stft runs the fused render + STFT kernel on
+ *                    it as a block table;
+ *   DSP_BLOCK_GAIN   a callback that returns g x per sample (gain_test.cpp)
+ *                    runs as the gain map with the g its callback gives x = 1.
+ * The class is found by running the callback on probe blocks (zeros, two
+ * uniform noises, signed steps) and comparing outputs bit for bit, once per
+ * (Parameters, C, B, sample rate) -- the first render with a new set
+ * synchronises its stream once.  Probing is evidence, not proof: a plugin
+ * whose input dependence no probe exposes would be misclassified, and
+ * DSP_EXEC_NO_SPECIALIZE (dspbench.h) runs the callback on every block. */
+enum dsp_block_class { DSP_BLOCK_CALLBACK = 0, DSP_BLOCK_TABLE = 1, DSP_BLOCK_GAIN = 2 };
+
+/* The block class of `params` for C channels of B-sample blocks at sample
+ * rate sr (probing on ex->stream if not known yet); *gain receives g for
+ * DSP_BLOCK_GAIN (may be NULL). */
+int dsp_module_block_class(dsp_module *m, const void *params, uint32_t params_size, uint32_t C, uint32_t B,
+                           float sr, int32_t *block_class, float *gain, const dsp_exec *ex);
 
 #ifdef __cplusplus
 }

@@ -112,9 +112,11 @@ def test_capture_on_a_cold_stream_is_refused_cleanly(torch_cuda):
 
 
 def test_generic_plugin_capture_is_refused(torch_cuda):
-    """A GENERIC plugin's Parameters go up through a host-staged copy, which a
-    graph replay would not repeat: capturing its render is refused with a
-    clear error, and the eager call still works afterwards."""
+    """A GENERIC plugin run by its callback has its Parameters go up through a
+    host-staged copy, which a graph replay would not repeat: capturing its
+    render is refused with a clear error, and the eager call still works
+    afterwards.  The same plugin run as its block class (here gain_test.cpp:
+    the gain map, known from an eager call) captures and replays bit for bit."""
     import os
     torch = torch_cuda
     mods = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "dsp-bench_amd", "modules")
@@ -122,13 +124,19 @@ def test_generic_plugin_capture_is_refused(torch_cuda):
         mod = d.module.Module(f.read())
     params = mod.default_parameters()
     mod.initialize_state(params, 2, 48000.0)
-    p = mod.plugin(params, "gain_test")
+    p = mod.plugin(params, "gain_test", specialize=False)
     x = torch.rand((2, 4096), device="cuda")
     want = d.render_offline(x, 2, 512, 48000.0, p).clone()
     torch.cuda.synchronize()
     msg = _refused_capture(torch, lambda: d.render_offline(x, 2, 512, 48000.0, p))
     assert "captured" in msg, msg
     assert torch.equal(d.render_offline(x, 2, 512, 48000.0, p), want)
+    ps = mod.plugin(params, "gain_test")
+    out = torch.empty((2, 4096), device="cuda")
+
+    def fn(xx):
+        return (d.render_offline(xx, 2, 512, 48000.0, ps, out=out),)
+    _eager_and_graph(torch, fn, x)
 
 
 def test_first_use_table_under_capture_is_refused(torch_cuda):
@@ -136,19 +144,19 @@ def test_first_use_table_under_capture_is_refused(torch_cuda):
     used) is refused with the 'eager call first' error instead of uploading
     on the legacy stream mid-capture; after one eager call the capture works."""
     torch = torch_cuda
-    x = torch.rand((1, 3 * 2048), device="cuda")
-    msg = _refused_capture(torch, lambda: d.stft_magnitude(x, N=2048, H=777, window=d.DSP_WIN_RECT, K=1025))
+    x = torch.rand((1, 3 * 2048), device="cuda")  # (N = 8: a window no other test creates)
+    msg = _refused_capture(torch, lambda: d.stft_magnitude(x, N=8, H=3, window=d.DSP_WIN_RECT, K=5))
     assert "eager call" in msg, msg
     side = torch.cuda.Stream()
-    want = d.stft_magnitude(x, N=2048, H=777, window=d.DSP_WIN_RECT, K=1025).clone()
+    want = d.stft_magnitude(x, N=8, H=3, window=d.DSP_WIN_RECT, K=5).clone()
     out = torch.empty_like(want)
     side.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(side):
-        d.stft_magnitude(x, N=2048, H=777, window=d.DSP_WIN_RECT, K=1025, out=out)
+        d.stft_magnitude(x, N=8, H=3, window=d.DSP_WIN_RECT, K=5, out=out)
     torch.cuda.synchronize()
     g2 = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g2, stream=side):
-        d.stft_magnitude(x, N=2048, H=777, window=d.DSP_WIN_RECT, K=1025, out=out)
+        d.stft_magnitude(x, N=8, H=3, window=d.DSP_WIN_RECT, K=5, out=out)
     g2.replay()
     torch.cuda.synchronize()
     assert torch.equal(out, want)

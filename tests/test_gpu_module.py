@@ -104,7 +104,8 @@ def test_stateless_plugin_staged_edges(torch_cuda, oracle, name, B):
     mod.initialize_state(params, 2, 48000.0)
     ref = oracle.RefPlugin(name, 2, 48000.0)
     x = np.random.default_rng(5).uniform(-1, 1, (1, 300_000 + 13)).astype(np.float32)
-    got = d.render_offline(torch_cuda.from_numpy(x).cuda(), 2, B, 48000.0, mod.plugin(params, name)).cpu().numpy()
+    got = d.render_offline(torch_cuda.from_numpy(x).cuda(), 2, B, 48000.0,
+                           mod.plugin(params, name, specialize=False)).cpu().numpy()
     want = oracle.render_offline([x[0]], 2, B, 48000.0, ref.as_oracle())
     assert got.shape == want.shape
     assert np.array_equal(got, want)
@@ -133,14 +134,14 @@ def test_stateless_plugin_lds_path(torch_cuda, oracle, name, cin, C, B):
     want = oracle.render_offline([x[c] for c in range(cin)], C, B, 48000.0, ref.as_oracle())
     xg = torch_cuda.from_numpy(x).cuda()
     for _ in range(2):
-        got = d.render_offline(xg, C, B, 48000.0, mod.plugin(params, name)).cpu().numpy()
+        got = d.render_offline(xg, C, B, 48000.0, mod.plugin(params, name, specialize=False)).cpu().numpy()
         assert np.array_equal(got, want)
     if cin == C:
         # in place (the file is the output buffer): a round stages all its
         # blocks into LDS before it stores any
         buf = torch_cuda.zeros((C, (L + B - 1) // B * B), dtype=torch_cuda.float32, device="cuda")
         buf[:, :L] = xg
-        d.render_offline(buf, C, B, 48000.0, mod.plugin(params, name), out=buf, L_file=L)
+        d.render_offline(buf, C, B, 48000.0, mod.plugin(params, name, specialize=False), out=buf, L_file=L)
         assert np.array_equal(buf.cpu().numpy(), want)
 
 
@@ -159,7 +160,7 @@ def test_stateless_plugin_lds_pipelined_unaligned_file(torch_cuda, oracle, name)
     x = np.random.default_rng(8).uniform(-1, 1, (2, L + 1)).astype(np.float32)
     xg = torch_cuda.from_numpy(x).cuda()[:, 1:]
     assert xg.data_ptr() % 16 == 4
-    got = d.render_offline(xg, 2, 512, 48000.0, mod.plugin(params, name)).cpu().numpy()
+    got = d.render_offline(xg, 2, 512, 48000.0, mod.plugin(params, name, specialize=False)).cpu().numpy()
     want = oracle.render_offline([x[0, 1:], x[1, 1:]], 2, 512, 48000.0, ref.as_oracle())
     assert np.array_equal(got, want)
 
@@ -173,7 +174,8 @@ def test_stateless_plugin_runs_blocks_in_parallel(torch_cuda, oracle):
     params = struct.pack("<f", 0.37)
     mod.initialize_state(params, 2, 48000.0)
     x = np.random.default_rng(4).uniform(-1, 1, (2, 2_000_000)).astype(np.float32)
-    got = d.render_offline(torch_cuda.from_numpy(x).cuda(), 2, 512, 48000.0, mod.plugin(params)).cpu().numpy()
+    got = d.render_offline(torch_cuda.from_numpy(x).cuda(), 2, 512, 48000.0,
+                           mod.plugin(params, specialize=False)).cpu().numpy()
     want = oracle.render_offline([x[0], x[1]], 2, 512, 48000.0, oracle.restated_plugin("gain_test", [0.37]))
     assert np.array_equal(got, want)
     # and the same as the specialised GAIN kernel
@@ -219,7 +221,8 @@ def _check_stft(oracle, got, m, tol=1e-6):
 @pytest.mark.parametrize("name", ["gain_test", "IR_test", "handmade_test", "sine_test"])
 @pytest.mark.parametrize("cin,C,B", [(2, 2, 512), (1, 2, 256), (1, 1, 512), (2, 2, 384), (1, 2, 100)])
 @pytest.mark.parametrize("L", [8192, 5 * 8192 + 1000, 600_077])
-def test_generic_render_stft(torch_cuda, oracle, name, cin, C, B, L):
+@pytest.mark.parametrize("spec", [True, False], ids=["class", "callback"])
+def test_generic_render_stft(torch_cuda, oracle, name, cin, C, B, L, spec):
     if not have(name):
         pytest.skip("modules / oracle/_ref not built")
     torch = torch_cuda
@@ -228,7 +231,7 @@ def test_generic_render_stft(torch_cuda, oracle, name, cin, C, B, L):
     mod.initialize_state(params, C, 48000.0)
     ref = oracle.RefPlugin(name, C, 48000.0)
     x = np.random.default_rng(L + B).uniform(-1, 1, (cin, L)).astype(np.float32)
-    out, mag = d.render_stft(torch.from_numpy(x).cuda(), C, B, 48000.0, mod.plugin(params, name))
+    out, mag = d.render_stft(torch.from_numpy(x).cuda(), C, B, 48000.0, mod.plugin(params, name, specialize=spec))
     got = out.cpu().numpy()
     want = oracle.render_offline([x[c] for c in range(cin)], C, B, 48000.0, ref.as_oracle())
     if name in TOL:
@@ -240,10 +243,11 @@ def test_generic_render_stft(torch_cuda, oracle, name, cin, C, B, L):
 
 @pytest.mark.gpu
 def test_generic_render_stft_full_hour(torch_cuda, oracle):
-    """1 h of 48 kHz stereo: IR_test.cpp compiled unchanged through the
-    generic path gives the specialised fused kernel's render bit for bit and
-    its spectra within 1e-6 of each frame's peak (two FFT kernels: the fused
-    PER path and the memory path)."""
+    """1 h of 48 kHz stereo: IR_test.cpp compiled unchanged gives the stock
+    fused kernel's render and spectra bit for bit (its block class runs the
+    plugin's own block through the same kernel); with the callback on every
+    block, the render bit for bit and the spectra within 1e-6 of each frame's
+    peak (two FFT kernels: the fused PER path and the memory path)."""
     if not have("IR_test"):
         pytest.skip("modules / oracle/_ref not built")
     torch = torch_cuda
@@ -252,8 +256,10 @@ def test_generic_render_stft_full_hour(torch_cuda, oracle):
     mod.initialize_state(params, 2, 48000.0)
     L = 48_000 * 3600
     x = torch.zeros((2, L), device="cuda")
-    out, mag = d.render_stft(x, 2, 512, 48000.0, mod.plugin(params, "IR_test"))
     out2, mag2 = d.render_stft(x, 2, 512, 48000.0, d.Plugin.ir_test())
+    out, mag = d.render_stft(x, 2, 512, 48000.0, mod.plugin(params, "IR_test"))
+    assert torch.equal(out, out2) and torch.equal(mag, mag2)
+    out, mag = d.render_stft(x, 2, 512, 48000.0, mod.plugin(params, "IR_test", specialize=False))
     assert torch.equal(out, out2)
     rel = ((mag - mag2).abs().amax(dim=2) / mag2.amax(dim=2)).max()
     assert float(rel) <= 1e-6
