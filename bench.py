@@ -194,8 +194,17 @@ def cpu_baseline(seconds_budget: float):
                     return done / el / 1e6, done
     v1, d1 = run(1, seconds_budget / 2)
     vn, dn = run(threads, seconds_budget / 2) if threads > 1 else (v1, d1)
+    omp = os.environ.get("OMP_NUM_THREADS")
     return {"value": round(vn, 2), "unit": "Msamples/s", "cores": threads, "kind": "port",
             "value_1_thread": round(v1, 2), "nproc": os.cpu_count(), "cpus_available": aff,
+            "cores_note": (f"the job's CPU share: OMP_NUM_THREADS={omp} (the GPU box's share per GPU; "
+                           f"sched_getaffinity reports the machine's {aff}, which other jobs share, so more threads "
+                           "would oversubscribe this share, not add cores)" if omp else
+                           "every CPU this process may run on (sched_getaffinity)"),
+            "value_all_cpus_linear_bound": round(vn / threads * aff, 1) if aff > threads else None,
+            "value_all_cpus_linear_bound_note": ("not measured: the measured per-thread rate x all the machine's "
+                                                 "CPUs, an upper bound (1 -> N threads scaled "
+                                                 f"{vn / max(v1, 1e-9):.1f}x here)") if aff > threads else None,
             "sample": f"{dn // CH / SR:.0f} s ({threads} threads) and {d1 // CH / SR:.0f} s (1 thread) of 48 kHz "
                       f"stereo: render through {render_src}, block by block; fp32 radix-4 Stockham real-FFT "
                       "STFT (oracle/oracle.c, OpenMP over frames). CPU restatement, not IPP"}

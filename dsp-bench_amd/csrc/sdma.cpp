@@ -10,6 +10,7 @@
 #include <hsa/hsa.h>
 #include <hsa/hsa_ext_amd.h>
 
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -196,7 +197,10 @@ void SdmaDownloader::run() {
     // beside the uploads, 0x2 (alone or with 0x4) in 60-67 ms, 0x10 in
     // 222 ms (profiles/r03_e2e_sdma_engines.txt).  DSPB_SDMA_ENGINES (a hex
     // mask) overrides, for A/B runs.
-    uint32_t mask = ag.preferred & ag.engines;
+    // A runtime that reports no preference (the ROCm 7.0 runtime PyTorch
+    // bundles: preferred 0x0) gets what ROCm 7.2 prefers for D2H on MI355X
+    // (0x6) -> 0x4; its lowest free engine, 0x1, downloads 1 h in 65 ms.
+    uint32_t mask = (ag.preferred ? ag.preferred : 0x6u) & ag.engines;
     if (mask) mask = 1u << (31 - __builtin_clz(mask));
     if (!mask) mask = ag.engines & (0u - ag.engines);  // the lowest free one
     if (const char *e = std::getenv("DSPB_SDMA_ENGINES")) mask = (uint32_t)std::strtoul(e, nullptr, 16) & ag.engines;
@@ -204,6 +208,9 @@ void SdmaDownloader::run() {
     std::vector<hsa_amd_sdma_engine_id_t> eng;
     for (uint32_t b = 0; b < 32; ++b)
         if (mask & (1u << b)) eng.push_back((hsa_amd_sdma_engine_id_t)(1u << b));
+    if (std::getenv("DSPB_SDMA_VERBOSE"))
+        std::fprintf(stderr, "dspbench: SDMA downloads on engine mask 0x%x (free 0x%x, preferred 0x%x)\n", mask,
+                     ag.engines, ag.preferred);
     size_t next = 0;
     while (true) {
         Job job;
