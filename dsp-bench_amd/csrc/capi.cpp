@@ -745,7 +745,7 @@ int dsp_abi_version(void) { return DSPBENCH_ABI_VERSION; }
 #ifdef DSPB_AB_BUILD
 int dsp_stft_pk_ab_options(int opt) {
     const int old = g_pk_ab_opt;
-    if (opt >= 0 && opt <= 0xfffff) g_pk_ab_opt = opt;
+    if (opt >= 0 && opt <= 0x3fffff) g_pk_ab_opt = opt;
     return old;
 }
 #endif

@@ -170,7 +170,8 @@ __device__ __forceinline__ void transpose_pl(const cx2 (&Q)[32], float *lds, uin
 // DFT32 halves (combine64p / combine64_dir finish it).
 // PL: the transpose goes through transpose_pl's 64 x 33 tile.
 // HOOK: called once the transpose's last LDS read has completed (the tile
-// is free from there on; stft8192_mem_pf_kernel prefetches into it).
+// is free from there on; the A/B kernel stft8192_mem_pf_kernel, stft_pk_ab.hip,
+// prefetches into it).
 struct NoHook {
     __device__ void operator()() const {}
 };

@@ -79,6 +79,7 @@ int launch_stft8192_pk(const Stft8kArgs &A, uint32_t C, bool fused, int opt, hip
     }
 #ifdef DSPB_AB_BUILD
     if (!fused && winc && (opt & kPkMemPf)) return launch_mem_pf(A, C, stream);
+    if (!fused && winc && (opt & kPkMemHop)) return launch_mem_hop(A, C, stream);
     if (!fused && winc && (opt & kPkMemAos)) return launch_pk_ab(A, fused, opt, grid, stream);
 #else
     (void)opt;  // the A/B options exist only in the tools build (make ab)

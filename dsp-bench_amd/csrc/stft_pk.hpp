@@ -42,8 +42,10 @@ namespace dspb {
 // fewer per frame, the same bits)
 enum { kPkNoBarDft = 1, kPkNoBarTw = 2, kPkNoBarSplit = 4, kPkRenderCached = 8, kPkNtMag = 16, kPkMagLds = 32,
        kPkOldSplit = 64, kPkAbNoRender = 128, kPkAbNoMag = 256, kPkMagStage = 512, kPkOcc3 = 1024,
-       kPkMemAos = 2048, kPkNoRemap = 4096, kPkAbNoXpose = 8192, kPkMemPf = 16384, kPkW1 = 65536 };
+       kPkMemAos = 2048, kPkNoRemap = 4096, kPkAbNoXpose = 8192, kPkMemPf = 16384, kPkW1 = 65536,
+       kPkMemHop = 131072 };
 // 65536 = one wave per workgroup (64 threads, one 64 x 65 tile): a slot frees as its frame ends
+// 131072 = memory frames on stft8192_mem_hop_kernel (a workgroup's 5 hops staged once in LDS)
 // 16384 = memory frames on stft8192_mem_pf_kernel (persistent, LDS hop prefetch)
 // 8192: ablation only (results discarded): no LDS transpose
 // 4096 = frames in dispatch order (no XCD remap: all XCDs write one frontier)
@@ -500,124 +502,10 @@ void stft8192_pk_kernel(Stft8kArgs A) {
     }
 }
 
-// Memory-source STFT (4097 bins, computed window, H = 4096, every frame
-// whole) on a persistent grid: wave w takes units u = w, w + W, ... of the
-// (channel, frame) sequence, and while frame u's second DFT64 and real split
-// run, the first hop of frame u + W travels into the wave's LDS tile (free
-// once the transpose's reads are done) as 16 global_load_lds_dwordx4.  At the
-// next frame only the second hop is loaded into VGPRs -- the first hop of
-// the neighbouring wave's frame, fetched into L2 one frame earlier.  The
-// arithmetic is stft8192_pk_kernel's MSOA path, instruction for instruction.
-__device__ __forceinline__ void pf_hop(const float *src, float *lds, uint32_t lane) {
-    typedef __attribute__((address_space(3))) float lfloat;
-    typedef __attribute__((address_space(3))) void lvoid;
-    lfloat *l3 = (lfloat *)lds;
-#pragma unroll
-    for (int i = 0; i < 16; ++i)
-        __builtin_amdgcn_global_load_lds((const void *)(src + 256u * (uint32_t)i + 4u * lane), (lvoid *)(l3 + 256 * i),
-                                         16, 0, 0);
-}
-
-template <int OPT = 0>
-__global__ __launch_bounds__(256, 2) void stft8192_mem_pf_kernel(Stft8kArgs A, uint32_t nch) {
-    __shared__ __attribute__((aligned(16))) float lds_all[4][64 * 65];
-    __shared__ float4 wuv[4][64];  // the lane's window coefficients, read back per frame
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint64_t W = (uint64_t)gridDim.x * 4u;
-    const uint64_t U = A.F * nch;
-    uint64_t u = (uint64_t)xcd_remap(blockIdx.x, gridDim.x) * 4u + wave;
-    if (u >= U) return;
-    float *lds = lds_all[wave];
-    cx tlo[8];
-    cx2 thp[4];
-#pragma unroll
-    for (int j = 1; j < 8; ++j) {
-        const v2f a = (A.tw + 8192u + 64u * (uint32_t)(j - 1))[lane];
-        tlo[j] = cx{a.x, a.y};
-    }
-    {
-        const float4 *tp4 = reinterpret_cast<const float4 *>(A.tw + 8192u + 896u);
-#pragma unroll
-        for (int h = 0; h < 4; ++h) {
-            const float4 t = tp4[64u * (uint32_t)h + lane];
-            thp[h] = cx2{v2f{t.x, t.y}, v2f{t.z, t.w}};
-        }
-    }
-    {
-        const float4 wbase = A.wbase[lane];
-        wuv[wave][lane] = float4{A.wb * wbase.x, A.wb * wbase.y, A.wb * wbase.z, A.wb * wbase.w};
-    }
-    // (channel, frame) of unit u, stepped by W without a division per frame
-    // (host: F C < 2^32)
-    const uint32_t F = (uint32_t)A.F, Wn = (uint32_t)W;
-    uint32_t c = (uint32_t)u / F, f = (uint32_t)u - c * F;
-    pf_hop(A.in.p[c] + (uint64_t)f * 4096u, lds, lane);
-    __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): the first frame's first hop
-    for (;;) {
-        const float *x = A.in.p[c] + (uint64_t)f * 4096u;
-        uint32_t cn = c, fn = f + Wn;
-        while (fn >= F) {  // wave-uniform
-            fn -= F;
-            ++cn;
-        }
-        // opaque per frame: the window stays computed inside the loop (hoisted,
-        // its 128 values would spill)
-        // (an LDS read: kept in VGPRs they spill, and the reload's vmcnt(0)
-        // would wait for the previous frame's stores)
-        const float4 wl4 = wuv[wave][lane];
-        float ue = wl4.x, ve = wl4.y, uo = wl4.z, vo = wl4.w;
-        asm volatile("" : "+v"(ue), "+v"(ve), "+v"(uo), "+v"(vo));
-        // likewise the stage twiddles (their products) and the split's table
-#pragma unroll
-        for (int j = 1; j < 8; ++j) asm volatile("" : "+v"(tlo[j].r), "+v"(tlo[j].i));
-#pragma unroll
-        for (int h = 0; h < 4; ++h) asm volatile("" : "+v"(thp[h].r), "+v"(thp[h].i));
-        const v2f *tw = A.tw;
-        asm volatile("" : "+s"(tw));
-        cx2 P[32];
-        // the second hop from global (in flight while the first is read from LDS)
-        v2f ga[16], gb[16];
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            ga[j] = reinterpret_cast<const v2f *>(x + 4096u + 256u * (uint32_t)j)[lane];
-            gb[j] = reinterpret_cast<const v2f *>(x + 4096u + 256u * (uint32_t)j + 128u)[lane];
-        }
-#pragma unroll
-        for (int j = 0; j < 32; ++j) {
-            const v2f C = v2f{kWinB_c[2 * j], kWinB_c[2 * j + 1]}, S = v2f{kWinB_s[2 * j], kWinB_s[2 * j + 1]};
-            const v2f we = (v2f{ve, ve} * S + v2f{A.wa, A.wa}) - v2f{ue, ue} * C;
-            const v2f wo = (v2f{vo, vo} * S + v2f{A.wa, A.wa}) - v2f{uo, uo} * C;
-            v2f a, b;
-            if (j < 16) {
-                a = reinterpret_cast<const v2f *>(lds + 256u * (uint32_t)j)[lane];
-                b = reinterpret_cast<const v2f *>(lds + 256u * (uint32_t)j + 128u)[lane];
-            } else {
-                a = ga[j - 16];
-                b = gb[j - 16];
-            }
-            P[j] = cx2{v2f{a.x, b.x} * we, v2f{a.y, b.y} * wo};
-        }
-        const uint64_t un = u + W;
-        const bool more = un < U;
-        cx2 Y2[32];
-        fft4096_pk_y2<true, true>(P, lds, tlo, thp, lane, Y2, [&]() {
-            if (more) pf_hop(A.in.p[cn] + (uint64_t)fn * 4096u, lds, lane);
-        });
-        // the prefetch lands before the split's stores are issued, so the
-        // wait below covers it alone
-        __builtin_amdgcn_s_waitcnt(0x0f70);
-        split_y2<kKHalf, true>(Y2, A.mag.p[c] + f * A.ld, A.K, tw, lane, lds);
-        if (!more) break;
-        u = un;
-        c = cn;
-        f = fn;
-    }
-}
-
 // the launches of stft_pk_paths.hip / stft_pk_ab.hip (DSP_OK or a status)
 int launch_pk_paths(const Stft8kArgs &A, bool fused, int km, bool pow2, bool winc, dim3 grid, hipStream_t s);
 int launch_pk_ab(const Stft8kArgs &A, bool fused, int opt, dim3 grid, hipStream_t s);
 int launch_mem_pf(const Stft8kArgs &A, uint32_t C, hipStream_t s);
+int launch_mem_hop(const Stft8kArgs &A, uint32_t C, hipStream_t s);
 
 }  // namespace dspb

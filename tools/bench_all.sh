@@ -1,8 +1,17 @@
 # every bench workload once at the bench's defaults (no CPU baseline, no
-# end-to-end pass): one JSON line each into gpurun_out/bench_all.jsonl
+# end-to-end pass): one JSON line each into gpurun_out/bench_all.jsonl, and a
+# summary table
+set -o pipefail
 mkdir -p gpurun_out
 rm -f gpurun_out/bench_all.jsonl
-for wl in stft96k gain_stft generic generic_stft fir1024 gain10min ch96k wav16 wav16enc; do
+for wl in headline stft96k gain_stft generic generic_stft fir1024 gain10min ch96k wav16 wav24 wav16enc wav24enc ir; do
   timeout -k 10 200 python -u bench.py --workload $wl --no-cpu-baseline --no-e2e > gpurun_out/bench_$wl.log 2>&1 || exit 1
   tail -1 gpurun_out/bench_$wl.log >> gpurun_out/bench_all.jsonl
 done
+python3 - <<'PY'
+import json
+for line in open("gpurun_out/bench_all.jsonl"):
+    l = json.loads(line)
+    r = l["roofline"]
+    print(f'{l["config"]["workload"][:70]:72s} {l["value"]:>12.1f} {l["ms_per_step"]:8.4f} {r.get("frac", 0):7.4f} {r.get("kernel_avg_ms", 0)}')
+PY
