@@ -235,6 +235,25 @@ int launch_pk_ab(const Stft8kArgs &A, bool fused, int opt, dim3 grid_default, hi
         DSPB_HIP(hipGetLastError());
         return DSP_OK;
     }
+    if (opt & kPkW1) {  // one-wave workgroups, as the product's PER kernel: one group per frame
+        const uint64_t tail = A.tail_end > A.F * A.H ? (A.tail_end - A.F * A.H + A.H - 1) / A.H : 0;
+        const dim3 g1((uint32_t)(A.F + tail), grid_default.y);
+        switch (opt) {
+#define DSPB_PK_W1(o)                                                                                            \
+    case (o):                                                                                                    \
+        hipLaunchKernelGGL((stft8192_pk_kernel<kSrcRender, kKHalf, MapKind::Ramp, true, true, 4, (o)>), g1, dim3(64), \
+                           0, stream, A);                                                                        \
+        break
+            DSPB_PK_W1(kPkPerOpt | kPkMagStage);
+            DSPB_PK_W1(kPkPerOpt | kPkMagStage | kPkNtMag);
+            DSPB_PK_W1(kPkPerOpt | kPkNtMag);
+            DSPB_PK_W1(kPkPerOpt | kPkRenderCached);
+#undef DSPB_PK_W1
+        default: return DSP_ERR_INVALID;
+        }
+        DSPB_HIP(hipGetLastError());
+        return DSP_OK;
+    }
     switch (opt) {
 #define DSPB_PK_CASE(o)                                                                                     \
     case (o):                                                                                               \
