@@ -260,6 +260,17 @@ def loopback(world: int, device: int = -1) -> list:
     return [_Handle(C.c_void_p(arr[r])) for r in range(world)]
 
 
+def _hip_runtime():
+    """The HIP runtime already in this process (libdspbench's, which in a
+    torch process is torch's own copy): by soname, never a second runtime."""
+    import os
+    L.lib()  # libdspbench (and its libamdhip64.so.7) loaded first
+    try:
+        return C.CDLL("libamdhip64.so.7", mode=os.RTLD_NOLOAD | os.RTLD_NOW)
+    except OSError:
+        return C.CDLL("libamdhip64.so.7")
+
+
 class TorchComm(_Comm):
     """A torch.distributed group (gloo) as a dsp_comm transport
     (dsp_comm_init_transport): the C++ driver's sends and recvs of device rows
@@ -270,7 +281,7 @@ class TorchComm(_Comm):
         import torch.distributed as dist
         self.group = group
         rank, world = dist.get_rank(group), dist.get_world_size(group)
-        self._hip = C.CDLL("libamdhip64.so")
+        self._hip = _hip_runtime()
         self._hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
         self._hip.hipStreamSynchronize.argtypes = [C.c_void_p]
         self._depth, self._ops = 0, []

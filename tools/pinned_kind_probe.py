@@ -8,17 +8,24 @@ non-blocking stream, in the order printed; the trace tells which engine ran
 each copy (a copyBuffer kernel, or a MEMORY_COPY_DEVICE_TO_HOST record).
 """
 import ctypes as C
+import os
 import time
 
 import torch
 
-hip = C.CDLL("libamdhip64.so")
+torch.cuda.init()
+# the runtime torch already loaded (by soname), not a second copy from /opt/rocm
+hip = C.CDLL("libamdhip64.so.7", mode=os.RTLD_NOLOAD | os.RTLD_NOW)
 hip.hipHostMalloc.argtypes = [C.POINTER(C.c_void_p), C.c_size_t, C.c_uint]
 hip.hipHostGetFlags.argtypes = [C.POINTER(C.c_uint), C.c_void_p]
 hip.hipMemcpyAsync.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_void_p]
 hip.hipStreamCreateWithFlags.argtypes = [C.POINTER(C.c_void_p), C.c_uint]
 hip.hipStreamSynchronize.argtypes = [C.c_void_p]
 hip.hipHostRegister.argtypes = [C.c_void_p, C.c_size_t, C.c_uint]
+
+for line in open("/proc/self/maps"):  # which HIP runtime(s) this process has mapped
+    if "libamdhip64" in line and "r-xp" in line:
+        print("mapped:", line.split()[-1], flush=True)
 
 NB = 64 << 20
 src = torch.rand(NB // 4, device="cuda")
