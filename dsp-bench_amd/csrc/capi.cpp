@@ -900,6 +900,7 @@ int dsp_render_loop(const float *const *in, uint32_t in_channels, uint64_t L, ui
     SampleMap map;
     int st = plugin_map(plugin, B, g.dev, s, &map, sr, ex ? ex->flags : 0);
     if (st) return st;
+    if ((st = specialize_generic(&map, C, B, s, ex))) return st;
     if ((st = ensure_ramp_table(map, s))) return st;
     const uint32_t in_ch = std::min(in_channels, C);  // channels_to_write (audio.cpp:66)
     auto wrap = [&](const float *const *src, float *const *dst, uint32_t nc, const SampleMap &m) -> int {

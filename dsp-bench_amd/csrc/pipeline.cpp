@@ -29,6 +29,7 @@
 #include <cstring>
 #include <vector>
 
+#include "dspbench/module.h"
 #include "dspbench/shard.h"
 #include "dspbench/wav.h"
 #include "sdma.hpp"
@@ -143,9 +144,13 @@ int run(const Source &src, uint32_t C, uint32_t B, float sr, const dsp_plugin *p
     // render-only: chunks of whole blocks without a halo (N = H = B)
     const uint32_t pN = stft ? N : B, pH = stft ? H : B;
     // the FIR's history and a GENERIC plugin's State carry across blocks:
-    // one chunk (a stateless GENERIC plugin could chunk; the dsp_plugin alone
-    // does not tell)
-    const bool one = plugin && (plugin->kind == DSP_PLUGIN_FIR || plugin->kind == DSP_PLUGIN_GENERIC);
+    // one chunk (a GENERIC plugin without a State chunks like the map plugins)
+    int stateless = 1;
+    if (plugin && plugin->kind == DSP_PLUGIN_GENERIC) {
+        if (!plugin->module) return invalid("GENERIC plugin needs a loaded dsp_module");
+        if (int e = dsp_module_sizes((const dsp_module *)plugin->module, nullptr, nullptr, &stateless)) return e;
+    }
+    const bool one = plugin && (plugin->kind == DSP_PLUGIN_FIR || (plugin->kind == DSP_PLUGIN_GENERIC && !stateless));
     dsp_shard whole{};
     int st = dsp_shard_plan(L, C, 1, 0, B, pN, pH, DSP_SHARD_TIME, 1, &whole);
     if (st) return st;
@@ -265,7 +270,7 @@ int run(const Source &src, uint32_t C, uint32_t B, float sr, const dsp_plugin *p
         PL_HIP(hipStreamWaitEvent(cs, s.up_done, 0));
         dsp_exec e{};
         e.device = -1;
-        e.flags = ex ? (ex->flags & DSP_EXEC_FIR_DIRECT) : 0;
+        e.flags = ex ? (ex->flags & DSP_EXEC_METHOD_FLAGS) : 0;
         e.stream = cs;
         e.sample_offset = goff + c.start;
         std::vector<const float *> rin(Cin);

@@ -25,6 +25,7 @@
 
 #include <rccl/rccl.h>
 
+#include "dspbench/module.h"
 #include "dspbench/shard.h"
 
 namespace dspb {
@@ -592,8 +593,16 @@ int dsp_render_stft_sharded(const float *const *in, uint32_t in_channels, uint64
     const bool gather = comm ? true : (world == 1 && (all_out || all_mag));
     if (gather && rank == root && !(all_out && all_mag)) return invalid("the root needs both all_out and all_mag");
     const uint64_t goff0 = ex ? ex->sample_offset : 0;
-    if (sh->mode == DSP_SHARD_TIME && plugin && plugin->kind == DSP_PLUGIN_GENERIC && plugin->state_size)
-        return invalid("time sharding needs a state-free plugin");
+    // a GENERIC plugin's State lives in its module (plugin->state_size is 0):
+    // ask the module whether it has one
+    int stateless = 1;
+    if (plugin && plugin->kind == DSP_PLUGIN_GENERIC) {
+        if (!plugin->module) return invalid("GENERIC plugin needs a loaded dsp_module");
+        if (int st = dsp_module_sizes((const dsp_module *)plugin->module, nullptr, nullptr, &stateless)) return st;
+    }
+    const bool stateful_generic = plugin && plugin->kind == DSP_PLUGIN_GENERIC && !stateless;
+    if (sh->mode == DSP_SHARD_TIME && sh->world > 1 && stateful_generic)
+        return invalid("time sharding needs a state-free plugin (this module has a State)");
 
     int prev = -1;
     SH_HIP(hipGetDevice(&prev));
@@ -612,9 +621,9 @@ int dsp_render_stft_sharded(const float *const *in, uint32_t in_channels, uint64
     const bool halo_fits = (uint64_t)(N - H + B - 1) / B * B < N;
     if (!halo_fits && sh->mode == DSP_SHARD_TIME && sh->world > 1)
         return invalid("time sharding needs ceil((N - H) / B) B < N (B = %u, N = %u, H = %u)", B, N, H);
-    // this rank's chunks (a GENERIC plugin is rendered as one call: its
-    // State, if any, carries through the whole channel)
-    const bool one_chunk = (plugin && plugin->kind == DSP_PLUGIN_GENERIC) || !halo_fits;
+    // this rank's chunks (a GENERIC plugin with a State is rendered as one
+    // call: the State carries through the whole channel)
+    const bool one_chunk = stateful_generic || !halo_fits;
     const uint64_t eff_chunk = one_chunk ? 0 : chunk;
     const int64_t nch = dsp_shard_chunks(sh, L, B, N, H, 1, eff_chunk, nullptr, 0);
     if (nch < 0) return (int)nch;
@@ -658,7 +667,7 @@ int dsp_render_stft_sharded(const float *const *in, uint32_t in_channels, uint64
             }
             dsp_exec e{};
             e.device = dev;
-            e.flags = ex ? (ex->flags & DSP_EXEC_FIR_DIRECT) : 0;
+            e.flags = ex ? (ex->flags & DSP_EXEC_METHOD_FLAGS) : 0;
             e.stream = s;
             e.sample_offset = goff0 + c.start;
             const uint64_t Fc = frames_of((Lc + B - 1) / B * B, N, H);

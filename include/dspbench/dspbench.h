@@ -94,6 +94,9 @@ typedef struct dsp_plugin {
                                       the same block whatever it is given, on every channel) or
                                       scales it by one factor runs as that block tiled / that gain
                                       in the fused kernels (module.h) */
+/* the flags that choose how a call computes (not where its buffers live):
+ * the chunked and sharded drivers pass them on to every chunk */
+#define DSP_EXEC_METHOD_FLAGS (DSP_EXEC_FIR_DIRECT | DSP_EXEC_NO_SPECIALIZE)
 
 typedef struct dsp_exec {
     int32_t device;         /* HIP device ordinal; -1 = current device */

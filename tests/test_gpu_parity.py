@@ -402,11 +402,14 @@ def test_render_loop_generic_and_fir(torch_cuda, oracle):
     if os.path.exists(co):
         mod = d.module.Module(open(co, "rb").read())
         mod.initialize_state(mod.default_parameters(), 2, 48000.0)
-        got, _ = d.render_loop(to_dev(torch, x), 2, B, nb, 48000.0, mod.plugin_from_values({"gain": 0.45}),
-                               cursor=cursor)
         ref, _ = oracle.render_loop([x[0], x[1]], 2, B, nb, 48000.0, oracle.restated_plugin("gain_test", [0.45]),
                                     cursor=cursor)
-        assert np.array_equal(got.cpu().numpy(), ref)
+        for spec in (True, False):  # its block class (the gain map in the wrap kernel), and the callback
+            p = mod.plugin_from_values({"gain": 0.45})
+            if not spec:
+                p.exec_flags = d._lib.DSP_EXEC_NO_SPECIALIZE
+            got, _ = d.render_loop(to_dev(torch, x), 2, B, nb, 48000.0, p, cursor=cursor)
+            assert np.array_equal(got.cpu().numpy(), ref), spec
     taps = rnd((1, 300), 73)[0] * 0.05
     got, _ = d.render_loop(to_dev(torch, x), 2, B, nb, 48000.0, d.Plugin.fir(taps), cursor=cursor)
     idx = (cursor + np.arange(nb * B)) % L

@@ -78,3 +78,33 @@ def test_wav_pipeline_matches_decode_and_oracle(torch_cuda, oracle, Cf, C_out, b
     xd[:, :L] = torch.from_numpy(np.ascontiguousarray(x[:nin])).cuda()
     _, dmag = d.render_stft(xd[:, :L], C_out, 512, 48000.0, d.Plugin.gain_test(0.2), L_file=L)
     assert np.array_equal(mag, dmag.cpu().numpy())
+
+
+@pytest.mark.parametrize("name,spec", [("IR_test", True), ("IR_test", False), ("gain_test", True),
+                                       ("gain_test", False), ("sine_test", True)])
+def test_host_pipeline_generic_plugin(torch_cuda, name, spec):
+    """A plugin compiled from source through the host pipeline: a stateless
+    one chunks like the stock maps (its block class, or its callback on every
+    block); one with a State (sine_test) runs as one chunk.  Bit-identical to
+    the device call."""
+    import os
+    torch = torch_cuda
+    mods = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "dsp-bench_amd", "modules")
+    co = os.path.join(mods, f"mod_{name}.co")
+    if not os.path.exists(co):
+        pytest.skip("modules not built")
+    mod = d.module.Module(open(co, "rb").read())
+    params = mod.default_parameters()
+    L, B = 8192 * 11 + 77, 512
+    x = rnd((2, L), 84)
+    xp = torch.zeros((2, L + 3), device="cuda")
+    xp[:, :L] = torch.from_numpy(x).cuda()
+    mod.initialize_state(params, 2, 48000.0)
+    want_out, want_mag = d.render_stft(xp[:, :L], 2, B, 48000.0, mod.plugin(params, name, specialize=spec),
+                                       window=d.DSP_WIN_HANN, L_file=L)
+    torch.cuda.synchronize()
+    mod.initialize_state(params, 2, 48000.0)  # (a State restarts from initialize_state, as on the device call)
+    got_out, got_mag = d.render_stft_host(x, 2, B, 48000.0, mod.plugin(params, name, specialize=spec),
+                                          chunk=3 * 4096)
+    assert np.array_equal(np.asarray(got_out), want_out.cpu().numpy())
+    assert np.array_equal(np.asarray(got_mag), want_mag.cpu().numpy())

@@ -189,6 +189,52 @@ def _where(torch, got, ref):
     return "; ".join(lines)
 
 
+@pytest.mark.parametrize("spec", [True, False])
+def test_time_shards_of_a_stateless_source_plugin(torch_cuda, spec):
+    """IR_test.cpp compiled from source, time-sharded over two loopback ranks
+    with chunks inside each rank (its block class, or its callback on every
+    block): the root's rows equal the whole-file call bit for bit.  A plugin
+    with a State (sine_test.cpp) is refused for time shards at world > 1."""
+    import os
+    torch = torch_cuda
+    mods = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "dsp-bench_amd", "modules")
+    if not os.path.exists(os.path.join(mods, "mod_IR_test.co")):
+        pytest.skip("modules not built")
+    mod = d.module.Module(open(os.path.join(mods, "mod_IR_test.co"), "rb").read())
+    params = mod.default_parameters()
+    mod.initialize_state(params, 2, 48000.0)
+    plugin = mod.plugin(params, "IR_test", specialize=spec)
+    L, B, K, world = 8192 * 12 + 999, 512, 4097, 2
+    x = (torch.rand((2, L + 1), device="cuda") * 2 - 1)[:, :L]
+    ref_out, ref_mag = _whole(torch, x, 2, B, plugin, L)
+    all_out = torch.full_like(ref_out, -7.0)
+    all_mag = torch.full_like(ref_mag, -7.0)
+    comms = sh.loopback(world, 0)
+
+    def rank_fn(r):
+        s = sh.plan(L, world, r, B, 8192, 4096, True, 2, sh.TIME)
+        out = torch.empty((2, -(-s.read_len // B) * B), device="cuda")
+        mag = torch.empty((2, max(s.frames, 1), K), device="cuda")
+        st = torch.cuda.Stream()
+        sh.render_stft_sharded(x[:, s.start:s.start + s.read_len], L, 2, B, 96000.0, plugin, s, out, mag,
+                               comm=comms[r], root=0, all_out=all_out if r == 0 else None,
+                               all_mag=all_mag if r == 0 else None, chunk=3 * 4096, stream=st.cuda_stream)
+        st.synchronize()
+    _run_ranks(torch, world, rank_fn)
+    for c in comms:
+        c.close()
+    assert torch.equal(all_out, ref_out), _where(torch, all_out, ref_out)
+    assert torch.equal(all_mag, ref_mag), _where(torch, all_mag, ref_mag)
+    smod = d.module.Module(open(os.path.join(mods, "mod_sine_test.co"), "rb").read())
+    sp = smod.default_parameters()
+    smod.initialize_state(sp, 2, 48000.0)
+    s0 = sh.plan(L, world, 0, B, 8192, 4096, True, 2, sh.TIME)
+    with pytest.raises(d.DspError):
+        sh.render_stft_sharded(x[:, :s0.read_len], L, 2, B, 96000.0, smod.plugin(sp, "sine_test"), s0,
+                               torch.empty((2, -(-s0.read_len // B) * B), device="cuda"),
+                               torch.empty((2, s0.frames, K), device="cuda"), comm=None, gather=False)
+
+
 def test_loopback_gather_and_errors(torch_cuda):
     """dsp_comm_gather over the loopback (3 ranks, root 2); a count mismatch
     between a send and its recv fails both sides instead of copying."""
