@@ -50,6 +50,7 @@
 
 #include <ctime>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -116,7 +117,9 @@ bool exchange_comm_id(const std::string &path, uint32_t rank, const std::string 
         return ok && std::rename(tmp.c_str(), path.c_str()) == 0;
     }
     std::vector<unsigned char> buf(DSP_COMM_ID_BYTES + run_id.size() + 1);
-    for (int i = 0; i < 1200; ++i, usleep(100000)) {
+    int tries = 1200;  // two minutes; DSPB_COMM_WAIT_S shortens it (tests)
+    if (const char *w = std::getenv("DSPB_COMM_WAIT_S")) tries = std::max(1, std::atoi(w) * 10);
+    for (int i = 0; i < tries; ++i, usleep(100000)) {
         struct stat sb;
         if (stat(path.c_str(), &sb) != 0) continue;
         if (run_id.empty() && sb.st_mtime < started) continue;  // stale: before this launch

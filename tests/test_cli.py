@@ -26,8 +26,8 @@ BIQUAD = os.path.join(ROOT, "dsp-bench_amd", "plugins", "biquad.cpp")
 needs_cli = pytest.mark.skipif(not os.path.exists(CLI), reason="dspbench_render not built")
 
 
-def run(*args):
-    return subprocess.run([CLI, *args], capture_output=True, text=True, timeout=300)
+def run(*args, env=None):
+    return subprocess.run([CLI, *args], capture_output=True, text=True, timeout=300, env=env)
 
 
 @needs_cli
@@ -194,3 +194,30 @@ def test_multi_rank_cli_one_rank(torch_cuda, oracle, tmp_path):
     assert r.returncode == 0, r.stderr
     assert a.read_bytes() == b.read_bytes()
     assert am.read_bytes() == bm.read_bytes()
+    assert not (tmp_path / "rccl.id").exists(), "rank 0 leaves the spent id file behind"
+
+
+@needs_cli
+@pytest.mark.gpu
+def test_multi_rank_cli_ignores_a_stale_id_file(torch_cuda, tmp_path):
+    """A rank other than 0 never reads an id file another launch left: one
+    written before it started (no run id), or one carrying another run id.
+    With nothing fresh to read it gives up (DSPB_COMM_WAIT_S = 2) instead of
+    joining a dead communicator."""
+    import os
+    import time
+    src, raw = _pcm16(tmp_path, 2, 8192 * 3, 96000, 14)
+    idf = tmp_path / "rccl.id"
+    idf.write_bytes(bytes(128))                      # a previous launch's file, no run id
+    old = time.time() - 60
+    os.utime(idf, (old, old))
+    env = dict(os.environ, DSPB_COMM_WAIT_S="2")
+    env.pop("DSPB_RUN_ID", None)
+    env.pop("TORCHELASTIC_RUN_ID", None)
+    args = [str(src), str(tmp_path / "o.wav"), "--plugin", "IR_test", "--stft", str(tmp_path / "o.f32"),
+            "--comm-id", str(idf), "--world", "2", "--rank", "1", "--device", "0"]
+    r = run(*args, env=env)
+    assert r.returncode != 0 and "no communicator id" in r.stderr, r.stderr
+    idf.write_bytes(bytes(128) + b"run-A")           # fresh, but another run's id
+    r = run(*args, "--run-id", "run-B", env=env)
+    assert r.returncode != 0 and "no communicator id" in r.stderr, r.stderr
