@@ -57,6 +57,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
     ap.add_argument("--no-gather", action="store_true",
                     help="N > 1: skip the timed pass of the sharded driver with the RCCL gather to rank 0")
+    ap.add_argument("--gather-timeout", type=float, default=240.0,
+                    help="N > 1: seconds before a gather pass that has not finished is abandoned (the line is "
+                         "printed with render_gather_error)")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (host WAV -> host spectra) pass")
     ap.add_argument("--launch-events", action="store_true",
                     help="one-kernel workloads: bracket every launch with the library's HIP events inside the "
@@ -96,11 +99,13 @@ PK_INST = {
 }
 
 
-def pmc_traffic(workload: str):
+def pmc_traffic(workload: str, alg_bytes: float):
     """HBM bytes per launch of the workload's kernel instantiation from the
     newest committed PMC summary of the same bench command (rocprofv3 --pmc
     FETCH_SIZE / WRITE_SIZE in separate passes, tools/pmc_summary.py --json:
-    FETCH_SIZE x2 + WRITE_SIZE per MI355X_MICROARCH.md), or (None, None, None)."""
+    FETCH_SIZE x2 + WRITE_SIZE per MI355X_MICROARCH.md), or (None, None, None).
+    The summaries are of the default sizes: a run of another size (--minutes)
+    gets no traffic figure rather than another launch's."""
     import glob
     inst = PK_INST.get(workload)
     if inst is None:
@@ -109,7 +114,10 @@ def pmc_traffic(workload: str):
         doc = json.load(open(path))
         for name, m in doc.get("kernels", {}).items():
             if name.endswith(inst) and "hbm_bytes" in m:
-                return float(m["hbm_bytes"]), os.path.relpath(path, REPO), inst
+                t = float(m["hbm_bytes"])
+                if not alg_bytes or not 0.9 <= t / alg_bytes <= 1.5:
+                    return None, f"{os.path.relpath(path, REPO)} (a launch of another size: not used)", inst
+                return t, os.path.relpath(path, REPO), inst
     return None, None, inst
 
 
@@ -561,25 +569,8 @@ def main():
     # one-GPU rehearsal uses gloo as the transport), timed on its own,
     # outside `value`
     gather_ms = None
-    if not args.no_gather and world > 1 and wl in ("headline", "ch96k"):
-        comm = d.shard.TorchComm(device=local) if rehearsal else d.shard.RcclComm.from_torch(device=local)
-        Ctot = world if wl == "ch96k" else CH
-        Lfile = L if wl == "ch96k" else world * L
-        Lpad = d.num_blocks(Lfile, B) * B
-        Ftot = d.stft_frames(Lpad, N_FFT, HOP)
-        all_out = torch.empty((Ctot, Lpad), device=dev) if rank == 0 else None
-        all_mag = torch.empty((Ctot, Ftot, K_BINS), device=dev) if rank == 0 else None
-        torch.cuda.synchronize()
-        dist.barrier()
-        tg = time.perf_counter()
-        d.shard.render_stft_sharded(x, Lfile, Ctot, B, float(sr), plugin, sh, out, mag, comm=comm, root=0,
-                                    all_out=all_out, all_mag=all_mag, chunk=1 << 24, N=N_FFT, H=HOP,
-                                    window=d.DSP_WIN_HANN, K=K_BINS)
-        torch.cuda.synchronize()
-        dist.barrier()
-        gather_ms = (time.perf_counter() - tg) * 1e3
-        comm.close()
-        del all_out, all_mag
+    gather_err = None
+    gather_pending = not args.no_gather and world > 1 and wl in ("headline", "ch96k")
 
     # end to end: the same hour as a 16-bit PCM WAV payload in
     # pinned host memory -> chunked H2D -> GPU decode -> render + STFT -> D2H
@@ -614,7 +605,7 @@ def main():
                          "(profiles/r03_d2h_probe.txt)"}
         del pay, h_out, h_mag
 
-    traffic, traffic_src, traffic_inst = pmc_traffic(wl)
+    traffic, traffic_src, traffic_inst = pmc_traffic(wl, bytes_per_launch)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and wl == "headline":
@@ -622,7 +613,9 @@ def main():
     elif rank == 0 and world == 1 and not args.no_cpu_baseline and wl == "generic" and not args.plugin:
         cpu = cpu_baseline_generic(min(args.cpu_seconds, 5.0))
 
-    if rank == 0:
+    def emit(gather_ms, gather_err):
+        if rank != 0:
+            return
         line = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -649,6 +642,7 @@ def main():
                              "dsp_render_stft_sharded), no data-path collective" if wl == "ch96k" else
                              "time-chunk per GPU, 4096-sample halo, no data-path collective"),
                 "render_gather_ms": None if gather_ms is None else round(gather_ms, 3),
+                "render_gather_error": gather_err,
                 "render_gather": ("one pass of the product's pipelined sharded driver with the gather of every "
                                   "rank's render and spectra to rank 0 (dsp_render_stft_sharded over "
                                   + ("gloo, the one-GPU rehearsal)" if rehearsal else "RCCL / xGMI)")
@@ -679,7 +673,7 @@ def main():
                 "traffic": None if traffic is None else round(traffic / 1e9, 4),
                 "traffic_unit": "GB per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
                 "traffic_source": traffic_src,
-                "traffic_kernel": traffic_inst if traffic is not None else None,
+                "traffic_kernel": traffic_inst if traffic_src is not None else None,
                 "traffic_over_algorithmic": (round(traffic / bytes_per_launch, 5)
                                              if traffic is not None and bytes_per_launch else None),
                 "kernel_avg_ms": round(kernel_avg_ms, 5),
@@ -705,6 +699,44 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
+
+    if gather_pending:
+        # a watchdog: a gather that never completes (a peer lost, a transport
+        # hang) must not take the measured line with it -- every rank stops
+        # after --gather-timeout s, rank 0 printing the line with the error
+        import threading
+
+        def _expired():
+            print(f"rank {rank}: the gather pass exceeded {args.gather_timeout} s", file=sys.stderr, flush=True)
+            emit(None, f"timed out after {args.gather_timeout} s")
+            os._exit(0)
+        dog = threading.Timer(args.gather_timeout, _expired)
+        dog.daemon = True
+        dog.start()
+        try:
+            comm = d.shard.TorchComm(device=local) if rehearsal else d.shard.RcclComm.from_torch(device=local)
+            Ctot = world if wl == "ch96k" else CH
+            Lfile = L if wl == "ch96k" else world * L
+            Lpad = d.num_blocks(Lfile, B) * B
+            Ftot = d.stft_frames(Lpad, N_FFT, HOP)
+            all_out = torch.empty((Ctot, Lpad), device=dev) if rank == 0 else None
+            all_mag = torch.empty((Ctot, Ftot, K_BINS), device=dev) if rank == 0 else None
+            torch.cuda.synchronize()
+            dist.barrier()
+            tg = time.perf_counter()
+            d.shard.render_stft_sharded(x, Lfile, Ctot, B, float(sr), plugin, sh, out, mag, comm=comm, root=0,
+                                        all_out=all_out, all_mag=all_mag, chunk=1 << 24, N=N_FFT, H=HOP,
+                                        window=d.DSP_WIN_HANN, K=K_BINS)
+            torch.cuda.synchronize()
+            dist.barrier()
+            gather_ms = (time.perf_counter() - tg) * 1e3
+            comm.close()
+            del all_out, all_mag
+        except Exception as e:  # reported in the line; `value` stands on its own
+            gather_ms, gather_err = None, f"{type(e).__name__}: {e}"
+            print(f"rank {rank}: gather pass failed: {gather_err}", file=sys.stderr, flush=True)
+        dog.cancel()
+    emit(gather_ms, gather_err)
     if world > 1:
         dist.destroy_process_group()
 
