@@ -606,12 +606,6 @@ static int render_device(const float *const *in, uint32_t in_ch, uint64_t L, flo
                 A.H = map.olsH;
                 A.h2048 = v2f{map.olsH2048[0], map.olsH2048[1]};
                 A.tw = tw;
-#ifdef DSPB_AB_BUILD
-                if (pk_options() & (kFirAbPersist4 | kFirAbPersist8)) {
-                    if ((st = launch_fir_fft_ab(A, cn, pk_options(), s))) return st;
-                    continue;
-                }
-#endif
                 if ((st = launch_fir_fft(A, cn, s))) return st;
             }
             return DSP_OK;

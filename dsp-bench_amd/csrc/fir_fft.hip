@@ -211,68 +211,6 @@ static uint64_t interior_end(const FirFftArgs &A) {
     return fe;
 }
 
-#ifdef DSPB_AB_BUILD
-// A/B (tools build): persistent waves.  A launch of one wave per frame starts
-// every wave slot on a load at once and, the frames being equal work, keeps
-// the two waves of a SIMD in step: they load together and compute together.
-// Here the grid is one wave per slot (WPB-wave groups, 8 waves per CU), each
-// wave walks units u = its index + k * (waves in the grid), u = ch * F + f;
-// STAGGER: the second half of a group's waves (WPB = 8: the SIMD's second
-// wave) sleeps STAGGER x 8128 cycles first, so its loads meet the other
-// wave's arithmetic.
-template <int WPB>
-__global__ __launch_bounds__(64 * WPB, 8 / WPB) void fir_fft_persist_kernel(FirFftArgs A, uint64_t fe, uint32_t C,
-                                                                           uint32_t stagger) {
-    __shared__ __attribute__((aligned(16))) float lds_all[WPB][64 * 33];
-    __shared__ float4 hs[2048];
-    {
-        const float4 *H4 = reinterpret_cast<const float4 *>(A.H);
-#pragma unroll
-        for (int i = 0; i < 32 / WPB; ++i) {
-            const uint32_t g = threadIdx.x + 64u * WPB * (uint32_t)i;
-            const uint32_t ka = g >> 7, ln = (g & 127u) >> 1, h = g & 1u;
-            hs[(2u * ka + h) * 64u + ln] = H4[g];
-        }
-        __syncthreads();
-    }
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (wave >= WPB / 2)
-        for (uint32_t i = 0; i < stagger; ++i) __builtin_amdgcn_s_sleep(127);
-    const uint64_t nw = (uint64_t)gridDim.x * WPB, units = (uint64_t)C * A.F;
-    for (uint64_t u = (uint64_t)xcd_remap(blockIdx.x, gridDim.x) * WPB + wave; u < units; u += nw) {
-        const uint32_t ch = (uint32_t)(u / A.F);
-        const uint64_t f = u - (uint64_t)ch * A.F;
-        // an opaque copy of the lane index per frame: otherwise the compiler
-        // hoists the frame's lane-dependent offsets out of the loop and
-        // spills them
-        uint32_t ln = lane;
-        asm volatile("" : "+v"(ln));
-        if (f == 0 || f >= fe) fir_fft_frame<true>(A, f, ch, lds_all[wave], hs, ln);
-        else fir_fft_frame<false>(A, f, ch, lds_all[wave], hs, ln);
-    }
-}
-
-int launch_fir_fft_ab(const FirFftArgs &A, uint32_t C, int opt, hipStream_t s) {
-    if (A.F == 0 || C == 0) return DSP_OK;
-    const uint64_t fe = interior_end(A);
-    int dev = 0, cus = 0;
-    DSPB_HIP(hipGetDevice(&dev));
-    DSPB_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    const uint32_t stagger = (uint32_t)(opt >> 20) & 3u;
-    const uint64_t units = (uint64_t)C * A.F;
-    if (opt & kFirAbPersist8) {
-        const uint64_t g = std::min<uint64_t>((uint64_t)cus, (units + 7) / 8);
-        hipLaunchKernelGGL(fir_fft_persist_kernel<8>, dim3((uint32_t)g), dim3(512), 0, s, A, fe, C, stagger);
-    } else {
-        const uint64_t g = std::min<uint64_t>(2ull * (uint64_t)cus, (units + 3) / 4);
-        hipLaunchKernelGGL(fir_fft_persist_kernel<4>, dim3((uint32_t)g), dim3(256), 0, s, A, fe, C, stagger);
-    }
-    DSPB_HIP(hipGetLastError());
-    return DSP_OK;
-}
-#endif
-
 int launch_fir_fft(const FirFftArgs &A, uint32_t C, hipStream_t s) {
     if (A.F == 0 || C == 0) return DSP_OK;
     const uint64_t fe = interior_end(A);

@@ -93,12 +93,6 @@ struct FirFftArgs {
     const v2f *tw;       // T8192 + lane-major stage twiddles (capi.cpp get_tw)
 };
 int launch_fir_fft(const FirFftArgs &A, uint32_t C, hipStream_t s);
-#ifdef DSPB_AB_BUILD
-// A/B (tools build, dsp_stft_pk_ab_options bits): persistent overlap-save
-// grids of 4- or 8-wave groups; bits 20-21: the stagger (fir_fft.hip)
-enum { kFirAbPersist4 = 1 << 18, kFirAbPersist8 = 1 << 19 };
-int launch_fir_fft_ab(const FirFftArgs &A, uint32_t C, int opt, hipStream_t s);
-#endif
 int launch_fir(const float *x, uint64_t L, float *y, uint64_t Ly, const float *h8, uint32_t T8,
                bool y_aligned16, hipStream_t s);
 int launch_minmax(const float *x, uint64_t n, uint32_t P, float *vmax, float *vmin, hipStream_t s);

@@ -9,7 +9,11 @@ cycles first).
 
 Each round runs each option for 20 launches after 10 warm ones, rotating 4
 inputs as bench.py does, and records the average launch time from
-libdspbench's own HIP events; round 0 checks the renders are bit-identical."""
+libdspbench's own HIP events; round 0 checks the renders against opt 0.
+The variants were measured and removed (profiles/r03_fir_persist_ab.txt): the
+persistent grids are in commit 91c8a58's tools build, the 3-waves-per-SIMD
+build was never committed (fir_fft.hip at 12-wave groups with the stage
+twiddles loaded inside each transform)."""
 import ctypes as C
 import hashlib
 import os
@@ -63,8 +67,11 @@ for rnd in range(rounds):
                 print(f"opt {o}: render sha1 {hashlib.sha1(ref.cpu().numpy().tobytes()).hexdigest()[:16]}", flush=True)
             else:
                 same = torch.equal(out, ref)
-                print(f"opt {o}: bit-identical to opt {OPTS[0]}: {same}", flush=True)
-                assert same, f"option {o} changed the render"
+                rel = float((out - ref).abs().max() / ref.abs().max())
+                nbad = int((out != ref).sum())
+                print(f"opt {o}: bit-identical to opt {OPTS[0]}: {same} (peak-relative max diff {rel:.3g}, "
+                      f"{nbad} samples differ)", flush=True)
+                assert rel <= 2e-6, f"option {o} changed the render beyond the overlap-save bar"
         for _ in range(10):
             step()
         torch.cuda.synchronize()
