@@ -105,12 +105,17 @@ def pmc_traffic(workload: str, alg_bytes: float):
     FETCH_SIZE / WRITE_SIZE in separate passes, tools/pmc_summary.py --json:
     FETCH_SIZE x2 + WRITE_SIZE per MI355X_MICROARCH.md), or (None, None, None).
     The summaries are of the default sizes: a run of another size (--minutes)
-    gets no traffic figure rather than another launch's."""
+    gets no traffic figure rather than another launch's (within 0.9-1.5x of
+    the algorithmic bytes counts as the same launch)."""
     import glob
     inst = PK_INST.get(workload)
     if inst is None:
         return None, None, None
-    for path in sorted(glob.glob(os.path.join(REPO, "profiles", f"r*_pmc_{workload}.json")), reverse=True):
+    # the workload's own summaries first, then any other of the same
+    # instantiation (ch96k runs the headline's kernel on as many frames)
+    own = sorted(glob.glob(os.path.join(REPO, "profiles", f"r*_pmc_{workload}.json")), reverse=True)
+    rest = sorted(set(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_*.json"))) - set(own), reverse=True)
+    for path in own + rest:
         doc = json.load(open(path))
         for name, m in doc.get("kernels", {}).items():
             if name.endswith(inst) and "hbm_bytes" in m:

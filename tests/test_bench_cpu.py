@@ -1,0 +1,39 @@
+"""bench.py's host-side helpers (CPU): the PMC traffic figure applies only to
+a launch of the profiled size, and every workload with an instantiation
+names a committed summary."""
+import importlib.util
+import os
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def bench():
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+HEADLINE_BYTES = 2 * 42186 * (4 * 4096 + 4 * 4097)  # C * F * (4H + 4K), 1 h stereo at 48 kHz
+
+
+def test_pmc_traffic_of_the_profiled_launch(bench):
+    t, src, inst = bench.pmc_traffic("headline", HEADLINE_BYTES)
+    assert t is not None and src.startswith("profiles/") and inst
+    assert 0.99 < t / HEADLINE_BYTES < 1.01
+
+
+def test_pmc_traffic_refuses_another_size(bench):
+    # a 5-minute run (one twelfth of the bytes) must not borrow the 1 h launch's figure
+    t, src, inst = bench.pmc_traffic("headline", HEADLINE_BYTES / 12)
+    assert t is None and "another size" in src and inst
+
+
+def test_every_instantiation_has_a_summary(bench):
+    for wl, inst in bench.PK_INST.items():
+        _, src, got = bench.pmc_traffic(wl, 0)  # size 0: no figure, but the summary is found
+        assert got == inst
+        assert src is not None, f"{wl}: no committed PMC summary names {inst}"
