@@ -402,7 +402,8 @@ def main():
         workload = (f"FIR render, 1024 taps = compute_IR(IR_test)[0:1024], B=512, {minutes:g} min of "
                     f"48 kHz stereo per GPU (cfg 3b), {'FFT overlap-save' if ols else 'direct form'}")
         if ols:  # HBM-bound: the library times it with read + write bytes
-            kname = "fir_fft_kernel (8192-pt overlap-save, 7168 outputs / frame)"
+            kname = ("fir_pair_kernel (overlap-save, a channel pair as one complex 4096-pt frame, "
+                     "3072 outputs per channel per frame)")
         else:
             kname = "fir_kernel (packed fp32 direct form)"
             alg_flops = 2.0 * 1024 * CH * nb * B

@@ -353,9 +353,10 @@ static bool aligned(const void *p, size_t a) { return ((uintptr_t)p % a) == 0; }
 // fir_fft.hip: for ka < 16 and lane l, 8 floats
 //   (Re H[k1], Re H[k2], Im H[k1], Im H[k2], Re H[M-k1], Re H[M-k2], Im H[M-k1], Im H[M-k2])
 // with k1 = l + 64 ka, k2 = k1 + 1024, M = 4096; then H[2048] (re, im).
-static void ols_table(const float *taps, uint32_t T, float *out) {
-    const int n = 8192;
-    std::vector<double> re(n, 0.0), im(n, 0.0);
+// FFT_n(taps zero-padded) in float64 (iterative radix-2, forward e^-i)
+static void taps_spectrum(const float *taps, uint32_t T, int n, std::vector<double> &re, std::vector<double> &im) {
+    re.assign(n, 0.0);
+    im.assign(n, 0.0);
     for (uint32_t i = 0; i < T; ++i) re[i] = taps[i];
     for (int i = 1, j = 0; i < n; ++i) {  // iterative radix-2, forward (e^-i)
         int bit = n >> 1;
@@ -377,6 +378,12 @@ static void ols_table(const float *taps, uint32_t T, float *out) {
             }
         }
     }
+}
+
+// the 8192-point table of fir_fft_kernel (kOlsHop 7168, one channel per frame)
+static void ols_table(const float *taps, uint32_t T, float *out) {
+    std::vector<double> re, im;
+    taps_spectrum(taps, T, 8192, re, im);
     const double sc = 1.0 / 16384.0;
     for (int ka = 0; ka < 16; ++ka)
         for (int l = 0; l < 64; ++l) {
@@ -389,6 +396,23 @@ static void ols_table(const float *taps, uint32_t T, float *out) {
         }
     out[8192] = (float)(re[2048] * sc);
     out[8193] = (float)(im[2048] * sc);
+}
+
+// the 4096-point table of fir_pair_kernel (two channels as one complex
+// signal): H = FFT_4096(taps) / 4096 (the inverse's scale), as float4
+// [q][lane] = (Re H[l + 64 q], Re H[l + 64 (q + 32)], Im .., Im ..), the
+// pairing of the transform's packed last combine
+static void pair_table(const float *taps, uint32_t T, float *out) {
+    std::vector<double> re, im;
+    taps_spectrum(taps, T, 4096, re, im);
+    const double sc = 1.0 / 4096.0;
+    for (int q = 0; q < 32; ++q)
+        for (int l = 0; l < 64; ++l) {
+            const int k0 = l + 64 * q, k1 = k0 + 2048;
+            float *o = out + 4 * (64 * q + l);
+            o[0] = (float)(re[k0] * sc); o[1] = (float)(re[k1] * sc);
+            o[2] = (float)(im[k0] * sc); o[3] = (float)(im[k1] * sc);
+        }
 }
 
 // IR_test (build/IR_test.cpp:47-58) runs `gain -= step` in double from the
@@ -484,9 +508,13 @@ static int plugin_map(const dsp_plugin *p, uint32_t B, int dev, hipStream_t s, S
                 if (e.taps == key) { ft = &e; break; }
             if (!ft) {
                 if (int st = refuse_capture(s, "a FIR filter's device taps")) return st;
-                std::vector<float> h(T8 + 8192 + 2, 0.f);
+                // [taps, T8][8192-point table, 8194 (+ 2 pad)][4096-point pair table, 8192]
+                std::vector<float> h(T8 + 8196 + 8192, 0.f);
                 std::memcpy(h.data(), key.data(), 4 * (size_t)T);
-                if (T <= 1025) ols_table(h.data(), T, h.data() + T8);
+                if (T <= 1025) {
+                    ols_table(h.data(), T, h.data() + T8);
+                    pair_table(h.data(), T, h.data() + T8 + 8196);
+                }
                 float *d = nullptr;
                 DSPB_HIP(hipMalloc(&d, sizeof(float) * h.size()));
                 if (int st = upload_table(d, h.data(), sizeof(float) * h.size())) {
@@ -506,6 +534,7 @@ static int plugin_map(const dsp_plugin *p, uint32_t B, int dev, hipStream_t s, S
         m->ntaps8 = T8;
         m->ntaps = T;
         m->olsH = ft->dev + T8;
+        m->pairH = ft->dev + T8 + 8196;  // 16-byte aligned: T8 and 8196 are multiples of 4
         m->olsH2048[0] = ft->h2048r;
         m->olsH2048[1] = ft->h2048i;
         return DSP_OK;
@@ -584,7 +613,10 @@ static int render_device(const float *const *in, uint32_t in_ch, uint64_t L, flo
     }
     if (map.kind == MapKind::Fir) {  // convolution from the start of the file
         if (start != 0 || goff != 0) return invalid("FIR render: whole files only (sample_offset 0)");
-        if (map.ntaps <= 1025 && !map.fir_direct) {  // overlap-save, 8192-point frames
+        if (map.ntaps <= 1025 && !map.fir_direct) {
+            // overlap-save: channel pairs as one complex signal (fir_pair_kernel,
+            // 4096-point frames); an odd last channel on its own
+            // (fir_fft_kernel, 8192-point real frames)
             const v2f *tw = nullptr;
             int dev = 0;
             DSPB_HIP(hipGetDevice(&dev));
@@ -592,21 +624,39 @@ static int render_device(const float *const *in, uint32_t in_ch, uint64_t L, flo
             if (st) return st;
             for (uint32_t c0 = 0; c0 < C; c0 += kMaxChannels) {
                 const uint32_t cn = (C - c0) < (uint32_t)kMaxChannels ? (C - c0) : kMaxChannels;
-                FirFftArgs A{};
-                for (uint32_t j = 0; j < cn; ++j) {
-                    A.out.p[j] = out[c0 + j];
-                    if (c0 + j < in_ch) {
-                        A.in.p[j] = in[c0 + j];
-                        A.in_ch = j + 1;
+                const uint32_t np = cn & ~1u;  // (kMaxChannels is even)
+                if (np) {
+                    FirFftArgs A{};
+                    for (uint32_t j = 0; j < np; ++j) {
+                        A.out.p[j] = out[c0 + j];
+                        if (c0 + j < in_ch) {
+                            A.in.p[j] = in[c0 + j];
+                            A.in_ch = j + 1;
+                        }
                     }
+                    A.L = L;
+                    A.Ly = end;
+                    A.F = (end + kPairHop - 1) / kPairHop;
+                    A.H = map.pairH;
+                    A.tw = tw;
+                    if ((st = launch_fir_pair(A, np, s))) return st;
                 }
-                A.L = L;
-                A.Ly = end;
-                A.F = (end + 7167) / 7168;
-                A.H = map.olsH;
-                A.h2048 = v2f{map.olsH2048[0], map.olsH2048[1]};
-                A.tw = tw;
-                if ((st = launch_fir_fft(A, cn, s))) return st;
+                if (cn & 1) {
+                    const uint32_t c = c0 + cn - 1;
+                    FirFftArgs A{};
+                    A.out.p[0] = out[c];
+                    if (c < in_ch) {
+                        A.in.p[0] = in[c];
+                        A.in_ch = 1;
+                    }
+                    A.L = L;
+                    A.Ly = end;
+                    A.F = (end + 7167) / 7168;
+                    A.H = map.olsH;
+                    A.h2048 = v2f{map.olsH2048[0], map.olsH2048[1]};
+                    A.tw = tw;
+                    if ((st = launch_fir_fft(A, 1, s))) return st;
+                }
             }
             return DSP_OK;
         }

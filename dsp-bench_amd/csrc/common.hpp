@@ -35,6 +35,7 @@ struct SampleMap {
     uint32_t fir_direct; // Fir: the caller asked for the direct form (DSP_EXEC_FIR_DIRECT)
     const float *olsH;   // Fir: FFT(taps)/16384 in fir_fft.hip's lane-major pair layout
     float olsH2048[2];   // Fir: H[2048]/16384
+    const float *pairH;  // Fir: FFT_4096(taps)/4096 in fir_pair_kernel's layout (fir_fft.hip)
     void *module;        // Generic: the dsp_module running the plugin's own audio_callback
     const void *gparams; // Generic: host Parameters blob
     uint32_t gparams_size;

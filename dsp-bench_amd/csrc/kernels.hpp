@@ -91,8 +91,13 @@ struct FirFftArgs {
     const float *H;      // FFT(taps)/16384, lane-major pairs (fir_fft.hip)
     v2f h2048;           // H[2048]
     const v2f *tw;       // T8192 + lane-major stage twiddles (capi.cpp get_tw)
+    uint32_t nout;       // fir_pair_kernel: output channels in `out` (set by launch_fir_pair)
 };
 int launch_fir_fft(const FirFftArgs &A, uint32_t C, hipStream_t s);
+// two channels per frame as one complex signal, 4096-point frames, hop 3072
+// (C even; F = ceil(Ly / kPairHop); H = SampleMap::pairH; h2048 unused)
+constexpr uint32_t kPairHop = 3072;
+int launch_fir_pair(const FirFftArgs &A, uint32_t C, hipStream_t s);
 int launch_fir(const float *x, uint64_t L, float *y, uint64_t Ly, const float *h8, uint32_t T8,
                bool y_aligned16, hipStream_t s);
 int launch_minmax(const float *x, uint64_t n, uint32_t P, float *vmax, float *vmin, hipStream_t s);

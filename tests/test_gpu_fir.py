@@ -23,7 +23,10 @@ def cfg3b_taps():
     return G["ir_IR_test"][0][:1024].copy()   # compute_IR(IR_test) of the reference plugin
 
 
-OLS_TOL = 2e-6  # overlap-save: max |y - y64| <= OLS_TOL * max |y64| (fp32 FFT round trip)
+# overlap-save: max |y - y64| <= OLS_TOL * max |y64| (fp32 FFT round trip); the
+# channels of a pair (fir_pair_kernel) share one complex transform, so for them
+# the max is the pair's (test_gpu_fir_pair_shares_its_rounding)
+OLS_TOL = 2e-6
 
 
 @pytest.fixture(params=[1, 2], ids=["direct", "ols"])
@@ -79,6 +82,47 @@ def test_gpu_fir_channels_and_missing_input(torch_cuda, oracle, fir_method):
     out = d.render_offline(torch_cuda.from_numpy(x).cuda(), 3, 512, 48000.0, fplug(taps, fir_method)).cpu().numpy()
     check_fir(oracle, out[0], x[0], taps, out.shape[1], fir_method)
     assert not out[1:].any()   # extra channels: zero input through the FIR
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("C,in_ch", [(1, 1), (3, 3), (4, 4), (5, 4), (4, 3), (17, 17)])
+@pytest.mark.parametrize("L,B", [(3073, 64), (6144, 512), (12_289, 1)])
+def test_gpu_fir_channel_counts(torch_cuda, oracle, fir_method, C, in_ch, L, B):
+    """Overlap-save runs channel pairs as one complex signal (fir_pair_kernel)
+    and an odd last channel on its own (fir_fft_kernel): odd and even counts,
+    a pair with its second channel missing, more than one launch's 16
+    channels, lengths at and beside the pair kernel's 3072-sample hop."""
+    rng = np.random.default_rng(C * 1000 + L)
+    x = rng.uniform(-1, 1, (in_ch, L)).astype(np.float32)
+    taps = (rng.standard_normal(1024) / 32).astype(np.float32)
+    out = d.render_offline(torch_cuda.from_numpy(x).cuda(), C, B, 48000.0, fplug(taps, fir_method)).cpu().numpy()
+    Ly = -(-L // B) * B
+    assert out.shape == (C, Ly)
+    for c in range(C):
+        if c < in_ch:
+            check_fir(oracle, out[c], x[c], taps, Ly, fir_method)
+        else:
+            assert not out[c].any()
+
+
+@pytest.mark.gpu
+def test_gpu_fir_pair_shares_its_rounding(torch_cuda, oracle):
+    """Overlap-save transforms a channel pair as one complex signal, so a
+    channel's rounding error is bounded by the PAIR's peak: a quiet channel
+    beside a loud one (60 dB down), and a silent one, stay within OLS_TOL of
+    the pair's peak; a channel the file lacks is exact zeros."""
+    rng = np.random.default_rng(12)
+    L = 50_000
+    loud = rng.uniform(-1, 1, L).astype(np.float32)
+    x = np.stack([loud, (rng.uniform(-1, 1, L) * 1e-3).astype(np.float32), np.zeros(L, np.float32)])
+    taps = cfg3b_taps()
+    out = d.render_offline(torch_cuda.from_numpy(x).cuda(), 4, 512, 48000.0, fplug(taps, 2)).cpu().numpy()
+    y64 = [oracle.fir_f64(x[c], taps, out.shape[1]) for c in range(3)]
+    peak01 = max(np.max(np.abs(y64[0])), np.max(np.abs(y64[1])))
+    for c in (0, 1):
+        assert np.max(np.abs(out[c] - y64[c])) <= OLS_TOL * peak01
+    # channels 2 (silent) and 3 (missing) form the second pair: both exact zeros
+    assert not out[2].any() and not out[3].any()
 
 
 @pytest.mark.gpu

@@ -10,7 +10,8 @@ cycles first).
 Each round runs each option for 20 launches after 10 warm ones, rotating 4
 inputs as bench.py does, and records the average launch time from
 libdspbench's own HIP events; round 0 checks the renders against opt 0.
-The variants were measured and removed (profiles/r03_fir_persist_ab.txt): the
+The variants were measured and removed (profiles/r03_fir_persist_ab.txt,
+r03_fir_pair_ab.txt -- the pair kernel is now the product's): the
 persistent grids are in commit 91c8a58's tools build, the 3-waves-per-SIMD
 build was never committed (fir_fft.hip at 12-wave groups with the stage
 twiddles loaded inside each transform)."""
