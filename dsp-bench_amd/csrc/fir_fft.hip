@@ -315,6 +315,9 @@ __device__ __forceinline__ void fir_pair_frame(const FirFftArgs &A, uint64_t f, 
     // the rounding of the other channel's transform, not silence)
     const uint32_t c1 = c0 + 1;
     const bool two = c1 < A.nout;  // (wave-uniform)
+    // the lane index through an opaque copy: the stores' offsets are formed
+    // here, not hoisted to the kernel's start and held across the frame (250 -> 214 VGPRs)
+    asm volatile("" : "+v"(lane));
     float *o0 = A.out.p[c0] + f * kPairHop;
     float *o1 = two ? A.out.p[c1] + f * kPairHop : o0;
     if (f * kPairHop + kPairHop <= A.Ly) {
