@@ -176,3 +176,46 @@ def test_render_loop_random_case(torch_cuda, oracle, seed):
     assert gcur == wcur, case
     got = got.cpu().numpy()
     assert np.array_equal(got.view(np.uint32), np.asarray(want, np.float32).view(np.uint32)), case
+
+
+# ---- the FIR (DSP_PLUGIN_FIR, build-defined cfg 3b) -------------------------
+# Random taps count (both kernels: overlap-save for T <= 1025, the direct form
+# above and when asked), channel counts (overlap-save pairs channels as one
+# complex signal, an odd last one runs alone), file channels, lengths and
+# block sizes, against the float64 convolution.  Bars as test_gpu_fir.py: the
+# direct form within its rigorous bound, overlap-save within OLS_TOL of the
+# pair's peak.
+from test_gpu_fir import OLS_TOL, U  # noqa: E402
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_fir_random_case(torch_cuda, oracle, seed):
+    r = np.random.default_rng(5000 + seed)
+    T = int(r.choice([1, 2, 15, 16, 17, 255, 1023, 1024, 1025, 1026, 2048, int(r.integers(1, 2049))]))
+    direct = bool(r.integers(2)) if T <= 1025 else True
+    C_out = int(r.integers(1, 7))
+    C_in = int(r.integers(0, C_out + 2))
+    L = int(r.integers(1, 40_000))
+    B = int(r.choice([1, 7, 64, 512, 1000, 4096]))
+    taps = (r.standard_normal(T) / np.sqrt(T)).astype(np.float32)
+    x = r.uniform(-1, 1, (max(C_in, 1), L)).astype(np.float32)[:C_in]
+    file = torch_cuda.from_numpy(np.ascontiguousarray(x)).cuda() if C_in else None
+    Ly = -(-L // B) * B
+    dst = torch_cuda.empty((C_out, Ly), device="cuda")
+    out = d.render_offline(file, C_out, B, 48000.0, d.Plugin.fir(taps, direct=direct), out=dst,
+                           L_file=L).cpu().numpy()
+    case = (T, direct, C_out, C_in, L, B)
+    assert out.shape == (C_out, Ly), case
+    y64 = [oracle.fir_f64(x[c] if c < C_in else None, taps, Ly) for c in range(C_out)]
+    for c in range(C_out):
+        if c >= C_in:
+            assert not out[c].any(), case  # a channel the file lacks: exact zeros
+            continue
+        err = np.abs(out[c].astype(np.float64) - y64[c])
+        if direct:
+            bound = oracle.fir_f64(np.abs(x[c]), np.abs(taps), Ly) * (T + 1) * U
+            assert np.all(err <= bound + 1e-30), case
+        else:
+            pair = [p for p in (c - c % 2, c - c % 2 + 1) if p < C_out and p < C_in]
+            peak = max(float(np.max(np.abs(y64[p]))) for p in pair)
+            assert float(np.max(err)) <= OLS_TOL * max(peak, 1e-30), case
