@@ -25,7 +25,7 @@ xs = [x] + ([x.clone() for _ in range(3)] if MODE == "fir" else [])
 it = [0]
 def nx():
     it[0] += 1
-    return xs[it[0] % len(xs)]
+    return xs[it[0] %% len(xs)]
 nb = d.num_blocks(L_, 512)
 F = d.stft_frames(nb * 512, 8192, 4096)
 out = torch.empty((2, nb * 512), device="cuda"); mag = torch.empty((2, F, 4097), device="cuda")
