@@ -1,11 +1,6 @@
 // stft_pk.hip -- the 8192-point STFT dispatcher and the fused IR_test
 // kernels of the headline (PER path); the kernel is in stft_pk.hpp.
 #include "stft_pk.hpp"
-#include "stft_persist.hpp"
-
-#ifndef DSPB_PERSIST
-#define DSPB_PERSIST 0
-#endif
 
 namespace dspb {
 
@@ -63,12 +58,6 @@ int launch_stft8192_pk(const Stft8kArgs &A, uint32_t C, bool fused, int opt, hip
         const uint32_t per = A.map.B <= 128u ? 1u : A.map.B / 128u;
 #ifdef DSPB_AB_BUILD
         if (per == 4 && opt) return launch_pk_ab(A, fused, opt, grid, stream);  // A/B at the headline shape
-#endif
-#if DSPB_PERSIST
-        if (per == 1 || per == 2 || per == 4 || per == 8 || per == 16) {
-            const int st = launch_per_persist<DSPB_PERSIST == 2>(A, C, per, tail, stream);
-            if (st != DSP_ERR_INVALID) return st;
-        }
 #endif
 #define DSPB_PK_PER(p) \
     hipLaunchKernelGGL((stft8192_pk_kernel<kSrcRender, kKHalf, MapKind::Ramp, true, true, p, kPkPerOpt>), grid_per, \
