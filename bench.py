@@ -82,10 +82,39 @@ def parse():
                          "planar stereo into an interleaved int16 / int24 WAV payload")
     ap.add_argument("--plugin", default=None, choices=["gain_test", "IR_test"],
                     help="generic / generic_stft: the reference plugin source (default gain_test / IR_test)")
+    ap.add_argument("--ir-plugin", default="source", choices=["source", "enum"],
+                    help="headline / ch96k: source = the reference's IR_test.cpp compiled unchanged for gfx950 "
+                         "(dsp-bench_amd/modules/mod_IR_test.co) and dispatched through its probed block class "
+                         "(the default: the plugin's own code on the measured path); enum = DSP_PLUGIN_IR_RAMP, "
+                         "the library's restatement of the same callback (closed-form ramp)")
     ap.add_argument("--no-specialize", action="store_true",
                     help="generic / generic_stft: run the plugin's callback on every block "
                          "(DSP_EXEC_NO_SPECIALIZE) instead of its probed block class")
     return ap.parse_args()
+
+
+def source_plugin(d, pname: str, C: int, B: int, sr: int, specialize: bool = True):
+    """A reference plugin source compiled unchanged by the product's plugin
+    compiler (hiprtc -> gfx950, dsp-bench_amd/modules/mod_<pname>.co, built by
+    tools/make_plugin_modules.py) as a DSP_PLUGIN_GENERIC plugin with its
+    default Parameters.  Returns (module, plugin, block class); the module
+    must outlive every call that uses the plugin."""
+    # (DSPB_MODULES_DIR: A/B builds of the driver, tools/build_lds_variants.sh)
+    mdir = os.environ.get("DSPB_MODULES_DIR", os.path.join(REPO, "dsp-bench_amd", "modules"))
+    with open(os.path.join(mdir, f"mod_{pname}.co"), "rb") as f:
+        gmod = d.module.Module(f.read())
+    gparams = gmod.default_parameters()
+    gmod.initialize_state(gparams, C, float(sr))
+    gplug = gmod.plugin(gparams, pname, specialize=specialize)
+    block_class = "callback" if not specialize else gmod.block_class(gparams, C, B, float(sr))[0]
+    return gmod, gplug, block_class
+
+
+def source_plugin_name(pname: str, block_class: str) -> str:
+    return (f"{pname}.cpp (DSP_PLUGIN_GENERIC, compiled unchanged from the reference source; block class "
+            f"{block_class}: " + {"table": "its own callback's block, tiled, in the fused kernel",
+                                  "gain": "the gain its callback gives, in the gain map",
+                                  "callback": "the callback on every block"}[block_class] + ")")
 
 
 # the instantiation each workload's dominant launch runs (stft_pk.hip /
@@ -347,6 +376,20 @@ def main():
     mag = (torch.empty((CH, max(F, 1), K_BINS), device=dev)
            if wl in ("headline", "stft96k", "ch96k", "generic_stft", "gain_stft") else None)
     plugin = d.Plugin.ir_test(0.9, 0.002) if wl in ("headline", "ch96k") else d.Plugin.gain_test(0.2)
+    block_class = None
+    ir_note = None
+    if (wl in ("headline", "ch96k") and args.ir_plugin == "source" and not os.path.exists(
+            os.path.join(os.environ.get("DSPB_MODULES_DIR", os.path.join(REPO, "dsp-bench_amd", "modules")),
+                         "mod_IR_test.co"))):
+        # the module is compiled from /root/reference/build/IR_test.cpp by
+        # build(); a tree built without the reference has only the enum
+        ir_note = "mod_IR_test.co not built (no reference source at build time): DSP_PLUGIN_IR_RAMP"
+        print(f"bench: {ir_note}", file=sys.stderr, flush=True)
+    if wl in ("headline", "ch96k") and args.ir_plugin == "source" and ir_note is None:
+        # the reference's IR_test.cpp (default Parameters {0.9, 0.002}, the
+        # enum's values) compiled unchanged; its block class is probed once by
+        # running its own callback, and the fused kernel renders that block
+        hmod, plugin, block_class = source_plugin(d, "IR_test", CH, B, sr, specialize=not args.no_specialize)
     stream = torch.cuda.current_stream(dev)
     soff = sh.start
 
@@ -356,7 +399,8 @@ def main():
     alg_desc = ("fused: C*F*(4H + 4K) B (render write + |X| write; IR_test reads no input); "
                 "memory: C*F*(4H + 4K) B (each sample read once + |X| write)")
     plug_name = plugin.name
-    block_class = None
+    if block_class is not None:
+        plug_name = source_plugin_name("IR_test", block_class)
     if wl == "headline":
         def step():
             d.render_stft(x, CH, B, float(sr), plugin, N=N_FFT, H=HOP, window=d.DSP_WIN_HANN,
@@ -364,6 +408,11 @@ def main():
         workload = ("IR_test render (B=512) + 8192-pt Hann STFT, hop 4096, 4097 bins, "
                     f"{minutes:g} min of 48 kHz stereo per GPU")
         kname = f"{KERNEL}<render> (fused render + window + FFT + |X|)"
+        if block_class == "table":
+            kname = (f"{KERNEL}<render> (fused render + window + FFT + |X|; the render is IR_test.cpp's own "
+                     "callback block, tiled)")
+        elif block_class == "callback":
+            kname = "dspb_render_lds (generic driver) then stft8192_pk<memory> on one stream"
     elif wl == "gain_stft":
         # the headline's shape with an input-dependent plugin: gain_test
         # (DSP_PLUGIN_GAIN) fused into the STFT wave, so every frame's hop is
@@ -420,18 +469,8 @@ def main():
         # gfx950, dsp-bench_amd/modules/mod_*.co, built by
         # tools/make_plugin_modules.py) and run by the generic driver
         pname = args.plugin or ("gain_test" if wl == "generic" else "IR_test")
-        # (DSPB_MODULES_DIR: A/B builds of the driver, tools/build_lds_variants.sh)
-        mdir = os.environ.get("DSPB_MODULES_DIR", os.path.join(REPO, "dsp-bench_amd", "modules"))
-        with open(os.path.join(mdir, f"mod_{pname}.co"), "rb") as f:
-            gmod = d.module.Module(f.read())
-        gparams = gmod.default_parameters()
-        gmod.initialize_state(gparams, CH, float(sr))
-        gplug = gmod.plugin(gparams, pname, specialize=not args.no_specialize)
-        block_class = "callback" if args.no_specialize else gmod.block_class(gparams, CH, B, float(sr))[0]
-        plug_name = (f"{pname}.cpp (DSP_PLUGIN_GENERIC, compiled unchanged from the reference source; block class "
-                     f"{block_class}: " + {"table": "its own callback's block, tiled, in the fused kernel",
-                                           "gain": "the gain its callback gives, in the gain map",
-                                           "callback": "the callback on every block"}[block_class] + ")")
+        gmod, gplug, block_class = source_plugin(d, pname, CH, B, sr, specialize=not args.no_specialize)
+        plug_name = source_plugin_name(pname, block_class)
         if wl == "generic":
             def step():
                 d.render_offline(x, CH, B, float(sr), gplug, out=out)
@@ -497,8 +536,8 @@ def main():
     torch.cuda.synchronize()
     # one kernel per step: the timed region's own stream events give its
     # average launch duration, and no per-launch events sit between launches
-    region_timed = (wl in ("headline", "ch96k", "gain_stft", "stft96k") or
-                    (wl == "generic_stft" and block_class != "callback")) and not args.launch_events
+    region_timed = (wl in ("headline", "ch96k", "gain_stft", "stft96k", "generic_stft") and
+                    block_class != "callback" and not args.launch_events)
     bytes_probe = 0
     if region_timed:  # the library's byte count of one launch, from the first call
         d.lib().dsp_kernel_timing(None, None, None)
@@ -642,6 +681,8 @@ def main():
                 "workload": workload,
                 "plugin": plug_name,
                 "block_class": block_class,
+                "ir_plugin": (None if wl not in ("headline", "ch96k") else
+                              ir_note or ("source" if args.ir_plugin == "source" else "enum")),
                 "samples_per_gpu": samples_per_rank,
                 "frames_per_gpu": CH * F if mag is not None else 0,
                 "sharding": ("one 96 kHz channel per GPU (a world-channel file, dsp_shard_plan CHANNELS, "

@@ -293,7 +293,7 @@ static int pk_options() { return 0; }
 // a closed-form IR ramp (plugin_map) leaves the block table unbuilt; every
 // fused path but stft_pk's PER path reads it
 static int ensure_ramp_table(const SampleMap &m, hipStream_t s) {
-    if (m.kind != MapKind::Ramp || !m.closed) return DSP_OK;
+    if (m.kind != MapKind::Ramp || m.closed != 1) return DSP_OK;  // 2: the table holds it already
     return launch_ramp_table(const_cast<float *>(m.table), m.B, (float)m.rg0, (float)m.rs, s);
 }
 
@@ -562,6 +562,11 @@ static int specialize_generic(SampleMap *m, uint32_t C, uint32_t B, hipStream_t 
         m->kind = MapKind::Ramp;  // value = table[(global sample) mod B]
         m->table = sp.table;
         m->closed = 0;
+        if (sp.affine) {  // ... = (float)fma(-i, rs, rg0), checked against every table value
+            m->closed = 2;  // (the table is the callback's own block: nothing to build)
+            m->rg0 = sp.rg0;
+            m->rs = sp.rs;
+        }
     } else if (sp.kind == kSpecGain) {
         m->kind = MapKind::Gain;
         m->a = sp.gain;

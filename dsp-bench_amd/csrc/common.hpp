@@ -43,7 +43,9 @@ struct SampleMap {
     // Ramp: table[i] = (float)(gain - i step) in closed form when the host
     // verified that IR_test's sequential f64 recurrence is exact for these
     // parameters and this B (capi.cpp ramp_closed_form); the table is then
-    // only built for kernels that still read it
+    // only built for kernels that still read it (closed = 1); closed = 2: a
+    // GENERIC plugin's block table (module.cpp affine_ramp) that the same
+    // closed form reproduces bit for bit -- the table exists already
     uint32_t closed;
     double rg0, rs;
 };

@@ -78,6 +78,11 @@ struct ModuleSpec {
     int kind = kSpecNone;
     float gain = 1.f;             // kSpecGain: y = gain x
     const float *table = nullptr; // kSpecTable: the block every block renders (B floats, every channel)
+    // kSpecTable: the block is an f64 ramp rounded to f32, table[i] =
+    // (float)fma(-i, rs, rg0) for every i < B, checked bit for bit on the host
+    // (the fused kernels then evaluate it instead of loading the table)
+    bool affine = false;
+    double rg0 = 0.0, rs = 0.0;
 };
 int module_specialize(::dsp_module *m, const void *params, uint32_t params_size, uint32_t C, uint32_t B, float sr,
                       hipStream_t s, ModuleSpec *out);

@@ -1235,6 +1235,49 @@ static uint32_t xorshift(uint32_t &x) {
 
 static bool same_bits(float a, float b) { return std::memcmp(&a, &b, 4) == 0; }
 
+// Is the callback's block t[0, B) an f64 ramp rounded to f32 -- t[i] =
+// (float)fma(-i, s, g0), the closed form common.hpp ramp_value evaluates --
+// for some (g0, s)?  IR_test.cpp (build/IR_test.cpp:47-58: `gain -= step` in
+// double from float Parameters) gives one whenever its recurrence is exact.
+// Candidates: g0 = t[0]; s = the float nearest the end-to-end slope and its
+// neighbours (a float Parameter widened to double), then the slope itself.
+// Only a candidate that reproduces all B values bit for bit is taken, so the
+// closed form renders exactly the callback's block.
+static bool affine_ramp(const float *t, uint32_t B, double *g0, double *s) {
+    const double a = t[0];
+    auto fits = [&](double sc) {
+        for (uint32_t i = 0; i < B; ++i)
+            if (!same_bits((float)std::fma(-(double)i, sc, a), t[i])) return false;
+        return true;
+    };
+    if (!std::isfinite(a)) return false;
+    if (B == 1) {
+        *g0 = a;
+        *s = 0.0;
+        return true;
+    }
+    const double slope = (a - (double)t[B - 1]) / (double)(B - 1);
+    if (!std::isfinite(slope)) return false;
+    std::vector<double> cand;
+    const float sf = (float)slope;
+    cand.push_back(sf);
+    float up = sf, dn = sf;
+    for (int k = 0; k < 8; ++k) {
+        up = std::nextafter(up, INFINITY);
+        dn = std::nextafter(dn, -INFINITY);
+        cand.push_back(up);
+        cand.push_back(dn);
+    }
+    cand.push_back(slope);
+    for (double sc : cand)
+        if (fits(sc)) {
+            *g0 = a;
+            *s = sc;
+            return true;
+        }
+    return false;
+}
+
 int module_specialize(dsp_module *m, const void *params, uint32_t params_size, uint32_t C, uint32_t B, float sr,
                       hipStream_t s, ModuleSpec *out) {
     *out = ModuleSpec{};
@@ -1295,6 +1338,7 @@ int module_specialize(dsp_module *m, const void *params, uint32_t params_size, u
         MOD_HIP(hipMemcpyAsync(t, d, sizeof(float) * B, hipMemcpyDeviceToDevice, s));
         res.kind = kSpecTable;
         res.table = t;
+        res.affine = affine_ramp(r.data(), B, &res.rg0, &res.rs);
     } else if (gain) {
         res.kind = kSpecGain;
         res.gain = g;

@@ -113,6 +113,32 @@ def test_ir_test_source_render_stft_fused(torch_cuda, oracle, B):
         assert float(np.max(np.abs(mm - m64).max(axis=1) / m64.max(axis=1))) <= PEAK_REL_TOL
 
 
+@pytest.mark.parametrize("soff", [0, 4096 * 37, 512 * 3 + 4096])
+def test_ir_test_source_is_the_headline(torch_cuda, soff):
+    """The bench's headline call (bench.py --ir-plugin source, the default):
+    IR_test.cpp compiled unchanged, 4097-bin Hann 8192 / 4096 STFT at a rank's
+    sample offset, gives the render and spectra of the stock fused IR_test
+    kernel (DSP_PLUGIN_IR_RAMP, closed-form ramp) bit for bit: the same
+    instantiation (PER path), its block read from the callback's table."""
+    if not have("IR_test"):
+        pytest.skip("modules / oracle/_ref not built")
+    torch = torch_cuda
+    mod = load("IR_test")
+    params = mod.default_parameters()
+    gain, step = struct.unpack("<ff", params[:8])
+    mod.initialize_state(params, 2, 48000.0)
+    assert mod.block_class(params, 2, 512, 48000.0)[0] == "table"
+    L = 4096 * 64 + 4096
+    x = torch.zeros((2, L), device="cuda")
+    out, mag = d.render_stft(x, 2, 512, 48000.0, mod.plugin(params, "IR_test"), window=d.DSP_WIN_HANN,
+                             sample_offset=soff)
+    s_out, s_mag = d.render_stft(x, 2, 512, 48000.0, d.Plugin.ir_test(gain, step), window=d.DSP_WIN_HANN,
+                                 sample_offset=soff)
+    torch.cuda.synchronize()
+    assert torch.equal(out, s_out)
+    assert torch.equal(mag, s_mag)
+
+
 CLIP_SRC = r'''
 #include "plugin_header.h"
 struct Parameters { FLOAT_PARAM(0.0f, 1.0f) g; };
@@ -169,6 +195,61 @@ def test_probes_keep_the_callback_where_needed(torch_cuda, src, name, cls):
     a = d.render_offline(x, 2, 480, 44100.0, mod.plugin(params, name))
     b = d.render_offline(x, 2, 480, 44100.0, mod.plugin(params, name, specialize=False))
     assert torch.equal(a, b)
+
+
+RAMP_F32_SRC = r'''
+#include "plugin_header.h"
+struct Parameters { FLOAT_PARAM(0.0f, 1.0f) g; FLOAT_PARAM(0.0f, 0.1f) st; };
+struct State {};
+Parameters default_parameters() { Parameters p = {0.7f, 0.0013f}; return p; }
+State initialize_state(const Parameters& p, const unsigned C, const float sr, void* ctx) { State s; return s; }
+void audio_callback(const Parameters& p, State& st, float** out, const u32 C, const u32 B, const real32 sr) {
+    float g = p.g;
+    for (u32 s = 0; s < B; ++s) {
+        for (u32 c = 0; c < C; ++c) out[c][s] = g;
+        g -= p.st;
+    }
+}
+'''
+
+RAMP_F64_SRC = r'''
+#include "plugin_header.h"
+struct Parameters { FLOAT_PARAM(-1.0f, 1.0f) g; FLOAT_PARAM(-0.1f, 0.1f) st; };
+struct State {};
+Parameters default_parameters() { Parameters p = {-0.3f, -0.00071f}; return p; }
+State initialize_state(const Parameters& p, const unsigned C, const float sr, void* ctx) { State s; return s; }
+void audio_callback(const Parameters& p, State& st, float** out, const u32 C, const u32 B, const real32 sr) {
+    for (u32 s = 0; s < B; ++s)
+        for (u32 c = 0; c < C; ++c) out[c][s] = (float)((double)p.g - (double)s * (double)p.st);
+}
+'''
+
+
+@pytest.mark.parametrize("src,name", [(RAMP_F32_SRC, "ramp_f32"), (RAMP_F64_SRC, "ramp_f64")])
+@pytest.mark.parametrize("B", [512, 256, 480])
+def test_ramp_blocks_in_closed_form_or_table(torch_cuda, oracle, src, name, B):
+    """Table-class blocks that are ramps: a float recurrence (its rounding
+    drifts from any f64 affine form) and an f64 affine ramp with negative
+    values (module.cpp affine_ramp finds its closed form).  Whichever the
+    fused kernel evaluates -- the closed form, checked against every table
+    value, or the table -- the render equals the callback on every block bit
+    for bit, and the spectra are within 1e-6 of the peak of float64."""
+    torch = torch_cuda
+    mod = d.module.Module(d.module.compile_source(src, f"{name}.cpp"))
+    params = mod.default_parameters()
+    mod.initialize_state(params, 2, 48000.0)
+    assert mod.block_class(params, 2, B, 48000.0)[0] == "table"
+    L = 4096 * 20 + 8192
+    x = torch.zeros((2, L), device="cuda")
+    out, mag = d.render_stft(x, 2, B, 48000.0, mod.plugin(params, name), window=d.DSP_WIN_HANN, sample_offset=B * 3)
+    want = d.render_offline(x, 2, B, 48000.0, mod.plugin(params, name, specialize=False))
+    torch.cuda.synchronize()
+    nb = d.num_blocks(L, B)
+    # sample_offset shifts only the block phase: B * 3 keeps it at 0
+    assert torch.equal(out[:, :nb * B], want[:, :nb * B])
+    m64 = oracle.np_stft_mag(want[0].cpu().numpy(), 8192, 4096, d.DSP_WIN_HANN, 4097)
+    mm = mag[0].cpu().numpy().astype(np.float64)
+    assert float(np.max(np.abs(mm - m64).max(axis=1) / m64.max(axis=1))) <= PEAK_REL_TOL
 
 
 def test_new_parameters_are_probed_again(torch_cuda):
