@@ -17,6 +17,7 @@
 #include <hip/hiprtc.h>
 
 #include <algorithm>
+#include <cfloat>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -1251,6 +1252,10 @@ static bool affine_ramp(const float *t, uint32_t B, double *g0, double *s) {
         return true;
     };
     if (!std::isfinite(a)) return false;
+    // (a subnormal value keeps the table: the device's f64 -> f32 conversion
+    // is not checked against the host's there)
+    for (uint32_t i = 0; i < B; ++i)
+        if (t[i] != 0.f && std::fabs(t[i]) < FLT_MIN) return false;
     if (B == 1) {
         *g0 = a;
         *s = 0.0;
