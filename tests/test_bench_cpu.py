@@ -37,3 +37,13 @@ def test_every_instantiation_has_a_summary(bench):
         _, src, got = bench.pmc_traffic(wl, 0)  # size 0: no figure, but the summary is found
         assert got == inst
         assert src is not None, f"{wl}: no committed PMC summary names {inst}"
+
+
+def test_headline_plugin_defaults_to_the_source(bench, monkeypatch):
+    # the headline measures IR_test.cpp compiled unchanged unless --ir-plugin enum
+    monkeypatch.setattr("sys.argv", ["bench.py"])
+    assert bench.parse().ir_plugin == "source"
+    monkeypatch.setattr("sys.argv", ["bench.py", "--ir-plugin", "enum"])
+    assert bench.parse().ir_plugin == "enum"
+    name = bench.source_plugin_name("IR_test", "table")
+    assert "IR_test.cpp" in name and "compiled unchanged" in name and "table" in name
