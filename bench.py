@@ -87,6 +87,9 @@ def parse():
                          "(dsp-bench_amd/modules/mod_IR_test.co) and dispatched through its probed block class "
                          "(the default: the plugin's own code on the measured path); enum = DSP_PLUGIN_IR_RAMP, "
                          "the library's restatement of the same callback (closed-form ramp)")
+    ap.add_argument("--mag-ld", type=int, default=None,
+                    help="headline / gain_stft / stft96k / generic_stft: row stride of the spectra in floats "
+                         "(default K = 4097, rows packed); the K bins written per row are the same")
     ap.add_argument("--no-specialize", action="store_true",
                     help="generic / generic_stft: run the plugin's callback on every block "
                          "(DSP_EXEC_NO_SPECIALIZE) instead of its probed block class")
@@ -373,7 +376,9 @@ def main():
            if wl in ("headline", "ch96k", "gain10min", "fir1024", "generic", "generic_stft", "gain_stft") else None)
     if wl == "generic_stft":
         F = d.stft_frames(nb * B, N_FFT, HOP)
-    mag = (torch.empty((CH, max(F, 1), K_BINS), device=dev)
+    LD = args.mag_ld or K_BINS
+    assert LD >= K_BINS, "--mag-ld below K"
+    mag = (torch.empty((CH, max(F, 1), LD), device=dev)
            if wl in ("headline", "stft96k", "ch96k", "generic_stft", "gain_stft") else None)
     plugin = d.Plugin.ir_test(0.9, 0.002) if wl in ("headline", "ch96k") else d.Plugin.gain_test(0.2)
     block_class = None
@@ -404,7 +409,7 @@ def main():
     if wl == "headline":
         def step():
             d.render_stft(x, CH, B, float(sr), plugin, N=N_FFT, H=HOP, window=d.DSP_WIN_HANN,
-                          K=K_BINS, out=out, mag=mag, sample_offset=soff)
+                          K=K_BINS, ld=LD, out=out, mag=mag, sample_offset=soff)
         workload = ("IR_test render (B=512) + 8192-pt Hann STFT, hop 4096, 4097 bins, "
                     f"{minutes:g} min of 48 kHz stereo per GPU")
         kname = f"{KERNEL}<render> (fused render + window + FFT + |X|)"
@@ -419,7 +424,7 @@ def main():
         # read from HBM, rendered and written, and its spectrum written
         def step():
             d.render_stft(x, CH, B, float(sr), plugin, N=N_FFT, H=HOP, window=d.DSP_WIN_HANN,
-                          K=K_BINS, out=out, mag=mag, sample_offset=soff)
+                          K=K_BINS, ld=LD, out=out, mag=mag, sample_offset=soff)
         workload = ("gain_test render (B=512) fused with the 8192-pt Hann STFT, hop 4096, 4097 bins, "
                     f"{minutes:g} min of 48 kHz stereo per GPU")
         kname = f"{KERNEL}<render> (fused file read + gain + window + FFT + |X|)"
@@ -435,7 +440,7 @@ def main():
         kname = f"{KERNEL}<render> (fused render + window + FFT + |X|)"
     elif wl == "stft96k":
         def step():
-            d.stft_magnitude(x, N=N_FFT, H=HOP, window=d.DSP_WIN_HANN, K=K_BINS, out=mag)
+            d.stft_magnitude(x, N=N_FFT, H=HOP, window=d.DSP_WIN_HANN, K=K_BINS, ld=LD, out=mag)
         workload = f"8192-pt Hann STFT, hop 4096, 4097 bins, {minutes:g} min of 96 kHz stereo per GPU (cfg 4)"
         kname = f"{KERNEL}<memory> (window + FFT + |X|)"
     elif wl == "fir1024":
@@ -482,7 +487,7 @@ def main():
         else:
             def step():
                 d.render_stft(x, CH, B, float(sr), gplug, N=N_FFT, H=HOP, window=d.DSP_WIN_HANN,
-                              K=K_BINS, out=out, mag=mag)
+                              K=K_BINS, ld=LD, out=out, mag=mag)
             workload = (f"{pname}.cpp via the generic plugin driver (B=512) + 8192-pt Hann STFT, hop 4096, "
                         f"4097 bins, {minutes:g} min of 48 kHz stereo per GPU")
             if block_class == "callback":
@@ -681,6 +686,7 @@ def main():
                 "workload": workload,
                 "plugin": plug_name,
                 "block_class": block_class,
+                "mag_row_stride": LD if mag is not None else None,
                 "ir_plugin": (None if wl not in ("headline", "ch96k") else
                               ir_note or ("source" if args.ir_plugin == "source" else "enum")),
                 "samples_per_gpu": samples_per_rank,
