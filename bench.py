@@ -541,20 +541,33 @@ def main():
     torch.cuda.synchronize()
     # one kernel per step: the timed region's own stream events give its
     # average launch duration, and no per-launch events sit between launches
-    region_timed = (wl in ("headline", "ch96k", "gain_stft", "stft96k", "generic_stft") and
-                    block_class != "callback" and not args.launch_events)
+    # the one-launch STFT workloads are timed by the region's stream events
+    # (no events between their launches); the first call confirms one timed
+    # launch per call and gives its algorithmic bytes.  The short launches
+    # (fir1024, gain10min: 0.08-0.12 ms) keep events around every launch,
+    # which measure the kernel alone, as rocprofv3 does (fir1024: 0.1182 ms
+    # against rocprofv3's 0.1161 over all 350 launches of the same run,
+    # profiles/r03_final_fir_*), not the few us between launches that the
+    # region's events would add (profiles/r03_bench_all_region.jsonl)
+    region_wl = (wl in ("headline", "ch96k", "gain_stft", "stft96k", "generic_stft") and
+                 block_class != "callback")
+    probe_launches = not args.launch_events
+    launches_per_call = None
+    region_timed = False
     bytes_probe = 0
-    if region_timed:  # the library's byte count of one launch, from the first call
+    if probe_launches:
         d.lib().dsp_kernel_timing(None, None, None)
         d.lib().dsp_kernel_timing_enable(1)
     tf = time.perf_counter()
     step()
     torch.cuda.synchronize()
     first_call_ms = (time.perf_counter() - tf) * 1e3
-    if region_timed:
+    if probe_launches:
         d.lib().dsp_kernel_timing_enable(0)
         pm, pn, pb = C.c_double(), C.c_uint64(), C.c_uint64()
         d.lib().dsp_kernel_timing(C.byref(pm), C.byref(pn), C.byref(pb))
+        region_timed = region_wl and pn.value == 1
+        launches_per_call = int(pn.value)
         bytes_probe = pb.value / max(1, pn.value)
     for _ in range(max(0, args.warmup - 1)):
         step()
@@ -687,6 +700,7 @@ def main():
                 "plugin": plug_name,
                 "block_class": block_class,
                 "mag_row_stride": LD if mag is not None else None,
+                "timed_launches_per_call": launches_per_call,
                 "ir_plugin": (None if wl not in ("headline", "ch96k") else
                               ir_note or ("source" if args.ir_plugin == "source" else "enum")),
                 "samples_per_gpu": samples_per_rank,
