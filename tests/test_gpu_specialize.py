@@ -139,6 +139,38 @@ def test_ir_test_source_is_the_headline(torch_cuda, soff):
     assert torch.equal(mag, s_mag)
 
 
+@pytest.mark.parametrize("seed", range(8))
+def test_ir_test_source_random_parameters(torch_cuda, oracle, seed):
+    """IR_test.cpp compiled unchanged with random Parameters and block sizes
+    (seed 7: a step 2^-30 of the gain, whose f64 recurrence rounds): the
+    render bit-exact against the reference plugin compiled for the CPU with
+    the same Parameters, the spectra bit-exact against DSP_PLUGIN_IR_RAMP --
+    whether the block went to the closed form (module.cpp affine_ramp) or
+    stayed a table."""
+    if not have("IR_test"):
+        pytest.skip("modules / oracle/_ref not built")
+    torch = torch_cuda
+    rng = np.random.default_rng(100 + seed)
+    g = float(np.float32(rng.uniform(0.0, 1.0)))
+    st = float(np.float32(rng.uniform(0.001, 0.1) if seed < 7 else g * 2.0 ** -30))
+    B = int(rng.choice([512, 256, 1024, 2048, 480, 128]))
+    params = struct.pack("<ff", g, st)
+    mod = load("IR_test")
+    mod.initialize_state(params, 2, 48000.0)
+    assert mod.block_class(params, 2, B, 48000.0)[0] == "table"
+    L = 8192 * 5 + 1234
+    x = torch.zeros((2, L), device="cuda")
+    out, mag = d.render_stft(x, 2, B, 48000.0, mod.plugin(params, "IR_test"), window=d.DSP_WIN_HANN)
+    s_out, s_mag = d.render_stft(x, 2, B, 48000.0, d.Plugin.ir_test(g, st), window=d.DSP_WIN_HANN)
+    torch.cuda.synchronize()
+    ref = oracle.RefPlugin("IR_test", 2, 48000.0)
+    ref.params[:8] = np.frombuffer(params, np.uint8)
+    want = oracle.render_offline([np.zeros(L, np.float32)] * 2, 2, B, 48000.0, ref.as_oracle())
+    assert np.array_equal(out.cpu().numpy(), want)
+    assert torch.equal(out, s_out)
+    assert torch.equal(mag, s_mag)
+
+
 CLIP_SRC = r'''
 #include "plugin_header.h"
 struct Parameters { FLOAT_PARAM(0.0f, 1.0f) g; };
