@@ -235,6 +235,48 @@ def test_time_shards_of_a_stateless_source_plugin(torch_cuda, spec):
                                torch.empty((2, s0.frames, K), device="cuda"), comm=None, gather=False)
 
 
+def test_channel_shards_of_the_source_headline_plugin(torch_cuda):
+    """cfg 5's shape with the bench's headline plugin (IR_test.cpp compiled
+    unchanged, its block in the verified closed form): 8 device channels from
+    a 6-channel file, channel-sharded over 4 loopback ranks, gathered to root
+    3 -- equal bit for bit to the whole-file call, and to the enum's."""
+    import os
+    torch = torch_cuda
+    mods = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "dsp-bench_amd", "modules")
+    if not os.path.exists(os.path.join(mods, "mod_IR_test.co")):
+        pytest.skip("modules not built")
+    mod = d.module.Module(open(os.path.join(mods, "mod_IR_test.co"), "rb").read())
+    params = mod.default_parameters()
+    mod.initialize_state(params, 8, 96000.0)
+    plugin = mod.plugin(params, "IR_test")
+    L, B, K, world, root = 8192 * 10 + 4321, 512, 4097, 4, 3
+    x = (torch.rand((6, L + 1), device="cuda") * 2 - 1)[:, :L]
+    ref_out, ref_mag = _whole(torch, x, 8, B, plugin, L)
+    e_out, e_mag = _whole(torch, x, 8, B, d.Plugin.ir_test(0.9, 0.002), L)
+    assert torch.equal(ref_out, e_out) and torch.equal(ref_mag, e_mag)
+    all_out = torch.full_like(ref_out, -7.0)
+    all_mag = torch.full_like(ref_mag, -7.0)
+    comms = sh.loopback(world, 0)
+
+    def rank_fn(r):
+        s = sh.plan(L, world, r, B, 8192, 4096, True, 8, sh.CHANNELS)
+        nf = max(0, min(s.chan0 + s.channels, 6) - s.chan0)
+        xl = x[s.chan0:s.chan0 + nf, s.start:s.start + s.read_len] if nf else None
+        out = torch.empty((max(s.channels, 1), -(-s.read_len // B) * B), device="cuda")
+        mag = torch.empty((max(s.channels, 1), max(s.frames, 1), K), device="cuda")
+        st = torch.cuda.Stream()
+        sh.render_stft_sharded(xl, L, 8, B, 96000.0, plugin, s, out, mag, comm=comms[r], root=root,
+                               all_out=all_out if r == root else None, all_mag=all_mag if r == root else None,
+                               chunk=1 << 15, stream=st.cuda_stream)
+        st.synchronize()
+    _run_ranks(torch, world, rank_fn)
+    torch.cuda.synchronize()
+    for c in comms:
+        c.close()
+    assert torch.equal(all_out, ref_out), _where(torch, all_out, ref_out)
+    assert torch.equal(all_mag, ref_mag), _where(torch, all_mag, ref_mag)
+
+
 def test_loopback_gather_and_errors(torch_cuda):
     """dsp_comm_gather over the loopback (3 ranks, root 2); a count mismatch
     between a send and its recv fails both sides instead of copying."""

@@ -113,8 +113,8 @@ def test_ir_test_source_render_stft_fused(torch_cuda, oracle, B):
         assert float(np.max(np.abs(mm - m64).max(axis=1) / m64.max(axis=1))) <= PEAK_REL_TOL
 
 
-@pytest.mark.parametrize("soff", [0, 4096 * 37, 512 * 3 + 4096])
-def test_ir_test_source_is_the_headline(torch_cuda, soff):
+@pytest.mark.parametrize("soff,C", [(0, 2), (4096 * 37, 2), (512 * 3 + 4096, 2), (512 * 7, 2), (0, 1), (4096 * 5, 8)])
+def test_ir_test_source_is_the_headline(torch_cuda, soff, C):
     """The bench's headline call (bench.py --ir-plugin source, the default):
     IR_test.cpp compiled unchanged, 4097-bin Hann 8192 / 4096 STFT at a rank's
     sample offset, gives the render and spectra of the stock fused IR_test
@@ -126,17 +126,19 @@ def test_ir_test_source_is_the_headline(torch_cuda, soff):
     mod = load("IR_test")
     params = mod.default_parameters()
     gain, step = struct.unpack("<ff", params[:8])
-    mod.initialize_state(params, 2, 48000.0)
-    assert mod.block_class(params, 2, 512, 48000.0)[0] == "table"
+    mod.initialize_state(params, C, 48000.0)
+    assert mod.block_class(params, C, 512, 48000.0)[0] == "table"
     L = 4096 * 64 + 4096
-    x = torch.zeros((2, L), device="cuda")
-    out, mag = d.render_stft(x, 2, 512, 48000.0, mod.plugin(params, "IR_test"), window=d.DSP_WIN_HANN,
+    x = torch.zeros((min(C, 2), L), device="cuda")  # C = 8: six channels the file lacks
+    out, mag = d.render_stft(x, C, 512, 48000.0, mod.plugin(params, "IR_test"), window=d.DSP_WIN_HANN,
                              sample_offset=soff)
-    s_out, s_mag = d.render_stft(x, 2, 512, 48000.0, d.Plugin.ir_test(gain, step), window=d.DSP_WIN_HANN,
+    s_out, s_mag = d.render_stft(x, C, 512, 48000.0, d.Plugin.ir_test(gain, step), window=d.DSP_WIN_HANN,
                                  sample_offset=soff)
     torch.cuda.synchronize()
     assert torch.equal(out, s_out)
     assert torch.equal(mag, s_mag)
+    with pytest.raises(d.DspError):  # a shard starts on a block boundary (the library's contract)
+        d.render_stft(x, C, 512, 48000.0, mod.plugin(params, "IR_test"), window=d.DSP_WIN_HANN, sample_offset=777)
 
 
 @pytest.mark.parametrize("seed", range(8))
