@@ -378,6 +378,7 @@ def main():
         F = d.stft_frames(nb * B, N_FFT, HOP)
     LD = args.mag_ld or K_BINS
     assert LD >= K_BINS, "--mag-ld below K"
+    assert LD == K_BINS or (world == 1 and wl != "ch96k"), "--mag-ld: single-GPU STFT workloads only"
     mag = (torch.empty((CH, max(F, 1), LD), device=dev)
            if wl in ("headline", "stft96k", "ch96k", "generic_stft", "gain_stft") else None)
     plugin = d.Plugin.ir_test(0.9, 0.002) if wl in ("headline", "ch96k") else d.Plugin.gain_test(0.2)
