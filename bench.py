@@ -61,6 +61,8 @@ def parse():
                     help="N > 1: seconds before a gather pass that has not finished is abandoned (the line is "
                          "printed with render_gather_error)")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (host WAV -> host spectra) pass")
+    ap.add_argument("--no-companion", action="store_true",
+                    help="headline: skip the input-reading companion pass (gain_test.cpp fused with the STFT)")
     ap.add_argument("--launch-events", action="store_true",
                     help="one-kernel workloads: bracket every launch with the library's HIP events inside the "
                          "timed region (costs 0.7-1%% of a step, profiles/r02_launch_events_ab.txt); default: "
@@ -118,6 +120,47 @@ def source_plugin_name(pname: str, block_class: str) -> str:
             f"{block_class}: " + {"table": "its own callback's block, tiled, in the fused kernel",
                                   "gain": "the gain its callback gives, in the gain map",
                                   "callback": "the callback on every block"}[block_class] + ")")
+
+
+def measure_companion(d, lib, args, x, out, mag, CH, B, sr, L, LD, soff, stream):
+    """The headline's input-reading companion: gain_test.cpp compiled
+    unchanged (block class GAIN) fused with the same STFT, on the headline's
+    buffers; returns the line's `input_reading_companion` object."""
+    import torch
+    cmod, cplug, ccls = source_plugin(d, "gain_test", CH, B, sr)
+
+    def cstep():
+        d.render_stft(x, CH, B, float(sr), cplug, N=N_FFT, H=HOP, window=d.DSP_WIN_HANN,
+                      K=K_BINS, ld=LD, out=out, mag=mag, sample_offset=soff)
+    lib.dsp_kernel_timing(None, None, None)
+    lib.dsp_kernel_timing_enable(1)
+    cstep()
+    torch.cuda.synchronize()
+    lib.dsp_kernel_timing_enable(0)
+    cm, cn, cb = C.c_double(), C.c_uint64(), C.c_uint64()
+    lib.dsp_kernel_timing(C.byref(cm), C.byref(cn), C.byref(cb))
+    for _ in range(max(0, args.warmup - 1)):
+        cstep()
+    c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    c0.record(stream)
+    for _ in range(args.steps):
+        cstep()
+    c1.record(stream)
+    torch.cuda.synchronize()
+    cms = c0.elapsed_time(c1) / args.steps
+    cbytes = cb.value / max(1, cn.value)
+    companion = {
+        "workload": ("gain_test.cpp compiled unchanged (block class " + ccls + ") fused with the same STFT: "
+                     "the headline's shape with the input read"),
+        "ms_per_step": round(cms, 4),
+        "msamples_per_s": round(CH * L / (cms / 1e3) / 1e6, 1),
+        "algorithmic_bytes_per_launch": int(cbytes),
+        "frac_of_hbm": round(cbytes / (cms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4) if cn.value == 1 else None,
+        "timing": f"region events over {args.steps} launches after {args.warmup} untimed, right after the "
+                  "headline's passes",
+    }
+    return companion
 
 
 # the instantiation each workload's dominant launch runs (stft_pk.hip /
@@ -636,6 +679,20 @@ def main():
     gather_err = None
     gather_pending = not args.no_gather and world > 1 and wl in ("headline", "ch96k")
 
+    # the same fused kernel with a plugin that reads its input: gain_test.cpp
+    # compiled unchanged (block class GAIN), the headline's shape and buffers,
+    # each frame's hop read from HBM -- IR_test ignores its input, so every
+    # headline frame is the same spectrum; this companion is not.  Timed as the
+    # headline (region events, --warmup untimed then --steps); never `value`
+    companion = None
+    mdir = os.environ.get("DSPB_MODULES_DIR", os.path.join(REPO, "dsp-bench_amd", "modules"))
+    if (wl == "headline" and world == 1 and not args.no_companion and
+            os.path.exists(os.path.join(mdir, "mod_gain_test.co"))):
+        try:
+            companion = measure_companion(d, lib, args, x, out, mag, CH, B, sr, L, LD, soff, stream)
+        except Exception as e:  # reported in the line; `value` stands on its own
+            companion = {"error": f"{type(e).__name__}: {e}"}
+
     # end to end: the same hour as a 16-bit PCM WAV payload in
     # pinned host memory -> chunked H2D -> GPU decode -> render + STFT -> D2H
     # of the render and the spectra into pinned host rows
@@ -717,6 +774,7 @@ def main():
                                   if gather_ms is not None else None),
                 "first_call_ms": round(first_call_ms, 4),
                 "end_to_end": e2e,
+                "input_reading_companion": companion,
                 "settled_step_ms_p50": round(pct(0.5), 4),
                 "step_ms_p10_p50_p90": [round(pct(0.1), 4), round(pct(0.5), 4), round(pct(0.9), 4)],
                 "step_ms_distribution": f"{nd} further steps, one event after each (outside the timed region)",
