@@ -415,25 +415,6 @@ static void pair_table(const float *taps, uint32_t T, float *out) {
         }
 }
 
-// the two-wave table of fir_pair2w_kernel: H = FFT_8192(taps) / 8192 (the
-// scale of its two unnormalised 4096-point inverse halves, a power of 2), as
-// float4 [half][q][lane] = (Re H[k0], Re H[k1], Im .., Im ..), k0 = 4096 half
-// + l + 64 q, k1 = k0 + 2048: wave A (half 0) multiplies bins [0, 4096),
-// wave B bins [4096, 8192) (tools/ols2w_model.py)
-static void pair2_table(const float *taps, uint32_t T, float *out) {
-    std::vector<double> re, im;
-    taps_spectrum(taps, T, 8192, re, im);
-    const double sc = 1.0 / 8192.0;
-    for (int h = 0; h < 2; ++h)
-        for (int q = 0; q < 32; ++q)
-            for (int l = 0; l < 64; ++l) {
-                const int k0 = 4096 * h + l + 64 * q, k1 = k0 + 2048;
-                float *o = out + 4 * ((32 * h + q) * 64 + l);
-                o[0] = (float)(re[k0] * sc); o[1] = (float)(re[k1] * sc);
-                o[2] = (float)(im[k0] * sc); o[3] = (float)(im[k1] * sc);
-            }
-}
-
 // IR_test (build/IR_test.cpp:47-58) runs `gain -= step` in double from the
 // float parameters.  The sequence is often exact -- every partial result a
 // double -- and then table[i] = (float)(gain - i step) is one f64 FMA, with
@@ -469,7 +450,6 @@ static int plugin_map(const dsp_plugin *p, uint32_t B, int dev, hipStream_t s, S
     m->B = B;
     m->b_mask = is_pow2(B) ? B - 1 : 0;
     m->taps = nullptr;
-    m->pair2H = nullptr;
     m->ntaps8 = 0;
     m->module = nullptr;
     m->gparams = nullptr;
@@ -529,13 +509,11 @@ static int plugin_map(const dsp_plugin *p, uint32_t B, int dev, hipStream_t s, S
             if (!ft) {
                 if (int st = refuse_capture(s, "a FIR filter's device taps")) return st;
                 // [taps, T8][8192-point table, 8194 (+ 2 pad)][4096-point pair table, 8192]
-                // [two-wave 8192-point pair table, 16384]
-                std::vector<float> h(T8 + 8196 + 8192 + 16384, 0.f);
+                std::vector<float> h(T8 + 8196 + 8192, 0.f);
                 std::memcpy(h.data(), key.data(), 4 * (size_t)T);
                 if (T <= 1025) {
                     ols_table(h.data(), T, h.data() + T8);
                     pair_table(h.data(), T, h.data() + T8 + 8196);
-                    pair2_table(h.data(), T, h.data() + T8 + 8196 + 8192);
                 }
                 float *d = nullptr;
                 DSPB_HIP(hipMalloc(&d, sizeof(float) * h.size()));
@@ -557,7 +535,6 @@ static int plugin_map(const dsp_plugin *p, uint32_t B, int dev, hipStream_t s, S
         m->ntaps = T;
         m->olsH = ft->dev + T8;
         m->pairH = ft->dev + T8 + 8196;  // 16-byte aligned: T8 and 8196 are multiples of 4
-        m->pair2H = ft->dev + T8 + 8196 + 8192;
         m->olsH2048[0] = ft->h2048r;
         m->olsH2048[1] = ft->h2048i;
         return DSP_OK;
@@ -664,16 +641,10 @@ static int render_device(const float *const *in, uint32_t in_ch, uint64_t L, flo
                     }
                     A.L = L;
                     A.Ly = end;
-                    A.tw = tw;
-#ifdef DSPB_FIR_PAIR2W  // (A/B build: 8192-point pair frames over two waves, fir_pair2w_kernel)
-                    A.F = (end + kPair2Hop - 1) / kPair2Hop;
-                    A.H = map.pair2H;
-                    if ((st = launch_fir_pair2w(A, np, s))) return st;
-#else
                     A.F = (end + kPairHop - 1) / kPairHop;
                     A.H = map.pairH;
+                    A.tw = tw;
                     if ((st = launch_fir_pair(A, np, s))) return st;
-#endif
                 }
                 if (cn & 1) {
                     const uint32_t c = c0 + cn - 1;

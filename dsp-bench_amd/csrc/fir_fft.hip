@@ -388,216 +388,6 @@ int launch_fir_pair(const FirFftArgs &A, uint32_t C, hipStream_t s) {
     return DSP_OK;
 }
 
-// ---------------------------------------------------------------------------
-// A channel pair as one 8192-point complex frame over TWO waves
-// (fir_pair2w_kernel; the numpy model is tools/ols2w_model.py).  Frame f
-// covers input [f P - 1024, f P + 7168), P = kPair2Hop = 7168, and owns
-// outputs [f P, (f + 1) P).  Decimation in time across the two waves of a
-// two-wave workgroup (half = wave index):
-//   load      u[2m + half], m = l + 64 r (lane l, register r), u = x0 + i x1
-//   forward   the packed 4096-point transform: Z (E on A, O on B) as
-//             Y2[q] = (Z[l + 64 q], Z[l + 64 (q + 32)]); B: T = W8192^k O
-//   exchange  A gets T, B gets E (lane-major through the waves' LDS tiles)
-//   multiply  A: (E + T) H[k], B: (E - T) H[k + 4096]
-//   exchange  A gets B's product, B gets A's
-//   inverse   A: IDFT4096(YA + YB) = y[2m]; B: IDFT4096((YA - YB) W8192^-k)
-//             = y[2m + 1]; stored for m >= 512 at f P + 2m + half - 1024
-// Per wave: the pair kernel's two transforms (+ B's twiddle each way) for
-// 7,168 outputs per channel per frame instead of 3,072 per 4096-point frame.
-
-// the B wave's twiddles for Y2[q]: (W8192^k, W8192^(k + 2048)) = (u, -i u),
-// u = W8192^(l + 64 q) = W8192^l W128^q
-__device__ __forceinline__ cx2 pair2_tw(const cx wl, int q) {
-    const cx u = cx{wl.r * kW128_re[q] - wl.i * kW128_im[q], wl.r * kW128_im[q] + wl.i * kW128_re[q]};
-    return cx2{v2f{u.r, u.i}, v2f{u.i, -u.r}};
-}
-
-// the pair's exchange of 32 cx2 (128 floats per lane) through the two waves'
-// LDS tiles (64 x 33 floats each), 32 floats per lane per pass, lane-major;
-// each pass's values from the peer are merged at once, v[q] = fn(q, v[q],
-// peer's v[q]), so no second 128-float array is live
-template <typename FN>
-__device__ __forceinline__ void pair2_exchange(cx2 (&v)[32], float *own, const float *peer, uint32_t lane,
-                                               const FN &fn) {
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const cx2 a = v[8 * p + i];
-            own[(4 * i + 0) * 64 + lane] = a.r.x;
-            own[(4 * i + 1) * 64 + lane] = a.r.y;
-            own[(4 * i + 2) * 64 + lane] = a.i.x;
-            own[(4 * i + 3) * 64 + lane] = a.i.y;
-        }
-        __syncthreads();
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const cx2 g = cx2{v2f{peer[(4 * i + 0) * 64 + lane], peer[(4 * i + 1) * 64 + lane]},
-                              v2f{peer[(4 * i + 2) * 64 + lane], peer[(4 * i + 3) * 64 + lane]}};
-            v[8 * p + i] = fn(8 * p + i, v[8 * p + i], g);
-        }
-        __syncthreads();
-    }
-}
-
-template <bool EDGE, uint32_t half>
-__device__ __forceinline__ void fir_pair2w_frame(const FirFftArgs &A, uint64_t f, uint32_t c0, float *own,
-                                                 const float *peer, uint32_t lane) {
-    const int64_t fs = (int64_t)(f * kPair2Hop) - (int64_t)kOlsHist + (int64_t)half;
-    const float *x0 = c0 < A.in_ch ? A.in.p[c0] : nullptr;
-    const float *x1 = c0 + 1 < A.in_ch ? A.in.p[c0 + 1] : nullptr;
-
-    cx tlo[8];
-    cx2 thp[4];
-    load_stage_tw(A.tw, lane, 0u, tlo, thp);
-
-    // u[2m + half], m = l + 128 j (.x) and l + 128 j + 64 (.y)
-    cx2 P[32];
-    if constexpr (!EDGE) {
-        const float *b0 = x0 + fs, *b1 = x1 + fs;
-#pragma unroll
-        for (int j = 0; j < 32; ++j) {
-            const uint32_t o = 2u * lane + 256u * (uint32_t)j;
-            P[j] = cx2{v2f{b0[o], b0[o + 128u]}, v2f{b1[o], b1[o + 128u]}};
-        }
-    } else {
-#pragma unroll
-        for (int j = 0; j < 32; ++j) {
-            const int64_t s0 = fs + 2 * (int64_t)lane + 256 * j, s1 = s0 + 128;
-            const bool in0 = s0 >= 0 && (uint64_t)s0 < A.L, in1 = s1 >= 0 && (uint64_t)s1 < A.L;
-            P[j] = cx2{v2f{(x0 && in0) ? x0[s0] : 0.f, (x0 && in1) ? x0[s1] : 0.f},
-                       v2f{(x1 && in0) ? x1[s0] : 0.f, (x1 && in1) ? x1[s1] : 0.f}};
-        }
-    }
-
-    const v2f wl2 = A.tw[lane];  // W8192^l
-    const cx wl = cx{wl2.x, wl2.y};
-    cx2 Q[32];
-    {
-        cx2 R[32], Y2[32];
-        fft4096_pk_front<false, false, false, true>(P, own, tlo, thp, lane, R);
-        combine64p(R, Y2);
-        if constexpr (half == 1) {
-#pragma unroll
-            for (int q = 0; q < 32; ++q) Y2[q] = cmul2(Y2[q], pair2_tw(wl, q));  // T = W^k O
-        }
-        // A: (E + T) H[k], B: (E - T) H[k + 4096], with the peer's E / T
-        const float4 *H4 = reinterpret_cast<const float4 *>(A.H) + 2048u * half;
-        pair2_exchange(Y2, own, peer, lane, [&](int q, cx2 mine, cx2 g) {
-            // (an opaque offset: the load stays in its pass, not hoisted
-            // to the frame's start with 128 VGPRs of H live)
-            uint32_t salt = 0u;
-            asm volatile("" : "+s"(salt));
-            const float4 h = (H4 + salt)[64u * (uint32_t)q + lane];
-            return cmul2(half == 1 ? g - mine : mine + g, cx2{v2f{h.x, h.y}, v2f{h.z, h.w}});
-        });
-        // A: YA + YB, B: (YA - YB) W^-k
-        pair2_exchange(Y2, own, peer, lane, [&](int q, cx2 mine, cx2 g) {
-            if constexpr (half == 1) {
-                const cx2 t = pair2_tw(wl, q);
-                return cmul2(g - mine, cx2{t.r, -t.i});
-            } else {
-                return mine + g;
-            }
-        });
-        // re-paired as the inverse's input pairs (Z'[l + 64 (2j)], Z'[l + 64 (2j + 1)])
-#pragma unroll
-        for (int j = 0; j < 32; ++j) {
-            const int r0 = 2 * j, r1 = 2 * j + 1;
-            const cx2 a = Y2[r0 & 31], b = Y2[r1 & 31];
-            if (r0 < 32) {
-                asm("v_pk_mov_b32 %0, %1, %2 op_sel:[0,0]" : "=v"(Q[j].r) : "v"(a.r), "v"(b.r));
-                asm("v_pk_mov_b32 %0, %1, %2 op_sel:[0,0]" : "=v"(Q[j].i) : "v"(a.i), "v"(b.i));
-            } else {
-                asm("v_pk_mov_b32 %0, %1, %2 op_sel:[1,1]" : "=v"(Q[j].r) : "v"(a.r), "v"(b.r));
-                asm("v_pk_mov_b32 %0, %1, %2 op_sel:[1,1]" : "=v"(Q[j].i) : "v"(a.i), "v"(b.i));
-            }
-        }
-    }
-    {
-        uint32_t salt = 0u;
-        asm volatile("" : "+s"(salt));
-        load_stage_tw(A.tw, lane, salt, tlo, thp);
-    }
-    cx yp[32], ym[32];
-    {
-        cx2 R[32], Y2[32];
-        fft4096_pk_front<true, false, false, true>(Q, own, tlo, thp, lane, R);
-        combine64p_dir<true>(R, Y2);
-#pragma unroll
-        for (int q = 0; q < 32; ++q) {
-            yp[q] = cx{Y2[q].r.x, Y2[q].i.x};
-            ym[q] = cx{Y2[q].r.y, Y2[q].i.y};
-        }
-    }
-
-    // y[2m + half], m = l + 64 q, q >= 8 -> out[f P + 2 l + 128 (q - 8) + half]
-    const uint32_t c1 = c0 + 1;
-    const bool two = c1 < A.nout;  // (wave-uniform)
-    asm volatile("" : "+v"(lane));
-    float *o0 = A.out.p[c0] + f * kPair2Hop + half;
-    float *o1 = two ? A.out.p[c1] + f * kPair2Hop + half : o0;
-    if (f * kPair2Hop + kPair2Hop <= A.Ly) {
-#pragma unroll
-        for (int q = 8; q < 64; ++q) {
-            const cx z = q < 32 ? yp[q] : ym[q - 32];
-            const uint32_t o = 2u * lane + 128u * (uint32_t)(q - 8);
-            __builtin_nontemporal_store(z.r, o0 + o);
-            if (two) __builtin_nontemporal_store(x1 ? z.i : 0.f, o1 + o);
-        }
-    } else {
-        const uint64_t n = A.Ly - f * kPair2Hop;
-#pragma unroll
-        for (int q = 8; q < 64; ++q) {
-            const cx z = q < 32 ? yp[q] : ym[q - 32];
-            const uint32_t o = 2u * lane + 128u * (uint32_t)(q - 8);
-            if (o + half < n) {
-                o0[o] = z.r;
-                if (two) o1[o] = x1 ? z.i : 0.f;
-            }
-        }
-    }
-}
-
-// grid (frames, channel pairs); two waves per workgroup (one frame), their
-// two 64 x 33 LDS tiles; two waves per SIMD (four workgroups per CU)
-__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))) void fir_pair2w_kernel(FirFftArgs A,
-                                                                                                    uint64_t fe) {
-    __shared__ __attribute__((aligned(16))) float lds_all[2][64 * 33];
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t half = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t c0 = 2u * blockIdx.y;
-    const uint64_t f = (uint64_t)xcd_remap(blockIdx.x, gridDim.x);
-    if (f >= A.F) return;  // (workgroup-uniform: both waves leave)
-    float *own = lds_all[half];
-    const float *peer = lds_all[half ^ 1u];
-    // (each wave of the pair runs its own specialised code; both execute the
-    // same barriers, the exchanges' eight each)
-    const bool edge = f == 0 || f >= fe || c0 + 1 >= A.in_ch;
-    if (half) {
-        if (edge) fir_pair2w_frame<true, 1>(A, f, c0, own, peer, lane);
-        else fir_pair2w_frame<false, 1>(A, f, c0, own, peer, lane);
-    } else {
-        if (edge) fir_pair2w_frame<true, 0>(A, f, c0, own, peer, lane);
-        else fir_pair2w_frame<false, 0>(A, f, c0, own, peer, lane);
-    }
-}
-
-int launch_fir_pair2w(const FirFftArgs &A, uint32_t C, hipStream_t s) {
-    if (A.F == 0 || C == 0) return DSP_OK;
-    // interior frames: [1, fe) with (f P - 1024) + 8192 <= L
-    uint64_t fe = 1;
-    if (A.L >= kPair2Hop) fe = (A.L - kPair2Hop) / kPair2Hop + 1;
-    if (fe > A.F) fe = A.F;
-    if (fe < 1) fe = 1;
-    if (A.F > 0x7fffffffull) return DSP_ERR_INVALID;
-    FirFftArgs B = A;
-    B.nout = C;
-    hipLaunchKernelGGL(fir_pair2w_kernel, dim3((uint32_t)A.F, (C + 1) / 2), dim3(128), 0, s, B, fe);
-    DSPB_HIP(hipGetLastError());
-    return DSP_OK;
-}
-
 int launch_fir_fft(const FirFftArgs &A, uint32_t C, hipStream_t s) {
     if (A.F == 0 || C == 0) return DSP_OK;
     const uint64_t fe = interior_end(A);

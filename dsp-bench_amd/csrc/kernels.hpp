@@ -103,10 +103,6 @@ int launch_fir_fft(const FirFftArgs &A, uint32_t C, hipStream_t s);
 // (C even; F = ceil(Ly / kPairHop); H = SampleMap::pairH; h2048 unused)
 constexpr uint32_t kPairHop = 3072;
 int launch_fir_pair(const FirFftArgs &A, uint32_t C, hipStream_t s);
-// fir_pair2w_kernel: a channel pair as one 8192-point complex frame over two
-// waves (C even; F = ceil(Ly / kPair2Hop); H = SampleMap::pair2H)
-constexpr uint32_t kPair2Hop = 7168;
-int launch_fir_pair2w(const FirFftArgs &A, uint32_t C, hipStream_t s);
 int launch_fir(const float *x, uint64_t L, float *y, uint64_t Ly, const float *h8, uint32_t T8,
                bool y_aligned16, hipStream_t s);
 int launch_minmax(const float *x, uint64_t n, uint32_t P, float *vmax, float *vmin, hipStream_t s);
