@@ -21,6 +21,9 @@ N > 1 one more pass then runs the product's pipelined sharded driver
 to rank 0 over RCCL (xGMI), timed separately ("render_gather_ms", the
 north_star's "final RCCL gather"), outside `value` (--no-gather skips it).
 
+`--gpus N` outside a launcher starts the N ranks itself (torch.distributed.run
+as a child process); under a launcher, WORLD_SIZE must equal N.
+
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--minutes M]
                        [--no-cpu-baseline] [--no-gather]
 """
@@ -354,8 +357,41 @@ def bench_ir(args, dev, world, rank):
         print(json.dumps(line), flush=True)
 
 
+def rank_launch_cmd(n: int, argv: list[str]) -> list[str]:
+    """`bench.py --gpus N` started outside a launcher: the N ranks come from
+    torch.distributed.run in a child process (one process per GPU, rendezvous
+    on 127.0.0.1 at a port the c10d store picks), with this script's own
+    arguments; rank 0 prints the line on the inherited stdout."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(n),
+            "--rdzv-backend", "c10d", "--rdzv-endpoint", "127.0.0.1:0", "--local-addr", "127.0.0.1",
+            os.path.abspath(__file__), *argv]
+
+
+def check_world(gpus: int, env) -> tuple[str, str | None]:
+    """What main() does for --gpus N in environment `env`: ("run", None) in a
+    rank (or N = 1 unlaunched), ("launch", None) to start N ranks, or
+    ("error", why) when a launcher's WORLD_SIZE disagrees with --gpus."""
+    if gpus < 1:
+        return "error", f"--gpus {gpus}: at least 1"
+    ws = env.get("WORLD_SIZE")
+    if ws is None:
+        return ("launch", None) if gpus > 1 else ("run", None)
+    if int(ws) != gpus:
+        return "error", f"WORLD_SIZE={ws} from the launcher but --gpus {gpus}"
+    return "run", None
+
+
 def main():
     args = parse()
+    what, why = check_world(args.gpus, os.environ)
+    if what == "error":
+        print(f"bench.py: {why}", file=sys.stderr, flush=True)
+        sys.exit(2)
+    if what == "launch":
+        # this process has made no GPU call: the ranks are children, and this
+        # process exits with their launcher's status
+        import subprocess
+        sys.exit(subprocess.call(rank_launch_cmd(args.gpus, sys.argv[1:])))
     import torch
     import torch.distributed as dist
 

@@ -47,3 +47,29 @@ def test_headline_plugin_defaults_to_the_source(bench, monkeypatch):
     assert bench.parse().ir_plugin == "enum"
     name = bench.source_plugin_name("IR_test", "table")
     assert "IR_test.cpp" in name and "compiled unchanged" in name and "table" in name
+
+
+def test_gpus_flag_launches_or_checks_the_world(bench):
+    """--gpus N: unlaunched N > 1 starts N ranks (torch.distributed.run as a
+    child, rendezvous on 127.0.0.1); under a launcher WORLD_SIZE must equal
+    N; N = 1 unlaunched runs in place."""
+    assert bench.check_world(1, {}) == ("run", None)
+    assert bench.check_world(8, {}) == ("launch", None)
+    assert bench.check_world(8, {"WORLD_SIZE": "8"}) == ("run", None)
+    what, why = bench.check_world(8, {"WORLD_SIZE": "2"})
+    assert what == "error" and "WORLD_SIZE=2" in why
+    assert bench.check_world(0, {})[0] == "error"
+    cmd = bench.rank_launch_cmd(4, ["--gpus", "4", "--steps", "5"])
+    i = cmd.index("--nproc-per-node")
+    assert cmd[i + 1] == "4" and "torch.distributed.run" in cmd
+    assert "127.0.0.1:0" in cmd
+    assert cmd[-5].endswith("bench.py") and cmd[-4:] == ["--gpus", "4", "--steps", "5"]
+
+
+def test_world_mismatch_exits_nonzero():
+    import subprocess
+    import sys
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4"], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2 and "WORLD_SIZE=2" in r.stderr

@@ -9,14 +9,13 @@ as the transport; each must reassemble the whole-file result bit for bit.
 The 8-GPU run itself is the driver's.
 """
 import threading
-import os
-import socket
 
 import numpy as np
 import pytest
 
 import dspbench as d
 import dspbench.shard as sh
+import rankrun
 
 pytestmark = pytest.mark.gpu
 
@@ -115,7 +114,9 @@ def _run_ranks(torch, world, fn):
             fn(r)
         except BaseException as e:  # noqa: BLE001
             errs[r] = e
-    ts = [threading.Thread(target=body, args=(r,)) for r in range(world)]
+    # daemon threads: a rank stuck in a GPU call cannot hold the interpreter
+    # at exit after the assertion below has failed the test
+    ts = [threading.Thread(target=body, args=(r,), daemon=True) for r in range(world)]
     for t in ts:
         t.start()
     for t in ts:
@@ -311,57 +312,37 @@ def test_loopback_gather_and_errors(torch_cuda):
         c.close()
 
 
-def _free_port():
-    with socket.socket() as so:
-        so.bind(("127.0.0.1", 0))
-        return so.getsockname()[1]
-
-
-def _rehearsal_worker(rank, world, port, q):
+def _rehearsal_worker(rank, world):
     """One rank of the N > 1 cfg 5 path on cuda:0, one process per rank: the
     C++ sharded driver (plan, chunks, GPU render + fused STFT, gather
     schedule) with gloo as its transport (dsp_comm_init_transport)."""
     import torch
-    import torch.distributed as dist
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    try:
-        torch.cuda.set_device(0)
-        C_total, L, B = 4, 8192 * 12 + 999, 512
-        g = torch.Generator(device="cuda").manual_seed(11)
-        x = torch.rand((C_total, L), device="cuda", generator=g) * 2 - 1
-        plugin = d.Plugin.ir_test(0.9, 0.002)
-        s = sh.plan(L, world, rank, B, 8192, 4096, True, C_total, sh.CHANNELS)
-        nb = -(-L // B)
-        xl = x[s.chan0:s.chan0 + s.channels].contiguous()
-        out = torch.empty((s.channels, nb * B), device="cuda")
-        mag = torch.empty((s.channels, s.frames, 4097), device="cuda")
-        all_out = torch.zeros((C_total, nb * B), device="cuda") if rank == 0 else None
-        all_mag = torch.zeros((C_total, s.frames, 4097), device="cuda") if rank == 0 else None
-        comm = sh.TorchComm(device=0)  # gloo as the transport of the C++ driver
-        sh.render_stft_sharded(xl, L, C_total, B, 96000.0, plugin, s, out, mag, comm=comm, root=0,
-                               all_out=all_out, all_mag=all_mag, chunk=1 << 15)
+    torch.cuda.set_device(0)
+    C_total, L, B = 4, 8192 * 12 + 999, 512
+    g = torch.Generator(device="cuda").manual_seed(11)
+    x = torch.rand((C_total, L), device="cuda", generator=g) * 2 - 1
+    plugin = d.Plugin.ir_test(0.9, 0.002)
+    s = sh.plan(L, world, rank, B, 8192, 4096, True, C_total, sh.CHANNELS)
+    nb = -(-L // B)
+    xl = x[s.chan0:s.chan0 + s.channels].contiguous()
+    out = torch.empty((s.channels, nb * B), device="cuda")
+    mag = torch.empty((s.channels, s.frames, 4097), device="cuda")
+    all_out = torch.zeros((C_total, nb * B), device="cuda") if rank == 0 else None
+    all_mag = torch.zeros((C_total, s.frames, 4097), device="cuda") if rank == 0 else None
+    comm = sh.TorchComm(device=0)  # gloo as the transport of the C++ driver
+    sh.render_stft_sharded(xl, L, C_total, B, 96000.0, plugin, s, out, mag, comm=comm, root=0,
+                           all_out=all_out, all_mag=all_mag, chunk=1 << 15)
+    torch.cuda.synchronize()
+    comm.close()
+    if rank == 0:
+        ref_out, ref_mag = d.render_stft(x, C_total, B, 96000.0, plugin, window=d.DSP_WIN_HANN)
         torch.cuda.synchronize()
-        comm.close()
-        if rank == 0:
-            torch.cuda.synchronize()
-            ref_out, ref_mag = d.render_stft(x, C_total, B, 96000.0, plugin, window=d.DSP_WIN_HANN)
-            torch.cuda.synchronize()
-            q.put((bool(torch.equal(all_out, ref_out)), bool(torch.equal(all_mag, ref_mag))))
-    finally:
-        dist.destroy_process_group()
+        return bool(torch.equal(all_out, ref_out)), bool(torch.equal(all_mag, ref_mag))
+    return None
 
 
-def test_two_rank_rehearsal_on_one_gpu(torch_cuda):
-    import torch.multiprocessing as mp
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_rehearsal_worker, args=(r, 2, port, q)) for r in range(2)]
-    for p in procs:
-        p.start()
-    ok_r, ok_m = q.get(timeout=100)
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
+def test_two_rank_rehearsal_on_one_gpu(torch_cuda, tmp_path):
+    """Two processes on cuda:0 (FileStore rendezvous, bounded waits, daemon
+    ranks reaped on any failure: tests/rankrun.py)."""
+    ok_r, ok_m = rankrun.run(_rehearsal_worker, 2, tmp_path, timeout=100, init_timeout=60)
     assert ok_r and ok_m
