@@ -812,5 +812,11 @@ const char *error_name(int e) {
     }
 }
 
+std::string hex_literal(const std::string &s) { return hex_bytes(s); }
+
+bool code_symbol(const void *code, size_t size, const char *name, std::string *out) {
+    return elf_symbol((const unsigned char *)code, size, name, out);
+}
+
 }  // namespace desc
 }  // namespace dspb

@@ -59,5 +59,11 @@ int read(const void *code, size_t size, Descriptor *d, std::string *err);
 
 const char *error_name(int e);
 
+// "0x.., 0x.., ..." initialiser text of a byte string (generated device arrays)
+std::string hex_literal(const std::string &s);
+
+// the bytes of a defined object symbol of a code object's ELF (host only)
+bool code_symbol(const void *code, size_t size, const char *name, std::string *out);
+
 }  // namespace desc
 }  // namespace dspb

@@ -1,0 +1,875 @@
+// ir_proof.cpp -- facts about a plugin's audio_callback from its LLVM IR
+// (ir_proof.hpp).
+//
+// dsp_module_compile compiles the plugin a second time, through comgr, into
+// a flattened analysis kernel
+//
+//   dspb_proof(Parameters *P, State *S, float **out, unsigned C, unsigned B, float sr)
+//   { audio_callback(*P, *S, out, C, B, sr); }
+//
+// at -O2 without vectorisation or unrolling (the same source and IEEE
+// semantics as the code that runs: only the schedule differs), and reads the
+// optimised IR of that kernel.  Every SSA value gets
+//
+//   an origin (pointers): BUF (a block sample pointer: an element of `out`),
+//     TBL (`out` itself), PRM (Parameters), STA (State), LOC (private
+//     memory), GC / GM (constant / mutable global), EXT (a pointer read from
+//     memory other than `out`), UNK (made from an integer);
+//   dependence bits: IN (depends on a block sample), VAR (may differ between
+//     the callback's iterations: a phi, a private or block load, State that
+//     is written), ADDR (depends on an address as a number),
+//
+// iterated to a fixpoint over the phis.  Anything outside the model -- a call
+// that may touch memory, an atomic, a store to Parameters / `out` / a global,
+// a pointer stored to memory, a block address compared or turned into an
+// integer -- ends the analysis with `analyzed` false, and the product then
+// runs the callback on every block.
+//
+// What the facts prove (module.cpp uses them, plus probes of the callback):
+//   !reads_block: the callback reads no sample of its block (nor an address
+//       of one), so its output is a function of (Parameters, State, C, B, sr)
+//       only -- every block renders the same values (DSP_BLOCK_TABLE; which
+//       elements are written is pinned by two probes that differ everywhere);
+//   gain_form && !input_control: the sequence of block stores is the same on
+//       every call and each stores fl(x g) for the x loaded from that same
+//       address and one call-invariant g (DSP_BLOCK_GAIN; a probe of ones
+//       pins g and that every element is stored once);
+//   !writes_state: blocks are independent given the State, so a plugin with
+//       a State it only reads renders its blocks in parallel.
+#include "ir_proof.hpp"
+
+#include <dlfcn.h>
+
+#include <amd_comgr/amd_comgr.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <set>
+#include <sstream>
+
+namespace dspb {
+namespace irp {
+
+namespace {
+
+enum : uint32_t { O_BUF = 1, O_TBL = 2, O_PRM = 4, O_STA = 8, O_LOC = 16, O_GC = 32, O_GM = 64, O_EXT = 128, O_UNK = 256 };
+enum : uint32_t { D_IN = 1, D_VAR = 2, D_ADDR = 4 };
+
+struct Val {
+    uint32_t org = 0, data = 0;
+};
+
+struct Inst {
+    std::string res, op, text;      // result (or ""), opcode, operand text after the opcode
+    std::vector<std::string> parts; // `text` split at top-level commas
+};
+
+bool ident_char(char c) {
+    return (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z') || (c >= '0' && c <= '9') || c == '.' || c == '_' ||
+           c == '$' || c == '-';
+}
+
+std::string trim(const std::string &s) {
+    size_t a = 0, b = s.size();
+    while (a < b && (s[a] == ' ' || s[a] == '\t')) ++a;
+    while (b > a && (s[b - 1] == ' ' || s[b - 1] == '\t' || s[b - 1] == '\r')) --b;
+    return s.substr(a, b - a);
+}
+
+// the line without its `;` comment (outside string literals)
+std::string strip_comment(const std::string &s) {
+    bool q = false;
+    for (size_t i = 0; i < s.size(); ++i) {
+        if (s[i] == '"') q = !q;
+        else if (s[i] == ';' && !q) return s.substr(0, i);
+    }
+    return s;
+}
+
+std::vector<std::string> split_top(const std::string &s) {
+    std::vector<std::string> out;
+    int depth = 0;
+    bool q = false;
+    size_t start = 0;
+    for (size_t i = 0; i < s.size(); ++i) {
+        const char c = s[i];
+        if (c == '"') q = !q;
+        if (q) continue;
+        if (c == '(' || c == '[' || c == '{' || c == '<') ++depth;
+        else if (c == ')' || c == ']' || c == '}' || c == '>') --depth;
+        else if (c == ',' && depth == 0) {
+            out.push_back(trim(s.substr(start, i - start)));
+            start = i + 1;
+        }
+    }
+    const std::string last = trim(s.substr(start));
+    if (!last.empty()) out.push_back(last);
+    return out;
+}
+
+struct Module {
+    std::set<std::string> types;                       // %named types
+    std::map<std::string, bool> global_const;          // @global -> constant
+    std::map<std::string, std::string> fn_attrs;       // @function -> its attribute groups' text
+    std::map<std::string, std::string> attr_groups;    // #N -> text
+    std::map<std::string, std::vector<std::string>> fn_groups;  // @function -> #N ids
+};
+
+// value tokens (%x / @x) of an operand text, in order; named types and
+// `label %x` operands excluded
+std::vector<std::string> values_in(const std::string &s, const Module &M) {
+    std::vector<std::string> v;
+    for (size_t i = 0; i < s.size(); ++i) {
+        if (s[i] != '%' && s[i] != '@') continue;
+        size_t j = i + 1;
+        if (j < s.size() && s[j] == '"') {
+            const size_t e = s.find('"', j + 1);
+            if (e == std::string::npos) break;
+            j = e + 1;
+        } else {
+            while (j < s.size() && ident_char(s[j])) ++j;
+        }
+        const std::string tok = s.substr(i, j - i);
+        const bool is_label = i >= 6 && s.compare(i - 6, 6, "label ") == 0;
+        if (tok.size() > 1 && !is_label && !(s[i] == '%' && M.types.count(tok))) v.push_back(tok);
+        i = j - 1;
+    }
+    return v;
+}
+
+std::string first_value(const std::string &s, const Module &M) {
+    const auto v = values_in(s, M);
+    return v.empty() ? std::string() : v.front();
+}
+
+// the attribute-group ids (#N) after the argument list of a define / declare / call
+std::vector<std::string> groups_after_args(const std::string &s, size_t open) {
+    std::vector<std::string> g;
+    int depth = 0;
+    size_t i = open;
+    for (; i < s.size(); ++i) {
+        if (s[i] == '(') ++depth;
+        else if (s[i] == ')' && --depth == 0) break;
+    }
+    for (; i < s.size(); ++i) {
+        if (s[i] == '#') {
+            size_t j = i + 1;
+            while (j < s.size() && s[j] >= '0' && s[j] <= '9') ++j;
+            g.push_back(s.substr(i, j - i));
+            i = j;
+        }
+    }
+    return g;
+}
+
+bool starts_with(const std::string &s, const char *p) { return s.compare(0, std::strlen(p), p) == 0; }
+
+struct Analysis {
+    const Module &M;
+    std::map<std::string, Val> val;
+    std::map<std::string, const Inst *> def;
+    std::vector<Inst> body;
+    std::vector<std::string> args;  // the kernel's six parameters
+    uint32_t loc_data = 0, sta_data = 0;
+    Facts f;
+    std::string fail;
+
+    explicit Analysis(const Module &m) : M(m) {}
+
+    void stop(const std::string &why) {
+        if (fail.empty()) fail = why;
+    }
+
+    Val get(const std::string &tok) const {
+        Val v;
+        if (tok.empty()) return v;
+        if (tok[0] == '@') {
+            auto g = M.global_const.find(tok);
+            if (g != M.global_const.end()) v.org = g->second ? O_GC : O_GM;
+            return v;
+        }
+        auto it = val.find(tok);
+        return it == val.end() ? v : it->second;
+    }
+
+    bool callee_pure(const std::string &callee, const std::string &site_attrs) const {
+        std::string attrs = site_attrs;
+        auto g = M.fn_attrs.find(callee);
+        if (g != M.fn_attrs.end()) attrs += " " + g->second;
+        if (attrs.find("memory(none)") != std::string::npos) return true;
+        // device-library routines that only read constant tables
+        if (starts_with(callee, "@__ocml_") || starts_with(callee, "@__ockl_")) {
+            const size_t m = attrs.find("memory(");
+            if (m != std::string::npos) {
+                const size_t e = attrs.find(')', m);
+                const std::string mem = attrs.substr(m, e == std::string::npos ? std::string::npos : e - m);
+                if (mem.find("write") == std::string::npos) return true;
+            }
+        }
+        return false;
+    }
+
+    // one transfer step for instruction I; returns true when a value grew
+    bool step(const Inst &I, bool final_pass) {
+        Val r;
+        const std::string &op = I.op;
+        auto merge_all = [&](const std::string &s) {
+            for (const auto &t : values_in(s, M)) {
+                const Val v = get(t);
+                r.org |= v.org;
+                r.data |= v.data;
+            }
+        };
+        auto store_to = [&](const Val &P, const Val &Vv, bool val_is_ptr, const std::string &what) {
+            if (P.org & (O_TBL | O_PRM | O_GC | O_GM | O_EXT | O_UNK)) {
+                stop(what + " to " + (P.org & O_TBL ? "the block pointer table" : P.org & O_PRM ? "Parameters" :
+                                      (P.org & (O_GC | O_GM)) ? "global memory" : "memory behind a loaded pointer"));
+                return;
+            }
+            if (val_is_ptr && (Vv.org & (O_BUF | O_TBL | O_STA | O_PRM | O_LOC | O_EXT))) {
+                stop("a pointer is stored to memory");
+                return;
+            }
+            if (P.org & O_STA) {
+                f.writes_state = true;
+                sta_data |= Vv.data | P.data;
+            }
+            if (P.org & O_LOC) loc_data |= Vv.data | P.data;
+            if ((P.org & O_BUF) && (P.data & D_IN)) f.input_control = true;  // an input-dependent address
+        };
+        auto load_from = [&](const Val &P, bool ptr_result) {
+            Val v;
+            if (P.org & O_GM) stop("a load of mutable global memory");
+            if (P.org & O_UNK) stop("a load through a pointer made from an integer");
+            v.data = P.data & (D_IN | D_VAR | D_ADDR);
+            if (P.org & O_BUF) {
+                v.data |= D_IN | D_VAR;
+                f.reads_block = true;
+            }
+            if (P.org & O_LOC) v.data |= loc_data | D_VAR;
+            if (P.org & O_STA) v.data |= f.writes_state ? (sta_data | D_VAR) : 0u;
+            if (P.org & O_TBL) {
+                if (ptr_result) v.org |= O_BUF;
+                else stop("the block pointer table is read as data");
+            }
+            if (ptr_result && (P.org & (O_PRM | O_STA | O_LOC | O_GC | O_EXT))) v.org |= O_EXT;
+            if (ptr_result && (P.org & O_BUF)) v.org |= O_UNK;
+            return v;
+        };
+        if (op == "alloca") {
+            r.org = O_LOC;
+        } else if (op == "load") {
+            if (I.parts.size() < 2) return stop("unparsed load: " + I.text), false;
+            if (starts_with(I.text, "atomic")) return stop("an atomic load"), false;
+            const std::string &ty = I.parts[0];
+            const bool ptr_result = starts_with(ty, "ptr") || ty.find("x ptr") != std::string::npos ||
+                                    starts_with(ty, "volatile ptr");
+            r = load_from(get(first_value(I.parts[1], M)), ptr_result);
+        } else if (op == "store") {
+            if (I.parts.size() < 2) return stop("unparsed store: " + I.text), false;
+            if (starts_with(I.text, "atomic")) return stop("an atomic store"), false;
+            const std::string vt = first_value(I.parts[0], M);
+            const Val P = get(first_value(I.parts[1], M));
+            const Val Vv = get(vt);
+            const bool val_is_ptr = starts_with(I.parts[0], "ptr") || starts_with(I.parts[0], "volatile ptr") ||
+                                    I.parts[0].find("x ptr>") != std::string::npos;
+            if (final_pass) store_to(P, Vv, val_is_ptr, "a store");
+            else {
+                if (P.org & O_STA) {
+                    f.writes_state = true;
+                    sta_data |= Vv.data | P.data;
+                }
+                if (P.org & O_LOC) loc_data |= Vv.data | P.data;
+            }
+            return false;
+        } else if (op == "getelementptr") {
+            if (I.parts.size() < 2) return stop("unparsed getelementptr: " + I.text), false;
+            const Val b = get(first_value(I.parts[1], M));
+            r.org = b.org;
+            r.data = b.data;
+            for (size_t k = 2; k < I.parts.size(); ++k)
+                for (const auto &t : values_in(I.parts[k], M)) r.data |= get(t).data;
+        } else if (op == "bitcast" || op == "addrspacecast" || op == "freeze") {
+            merge_all(I.text);
+        } else if (op == "ptrtoint") {
+            const Val p = get(first_value(I.text, M));
+            if (p.org & (O_BUF | O_TBL | O_LOC | O_STA | O_PRM | O_EXT)) stop("an address is turned into an integer");
+            r.data = p.data | D_ADDR;
+        } else if (op == "inttoptr") {
+            r.org = O_UNK;
+            r.data = get(first_value(I.text, M)).data;
+        } else if (op == "icmp") {
+            merge_all(I.text);
+            if (r.org & (O_BUF | O_TBL)) stop("block addresses are compared");
+            r.org = 0;
+        } else if (op == "phi") {
+            // [ value, %block ], ...
+            for (const auto &p : split_top(I.text.substr(I.text.find('[') == std::string::npos ? 0
+                                                                                                : I.text.find('[')))) {
+                std::string in = p;
+                const size_t a = in.find('['), b = in.rfind(']');
+                if (a != std::string::npos && b != std::string::npos && b > a) in = in.substr(a + 1, b - a - 1);
+                const auto two = split_top(in);
+                if (two.empty()) continue;
+                const Val v = get(first_value(two[0], M));
+                r.org |= v.org;
+                r.data |= v.data;
+            }
+            r.data |= D_VAR;
+        } else if (op == "call") {
+            // the callee: the first value token directly followed by its
+            // argument list (`@f(` direct, `%fp(` indirect)
+            std::string callee;
+            size_t e = std::string::npos;
+            for (size_t i = 0; i < I.text.size(); ++i) {
+                if (I.text[i] != '@' && I.text[i] != '%') continue;
+                size_t j = i + 1;
+                while (j < I.text.size() && ident_char(I.text[j])) ++j;
+                if (j < I.text.size() && I.text[j] == '(') {
+                    callee = I.text.substr(i, j - i);
+                    e = j;
+                    break;
+                }
+                i = j - 1;
+            }
+            if (callee.empty()) return stop("an unparsed call: " + I.text), false;
+            if (callee[0] == '%') return stop("an indirect call"), false;
+            const size_t open = I.text.find('(', e);
+            std::string argtext;
+            if (open != std::string::npos) {
+                int depth = 0;
+                size_t k = open;
+                for (; k < I.text.size(); ++k) {
+                    if (I.text[k] == '(') ++depth;
+                    else if (I.text[k] == ')' && --depth == 0) break;
+                }
+                argtext = I.text.substr(open + 1, k > open ? k - open - 1 : 0);
+            }
+            const auto a = split_top(argtext);
+            std::string site;
+            for (const auto &g : groups_after_args(I.text, open == std::string::npos ? I.text.size() : open)) {
+                auto it = M.attr_groups.find(g);
+                if (it != M.attr_groups.end()) site += " " + it->second;
+            }
+            if (starts_with(callee, "@llvm.memcpy") || starts_with(callee, "@llvm.memmove")) {
+                if (a.size() < 3) return stop("unparsed memcpy"), false;
+                const Val src = get(first_value(a[1], M));
+                Val v = load_from(src, false);
+                v.data |= get(first_value(a[2], M)).data;
+                const Val dst = get(first_value(a[0], M));
+                if (final_pass) store_to(dst, v, false, "a memcpy");
+                else {
+                    if (dst.org & O_STA) { f.writes_state = true; sta_data |= v.data | dst.data; }
+                    if (dst.org & O_LOC) loc_data |= v.data | dst.data;
+                }
+                if (final_pass && (dst.org & O_BUF)) gain_breakers.insert("a memcpy into the block");
+                return false;
+            }
+            if (starts_with(callee, "@llvm.memset")) {
+                if (a.size() < 3) return stop("unparsed memset"), false;
+                Val v = get(first_value(a[1], M));
+                v.data |= get(first_value(a[2], M)).data;
+                const Val dst = get(first_value(a[0], M));
+                if (final_pass) store_to(dst, v, false, "a memset");
+                else {
+                    if (dst.org & O_STA) { f.writes_state = true; sta_data |= v.data | dst.data; }
+                    if (dst.org & O_LOC) loc_data |= v.data | dst.data;
+                }
+                if (final_pass && (dst.org & O_BUF)) gain_breakers.insert("a memset of the block");
+                return false;
+            }
+            static const char *kIgnore[] = {"@llvm.lifetime.", "@llvm.assume", "@llvm.experimental.noalias.scope.decl",
+                                            "@llvm.dbg.", "@llvm.donothing", "@llvm.trap", "@llvm.debugtrap",
+                                            "@llvm.sideeffect", "@llvm.pseudoprobe"};
+            for (const char *p : kIgnore)
+                if (starts_with(callee, p)) return false;
+            static const char *kLane[] = {"workitem", "workgroup", "dispatch", "implicitarg", "readfirstlane",
+                                          "readlane", "ballot", "mbcnt", ".ds.", "getreg", "memtime", "memrealtime",
+                                          "s.sleep", "wave", "lds", "cluster", "queue", "permlane", "update.dpp",
+                                          "mov.dpp", "icmp", "fcmp", "wqm", "wwm", "barrier", "s.wait"};
+            if (starts_with(callee, "@llvm.amdgcn."))
+                for (const char *p : kLane)
+                    if (callee.find(p) != std::string::npos) return stop("a lane-dependent builtin: " + callee), false;
+            if (!callee_pure(callee, site)) return stop("a call that may touch memory: " + callee), false;
+            for (const auto &x : a)
+                for (const auto &t : values_in(x, M)) {
+                    const Val v = get(t);
+                    r.data |= v.data;
+                    if (v.org & (O_BUF | O_TBL)) stop("a block pointer is passed to " + callee);
+                }
+        } else if (op == "atomicrmw" || op == "cmpxchg" || op == "fence" || op == "va_arg" || op == "invoke" ||
+                   op == "callbr" || op == "indirectbr" || op == "landingpad" || op == "resume") {
+            stop("a `" + op + "` instruction");
+        } else if (op == "br" || op == "switch") {
+            if (final_pass) {
+                const std::string c = first_value(I.text, M);
+                if (get(c).data & D_IN) f.input_control = true;
+            }
+            return false;
+        } else if (op == "ret" || op == "unreachable") {
+            return false;
+        } else {  // arithmetic, casts, compares, selects, aggregates, vectors
+            merge_all(I.text);
+        }
+        if (I.res.empty()) return false;
+        Val &cur = val[I.res];
+        const Val before = cur;
+        cur.org |= r.org;
+        cur.data |= r.data;
+        return cur.org != before.org || cur.data != before.data;
+    }
+
+    std::set<std::string> gain_breakers;
+    std::map<std::string, std::string> canon_memo;
+
+    // canonical text of a call-invariant value (an operand part or a token)
+    std::string canon_tok(const std::string &tok, int depth) {
+        if (depth > 48) return "?";
+        if (tok[0] == '@') return tok;
+        for (size_t i = 0; i < args.size(); ++i)
+            if (args[i] == tok) return "arg" + std::to_string(i);
+        auto m = canon_memo.find(tok);
+        if (m != canon_memo.end()) return m->second;
+        auto d = def.find(tok);
+        if (d == def.end()) return "?";
+        const Inst &I = *d->second;
+        if (I.op == "phi") return "?";
+        std::string c = I.op + "(";
+        for (const auto &p : I.parts)
+            if (p.empty() || p[0] != '!') c += canon_part(p, depth + 1) + ",";  // (metadata dropped)
+        c += ")";
+        canon_memo[tok] = c;
+        return c;
+    }
+    std::string canon_part(const std::string &part, int depth) {
+        std::string out;
+        const auto toks = values_in(part, M);
+        size_t pos = 0;
+        for (const auto &t : toks) {
+            const size_t at = part.find(t, pos);
+            if (at == std::string::npos) break;
+            out += part.substr(pos, at - pos) + "{" + canon_tok(t, depth) + "}";
+            pos = at + t.size();
+        }
+        return out + part.substr(pos);
+    }
+
+    void check_gain() {
+        std::string g_all;
+        int stores = 0;
+        for (const Inst &I : body) {
+            if (I.op != "store" || I.parts.size() < 2) continue;
+            const std::string ptr = first_value(I.parts[1], M);
+            if (!(get(ptr).org & O_BUF)) continue;
+            ++stores;
+            auto fail_gain = [&](const std::string &w) { gain_breakers.insert(w); };
+            if (!starts_with(I.parts[0], "float ")) { fail_gain("a block store that is not one float"); continue; }
+            if (get(ptr).data & (D_IN | D_ADDR)) { fail_gain("an input-dependent block address"); continue; }
+            const std::string v = first_value(I.parts[0], M);
+            auto d = def.find(v);
+            if (v.empty() || d == def.end() || d->second->op != "fmul") {
+                fail_gain("a block store that is not a product");
+                continue;
+            }
+            const Inst &mul = *d->second;
+            const auto ops = values_in(mul.text, M);
+            std::string load_tok, g_part;
+            const auto mparts = split_top(mul.text);
+            if (mparts.size() != 2) { fail_gain("an unparsed product"); continue; }
+            for (int k = 0; k < 2; ++k) {
+                const std::string t = first_value(mparts[k], M);
+                auto ld = def.find(t);
+                if (load_tok.empty() && !t.empty() && ld != def.end() && ld->second->op == "load" &&
+                    ld->second->parts.size() >= 2 && first_value(ld->second->parts[1], M) == ptr) {
+                    load_tok = t;
+                    g_part = mparts[1 - k];
+                }
+            }
+            if (load_tok.empty()) { fail_gain("a block store of a product that is not x * g at its own address"); continue; }
+            const std::string gt = first_value(g_part, M);
+            if (!gt.empty() && (get(gt).data & (D_IN | D_VAR | D_ADDR))) {
+                fail_gain("a gain that varies within the call");
+                continue;
+            }
+            // the type word of the first operand part ("float %x") is dropped
+            std::string gp = g_part;
+            if (starts_with(gp, "float ")) gp = gp.substr(6);
+            const std::string c = canon_part(gp, 0);
+            if (c.find('?') != std::string::npos) { fail_gain("a gain outside the canonical forms"); continue; }
+            if (g_all.empty()) {
+                g_all = c;
+                if (!gain_source(gp, gt)) fail_gain("a gain not read directly from Parameters / State / a constant");
+            } else if (g_all != c) {
+                fail_gain("two different gains");
+            }
+        }
+        // (no block store at all: the identity, g = 1)
+        f.gain_form = gain_breakers.empty();
+        if (f.gain_form && !stores) {
+            f.gain_src = 'K';
+            f.gain_bits = 0x3f800000u;
+        }
+        if (f.gain_form) f.gain_expr = stores ? g_all : "1 (no block store)";
+        else if (f.why.empty()) f.why = "not a gain: " + *gain_breakers.begin();
+    }
+
+    // Where g comes from, so that the host knows its value without running
+    // the callback: a float constant, the sample rate argument, or a float
+    // load at a constant byte offset of Parameters / State.
+    bool gain_source(const std::string &gp, const std::string &gt) {
+        if (gt.empty()) {  // a constant: LLVM writes floats as decimal or as the f64 bits in hex
+            double v = 0.0;
+            if (starts_with(gp, "0x") && gp.size() == 18) {
+                const unsigned long long b = std::strtoull(gp.c_str() + 2, nullptr, 16);
+                std::memcpy(&v, &b, 8);
+            } else {
+                char *e = nullptr;
+                v = std::strtod(gp.c_str(), &e);
+                if (!e || e == gp.c_str()) return false;
+            }
+            const float fv = (float)v;
+            if ((double)fv != v) return false;
+            f.gain_src = 'K';
+            std::memcpy(&f.gain_bits, &fv, 4);
+            return true;
+        }
+        if (args.size() == 6 && gt == args[5]) {
+            f.gain_src = 'R';
+            return true;
+        }
+        auto d = def.find(gt);
+        if (d == def.end() || d->second->op != "load" || d->second->parts.size() < 2 ||
+            d->second->parts[0] != "float")
+            return false;
+        const std::string p = first_value(d->second->parts[1], M);
+        uint64_t off = 0;
+        std::string base = p;
+        auto g = def.find(p);
+        if (g != def.end() && g->second->op == "getelementptr") {
+            const Inst &G = *g->second;
+            if (G.parts.size() != 3) return false;
+            const std::string &et = G.parts[0];
+            const uint64_t esz = et == "i8" ? 1 : (et == "float" || et == "i32") ? 4 : (et == "double" || et == "i64") ? 8 : 0;
+            if (!esz || !values_in(G.parts[2], M).empty()) return false;
+            const size_t sp = G.parts[2].find(' ');
+            if (sp == std::string::npos) return false;
+            char *e = nullptr;
+            const long long k = std::strtoll(G.parts[2].c_str() + sp + 1, &e, 10);
+            if (k < 0 || k > (1 << 20)) return false;
+            off = (uint64_t)k * esz;
+            base = first_value(G.parts[1], M);
+        }
+        if (args.size() != 6 || (base != args[0] && base != args[1])) return false;
+        f.gain_src = base == args[0] ? 'P' : 'S';
+        f.gain_off = (uint32_t)off;
+        return true;
+    }
+};
+
+Module scan_module(const std::string &ir) {
+    Module M;
+    std::istringstream in(ir);
+    std::string line;
+    while (std::getline(in, line)) {
+        if (starts_with(line, "%")) {
+            const size_t e = line.find(" = type ");
+            if (e != std::string::npos) M.types.insert(line.substr(0, e));
+        } else if (starts_with(line, "@")) {
+            const size_t e = line.find(" = ");
+            if (e == std::string::npos) continue;
+            const std::string name = line.substr(0, e);
+            std::istringstream w(line.substr(e + 3));
+            std::string tok;
+            bool is_const = false, found = false;
+            while (w >> tok) {
+                if (tok == "constant") { is_const = true; found = true; break; }
+                if (tok == "global") { found = true; break; }
+            }
+            if (found) M.global_const[name] = is_const;
+        } else if (starts_with(line, "attributes #")) {
+            const size_t e = line.find(" = ");
+            if (e != std::string::npos) M.attr_groups[line.substr(11, e - 11)] = line.substr(e + 3);
+        } else if (starts_with(line, "define ") || starts_with(line, "declare ")) {
+            const size_t at = line.find('@');
+            if (at == std::string::npos) continue;
+            size_t e = at + 1;
+            while (e < line.size() && ident_char(line[e])) ++e;
+            M.fn_groups[line.substr(at, e - at)] = groups_after_args(line, line.find('(', e));
+        }
+    }
+    for (auto &fg : M.fn_groups) {
+        std::string t;
+        for (const auto &g : fg.second) {
+            auto it = M.attr_groups.find(g);
+            if (it != M.attr_groups.end()) t += " " + it->second;
+        }
+        M.fn_attrs[fg.first] = t;
+    }
+    return M;
+}
+
+}  // namespace
+
+Facts analyze(const std::string &ir, const char *fn) {
+    Module M = scan_module(ir);
+    Analysis A(M);
+    std::istringstream in(ir);
+    std::string line;
+    const std::string want = std::string("@") + fn + "(";
+    bool inside = false;
+    std::string pending;  // a switch spanning lines
+    while (std::getline(in, line)) {
+        if (!inside) {
+            if (starts_with(line, "define ") && line.find(want) != std::string::npos) {
+                inside = true;
+                const size_t open = line.find(want) + want.size() - 1;
+                int depth = 0;
+                size_t k = open;
+                for (; k < line.size(); ++k) {
+                    if (line[k] == '(') ++depth;
+                    else if (line[k] == ')' && --depth == 0) break;
+                }
+                for (const auto &p : split_top(line.substr(open + 1, k - open - 1))) {
+                    const auto v = values_in(p, M);
+                    A.args.push_back(v.empty() ? std::string() : v.back());
+                }
+            }
+            continue;
+        }
+        std::string s = trim(strip_comment(line));
+        if (s == "}") break;
+        if (s.empty()) continue;
+        if (!pending.empty()) {
+            pending += " " + s;
+            if (s.find(']') == std::string::npos) continue;
+            s = pending;
+            pending.clear();
+        } else if (starts_with(s, "switch ") && s.find(']') == std::string::npos) {
+            pending = s;
+            continue;
+        }
+        if (s.back() == ':' && s.find(' ') == std::string::npos) continue;  // a block label
+        Inst I;
+        std::string rest = s;
+        if (s[0] == '%') {
+            const size_t e = s.find(" = ");
+            if (e == std::string::npos) continue;
+            I.res = s.substr(0, e);
+            rest = s.substr(e + 3);
+        }
+        std::istringstream w(rest);
+        std::string word;
+        w >> word;
+        while (word == "tail" || word == "musttail" || word == "notail") w >> word;
+        I.op = word;
+        std::string tail;
+        std::getline(w, tail);
+        tail = trim(tail);
+        // fast-math and wrap flags before the operands
+        static const std::set<std::string> kFlags = {"nnan", "ninf", "nsz", "arcp", "contract", "afn", "reassoc",
+                                                     "fast", "nuw", "nsw", "exact", "disjoint", "nneg", "samesign",
+                                                     "volatile", "inbounds", "inrange"};
+        for (;;) {
+            const size_t sp = tail.find(' ');
+            if (sp == std::string::npos || !kFlags.count(tail.substr(0, sp))) break;
+            tail = trim(tail.substr(sp + 1));
+        }
+        if (I.op == "icmp" || I.op == "fcmp") {  // the predicate
+            const size_t sp = tail.find(' ');
+            if (sp != std::string::npos) tail = trim(tail.substr(sp + 1));
+        }
+        I.text = tail;
+        I.parts = split_top(tail);
+        A.body.push_back(I);
+    }
+    if (!inside) {
+        A.f.why = std::string("no function ") + fn + " in the IR";
+        return A.f;
+    }
+    if (A.args.size() != 6) {
+        A.f.why = "the analysis kernel does not have six parameters";
+        return A.f;
+    }
+    for (const Inst &I : A.body)
+        if (!I.res.empty()) A.def[I.res] = &I;
+    A.val[A.args[0]].org = O_PRM;
+    A.val[A.args[1]].org = O_STA;
+    A.val[A.args[2]].org = O_TBL;
+    for (int it = 0; it < 64; ++it) {
+        bool grew = false;
+        const uint32_t ld = A.loc_data, sd = A.sta_data;
+        const bool ws = A.f.writes_state;
+        for (const Inst &I : A.body) grew |= A.step(I, false);
+        if (!grew && ld == A.loc_data && sd == A.sta_data && ws == A.f.writes_state) break;
+    }
+    for (const Inst &I : A.body) A.step(I, true);
+    if (!A.fail.empty()) {
+        A.f.why = A.fail;
+        A.f.analyzed = false;
+        A.f.gain_form = false;
+        return A.f;
+    }
+    A.f.analyzed = true;
+    A.check_gain();
+    if (A.f.input_control && A.f.gain_form) {
+        A.f.gain_form = false;
+        A.f.why = "not a gain: which samples are stored depends on a sample (a branch or an address)";
+    }
+    return A.f;
+}
+
+// ---------------------------------------------------------------------------
+// comgr: plugin TU -> optimised IR text
+// ---------------------------------------------------------------------------
+namespace {
+
+struct Comgr {
+    amd_comgr_data_set_t in{}, out{};
+    amd_comgr_action_info_t ai{};
+    bool have_in = false, have_out = false, have_ai = false;
+    ~Comgr() {
+        if (have_ai) amd_comgr_destroy_action_info(ai);
+        if (have_out) amd_comgr_destroy_data_set(out);
+        if (have_in) amd_comgr_destroy_data_set(in);
+    }
+};
+
+bool add_data(amd_comgr_data_set_t set, amd_comgr_data_kind_t k, const std::string &txt, const char *name) {
+    amd_comgr_data_t d;
+    if (amd_comgr_create_data(k, &d)) return false;
+    const bool ok = !amd_comgr_set_data(d, txt.size(), txt.data()) && !amd_comgr_set_data_name(d, name) &&
+                    !amd_comgr_data_set_add(set, d);
+    amd_comgr_release_data(d);
+    return ok;
+}
+
+bool get_data(amd_comgr_data_set_t set, amd_comgr_data_kind_t k, std::string *out) {
+    size_t n = 0;
+    if (amd_comgr_action_data_count(set, k, &n) || n == 0) return false;
+    amd_comgr_data_t d;
+    if (amd_comgr_action_data_get_data(set, k, 0, &d)) return false;
+    size_t sz = 0;
+    bool ok = !amd_comgr_get_data(d, &sz, nullptr);
+    if (ok) {
+        out->assign(sz, '\0');
+        ok = !amd_comgr_get_data(d, &sz, &(*out)[0]);
+    }
+    amd_comgr_release_data(d);
+    return ok;
+}
+
+// hiprtc's runtime header (libhiprtc-builtins), which hiprtc pre-includes
+bool hiprtc_runtime_header(std::string *out) {
+    static std::string text;
+    static bool tried = false, ok = false;
+    if (!tried) {
+        tried = true;
+        void *h = dlopen("libhiprtc-builtins.so.7", RTLD_NOW | RTLD_LOCAL);
+        if (!h) h = dlopen("libhiprtc-builtins.so", RTLD_NOW | RTLD_LOCAL);
+        if (h) {
+            const char *hdr = (const char *)dlsym(h, "__hipRTC_header");
+            const unsigned *sz = (const unsigned *)dlsym(h, "__hipRTC_header_size");
+            if (hdr && sz) {
+                text.assign(hdr, *sz);
+                ok = true;
+            }
+        }
+    }
+    *out = text;
+    return ok;
+}
+
+}  // namespace
+
+int compile_to_ir(const std::string &tu, const std::vector<std::pair<std::string, std::string>> &includes,
+                  const std::vector<std::string> &options, std::string *ir, std::string *log) {
+    std::string rt;
+    if (!hiprtc_runtime_header(&rt)) {
+        *log = "libhiprtc-builtins (the hiprtc runtime header) not found";
+        return -1;
+    }
+    Comgr c;
+    if (amd_comgr_create_data_set(&c.in)) return *log = "comgr: data set", -1;
+    c.have_in = true;
+    if (amd_comgr_create_data_set(&c.out)) return *log = "comgr: data set", -1;
+    c.have_out = true;
+    if (!add_data(c.in, AMD_COMGR_DATA_KIND_SOURCE, tu, "dspb_proof.hip") ||
+        !add_data(c.in, AMD_COMGR_DATA_KIND_INCLUDE, rt, "hiprtc_runtime.h"))
+        return *log = "comgr: input", -1;
+    for (const auto &inc : includes)
+        if (!add_data(c.in, AMD_COMGR_DATA_KIND_INCLUDE, inc.second, inc.first.c_str()))
+            return *log = "comgr: include " + inc.first, -1;
+    if (amd_comgr_create_action_info(&c.ai)) return *log = "comgr: action info", -1;
+    c.have_ai = true;
+    std::vector<const char *> opts = {"-S", "-emit-llvm", "-nogpuinc", "-D__HIPCC_RTC__", "-include", "hiprtc_runtime.h"};
+    for (const auto &o : options) opts.push_back(o.c_str());
+    if (amd_comgr_action_info_set_language(c.ai, AMD_COMGR_LANGUAGE_HIP) ||
+        amd_comgr_action_info_set_isa_name(c.ai, "amdgcn-amd-amdhsa--gfx950") ||
+        amd_comgr_action_info_set_option_list(c.ai, opts.data(), opts.size()) ||
+        amd_comgr_action_info_set_logging(c.ai, true))
+        return *log = "comgr: options", -1;
+    const amd_comgr_status_t st =
+        amd_comgr_do_action(AMD_COMGR_ACTION_COMPILE_SOURCE_WITH_DEVICE_LIBS_TO_BC, c.ai, c.in, c.out);
+    std::string lg;
+    get_data(c.out, AMD_COMGR_DATA_KIND_LOG, &lg);
+    *log = lg;
+    if (st != AMD_COMGR_STATUS_SUCCESS || !get_data(c.out, AMD_COMGR_DATA_KIND_BC, ir)) {
+        if (log->empty()) *log = "comgr: compile failed";
+        return -1;
+    }
+    if (ir->compare(0, 1, ";") != 0 && ir->find("define ") == std::string::npos) {
+        *log = "comgr returned no IR text";
+        return -1;
+    }
+    return 0;
+}
+
+// ---------------------------------------------------------------------------
+std::string encode(const Facts &f) {
+    auto clean = [](std::string s) {
+        for (char &c : s)
+            if (c == '\n' || c == '\0') c = ' ';
+        return s;
+    };
+    std::string s = "dspb_facts 1\n";
+    s += "analyzed=" + std::to_string(f.analyzed) + "\n";
+    s += "reads_block=" + std::to_string(f.reads_block) + "\n";
+    s += "writes_state=" + std::to_string(f.writes_state) + "\n";
+    s += "input_control=" + std::to_string(f.input_control) + "\n";
+    s += "gain_form=" + std::to_string(f.gain_form) + "\n";
+    s += "gain=" + clean(f.gain_expr.substr(0, 512)) + "\n";
+    s += "gain_src=" + std::string(f.gain_src ? 1 : 0, f.gain_src) + "\n";
+    s += "gain_off=" + std::to_string(f.gain_off) + "\n";
+    s += "gain_bits=" + std::to_string(f.gain_bits) + "\n";
+    s += "why=" + clean(f.why.substr(0, 512)) + "\n";
+    return s;
+}
+
+bool decode(const std::string &s, Facts *f) {
+    *f = Facts{};
+    std::istringstream in(s);
+    std::string line;
+    if (!std::getline(in, line) || line != "dspb_facts 1") return false;
+    bool have_analyzed = false;
+    while (std::getline(in, line)) {
+        const size_t e = line.find('=');
+        if (e == std::string::npos) continue;
+        const std::string k = line.substr(0, e), v = line.substr(e + 1);
+        if (k == "analyzed") f->analyzed = v == "1", have_analyzed = true;
+        else if (k == "reads_block") f->reads_block = v == "1";
+        else if (k == "writes_state") f->writes_state = v == "1";
+        else if (k == "input_control") f->input_control = v == "1";
+        else if (k == "gain_form") f->gain_form = v == "1";
+        else if (k == "gain") f->gain_expr = v;
+        else if (k == "gain_src") f->gain_src = v.empty() ? 0 : v[0];
+        else if (k == "gain_off") f->gain_off = (uint32_t)std::strtoul(v.c_str(), nullptr, 10);
+        else if (k == "gain_bits") f->gain_bits = (uint32_t)std::strtoul(v.c_str(), nullptr, 10);
+        else if (k == "why") f->why = v;
+    }
+    return have_analyzed;
+}
+
+}  // namespace irp
+}  // namespace dspb

@@ -1,0 +1,55 @@
+// ir_proof.hpp -- what a plugin's audio_callback does with its block, read
+// from the callback's own LLVM IR (ir_proof.cpp).
+//
+// The reference calls the compiled callback on every block
+// (audio.cpp:160-165 -> compiler.cpp:1181-1187).  The product may render a
+// block class instead (module.h DSP_BLOCK_TABLE / DSP_BLOCK_GAIN) or run the
+// blocks of a plugin with a State in parallel; it does so only on facts this
+// analysis establishes about the callback's code, never on probe outputs
+// alone.
+#pragma once
+#include <stdint.h>
+
+#include <string>
+#include <utility>
+#include <vector>
+
+namespace dspb {
+namespace irp {
+
+struct Facts {
+    bool analyzed = false;      // every instruction of the callback was inside the analysis
+    bool reads_block = false;   // a load (or memcpy source) through a block sample pointer
+    bool writes_state = false;  // a store (or memset / memcpy destination) through State
+    bool input_control = false; // a branch / switch condition depends on a block sample
+    bool gain_form = false;     // every block store is fl(x g) at the address x was loaded
+                                // from, with one g for the whole call (no sample, no
+                                // loop-carried value, no address in it); no block store
+                                // at all is the identity (g = 1)
+    std::string gain_expr;      // g, canonical (diagnostics)
+    // gain_form: where g comes from -- 'P' / 'S' a float at byte gain_off of
+    // Parameters / State, 'K' the constant with bits gain_bits, 'R' the
+    // sample-rate argument -- so that its value is known without the callback
+    char gain_src = 0;
+    uint32_t gain_off = 0, gain_bits = 0;
+    std::string why;            // the first construct that ended the analysis, or why a
+                                // property does not hold
+};
+
+// Analyse kernel `fn` of module text `ir`, a kernel of the form
+//   fn(Parameters *P, State *S, float **out, unsigned C, unsigned B, float sr)
+//   { audio_callback(*P, *S, out, C, B, sr); }   (flattened: the callback inlined)
+Facts analyze(const std::string &ir, const char *fn);
+
+// Compile a HIP translation unit to optimised LLVM IR text for gfx950 through
+// comgr (the same front end hiprtc drives), with the hiprtc runtime header
+// pre-included as hiprtc does.  0 on success, else -1 with *log set.
+int compile_to_ir(const std::string &tu, const std::vector<std::pair<std::string, std::string>> &includes,
+                  const std::vector<std::string> &options, std::string *ir, std::string *log);
+
+// Facts <-> the compact text stored in a code object (dspb_callback_facts).
+std::string encode(const Facts &f);
+bool decode(const std::string &s, Facts *f);
+
+}  // namespace irp
+}  // namespace dspb

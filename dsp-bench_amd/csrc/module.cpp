@@ -28,6 +28,7 @@
 #include <vector>
 
 #include "descriptor.hpp"
+#include "ir_proof.hpp"
 #include "dspbench/module.h"
 #include "kernels.hpp"
 
@@ -75,6 +76,7 @@ struct RenderArgsG {
     unsigned lds;  // path: stateful 1 = LDS double buffer; stateless 1/2 private, 3 LDS blocks
     unsigned lds_nb;      // stateless LDS path: blocks per workgroup round
     unsigned lds_stride;  // stateless LDS path: floats per block in LDS (C B + 1)
+    unsigned par;         // blocks render independently (dsp_module: par), in parallel
 };
 
 const char *kDriver = R"DSPB(
@@ -93,6 +95,7 @@ struct dspb_render_args {
     unsigned lds;
     unsigned lds_nb;
     unsigned lds_stride;
+    unsigned par;
 };
 extern "C" __global__ void dspb_sizes(unsigned *o) {
     o[0] = sizeof(Parameters);
@@ -147,6 +150,21 @@ typedef __attribute__((address_space(1))) float dspb_gfloat;
 template <class T> __device__ static inline T dspb_from_global(const void *p) {
     return *(const __attribute__((address_space(1))) T *)p;
 }
+// the State of a parallel render: empty, or one the callback never writes
+// (dsp_module_facts: proven from the callback's IR, with no global memory
+// written).  Each lane calls the
+// callback with a private copy when the State is small (its fields then stay
+// in registers), else with the shared blob itself (read only).
+template <bool kSmall = (sizeof(State) <= 256)> struct dspb_ro_state {
+    State s;
+    __device__ explicit dspb_ro_state(const void *p) : s(dspb_from_global<State>(p)) {}
+    __device__ State &get() { return s; }
+};
+template <> struct dspb_ro_state<false> {
+    State *s;
+    __device__ explicit dspb_ro_state(const void *p) : s((State *)p) {}
+    __device__ State &get() { return *s; }
+};
 // a generic pointer the compiler can prove is global memory (global_load /
 // global_store in the inlined callback, not flat ops that also wait on LDS)
 __device__ static inline float *dspb_global(float *p) { return (float *)(dspb_gfloat *)p; }
@@ -160,7 +178,7 @@ __device__ static inline float *dspb_global(float *p) { return (float *)(dspb_gf
 // lives in registers instead of scratch.
 template <unsigned CC>
 __device__ static void dspb_stateless(const dspb_render_args &A) {
-    State local = dspb_from_global<State>(A.S);
+    dspb_ro_state<> local(A.S);
     // a private copy: the callback's stores cannot alias it, so its fields
     // stay in registers instead of being reloaded after every store
     Parameters prm = dspb_from_global<Parameters>(A.P);
@@ -189,7 +207,7 @@ __device__ static void dspb_stateless(const dspb_render_args &A) {
         if (t < nb) {
             float *ptrs[CC ? CC : 16];
             for (unsigned c = 0; c < C; ++c) ptrs[c] = dspb_global(A.out[c] + (i0 + (unsigned long long)t * A.B));
-            audio_callback(prm, local, ptrs, C, A.B, A.sr);
+            audio_callback(prm, local.get(), ptrs, C, A.B, A.sr);
         }
         __syncthreads();
     }
@@ -245,7 +263,7 @@ __device__ static void dspb_stateful_lds(const dspb_render_args &A) {
 template <unsigned CC, unsigned BB>
 __device__ static void dspb_stateless_lds(const dspb_render_args &A) {
     extern __shared__ float dspb_lbuf[];
-    State local = dspb_from_global<State>(A.S);
+    dspb_ro_state<> local(A.S);
     Parameters prm = dspb_from_global<Parameters>(A.P);
     const unsigned C = CC ? CC : A.C, B = BB ? BB : A.B, NB = A.lds_nb, SB = A.lds_stride;
     const unsigned t = threadIdx.x, nt = blockDim.x;
@@ -294,7 +312,7 @@ __device__ static void dspb_stateless_lds(const dspb_render_args &A) {
             float *blk = dspb_lbuf + t * SB;
             float *ptrs[CC ? CC : 16];
             for (unsigned c = 0; c < C; ++c) ptrs[c] = blk + c * B;
-            audio_callback(prm, local, ptrs, C, B, A.sr);
+            audio_callback(prm, local.get(), ptrs, C, B, A.sr);
         }
         __syncthreads();
         for (unsigned c = 0; c < C; ++c) {
@@ -341,7 +359,7 @@ __device__ static void dspb_stateless_lds_pf(const dspb_render_args &A) {
     constexpr unsigned N4 = NB * B / 4u, PT = (N4 + 255u) / 256u;  // float4 per channel per round / per thread
     static_assert(NB <= 64 && B % 4 == 0, "one wave runs a round's callbacks");
     typedef __attribute__((address_space(1))) float4 gfloat4;
-    State local = dspb_from_global<State>(A.S);
+    dspb_ro_state<> local(A.S);
     Parameters prm = dspb_from_global<Parameters>(A.P);
     const unsigned t = threadIdx.x, lane = t & 63u;
     const unsigned long long stride = (unsigned long long)gridDim.x * NB;
@@ -405,7 +423,7 @@ __device__ static void dspb_stateless_lds_pf(const dspb_render_args &A) {
             float *blk = dspb_lbuf + lane * SB;
             float *ptrs[C];
             for (unsigned c = 0; c < C; ++c) ptrs[c] = blk + c * B;
-            audio_callback(prm, local, ptrs, C, B, A.sr);
+            audio_callback(prm, local.get(), ptrs, C, B, A.sr);
         }
         __syncthreads();
         for (unsigned c = 0; c < C; ++c) {
@@ -434,7 +452,7 @@ __device__ static void dspb_stateless_lds_pf(const dspb_render_args &A) {
 #define DSPB_LDS_KERNEL(name, CC, BB)                                                  \
     extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) void name(  \
         dspb_render_args A) {                                                          \
-        if constexpr (__is_empty(State)) {                                             \
+        if (A.par) {                                                                   \
             if constexpr (CC > 0 && BB > 0 && BB % 4 == 0) dspb_stateless_lds_pf<CC, BB>(A); \
             else dspb_stateless_lds<CC, BB>(A);                                        \
         }                                                                              \
@@ -448,7 +466,7 @@ DSPB_LDS_KERNEL(dspb_render_lds_c2, 2, 0)
 DSPB_LDS_KERNEL(dspb_render_lds, 0, 0)
 extern "C" __global__ void dspb_render(dspb_render_args A) {
     extern __shared__ float dspb_lbuf[];
-    if (__is_empty(State)) {
+    if (A.par) {
         if (A.C == 1) dspb_stateless<1>(A);
         else if (A.C == 2) dspb_stateless<2>(A);
         else dspb_stateless<0>(A);
@@ -476,7 +494,7 @@ extern "C" __global__ void dspb_render(dspb_render_args A) {
 #define DSPB_ST_KERNEL(name, CC, BB)                                                   \
     extern "C" __global__ void name(dspb_render_args A) {                              \
         extern __shared__ float dspb_lbuf[];                                           \
-        if (!__is_empty(State) && blockIdx.x == 0) dspb_stateful_lds<CC, BB>(A);       \
+        if (!A.par && blockIdx.x == 0) dspb_stateful_lds<CC, BB>(A);                   \
     }
 DSPB_ST_KERNEL(dspb_render_st_c2b512, 2, 512)
 DSPB_ST_KERNEL(dspb_render_st_c2b256, 2, 256)
@@ -516,7 +534,14 @@ struct dsp_module {
     hipFunction_t f_sizes = nullptr, f_defaults = nullptr, f_init = nullptr, f_render = nullptr,
                   f_callback = nullptr;
     uint32_t params_size = 0, state_size = 0;
-    int stateless = 0;
+    int stateless = 0;                 // State is empty
+    // blocks render independently, so in parallel: the callback's IR was
+    // analysed completely (no global memory written, no unknown call) and it
+    // never writes its State (facts); otherwise the blocks run in order on
+    // one lane, as the reference's audio thread runs them
+    int par = 0;
+    bool has_facts = false;            // the code object carries dspb_callback_facts
+    dspb::irp::Facts facts;            // what the callback's IR shows (ir_proof.hpp)
     int cus = 256;                     // compute units of the device (persistent grids)
     void *h_params = nullptr;          // pinned staging of the Parameters upload
     hipEvent_t upload_ev = nullptr;    // the last upload from h_params
@@ -535,6 +560,7 @@ struct dsp_module {
         dspb::ModuleSpec r;
     };
     std::vector<Spec> spec;
+    std::vector<float *> retired;  // tables of evicted entries, freed by dsp_module_destroy
     std::mutex mu;
 };
 
@@ -610,17 +636,12 @@ int init_slot(dsp_module *m, int slot, const void *params, uint32_t C, float sr,
 
 }  // namespace
 
-extern "C" {
+namespace {
 
-int dsp_module_compile(const char *source, const char *name, void **code, uint64_t *code_size, char *log,
-                       uint64_t log_cap) {
-    if (log && log_cap) log[0] = 0;
-    if (!source || !code || !code_size) {
-        set_last_error("dsp_module_compile: NULL argument");
-        return DSP_ERR_INVALID;
-    }
-    *code = nullptr;
-    *code_size = 0;
+// The plugin source inside the device-service header and a
+// force_cuda_host_device region: the head of both translation units (the
+// module's and the analysis kernel's).
+std::string plugin_prelude() {
     std::string tu;
     tu += "#include \"plugin_header.h\"\n";
     tu += "#pragma clang force_cuda_host_device begin\n";
@@ -632,8 +653,52 @@ int dsp_module_compile(const char *source, const char *name, void **code, uint64
     tu += "#include \"dspb_plugin_source.cpp\"\n";
     tu += "#undef annotate\n#undef __annotate__\n";
     tu += "#pragma clang force_cuda_host_device end\n";
+    return tu;
+}
+
+// The callback's facts (ir_proof.hpp): the plugin compiled again, as a
+// flattened analysis kernel, at -O2 without vectorisation or unrolling (the
+// same IEEE semantics as the module's -O3 code; scalar IR is what the
+// analysis reads), with the module compile's language options.
+dspb::irp::Facts analyze_source(const char *source) {
+    static const char *kProof =
+        "extern \"C\" __global__ __attribute__((flatten)) void dspb_proof(Parameters *P, State *S, float **out, "
+        "unsigned C, unsigned B, float sr) { audio_callback(*P, *S, out, C, B, sr); }\n";
+    dspb::irp::Facts f;
+    std::string ir, log;
+    const int rc = dspb::irp::compile_to_ir(plugin_prelude() + kProof,
+                                            {{"plugin_header.h", kPluginDeviceSrc}, {"dspb_plugin_source.cpp", source}},
+                                            {"-O2", "-std=c++20", "-ffp-contract=off", "-w", "-fno-vectorize",
+                                             "-fno-slp-vectorize", "-fno-unroll-loops"},
+                                            &ir, &log);
+    if (rc != 0) {
+        f.why = "the analysis compile failed: " + log.substr(0, 300);
+        return f;
+    }
+    return dspb::irp::analyze(ir, "dspb_proof");
+}
+
+}  // namespace
+
+extern "C" {
+
+int dsp_module_compile(const char *source, const char *name, void **code, uint64_t *code_size, char *log,
+                       uint64_t log_cap) {
+    if (log && log_cap) log[0] = 0;
+    if (!source || !code || !code_size) {
+        set_last_error("dsp_module_compile: NULL argument");
+        return DSP_ERR_INVALID;
+    }
+    *code = nullptr;
+    *code_size = 0;
+    std::string tu = plugin_prelude();
     std::string note;
     tu += dspb::desc::generate(source, kPluginDeviceSrc, &note);
+    // what the callback does with its block, from its own IR (ir_proof.cpp),
+    // stored in the code object for dsp_module_load
+    const dspb::irp::Facts facts = analyze_source(source);
+    tu += "extern \"C\" __attribute__((used, visibility(\"default\"))) __device__ const unsigned char "
+          "dspb_callback_facts[] = {" + dspb::desc::hex_literal(dspb::irp::encode(facts)) + "};\n";
     tu += kDriver;
     std::vector<const char *> hdrs = {kPluginDeviceSrc, source}, hnames = {"plugin_header.h", "dspb_plugin_source.cpp"};
     hiprtcProgram prog;
@@ -747,6 +812,14 @@ int dsp_module_load(const void *code, uint64_t code_size, int device, dsp_module
     m->params_size = h[0];
     m->state_size = h[1];
     m->stateless = (int)h[2];
+    {
+        std::string ft;
+        if (dspb::desc::code_symbol(code, code_size, "dspb_callback_facts", &ft)) {
+            while (!ft.empty() && ft.back() == '\0') ft.pop_back();
+            m->has_facts = dspb::irp::decode(ft, &m->facts);
+        }
+        m->par = (m->has_facts && m->facts.analyzed && !m->facts.writes_state) ? 1 : 0;
+    }
     if ((e = hipMalloc(&m->d_params, m->params_size ? m->params_size : 1)) != hipSuccess ||
         (e = hipMalloc(&m->d_state[0], m->state_size ? m->state_size : 1)) != hipSuccess ||
         (e = hipMalloc(&m->d_state[1], m->state_size ? m->state_size : 1)) != hipSuccess)
@@ -768,8 +841,10 @@ void dsp_module_destroy(dsp_module *m) {
             if (m->arena_mem[i]) (void)hipFree(m->arena_mem[i]);
         }
         if (m->d_params) (void)hipFree(m->d_params);
+        (void)hipDeviceSynchronize();  // no launch may still read a table
         for (auto &e : m->spec)
             if (e.r.table) (void)hipFree(const_cast<float *>(e.r.table));
+        for (float *t : m->retired) (void)hipFree(t);
         for (hipEvent_t e : {m->upload_ev, m->use_ev})
             if (e) {
                 (void)hipEventSynchronize(e);
@@ -806,7 +881,7 @@ int dsp_module_sizes(const dsp_module *m, uint32_t *params_size, uint32_t *state
     if (!m) return DSP_ERR_INVALID;
     if (params_size) *params_size = m->params_size;
     if (state_size) *state_size = m->state_size;
-    if (stateless) *stateless = m->stateless;
+    if (stateless) *stateless = m->par;
     return DSP_OK;
 }
 
@@ -837,6 +912,11 @@ int dsp_module_initialize_state(dsp_module *m, const void *params, uint32_t C, f
     if (st) return st;
     st = init_slot(m, 0, params, C, sr, arena_bytes, nullptr);
     m->initialized = (st == DSP_OK);
+    // block classes were found with the previous State: forget them (their
+    // tables stay allocated until dsp_module_destroy)
+    for (auto &e : m->spec)
+        if (e.r.table) m->retired.push_back(const_cast<float *>(e.r.table));
+    m->spec.clear();
     if (prev >= 0 && prev != m->device) (void)hipSetDevice(prev);
     return st;
 }
@@ -1001,6 +1081,49 @@ int dsp_param_denormalize(const dsp_param_desc *p, const int64_t *enum_values, f
     }
 }
 
+static void facts_out(const dspb::irp::Facts &f, bool present, dsp_callback_facts *o) {
+    std::memset(o, 0, sizeof *o);
+    o->present = present ? 1 : 0;
+    o->analyzed = f.analyzed;
+    o->reads_block = f.reads_block;
+    o->writes_state = f.writes_state;
+    o->input_control = f.input_control;
+    o->gain_form = f.gain_form;
+    std::strncpy(o->gain, f.gain_expr.c_str(), sizeof o->gain - 1);
+    o->gain_source = f.gain_src;
+    o->gain_offset = f.gain_off;
+    std::memcpy(&o->gain_constant, &f.gain_bits, 4);
+    std::strncpy(o->why, f.why.c_str(), sizeof o->why - 1);
+}
+
+int dsp_module_facts(const dsp_module *m, dsp_callback_facts *out) {
+    if (!m || !out) return DSP_ERR_INVALID;
+    facts_out(m->facts, m->has_facts, out);
+    return DSP_OK;
+}
+
+int dsp_code_facts(const void *code, uint64_t code_size, dsp_callback_facts *out) {
+    if (!code || !out) return DSP_ERR_INVALID;
+    dspb::irp::Facts f;
+    std::string ft;
+    bool present = false;
+    if (dspb::desc::code_symbol(code, code_size, "dspb_callback_facts", &ft)) {
+        while (!ft.empty() && ft.back() == '\0') ft.pop_back();
+        present = dspb::irp::decode(ft, &f);
+    }
+    facts_out(f, present, out);
+    return DSP_OK;
+}
+
+int dsp_plugin_analyze(const char *source, dsp_callback_facts *out) {
+    if (!source || !out) {
+        set_last_error("dsp_plugin_analyze: NULL argument");
+        return DSP_ERR_INVALID;
+    }
+    facts_out(analyze_source(source), true, out);
+    return DSP_OK;
+}
+
 int dsp_module_read_state(const dsp_module *m, void *state) {
     if (!m || (!state && m->state_size)) return DSP_ERR_INVALID;
     if (int st = wait_uses(const_cast<dsp_module *>(m))) return st;
@@ -1093,7 +1216,8 @@ int module_render(dsp_module *m, const void *params, uint32_t params_size, const
         set_last_error("sample_offset must be a multiple of B");
         return DSP_ERR_INVALID;
     }
-    if (!m->stateless && goff) {
+    const bool par = m->par != 0;
+    if (!par && goff) {
         set_last_error("GENERIC plugin with State: whole files only (sample_offset 0)");
         return DSP_ERR_INVALID;
     }
@@ -1111,10 +1235,11 @@ int module_render(dsp_module *m, const void *params, uint32_t params_size, const
     A.C = C;
     A.B = B;
     A.sr = sr;
+    A.par = (unsigned)m->par;
     if (A.nblocks == 0) return DSP_OK;
     void *args[] = {&A};
     unsigned grid = 1, block = 1, lds_bytes = 0;
-    if (m->stateless) {
+    if (par) {
         // default: the LDS-blocks path (dspb_render_lds) when a round of at
         // least 4 blocks fits the per-workgroup LDS budget, else the
         // in-place wave path; DSPB_STATELESS_PATH=0/3 forces one
@@ -1155,7 +1280,7 @@ int module_render(dsp_module *m, const void *params, uint32_t params_size, const
         grid = (unsigned)(g < 65535 ? g : 65535);
     }
     hipFunction_t f = m->f_render;
-    if (!m->stateless && 2ull * C * B * sizeof(float) <= kStagedLdsBytes) {
+    if (!par && 2ull * C * B * sizeof(float) <= kStagedLdsBytes) {
         // stateful: 4 waves, the block double-buffer in LDS (the callback's
         // loads and stores hit LDS, the copies run on 192 lanes beside it)
         A.lds = 1;
@@ -1207,23 +1332,28 @@ int module_ir(dsp_module *m, const void *params, uint32_t params_size, float *co
 
 
 // ---------------------------------------------------------------------------
-// Block classes of a stateless plugin (kernels.hpp ModuleSpec).  A plugin
-// with an empty State computes each block as f(Parameters, block, C, B, sr):
-// it cannot see the block's position, so if f ignores the block's samples
-// every block renders the same output, and if f is y = g x per sample it is
-// the gain map.  The plugin's own callback is run on kProbes probe blocks
-// (zeros; uniform in [-1, 1] with x = 1 at each channel's first sample;
-// uniform in [-1000, 1000]; small signed steps with a -0) and the outputs
-// are compared bit for bit:
-//   TABLE  every probe renders the same block, the same on every channel:
-//          the render is that block (computed by the callback) tiled, and the
-//          fused kernels read it as a block table (MapKind::Ramp);
-//   GAIN   every output is fl(g x) for the g the callback gives x = 1
-//          (MapKind::Gain, a = g).
-// This is probing, not proof: a plugin whose input dependence none of the
-// probes exposes would be misclassified; DSP_EXEC_NO_SPECIALIZE runs the
-// callback on every block instead.
-constexpr int kProbes = 4;
+// Block classes (kernels.hpp ModuleSpec).  A plugin whose blocks are
+// independent (an empty State, or one its callback never writes) computes
+// each block as f(Parameters, State, block, C, B, sr): it cannot see where
+// the block lies in the file.  A class is taken only when the callback's own
+// IR proves it (dsp_module_facts, ir_proof.cpp) and the callback, run on
+// probe blocks, pins what the IR leaves open:
+//   TABLE  the callback reads no sample of its block (IR), so its output is
+//          one block B for every input; two probes that differ in every
+//          element (zeros, noise) render the same values, so every element
+//          is written: the render is that block (computed by the callback)
+//          tiled, read by the fused kernels as a block table
+//          (MapKind::Ramp).  All channels must render the same row.
+//   GAIN   every block store is fl(x g) at the address x was loaded from,
+//          with one call-invariant g, under input-independent control flow
+//          (IR); a probe of ones renders g in every element, so every element
+//          is stored exactly once (or the map is fl(x g) anyway): the gain
+//          map with that g (MapKind::Gain).  A callback with no block store
+//          at all is the identity (g = 1).
+// The other probes (uniform in [-1000, 1000], signed steps with a -0) are a
+// second check of the same class.  Without facts (a code object compiled
+// before them) or without a proof, the callback runs on every block.
+constexpr int kProbes = 5;  // zeros, noise [-1, 1], noise [-1000, 1000], steps, ones
 constexpr uint32_t kSpecMaxB = 1u << 16;
 constexpr size_t kSpecCache = 4;
 
@@ -1286,8 +1416,12 @@ static bool affine_ramp(const float *t, uint32_t B, double *g0, double *s) {
 int module_specialize(dsp_module *m, const void *params, uint32_t params_size, uint32_t C, uint32_t B, float sr,
                       hipStream_t s, ModuleSpec *out) {
     *out = ModuleSpec{};
-    if (!m || !m->initialized || !m->stateless || C == 0 || C > (uint32_t)kMaxChannels || B == 0 || B > kSpecMaxB)
+    if (!m || !m->initialized || !m->par || C == 0 || C > (uint32_t)kMaxChannels || B == 0 || B > kSpecMaxB)
         return DSP_OK;
+    const dspb::irp::Facts &F = m->facts;
+    const bool may_table = m->has_facts && F.analyzed && !F.writes_state && !F.reads_block;
+    const bool may_gain = m->has_facts && F.analyzed && !F.writes_state && F.gain_form && !F.input_control;
+    if (!may_table && !may_gain) return DSP_OK;  // the callback on every block
     if (params_size != m->params_size || (!params && params_size)) return DSP_OK;  // module_render reports it
     if (int st = check_device(m)) return st;
     std::lock_guard<std::mutex> lk(m->mu);
@@ -1303,9 +1437,12 @@ int module_specialize(dsp_module *m, const void *params, uint32_t params_size, u
     std::vector<float> h((size_t)(kProbes * n), 0.f);
     uint32_t seed = 0x9e3779b9u;
     for (uint64_t i = 0; i < n; ++i) {
+        // (xorshift32 never yields 0, so no noise element is 0: probes 0 and
+        // 1 differ in every element)
         h[n + i] = (float)((int32_t)xorshift(seed)) * (1.0f / 2147483648.0f);
         h[2 * n + i] = (float)((int32_t)xorshift(seed)) * (1000.0f / 2147483648.0f);
         h[3 * n + i] = (float)((int)(i % 13) - 6) * 0.125f;
+        h[4 * n + i] = 1.0f;
     }
     for (uint32_t c = 0; c < C; ++c) h[n + (uint64_t)c * B] = 1.0f;
     h[3 * n + (B > 1 ? 1 : 0)] = -0.0f;
@@ -1330,12 +1467,34 @@ int module_specialize(dsp_module *m, const void *params, uint32_t params_size, u
     MOD_HIP(hipEventRecord(m->use_ev, s));
     std::vector<float> r(h.size());
     MOD_HIP(hipMemcpyAsync(r.data(), d, sizeof(float) * r.size(), hipMemcpyDeviceToHost, s));
+    // g's value from where the IR says the callback reads it -- not from the
+    // callback's output -- so that the probe of ones checks how often each
+    // element is scaled: fl(g^k) == g for k != 1 only for g = 0, 1, -1,
+    // where x g ... g = x g for every x
+    float ge = 0.f;
+    bool have_ge = false;
+    if (may_gain) {
+        if (F.gain_src == 'K') {
+            std::memcpy(&ge, &F.gain_bits, 4);
+            have_ge = true;
+        } else if (F.gain_src == 'R') {
+            ge = sr;
+            have_ge = true;
+        } else if (F.gain_src == 'P' && (uint64_t)F.gain_off + 4 <= params_size) {
+            std::memcpy(&ge, (const char *)params + F.gain_off, 4);
+            have_ge = true;
+        } else if (F.gain_src == 'S' && (uint64_t)F.gain_off + 4 <= m->state_size) {
+            MOD_HIP(hipMemcpyAsync(&ge, (const char *)m->d_state[0] + F.gain_off, 4, hipMemcpyDeviceToHost, s));
+            have_ge = true;
+        }
+    }
     MOD_HIP(hipStreamSynchronize(s));
     ModuleSpec res{};
-    bool table = true;
+    bool table = may_table;
     for (uint64_t i = 0; i < kProbes * n && table; ++i) table = same_bits(r[i], r[i % B]);
-    const float g = r[n];  // the callback's output for x = 1
-    bool gain = !table && std::isfinite(g);
+    const float g = ge;
+    bool gain = !table && may_gain && have_ge && std::isfinite(g);
+    for (uint64_t i = 4 * n; i < 5 * n && gain; ++i) gain = same_bits(r[i], g);  // ones -> g, every element
     for (uint64_t i = 0; i < kProbes * n && gain; ++i) gain = same_bits(r[i], h[i] * g);
     if (table) {
         float *t = nullptr;
@@ -1348,9 +1507,10 @@ int module_specialize(dsp_module *m, const void *params, uint32_t params_size, u
         res.kind = kSpecGain;
         res.gain = g;
     }
-    if (m->spec.size() >= kSpecCache) {  // the oldest goes (its table after the stream's last use)
-        MOD_HIP(hipStreamSynchronize(s));
-        if (m->spec.front().r.table) (void)hipFree(const_cast<float *>(m->spec.front().r.table));
+    // a table stays allocated while the module lives (a graph or another
+    // thread may still hold it): the cache evicts its entry, not the table
+    if (m->spec.size() >= kSpecCache) {
+        if (m->spec.front().r.table) m->retired.push_back(const_cast<float *>(m->spec.front().r.table));
         m->spec.erase(m->spec.begin());
     }
     m->spec.push_back({std::vector<unsigned char>((const unsigned char *)params,

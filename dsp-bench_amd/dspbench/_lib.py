@@ -87,6 +87,21 @@ class dsp_param_value(C.Union):
     _fields_ = [("int_value", C.c_int32), ("float_value", C.c_float), ("enum_value", C.c_int32)]
 
 
+class dsp_callback_facts(C.Structure):  # module.h
+    _fields_ = [("present", C.c_int32), ("analyzed", C.c_int32), ("reads_block", C.c_int32),
+                ("writes_state", C.c_int32), ("input_control", C.c_int32), ("gain_form", C.c_int32),
+                ("gain_source", C.c_int32), ("gain_offset", C.c_uint32), ("gain_constant", C.c_float),
+                ("gain", C.c_char * 128), ("why", C.c_char * 256)]
+
+    def as_dict(self) -> dict:
+        return {"present": bool(self.present), "analyzed": bool(self.analyzed),
+                "reads_block": bool(self.reads_block), "writes_state": bool(self.writes_state),
+                "input_control": bool(self.input_control), "gain_form": bool(self.gain_form),
+                "gain_source": chr(self.gain_source) if self.gain_source else "",
+                "gain_offset": int(self.gain_offset), "gain_constant": float(self.gain_constant),
+                "gain": self.gain.decode(errors="replace"), "why": self.why.decode(errors="replace")}
+
+
 # name -> (restype, argtypes)
 _SIGS = {
     "dsp_abi_version": (C.c_int, []),
@@ -137,6 +152,9 @@ _SIGS = {
     "dsp_module_read_state": (C.c_int, [C.c_void_p, C.c_void_p]),
     "dsp_module_block_class": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_float,
                                          C.POINTER(C.c_int32), C.POINTER(C.c_float), C.POINTER(dsp_exec)]),
+    "dsp_module_facts": (C.c_int, [C.c_void_p, C.POINTER(dsp_callback_facts)]),
+    "dsp_plugin_analyze": (C.c_int, [C.c_char_p, C.POINTER(dsp_callback_facts)]),
+    "dsp_code_facts": (C.c_int, [C.c_void_p, C.c_uint64, C.POINTER(dsp_callback_facts)]),
     "dsp_descriptor_from_code": (C.c_int, [C.c_void_p, C.c_uint64, C.POINTER(C.c_void_p)]),
     "dsp_descriptor_destroy": (None, [C.c_void_p]),
     "dsp_module_descriptor": (C.c_void_p, [C.c_void_p]),

@@ -157,6 +157,22 @@ def compile_source(source: str, name: str = "plugin.cpp") -> bytes:
         lib.dsp_module_free_code(code)
 
 
+def analyze_source(source: str) -> dict:
+    """The facts dsp_module_compile stores for this source (dsp_plugin_analyze:
+    the callback's LLVM IR read by the analysis; no GPU)."""
+    f = L.dsp_callback_facts()
+    check(L.lib().dsp_plugin_analyze(source.encode(), C.byref(f)), "dsp_plugin_analyze")
+    return f.as_dict()
+
+
+def code_facts(code: bytes) -> dict:
+    """The facts a code object carries (dsp_code_facts; no GPU)."""
+    f = L.dsp_callback_facts()
+    buf = C.create_string_buffer(code, len(code))
+    check(L.lib().dsp_code_facts(buf, len(code), C.byref(f)), "dsp_code_facts")
+    return f.as_dict()
+
+
 class Module:
     """A plugin's code object loaded on a GPU, with its device State."""
 
@@ -200,6 +216,14 @@ class Module:
         values over the defaults (plugin_populate_from_descriptor then
         plugin_set_parameter_holder_from_values, plugin.cpp:147-171,335-364)."""
         return self.plugin(self.descriptor.params_from_values(values, self.default_parameters()), name)
+
+    @property
+    def facts(self) -> dict:
+        """What the callback's IR shows (dsp_module_facts): analyzed,
+        reads_block, writes_state, input_control, gain_form, gain, why."""
+        f = L.dsp_callback_facts()
+        check(L.lib().dsp_module_facts(self.handle, C.byref(f)), "dsp_module_facts")
+        return f.as_dict()
 
     def read_state(self) -> bytes:
         buf = C.create_string_buffer(max(1, self.state_size))

@@ -51,7 +51,10 @@ void dsp_module_free_code(void *code);
 int dsp_module_load(const void *code, uint64_t code_size, int device, dsp_module **out);
 void dsp_module_destroy(dsp_module *m);
 
-/* sizeof(Parameters), sizeof(State), whether State is empty. */
+/* sizeof(Parameters), sizeof(State), and whether blocks render independently
+ * (1: State is empty, or the callback provably never writes it -- see
+ * dsp_module_facts; such a plugin renders its blocks in parallel and may be
+ * time-sharded). */
 int dsp_module_sizes(const dsp_module *m, uint32_t *params_size, uint32_t *state_size, int *stateless);
 
 /* default_parameters() into a host blob of params_size bytes
@@ -159,22 +162,29 @@ int dsp_param_denormalize(const dsp_param_desc *p, const int64_t *enum_values, f
  * initialises a separate scratch State per call (compute_IR,
  * plugin.cpp:17-58).
  *
- * Block classes.  A plugin with an empty State computes each block from the
- * block alone (it cannot tell where the block lies in the file), so:
- *   DSP_BLOCK_TABLE  a callback that ignores the samples it is given renders
- *                    the same block everywhere (IR_test.cpp,
- *                    build/IR_test.cpp:40-60): the render is that block --
- *                    computed once by the plugin's own callback -- tiled, and
+ * Block classes.  A plugin whose blocks are independent -- an empty State,
+ * or a State its callback never writes (dsp_module_facts) -- computes each
+ * block from the block alone (it cannot tell where the block lies in the
+ * file), so:
+ *   DSP_BLOCK_TABLE  a callback that reads no sample of its block
+ *                    (IR_test.cpp, build/IR_test.cpp:40-60) renders the same
+ *                    block everywhere: the render is that block -- computed
+ *                    once by the plugin's own callback -- tiled, and
  *                    dsp_render_stft runs the fused render + STFT kernel on
  *                    it as a block table;
- *   DSP_BLOCK_GAIN   a callback that returns g x per sample (gain_test.cpp)
+ *   DSP_BLOCK_GAIN   a callback whose every block store is x * g at the
+ *                    address x came from, with one g per call, under control
+ *                    flow that reads no sample (gain_test.cpp,
+ *                    static_gain_plugin.cpp; no store at all = the identity)
  *                    runs as the gain map with the g its callback gives x = 1.
- * The class is found by running the callback on probe blocks (zeros, two
- * uniform noises, signed steps) and comparing outputs bit for bit, once per
- * (Parameters, C, B, sample rate) -- the first render with a new set
- * synchronises its stream once.  Probing is evidence, not proof: a plugin
- * whose input dependence no probe exposes would be misclassified, and
- * DSP_EXEC_NO_SPECIALIZE (dspbench.h) runs the callback on every block. */
+ * A class is taken only when the callback's own LLVM IR proves it
+ * (dsp_module_facts: dsp_module_compile analyses the plugin's code and stores
+ * the facts in the code object) and probe blocks run through the callback
+ * pin what the IR leaves open (which elements are written; the value of g),
+ * once per (Parameters, C, B, sample rate) -- the first render with a new set
+ * synchronises its stream once.  Anything else, including every code object
+ * without facts, runs the callback on every block, as does
+ * DSP_EXEC_NO_SPECIALIZE (dspbench.h). */
 enum dsp_block_class { DSP_BLOCK_CALLBACK = 0, DSP_BLOCK_TABLE = 1, DSP_BLOCK_GAIN = 2 };
 
 /* The block class of `params` for C channels of B-sample blocks at sample
@@ -182,6 +192,40 @@ enum dsp_block_class { DSP_BLOCK_CALLBACK = 0, DSP_BLOCK_TABLE = 1, DSP_BLOCK_GA
  * DSP_BLOCK_GAIN (may be NULL). */
 int dsp_module_block_class(dsp_module *m, const void *params, uint32_t params_size, uint32_t C, uint32_t B,
                            float sr, int32_t *block_class, float *gain, const dsp_exec *ex);
+
+/* ---- what the callback does with its block (no GPU) ----------------------
+ * dsp_module_compile compiles the plugin a second time into an analysis
+ * kernel, dspb_proof(P, S, out, C, B, sr) { audio_callback(*P, *S, out, C, B,
+ * sr); }, flattened, and reads its optimised LLVM IR: which memory every
+ * load and store can touch (a block sample, the pointer table, Parameters,
+ * State, private or global memory) and which values depend on a block sample
+ * or differ between iterations.  A construct outside that model (a call that
+ * may touch memory, an atomic, a store to a global or to Parameters, a
+ * pointer stored to memory, an address used as a number) leaves `analyzed`
+ * 0, and nothing is concluded from the IR. */
+typedef struct dsp_callback_facts {
+    int32_t present;       /* the code object carries facts (compiled with them) */
+    int32_t analyzed;      /* every instruction of the callback was inside the analysis */
+    int32_t reads_block;   /* loads a sample of its block (or copies from it) */
+    int32_t writes_state;  /* stores through its State */
+    int32_t input_control; /* a branch condition or a store address depends on a sample */
+    int32_t gain_form;     /* every block store is x * g at x's address, one g per call
+                              (or no block store: the identity) */
+    int32_t gain_source;   /* gain_form: where g is read -- 'P' / 'S' a float at byte gain_offset
+                              of Parameters / State, 'K' the constant gain_constant, 'R' the
+                              sample rate; the host reads g from there (0: not known) */
+    uint32_t gain_offset;
+    float gain_constant;
+    char gain[128];        /* g as the analysis wrote it (diagnostics) */
+    char why[256];         /* why the analysis stopped, or why a property fails */
+} dsp_callback_facts;
+
+/* The facts of a loaded module (present = 0 for a code object without). */
+int dsp_module_facts(const dsp_module *m, dsp_callback_facts *out);
+/* The facts stored in a code object (present = 0 when it has none; no GPU). */
+int dsp_code_facts(const void *code, uint64_t code_size, dsp_callback_facts *out);
+/* The same analysis of plugin source text, without building a module (no GPU). */
+int dsp_plugin_analyze(const char *source, dsp_callback_facts *out);
 
 #ifdef __cplusplus
 }

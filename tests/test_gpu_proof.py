@@ -1,0 +1,237 @@
+"""GENERIC plugins whose fast path the callback's IR decides (module.h
+dsp_callback_facts, csrc/ir_proof.cpp), rendered on the GPU and compared bit
+for bit with the plugin's semantics computed here in numpy (each test plugin
+is a few lines: tests/plugins/).  The reference calls the callback on every
+block, in order (audio.cpp:160-165), so whatever path the library takes --
+a block class, parallel blocks, or the blocks in order on one lane -- the
+render must equal that.
+
+The plugins are the cases round 3's probes could not tell from a gain or a
+table: a clip beyond the probes' range, an exact-value branch, a branch on a
+sample, a function-local static counter; plus a per-position gain, per-channel
+gains, a gain applied twice, a State that is only read, a constant level.
+"""
+import os
+import struct
+
+import numpy as np
+import pytest
+
+import dspbench as d
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PLUG = os.path.join(HERE, "plugins")
+PEAK_REL_TOL = 1e-6
+F = np.float32
+
+
+def load(name):
+    with open(os.path.join(PLUG, name + ".cpp")) as f:
+        src = f.read()
+    return d.module.Module(d.module.compile_source(src, name + ".cpp"))
+
+
+def blocks(x, C, B):
+    """render_audio's input to each callback: the file in blocks of B, zero
+    past EOF and for the channels the file lacks (audio.cpp:13-175)."""
+    cin, L = x.shape
+    nb = -(-L // B)
+    buf = np.zeros((C, nb * B), F)
+    buf[:min(cin, C), :L] = x[:C]
+    return buf.reshape(C, nb, B)
+
+
+def semantics(name, xb, params, state=None, call0=0):
+    """The plugin's callback applied to every block, in numpy float32 (the
+    operations in the order the source writes them)."""
+    g = F(struct.unpack("<f", params[:4])[0])
+    C, nb, B = xb.shape
+    y = xb.copy()
+    if name == "clip_beyond_2000":
+        y = np.where(np.abs(xb) > F(2000), F(0), xb * g).astype(F)
+    elif name == "exact_value_branch":
+        y = np.where(xb == F(0.25), F(7), xb * g).astype(F)
+    elif name == "gain_until_loud":
+        for c in range(C):
+            for k in range(nb):
+                row = xb[c, k]
+                loud = np.nonzero(row > F(5000))[0]
+                stop = loud[0] if loud.size else B
+                y[c, k, :stop] = row[:stop] * g
+    elif name == "static_counter":
+        for k in range(nb):
+            calls = call0 + k + 1
+            gk = F(g * (F(1) if calls % 2 else F(0.5)))
+            y[:, k] = xb[:, k] * gk
+    elif name == "fade_in":
+        s = np.arange(B, dtype=F)
+        gs = (g * s).astype(F) / F(B)
+        y = (xb * gs.astype(F)).astype(F)
+    elif name == "balance":
+        left, right = struct.unpack("<ff", params[:8])
+        y[0] = xb[0] * F(left)
+        if C > 1:
+            y[1] = xb[1] * F(right)
+    elif name == "gain_twice":
+        y = ((xb * g).astype(F) * g).astype(F)
+    elif name == "state_shaper":
+        a, b = F(-g / F(3)), F(F(1) + g)
+        t = ((a * xb).astype(F) * xb).astype(F) * xb
+        y = (t.astype(F) + (b * xb).astype(F)).astype(F)
+    elif name == "dc_level":
+        y[:] = g
+    return y.reshape(C, -1)
+
+
+# name -> (block class at the defaults, blocks in parallel)
+EXPECT = {
+    "clip_beyond_2000": ("callback", True),
+    "exact_value_branch": ("callback", True),
+    "gain_until_loud": ("callback", True),
+    "static_counter": ("callback", False),
+    "fade_in": ("callback", True),
+    "balance": ("callback", True),
+    "gain_twice": ("callback", True),
+    "state_shaper": ("callback", True),
+    "dc_level": ("table", True),
+}
+
+
+def make_input(L, C=2, seed=0):
+    """Noise over +-3000 with exact 0.25 values and samples above 5000."""
+    rng = np.random.default_rng(seed)
+    x = rng.uniform(-3000, 3000, (C, L)).astype(F)
+    x[:, ::97] = F(0.25)
+    x[:, 5::1013] = F(6000)
+    x[:, 7::211] = F(-2500)
+    return x
+
+
+@pytest.mark.parametrize("name", sorted(EXPECT))
+@pytest.mark.parametrize("C,B,L", [(2, 512, 512 * 37 + 101), (1, 480, 480 * 20), (3, 256, 9_999)])
+def test_render_equals_the_callback_on_every_block(torch_cuda, name, C, B, L):
+    torch = torch_cuda
+    mod = load(name)
+    params = mod.default_parameters()
+    mod.initialize_state(params, C, 48000.0)
+    cls, _ = mod.block_class(params, C, B, 48000.0)
+    want_cls, want_par = EXPECT[name]
+    assert cls == want_cls, (name, cls, mod.facts)
+    assert mod.stateless == want_par, mod.facts
+    x = make_input(L, min(C, 2), seed=B)
+    want = semantics(name, blocks(x, C, B), params)
+    got = d.render_offline(torch.from_numpy(x).cuda(), C, B, 48000.0, mod.plugin(params, name)).cpu().numpy()
+    assert np.array_equal(got, want), name
+
+
+def test_static_counter_runs_in_order_across_calls(torch_cuda):
+    """The counter lives outside State: blocks run in order, and a second
+    render continues the count where the first stopped (the JIT's static
+    persists in the reference too)."""
+    torch = torch_cuda
+    mod = load("static_counter")
+    params = mod.default_parameters()
+    mod.initialize_state(params, 2, 48000.0)
+    assert not mod.stateless and not mod.facts["analyzed"]
+    B, L = 512, 512 * 11
+    x = make_input(L)
+    xg = torch.from_numpy(x).cuda()
+    nb = L // B
+    a = d.render_offline(xg, 2, B, 48000.0, mod.plugin(params, "static_counter")).cpu().numpy()
+    b = d.render_offline(xg, 2, B, 48000.0, mod.plugin(params, "static_counter")).cpu().numpy()
+    assert np.array_equal(a, semantics("static_counter", blocks(x, 2, B), params, call0=0))
+    assert np.array_equal(b, semantics("static_counter", blocks(x, 2, B), params, call0=nb))
+
+
+@pytest.mark.parametrize("name", ["clip_beyond_2000", "state_shaper", "dc_level", "gain_until_loud"])
+def test_render_stft_of_proof_plugins(torch_cuda, oracle, name):
+    """render + STFT through the same dispatch: the render bit for bit, the
+    spectra within 1e-6 of the peak of float64."""
+    torch = torch_cuda
+    mod = load(name)
+    params = mod.default_parameters()
+    mod.initialize_state(params, 2, 48000.0)
+    B, L = 512, 8192 * 6 + 333
+    x = make_input(L, seed=3)
+    want = semantics(name, blocks(x, 2, B), params)
+    out, mag = d.render_stft(torch.from_numpy(x).cuda(), 2, B, 48000.0, mod.plugin(params, name),
+                             window=d.DSP_WIN_HANN)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), want)
+    m64 = oracle.np_stft_mag(want[0], 8192, 4096, d.DSP_WIN_HANN, 4097)
+    mm = mag[0].cpu().numpy().astype(np.float64)
+    peak = np.maximum(m64.max(axis=1), 1e-30)
+    assert float(np.max(np.abs(mm - m64).max(axis=1) / peak)) <= PEAK_REL_TOL
+
+
+def test_gain_twice_is_a_gain_only_when_g_squared_is_g(torch_cuda):
+    """Every store of gain_twice.cpp is x * g at x's address (the IR's gain
+    form); the probe of ones sees g^2: the class is refused for g = 0.5 and
+    taken for g = 1 and g = 0, where x g g = x g for every x."""
+    torch = torch_cuda
+    mod = load("gain_twice")
+    mod.initialize_state(mod.default_parameters(), 2, 48000.0)
+    assert mod.facts["gain_form"]
+    x = torch.from_numpy(make_input(512 * 9)).cuda()
+    for g, cls in ((0.5, "callback"), (1.0, "gain"), (0.0, "gain")):
+        params = struct.pack("<f", g)
+        assert mod.block_class(params, 2, 512, 48000.0)[0] == cls, g
+        got = d.render_offline(x, 2, 512, 48000.0, mod.plugin(params, "gain_twice")).cpu().numpy()
+        assert np.array_equal(got, semantics("gain_twice", blocks(x.cpu().numpy(), 2, 512), params))
+
+
+def test_static_gain_plugin_is_a_proven_gain(torch_cuda, oracle):
+    """test/static_gain_plugin.cpp (State {gain} set by initialize_state, only
+    read by the callback): parallel blocks, the gain class with g = state.gain
+    = 0.1f, bit-exact against the reference plugin compiled for the CPU; a new
+    initialize_state forgets the class it found."""
+    mods = os.path.join(os.path.dirname(HERE), "dsp-bench_amd", "modules")
+    if not os.path.exists(os.path.join(mods, "mod_static_gain_plugin.co")):
+        pytest.skip("modules not built")
+    torch = torch_cuda
+    with open(os.path.join(mods, "mod_static_gain_plugin.co"), "rb") as f:
+        mod = d.module.Module(f.read())
+    params = mod.default_parameters()
+    mod.initialize_state(params, 2, 48000.0)
+    assert mod.stateless and mod.facts["gain_form"] and not mod.facts["writes_state"]
+    cls, g = mod.block_class(params, 2, 512, 48000.0)
+    assert cls == "gain" and g == F(0.1)
+    x = np.random.default_rng(4).uniform(-1, 1, (2, 512 * 50 + 7)).astype(F)
+    got = d.render_offline(torch.from_numpy(x).cuda(), 2, 512, 48000.0, mod.plugin(params, "static_gain")).cpu()
+    ref = oracle.RefPlugin("static_gain_plugin", 2, 48000.0)
+    want = oracle.render_offline([x[0], x[1]], 2, 512, 48000.0, ref.as_oracle())
+    assert np.array_equal(got.numpy(), want)
+
+
+def test_evicted_table_outlives_a_captured_graph(torch_cuda):
+    """A table-class render captured into a graph keeps its table: four more
+    Parameters sets push its entry out of the module's class cache, and the
+    replay still renders the first level (module.cpp: evicted tables are
+    freed only by dsp_module_destroy)."""
+    torch = torch_cuda
+    mod = load("dc_level")
+    p0 = struct.pack("<f", 0.125)
+    mod.initialize_state(p0, 2, 48000.0)
+    assert mod.block_class(p0, 2, 512, 48000.0)[0] == "table"
+    x = torch.zeros((2, 512 * 8), device="cuda")
+    plug = mod.plugin(p0, "dc_level")
+    out = torch.empty((2, 512 * 8), device="cuda")
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        d.render_offline(x, 2, 512, 48000.0, plug, out=out)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=side):
+        d.render_offline(x, 2, 512, 48000.0, plug, out=out)
+    for v in (0.25, 0.5, -0.75, 0.875, 0.0625):
+        p = struct.pack("<f", v)
+        assert mod.block_class(p, 2, 512, 48000.0)[0] == "table"
+        y = d.render_offline(x, 2, 512, 48000.0, mod.plugin(p, "dc_level"))
+        assert bool((y == v).all())
+    out.fill_(-1.0)
+    g.replay()
+    torch.cuda.synchronize()
+    assert bool((out == 0.125).all())

@@ -1,15 +1,18 @@
-"""Block classes of stateless plugins (module.h dsp_module_block_class): a
-plugin compiled unchanged from its source whose callback ignores its input
-(IR_test.cpp, handmade_test.cpp) or scales it (gain_test.cpp, no_op.cpp)
-runs as its own callback's block tiled / as that gain, in the fused kernels.
+"""Block classes (module.h dsp_module_block_class): a plugin compiled
+unchanged from its source whose callback provably ignores its input
+(IR_test.cpp, handmade_test.cpp) or scales it (gain_test.cpp,
+static_gain_plugin.cpp, no_op.cpp) -- facts from its own IR, values pinned by
+probes -- runs as its own callback's block tiled / as that gain, in the fused
+kernels.
 
 Bars: the render bit-exact against the reference plugin compiled for the CPU
 with the JIT flags (oracle/_ref, through the oracle's render_audio loop,
 audio.cpp:13-175) and against the same plugin with the callback on every
 block (DSP_EXEC_NO_SPECIALIZE); IR_test's spectra bit-exact against the stock
 fused IR_test kernel with the same parameters, within 1e-6 of the peak
-against float64.  Plugins whose input dependence the probes expose, and
-input-independent plugins whose channels differ, keep the callback.
+against float64.  Plugins whose IR shows input dependence, and
+input-independent plugins whose channels differ, keep the callback
+(tests/test_gpu_proof.py: the cases probes alone could not see).
 """
 import os
 import struct
@@ -28,9 +31,11 @@ PEAK_REL_TOL = 1e-6
 
 # the class each stock plugin's default Parameters must get (stateful plugins
 # keep the callback: their blocks depend on the State)
+# (static_gain_plugin and plugin_with_parameters have a State the callback
+# never writes -- the IR shows it -- so their blocks are independent too)
 EXPECTED = {"IR_test": "table", "handmade_test": "table", "gain_test": "gain", "no_op": "gain",
-            "template_plugin": "gain", "static_gain_plugin": "callback", "sine_test": "callback",
-            "buffer_test": "callback", "plugin_with_parameters": "callback"}
+            "template_plugin": "gain", "static_gain_plugin": "gain", "sine_test": "callback",
+            "buffer_test": "callback", "plugin_with_parameters": "gain"}
 
 
 def have(name):
@@ -54,11 +59,13 @@ def test_stock_plugin_block_classes(torch_cuda, name):
     assert cls == EXPECTED[name], (name, cls, g)
     if name == "gain_test":
         assert g == struct.unpack("<f", params[:4])[0]
-    if name in ("no_op", "template_plugin"):
+    if name in ("no_op", "template_plugin", "plugin_with_parameters"):
         assert g == 1.0
+    if name == "static_gain_plugin":
+        assert g == np.float32(0.1)
 
 
-@pytest.mark.parametrize("name", ["IR_test", "handmade_test", "gain_test", "no_op"])
+@pytest.mark.parametrize("name", ["IR_test", "handmade_test", "gain_test", "no_op", "static_gain_plugin"])
 @pytest.mark.parametrize("cin,C,B,L", [(2, 2, 512, 20_000 + 37), (1, 2, 384, 50_001), (2, 2, 100, 9_999),
                                        (2, 3, 1024, 70_000)])
 def test_specialized_render_is_the_plugins_own(torch_cuda, oracle, name, cin, C, B, L):
@@ -215,7 +222,7 @@ void audio_callback(const Parameters& p, State& st, float** out, const u32 C, co
 @pytest.mark.parametrize("src,name,cls", [(CLIP_SRC, "clip", "callback"), (PER_CHANNEL_SRC, "per_channel", "callback"),
                                           (TONE_SRC, "tone", "table")])
 def test_probes_keep_the_callback_where_needed(torch_cuda, src, name, cls):
-    """A gain that clips above 5 (only the +-1000 probe sees it) and an
+    """A gain that clips above 5 (the IR stores a select on the sample) and an
     input-independent plugin whose channels differ keep the callback; a tone
     whose block depends on the sample rate is a table.  Whatever the class,
     the render equals the callback on every block bit for bit."""

@@ -1,0 +1,128 @@
+"""What a plugin's audio_callback does with its block, read from its own
+LLVM IR (csrc/ir_proof.cpp; module.h dsp_callback_facts) -- CPU only: the
+analysis compiles the plugin through comgr, no GPU.
+
+The facts decide every fast path of a GENERIC plugin (module.cpp): a block
+class (TABLE: reads no sample; GAIN: every store x * g at x's address, one g,
+control flow free of samples) and parallel blocks (the State never written,
+no global memory written).  The reference runs the callback on every block,
+in order (audio.cpp:160-165), so each fact must be conservative: the test
+plugins under tests/plugins/ are the cases a probe cannot see.
+"""
+import os
+
+import pytest
+
+import dspbench.module as dm
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PLUG = os.path.join(HERE, "plugins")
+REF = "/root/reference"
+
+
+def facts_of(path):
+    with open(path) as f:
+        return dm.analyze_source(f.read())
+
+
+# (analyzed, reads_block, writes_state, input_control, gain_form) per plugin
+STOCK = {
+    "build/IR_test.cpp": (True, False, False, False, False),        # a table: the ramp, no sample read
+    "build/handmade_test.cpp": (True, False, False, False, False),  # a table
+    "build/gain_test.cpp": (True, True, False, False, True),        # x * param.gain
+    "test/static_gain_plugin.cpp": (True, True, False, False, True),  # x * state.gain, State only read
+    "test/no_op.cpp": (True, False, False, False, True),            # no store: the identity
+    "build/template_plugin.cpp": (True, False, False, False, True),
+    "test/plugin_with_parameters.cpp": (True, False, False, False, True),
+    "build/sine_test.cpp": (True, False, True, False, False),       # writes its phase to State
+    "build/buffer_test.cpp": (False, False, True, False, False),    # stores through arena pointers
+}
+
+
+@pytest.mark.parametrize("rel", sorted(STOCK))
+def test_stock_plugin_facts(rel):
+    path = os.path.join(REF, rel)
+    if not os.path.exists(path):
+        pytest.skip("reference sources not present")
+    f = facts_of(path)
+    got = (f["analyzed"], f["reads_block"], f["writes_state"], f["input_control"], f["gain_form"])
+    assert got == STOCK[rel], (rel, f)
+    # where g is read, so that the host knows it without the callback
+    if rel.endswith("gain_test.cpp"):
+        assert (f["gain_source"], f["gain_offset"]) == ("P", 0)  # Parameters.gain
+    if rel.endswith("static_gain_plugin.cpp"):
+        assert (f["gain_source"], f["gain_offset"]) == ("S", 0)  # State.gain
+    if rel.endswith("no_op.cpp"):
+        assert (f["gain_source"], f["gain_constant"]) == ("K", 1.0)  # no store: the identity
+
+
+# test plugins (tests/plugins, written for these tests): what the probes of
+# round 3 could not tell apart from a gain / a table
+TEST = {
+    "clip_beyond_2000.cpp": (True, True, False, False, False),   # stores a select on the sample
+    "exact_value_branch.cpp": (True, True, False, False, False),  # x == 0.25 -> 7
+    "gain_until_loud.cpp": (True, True, False, True, False),     # a branch on a sample: input control
+    "static_counter.cpp": (False, True, False, False, False),    # a function-local static: global memory
+    "fade_in.cpp": (True, True, False, False, False),            # g varies with the position
+    "balance.cpp": (True, True, False, False, False),            # two different gains
+    "gain_twice.cpp": (True, True, False, False, True),          # x * g twice: the probe of ones refuses it
+    "state_shaper.cpp": (True, True, False, False, False),       # State read only: parallel, no class
+    "dc_level.cpp": (True, False, False, False, False),          # a table (set_array)
+}
+
+
+@pytest.mark.parametrize("name", sorted(TEST))
+def test_test_plugin_facts(name):
+    f = facts_of(os.path.join(PLUG, name))
+    got = (f["analyzed"], f["reads_block"], f["writes_state"], f["input_control"], f["gain_form"])
+    assert got == TEST[name], (name, f)
+    if not f["analyzed"] or not f["gain_form"]:
+        assert f["why"], f  # the reason is reported
+
+
+def test_facts_travel_in_the_code_object():
+    """dsp_module_compile stores the facts in the code object; dsp_code_facts
+    reads them back without a GPU, equal to a fresh analysis."""
+    src = open(os.path.join(PLUG, "gain_until_loud.cpp")).read()
+    code = dm.compile_source(src, "gain_until_loud.cpp")
+    f = dm.code_facts(code)
+    assert f["present"] and f == dm.analyze_source(src)
+
+
+SNIPPETS = {
+    # an atomic on a global: outside the analysis
+    "atomic": ("__device__ int hits; ", "atomicAdd(&hits, 1); out[0][0] *= p.g;", (False, None)),
+    # a pointer into the block kept in private memory and used later
+    "alias_local": ("", "float *q[2] = {out[0], out[0] + 1}; for (u32 s = 0; s + 1 < B; ++s) q[s & 1][s / 2] = 0.0f;",
+                    (None, None)),
+    # the block's address as a number decides the output
+    "address": ("", "out[0][0] = (float)(((unsigned long long)out[0]) & 255);", (False, None)),
+    # reads a neighbour: not a gain
+    "neighbour": ("", "for (u32 s = 1; s < B; ++s) out[0][s] = out[0][s - 1] * p.g;", (True, False)),
+    # a double-precision product rounded back: the optimiser proves it is the
+    # float product (24 x 24 bits fit f64 exactly, one rounding), so a gain
+    "f64": ("", "for (u32 s = 0; s < B; ++s) out[0][s] = (float)((double)out[0][s] * (double)p.g);", (True, True)),
+}
+
+
+@pytest.mark.parametrize("case", sorted(SNIPPETS))
+def test_constructs_outside_the_model(case):
+    pre, body, (want_analyzed, want_gain) = SNIPPETS[case]
+    src = ("#include \"plugin_header.h\"\n" + pre +
+           "struct Parameters { FLOAT_PARAM(0.0f, 1.0f) g; };\nstruct State {};\n"
+           "Parameters default_parameters() { Parameters p = {0.5f}; return p; }\n"
+           "State initialize_state(const Parameters &p, const unsigned C, const float sr, void *ctx) "
+           "{ State s; return s; }\n"
+           "void audio_callback(const Parameters &p, State &st, float **out, const u32 C, const u32 B, "
+           "const real32 sr) {\n" + body + "\n}\n")
+    f = dm.analyze_source(src)
+    if want_analyzed is not None:
+        assert f["analyzed"] == want_analyzed, f
+    if want_gain is not None:
+        assert f["gain_form"] == want_gain, f
+    # whatever the verdict, nothing unsafe is concluded: a block read is
+    # seen, and no gain form for the bodies that are no gain
+    if case in ("neighbour", "f64"):
+        assert f["reads_block"]
+    if case != "f64":
+        assert not f["gain_form"]
