@@ -1,15 +1,17 @@
 // sdma.cpp -- device -> pinned host downloads on an SDMA engine (sdma.hpp).
 //
 // The HSA runtime is the one the process has already loaded with its HIP
-// runtime (dlopen by soname, RTLD_NOLOAD first: a PyTorch process carries its
-// own copy, and a second runtime in one process would be fatal); the types
-// come from /opt/rocm/include/hsa.
+// runtime (dlopen by soname with RTLD_NOLOAD only: a PyTorch process carries
+// its own copy, and a second runtime in one process would be fatal -- when
+// none is loaded, the downloads take hipMemcpyAsync instead); the types come
+// from /opt/rocm/include/hsa.
 #include "sdma.hpp"
 
 #include <dlfcn.h>
 #include <hsa/hsa.h>
 #include <hsa/hsa_ext_amd.h>
 
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -22,6 +24,8 @@ void set_last_error(const char *fmt, ...);
 int hip_fail(hipError_t e, const char *what);
 
 namespace {
+
+constexpr int kCopyTimeoutS = 120;  // one chunk's downloads: ~10 ms at the engine's 57 GB/s
 
 struct Hsa {
     bool ok = false;
@@ -42,8 +46,7 @@ Hsa &hsa() {
     static std::once_flag once;
     std::call_once(once, [] {
         void *l = dlopen("libhsa-runtime64.so.1", RTLD_NOW | RTLD_NOLOAD);
-        if (!l) l = dlopen("libhsa-runtime64.so.1", RTLD_NOW);
-        if (!l) return;
+        if (!l) return;  // never a runtime of our own: not usable
         bool all = true;
         auto sym = [&](const char *n) {
             void *p = dlsym(l, n);
@@ -243,8 +246,18 @@ void SdmaDownloader::run() {
                 }
                 ++issued;
             }
-            h.signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, (hsa_signal_value_t)(n - issued + 1), UINT64_MAX,
-                                    HSA_WAIT_STATE_BLOCKED);
+            // bounded: a copy that never lands fails the render instead of
+            // hanging this worker (and the join in finish())
+            const hsa_signal_value_t want = (hsa_signal_value_t)(n - issued + 1);
+            const auto t0 = std::chrono::steady_clock::now();
+            while (h.signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, want, 1000000ull, HSA_WAIT_STATE_BLOCKED) >=
+                   want) {
+                if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(kCopyTimeoutS)) {
+                    set_last_error("SDMA download: copies did not land within %d s", kCopyTimeoutS);
+                    if (!st) st = DSP_ERR_HIP;
+                    break;
+                }
+            }
         }
         {
             std::lock_guard<std::mutex> g(mu_);

@@ -166,7 +166,10 @@ const dsp_comm_transport kRcclTransport = {rccl_group_start, rccl_group_end, rcc
 // copies device to device, records `done` and hands it back; the sender's
 // stream waits for `done`.  Inside a group, recvs and the sends' completion
 // are deferred to group_end (sends post at once), so a group never blocks on
-// its peers' issue order.
+// its peers' issue order.  A wait that times out fails the hub: every rank's
+// later call returns an error at once (no recv can pair with a stale message
+// of the failed step), and the failing rank takes its own unreceived
+// messages back out of the mailboxes.
 constexpr int kLoopWaitSeconds = 120;
 
 struct LoopMsg {
@@ -182,6 +185,7 @@ struct LoopHub {
     std::mutex mu;
     std::condition_variable cv;
     uint32_t world = 0;
+    bool failed = false;  // a rank timed out: every later call fails
     std::vector<std::deque<std::shared_ptr<LoopMsg>>> box;  // [src * world + dst]
 };
 
@@ -205,6 +209,29 @@ struct LoopRank {
 
 int loop_flush(LoopRank *lr);
 
+// after a failure: this rank's pending recvs are dropped, and its sends that
+// no recv has taken leave their mailboxes (their events destroyed); a send a
+// recv has taken but not finished keeps its events (the copy may use them)
+void loop_abandon(LoopRank *lr) {
+    LoopHub &h = *lr->hub;
+    lr->recvs.clear();
+    std::vector<LoopRank::Sent> sent;
+    sent.swap(lr->sent);
+    std::lock_guard<std::mutex> g(h.mu);
+    for (const LoopRank::Sent &s : sent) {
+        if (s.m->taken) continue;
+        for (auto &q : h.box) {
+            for (auto it = q.begin(); it != q.end(); ++it)
+                if (*it == s.m) {
+                    q.erase(it);
+                    break;
+                }
+        }
+        (void)hipEventDestroy(s.m->ready);
+        (void)hipEventDestroy(s.m->done);
+    }
+}
+
 int loop_group_start(void *u) {
     ++((LoopRank *)u)->depth;
     return DSP_OK;
@@ -216,10 +243,17 @@ int loop_group_end(void *u) {
     return --lr->depth == 0 ? loop_flush(lr) : DSP_OK;
 }
 
+int hub_failed(LoopHub &h, uint32_t rank) {
+    std::lock_guard<std::mutex> g(h.mu);
+    return h.failed ? invalid("loopback: rank %u: the communicators failed in an earlier call (a timeout)", rank)
+                    : DSP_OK;
+}
+
 int loop_send(void *u, const float *buf, uint64_t count, uint32_t peer, void *stream) {
     LoopRank *lr = (LoopRank *)u;
     LoopHub &h = *lr->hub;
     if (peer >= h.world || peer == lr->rank) return invalid("loopback: bad peer %u (rank %u)", peer, lr->rank);
+    if (int st = hub_failed(h, lr->rank)) return st;
     auto m = std::make_shared<LoopMsg>();
     m->ptr = buf;
     m->count = count;
@@ -238,6 +272,7 @@ int loop_send(void *u, const float *buf, uint64_t count, uint32_t peer, void *st
 int loop_recv(void *u, float *buf, uint64_t count, uint32_t peer, void *stream) {
     LoopRank *lr = (LoopRank *)u;
     if (peer >= lr->hub->world || peer == lr->rank) return invalid("loopback: bad peer %u (rank %u)", peer, lr->rank);
+    if (int st = hub_failed(*lr->hub, lr->rank)) return st;
     lr->recvs.push_back({buf, count, peer, (hipStream_t)stream});
     return lr->depth ? DSP_OK : loop_flush(lr);
 }
@@ -253,9 +288,16 @@ int loop_flush(LoopRank *lr) {
         {
             std::unique_lock<std::mutex> g(h.mu);
             auto &q = h.box[(size_t)r.peer * h.world + lr->rank];
-            if (!h.cv.wait_until(g, deadline, [&] { return !q.empty(); }))
-                return invalid("loopback: rank %u waited %d s for a send from rank %u", lr->rank, kLoopWaitSeconds,
-                               r.peer);
+            if (!h.cv.wait_until(g, deadline, [&] { return h.failed || !q.empty(); }) || h.failed) {
+                const bool mine = !h.failed;
+                h.failed = true;
+                g.unlock();
+                h.cv.notify_all();
+                loop_abandon(lr);
+                return mine ? invalid("loopback: rank %u waited %d s for a send from rank %u", lr->rank,
+                                      kLoopWaitSeconds, r.peer)
+                            : invalid("loopback: rank %u: another rank timed out", lr->rank);
+            }
             m = q.front();
             q.pop_front();
             m->taken = true;
@@ -283,10 +325,14 @@ int loop_flush(LoopRank *lr) {
     for (const LoopRank::Sent &s : sent) {
         {
             std::unique_lock<std::mutex> g(h.mu);
-            if (!h.cv.wait_until(g, deadline, [&] { return s.m->copied; })) {
-                if (!st) st = invalid("loopback: rank %u waited %d s for its send to be received", lr->rank,
+            if (!h.cv.wait_until(g, deadline, [&] { return s.m->copied || h.failed; }) || !s.m->copied) {
+                h.failed = true;
+                g.unlock();
+                h.cv.notify_all();
+                lr->sent.push_back(s);  // (and the rest: loop_abandon takes them back)
+                if (!st) st = invalid("loopback: rank %u: its send was not received in %d s", lr->rank,
                                       kLoopWaitSeconds);
-                continue;  // the message stays in the mailbox; its events leak with it
+                continue;
             }
         }
         if (s.m->status == DSP_OK) {
@@ -300,6 +346,7 @@ int loop_flush(LoopRank *lr) {
         (void)hipEventDestroy(s.m->ready);
         (void)hipEventDestroy(s.m->done);
     }
+    if (!lr->sent.empty()) loop_abandon(lr);  // the sends no recv took after a timeout
     return st;
 }
 

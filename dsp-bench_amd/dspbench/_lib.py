@@ -189,6 +189,9 @@ _OPTIONAL_SIGS = {
 _lib: C.CDLL | None = None
 
 
+ABI_VERSION = 2  # include/dspbench/dspbench.h DSPBENCH_ABI_VERSION this binding is written against
+
+
 def lib() -> C.CDLL:
     global _lib
     if _lib is None:
@@ -205,6 +208,9 @@ def lib() -> C.CDLL:
             if fn is not None:
                 fn.restype = res
                 fn.argtypes = args
+        if L.dsp_abi_version() != ABI_VERSION:
+            raise ImportError(f"{LIB_PATH}: ABI version {L.dsp_abi_version()}, this binding needs {ABI_VERSION} "
+                              "(rebuild the library)")
         _lib = L
     return _lib
 

@@ -267,8 +267,9 @@ def _hip_runtime():
     L.lib()  # libdspbench (and its libamdhip64.so.7) loaded first
     try:
         return C.CDLL("libamdhip64.so.7", mode=os.RTLD_NOLOAD | os.RTLD_NOW)
-    except OSError:
-        return C.CDLL("libamdhip64.so.7")
+    except OSError as e:  # loading a second runtime here would be fatal later
+        raise RuntimeError("TorchComm: libamdhip64.so.7 is not loaded in this process (libdspbench links it; "
+                           "is the library built against another HIP?)") from e
 
 
 class TorchComm(_Comm):

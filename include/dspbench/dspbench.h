@@ -43,7 +43,11 @@
 extern "C" {
 #endif
 
-#define DSPBENCH_ABI_VERSION 1
+/* 2 (round 4): dsp_fir_method removed (DSP_EXEC_FIR_DIRECT in dsp_exec.flags
+ * selects the direct form), the transport / gather-plan entry points and the
+ * dsp_comm layout of shard.h, dsp_callback_facts and the fact-gated block
+ * classes of module.h.  A binding written against 1 must not assume those. */
+#define DSPBENCH_ABI_VERSION 2
 
 enum dsp_status {
     DSP_OK = 0,
