@@ -85,8 +85,9 @@ def parse():
                          "gain_stft = gain_test render fused with the STFT (the input is read: the headline "
                          "shape with an input-dependent plugin); wav16enc / wav24enc = GPU encode of 1 h of "
                          "planar stereo into an interleaved int16 / int24 WAV payload")
-    ap.add_argument("--plugin", default=None, choices=["gain_test", "IR_test"],
-                    help="generic / generic_stft: the reference plugin source (default gain_test / IR_test)")
+    ap.add_argument("--plugin", default=None, choices=["gain_test", "IR_test", "static_gain_plugin"],
+                    help="generic / generic_stft: the reference plugin source (default gain_test / IR_test; "
+                         "static_gain_plugin = test/static_gain_plugin.cpp, a State the callback only reads)")
     ap.add_argument("--ir-plugin", default="source", choices=["source", "enum"],
                     help="headline / ch96k: source = the reference's IR_test.cpp compiled unchanged for gfx950 "
                          "(dsp-bench_amd/modules/mod_IR_test.co) and dispatched through its probed block class "
@@ -204,15 +205,15 @@ def pmc_traffic(workload: str, alg_bytes: float):
     return None, None, inst
 
 
-def cpu_baseline_generic(seconds_budget: float):
-    """The reference's own gain_test.cpp, compiled from its source with the
-    JIT's flags (oracle/_ref/libref_gain_test.so), called block by block by
-    the oracle's render loop on one host core: chunks of 60 s stereo until
-    the budget."""
+def cpu_baseline_generic(seconds_budget: float, pname: str = "gain_test"):
+    """The reference's own plugin source (gain_test.cpp by default), compiled
+    with the JIT's flags (oracle/_ref/libref_<pname>.so), called block by
+    block by the oracle's render loop on one host core: chunks of 60 s
+    stereo until the budget."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import numpy as np
     import oracle as o
-    ref = o.RefPlugin("gain_test", CH, float(SR))
+    ref = o.RefPlugin(pname, CH, float(SR))
     chunk = SR * 60
     x = np.random.default_rng(1).uniform(-1, 1, (CH, chunk)).astype(np.float32)
     done = 0
@@ -224,7 +225,7 @@ def cpu_baseline_generic(seconds_budget: float):
         if el >= seconds_budget:
             break
     return {"value": done / el / 1e6, "unit": "Msamples/s", "cores": 1, "kind": "reference",
-            "sample": f"{done // CH / SR:.0f} s of 48 kHz stereo through the reference's gain_test.cpp "
+            "sample": f"{done // CH / SR:.0f} s of 48 kHz stereo through the reference's {pname}.cpp "
                       "(compiled from source, -Ofast) and the oracle's render_audio loop, 1 thread"}
 
 
@@ -767,8 +768,8 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and wl == "headline":
         cpu = cpu_baseline(args.cpu_seconds)
-    elif rank == 0 and world == 1 and not args.no_cpu_baseline and wl == "generic" and not args.plugin:
-        cpu = cpu_baseline_generic(min(args.cpu_seconds, 5.0))
+    elif rank == 0 and world == 1 and not args.no_cpu_baseline and wl == "generic" and args.plugin != "IR_test":
+        cpu = cpu_baseline_generic(min(args.cpu_seconds, 5.0), args.plugin or "gain_test")
 
     def emit(gather_ms, gather_err):
         if rank != 0:

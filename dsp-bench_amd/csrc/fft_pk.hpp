@@ -83,11 +83,13 @@ __device__ __forceinline__ cx conj1(cx a) {
 }
 
 // DFT32 of both halves; INV: the unnormalised inverse, conj(DFT(conj(x)))
-template <bool BAR, bool INV>
+// (PRE4: forward, the first DFT4s done by the caller)
+template <bool BAR, bool INV, bool PRE4 = false>
 __device__ __forceinline__ void x2dft32_dir(cx2 (&v)[32]) {
+    static_assert(!(INV && PRE4), "PRE4: forward only");
 #pragma unroll
     for (int j = 0; j < 32; ++j) v[j] = conj2<INV>(v[j]);
-    x2dft32<BAR>(v);
+    x2dft32<BAR, PRE4>(v);
 #pragma unroll
     for (int j = 0; j < 32; ++j) v[j] = conj2<INV>(v[j]);
 }
@@ -175,11 +177,13 @@ __device__ __forceinline__ void transpose_pl(const cx2 (&Q)[32], float *lds, uin
 struct NoHook {
     __device__ void operator()() const {}
 };
-template <bool INV, bool BAR_DFT, bool BAR_TW, bool PL = false, bool AB_NOXP = false, typename HOOK = NoHook>
+template <bool INV, bool BAR_DFT, bool BAR_TW, bool PL = false, bool AB_NOXP = false, typename HOOK = NoHook,
+          bool PRE4 = false>
 __device__ __forceinline__ void fft4096_pk_front(cx2 (&P)[32], float *lds, const cx (&tlo)[8], const cx2 (&thp)[4],
                                                  uint32_t lane, cx2 (&R)[32], const HOOK &hook = HOOK{}) {
     // DFT64 over the register index: even/odd DFT32 in the halves, combine
-    x2dft32_dir<BAR_DFT, INV>(P);
+    // (PRE4: P holds the first DFT4s' outputs already)
+    x2dft32_dir<BAR_DFT, INV, PRE4>(P);
     cx2 Q[32];  // Q[k] = (Y[k], Y[k+32]) * (W4096^(+-l k), W4096^(+-l (k+32)))
     {
         cx2 Y[32];
@@ -241,11 +245,11 @@ __device__ __forceinline__ void fft4096_pk(cx2 (&P)[32], float *lds, const cx (&
 // The same transform with a packed last combine: Y2[q] = (U[l + 64 q],
 // U[l + 64 (q + 32)]) in the halves of one cx2 (forward only) -- 6 packed
 // instructions per pair instead of 8 scalar ones.
-template <bool BAR_DFT = true, bool BAR_TW = true, bool AB_NOXP = false, typename HOOK = NoHook>
+template <bool BAR_DFT = true, bool BAR_TW = true, bool AB_NOXP = false, typename HOOK = NoHook, bool PRE4 = false>
 __device__ __forceinline__ void fft4096_pk_y2(cx2 (&P)[32], float *lds, const cx (&tlo)[8], const cx2 (&thp)[4],
                                               uint32_t lane, cx2 (&Y2)[32], const HOOK &hook = HOOK{}) {
     cx2 R[32];
-    fft4096_pk_front<false, BAR_DFT, BAR_TW, false, AB_NOXP, HOOK>(P, lds, tlo, thp, lane, R, hook);
+    fft4096_pk_front<false, BAR_DFT, BAR_TW, false, AB_NOXP, HOOK, PRE4>(P, lds, tlo, thp, lane, R, hook);
     combine64p(R, Y2);
 }
 

@@ -31,12 +31,17 @@ __device__ __forceinline__ void x2dft4(cx2 &a, cx2 &b, cx2 &c, cx2 &d) {
     d = t1 - t3;
 }
 
+// PRE4: the two DFT4s (evens u0 u2 u4 u6, odds u1 u3 u5 u7, in place) are
+// done already (the windowed periodic frames: stft_pk.hpp x2dft4_win)
+template <bool PRE4 = false>
 __device__ __forceinline__ void x2dft8(cx2 &u0, cx2 &u1, cx2 &u2, cx2 &u3, cx2 &u4, cx2 &u5,
                                        cx2 &u6, cx2 &u7) {
     cx2 e0 = u0, e1 = u2, e2 = u4, e3 = u6;
     cx2 o0 = u1, o1 = u3, o2 = u5, o3 = u7;
-    x2dft4(e0, e1, e2, e3);
-    x2dft4(o0, o1, o2, o3);
+    if constexpr (!PRE4) {
+        x2dft4(e0, e1, e2, e3);
+        x2dft4(o0, o1, o2, o3);
+    }
     const float r = 0x1.6a09e6p-1f;
     const cx2 w1 = cx2{(o1.r + o1.i) * r, (o1.i - o1.r) * r};
     const cx2 w2 = negi(o2);
@@ -113,13 +118,14 @@ __device__ __forceinline__ void x2dft32_stage2(cx2 (&v)[32]) {
 
 // 32-point DFT, natural order in, X[k] at v[perm32(k)] out (8 x 4).
 // BAR: pin one DFT8 / DFT4 at a time (bounds register pressure, costs ILP).
-template <bool BAR = true>
+// PRE4: the DFT8s' first DFT4s are done (x2dft8<true>).
+template <bool BAR = true, bool PRE4 = false>
 __device__ __forceinline__ void x2dft32(cx2 (&v)[32]) {
 #pragma unroll
     for (int j2 = 0; j2 < 4; ++j2) {
         if (BAR) __builtin_amdgcn_sched_barrier(0);
-        x2dft8(v[j2], v[4 + j2], v[8 + j2], v[12 + j2], v[16 + j2], v[20 + j2], v[24 + j2],
-               v[28 + j2]);
+        x2dft8<PRE4>(v[j2], v[4 + j2], v[8 + j2], v[12 + j2], v[16 + j2], v[20 + j2], v[24 + j2],
+                     v[28 + j2]);
     }
     x2dft32_stage2<0, BAR>(v);
     __builtin_amdgcn_sched_barrier(0);

@@ -234,6 +234,10 @@ void stft8192_pk_kernel(Stft8kArgs A) {
     // memory frames with the computed window: two dwordx2 loads per pair
     // (columns 2j, 2j+1) regrouped into even/odd halves
     constexpr bool MSOA = WINC && SRC == kSrcMemory && !(OPT & kPkMemAos);
+    // periodic frames whose period in j divides 8: the window is fused into
+    // the first DFT4s (x2dft4 over j0 + 8 m sees one x), on the default FFT
+    constexpr bool W4 = SOA && (8 % (PER >= 2 ? PER / 2 : 1)) == 0 && OCC == 2 &&
+                        !(OPT & (kPkOldSplit | kPkMagLds | kPkAbNoXpose));
     const uint64_t fs = f * (uint64_t)A.H;
     if (f >= A.F) {  // whole wave leaves; nothing below waits on other waves
         if constexpr (SOA) {
@@ -336,20 +340,69 @@ void stft8192_pk_kernel(Stft8kArgs A) {
         // w(n) = wa - wb cos(theta n) = wa - u C_b + v S_b per parity, with
         // u = wb cos(theta n0), v = wb sin(theta n0) of the lane's base angle
         const float ue = A.wb * wbase.x, ve = A.wb * wbase.y, uo = A.wb * wbase.z, vo = A.wb * wbase.w;
+        if constexpr (SOA) {
+            // the frame repeats with period NJ in j: x w = x wa - (x u) C + (x v) S
+            // with x wa, x u, x v formed once per distinct x (XA holds 4 x wa
+            // when the first DFT4s are fused: W4)
+            cx2 XA[NJ], XU[NJ], XV[NJ];
+            const float wa = W4 ? 4.f * A.wa : A.wa;
+#pragma unroll
+            for (int jj = 0; jj < NJ; ++jj) {
+                XA[jj] = cx2{X[jj].r * v2f{wa, wa}, X[jj].i * v2f{wa, wa}};
+                XU[jj] = cx2{X[jj].r * v2f{ue, ue}, X[jj].i * v2f{uo, uo}};
+                XV[jj] = cx2{X[jj].r * v2f{ve, ve}, X[jj].i * v2f{vo, vo}};
+            }
+            auto fma2 = [](v2f a, v2f b, v2f c) { return __builtin_elementwise_fma(a, b, c); };
+            if constexpr (W4) {
+                // the first DFT32's first DFT4s, over j = j0 + 8 m (m < 4), of
+                // the windowed frame P[j] = XA + XV S_j - XU C_j: every input of
+                // one DFT4 has the same x (8 is a multiple of NJ), so each output
+                // is XA, XV and XU times sums of window constants -- 20 packed
+                // instructions per DFT4 instead of 16 for the window and 16 for
+                // the butterflies (x2dft8<true> continues from here)
+                auto Sv = [](int j) { return v2f{kWinB_s[2 * j], kWinB_s[2 * j + 1]}; };
+                auto Cv = [](int j) { return v2f{kWinB_c[2 * j], kWinB_c[2 * j + 1]}; };
+#pragma unroll
+                for (int j0 = 0; j0 < 8; ++j0) {
+                    const int jj = j0 % NJ;
+                    const v2f s0 = Sv(j0), s1 = Sv(j0 + 8), s2 = Sv(j0 + 16), s3 = Sv(j0 + 24);
+                    const v2f c0 = Cv(j0), c1 = Cv(j0 + 8), c2 = Cv(j0 + 16), c3 = Cv(j0 + 24);
+                    const cx2 xa = XA[jj], xu = XU[jj], xv = XV[jj];
+                    // X0 = 4 XA + XV (s0 + s1 + s2 + s3) - XU (c0 + ... + c3)
+                    const v2f sA = (s0 + s1) + (s2 + s3), cA = (c0 + c1) + (c2 + c3);
+                    P[j0] = cx2{fma2(-xu.r, cA, fma2(xv.r, sA, xa.r)), fma2(-xu.i, cA, fma2(xv.i, sA, xa.i))};
+                    // X2 = XV (s0 - s1 + s2 - s3) - XU (...)
+                    const v2f sC = (s0 - s1) + (s2 - s3), cC = (c0 - c1) + (c2 - c3);
+                    P[j0 + 16] = cx2{fma2(-xu.r, cC, xv.r * sC), fma2(-xu.i, cC, xv.i * sC)};
+                    // t1 = P[j0] - P[j0 + 16] terms, q = P[j0 + 8] - P[j0 + 24]:
+                    // X1 = t1 - i q, X3 = t1 + i q
+                    const v2f sT = s0 - s2, cT = c0 - c2, sQ = s1 - s3, cQ = c1 - c3;
+                    const cx2 t1 = cx2{fma2(-xu.r, cT, xv.r * sT), fma2(-xu.i, cT, xv.i * sT)};
+                    const cx2 q = cx2{fma2(-xu.r, cQ, xv.r * sQ), fma2(-xu.i, cQ, xv.i * sQ)};
+                    P[j0 + 8] = cx2{t1.r + q.i, t1.i - q.r};
+                    P[j0 + 24] = cx2{t1.r - q.i, t1.i + q.r};
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < 32; ++j) {
+                    const v2f C = v2f{kWinB_c[2 * j], kWinB_c[2 * j + 1]}, S = v2f{kWinB_s[2 * j], kWinB_s[2 * j + 1]};
+                    const int jj = j % NJ;
+                    P[j] = cx2{fma2(-XU[jj].r, C, fma2(XV[jj].r, S, XA[jj].r)),
+                               fma2(-XU[jj].i, C, fma2(XV[jj].i, S, XA[jj].i))};
+                }
+            }
+        } else {
 #pragma unroll
         for (int j = 0; j < 32; ++j) {
             const v2f C = v2f{kWinB_c[2 * j], kWinB_c[2 * j + 1]}, S = v2f{kWinB_s[2 * j], kWinB_s[2 * j + 1]};
             const v2f we = (v2f{ve, ve} * S + v2f{A.wa, A.wa}) - v2f{ue, ue} * C;
             const v2f wo = (v2f{vo, vo} * S + v2f{A.wa, A.wa}) - v2f{uo, uo} * C;
-            cx2 xj;
-            if constexpr (SOA) {
-                xj = X[j % NJ];
-            } else {  // (x[2l + 256 j], x[2l + 256 j + 1]) and 128 samples on
-                const v2f a = reinterpret_cast<const v2f *>(x + fs + 256u * (uint32_t)j)[lane];
-                const v2f b = reinterpret_cast<const v2f *>(x + fs + 256u * (uint32_t)j + 128u)[lane];
-                xj = cx2{v2f{a.x, b.x}, v2f{a.y, b.y}};
-            }
+            // (x[2l + 256 j], x[2l + 256 j + 1]) and 128 samples on
+            const v2f a = reinterpret_cast<const v2f *>(x + fs + 256u * (uint32_t)j)[lane];
+            const v2f b = reinterpret_cast<const v2f *>(x + fs + 256u * (uint32_t)j + 128u)[lane];
+            const cx2 xj = cx2{v2f{a.x, b.x}, v2f{a.y, b.y}};
             P[j] = cx2{xj.r * we, xj.i * wo};
+        }
         }
     } else {
     // ---- 1. frame (+ fused render) -----------------------------------------
@@ -418,7 +471,8 @@ void stft8192_pk_kernel(Stft8kArgs A) {
         // Y2[q] = (Z[l + 64 q], Z[l + 64 (q + 32)])
         cx2 Y2[32];
         if constexpr (OCC >= 3) fft4096_pk_y2_lo<!(OPT & kPkNoBarDft)>(P, lds, A.tw, lane, Y2);
-        else fft4096_pk_y2<!(OPT & kPkNoBarDft), !(OPT & kPkNoBarTw), (OPT & kPkAbNoXpose) != 0>(P, lds, tlo, thp, lane, Y2);
+        else fft4096_pk_y2<!(OPT & kPkNoBarDft), !(OPT & kPkNoBarTw), (OPT & kPkAbNoXpose) != 0, NoHook, W4>(
+            P, lds, tlo, thp, lane, Y2);
         split_y2<KM, !(OPT & kPkNoBarSplit), (OPT & kPkAbNoMag) != 0, KM == kKHalf && (OPT & kPkMagStage) != 0,
                  (OPT & kPkNtMag) != 0>(Y2, A.mag.p[ch] + f * A.ld, A.K, A.tw, lane, lds);
         return;
