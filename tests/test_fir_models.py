@@ -26,3 +26,16 @@ def test_two_wave_pair_frame_model():
         y = m.render(x0, x1, taps)
         assert np.abs(y.real - np.convolve(x0, taps)[:L]).max() < 1e-9
         assert np.abs(y.imag - np.convolve(x1, taps)[:L]).max() < 1e-9
+
+
+def test_dif_two_wave_frame_model():
+    """fir_dif2_kernel's algebra and H table layout (tools/olsdif_model.py):
+    decimation in frequency over the two waves, one exchange of outputs."""
+    m = _load("olsdif_model")
+    rng = np.random.default_rng(5)
+    for L, T in [(7168 * 2 + 4321, 1024), (777, 1025), (15_000, 3)]:
+        taps = rng.standard_normal(T) / np.sqrt(T)
+        x0, x1 = rng.uniform(-1, 1, L), rng.uniform(-1, 1, L)
+        y = m.render(x0, x1, taps)
+        assert np.abs(y.real - np.convolve(x0, taps)[:L]).max() < 1e-9
+        assert np.abs(y.imag - np.convolve(x1, taps)[:L]).max() < 1e-9
