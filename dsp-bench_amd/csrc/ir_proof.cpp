@@ -46,6 +46,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <mutex>
 #include <set>
 #include <sstream>
 
@@ -763,9 +764,9 @@ bool get_data(amd_comgr_data_set_t set, amd_comgr_data_kind_t k, std::string *ou
 // hiprtc's runtime header (libhiprtc-builtins), which hiprtc pre-includes
 bool hiprtc_runtime_header(std::string *out) {
     static std::string text;
-    static bool tried = false, ok = false;
-    if (!tried) {
-        tried = true;
+    static bool ok = false;
+    static std::once_flag once;
+    std::call_once(once, [] {
         void *h = dlopen("libhiprtc-builtins.so.7", RTLD_NOW | RTLD_LOCAL);
         if (!h) h = dlopen("libhiprtc-builtins.so", RTLD_NOW | RTLD_LOCAL);
         if (h) {
@@ -776,7 +777,7 @@ bool hiprtc_runtime_header(std::string *out) {
                 ok = true;
             }
         }
-    }
+    });
     *out = text;
     return ok;
 }
