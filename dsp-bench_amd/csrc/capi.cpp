@@ -599,6 +599,67 @@ static int specialize_generic(SampleMap *m, uint32_t C, uint32_t B, hipStream_t 
     return DSP_OK;
 }
 
+// DSP_EXEC_VERIFY_CLASS: after a GENERIC plugin rendered by its block class,
+// run its callback on blocks of the call's own input -- the first, the last
+// and two more (a hash of the call's length and offset) -- as render_audio
+// hands them over (audio.cpp:13-175: the file, zeros past EOF and for the
+// channels the file lacks), and compare with the rendered rows bit for bit.
+// *ok = false on any difference.  Synchronises the stream.
+static int verify_class(const SampleMap &orig, const float *const *in, uint32_t in_ch, uint64_t L,
+                        float *const *out, uint32_t C, uint32_t B, uint64_t goff, hipStream_t s, bool *ok) {
+    *ok = true;
+    const uint64_t nb = (L + B - 1) / B;
+    if (nb == 0) return DSP_OK;
+    uint64_t pick[4] = {0, nb - 1, 0, 0};
+    uint64_t h = (L * 0x9e3779b97f4a7c15ull) ^ (goff + 0x632be59bd9b4e019ull);
+    for (int i = 2; i < 4; ++i) {
+        h ^= h >> 29;
+        h *= 0xbf58476d1ce4e5b9ull;
+        h ^= h >> 32;
+        pick[i] = h % nb;
+    }
+    const uint64_t n = (uint64_t)C * B;
+    float *d = nullptr;
+    DSPB_HIP(hipMalloc(&d, sizeof(float) * n));
+    struct Free {
+        float *p;
+        ~Free() { (void)hipFree(p); }
+    } fr{d};
+    std::vector<float> blk(n), got(n), want(n);
+    for (uint64_t b : pick) {
+        const uint64_t i0 = b * B;
+        const uint64_t m = L > i0 ? std::min<uint64_t>(B, L - i0) : 0;  // file samples in the block
+        std::fill(blk.begin(), blk.end(), 0.f);
+        for (uint32_t c = 0; c < std::min(in_ch, C); ++c)
+            if (m) DSPB_HIP(hipMemcpyAsync(blk.data() + (uint64_t)c * B, in[c] + i0, m * sizeof(float),
+                                           hipMemcpyDeviceToHost, s));
+        for (uint32_t c = 0; c < C; ++c)
+            DSPB_HIP(hipMemcpyAsync(got.data() + (uint64_t)c * B, out[c] + i0, (uint64_t)B * sizeof(float),
+                                    hipMemcpyDeviceToHost, s));
+        DSPB_HIP(hipStreamSynchronize(s));
+        DSPB_HIP(hipMemcpyAsync(d, blk.data(), sizeof(float) * n, hipMemcpyHostToDevice, s));
+        std::vector<float *> rows(C);
+        for (uint32_t c = 0; c < C; ++c) rows[c] = d + (uint64_t)c * B;
+        if (int st = module_callback_once((::dsp_module *)orig.module, orig.gparams, orig.gparams_size, rows.data(),
+                                          C, B, orig.sr, s))
+            return st;
+        DSPB_HIP(hipMemcpyAsync(want.data(), d, sizeof(float) * n, hipMemcpyDeviceToHost, s));
+        DSPB_HIP(hipStreamSynchronize(s));
+        if (std::memcmp(want.data(), got.data(), sizeof(float) * n) != 0) {
+            *ok = false;
+            set_last_error("DSP_EXEC_VERIFY_CLASS: block %llu rendered by the block class differs from the "
+                           "plugin's callback; rendered again with the callback",
+                           (unsigned long long)b);
+            return DSP_OK;
+        }
+    }
+    return DSP_OK;
+}
+
+static void set_result(const dsp_exec *ex, uint32_t bits) {
+    if (ex && ex->result) *ex->result = bits;
+}
+
 // ---------------------------------------------------------------------------
 // host-buffer staging (DSP_EXEC_HOST_BUFFERS)
 // ---------------------------------------------------------------------------
@@ -947,6 +1008,7 @@ int dsp_render_offline(const float *const *in, uint32_t in_channels, uint64_t L,
     SampleMap map;
     int st = plugin_map(plugin, B, g.dev, s, &map, sr, ex ? ex->flags : 0);
     if (st) return st;
+    const SampleMap orig = map;
     if ((st = specialize_generic(&map, C, B, s, ex))) return st;
     TimedLaunch tl{};
     if ((st = timing_begin(s, &tl))) return st;
@@ -956,6 +1018,19 @@ int dsp_render_offline(const float *const *in, uint32_t in_channels, uint64_t L,
         uint64_t bytes = (uint64_t)C * Lr * 4;
         if (map.kind != MapKind::Ramp) bytes += (uint64_t)std::min(in_channels, C) * L * 4;
         if ((st = timing_end(s, &tl, bytes))) return st;
+    }
+    if (orig.kind == MapKind::Generic && map.kind != MapKind::Generic) {
+        uint32_t res = DSP_RESULT_CLASS;
+        if (ex && (ex->flags & DSP_EXEC_VERIFY_CLASS)) {
+            bool ok = true;
+            if ((st = verify_class(orig, din.data(), in_channels, L, dout.data(), C, B, goff_of(ex), s, &ok))) return st;
+            res |= ok ? DSP_RESULT_VERIFIED : DSP_RESULT_RERENDERED;
+            if (!ok && (st = render_device(din.data(), in_channels, L, dout.data(), C, B, orig, 0, goff_of(ex), s)))
+                return st;
+        }
+        set_result(ex, res);
+    } else {
+        set_result(ex, 0);
     }
     if (host_mode(ex))
         for (uint32_t c = 0; c < C; ++c)
@@ -1109,8 +1184,10 @@ int dsp_render_stft(const float *const *in, uint32_t in_channels, uint64_t L,
     }
     SampleMap map;
     if ((st = plugin_map(plugin, B, g.dev, s, &map, sr, ex ? ex->flags : 0))) return st;
+    const SampleMap orig = map;
     if ((st = specialize_generic(&map, C, B, s, ex))) return st;
     const uint64_t goff = goff_of(ex);
+    set_result(ex, orig.kind == MapKind::Generic && map.kind != MapKind::Generic ? DSP_RESULT_CLASS : 0u);
 
     bool fused = (N == 8192) && (H % 128 == 0) && (H <= N) && (goff % 2 == 0) && F > 0 &&
                  map.kind != MapKind::Fir && map.kind != MapKind::Generic;
@@ -1183,6 +1260,14 @@ int dsp_render_stft(const float *const *in, uint32_t in_channels, uint64_t L,
             st = render_device(din.data(), in_channels, L, dout.data(), C, B, map, F * (uint64_t)H, goff, s);
             if (st) return st;
         }
+    }
+    if (orig.kind == MapKind::Generic && map.kind != MapKind::Generic && ex && (ex->flags & DSP_EXEC_VERIFY_CLASS)) {
+        bool ok = true;
+        if ((st = verify_class(orig, din.data(), in_channels, L, dout.data(), C, B, goff, s, &ok))) return st;
+        set_result(ex, DSP_RESULT_CLASS | (ok ? DSP_RESULT_VERIFIED : DSP_RESULT_RERENDERED));
+        if (!ok && (st = generic_render_stft(din.data(), in_channels, L, dout.data(), C, B, orig, N, H, window, K,
+                                             dmag.data(), ld, goff, g.dev, s)))
+            return st;
     }
     if (host_mode(ex)) {
         for (uint32_t c = 0; c < C; ++c) {

@@ -411,6 +411,12 @@ int launch_fir_pair(const FirFftArgs &A, uint32_t C, hipStream_t s) {
 // tools/ols2w_model.py's checks cover the same algebra (the DIT form); the
 // GPU tests compare this kernel with np.convolve (tests/test_gpu_fir.py).
 constexpr uint32_t kDif2Hop = 7168;
+#ifndef DSPB_DIF2_LB
+#define DSPB_DIF2_LB 16  // frame-load batch (columns pairs j per batch)
+#endif
+#ifndef DSPB_DIF2_HB
+#define DSPB_DIF2_HB 16  // H-load batch (q per batch)
+#endif
 
 // one pass of the output combine: ODD wave 1 (y[n + 4096] = ye - t, ye read
 // from the peer), else wave 0 (y[n] = ye + t for q' >= 16); stores at
@@ -454,9 +460,9 @@ __device__ __forceinline__ void fir_dif2_frame(const FirFftArgs &A, uint64_t f, 
     cx2 P[32];
 #pragma unroll
     for (int j = 0; j < 32; ++j) {
-        // (batches of four: the loads of the whole frame in flight at once
+        // (two batches: the loads of the whole frame in flight at once
         // would hold 256 VGPRs before the sums halve them)
-        if (j % 4 == 0) __builtin_amdgcn_sched_barrier(0);
+        if (j % DSPB_DIF2_LB == 0) __builtin_amdgcn_sched_barrier(0);
         cx2 lo, hi;  // u[m], u[m + 4096] for r = 2j, 2j + 1
         if constexpr (!EDGE) {
             const float *b0 = x0 + fs, *b1 = x1 + fs;
@@ -494,7 +500,7 @@ __device__ __forceinline__ void fir_dif2_frame(const FirFftArgs &A, uint64_t f, 
         for (int q = 0; q < 32; ++q) {
             // (batches of eight: all 32 loads hoisted would hold 128 VGPRs
             // beside the spectrum's 128)
-            if (q % 8 == 0) __builtin_amdgcn_sched_barrier(0);
+            if (q % DSPB_DIF2_HB == 0) __builtin_amdgcn_sched_barrier(0);
             const float4 h = H4[64u * (uint32_t)q + lane];
             Y2[q] = cmul2(Y2[q], cx2{v2f{h.x, h.y}, v2f{h.z, h.w}});
         }

@@ -1297,6 +1297,33 @@ int module_render(dsp_module *m, const void *params, uint32_t params_size, const
     return DSP_OK;
 }
 
+// The callback once on device buffers, with the live State (DSP_EXEC_VERIFY_CLASS:
+// blocks of a call rendered by a block class, re-run through the callback).
+// Only for a module whose blocks are independent (par): its callback never
+// writes the State, so this run leaves it as it was.
+int module_callback_once(dsp_module *m, const void *params, uint32_t params_size, float *const *bufs, uint32_t C,
+                         uint32_t B, float sr, hipStream_t s) {
+    if (!m || !m->par || !m->initialized) {
+        set_last_error("module_callback_once: a loaded module with independent blocks is needed");
+        return DSP_ERR_INVALID;
+    }
+    if (C == 0 || C > (uint32_t)kMaxChannels || params_size != m->params_size) return DSP_ERR_INVALID;
+    if (int st = check_device(m)) return st;
+    std::lock_guard<std::mutex> lk(m->mu);
+    if (int st = upload_params(m, params, params_size, s)) return st;
+    RenderArgsG A{};
+    A.P = m->d_params;
+    A.S = m->d_state[0];
+    for (uint32_t c = 0; c < C; ++c) A.out[c] = bufs[c];
+    A.C = C;
+    A.B = B;
+    A.sr = sr;
+    void *args[] = {&A};
+    MOD_HIP(hipModuleLaunchKernel(m->f_callback, 1, 1, 1, 1, 1, 1, 0, s, args, nullptr));
+    MOD_HIP(hipEventRecord(m->use_ev, s));
+    return DSP_OK;
+}
+
 // dsp_ir_analysis with DSP_PLUGIN_GENERIC: fresh scratch State (compute_IR,
 // plugin.cpp:33-49), then the callback once on the impulse buffers.
 int module_ir(dsp_module *m, const void *params, uint32_t params_size, float *const *bufs, uint32_t C,

@@ -32,6 +32,10 @@ DSP_EXEC_HOST_BUFFERS = 0x1
 DSP_EXEC_SYNC = 0x2
 DSP_EXEC_FIR_DIRECT = 0x4
 DSP_EXEC_NO_SPECIALIZE = 0x8
+DSP_EXEC_VERIFY_CLASS = 0x10
+DSP_RESULT_CLASS = 0x1
+DSP_RESULT_VERIFIED = 0x2
+DSP_RESULT_RERENDERED = 0x4
 DSP_BLOCK_CALLBACK, DSP_BLOCK_TABLE, DSP_BLOCK_GAIN = 0, 1, 2
 
 
@@ -48,7 +52,7 @@ class dsp_plugin(C.Structure):
 
 class dsp_exec(C.Structure):
     _fields_ = [("device", C.c_int32), ("flags", C.c_uint32), ("stream", C.c_void_p),
-                ("sample_offset", C.c_uint64)]
+                ("sample_offset", C.c_uint64), ("result", C.POINTER(C.c_uint32))]
 
 
 DSP_WAV_FORMAT_PCM = 1

@@ -23,6 +23,7 @@ from __future__ import annotations
 
 import ctypes as C
 import struct
+import threading
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -126,6 +127,21 @@ def num_blocks(L_: int, B: int) -> int:
 # entry points
 # --------------------------------------------------------------------------
 
+_tls = threading.local()
+
+
+def last_result() -> int:
+    """dsp_exec.result of this thread's last render_offline / render_stft
+    (DSP_RESULT_CLASS / _VERIFIED / _RERENDERED bits)."""
+    return getattr(_tls, "result", 0)
+
+
+def _track(ex):
+    r = C.c_uint32(0)
+    ex.result = C.pointer(r)
+    return r
+
+
 def render_offline(file, C_out: int, B: int, sr: float, plugin: Plugin | None,
                    out=None, sample_offset: int = 0, L_file: int | None = None, stream=None):
     """Offline one-shot render.  file: [Cin, L] (Cin may be 0 / None).
@@ -139,10 +155,12 @@ def render_offline(file, C_out: int, B: int, sr: float, plugin: Plugin | None,
     ex = _exec(oref, sample_offset, stream)
     ps = plugin.as_struct() if plugin is not None else None
     ex.flags |= plugin.exec_flags if plugin is not None else 0
+    res = _track(ex)
     st = L.lib().dsp_render_offline(chan_table(in_ptrs) if in_ptrs else None, len(in_ptrs), L_,
                                     chan_table(out_ptrs), C_out, B, sr,
                                     C.byref(ps) if ps is not None else None, C.byref(ex))
     check(st, "dsp_render_offline")
+    _tls.result = res.value
     return out[:, : nb * B]
 
 
@@ -206,11 +224,13 @@ def render_stft(file, C_out: int, B: int, sr: float, plugin: Plugin | None,
     ex = _exec(oref, sample_offset, stream)
     ps = plugin.as_struct() if plugin is not None else None
     ex.flags |= plugin.exec_flags if plugin is not None else 0
+    res = _track(ex)
     st = L.lib().dsp_render_stft(chan_table(in_ptrs) if in_ptrs else None, len(in_ptrs), L_,
                                  chan_table(out_ptrs), C_out, B, sr,
                                  C.byref(ps) if ps is not None else None, N, H, window, K,
                                  chan_table(mag_ptrs), ld, C.byref(ex))
     check(st, "dsp_render_stft")
+    _tls.result = res.value
     return out[:, : nb * B], mag[:, :F, :K]
 
 

@@ -230,14 +230,17 @@ class Module:
         check(L.lib().dsp_module_read_state(self.handle, buf), "dsp_module_read_state")
         return buf.raw[:self.state_size]
 
-    def plugin(self, params: bytes, name: str = "generic", specialize: bool = True):
+    def plugin(self, params: bytes, name: str = "generic", specialize: bool = True, verify: bool = False):
         """A GENERIC plugin over this module.  specialize=False runs the
         plugin's callback on every block (DSP_EXEC_NO_SPECIALIZE); by default
-        a stateless plugin of a known block class runs as that class
-        (block_class)."""
+        a plugin whose block class its IR proves runs as that class
+        (block_class).  verify=True checks blocks of every call against the
+        callback (DSP_EXEC_VERIFY_CLASS; dspbench.api.last_result())."""
         from .api import Plugin
-        return Plugin(L.DSP_PLUGIN_GENERIC, bytes(params), b"", name, self,
-                      exec_flags=0 if specialize else L.DSP_EXEC_NO_SPECIALIZE)
+        flags = 0 if specialize else L.DSP_EXEC_NO_SPECIALIZE
+        if verify:
+            flags |= L.DSP_EXEC_VERIFY_CLASS
+        return Plugin(L.DSP_PLUGIN_GENERIC, bytes(params), b"", name, self, exec_flags=flags)
 
     def block_class(self, params: bytes, channels: int, block: int, sample_rate: float, stream=None):
         """(class, gain): "table" | "gain" | "callback" (dsp_module_block_class),

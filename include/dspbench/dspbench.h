@@ -93,14 +93,25 @@ typedef struct dsp_plugin {
                                       FFT overlap-save with 8192-point frames for T <= 1025, the
                                       direct form above) */
 #define DSP_EXEC_NO_SPECIALIZE 0x8u /* DSP_PLUGIN_GENERIC: run the plugin's callback on every block.
-                                      Default: a stateless plugin whose callback, probed once per
-                                      (Parameters, C, B, sample rate), ignores its input (renders
-                                      the same block whatever it is given, on every channel) or
-                                      scales it by one factor runs as that block tiled / that gain
-                                      in the fused kernels (module.h) */
+                                      Default: a plugin whose callback the IR analysis proves to
+                                      ignore its input (then one block, the same on every channel)
+                                      or to scale it by one factor runs as that block tiled / that
+                                      gain in the fused kernels (module.h dsp_callback_facts) */
+#define DSP_EXEC_VERIFY_CLASS 0x10u /* DSP_PLUGIN_GENERIC rendered by a block class: afterwards run
+                                      the callback on the first, the last and two more blocks of the
+                                      call's own input and compare with the rendered rows bit for
+                                      bit; on a mismatch render the call again with the callback on
+                                      every block.  Reported through dsp_exec.result.  Costs a
+                                      stream synchronisation (dsp_render_offline / dsp_render_stft) */
 /* the flags that choose how a call computes (not where its buffers live):
  * the chunked and sharded drivers pass them on to every chunk */
-#define DSP_EXEC_METHOD_FLAGS (DSP_EXEC_FIR_DIRECT | DSP_EXEC_NO_SPECIALIZE)
+#define DSP_EXEC_METHOD_FLAGS (DSP_EXEC_FIR_DIRECT | DSP_EXEC_NO_SPECIALIZE | DSP_EXEC_VERIFY_CLASS)
+
+/* dsp_exec.result bits (written when result is not NULL) */
+#define DSP_RESULT_CLASS 0x1u      /* a GENERIC plugin ran as its block class */
+#define DSP_RESULT_VERIFIED 0x2u   /* DSP_EXEC_VERIFY_CLASS: the checked blocks matched */
+#define DSP_RESULT_RERENDERED 0x4u /* DSP_EXEC_VERIFY_CLASS: a checked block differed; the call was
+                                      rendered again with the callback on every block */
 
 typedef struct dsp_exec {
     int32_t device;         /* HIP device ordinal; -1 = current device */
@@ -108,6 +119,7 @@ typedef struct dsp_exec {
     void *stream;           /* hipStream_t; NULL = the legacy default stream */
     uint64_t sample_offset; /* global index of in[c][0] (time-chunk shards);
                                must be a multiple of the block size B */
+    uint32_t *result;       /* optional: DSP_RESULT_* of the call (NULL: not reported) */
 } dsp_exec;
 
 /* Number of frames of an STFT over L samples: L >= N ? (L - N) / H + 1 : 0. */

@@ -235,3 +235,51 @@ def test_evicted_table_outlives_a_captured_graph(torch_cuda):
     g.replay()
     torch.cuda.synchronize()
     assert bool((out == 0.125).all())
+
+
+def test_verify_class_reports_and_catches_a_wrong_class(torch_cuda):
+    """DSP_EXEC_VERIFY_CLASS, the second line of defence: a proven class is
+    checked against the callback on four blocks of the call's own input
+    (VERIFIED); a class taken on tampered facts -- gain_until_loud.cpp's code
+    object edited to claim the gain form -- renders wrong rows, the check sees
+    them, and the call is rendered again with the callback (RERENDERED): the
+    result equals the plugin's semantics either way."""
+    torch = torch_cuda
+    import dspbench._lib as L
+    from dspbench.api import last_result
+    mods = os.path.join(os.path.dirname(HERE), "dsp-bench_amd", "modules")
+    if not os.path.exists(os.path.join(mods, "mod_gain_test.co")):
+        pytest.skip("modules not built")
+    with open(os.path.join(mods, "mod_gain_test.co"), "rb") as f:
+        gmod = d.module.Module(f.read())
+    gp = gmod.default_parameters()
+    gmod.initialize_state(gp, 2, 48000.0)
+    x = torch.rand((2, 512 * 40 + 7), device="cuda") * 2 - 1
+    d.render_offline(x, 2, 512, 48000.0, gmod.plugin(gp, "gain_test", verify=True))
+    assert last_result() == L.DSP_RESULT_CLASS | L.DSP_RESULT_VERIFIED
+    d.render_stft(x, 2, 512, 48000.0, gmod.plugin(gp, "gain_test", verify=True), window=d.DSP_WIN_HANN)
+    assert last_result() == L.DSP_RESULT_CLASS | L.DSP_RESULT_VERIFIED
+    d.render_offline(x, 2, 512, 48000.0, gmod.plugin(gp, "gain_test"))
+    assert last_result() == L.DSP_RESULT_CLASS  # not checked without the flag
+
+    src = open(os.path.join(PLUG, "gain_until_loud.cpp")).read()
+    code = d.module.compile_source(src, "gain_until_loud.cpp")
+    assert b"gain_form=0" in code and b"input_control=1" in code and b"gain_src=P" in code
+    bad = code.replace(b"gain_form=0", b"gain_form=1").replace(b"input_control=1", b"input_control=0")
+    mod = d.module.Module(bad)
+    params = mod.default_parameters()
+    mod.initialize_state(params, 2, 48000.0)
+    assert mod.block_class(params, 2, 512, 48000.0)[0] == "gain"  # the probes stay below 5000
+    B, L_ = 512, 512 * 30
+    xs = make_input(L_, seed=8)
+    xs[:, ::300] = F(9000)  # every block has a sample above 5000
+    want = semantics("gain_until_loud", blocks(xs, 2, B), params)
+    xg = torch.from_numpy(xs).cuda()
+    wrong = d.render_offline(xg, 2, B, 48000.0, mod.plugin(params, "gul")).cpu().numpy()
+    assert not np.array_equal(wrong, want)  # the tampered class renders wrong rows
+    got = d.render_offline(xg, 2, B, 48000.0, mod.plugin(params, "gul", verify=True)).cpu().numpy()
+    assert last_result() == L.DSP_RESULT_CLASS | L.DSP_RESULT_RERENDERED
+    assert np.array_equal(got, want)
+    out, mag = d.render_stft(xg, 2, B, 48000.0, mod.plugin(params, "gul", verify=True), window=d.DSP_WIN_HANN)
+    assert last_result() == L.DSP_RESULT_CLASS | L.DSP_RESULT_RERENDERED
+    assert np.array_equal(out.cpu().numpy(), want)
