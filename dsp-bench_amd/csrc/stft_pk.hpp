@@ -67,7 +67,10 @@ constexpr int kPkDefaultOpt = kPkNoBarDft | kPkNoBarTw | kPkNoBarSplit;
 // 0.8-2.2% faster there, but 1-2% slower for the paths that read a signal
 // (memory, gain), whose four-frame workgroups share their hops in L2
 // (profiles/r02_w1_ab.txt)
-constexpr int kPkPerOpt = kPkDefaultOpt | kPkW1;
+#ifndef DSPB_PK_PER_EXTRA
+#define DSPB_PK_PER_EXTRA 0  // extra option bits of the PER kernels (A/B builds)
+#endif
+constexpr int kPkPerOpt = kPkDefaultOpt | kPkW1 | DSPB_PK_PER_EXTRA;
 
 typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));  // a row is only dword-aligned
 typedef float f4a __attribute__((ext_vector_type(4)));               // 16-byte aligned

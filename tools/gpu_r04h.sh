@@ -12,3 +12,8 @@ DSPBENCH_LIB=$R/build/dif2_16_16/libdspbench.so timeout -k 10 300 python -u -m p
 tail -1 $o/fir_tests.log
 timeout -k 10 500 python tools/ab_lib.py --fir 4 $R/libdspbench.so $R/build/dif2_16_16/libdspbench.so $R/build/dif2_32_32/libdspbench.so $R/build/dif2_8_8/libdspbench.so > $o/ab_fir.txt 2>&1 || { echo "ab rc=$?"; tail -5 $o/ab_fir.txt; exit 1; }
 cat $o/ab_fir.txt
+# the magnitude rows staged in LDS and stored as aligned non-temporal dwordx4
+# (kPkMagStage | kPkNtMag on the PER kernels, build/magst) under the driver's
+# command: round 3 measured it settled only (less energy per frame, +0.6% time)
+timeout -k 10 900 python -u tools/ab_driver.py 4 --pause 8 $R/libdspbench.so $R/build/magst/libdspbench.so > $o/ab_driver_magst.txt 2>&1 || { echo "ab rc=$?"; tail -20 $o/ab_driver_magst.txt; exit 1; }
+tail -2 $o/ab_driver_magst.txt
