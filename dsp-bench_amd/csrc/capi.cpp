@@ -576,10 +576,26 @@ static int plugin_map(const dsp_plugin *p, uint32_t B, int dev, hipStream_t s, S
     }
 }
 
+// whether any input row [in[c], in[c] + L) overlaps any output row [out[c'], out[c'] + Lr)
+static bool rows_overlap(const float *const *in, uint32_t in_ch, uint64_t L, const float *const *out, uint32_t C,
+                         uint64_t Lr) {
+    for (uint32_t a = 0; a < in_ch; ++a)
+        for (uint32_t b = 0; b < C; ++b) {
+            const uintptr_t i0 = reinterpret_cast<uintptr_t>(in[a]), o0 = reinterpret_cast<uintptr_t>(out[b]);
+            if (L && Lr && i0 < o0 + 4 * Lr && o0 < i0 + 4 * L) return true;
+        }
+    return false;
+}
+
 // A GENERIC plugin with a known block class (module.h dsp_module_block_class)
-// runs as that map: its own callback's block as a table, or its gain
-static int specialize_generic(SampleMap *m, uint32_t C, uint32_t B, hipStream_t s, const dsp_exec *ex) {
+// runs as that map: its own callback's block as a table, or its gain.
+// in_place: the call renders over its own input; with DSP_EXEC_VERIFY_CLASS
+// the callback then runs on every block, since the check needs the input
+// after the render (and a re-render would need it whole)
+static int specialize_generic(SampleMap *m, uint32_t C, uint32_t B, hipStream_t s, const dsp_exec *ex,
+                              bool in_place) {
     if (m->kind != MapKind::Generic || (ex && (ex->flags & DSP_EXEC_NO_SPECIALIZE))) return DSP_OK;
+    if (in_place && ex && (ex->flags & DSP_EXEC_VERIFY_CLASS)) return DSP_OK;
     ModuleSpec sp;
     int st = module_specialize((::dsp_module *)m->module, m->gparams, m->gparams_size, C, B, m->sr, s, &sp);
     if (st) return st;
@@ -1009,7 +1025,8 @@ int dsp_render_offline(const float *const *in, uint32_t in_channels, uint64_t L,
     int st = plugin_map(plugin, B, g.dev, s, &map, sr, ex ? ex->flags : 0);
     if (st) return st;
     const SampleMap orig = map;
-    if ((st = specialize_generic(&map, C, B, s, ex))) return st;
+    if ((st = specialize_generic(&map, C, B, s, ex, rows_overlap(din.data(), in_channels, L, dout.data(), C, Lr))))
+        return st;
     TimedLaunch tl{};
     if ((st = timing_begin(s, &tl))) return st;
     st = render_device(din.data(), in_channels, L, dout.data(), C, B, map, 0, goff_of(ex), s);
@@ -1062,7 +1079,7 @@ int dsp_render_loop(const float *const *in, uint32_t in_channels, uint64_t L, ui
     SampleMap map;
     int st = plugin_map(plugin, B, g.dev, s, &map, sr, ex ? ex->flags : 0);
     if (st) return st;
-    if ((st = specialize_generic(&map, C, B, s, ex))) return st;
+    if ((st = specialize_generic(&map, C, B, s, ex, false))) return st;
     if ((st = ensure_ramp_table(map, s))) return st;
     const uint32_t in_ch = std::min(in_channels, C);  // channels_to_write (audio.cpp:66)
     auto wrap = [&](const float *const *src, float *const *dst, uint32_t nc, const SampleMap &m) -> int {
@@ -1185,7 +1202,8 @@ int dsp_render_stft(const float *const *in, uint32_t in_channels, uint64_t L,
     SampleMap map;
     if ((st = plugin_map(plugin, B, g.dev, s, &map, sr, ex ? ex->flags : 0))) return st;
     const SampleMap orig = map;
-    if ((st = specialize_generic(&map, C, B, s, ex))) return st;
+    if ((st = specialize_generic(&map, C, B, s, ex, rows_overlap(din.data(), in_channels, L, dout.data(), C, Lr))))
+        return st;
     const uint64_t goff = goff_of(ex);
     set_result(ex, orig.kind == MapKind::Generic && map.kind != MapKind::Generic ? DSP_RESULT_CLASS : 0u);
 

@@ -102,7 +102,10 @@ typedef struct dsp_plugin {
                                       call's own input and compare with the rendered rows bit for
                                       bit; on a mismatch render the call again with the callback on
                                       every block.  Reported through dsp_exec.result.  Costs a
-                                      stream synchronisation (dsp_render_offline / dsp_render_stft) */
+                                      stream synchronisation (dsp_render_offline / dsp_render_stft).
+                                      A call whose output rows overlap its input rows (in place)
+                                      runs the callback on every block instead: the check and a
+                                      re-render need the input after the render */
 /* the flags that choose how a call computes (not where its buffers live):
  * the chunked and sharded drivers pass them on to every chunk */
 #define DSP_EXEC_METHOD_FLAGS (DSP_EXEC_FIR_DIRECT | DSP_EXEC_NO_SPECIALIZE | DSP_EXEC_VERIFY_CLASS)

@@ -261,6 +261,13 @@ def test_verify_class_reports_and_catches_a_wrong_class(torch_cuda):
     assert last_result() == L.DSP_RESULT_CLASS | L.DSP_RESULT_VERIFIED
     d.render_offline(x, 2, 512, 48000.0, gmod.plugin(gp, "gain_test"))
     assert last_result() == L.DSP_RESULT_CLASS  # not checked without the flag
+    # in place (out = the input rows): the check would need the input after
+    # the render, so a verified call runs the callback on every block
+    xi = torch.rand((2, 512 * 12), device="cuda") * 2 - 1
+    want_i = (xi * torch.tensor(struct.unpack("<f", gp[:4])[0], dtype=torch.float32)).cpu().numpy()
+    d.render_offline(xi, 2, 512, 48000.0, gmod.plugin(gp, "gain_test", verify=True), out=xi)
+    assert last_result() == 0
+    assert np.array_equal(xi.cpu().numpy(), want_i)
 
     src = open(os.path.join(PLUG, "gain_until_loud.cpp")).read()
     code = d.module.compile_source(src, "gain_until_loud.cpp")
