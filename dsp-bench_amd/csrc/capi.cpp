@@ -117,10 +117,6 @@ static int upload_table(void *dst, const void *src, size_t bytes) {
     return DSP_OK;
 }
 
-#ifndef DSPB_FIR_DIF2
-#define DSPB_FIR_DIF2 0  // 1: FIR channel pairs on fir_dif2_kernel (A/B)
-#endif
-
 static int get_tw(int dev, hipStream_t s, const v2f **out) {
     std::lock_guard<std::mutex> lk(g_mu);
     DeviceRes &r = g_res[dev];
@@ -419,24 +415,6 @@ static void pair_table(const float *taps, uint32_t T, float *out) {
         }
 }
 
-// the 8192-point tables of fir_dif2_kernel: H = FFT_8192(taps) / 8192, the
-// even bins (wave 0) then the odd bins (wave 1), each as float4 [q][lane] =
-// (Re H[2k], Re H[2k'], Im H[2k], Im H[2k']) (+1 for the odd table),
-// k = l + 64 q, k' = k + 2048: the pairing of the 4096-point packed combine
-static void dif2_table(const float *taps, uint32_t T, float *out) {
-    std::vector<double> re, im;
-    taps_spectrum(taps, T, 8192, re, im);
-    const double sc = 1.0 / 8192.0;
-    for (int odd = 0; odd < 2; ++odd)
-        for (int q = 0; q < 32; ++q)
-            for (int l = 0; l < 64; ++l) {
-                const int k0 = 2 * (l + 64 * q) + odd, k1 = 2 * (l + 64 * q + 2048) + odd;
-                float *o = out + 8192 * odd + 4 * (64 * q + l);
-                o[0] = (float)(re[k0] * sc); o[1] = (float)(re[k1] * sc);
-                o[2] = (float)(im[k0] * sc); o[3] = (float)(im[k1] * sc);
-            }
-}
-
 // IR_test (build/IR_test.cpp:47-58) runs `gain -= step` in double from the
 // float parameters.  The sequence is often exact -- every partial result a
 // double -- and then table[i] = (float)(gain - i step) is one f64 FMA, with
@@ -531,13 +509,11 @@ static int plugin_map(const dsp_plugin *p, uint32_t B, int dev, hipStream_t s, S
             if (!ft) {
                 if (int st = refuse_capture(s, "a FIR filter's device taps")) return st;
                 // [taps, T8][8192-point table, 8194 (+ 2 pad)][4096-point pair table, 8192]
-                // [8192-point even / odd bin tables, 2 x 8192]
-                std::vector<float> h(T8 + 8196 + 8192 + 16384, 0.f);
+                std::vector<float> h(T8 + 8196 + 8192, 0.f);
                 std::memcpy(h.data(), key.data(), 4 * (size_t)T);
                 if (T <= 1025) {
                     ols_table(h.data(), T, h.data() + T8);
                     pair_table(h.data(), T, h.data() + T8 + 8196);
-                    dif2_table(h.data(), T, h.data() + T8 + 8196 + 8192);
                 }
                 float *d = nullptr;
                 DSPB_HIP(hipMalloc(&d, sizeof(float) * h.size()));
@@ -559,7 +535,6 @@ static int plugin_map(const dsp_plugin *p, uint32_t B, int dev, hipStream_t s, S
         m->ntaps = T;
         m->olsH = ft->dev + T8;
         m->pairH = ft->dev + T8 + 8196;  // 16-byte aligned: T8 and 8196 are multiples of 4
-        m->difH = ft->dev + T8 + 8196 + 8192;
         m->olsH2048[0] = ft->h2048r;
         m->olsH2048[1] = ft->h2048i;
         return DSP_OK;
@@ -744,16 +719,9 @@ static int render_device(const float *const *in, uint32_t in_ch, uint64_t L, flo
                     A.L = L;
                     A.Ly = end;
                     A.tw = tw;
-#if DSPB_FIR_DIF2
-                    // 8192-point pair frames over two waves (fir_dif2_kernel)
-                    A.F = (end + kDif2HopHost - 1) / kDif2HopHost;
-                    A.H = map.difH;
-                    if ((st = launch_fir_dif2(A, np, s))) return st;
-#else
                     A.F = (end + kPairHop - 1) / kPairHop;
                     A.H = map.pairH;
                     if ((st = launch_fir_pair(A, np, s))) return st;
-#endif
                 }
                 if (cn & 1) {
                     const uint32_t c = c0 + cn - 1;

@@ -36,7 +36,6 @@ struct SampleMap {
     const float *olsH;   // Fir: FFT(taps)/16384 in fir_fft.hip's lane-major pair layout
     float olsH2048[2];   // Fir: H[2048]/16384
     const float *pairH;  // Fir: FFT_4096(taps)/4096 in fir_pair_kernel's layout (fir_fft.hip)
-    const float *difH;   // Fir: FFT_8192(taps)/8192, even bins then odd bins (fir_dif2_kernel)
     void *module;        // Generic: the dsp_module running the plugin's own audio_callback
     const void *gparams; // Generic: host Parameters blob
     uint32_t gparams_size;

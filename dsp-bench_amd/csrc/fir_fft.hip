@@ -388,217 +388,6 @@ int launch_fir_pair(const FirFftArgs &A, uint32_t C, hipStream_t s) {
     return DSP_OK;
 }
 
-// ---------------------------------------------------------------------------
-// 8192-point channel-pair frames over the two waves of a workgroup
-// (fir_dif2_kernel), decimated in frequency across the waves.  Frame f
-// covers input [f P - 1024, f P + 7168), P = kDif2Hop = 7168, u = x0 + i x1,
-// and owns outputs [f P, (f + 1) P):
-//
-//   wave 0   a[m] = u[m] + u[m + 4096]            (m = l + 64 r)
-//            X[2k] = DFT4096(a)[k],  Y_e = X[2k] H[2k]
-//            ye = IDFT4096(Y_e)                    (unnormalised)
-//   wave 1   b[m] = (u[m] - u[m + 4096]) W8192^m
-//            X[2k+1] = DFT4096(b)[k], Y_o = X[2k+1] H[2k+1]
-//            t = W8192^-n IDFT4096(Y_o)[n]
-//   y[n] = ye[n] + t[n], y[n + 4096] = ye[n] - t[n]  (H = FFT_8192(taps) / 8192)
-//
-// Each wave loads the whole frame (the halves' sum or difference: the partner
-// reads the same lines, from L2) and runs the pair kernel's two 4096-point
-// transforms; wave 1 adds a twiddle multiply each way.  One exchange of the
-// outputs through the waves' own transpose tiles, in two passes: wave 0 stores
-// y[n], n in [1024, 4096), wave 1 y[n + 4096], n in [0, 4096) -- 7,168 outputs
-// per channel per workgroup where a one-wave 4096-point frame gives 3,072.
-// tools/ols2w_model.py's checks cover the same algebra (the DIT form); the
-// GPU tests compare this kernel with np.convolve (tests/test_gpu_fir.py).
-constexpr uint32_t kDif2Hop = 7168;
-#ifndef DSPB_DIF2_LB
-#define DSPB_DIF2_LB 16  // frame-load batch (columns pairs j per batch)
-#endif
-#ifndef DSPB_DIF2_HB
-#define DSPB_DIF2_HB 16  // H-load batch (q per batch)
-#endif
-
-// one pass of the output combine: ODD wave 1 (y[n + 4096] = ye - t, ye read
-// from the peer), else wave 0 (y[n] = ye + t for q' >= 16); stores at
-// p[64 q'] (both channels: Re, Im; a channel the file lacks: zeros)
-template <bool ODD>
-__device__ __forceinline__ void dif2_emit(const cx2 (&Y2)[32], int pass, const v2f *pw, uint32_t lane, float *p0,
-                                          float *p1, bool two, bool have1, bool full, int64_t lim) {
-#pragma unroll
-    for (int q = 0; q < 32; ++q) {
-        if (q % 8 == 0) __builtin_amdgcn_sched_barrier(0);
-        const int qp = 32 * pass + q;
-        if (!ODD && qp < 16) continue;
-        const v2f m = pass ? v2f{Y2[q].r.y, Y2[q].i.y} : v2f{Y2[q].r.x, Y2[q].i.x};
-        const v2f pv = pw[64u * (uint32_t)q + lane];
-        const v2f y = ODD ? pv - m : m + pv;
-        const float yi = have1 ? y.y : 0.f;
-        if (full) {
-            __builtin_nontemporal_store(y.x, p0 + 64 * qp);
-            if (two) __builtin_nontemporal_store(yi, p1 + 64 * qp);
-        } else if (64 * qp < lim) {
-            p0[64 * qp] = y.x;
-            if (two) p1[64 * qp] = yi;
-        }
-    }
-}
-
-template <bool EDGE>
-__device__ __forceinline__ void fir_dif2_frame(const FirFftArgs &A, uint64_t f, uint32_t c0, float *own,
-                                               const float *peer, bool odd, uint32_t lane) {
-    const int64_t fs = (int64_t)(f * kDif2Hop) - (int64_t)kOlsHist;
-    const float *x0 = c0 < A.in_ch ? A.in.p[c0] : nullptr;
-    const float *x1 = c0 + 1 < A.in_ch ? A.in.p[c0 + 1] : nullptr;
-    const v2f wl2 = A.tw[lane];  // W8192^l
-    const cx wl = cx{wl2.x, wl2.y};
-
-    cx tlo[8];
-    cx2 thp[4];
-    load_stage_tw(A.tw, lane, 0u, tlo, thp);
-
-    // ---- a or b: P[j] = (v[2j], v[2j+1]), v[r] for m = l + 64 r -------------
-    cx2 P[32];
-#pragma unroll
-    for (int j = 0; j < 32; ++j) {
-        // (two batches: the loads of the whole frame in flight at once
-        // would hold 256 VGPRs before the sums halve them)
-        if (j % DSPB_DIF2_LB == 0) __builtin_amdgcn_sched_barrier(0);
-        cx2 lo, hi;  // u[m], u[m + 4096] for r = 2j, 2j + 1
-        if constexpr (!EDGE) {
-            const float *b0 = x0 + fs, *b1 = x1 + fs;
-            const uint32_t o = lane + 128u * (uint32_t)j;
-            lo = cx2{v2f{b0[o], b0[o + 64u]}, v2f{b1[o], b1[o + 64u]}};
-            hi = cx2{v2f{b0[o + 4096u], b0[o + 4160u]}, v2f{b1[o + 4096u], b1[o + 4160u]}};
-        } else {
-            float v[8];
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {  // (channel, half, r parity)
-                const float *x = (e & 4) ? x1 : x0;
-                const int64_t s = fs + (int64_t)lane + 128 * j + ((e & 2) ? 4096 : 0) + ((e & 1) ? 64 : 0);
-                v[e] = (x && s >= 0 && (uint64_t)s < A.L) ? x[s] : 0.f;
-            }
-            lo = cx2{v2f{v[0], v[1]}, v2f{v[4], v[5]}};
-            hi = cx2{v2f{v[2], v[3]}, v2f{v[6], v[7]}};
-        }
-        if (!odd) {
-            P[j] = lo + hi;
-        } else {  // (u[m] - u[m + 4096]) W8192^(l + 64 r) = .. wl W128^r
-            const cx2 w = cmulb(wl, cx2{v2f{kW128_re[2 * j], kW128_re[2 * j + 1]},
-                                        v2f{kW128_im[2 * j], kW128_im[2 * j + 1]}});
-            P[j] = cmul2(lo - hi, w);
-        }
-    }
-
-    // ---- forward, times H (the wave's half of the 8192 bins), re-paired -----
-    const float4 *H4 = reinterpret_cast<const float4 *>(A.H) + (odd ? 2048u : 0u);
-    cx2 Q[32];
-    {
-        cx2 R[32], Y2[32];
-        fft4096_pk_front<false, false, false, true>(P, own, tlo, thp, lane, R);
-        combine64p(R, Y2);
-#pragma unroll
-        for (int q = 0; q < 32; ++q) {
-            // (batches of eight: all 32 loads hoisted would hold 128 VGPRs
-            // beside the spectrum's 128)
-            if (q % DSPB_DIF2_HB == 0) __builtin_amdgcn_sched_barrier(0);
-            const float4 h = H4[64u * (uint32_t)q + lane];
-            Y2[q] = cmul2(Y2[q], cx2{v2f{h.x, h.y}, v2f{h.z, h.w}});
-        }
-#pragma unroll
-        for (int j = 0; j < 32; ++j) {
-            const int r0 = 2 * j, r1 = 2 * j + 1;
-            const cx2 a = Y2[r0 & 31], b = Y2[r1 & 31];
-            if (r0 < 32) {
-                asm("v_pk_mov_b32 %0, %1, %2 op_sel:[0,0]" : "=v"(Q[j].r) : "v"(a.r), "v"(b.r));
-                asm("v_pk_mov_b32 %0, %1, %2 op_sel:[0,0]" : "=v"(Q[j].i) : "v"(a.i), "v"(b.i));
-            } else {
-                asm("v_pk_mov_b32 %0, %1, %2 op_sel:[1,1]" : "=v"(Q[j].r) : "v"(a.r), "v"(b.r));
-                asm("v_pk_mov_b32 %0, %1, %2 op_sel:[1,1]" : "=v"(Q[j].i) : "v"(a.i), "v"(b.i));
-            }
-        }
-    }
-    {
-        uint32_t salt = 0u;
-        asm volatile("" : "+s"(salt));
-        load_stage_tw(A.tw, lane, salt, tlo, thp);
-    }
-    // ---- inverse: Y2[q] = (U[l + 64 q], U[l + 64 (q + 32)]); wave 1 times
-    // W8192^-n = conj(wl) conj(W128^q) and, for n + 2048, i times that
-    cx2 Y2[32];
-    {
-        cx2 R[32];
-        fft4096_pk_front<true, false, false, true>(Q, own, tlo, thp, lane, R);
-        combine64p_dir<true>(R, Y2);
-    }
-    if (odd) {
-        const cx cw = cx{wl.r, -wl.i};
-#pragma unroll
-        for (int q = 0; q < 32; ++q) {
-            const cx2 w = cmulb(cw, cx2{v2f{kW128_re[q], kW128_im[q]}, v2f{-kW128_im[q], kW128_re[q]}});
-            Y2[q] = cmul2(Y2[q], w);
-        }
-    }
-
-    // ---- exchange through the tiles, two passes: element n = l + 64 q' at
-    // float2 [q][lane] of the writer's tile.  Pass 1: q' < 32 (the .x halves),
-    // pass 2: q' >= 32 (.y).  Wave 0 needs t for q' >= 16, wave 1 ye for all.
-    // Frame output o = n - 1024 (wave 0, n >= 1024) or n + 3072 (wave 1).
-    const uint32_t c1 = c0 + 1;
-    const bool two = c1 < A.nout;
-    const int64_t bofs = (int64_t)(f * kDif2Hop) + (int64_t)lane + (odd ? 3072 : -1024);
-    float *p0 = A.out.p[c0] + bofs;
-    float *p1 = (two ? A.out.p[c1] : A.out.p[c0]) + bofs;
-    const bool full = f * kDif2Hop + kDif2Hop <= A.Ly;
-    // (valid outputs of the last frame: o < lim, o = lane + 64 q' + base)
-    const int64_t lim = (int64_t)A.Ly - bofs;
-    v2f *ow = reinterpret_cast<v2f *>(own);
-    const v2f *pw = reinterpret_cast<const v2f *>(peer);
-#pragma unroll
-    for (int pass = 0; pass < 2; ++pass) {
-#pragma unroll
-        for (int q = 0; q < 32; ++q) {
-            const int qp = 32 * pass + q;
-            const v2f e = pass ? v2f{Y2[q].r.y, Y2[q].i.y} : v2f{Y2[q].r.x, Y2[q].i.x};
-            if (!odd || qp >= 16) ow[64u * (uint32_t)q + lane] = e;
-        }
-        __syncthreads();
-        if (odd) dif2_emit<true>(Y2, pass, pw, lane, p0, p1, two, x1 != nullptr, full, lim);
-        else dif2_emit<false>(Y2, pass, pw, lane, p0, p1, two, x1 != nullptr, full, lim);
-        if (pass == 0) __syncthreads();  // the peer has read this pass before the next overwrites it
-    }
-}
-
-// grid (frames, channel pairs), two waves per workgroup (one frame): LDS the
-// two 64 x 65 transpose tiles, reused for the exchange
-__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))) void fir_dif2_kernel(FirFftArgs A,
-                                                                                                 uint64_t fe) {
-    __shared__ __attribute__((aligned(16))) float lds_all[2][64 * 65];
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t c0 = 2u * blockIdx.y;
-    const uint64_t f = (uint64_t)xcd_remap(blockIdx.x, gridDim.x);
-    if (f >= A.F) return;  // (whole workgroup)
-    if (f == 0 || f >= fe || c0 + 1 >= A.in_ch)
-        fir_dif2_frame<true>(A, f, c0, lds_all[wave], lds_all[wave ^ 1u], wave != 0, lane);
-    else
-        fir_dif2_frame<false>(A, f, c0, lds_all[wave], lds_all[wave ^ 1u], wave != 0, lane);
-}
-
-int launch_fir_dif2(const FirFftArgs &A, uint32_t C, hipStream_t s) {
-    if (A.F == 0 || C == 0) return DSP_OK;
-    // interior frames: [1, fe) with (f P - 1024) + 8192 <= L
-    uint64_t fe = 1;
-    if (A.L + kOlsHist >= 8192u) fe = (A.L + kOlsHist - 8192u) / kDif2Hop + 1;
-    if (fe > A.F) fe = A.F;
-    if (fe < 1) fe = 1;
-    if (A.F > 0x7fffffffull) return DSP_ERR_INVALID;
-    FirFftArgs B = A;
-    B.nout = C;
-    hipLaunchKernelGGL(fir_dif2_kernel, dim3((uint32_t)A.F, (C + 1) / 2), dim3(128), 0, s, B, fe);
-    DSPB_HIP(hipGetLastError());
-    return DSP_OK;
-}
-
 int launch_fir_fft(const FirFftArgs &A, uint32_t C, hipStream_t s) {
     if (A.F == 0 || C == 0) return DSP_OK;
     const uint64_t fe = interior_end(A);

@@ -105,10 +105,6 @@ int launch_fir_fft(const FirFftArgs &A, uint32_t C, hipStream_t s);
 // (C even; F = ceil(Ly / kPairHop); H = SampleMap::pairH; h2048 unused)
 constexpr uint32_t kPairHop = 3072;
 int launch_fir_pair(const FirFftArgs &A, uint32_t C, hipStream_t s);
-// channel pairs as 8192-point frames over two waves, hop 7168 (fir_dif2_kernel:
-// F = ceil(Ly / kDif2Hop); H = SampleMap::difH)
-constexpr uint32_t kDif2HopHost = 7168;
-int launch_fir_dif2(const FirFftArgs &A, uint32_t C, hipStream_t s);
 int launch_fir(const float *x, uint64_t L, float *y, uint64_t Ly, const float *h8, uint32_t T8,
                bool y_aligned16, hipStream_t s);
 int launch_minmax(const float *x, uint64_t n, uint32_t P, float *vmax, float *vmin, hipStream_t s);

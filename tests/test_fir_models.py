@@ -29,7 +29,8 @@ def test_two_wave_pair_frame_model():
 
 
 def test_dif_two_wave_frame_model():
-    """fir_dif2_kernel's algebra and H table layout (tools/olsdif_model.py):
+    """The algebra and H table layout of round 4's two-wave FIR attempt
+    (fir_dif2_kernel, removed: 62% slower; tools/olsdif_model.py):
     decimation in frequency over the two waves, one exchange of outputs."""
     m = _load("olsdif_model")
     rng = np.random.default_rng(5)
