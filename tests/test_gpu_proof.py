@@ -76,6 +76,8 @@ def semantics(name, xb, params, state=None, call0=0):
             y[1] = xb[1] * F(right)
     elif name == "gain_twice":
         y = ((xb * g).astype(F) * g).astype(F)
+    elif name == "half_block":
+        y[:, :, : B // 2] = (xb[:, :, : B // 2] * g).astype(F)
     elif name == "state_shaper":
         a, b = F(-g / F(3)), F(F(1) + g)
         t = ((a * xb).astype(F) * xb).astype(F) * xb
@@ -94,6 +96,7 @@ EXPECT = {
     "fade_in": ("callback", True),
     "balance": ("callback", True),
     "gain_twice": ("callback", True),
+    "half_block": ("callback", True),
     "state_shaper": ("callback", True),
     "dc_level": ("table", True),
 }
@@ -180,6 +183,23 @@ def test_gain_twice_is_a_gain_only_when_g_squared_is_g(torch_cuda):
         assert mod.block_class(params, 2, 512, 48000.0)[0] == cls, g
         got = d.render_offline(x, 2, 512, 48000.0, mod.plugin(params, "gain_twice")).cpu().numpy()
         assert np.array_equal(got, semantics("gain_twice", blocks(x.cpu().numpy(), 2, 512), params))
+
+
+def test_half_block_gain_is_refused_unless_it_is_the_identity(torch_cuda):
+    """half_block.cpp stores x * g (the IR's gain form) on the first half of
+    each block only: the probe of ones sees 1 in the second half, so the
+    class is refused for g = 0.5 and g = 0 and taken for g = 1, where the
+    callback is the identity."""
+    torch = torch_cuda
+    mod = load("half_block")
+    mod.initialize_state(mod.default_parameters(), 2, 48000.0)
+    assert mod.facts["gain_form"]
+    x = torch.from_numpy(make_input(512 * 9 + 5)).cuda()
+    for g, cls in ((0.5, "callback"), (0.0, "callback"), (1.0, "gain")):
+        params = struct.pack("<f", g)
+        assert mod.block_class(params, 2, 512, 48000.0)[0] == cls, g
+        got = d.render_offline(x, 2, 512, 48000.0, mod.plugin(params, "half_block")).cpu().numpy()
+        assert np.array_equal(got, semantics("half_block", blocks(x.cpu().numpy(), 2, 512), params)), g
 
 
 def test_static_gain_plugin_is_a_proven_gain(torch_cuda, oracle):

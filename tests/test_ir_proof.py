@@ -66,6 +66,7 @@ TEST = {
     "fade_in.cpp": (True, True, False, False, False),            # g varies with the position
     "balance.cpp": (True, True, False, False, False),            # two different gains
     "gain_twice.cpp": (True, True, False, False, True),          # x * g twice: the probe of ones refuses it
+    "half_block.cpp": (True, True, False, False, True),          # x * g on half the block: the probe refuses it
     "state_shaper.cpp": (True, True, False, False, False),       # State read only: parallel, no class
     "dc_level.cpp": (True, False, False, False, False),          # a table (set_array)
 }
@@ -102,20 +103,70 @@ SNIPPETS = {
     # a double-precision product rounded back: the optimiser proves it is the
     # float product (24 x 24 bits fit f64 exactly, one rounding), so a gain
     "f64": ("", "for (u32 s = 0; s < B; ++s) out[0][s] = (float)((double)out[0][s] * (double)p.g);", (True, True)),
+    # products stored at another element's address
+    "swap_channels": ("", "for (u32 s = 0; s < B; ++s) { float t = out[0][s]; out[0][s] = out[1][s] * p.g; "
+                          "out[1][s] = t * p.g; }", (True, False)),
+    "reverse": ("", "for (u32 s = 0; s < B / 2; ++s) { float t = out[0][s]; out[0][s] = out[0][B - 1 - s] * p.g; "
+                    "out[0][B - 1 - s] = t * p.g; }", (True, False)),
+    "sum_into_first": ("", "float acc = 0.0f; for (u32 s = 0; s < B; ++s) acc += out[0][s]; out[0][0] = acc * p.g;",
+                       (True, False)),
+    # a select / a conversion / a libm call on the sample
+    "nan_select": ("", "for (u32 s = 0; s < B; ++s) out[0][s] = (out[0][s] != out[0][s]) ? 0.0f : out[0][s] * p.g;",
+                   (True, False)),
+    "int_roundtrip": ("", "for (u32 s = 0; s < B; ++s) out[0][s] = (float)(int)(out[0][s] * p.g);", (True, False)),
+    "sin_of_sample": ("", "for (u32 s = 0; s < B; ++s) out[0][s] = sinf(out[0][s]) * p.g;", (True, False)),
+    "sample_as_index": ("__device__ const float lut[4] = {0.1f, 0.2f, 0.3f, 0.4f}; ",
+                        "for (u32 s = 0; s < B; ++s) out[0][s] = lut[((unsigned)out[0][s]) & 3u] * p.g;",
+                        (True, False)),
+    # a gain that is not one value read from Parameters / State or a constant
+    "sr_dependent_gain": ("", "float g = sr > 44100.0f ? p.g : 0.5f * p.g; for (u32 c = 0; c < C; ++c) "
+                              "for (u32 s = 0; s < B; ++s) out[c][s] *= g;", (True, False)),
+    "gain_by_channel": ("", "for (u32 c = 0; c < C; ++c) for (u32 s = 0; s < B; ++s) "
+                            "out[c][s] *= (c ? p.g : 1.0f);", (True, False)),
+    "block_length_gain": ("", "for (u32 c = 0; c < C; ++c) for (u32 s = 0; s < B; ++s) out[c][s] *= (float)B;",
+                          (True, False)),
+    # writes outside the model: Parameters, the pointer table, inline asm
+    "store_params": ("", "const_cast<Parameters &>(p).g = 1.0f; out[0][0] *= p.g;", (False, False)),
+    "pointer_table_write": ("", "out[0] = out[1]; for (u32 s = 0; s < B; ++s) out[0][s] *= p.g;", (False, False)),
+    "inline_asm": ("", "float v = out[0][0]; asm volatile(\"v_mov_b32 %0, %1\" : \"=v\"(v) : \"v\"(v)); "
+                       "out[0][0] = v * p.g;", (False, False)),
 }
+
+# the gain forms that are gains: a constant, and the sample rate argument
+GAIN_SOURCES = {
+    "const_gain": ("for (u32 c = 0; c < C; ++c) for (u32 s = 0; s < B; ++s) out[c][s] *= 0.5f;", ("K", 0.5)),
+    "sr_gain": ("for (u32 c = 0; c < C; ++c) for (u32 s = 0; s < B; ++s) out[c][s] *= sr;", ("R", None)),
+    "param_gain": ("for (u32 c = 0; c < C; ++c) for (u32 s = 0; s < B; ++s) out[c][s] *= p.g;", ("P", None)),
+}
+
+
+def snippet(pre, body):
+    return ("#include \"plugin_header.h\"\n" + pre +
+            "struct Parameters { FLOAT_PARAM(0.0f, 1.0f) g; };\nstruct State {};\n"
+            "Parameters default_parameters() { Parameters p = {0.5f}; return p; }\n"
+            "State initialize_state(const Parameters &p, const unsigned C, const float sr, void *ctx) "
+            "{ State s; return s; }\n"
+            "void audio_callback(const Parameters &p, State &st, float **out, const u32 C, const u32 B, "
+            "const real32 sr) {\n" + body + "\n}\n")
+
+
+@pytest.mark.parametrize("case", sorted(GAIN_SOURCES))
+def test_gain_sources(case):
+    """Where the host reads g: a constant (K, its value), the sample-rate
+    argument (R), a Parameters field (P, its byte offset)."""
+    body, (src, k) = GAIN_SOURCES[case]
+    f = dm.analyze_source(snippet("", body))
+    assert f["analyzed"] and f["gain_form"] and f["gain_source"] == src, f
+    if k is not None:
+        assert f["gain_constant"] == k
+    if src == "P":
+        assert f["gain_offset"] == 0
 
 
 @pytest.mark.parametrize("case", sorted(SNIPPETS))
 def test_constructs_outside_the_model(case):
     pre, body, (want_analyzed, want_gain) = SNIPPETS[case]
-    src = ("#include \"plugin_header.h\"\n" + pre +
-           "struct Parameters { FLOAT_PARAM(0.0f, 1.0f) g; };\nstruct State {};\n"
-           "Parameters default_parameters() { Parameters p = {0.5f}; return p; }\n"
-           "State initialize_state(const Parameters &p, const unsigned C, const float sr, void *ctx) "
-           "{ State s; return s; }\n"
-           "void audio_callback(const Parameters &p, State &st, float **out, const u32 C, const u32 B, "
-           "const real32 sr) {\n" + body + "\n}\n")
-    f = dm.analyze_source(src)
+    f = dm.analyze_source(snippet(pre, body))
     if want_analyzed is not None:
         assert f["analyzed"] == want_analyzed, f
     if want_gain is not None:
