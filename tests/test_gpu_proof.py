@@ -202,6 +202,41 @@ def test_half_block_gain_is_refused_unless_it_is_the_identity(torch_cuda):
         assert np.array_equal(got, semantics("half_block", blocks(x.cpu().numpy(), 2, 512), params)), g
 
 
+def test_subnormals_are_kept_as_on_the_audio_thread(torch_cuda):
+    """The reference's audio thread computes with IEEE subnormals: FTZ/DAZ are
+    set by ipp_initialize on the thread that calls it, the main thread
+    (dsp.cpp:141-142, main.cpp:235,247), not on the WASAPI thread that runs the
+    callback.  Every GPU kernel keeps f32 subnormals (.amdhsa_float_denorm_mode_32
+    3), so gain_test.cpp as its gain class and with its callback on every block
+    render the same bits, the exact products: subnormal x = k 2^-149 (k even)
+    times 0.5 is (k/2) 2^-149, times 2^20 is the normal k 2^-129."""
+    mods = os.path.join(os.path.dirname(HERE), "dsp-bench_amd", "modules")
+    if not os.path.exists(os.path.join(mods, "mod_gain_test.co")):
+        pytest.skip("modules not built")
+    torch = torch_cuda
+    with open(os.path.join(mods, "mod_gain_test.co"), "rb") as f:
+        mod = d.module.Module(f.read())
+    mod.initialize_state(mod.default_parameters(), 2, 48000.0)
+    rng = np.random.default_rng(11)
+    n = 512 * 8
+    # (k >= 16: the x 2^20 products are normal, so building the expected
+    # values on the host needs no subnormal arithmetic)
+    k = (rng.integers(8, 1 << 22, (2, n), dtype=np.uint32) * 2).astype(np.uint32)
+    sign = (rng.integers(0, 2, (2, n), dtype=np.uint32) << 31).astype(np.uint32)
+    xg = torch.from_numpy((k | sign).view(np.float32).copy()).cuda()
+    for g in (0.5, 2.0 ** 20):
+        params = struct.pack("<f", g)
+        assert mod.block_class(params, 2, 512, 48000.0)[0] == "gain"
+        a = d.render_offline(xg, 2, 512, 48000.0, mod.plugin(params, "gain_test")).cpu().numpy()
+        b = d.render_offline(xg, 2, 512, 48000.0, mod.plugin(params, "gain_test", specialize=False)).cpu().numpy()
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), g
+        if g == 0.5:  # (k / 2) 2^-149, sign kept: exact
+            assert np.array_equal(a.view(np.uint32), (k >> 1) | sign)
+        else:  # k 2^-129
+            want = (np.ldexp(k.astype(np.float64), -129) * np.where(sign != 0, -1.0, 1.0)).astype(np.float32)
+            assert np.array_equal(a.view(np.uint32), want.view(np.uint32))
+
+
 def test_static_gain_plugin_is_a_proven_gain(torch_cuda, oracle):
     """test/static_gain_plugin.cpp (State {gain} set by initialize_state, only
     read by the callback): parallel blocks, the gain class with g = state.gain
