@@ -194,15 +194,17 @@ def pmc_traffic(workload: str, alg_bytes: float):
     # instantiation (ch96k runs the headline's kernel on as many frames)
     own = sorted(glob.glob(os.path.join(REPO, "profiles", f"r*_pmc_{workload}.json")), reverse=True)
     rest = sorted(set(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_*.json"))) - set(own), reverse=True)
+    other = None
     for path in own + rest:
         doc = json.load(open(path))
         for name, m in doc.get("kernels", {}).items():
-            if name.endswith(inst) and "hbm_bytes" in m:
+            # "<instantiation> [grid G]": one entry per launch size (tools/pmc_summary.py)
+            if name.split(" [grid ")[0].endswith(inst) and "hbm_bytes" in m:
                 t = float(m["hbm_bytes"])
-                if not alg_bytes or not 0.9 <= t / alg_bytes <= 1.5:
-                    return None, f"{os.path.relpath(path, REPO)} (a launch of another size: not used)", inst
-                return t, os.path.relpath(path, REPO), inst
-    return None, None, inst
+                if alg_bytes and 0.9 <= t / alg_bytes <= 1.5:
+                    return t, os.path.relpath(path, REPO), inst
+                other = other or f"{os.path.relpath(path, REPO)} (a launch of another size: not used)"
+    return None, other, inst
 
 
 def cpu_baseline_generic(seconds_budget: float, pname: str = "gain_test"):

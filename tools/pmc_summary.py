@@ -3,7 +3,12 @@ per-wave / derived figures (quad-cycle counters -> cycles).
   usage: python tools/pmc_summary.py <pmc dir> [--json out.json]
 --json writes {kernel: {counter means..., "hbm_bytes", "fetch_bytes",
 "write_bytes"}} with the gfx950 corrections of MI355X_MICROARCH.md (HBM):
-FETCH_SIZE (KiB) x 2, WRITE_SIZE (KiB) as is."""
+FETCH_SIZE (KiB) x 2, WRITE_SIZE (KiB) as is.
+
+Dispatches of one instantiation with different grid sizes (a bench line's
+full-size launches beside the end-to-end pass's chunk launches) are separate
+entries, keyed "<instantiation> [grid G]"; each entry also records the
+dispatch ids it averages (first, last, count)."""
 import collections
 import csv
 import glob
@@ -29,14 +34,18 @@ def kname(n):
     return n
 
 agg = collections.defaultdict(lambda: collections.defaultdict(list))
+ids = collections.defaultdict(list)
 for p in sorted(glob.glob(f"{root}/p*/run_counter_collection.csv")):
     for r in csv.DictReader(open(p)):
-        agg[kname(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        key = f"{kname(r['Kernel_Name'])} [grid {r.get('Grid_Size', '?')}]"
+        agg[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        ids[key].append(int(r["Dispatch_Id"]))
 for k, d in agg.items():
     m = {c: sum(v) / len(v) for c, v in d.items()}
+    m["dispatch_ids"] = [min(ids[k]), max(ids[k]), len(set(ids[k]))]
     print(k)
     for c, v in sorted(m.items()):
-        print(f"   {c:26s} {v:.4g}")
+        print(f"   {c:26s} {v:.4g}" if not isinstance(v, list) else f"   {c:26s} {v}")
     w = m.get("SQ_WAVES")
     if w:
         for c in ("SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY",
