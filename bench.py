@@ -74,7 +74,8 @@ def parse():
                     help="fir1024: 0 auto (overlap-save), 1 direct form, 2 overlap-save")
     ap.add_argument("--workload", default="headline",
                     choices=["headline", "stft96k", "ch96k", "gain10min", "fir1024", "wav16", "wav24", "ir",
-                             "generic", "generic_stft", "gain_stft", "wav16enc", "wav24enc"],
+                             "generic", "generic_stft", "gain_stft", "wav16enc", "wav24enc", "biquad", "biquad_src",
+                             "sine_src"],
                     help="headline = IR_test + STFT 48 kHz (the metric); stft96k = BASELINE cfg 4 "
                          "(STFT of 1 h stereo 96 kHz from HBM); gain10min = cfg 2 render; "
                          "wav16 / wav24 = GPU decode of a 1 h stereo int16 / int24 WAV payload; "
@@ -84,7 +85,13 @@ def parse():
                          "generic_stft = the same + the 8192-pt STFT (render, then the STFT, one stream); "
                          "gain_stft = gain_test render fused with the STFT (the input is read: the headline "
                          "shape with an input-dependent plugin); wav16enc / wav24enc = GPU encode of 1 h of "
-                         "planar stereo into an interleaved int16 / int24 WAV payload")
+                         "planar stereo into an interleaved int16 / int24 WAV payload; biquad = DSP_PLUGIN_BIQUAD "
+                         "(plugins/biquad.cpp's low-pass as a block-parallel state scan, 1 h stereo); biquad_src / "
+                         "sine_src = plugins/biquad.cpp / the reference's sine_test.cpp compiled unchanged, the "
+                         "serial stateful chain (default 1 min of stereo)")
+    ap.add_argument("--sections", type=int, default=1, choices=[1, 2, 3, 4],
+                    help="biquad: sections in the cascade (1 = plugins/biquad.cpp's low-pass; more add RBJ "
+                         "peaking / high-pass sections)")
     ap.add_argument("--plugin", default=None, choices=["gain_test", "IR_test", "static_gain_plugin"],
                     help="generic / generic_stft: the reference plugin source (default gain_test / IR_test; "
                          "static_gain_plugin = test/static_gain_plugin.cpp, a State the callback only reads)")
@@ -207,15 +214,29 @@ def pmc_traffic(workload: str, alg_bytes: float):
     return None, other, inst
 
 
-def cpu_baseline_generic(seconds_budget: float, pname: str = "gain_test"):
+def rbj_section(kind: str, fc: float, q: float, gain_db: float = 0.0, sr: float = 48000.0):
+    """An RBJ-cookbook biquad section (b0, b1, b2, a1, a2) / a0, float64 then
+    float32: "lp" low-pass, "hp" high-pass, "peq" peaking EQ."""
+    import math
+    w0 = 2 * math.pi * fc / sr
+    al, c = math.sin(w0) / (2 * q), math.cos(w0)
+    A = 10 ** (gain_db / 40)
+    b, a = {"lp": ([(1 - c) / 2, 1 - c, (1 - c) / 2], [1 + al, -2 * c, 1 - al]),
+            "hp": ([(1 + c) / 2, -(1 + c), (1 + c) / 2], [1 + al, -2 * c, 1 - al]),
+            "peq": ([1 + al * A, -2 * c, 1 - al * A], [1 + al / A, -2 * c, 1 - al / A])}[kind]
+    return [b[0] / a[0], b[1] / a[0], b[2] / a[0], a[1] / a[0], a[2] / a[0]]
+
+
+def cpu_baseline_generic(seconds_budget: float, pname: str = "gain_test", prefix: str = "libref_"):
     """The reference's own plugin source (gain_test.cpp by default), compiled
-    with the JIT's flags (oracle/_ref/libref_<pname>.so), called block by
+    with the JIT's flags (oracle/_ref/libref_<pname>.so; prefix "libplug_":
+    one of this repository's plugins built the same way), called block by
     block by the oracle's render loop on one host core: chunks of 60 s
     stereo until the budget."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import numpy as np
     import oracle as o
-    ref = o.RefPlugin(pname, CH, float(SR))
+    ref = o.RefPlugin(pname, CH, float(SR), prefix=prefix)
     chunk = SR * 60
     x = np.random.default_rng(1).uniform(-1, 1, (CH, chunk)).astype(np.float32)
     done = 0
@@ -226,9 +247,11 @@ def cpu_baseline_generic(seconds_budget: float, pname: str = "gain_test"):
         el = time.perf_counter() - t0
         if el >= seconds_budget:
             break
-    return {"value": done / el / 1e6, "unit": "Msamples/s", "cores": 1, "kind": "reference",
-            "sample": f"{done // CH / SR:.0f} s of 48 kHz stereo through the reference's {pname}.cpp "
-                      "(compiled from source, -Ofast) and the oracle's render_audio loop, 1 thread"}
+    own = prefix == "libplug_"
+    return {"value": done / el / 1e6, "unit": "Msamples/s", "cores": 1, "kind": "port" if own else "reference",
+            "sample": f"{done // CH / SR:.0f} s of 48 kHz stereo through "
+                      f"{'plugins/' + pname + '.cpp built with the reference JIT flags (-Ofast, oracle/Makefile)' if own else 'the reference' + chr(39) + 's ' + pname + '.cpp (compiled from source, -Ofast)'}"
+                      " and the oracle's render_audio loop (B = 512), 1 thread"}
 
 
 def _cpu_threads():
@@ -428,6 +451,8 @@ def main():
     # cfg 5 shards by channel (one 96 kHz channel per GPU), the rest by time
     CH = 1 if wl == "ch96k" else globals()["CH"]
     minutes = args.minutes if wl not in ("gain10min", "fir1024") or args.minutes != 60.0 else 10.0
+    if wl in ("biquad_src", "sine_src") and args.minutes == 60.0:
+        minutes = 1.0  # the serial chain: ~10 Msamples/s
     L = int(round(minutes * 60 * sr))
     L -= L % HOP  # whole hops per rank (HOP is a multiple of B)
     # the file is world * L samples long; rank r owns [r L, (r+1) L) and
@@ -455,7 +480,8 @@ def main():
     nb = d.num_blocks(L_in, B)
     F = d.stft_frames(nb * B if wl in ("headline", "ch96k", "gain_stft") else L_in, N_FFT, HOP)
     out = (torch.empty((CH, nb * B), device=dev)
-           if wl in ("headline", "ch96k", "gain10min", "fir1024", "generic", "generic_stft", "gain_stft") else None)
+           if wl in ("headline", "ch96k", "gain10min", "fir1024", "generic", "generic_stft", "gain_stft", "biquad",
+                     "biquad_src", "sine_src") else None)
     if wl == "generic_stft":
         F = d.stft_frames(nb * B, N_FFT, HOP)
     LD = args.mag_ld or K_BINS
@@ -584,6 +610,33 @@ def main():
                 alg_desc = ("fused: C*F*(4H + 4K) B (render write + |X| write; the plugin ignores its input)"
                             if block_class == "table" else
                             "fused gain: C*F*(4H + 4H + 4K) B (file read + render write + |X| write)")
+    elif wl == "biquad":
+        # north_star's biquad as the build-defined kind: plugins/biquad.cpp's
+        # low-pass (initialize_state's coefficients) + optional sections
+        import numpy as np
+        rows = [d.Plugin.biquad_lowpass_coefficients(1000.0, 0.7071, float(sr))[0]]
+        rows += [rbj_section(*a, sr=float(sr)) for a in
+                 (("peq", 250.0, 1.5, 4.0), ("hp", 100.0, 0.7071, 0.0), ("peq", 1500.0, 2.0, 3.0))][:args.sections - 1]
+        bplug = d.Plugin.biquad(np.array(rows, np.float32))
+        plug_name = f"DSP_PLUGIN_BIQUAD, {args.sections} section(s): plugins/biquad.cpp's 1 kHz low-pass first"
+
+        def step():
+            d.render_offline(x, CH, B, float(sr), bplug, out=out)
+        workload = (f"biquad cascade ({args.sections} section(s), direct form I, zero initial state) render "
+                    f"(B=512), {minutes:g} min of 48 kHz stereo per GPU, block-parallel state scan")
+        kname = f"biquad_scan_kernel<{args.sections}> (tile = 64 lanes x 32 samples, windowed look-back)"
+        alg_desc = "C*L*(4 + 4) B (each input sample read once + each output sample written once)"
+    elif wl in ("biquad_src", "sine_src"):
+        pname = "biquad" if wl == "biquad_src" else "sine_test"
+        gmod, gplug, block_class = source_plugin(d, pname, CH, B, sr)
+        plug_name = (f"{pname}.cpp compiled unchanged (DSP_PLUGIN_GENERIC; its callback writes its State: "
+                     "the serial chain, one lane)")
+
+        def step():
+            d.render_offline(x, CH, B, float(sr), gplug, out=out)
+        workload = f"{pname}.cpp via the generic plugin driver (B=512), {minutes:g} min of 48 kHz stereo per GPU"
+        kname = "dspb_render_st_c2b512 (generic driver: one chain through the State, LDS double buffer)"
+        alg_desc = "C*L*(4 + 4) B (read + write)" if pname == "biquad" else "C*L*4 B (write; the input is ignored)"
     elif wl in ("wav16enc", "wav24enc"):
         # SURVEY 8(f) row 1, the writer: planar float -> interleaved PCM
         # (interleave + convert, audio.h:123-133; round half to even, clip)
@@ -772,6 +825,12 @@ def main():
         cpu = cpu_baseline(args.cpu_seconds)
     elif rank == 0 and world == 1 and not args.no_cpu_baseline and wl == "generic" and args.plugin != "IR_test":
         cpu = cpu_baseline_generic(min(args.cpu_seconds, 5.0), args.plugin or "gain_test")
+    elif rank == 0 and world == 1 and not args.no_cpu_baseline and wl in ("biquad", "biquad_src"):
+        cpu = cpu_baseline_generic(min(args.cpu_seconds, 8.0), "biquad", prefix="libplug_")
+        if wl == "biquad" and args.sections > 1:
+            cpu["note"] = "one section (plugins/biquad.cpp); the kind above runs more"
+    elif rank == 0 and world == 1 and not args.no_cpu_baseline and wl == "sine_src":
+        cpu = cpu_baseline_generic(min(args.cpu_seconds, 8.0), "sine_test")
 
     def emit(gather_ms, gather_err):
         if rank != 0:
@@ -855,6 +914,9 @@ def main():
                             "16 blocks per 64 KB workgroup round (DESIGN 4.6)"
                             if wl == "generic" and block_class == "callback" else
                             "the read + write stream (render_vec_kernel)" if wl == "generic" else
+                            "the read + write stream and the two recurrence passes (DESIGN 4.7)" if wl == "biquad" else
+                            "the serial chain: one lane runs the callback block after block (a State written "
+                            "every block); DESIGN 4.6" if wl in ("biquad_src", "sine_src") else
                             "the render (LDS-capacity-bound callbacks) then the power-capped memory STFT, "
                             "serial: DESIGN 4.6, profiles/r02_generic_stft_schedules.txt"
                             if wl == "generic_stft" and block_class == "callback" else

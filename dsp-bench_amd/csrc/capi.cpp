@@ -56,12 +56,30 @@ struct FirTaps {  // a FIR filter's device taps + overlap-save spectrum
     float h2048r, h2048i;
 };
 
+struct IirTab {  // a biquad cascade's coefficients + state-transition powers (biquad_tables)
+    std::vector<float> coef;
+    float *dev;
+    uint32_t window;  // biquad_tables' W
+};
+
+// the look-back workspace of biquad_scan_kernel, one per (device, stream):
+// calls on one stream run in order, so a launch only meets words tagged with
+// its own epoch (zeroed at allocation; epochs run 1 .. 2^32 - 1)
+struct IirWork {
+    uint64_t *aggw = nullptr, *inclw = nullptr;  // cap * 8 words each, one allocation
+    uint64_t cap = 0;
+    uint64_t epoch = 0;
+};
+
 struct DeviceRes {
     v2f *tw8192 = nullptr;  // exp(-2 pi i k / 8192), then 896 lane-major stage twiddles
     float4 *wbase = nullptr;  // (cos, sin)(theta 2l), (cos, sin)(theta (2l+1)), theta = 2 pi / 8191
     std::map<std::tuple<int, uint32_t, uint32_t, float>, float *> windows;  // (kind, N, valid, scale)
     std::map<std::pair<void *, int>, std::pair<float *, size_t>> scratch;  // per (stream, slot)
     std::vector<FirTaps> fir;                                  // FIR filters seen (plugin_map)
+    std::vector<IirTab> iir;                                   // biquad cascades seen (plugin_map)
+    std::map<void *, IirWork> iir_work;                        // per stream
+    uint32_t *iir_err_host = nullptr, *iir_err_dev = nullptr;  // host-mapped look-back error word
     float *delta = nullptr;  // 2048 floats: 1, 0, 0, ... (compute_IR's impulse, read-only)
 };
 
@@ -441,6 +459,138 @@ static bool ramp_closed_form(float gain, float step, uint32_t B) {
     return ok;
 }
 
+// DSP_PLUGIN_BIQUAD (iir.hip): the cascade's zero-input state transition over
+// T = biquad_lane_samples() samples, M (D x D, D = 2 S, state = (y1, y2) per
+// section; section k's x history is section k-1's y history), simulated in
+// float64 from each unit state, then its powers:
+//   [5 S coefficients, padded to 20][M^l, l = 0..64][M^(64 k), k = 0..256]
+// Returns W, the number of preceding tiles (of 64 T samples) whose aggregate
+// reaches a tile's entering state with a weight ||M^(64 k)||_inf above 2^-48
+// (every later power below it too): 1..256, or 0 when the transition does not
+// decay that fast (then the kernel's inclusive look-back).
+static uint32_t biquad_tables(const float *cf, uint32_t S, std::vector<float> &h) {
+    const int D = 2 * (int)S, T = (int)biquad_lane_samples();
+    std::vector<double> M((size_t)D * D);
+    for (int j = 0; j < D; ++j) {
+        double Y1[4], Y2[4], X1[4], X2[4];
+        for (int k = 0; k < (int)S; ++k) {
+            Y1[k] = (2 * k == j) ? 1.0 : 0.0;
+            Y2[k] = (2 * k + 1 == j) ? 1.0 : 0.0;
+        }
+        for (int k = 0; k < (int)S; ++k) {
+            X1[k] = k ? Y1[k - 1] : 0.0;
+            X2[k] = k ? Y2[k - 1] : 0.0;
+        }
+        for (int n = 0; n < T; ++n) {
+            double v = 0.0;
+            for (int k = 0; k < (int)S; ++k) {
+                const float *c = cf + 5 * k;
+                const double y = (double)c[0] * v + (double)c[1] * X1[k] + (double)c[2] * X2[k] -
+                                 (double)c[3] * Y1[k] - (double)c[4] * Y2[k];
+                X2[k] = X1[k];
+                X1[k] = v;
+                Y2[k] = Y1[k];
+                Y1[k] = y;
+                v = y;
+            }
+        }
+        for (int k = 0; k < (int)S; ++k) {
+            M[(size_t)(2 * k) * D + j] = Y1[k];
+            M[(size_t)(2 * k + 1) * D + j] = Y2[k];
+        }
+    }
+    auto mul = [D](const std::vector<double> &a, const std::vector<double> &b) {
+        std::vector<double> r((size_t)D * D, 0.0);
+        for (int i = 0; i < D; ++i)
+            for (int k = 0; k < D; ++k)
+                for (int j = 0; j < D; ++j) r[(size_t)i * D + j] += a[(size_t)i * D + k] * b[(size_t)k * D + j];
+        return r;
+    };
+    std::vector<double> I((size_t)D * D, 0.0);
+    for (int i = 0; i < D; ++i) I[(size_t)i * D + i] = 1.0;
+    h.assign(20 + (65 + 257) * (size_t)D * D, 0.f);
+    for (uint32_t q = 0; q < 5 * S; ++q) h[q] = cf[q];
+    std::vector<double> Q = I;
+    float *o = h.data() + 20;
+    for (int l = 0; l <= 64; ++l) {
+        for (int q = 0; q < D * D; ++q) o[(size_t)l * D * D + q] = (float)Q[q];
+        Q = mul(M, Q);
+    }
+    std::vector<double> Pm = I, step = I;
+    for (int l = 0; l < 64; ++l) step = mul(M, step);  // M^64 in float64
+    o += (size_t)65 * D * D;
+    uint32_t W = 0;  // the last k <= 256 whose weight is above the cut, + 1
+    bool finite = true;
+    for (int k = 0; k <= 256; ++k) {
+        double nrm = 0.0;
+        for (int i = 0; i < D; ++i) {
+            double row = 0.0;
+            for (int j = 0; j < D; ++j) row += std::fabs(Pm[(size_t)i * D + j]);
+            nrm = std::max(nrm, row);
+        }
+        finite = finite && std::isfinite(nrm);
+        if (nrm > std::ldexp(1.0, -48)) W = (uint32_t)k + 1;
+        for (int q = 0; q < D * D; ++q) o[(size_t)k * D * D + q] = (float)Pm[q];
+        Pm = mul(step, Pm);
+    }
+    // decayed within the table: the weights of the last 64 powers are all below the cut
+    return (finite && W <= 192) ? std::max<uint32_t>(W, 1) : 0u;
+}
+
+// takes the stream's workspace for one launch (a fresh epoch) and launches,
+// under one lock: launches on a stream are enqueued in epoch order
+static int iir_launch(int dev, hipStream_t s, BiquadArgs *A, uint32_t sections) {
+    const uint64_t tiles = (uint64_t)A->C * A->ntiles_ch;
+    {   // every launch takes a fresh epoch: a graph replay would reuse it
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        if (hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) {
+            set_last_error("stream capture: a BIQUAD render cannot be captured (its look-back state is per launch)");
+            return DSP_ERR_INVALID;
+        }
+    }
+    std::lock_guard<std::mutex> lk(g_mu);
+    DeviceRes &r = g_res[dev];
+    if (!r.iir_err_host) {
+        if (int st = refuse_capture(s, "the BIQUAD error word")) return st;
+        void *p = nullptr;
+        DSPB_HIP(hipHostMalloc(&p, 64, hipHostMallocMapped));
+        r.iir_err_host = (uint32_t *)p;
+        *r.iir_err_host = 0;
+        void *d = nullptr;
+        DSPB_HIP(hipHostGetDevicePointer(&d, p, 0));
+        r.iir_err_dev = (uint32_t *)d;
+    }
+    if (*r.iir_err_host) {  // a launch before this one gave up its look-back
+        *r.iir_err_host = 0;
+        set_last_error("a previous BIQUAD render on this device timed out in its look-back: its output is invalid");
+        return DSP_ERR_HIP;
+    }
+    IirWork &w = r.iir_work[(void *)s];
+    if (w.cap < tiles) {
+        if (int st = refuse_capture(s, "the BIQUAD look-back workspace")) return st;
+        if (w.aggw) {
+            DSPB_HIP(hipStreamSynchronize(s));
+            DSPB_HIP(hipFree(w.aggw));
+            w = IirWork{};
+        }
+        const uint64_t cap = std::max<uint64_t>(tiles, 1024);
+        const size_t bytes = 2 * cap * 8 * sizeof(uint64_t);
+        void *p = nullptr;
+        DSPB_HIP(hipMalloc(&p, bytes));
+        DSPB_HIP(hipMemsetAsync(p, 0, bytes, s));
+        w.aggw = (uint64_t *)p;
+        w.inclw = w.aggw + cap * 8;
+        w.cap = cap;
+    }
+    A->aggw = w.aggw;
+    A->inclw = w.inclw;
+    A->err = r.iir_err_dev;
+    w.epoch = w.epoch % 0xffffffffull + 1;
+    A->epoch = w.epoch;
+    if (int st = launch_biquad(*A, sections, s)) return st;
+    return DSP_OK;
+}
+
 static int plugin_map(const dsp_plugin *p, uint32_t B, int dev, hipStream_t s, SampleMap *m,
                       float sr = 48000.f, uint32_t flags = 0) {
     m->kind = MapKind::Noop;
@@ -451,6 +601,9 @@ static int plugin_map(const dsp_plugin *p, uint32_t B, int dev, hipStream_t s, S
     m->b_mask = is_pow2(B) ? B - 1 : 0;
     m->taps = nullptr;
     m->ntaps8 = 0;
+    m->iir_tab = nullptr;
+    m->sections = 0;
+    m->iir_window = 0;
     m->module = nullptr;
     m->gparams = nullptr;
     m->gparams_size = 0;
@@ -539,6 +692,44 @@ static int plugin_map(const dsp_plugin *p, uint32_t B, int dev, hipStream_t s, S
         m->olsH2048[1] = ft->h2048i;
         return DSP_OK;
     }
+    case DSP_PLUGIN_BIQUAD: {  // build-defined: Parameters{float coef[5 S]}, S = 1..4 sections
+        const uint32_t S = p->params_size / 20;
+        if (!p->params || S == 0 || S > 4 || p->params_size % 20)
+            return invalid("BIQUAD plugin needs 1..4 sections of 5 floats (b0 b1 b2 a1 a2) as its params blob");
+        std::vector<float> key((const float *)p->params, (const float *)p->params + 5 * S);
+        for (float v : key)
+            if (!std::isfinite(v)) return invalid("BIQUAD coefficients must be finite");
+        IirTab *it = nullptr;
+        {
+            std::lock_guard<std::mutex> lk(g_mu);
+            DeviceRes &r = g_res[dev];
+            for (auto &e : r.iir)
+                if (e.coef == key) { it = &e; break; }
+            if (!it) {
+                if (int st = refuse_capture(s, "a BIQUAD cascade's state-transition tables")) return st;
+                std::vector<float> h;
+                const uint32_t W = biquad_tables(key.data(), S, h);
+                float *d = nullptr;
+                DSPB_HIP(hipMalloc(&d, sizeof(float) * h.size()));
+                if (int st = upload_table(d, h.data(), sizeof(float) * h.size())) {
+                    (void)hipFree(d);
+                    return st;
+                }
+                if (r.iir.size() >= 8) {  // as the FIR cache: launches before the eviction finished
+                    DSPB_HIP(hipDeviceSynchronize());
+                    (void)hipFree(r.iir.front().dev);
+                    r.iir.erase(r.iir.begin());
+                }
+                r.iir.push_back(IirTab{key, d, W});
+                it = &r.iir.back();
+            }
+        }
+        m->kind = MapKind::Biquad;
+        m->iir_tab = it->dev;
+        m->sections = S;
+        m->iir_window = it->window;
+        return DSP_OK;
+    }
     case DSP_PLUGIN_GENERIC:  // the plugin's own audio_callback, compiled for gfx950 (module.h)
         if (!p->module) return invalid("GENERIC plugin needs a loaded dsp_module");
         m->kind = MapKind::Generic;
@@ -567,13 +758,28 @@ static bool rows_overlap(const float *const *in, uint32_t in_ch, uint64_t L, con
 // in_place: the call renders over its own input; with DSP_EXEC_VERIFY_CLASS
 // the callback then runs on every block, since the check needs the input
 // after the render (and a re-render would need it whole)
+// a table class's block held by a call: released (an event after the call's
+// launches on its stream) when the call returns, so an evicted table is freed
+// only after every launch that reads it
+struct SpecHold {
+    ::dsp_module *m = nullptr;
+    void *use = nullptr;
+    hipStream_t s = nullptr;
+    ~SpecHold() {
+        if (use) (void)module_spec_done(m, use, s);
+    }
+};
+
 static int specialize_generic(SampleMap *m, uint32_t C, uint32_t B, hipStream_t s, const dsp_exec *ex,
-                              bool in_place) {
+                              bool in_place, SpecHold *hold) {
     if (m->kind != MapKind::Generic || (ex && (ex->flags & DSP_EXEC_NO_SPECIALIZE))) return DSP_OK;
     if (in_place && ex && (ex->flags & DSP_EXEC_VERIFY_CLASS)) return DSP_OK;
     ModuleSpec sp;
     int st = module_specialize((::dsp_module *)m->module, m->gparams, m->gparams_size, C, B, m->sr, s, &sp);
     if (st) return st;
+    hold->m = (::dsp_module *)m->module;
+    hold->use = sp.use;
+    hold->s = s;
     if (sp.kind == kSpecTable) {
         m->kind = MapKind::Ramp;  // value = table[(global sample) mod B]
         m->table = sp.table;
@@ -692,6 +898,36 @@ static int render_device(const float *const *in, uint32_t in_ch, uint64_t L, flo
         if (start != 0) return invalid("GENERIC render: the fused tail path does not apply");
         return module_render((::dsp_module *)map.module, map.gparams, map.gparams_size, in, in_ch, L, out, C, B,
                              map.sr, goff, s);
+    }
+    if (map.kind == MapKind::Biquad) {  // the cascade from zero state at the start of the file
+        if (start != 0 || goff != 0) return invalid("BIQUAD render: whole files only (sample_offset 0)");
+        int dev = 0;
+        DSPB_HIP(hipGetDevice(&dev));
+        const uint32_t S = map.sections, D = 2 * S;
+        for (uint32_t c0 = 0; c0 < C; c0 += kMaxChannels) {
+            const uint32_t cn = (C - c0) < (uint32_t)kMaxChannels ? (C - c0) : kMaxChannels;
+            BiquadArgs A{};
+            A.in_aligned16 = A.out_aligned16 = 1;
+            for (uint32_t j = 0; j < cn; ++j) {
+                A.out.p[j] = out[c0 + j];
+                A.out_aligned16 &= aligned(out[c0 + j], 16) ? 1u : 0u;
+                if (c0 + j < in_ch) {
+                    A.in.p[j] = in[c0 + j];
+                    A.in_ch = j + 1;
+                    A.in_aligned16 &= aligned(in[c0 + j], 16) ? 1u : 0u;
+                }
+            }
+            A.L = L;
+            A.Ly = end;
+            A.C = cn;
+            A.ntiles_ch = biquad_tiles(end);
+            A.coef = map.iir_tab;
+            A.Q = map.iir_tab + 20;
+            A.P = A.Q + (size_t)65 * D * D;
+            A.window = map.iir_window;
+            if (int st = iir_launch(dev, s, &A, S)) return st;
+        }
+        return DSP_OK;
     }
     if (map.kind == MapKind::Fir) {  // convolution from the start of the file
         if (start != 0 || goff != 0) return invalid("FIR render: whole files only (sample_offset 0)");
@@ -946,6 +1182,15 @@ int dsp_device_count(void) {
     return n;
 }
 
+int dsp_biquad_plan(const float *coef, uint32_t sections, uint32_t *window) {
+    if (!coef || !window || sections == 0 || sections > 4) return invalid("dsp_biquad_plan: 1..4 sections");
+    for (uint32_t q = 0; q < 5 * sections; ++q)
+        if (!std::isfinite(coef[q])) return invalid("BIQUAD coefficients must be finite");
+    std::vector<float> h;
+    *window = biquad_tables(coef, sections, h);
+    return DSP_OK;
+}
+
 uint64_t dsp_stft_frame_count(uint64_t L, uint32_t N, uint32_t H) {
     if (N == 0 || H == 0 || L < N) return 0;
     return (L - N) / H + 1;
@@ -989,11 +1234,12 @@ int dsp_render_offline(const float *const *in, uint32_t in_channels, uint64_t L,
         for (uint32_t c = 0; c < in_channels; ++c) din[c] = in[c];
         for (uint32_t c = 0; c < C; ++c) dout[c] = out[c];
     }
+    SpecHold hold;  // released after the call's launches
     SampleMap map;
     int st = plugin_map(plugin, B, g.dev, s, &map, sr, ex ? ex->flags : 0);
     if (st) return st;
     const SampleMap orig = map;
-    if ((st = specialize_generic(&map, C, B, s, ex, rows_overlap(din.data(), in_channels, L, dout.data(), C, Lr))))
+    if ((st = specialize_generic(&map, C, B, s, ex, rows_overlap(din.data(), in_channels, L, dout.data(), C, Lr), &hold)))
         return st;
     TimedLaunch tl{};
     if ((st = timing_begin(s, &tl))) return st;
@@ -1044,10 +1290,11 @@ int dsp_render_loop(const float *const *in, uint32_t in_channels, uint64_t L, ui
     if (g.status) return g.status;
     hipStream_t s = stream_of(ex);
     const uint64_t Lr = nblocks * B;
+    SpecHold hold;  // released after the call's launches
     SampleMap map;
     int st = plugin_map(plugin, B, g.dev, s, &map, sr, ex ? ex->flags : 0);
     if (st) return st;
-    if ((st = specialize_generic(&map, C, B, s, ex, false))) return st;
+    if ((st = specialize_generic(&map, C, B, s, ex, false, &hold))) return st;
     if ((st = ensure_ramp_table(map, s))) return st;
     const uint32_t in_ch = std::min(in_channels, C);  // channels_to_write (audio.cpp:66)
     auto wrap = [&](const float *const *src, float *const *dst, uint32_t nc, const SampleMap &m) -> int {
@@ -1167,16 +1414,17 @@ int dsp_render_stft(const float *const *in, uint32_t in_channels, uint64_t L,
         for (uint32_t c = 0; c < in_channels; ++c) din[c] = in[c];
         for (uint32_t c = 0; c < C; ++c) { dout[c] = out[c]; dmag[c] = mag[c]; }
     }
+    SpecHold hold;  // released after the call's launches
     SampleMap map;
     if ((st = plugin_map(plugin, B, g.dev, s, &map, sr, ex ? ex->flags : 0))) return st;
     const SampleMap orig = map;
-    if ((st = specialize_generic(&map, C, B, s, ex, rows_overlap(din.data(), in_channels, L, dout.data(), C, Lr))))
+    if ((st = specialize_generic(&map, C, B, s, ex, rows_overlap(din.data(), in_channels, L, dout.data(), C, Lr), &hold)))
         return st;
     const uint64_t goff = goff_of(ex);
     set_result(ex, orig.kind == MapKind::Generic && map.kind != MapKind::Generic ? DSP_RESULT_CLASS : 0u);
 
     bool fused = (N == 8192) && (H % 128 == 0) && (H <= N) && (goff % 2 == 0) && F > 0 &&
-                 map.kind != MapKind::Fir && map.kind != MapKind::Generic;
+                 map.kind != MapKind::Fir && map.kind != MapKind::Generic && map.kind != MapKind::Biquad;
     for (uint32_t c = 0; c < C; ++c) fused = fused && aligned(dout[c], 8);
     for (uint32_t c = 0; c < in_channels; ++c) fused = fused && aligned(din[c], 8);
 

@@ -21,7 +21,7 @@ struct ChanOut {
 // Per-sample plugin maps that the render / fused kernels specialise on.
 // `table` is the IR_test ramp (B floats) computed on the device by
 // ramp_table_kernel; the others use the scalar `a`.
-enum class MapKind : int { Noop = 0, Gain = 1, Ramp = 3, Fir = 4, Generic = 5 };
+enum class MapKind : int { Noop = 0, Gain = 1, Ramp = 3, Fir = 4, Generic = 5, Biquad = 6 };
 
 struct SampleMap {
     MapKind kind;
@@ -36,6 +36,9 @@ struct SampleMap {
     const float *olsH;   // Fir: FFT(taps)/16384 in fir_fft.hip's lane-major pair layout
     float olsH2048[2];   // Fir: H[2048]/16384
     const float *pairH;  // Fir: FFT_4096(taps)/4096 in fir_pair_kernel's layout (fir_fft.hip)
+    const float *iir_tab; // Biquad: [5 S coefficients, padded to 20][M^(T l), l <= 64][M^(64 T k), k <= 256]
+    uint32_t sections;   // Biquad: S (1..4)
+    uint32_t iir_window; // Biquad: tiles of aggregates that reach a tile's state (0: inclusive look-back)
     void *module;        // Generic: the dsp_module running the plugin's own audio_callback
     const void *gparams; // Generic: host Parameters blob
     uint32_t gparams_size;

@@ -1,0 +1,387 @@
+// iir.hip -- DSP_PLUGIN_BIQUAD: a cascade of S <= 4 biquad sections over a
+// whole file, block-parallel.
+//
+// Each section is the direct-form-I difference equation of our stateful
+// example plugin (plugins/biquad.cpp:43-57, the callback the reference's audio
+// thread runs block after block, audio.cpp:160-165):
+//
+//   y[n] = b0 x[n] + b1 x[n-1] + b2 x[n-2] - a1 y[n-1] - a2 y[n-2]
+//
+// section k's input is section k-1's output, every history starts at zero
+// (initialize_state's State s = {}) and is carried across blocks, so the
+// render of ceil(L/B) blocks is the cascade run over the zero-padded file --
+// whatever B is.  A serial chain per channel would leave the chip idle (one
+// lane per channel), so the recurrence is split the way a linear scan is:
+//
+//   state s = (y1, y2) of every section, D = 2 S values.  Over T samples with
+//   zero input the cascade maps s to M s (M = M_T, D x D), and over a run of
+//   input from state s it ends in M s + e, where e is the end state of the same
+//   run started from s = 0 (section 1's x history is the file itself, known).
+//
+// One wavefront owns a tile of 64 T samples of one channel, lane l the T
+// samples [l T, (l + 1) T):
+//   1. the tile is staged through LDS (coalesced 16-byte loads) into each
+//      lane's registers; pass 1 runs the cascade from s = 0 -> e_l;
+//   2. a Kogge-Stone scan over the lanes with the powers M^(T 2^j) gives
+//      E_l = sum_{m <= l} M^(T (l - m)) e_m (the tile's state at the end of
+//      lane l, tile entered at s = 0); E_63 is the tile's aggregate;
+//   3. the tile publishes its aggregate; the state entering it is
+//      S_in = sum_k M^(64 T k) agg_(i-1-k).  For a filter whose transition
+//      decays (every stable one the host finds decaying within 256 tiles),
+//      the sum stops at the W tiles whose weight exceeds 2^-48 (lane k reads
+//      tile k + 1 back): only aggregates, a fixed summation order, the same
+//      bits every run.  Otherwise (W = 0) a decoupled look-back: predecessors'
+//      aggregates are combined back to the first that holds an inclusive state,
+//      and every tile publishes its own inclusive state E_63 + M^(64 T) S_in;
+//   4. lane l starts from E_(l-1) + M^(T l) S_in and runs the cascade again
+//      over its registers (pass 2), the real outputs, out through LDS.
+// So every sample is read once and written once from HBM (8 B per sample).
+// Tile g is the wave's place in launch order, so a tile only ever waits for
+// tiles of waves dispatched before it; the wait is bounded anyway
+// (kSpinLimit), and a wave that gives up sets the error word the host checks
+// (capi.cpp iir_launch).
+//
+// Arithmetic: fp32, each section as fma(-a1, y1, fma(-a2, y2, fma(b2, x2,
+// fma(b1, x1, b0 x)))); the matrix powers come from float64 (capi.cpp
+// biquad_tables).  Not bit-exact with a serial fp32 chain (nor is the serial
+// chain with the reference's -ffast-math build of the same source): the
+// parity bar is a bound against float64 derived from the filter's own
+// impulse responses (tests/test_gpu_biquad.py).
+#include "kernels.hpp"
+
+namespace dspb {
+
+constexpr int kIirT = 32;             // samples per lane
+constexpr int kIirTile = 64 * kIirT;  // samples per wavefront (tile)
+constexpr int kIirWaves = 4;          // wavefronts per workgroup
+constexpr int kIirLdsStride = kIirT + 1;  // floats per lane chunk in LDS (conflict-free column reads)
+constexpr uint32_t kSpinLimit = 1u << 16;  // s_sleep rounds before a wait gives up (legit waits: a few)
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+template <int S>
+struct Cascade {
+    static constexpr int D = 2 * S;
+    float b0[S], b1[S], b2[S], na1[S], na2[S];
+
+    __device__ explicit Cascade(const float *cf) {
+#pragma unroll
+        for (int k = 0; k < S; ++k) {
+            b0[k] = cf[5 * k];
+            b1[k] = cf[5 * k + 1];
+            b2[k] = cf[5 * k + 2];
+            na1[k] = -cf[5 * k + 3];
+            na2[k] = -cf[5 * k + 4];
+        }
+    }
+
+    // runs the cascade over x[0..T) from state st (y1, y2 per section; the x
+    // history of section k > 0 is section k - 1's (y1, y2)); section 1's x
+    // history is (xh1, xh2).  st ends as the state after x[T-1].  kWrite:
+    // x[n] becomes the last section's output.
+    template <bool kWrite>
+    __device__ __forceinline__ void run(float (&x)[kIirT], float xh1, float xh2, float (&st)[D]) const {
+        float X1[S], X2[S], Y1[S], Y2[S];
+#pragma unroll
+        for (int k = 0; k < S; ++k) {
+            Y1[k] = st[2 * k];
+            Y2[k] = st[2 * k + 1];
+            X1[k] = k ? st[2 * k - 2] : xh1;
+            X2[k] = k ? st[2 * k - 1] : xh2;
+        }
+#pragma unroll
+        for (int n = 0; n < kIirT; ++n) {
+            float v = x[n];
+#pragma unroll
+            for (int k = 0; k < S; ++k) {
+                const float acc = __builtin_fmaf(b2[k], X2[k], __builtin_fmaf(b1[k], X1[k], b0[k] * v));
+                const float y = __builtin_fmaf(na1[k], Y1[k], __builtin_fmaf(na2[k], Y2[k], acc));
+                X2[k] = X1[k];
+                X1[k] = v;
+                Y2[k] = Y1[k];
+                Y1[k] = y;
+                v = y;
+            }
+            if (kWrite) x[n] = v;
+        }
+#pragma unroll
+        for (int k = 0; k < S; ++k) {
+            st[2 * k] = Y1[k];
+            st[2 * k + 1] = Y2[k];
+        }
+    }
+};
+
+// r = m v for a D x D row-major matrix in memory
+template <int D>
+__device__ __forceinline__ void matvec(const float *m, const float (&v)[D], float (&r)[D]) {
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+        float a = 0.f;
+#pragma unroll
+        for (int j = 0; j < D; ++j) a = __builtin_fmaf(m[i * D + j], v[j], a);
+        r[i] = a;
+    }
+}
+
+template <int S>
+__global__ __launch_bounds__(256) void biquad_scan_kernel(BiquadArgs A) {
+    constexpr int D = 2 * S;
+    __shared__ float lds[kIirWaves][64 * kIirLdsStride];
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    float *buf = lds[wave];
+
+    // tile g = the wave's place in launch order: workgroups are dispatched in
+    // increasing id, so a tile's predecessors belong to waves already running
+    // or done (the waits are bounded anyway)
+    const uint64_t g = (uint64_t)blockIdx.x * kIirWaves + wave;
+    if (g >= (uint64_t)A.C * A.ntiles_ch) return;
+    const uint32_t c = (uint32_t)(g % A.C);
+    const uint64_t ti = g / A.C;
+    const uint64_t base = ti * kIirTile;  // first sample of the tile in the channel
+    const float *x = c < A.in_ch ? A.in.p[c] : nullptr;
+    const uint64_t lim = (x && A.L > base) ? A.L - base : 0;  // file samples in or after the tile
+
+    // 1. stage: 16-byte loads, element e of the tile -> LDS lane chunk e / T
+    if (lim >= (uint64_t)kIirTile && A.in_aligned16) {
+        const f4 *x4 = reinterpret_cast<const f4 *>(x + base);
+        f4 v[kIirTile / 256];
+#pragma unroll
+        for (int k = 0; k < kIirTile / 256; ++k) v[k] = __builtin_nontemporal_load(x4 + k * 64 + lane);
+#pragma unroll
+        for (int k = 0; k < kIirTile / 256; ++k) {
+            const uint32_t e = k * 256 + lane * 4;
+            float *d = buf + (e / kIirT) * kIirLdsStride + e % kIirT;
+            d[0] = v[k].x, d[1] = v[k].y, d[2] = v[k].z, d[3] = v[k].w;
+        }
+    } else {
+        for (uint32_t e = lane; e < (uint32_t)kIirTile; e += 64)
+            buf[(e / kIirT) * kIirLdsStride + e % kIirT] = e < lim ? x[base + e] : 0.f;
+    }
+    // section 1's x history at the tile start: the file's two samples before it
+    float h1 = 0.f, h2 = 0.f;
+    if (lane == 0 && x) {
+        if (base >= 1 && base - 1 < A.L) h1 = x[base - 1];
+        if (base >= 2 && base - 2 < A.L) h2 = x[base - 2];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    float xr[kIirT];
+#pragma unroll
+    for (int n = 0; n < kIirT; ++n) xr[n] = buf[lane * kIirLdsStride + n];
+    if (lane > 0) {
+        h1 = buf[(lane - 1) * kIirLdsStride + kIirT - 1];
+        h2 = buf[(lane - 1) * kIirLdsStride + kIirT - 2];
+    }
+
+    // pass 1: from state 0
+    const Cascade<S> cs(A.coef);
+    float E[D];
+#pragma unroll
+    for (int r = 0; r < D; ++r) E[r] = 0.f;
+    cs.template run<false>(xr, h1, h2, E);
+
+    // 2. scan over the lanes: E_l = sum_{m <= l} M^(T (l - m)) e_m
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+        const uint32_t d = 1u << j;
+        float t[D], r[D];
+#pragma unroll
+        for (int q = 0; q < D; ++q) t[q] = __shfl_up(E[q], d);
+        matvec<D>(A.Q + (size_t)d * D * D, t, r);
+        if (lane >= d) {
+#pragma unroll
+            for (int q = 0; q < D; ++q) E[q] += r[q];
+        }
+    }
+    float agg[D];
+#pragma unroll
+    for (int q = 0; q < D; ++q) agg[q] = __shfl(E[q], 63);
+
+    // 3. the state entering the tile.  A tile's aggregate (and, in the
+    // chained mode, its inclusive state) is published as D self-validating
+    // 64-bit words (launch tag << 32 | float bits), each one relaxed atomic
+    // store at device scope: a reader takes a value only when all D words
+    // carry this launch's tag -- no flag, so no release / acquire (no L2
+    // write-back or invalidate) on either side
+    float Sin[D];
+#pragma unroll
+    for (int q = 0; q < D; ++q) Sin[q] = 0.f;
+    const uint64_t tag = A.epoch << 32;
+    auto publish = [&](uint64_t *words, const float (&v)[D]) {
+        float mine = 0.f;
+#pragma unroll
+        for (int q = 0; q < D; ++q) mine = lane == (uint32_t)q ? v[q] : mine;
+        if (lane < (uint32_t)D)
+            __hip_atomic_store(words + g * D + lane, tag | __float_as_uint(mine), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    };
+    // the D words of tile gj: true when all carry this launch's tag
+    auto fetch = [&](const uint64_t *words, uint64_t gj, float (&v)[D]) {
+        bool ok = true;
+#pragma unroll
+        for (int q = 0; q < D; ++q) {
+            const uint64_t w = __hip_atomic_load(const_cast<uint64_t *>(words) + gj * D + q, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+            ok = ok && (w & 0xffffffff00000000ull) == tag;
+            v[q] = __uint_as_float((uint32_t)w);
+        }
+        return ok;
+    };
+    uint32_t spins = 0;
+    auto give_up = [&]() {  // never with a correct launch: bounded, and loud
+        if (++spins <= kSpinLimit) {
+            __builtin_amdgcn_s_sleep(1);
+            return false;
+        }
+        if (lane == 0) *A.err = 1u;
+        return true;
+    };
+    publish(A.aggw, agg);
+    if (A.window) {
+        // a filter whose transition decays: S_in = sum_{k < W} M^(64 T k)
+        // agg_(i-1-k), every older tile's weight being below 2^-48 (the host
+        // picked W).  Aggregates only, summed in a fixed order: no chain of
+        // inclusive states, and the same bits on every run.
+        for (uint32_t k0 = 0; k0 < A.window && (uint64_t)k0 < ti; k0 += 64) {
+            const uint32_t k = k0 + lane;
+            const bool valid = k < A.window && (uint64_t)k < ti;
+            const uint64_t gj = valid ? (ti - 1 - k) * A.C + c : 0;
+            float v[D], w[D];
+            for (;;) {
+                const bool ok = !valid || fetch(A.aggw, gj, v);
+                if (__ballot(!ok) == 0 || give_up()) break;
+            }
+#pragma unroll
+            for (int q = 0; q < D; ++q) v[q] = valid ? v[q] : 0.f;
+            matvec<D>(A.P + (size_t)(valid ? k : 0) * D * D, v, w);
+#pragma unroll
+            for (int q = 0; q < D; ++q) {
+                float a = w[q];
+#pragma unroll
+                for (int o = 32; o >= 1; o >>= 1) a += __shfl_xor(a, o);
+                Sin[q] += a;
+            }
+        }
+    } else {
+        // a filter that does not decay within the table (W = 0): decoupled
+        // look-back, predecessors' aggregates back to the first one holding an
+        // inclusive state; this tile then publishes its own
+        float mult[D * D];  // M^(64 T (i - 1 - jbase)), the window's weight
+#pragma unroll
+        for (int q = 0; q < D * D; ++q) mult[q] = (q % (D + 1)) == 0 ? 1.f : 0.f;
+        int64_t jbase = (int64_t)ti - 1;
+        while (jbase >= 0) {
+            const int64_t jj = jbase - (int64_t)lane;
+            const uint64_t gj = jj >= 0 ? (uint64_t)jj * A.C + c : 0;
+            float v[D], w[D];
+            uint32_t state = 2;  // before the channel's first tile: an inclusive zero
+#pragma unroll
+            for (int q = 0; q < D; ++q) v[q] = 0.f;
+            if (jj >= 0) state = fetch(A.inclw, gj, v) ? 2u : fetch(A.aggw, gj, v) ? 1u : 0u;
+            const uint64_t incl = __ballot(state == 2);
+            const uint64_t ready = __ballot(state != 0);
+            const uint32_t first = incl ? (uint32_t)__builtin_ctzll(incl) : 64u;
+            const uint64_t need = first >= 63 ? ~0ull : ((2ull << first) - 1);
+            if ((ready & need) != need) {
+                if (give_up()) break;
+                continue;
+            }
+#pragma unroll
+            for (int q = 0; q < D; ++q) v[q] = (lane <= first && jj >= 0) ? v[q] : 0.f;
+            matvec<D>(A.P + (size_t)lane * D * D, v, w);  // M^(64 T lane) v
+#pragma unroll
+            for (int q = 0; q < D; ++q) {
+                float a = w[q];
+#pragma unroll
+                for (int o = 32; o >= 1; o >>= 1) a += __shfl_xor(a, o);
+                w[q] = a;
+            }
+#pragma unroll
+            for (int q = 0; q < D; ++q) {
+                float a = Sin[q];
+#pragma unroll
+                for (int j = 0; j < D; ++j) a = __builtin_fmaf(mult[q * D + j], w[j], a);
+                Sin[q] = a;
+            }
+            if (first < 64) break;
+            // next window: weight by M^(64 T 64) more
+            float nm[D * D];
+            const float *p64 = A.P + (size_t)64 * D * D;
+#pragma unroll
+            for (int i = 0; i < D; ++i)
+#pragma unroll
+                for (int j = 0; j < D; ++j) {
+                    float a = 0.f;
+#pragma unroll
+                    for (int k = 0; k < D; ++k) a = __builtin_fmaf(mult[i * D + k], p64[k * D + j], a);
+                    nm[i * D + j] = a;
+                }
+#pragma unroll
+            for (int q = 0; q < D * D; ++q) mult[q] = nm[q];
+            jbase -= 64;
+        }
+        float inc[D], r[D];  // agg + M^(64 T) S_in
+        matvec<D>(A.P + (size_t)D * D, Sin, r);
+#pragma unroll
+        for (int q = 0; q < D; ++q) inc[q] = agg[q] + r[q];
+        publish(A.inclw, inc);
+    }
+
+    // 4. lane l from E_(l-1) + M^(T l) S_in, over its own samples
+    float s0[D];
+    {
+        float r[D];
+        matvec<D>(A.Q + (size_t)lane * D * D, Sin, r);
+#pragma unroll
+        for (int q = 0; q < D; ++q) {
+            const float prev = __shfl_up(E[q], 1);
+            s0[q] = (lane ? prev : 0.f) + r[q];
+        }
+    }
+    cs.template run<true>(xr, h1, h2, s0);
+#pragma unroll
+    for (int n = 0; n < kIirT; ++n) buf[lane * kIirLdsStride + n] = xr[n];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    float *y = A.out.p[c];
+    const uint64_t ny = A.Ly > base ? A.Ly - base : 0;
+    if (ny >= (uint64_t)kIirTile && A.out_aligned16) {
+        f4 *y4 = reinterpret_cast<f4 *>(y + base);
+#pragma unroll
+        for (int k = 0; k < kIirTile / 256; ++k) {
+            const uint32_t e = k * 256 + lane * 4;
+            const float *s = buf + (e / kIirT) * kIirLdsStride + e % kIirT;
+            __builtin_nontemporal_store(f4{s[0], s[1], s[2], s[3]}, y4 + k * 64 + lane);
+        }
+    } else {
+        for (uint32_t e = lane; e < (uint32_t)kIirTile && e < ny; e += 64)
+            y[base + e] = buf[(e / kIirT) * kIirLdsStride + e % kIirT];
+    }
+}
+
+uint64_t biquad_tiles(uint64_t Ly) { return (Ly + kIirTile - 1) / kIirTile; }
+uint32_t biquad_lane_samples() { return kIirT; }
+
+int launch_biquad(const BiquadArgs &A, uint32_t sections, hipStream_t s) {
+    const uint64_t waves = (uint64_t)A.C * A.ntiles_ch;
+    if (waves == 0) return DSP_OK;
+    const uint64_t groups = (waves + kIirWaves - 1) / kIirWaves;
+    if (groups > 0x7fffffffull || A.C == 0 || A.C > (uint32_t)kMaxChannels) return DSP_ERR_INVALID;
+    switch (sections) {
+    case 1: hipLaunchKernelGGL(biquad_scan_kernel<1>, dim3((uint32_t)groups), dim3(256), 0, s, A); break;
+    case 2: hipLaunchKernelGGL(biquad_scan_kernel<2>, dim3((uint32_t)groups), dim3(256), 0, s, A); break;
+    case 3: hipLaunchKernelGGL(biquad_scan_kernel<3>, dim3((uint32_t)groups), dim3(256), 0, s, A); break;
+    case 4: hipLaunchKernelGGL(biquad_scan_kernel<4>, dim3((uint32_t)groups), dim3(256), 0, s, A); break;
+    default: return DSP_ERR_INVALID;
+    }
+    DSPB_HIP(hipGetLastError());
+    return DSP_OK;
+}
+
+uint64_t biquad_waves_launched(uint64_t C, uint64_t ntiles_ch) {
+    return (C * ntiles_ch + kIirWaves - 1) / kIirWaves * kIirWaves;
+}
+
+}  // namespace dspb

@@ -224,6 +224,10 @@ struct Analysis {
             }
         };
         auto store_to = [&](const Val &P, const Val &Vv, bool val_is_ptr, const std::string &what) {
+            if (P.org == 0) {  // (store_to runs in the final pass: every origin has propagated)
+                stop(what + " through a pointer of unknown origin");
+                return;
+            }
             if (P.org & (O_TBL | O_PRM | O_GC | O_GM | O_EXT | O_UNK)) {
                 stop(what + " to " + (P.org & O_TBL ? "the block pointer table" : P.org & O_PRM ? "Parameters" :
                                       (P.org & (O_GC | O_GM)) ? "global memory" : "memory behind a loaded pointer"));
@@ -242,6 +246,7 @@ struct Analysis {
         };
         auto load_from = [&](const Val &P, bool ptr_result) {
             Val v;
+            if (final_pass && P.org == 0) stop("a load through a pointer of unknown origin");
             if (P.org & O_GM) stop("a load of mutable global memory");
             if (P.org & O_UNK) stop("a load through a pointer made from an integer");
             v.data = P.data & (D_IN | D_VAR | D_ADDR);
@@ -398,6 +403,9 @@ struct Analysis {
                 for (const auto &t : values_in(x, M)) {
                     const Val v = get(t);
                     r.data |= v.data;
+                    // a pointer it returns may be any argument moved (llvm.ptrmask
+                    // of __builtin_align_down): it keeps their origins
+                    r.org |= v.org;
                     if (v.org & (O_BUF | O_TBL)) stop("a block pointer is passed to " + callee);
                 }
         } else if (op == "atomicrmw" || op == "cmpxchg" || op == "fence" || op == "va_arg" || op == "invoke" ||
@@ -698,13 +706,16 @@ Facts analyze(const std::string &ir, const char *fn) {
     A.val[A.args[0]].org = O_PRM;
     A.val[A.args[1]].org = O_STA;
     A.val[A.args[2]].org = O_TBL;
-    for (int it = 0; it < 64; ++it) {
+    bool settled = false;
+    for (int it = 0; it < 64 && !settled; ++it) {
         bool grew = false;
         const uint32_t ld = A.loc_data, sd = A.sta_data;
         const bool ws = A.f.writes_state;
         for (const Inst &I : A.body) grew |= A.step(I, false);
-        if (!grew && ld == A.loc_data && sd == A.sta_data && ws == A.f.writes_state) break;
+        settled = !grew && ld == A.loc_data && sd == A.sta_data && ws == A.f.writes_state;
     }
+    // facts from values still growing would not be conservative
+    if (!settled) A.stop("no fixpoint after 64 passes");
     for (const Inst &I : A.body) A.step(I, true);
     if (!A.fail.empty()) {
         A.f.why = A.fail;

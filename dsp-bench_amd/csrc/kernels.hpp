@@ -85,9 +85,14 @@ struct ModuleSpec {
     // (the fused kernels then evaluate it instead of loading the table)
     bool affine = false;
     double rg0 = 0.0, rs = 0.0;
+    void *use = nullptr;  // kSpecTable: the hold on the table, released by module_spec_done
 };
 int module_specialize(::dsp_module *m, const void *params, uint32_t params_size, uint32_t C, uint32_t B, float sr,
                       hipStream_t s, ModuleSpec *out);
+// after the launches that read a table class's block (ModuleSpec::use)
+int module_spec_done(::dsp_module *m, void *use, hipStream_t s);
+void spec_reap(::dsp_module *m);
+size_t module_spec_retired(::dsp_module *m);  // tables evicted and not yet freed
 struct FirFftArgs {
     ChanIn in;           // input channels
     uint32_t in_ch;
@@ -107,6 +112,29 @@ constexpr uint32_t kPairHop = 3072;
 int launch_fir_pair(const FirFftArgs &A, uint32_t C, hipStream_t s);
 int launch_fir(const float *x, uint64_t L, float *y, uint64_t Ly, const float *h8, uint32_t T8,
                bool y_aligned16, hipStream_t s);
+// DSP_PLUGIN_BIQUAD (iir.hip): one launch renders C <= 16 channels of Ly
+// samples from zero state; tiles of 64 lanes x biquad_lane_samples() samples
+struct BiquadArgs {
+    ChanIn in;
+    uint32_t in_ch;
+    uint64_t L;            // file samples (zero past)
+    ChanOut out;
+    uint64_t Ly;           // rendered samples per channel
+    uint32_t C;            // channels of this launch
+    uint64_t ntiles_ch;    // biquad_tiles(Ly)
+    const float *coef;     // 5 S floats (b0 b1 b2 a1 a2 per section)
+    const float *Q;        // 65 D x D: M^(T l)
+    const float *P;        // 257 D x D: M^(64 T k)
+    uint32_t window;       // W: S_in from the W previous tiles' aggregates (0: inclusive look-back)
+    uint64_t *aggw, *inclw;  // per tile, D words: epoch << 32 | float bits (aggregate, inclusive)
+    uint64_t epoch;        // distinct per launch on one workspace (32 bits used)
+    uint32_t *err;         // host-mapped: set when a look-back gives up
+    uint32_t in_aligned16, out_aligned16;
+};
+uint64_t biquad_tiles(uint64_t Ly);
+uint32_t biquad_lane_samples();
+uint64_t biquad_waves_launched(uint64_t C, uint64_t ntiles_ch);
+int launch_biquad(const BiquadArgs &A, uint32_t sections, hipStream_t s);
 int launch_minmax(const float *x, uint64_t n, uint32_t P, float *vmax, float *vmin, hipStream_t s);
 int launch_spectro(const float *mag, uint64_t F, uint32_t K, uint64_t ld, uint32_t P, float *out,
                    hipStream_t s);

@@ -23,6 +23,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -553,14 +554,28 @@ struct dsp_module {
     bool initialized = false;
     // block classes found by module_specialize, per (Parameters, C, B, sr);
     // newest last, at most kSpecCache
+    // a table class's block: the calls that hold it (module_specialize hands
+    // it out, module_spec_done takes it back after the call's launches), an
+    // event per stream after its last use, and whether a captured graph may
+    // replay it (then it lives as long as the module)
+    struct SpecUse {
+        float *table = nullptr;
+        std::map<hipStream_t, hipEvent_t> ev;
+        int inflight = 0;
+        bool captured = false;
+    };
     struct Spec {
         std::vector<unsigned char> params;
         uint32_t C, B;
         float sr;
         dspb::ModuleSpec r;
+        std::shared_ptr<SpecUse> use;  // table classes only
     };
     std::vector<Spec> spec;
-    std::vector<float *> retired;  // tables of evicted entries, freed by dsp_module_destroy
+    // tables of evicted entries: freed once no call holds them and their
+    // streams have passed their last use (spec_reap), or by
+    // dsp_module_destroy when a captured graph may replay them
+    std::vector<std::shared_ptr<SpecUse>> retired;
     std::mutex mu;
 };
 
@@ -843,8 +858,11 @@ void dsp_module_destroy(dsp_module *m) {
         if (m->d_params) (void)hipFree(m->d_params);
         (void)hipDeviceSynchronize();  // no launch may still read a table
         for (auto &e : m->spec)
-            if (e.r.table) (void)hipFree(const_cast<float *>(e.r.table));
-        for (float *t : m->retired) (void)hipFree(t);
+            if (e.use) m->retired.push_back(e.use);
+        for (auto &u : m->retired) {
+            (void)hipFree(u->table);
+            for (auto &kv : u->ev) (void)hipEventDestroy(kv.second);
+        }
         for (hipEvent_t e : {m->upload_ev, m->use_ev})
             if (e) {
                 (void)hipEventSynchronize(e);
@@ -868,12 +886,19 @@ int dsp_module_block_class(dsp_module *m, const void *params, uint32_t params_si
     if (int st = with_device(ex && ex->device >= 0 ? ex->device : m->device, &prev)) return st;
     dspb::ModuleSpec r;
     const int st = dspb::module_specialize(m, params, params_size, C, B, sr, ex ? (hipStream_t)ex->stream : nullptr, &r);
+    if (!st && r.use) (void)dspb::module_spec_done(m, r.use, ex ? (hipStream_t)ex->stream : nullptr);  // no launch
     int cur = -1;
     if (hipGetDevice(&cur) == hipSuccess && prev >= 0 && prev != cur) (void)hipSetDevice(prev);
     if (st) return st;
     *block_class = r.kind == dspb::kSpecTable ? DSP_BLOCK_TABLE : r.kind == dspb::kSpecGain ? DSP_BLOCK_GAIN
                                                                                               : DSP_BLOCK_CALLBACK;
     if (gain) *gain = r.gain;
+    return DSP_OK;
+}
+
+int dsp_module_retired_tables(dsp_module *m, uint64_t *n) {
+    if (!m || !n) return DSP_ERR_INVALID;
+    *n = dspb::module_spec_retired(m);
     return DSP_OK;
 }
 
@@ -913,10 +938,11 @@ int dsp_module_initialize_state(dsp_module *m, const void *params, uint32_t C, f
     st = init_slot(m, 0, params, C, sr, arena_bytes, nullptr);
     m->initialized = (st == DSP_OK);
     // block classes were found with the previous State: forget them (their
-    // tables stay allocated until dsp_module_destroy)
+    // tables are freed once no call holds them, dspb::spec_reap)
     for (auto &e : m->spec)
-        if (e.r.table) m->retired.push_back(const_cast<float *>(e.r.table));
+        if (e.use) m->retired.push_back(e.use);
     m->spec.clear();
+    dspb::spec_reap(m);
     if (prev >= 0 && prev != m->device) (void)hipSetDevice(prev);
     return st;
 }
@@ -1440,6 +1466,52 @@ static bool affine_ramp(const float *t, uint32_t B, double *g0, double *s) {
     return false;
 }
 
+static bool capturing(hipStream_t s) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    return hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
+}
+
+// frees the retired tables no call holds and no stream still reads (m->mu held)
+void spec_reap(dsp_module *m) {
+    for (size_t i = 0; i < m->retired.size();) {
+        auto &u = m->retired[i];
+        bool done = !u->captured && u->inflight == 0;
+        for (auto &kv : u->ev) done = done && hipEventQuery(kv.second) == hipSuccess;
+        if (!done) {
+            ++i;
+            continue;
+        }
+        (void)hipFree(u->table);
+        for (auto &kv : u->ev) (void)hipEventDestroy(kv.second);
+        m->retired.erase(m->retired.begin() + (long)i);
+    }
+}
+
+// a call that rendered with a table class's block releases it: an event on
+// its stream after its launches (none under capture: the table then stays
+// until dsp_module_destroy)
+int module_spec_done(dsp_module *m, void *use, hipStream_t s) {
+    if (!m || !use) return DSP_OK;
+    std::lock_guard<std::mutex> lk(m->mu);
+    auto *u = static_cast<dsp_module::SpecUse *>(use);
+    --u->inflight;
+    if (capturing(s)) {
+        u->captured = true;
+    } else {
+        hipEvent_t &e = u->ev[s];
+        if (!e) MOD_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        MOD_HIP(hipEventRecord(e, s));
+    }
+    spec_reap(m);
+    return DSP_OK;
+}
+
+size_t module_spec_retired(dsp_module *m) {
+    std::lock_guard<std::mutex> lk(m->mu);
+    spec_reap(m);
+    return m->retired.size();
+}
+
 int module_specialize(dsp_module *m, const void *params, uint32_t params_size, uint32_t C, uint32_t B, float sr,
                       hipStream_t s, ModuleSpec *out) {
     *out = ModuleSpec{};
@@ -1452,10 +1524,15 @@ int module_specialize(dsp_module *m, const void *params, uint32_t params_size, u
     if (params_size != m->params_size || (!params && params_size)) return DSP_OK;  // module_render reports it
     if (int st = check_device(m)) return st;
     std::lock_guard<std::mutex> lk(m->mu);
+    spec_reap(m);
     for (const auto &e : m->spec)
         if (e.C == C && e.B == B && same_bits(e.sr, sr) && e.params.size() == params_size &&
             (!params_size || std::memcmp(e.params.data(), params, params_size) == 0)) {
             *out = e.r;
+            if (e.use) {
+                ++e.use->inflight;
+                out->use = e.use.get();
+            }
             return DSP_OK;
         }
     if (int st = refuse_capture(s)) return st;  // probing allocates and synchronises
@@ -1534,16 +1611,23 @@ int module_specialize(dsp_module *m, const void *params, uint32_t params_size, u
         res.kind = kSpecGain;
         res.gain = g;
     }
-    // a table stays allocated while the module lives (a graph or another
-    // thread may still hold it): the cache evicts its entry, not the table
+    // an evicted entry's table is retired, not freed: a call (this thread's
+    // or another's) or a captured graph may still read it (spec_reap)
     if (m->spec.size() >= kSpecCache) {
-        if (m->spec.front().r.table) m->retired.push_back(const_cast<float *>(m->spec.front().r.table));
+        if (m->spec.front().use) m->retired.push_back(m->spec.front().use);
         m->spec.erase(m->spec.begin());
+    }
+    std::shared_ptr<dsp_module::SpecUse> use;
+    if (res.table) {
+        use = std::make_shared<dsp_module::SpecUse>();
+        use->table = const_cast<float *>(res.table);
+        use->inflight = 1;
     }
     m->spec.push_back({std::vector<unsigned char>((const unsigned char *)params,
                                                   (const unsigned char *)params + params_size),
-                       C, B, sr, res});
+                       C, B, sr, res, use});
     *out = res;
+    out->use = use.get();
     return DSP_OK;
 }
 

@@ -143,14 +143,15 @@ int run(const Source &src, uint32_t C, uint32_t B, float sr, const dsp_plugin *p
     if (goff % B) return invalid("sample_offset must be a multiple of B");
     // render-only: chunks of whole blocks without a halo (N = H = B)
     const uint32_t pN = stft ? N : B, pH = stft ? H : B;
-    // the FIR's history and a GENERIC plugin's State carry across blocks:
+    // the FIR's and the BIQUAD's history and a GENERIC plugin's State carry across blocks:
     // one chunk (a GENERIC plugin without a State chunks like the map plugins)
     int stateless = 1;
     if (plugin && plugin->kind == DSP_PLUGIN_GENERIC) {
         if (!plugin->module) return invalid("GENERIC plugin needs a loaded dsp_module");
         if (int e = dsp_module_sizes((const dsp_module *)plugin->module, nullptr, nullptr, &stateless)) return e;
     }
-    const bool one = plugin && (plugin->kind == DSP_PLUGIN_FIR || (plugin->kind == DSP_PLUGIN_GENERIC && !stateless));
+    const bool one = plugin && (plugin->kind == DSP_PLUGIN_FIR || plugin->kind == DSP_PLUGIN_BIQUAD ||
+                                (plugin->kind == DSP_PLUGIN_GENERIC && !stateless));
     dsp_shard whole{};
     int st = dsp_shard_plan(L, C, 1, 0, B, pN, pH, DSP_SHARD_TIME, 1, &whole);
     if (st) return st;

@@ -26,6 +26,7 @@ DSP_PLUGIN_GAIN = 1
 DSP_PLUGIN_STATIC_GAIN = 2
 DSP_PLUGIN_IR_RAMP = 3
 DSP_PLUGIN_FIR = 4
+DSP_PLUGIN_BIQUAD = 5
 DSP_PLUGIN_GENERIC = 16
 
 DSP_EXEC_HOST_BUFFERS = 0x1

@@ -70,6 +70,28 @@ class Plugin:
         return Plugin(L.DSP_PLUGIN_FIR, t.tobytes(), b"", f"fir{t.size}",
                       exec_flags=L.DSP_EXEC_FIR_DIRECT if direct else 0)
 
+    @staticmethod
+    def biquad(sections) -> "Plugin":
+        """Build-defined cascade of 1..4 direct-form-I biquads (DSP_PLUGIN_BIQUAD):
+        `sections` = rows (b0, b1, b2, a1, a2), each y = b0 x + b1 x1 + b2 x2 -
+        a1 y1 - a2 y2 (plugins/biquad.cpp's section), zero initial state, the
+        whole file; rendered block-parallel by a state scan (iir.hip)."""
+        c = np.ascontiguousarray(np.asarray(sections, dtype=np.float32).reshape(-1, 5))
+        return Plugin(L.DSP_PLUGIN_BIQUAD, c.tobytes(), b"", f"biquad{c.shape[0]}")
+
+    @staticmethod
+    def biquad_lowpass_coefficients(cutoff: float = 1000.0, q: float = 0.7071, sr: float = 48000.0):
+        """The coefficients plugins/biquad.cpp's initialize_state computes
+        (RBJ cookbook low-pass in double, rounded to float), as one section row."""
+        import math
+        w0 = 2.0 * 3.14159265358979323846 * float(np.float32(cutoff)) / float(np.float32(sr))
+        alpha = math.sin(w0) / (2.0 * float(np.float32(q)))
+        c = math.cos(w0)
+        a0 = 1.0 + alpha
+        b0 = np.float32((1.0 - c) / 2.0 / a0)
+        return np.array([[b0, np.float32((1.0 - c) / a0), b0, np.float32(-2.0 * c / a0),
+                          np.float32((1.0 - alpha) / a0)]], np.float32)
+
     def as_struct(self) -> dsp_plugin:
         p = C.create_string_buffer(self.params, max(1, len(self.params)))
         s = C.create_string_buffer(self.state, max(1, len(self.state)))

@@ -242,6 +242,12 @@ class Module:
             flags |= L.DSP_EXEC_VERIFY_CLASS
         return Plugin(L.DSP_PLUGIN_GENERIC, bytes(params), b"", name, self, exec_flags=flags)
 
+    def retired_tables(self) -> int:
+        """Evicted TABLE-class blocks not freed yet (dsp_module_retired_tables)."""
+        n = C.c_uint64()
+        check(L.lib().dsp_module_retired_tables(self.handle, C.byref(n)), "dsp_module_retired_tables")
+        return n.value
+
     def block_class(self, params: bytes, channels: int, block: int, sample_rate: float, stream=None):
         """(class, gain): "table" | "gain" | "callback" (dsp_module_block_class),
         probing the plugin's callback on the current device if not known yet."""

@@ -74,6 +74,12 @@ enum dsp_plugin_kind {
     DSP_PLUGIN_FIR = 4,         /* build-defined cfg 3b: y[n] = sum_k taps[k] x[n-k], params = float taps[T],
                                    T <= 2048; state carries across blocks, so whole files only
                                    (sample_offset 0; shard by channel) */
+    DSP_PLUGIN_BIQUAD = 5,      /* build-defined: a cascade of S = params_size / 20 (1..4) direct-form-I
+                                   biquads, params = float {b0, b1, b2, a1, a2}[S], y = b0 x + b1 x1 +
+                                   b2 x2 - a1 y1 - a2 y2 (plugins/biquad.cpp's section), zero initial
+                                   state carried across blocks: whole files only (sample_offset 0;
+                                   shard by channel).  Block-parallel (a state scan), fp32 within a
+                                   bound of float64, not bit-exact with a serial chain; not in graphs */
     DSP_PLUGIN_GENERIC = 16     /* compiled audio_callback run on the GPU (module) */
 };
 
@@ -127,6 +133,14 @@ typedef struct dsp_exec {
 
 /* Number of frames of an STFT over L samples: L >= N ? (L - N) / H + 1 : 0. */
 uint64_t dsp_stft_frame_count(uint64_t L, uint32_t N, uint32_t H);
+
+/* DSP_PLUGIN_BIQUAD's plan for a cascade (host only, no device): *window =
+ * the number of preceding 2048-sample tiles whose end state still reaches a
+ * tile's entering state above 2^-48 (1..192: the render sums exactly those, in
+ * a fixed order, and is bitwise reproducible run to run), or 0 for a cascade
+ * that does not decay that fast (a chained look-back: within the same error
+ * bound, not bitwise reproducible).  DSP_ERR_INVALID for a bad blob. */
+int dsp_biquad_plan(const float *coef, uint32_t sections, uint32_t *window);
 
 /* Offline render, one-shot:
  *   nblocks = ceil(L / B); out[c] holds nblocks * B floats.

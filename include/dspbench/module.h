@@ -193,6 +193,13 @@ enum dsp_block_class { DSP_BLOCK_CALLBACK = 0, DSP_BLOCK_TABLE = 1, DSP_BLOCK_GA
 int dsp_module_block_class(dsp_module *m, const void *params, uint32_t params_size, uint32_t C, uint32_t B,
                            float sr, int32_t *block_class, float *gain, const dsp_exec *ex);
 
+/* The class cache keeps 4 (Parameters, C, B, sr) sets.  An evicted TABLE
+ * class's block is freed once no call holds it and every stream that read it
+ * has passed its last use (an event recorded when each call returns); one a
+ * captured graph used stays until dsp_module_destroy.  *n = evicted blocks not
+ * freed yet (diagnostic; frees what can be freed first). */
+int dsp_module_retired_tables(dsp_module *m, uint64_t *n);
+
 /* ---- what the callback does with its block (no GPU) ----------------------
  * dsp_module_compile compiles the plugin a second time into an analysis
  * kernel, dspb_proof(P, S, out, C, B, sr) { audio_callback(*P, *S, out, C, B,

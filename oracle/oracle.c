@@ -716,3 +716,47 @@ void oracle_fir_f64(const float *x, uint64_t L, const float *h, uint32_t T, doub
         y[n] = acc;
     }
 }
+
+/* DSP_PLUGIN_BIQUAD (dsp-bench_amd/csrc/iir.hip) and plugins/biquad.cpp:43-57 */
+void oracle_biquad_f64(const float *x, uint64_t L, uint64_t Ly, const float *coef, uint32_t S, double *y,
+                       double *lmax) {
+    double X1[4] = {0}, X2[4] = {0}, Y1[4] = {0}, Y2[4] = {0}, lm[4] = {0};
+    if (S > 4) S = 4;
+    for (uint64_t n = 0; n < Ly; ++n) {
+        double v = (x && n < L) ? (double)x[n] : 0.0;
+        for (uint32_t k = 0; k < S; ++k) {
+            const float *c = coef + 5 * k;
+            const double t = fabs((double)c[0] * v) + fabs((double)c[1] * X1[k]) + fabs((double)c[2] * X2[k]) +
+                             fabs((double)c[3] * Y1[k]) + fabs((double)c[4] * Y2[k]);
+            if (t > lm[k]) lm[k] = t;
+            const double yy = (double)c[0] * v + (double)c[1] * X1[k] + (double)c[2] * X2[k] -
+                              (double)c[3] * Y1[k] - (double)c[4] * Y2[k];
+            X2[k] = X1[k];
+            X1[k] = v;
+            Y2[k] = Y1[k];
+            Y1[k] = yy;
+            v = yy;
+        }
+        y[n] = v;
+    }
+    if (lmax)
+        for (uint32_t k = 0; k < S; ++k) lmax[k] = lm[k];
+}
+
+void oracle_biquad_f32(const float *x, uint64_t L, uint64_t Ly, const float *coef, uint32_t S, float *y) {
+    float X1[4] = {0}, X2[4] = {0}, Y1[4] = {0}, Y2[4] = {0};
+    if (S > 4) S = 4;
+    for (uint64_t n = 0; n < Ly; ++n) {
+        float v = (x && n < L) ? x[n] : 0.f;
+        for (uint32_t k = 0; k < S; ++k) {
+            const float *c = coef + 5 * k;
+            const float yy = c[0] * v + c[1] * X1[k] + c[2] * X2[k] - c[3] * Y1[k] - c[4] * Y2[k];
+            X2[k] = X1[k];
+            X1[k] = v;
+            Y2[k] = Y1[k];
+            Y1[k] = yy;
+            v = yy;
+        }
+        y[n] = v;
+    }
+}

@@ -136,8 +136,10 @@ class RefPlugin:
     Mirrors plugin_populate_from_descriptor (ref plugin.cpp:335-364):
     default_parameters -> initialize_state."""
 
-    def __init__(self, name: str, num_channels: int = 2, sample_rate: float = 48000.0):
-        path = os.path.join(REF_DIR, f"libref_{name}.so")
+    def __init__(self, name: str, num_channels: int = 2, sample_rate: float = 48000.0, prefix: str = "libref_"):
+        # prefix "libplug_": one of this repository's plugins (plugins/, tests/plugins/)
+        # built for the CPU the way the reference's JIT builds a plugin (oracle/Makefile)
+        path = os.path.join(REF_DIR, f"{prefix}{name}.so")
         self.lib = C.CDLL(path)
         self.lib.ref_sizeof_parameters.restype = C.c_ulong
         self.lib.ref_sizeof_state.restype = C.c_ulong
@@ -360,6 +362,74 @@ def spectrogram_decimate(mag: np.ndarray, pixels: int) -> np.ndarray:
                                               C.c_void_p]
     L.oracle_spectrogram_decimate(_ptr(mag), F, K, K, pixels, _ptr(out))
     return out
+
+
+def biquad_f64(x, coef, Ly: int | None = None):
+    """The biquad cascade (rows b0 b1 b2 a1 a2) over x zero-padded to Ly,
+    float64 (oracle.c oracle_biquad_f64).  Returns (y, lmax[S]): lmax[k] =
+    max_n of section k's |b0 v| + |b1 v1| + |b2 v2| + |a1 y1| + |a2 y2|."""
+    c = np.ascontiguousarray(np.asarray(coef, np.float32).reshape(-1, 5))
+    x = np.ascontiguousarray(x, np.float32) if x is not None else None
+    L_ = 0 if x is None else x.size
+    Ly = L_ if Ly is None else Ly
+    y = np.empty(max(Ly, 1), np.float64)
+    lm = np.zeros(4, np.float64)
+    Lb = lib()
+    Lb.oracle_biquad_f64.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p, C.c_uint32, C.c_void_p,
+                                     C.c_void_p]
+    Lb.oracle_biquad_f64(_ptr(x) if x is not None else None, L_, Ly, _ptr(c), c.shape[0], _ptr(y), _ptr(lm))
+    return y[:Ly], lm[:c.shape[0]]
+
+
+def biquad_f32(x, coef, Ly: int | None = None) -> np.ndarray:
+    """The serial fp32 cascade, evaluated as plugins/biquad.cpp writes it
+    (left to right, no contraction): oracle.c oracle_biquad_f32."""
+    c = np.ascontiguousarray(np.asarray(coef, np.float32).reshape(-1, 5))
+    x = np.ascontiguousarray(x, np.float32) if x is not None else None
+    L_ = 0 if x is None else x.size
+    Ly = L_ if Ly is None else Ly
+    y = np.empty(max(Ly, 1), np.float32)
+    Lb = lib()
+    Lb.oracle_biquad_f32.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p, C.c_uint32, C.c_void_p]
+    Lb.oracle_biquad_f32(_ptr(x) if x is not None else None, L_, Ly, _ptr(c), c.shape[0], _ptr(y))
+    return y[:Ly]
+
+
+def biquad_impulse_l1(coef, tol: float = 1e-13, max_len: int = 1 << 22):
+    """Per section: (||h||_1, ||g||_1) of the section's impulse response h
+    (b over a) and of its all-pole part g = 1 / (1 + a1 z^-1 + a2 z^-2), summed
+    in float64 until the tail is below tol relative (or max_len)."""
+    out = []
+    for b0, b1, b2, a1, a2 in np.asarray(coef, np.float64).reshape(-1, 5):
+        sums = []
+        for b in ((b0, b1, b2), (1.0, 0.0, 0.0)):
+            x1 = x2 = y1 = y2 = 0.0
+            acc, n, quiet = 0.0, 0, 0
+            while n < max_len:
+                v = 1.0 if n == 0 else 0.0
+                y = b[0] * v + b[1] * x1 + b[2] * x2 - a1 * y1 - a2 * y2
+                x2, x1, y2, y1 = x1, v, y1, y
+                acc += abs(y)
+                n += 1
+                quiet = quiet + 1 if abs(y) <= tol * max(acc, 1e-300) else 0
+                if quiet > 64:
+                    break
+            sums.append(acc)
+        out.append(tuple(sums))
+    return out
+
+
+def biquad_error_bound(coef, lmax, K: float = 16.0) -> float:
+    """A bound on |y_gpu - y64| for the cascade: section k's own roundings
+    (at most K u relative to its magnitude terms, u = 2^-24, K covering the
+    fp32 recurrence's five roundings and the block scan's state rounding) pass
+    through its all-pole part, and every earlier section's error through the
+    whole later sections:  e_k <= ||h_k||_1 e_(k-1) + K u ||g_k||_1 lmax_k."""
+    u = 2.0 ** -24
+    e = 0.0
+    for (h1, g1), lm in zip(biquad_impulse_l1(coef), lmax):
+        e = h1 * e + K * u * g1 * lm
+    return e
 
 
 def fir_f64(x, taps, Ly: int | None = None) -> np.ndarray:

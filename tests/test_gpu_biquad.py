@@ -1,0 +1,237 @@
+"""DSP_PLUGIN_BIQUAD: a cascade of 1..4 direct-form-I biquads rendered
+block-parallel (csrc/iir.hip), and our stateful example plugin
+plugins/biquad.cpp compiled unchanged (GENERIC, the serial chain).
+
+The reference's stateful plugins run on its audio thread one block after the
+other (audio.cpp:160-165); a biquad's state (x1, x2, y1, y2 per channel)
+carries across blocks, so the render of ceil(L/B) blocks is the cascade over
+the zero-padded file whatever B is.  The oracle is the float64 cascade
+(oracle.c oracle_biquad_f64); the kind is fp32 and not bit-exact with any
+serial fp32 chain (it scans the state), so the bar is a derived bound
+(oracle.biquad_error_bound):  e_k <= ||h_k||_1 e_(k-1) + 16 u ||g_k||_1 lmax_k
+per section k, u = 2^-24, h_k the section's impulse response, g_k its
+all-pole part, lmax_k the largest magnitude sum |b0 v| + |b1 v1| + |b2 v2| +
+|a1 y1| + |a2 y2| of the float64 run.  The reference has no biquad: parity is
+against the plugin's own difference equation (unpinned by any reference
+fixture).
+"""
+import math
+import os
+
+import numpy as np
+import pytest
+
+import dspbench as d
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+PLUGIN_DIR = os.path.join(ROOT, "dsp-bench_amd", "plugins")
+pytestmark = pytest.mark.gpu
+
+
+def rbj(kind: str, fc: float, q: float, sr: float = 48000.0, gain_db: float = 0.0):
+    """RBJ cookbook section (b0, b1, b2, a1, a2) / a0 in float64, rounded to float32."""
+    w0 = 2 * math.pi * fc / sr
+    al = math.sin(w0) / (2 * q)
+    c = math.cos(w0)
+    if kind == "lp":
+        b = [(1 - c) / 2, 1 - c, (1 - c) / 2]
+        a = [1 + al, -2 * c, 1 - al]
+    elif kind == "hp":
+        b = [(1 + c) / 2, -(1 + c), (1 + c) / 2]
+        a = [1 + al, -2 * c, 1 - al]
+    else:  # peaking EQ
+        A = 10 ** (gain_db / 40)
+        b = [1 + al * A, -2 * c, 1 - al * A]
+        a = [1 + al / A, -2 * c, 1 - al / A]
+    return [np.float32(b[0] / a[0]), np.float32(b[1] / a[0]), np.float32(b[2] / a[0]),
+            np.float32(a[1] / a[0]), np.float32(a[2] / a[0])]
+
+
+def random_cascade(rng, S):
+    rows = []
+    for _ in range(S):
+        kind = rng.choice(["lp", "hp", "peq"])
+        fc = float(np.exp(rng.uniform(np.log(40.0), np.log(15000.0))))
+        rows.append(rbj(kind, fc, float(rng.uniform(0.5, 4.0)), gain_db=float(rng.uniform(-12, 12))))
+    return np.array(rows, np.float32)
+
+
+def check(oracle, got, x, coef, Ly):
+    """every channel of `got` [C, Ly] against the float64 cascade of x[c] (None: zeros)"""
+    for c in range(got.shape[0]):
+        xc = x[c] if x is not None and c < x.shape[0] else None
+        y64, lmax = oracle.biquad_f64(xc, coef, Ly)
+        bound = oracle.biquad_error_bound(coef, lmax)
+        err = float(np.max(np.abs(got[c].astype(np.float64) - y64))) if Ly else 0.0
+        assert err <= bound, (c, err, bound)
+    return True
+
+
+def plan(coef):
+    import ctypes as C
+    w = C.c_uint32()
+    c = np.ascontiguousarray(coef, np.float32)
+    assert d.lib().dsp_biquad_plan(c.ctypes.data_as(C.c_void_p), c.shape[0], C.byref(w)) == 0
+    return w.value
+
+
+@pytest.mark.parametrize("S", [1, 2, 3, 4])
+@pytest.mark.parametrize("L", [1, 100, 2047, 2048, 2049, 4096 + 5, 64 * 2048 + 513, 300_000])
+def test_biquad_kind_against_float64(torch_cuda, oracle, S, L):
+    rng = np.random.default_rng(1000 * S + L % 997)
+    coef = random_cascade(rng, S)
+    x = rng.uniform(-1, 1, (2, L)).astype(np.float32)
+    B = 512
+    got = d.render_offline(torch_cuda.from_numpy(x).cuda(), 2, B, 48000.0, d.Plugin.biquad(coef)).cpu().numpy()
+    Ly = d.num_blocks(L, B) * B
+    assert got.shape == (2, Ly)
+    check(oracle, got, x, coef, Ly)
+
+
+@pytest.mark.parametrize("fc,q", [(20.0, 0.7071), (20.0, 10.0), (5.0, 0.7071), (2.0, 0.7071), (1000.0, 0.7071)])
+def test_biquad_slow_decay_windows_and_chain(torch_cuda, oracle, fc, q):
+    """Low cutoffs and high Q: the window W grows to 148 tiles (three windows
+    of 64 lanes), and W = 0 (the inclusive look-back) for a filter that does
+    not decay within 192 tiles; both within the bound."""
+    coef = np.array([rbj("lp", fc, q)], np.float32)
+    rng = np.random.default_rng(int(fc * 10 + q))
+    L = 2048 * 400 + 77
+    x = rng.uniform(-1, 1, (1, L)).astype(np.float32)
+    got = d.render_offline(torch_cuda.from_numpy(x).cuda(), 1, 256, 48000.0, d.Plugin.biquad(coef)).cpu().numpy()
+    check(oracle, got, x, coef, got.shape[1])
+
+
+def test_biquad_chain_mode_marginal_filter(torch_cuda, oracle):
+    """A resonator with its poles on the unit circle never decays: W = 0, the
+    chained look-back; bounded by the f64 run over a finite file."""
+    th = 2 * math.pi * 440 / 48000
+    coef = np.array([[1.0, 0.0, 0.0, -2 * math.cos(th), 1.0]], np.float32)
+    coef[0, 4] = np.float32(0.9999999)  # just inside the unit circle in f32
+    assert plan(coef) == 0
+    rng = np.random.default_rng(7)
+    L = 2048 * 300
+    x = np.zeros((1, L), np.float32)
+    x[0, :64] = rng.uniform(-1, 1, 64).astype(np.float32)
+    got = d.render_offline(torch_cuda.from_numpy(x).cuda(), 1, 512, 48000.0, d.Plugin.biquad(coef)).cpu().numpy()
+    y64, _ = oracle.biquad_f64(x[0], coef, got.shape[1])
+    # no decaying bound here: an undamped recurrence accumulates its roundings
+    # in any fp32 evaluation -- the bar is the serial fp32 chain's own error
+    err = float(np.max(np.abs(got[0].astype(np.float64) - y64)))
+    err32 = float(np.max(np.abs(oracle.biquad_f32(x[0], coef, got.shape[1]).astype(np.float64) - y64)))
+    assert err <= 4 * err32 + 1e-6 * float(np.abs(y64).max()), (err, err32)
+
+
+def test_biquad_reproducible_bits(torch_cuda):
+    """W > 0: the same bits on every run (a fixed summation order, no race)."""
+    coef = np.array([rbj("lp", 200.0, 2.0), rbj("peq", 3000.0, 1.0, gain_db=6.0)], np.float32)
+    assert plan(coef) > 0
+    x = torch_cuda.rand((2, 2_000_000), device="cuda") * 2 - 1
+    p = d.Plugin.biquad(coef)
+    a = d.render_offline(x, 2, 512, 48000.0, p)
+    for _ in range(3):
+        assert torch_cuda.equal(a, d.render_offline(x, 2, 512, 48000.0, p))
+
+
+@pytest.mark.parametrize("C,in_ch", [(1, 1), (3, 2), (2, 0), (17, 17)])
+def test_biquad_channels(torch_cuda, oracle, C, in_ch):
+    """Odd channel counts, a channel the file lacks (zeros, zero state: zeros),
+    more than one launch's 16 channels."""
+    coef = np.array([rbj("hp", 300.0, 0.9)], np.float32)
+    rng = np.random.default_rng(C * 10 + in_ch)
+    L = 5000
+    x = rng.uniform(-1, 1, (max(in_ch, 1), L)).astype(np.float32)
+    xin = torch_cuda.from_numpy(x[:in_ch]).cuda() if in_ch else torch_cuda.zeros((0, L), device="cuda")
+    got = d.render_offline(xin, C, 256, 48000.0, d.Plugin.biquad(coef)).cpu().numpy()
+    check(oracle, got, x[:in_ch] if in_ch else None, coef, got.shape[1])
+    for c in range(in_ch, C):
+        assert not np.any(got[c])
+
+
+def test_biquad_block_size_does_not_matter(torch_cuda):
+    """The state carries across blocks: B only sets the padded length."""
+    coef = np.array([rbj("lp", 800.0, 0.7)], np.float32)
+    x = torch_cuda.rand((2, 10_000), device="cuda") - 0.5
+    a = d.render_offline(x, 2, 512, 48000.0, d.Plugin.biquad(coef))
+    b = d.render_offline(x, 2, 128, 48000.0, d.Plugin.biquad(coef))
+    assert a.shape[1] == 10_240 and b.shape[1] == 10_112
+    assert torch_cuda.equal(a[:, :10_112], b)
+
+
+def test_biquad_render_stft_is_render_then_stft(torch_cuda):
+    coef = np.array([rbj("lp", 2000.0, 0.7)], np.float32)
+    x = torch_cuda.rand((2, 48_000), device="cuda") - 0.5
+    out, mag = d.render_stft(x, 2, 512, 48000.0, d.Plugin.biquad(coef))
+    out2 = d.render_offline(x, 2, 512, 48000.0, d.Plugin.biquad(coef))
+    assert torch_cuda.equal(out, out2)
+    mag2 = d.stft_magnitude(out2)
+    assert torch_cuda.equal(mag, mag2)
+
+
+def test_biquad_ir_analysis(torch_cuda, oracle):
+    """compute_IR of the cascade (plugin.cpp:17-58): its impulse response."""
+    coef = np.array([rbj("lp", 1000.0, 0.7071), rbj("hp", 100.0, 0.7071)], np.float32)
+    ir, mag = d.ir_analysis(d.Plugin.biquad(coef), C_out=2, sr=48000.0, ir_len=2048, device=torch_cuda.device("cuda"))
+    ir = ir.cpu().numpy()
+    delta = np.zeros(2048, np.float32)
+    delta[0] = 1
+    y64, lmax = oracle.biquad_f64(delta, coef, 2048)
+    bound = oracle.biquad_error_bound(coef, lmax)
+    assert float(np.max(np.abs(ir - y64[None, :]))) <= bound
+
+
+def test_biquad_graph_capture_refused(torch_cuda):
+    coef = np.array([rbj("lp", 1000.0, 0.7)], np.float32)
+    x = torch_cuda.rand((2, 4096), device="cuda")
+    out = torch_cuda.empty((2, 4096), device="cuda")
+    p = d.Plugin.biquad(coef)
+    d.render_offline(x, 2, 512, 48000.0, p, out=out)
+    torch_cuda.cuda.synchronize()
+    s = torch_cuda.cuda.Stream()
+    g = torch_cuda.cuda.CUDAGraph()
+    with pytest.raises(d.DspError):
+        with torch_cuda.cuda.graph(g, stream=s):
+            d.render_offline(x, 2, 512, 48000.0, p, out=out)
+
+
+def test_biquad_source_plugin_serial_and_kind(torch_cuda, oracle):
+    """plugins/biquad.cpp compiled unchanged runs the serial chain (its State
+    is written every block); the kind with the same coefficients (read back
+    from the device State) renders the same filter -- both within the bound
+    of float64, and the source bit-exact against the serial fp32 restatement
+    (oracle_biquad_f32: the same evaluation order, no contraction: the module
+    builds with -ffp-contract=off)."""
+    import struct
+    mod = d.module.Module(d.module.compile_source(open(os.path.join(PLUGIN_DIR, "biquad.cpp")).read(), "biquad.cpp"))
+    params = mod.default_parameters()
+    mod.initialize_state(params, 2, 48000.0)
+    coef = np.array([struct.unpack("<5f", mod.read_state()[:20])], np.float32)
+    assert np.allclose(coef, d.Plugin.biquad_lowpass_coefficients(1000.0, 0.7071, 48000.0), rtol=1e-6, atol=0)
+    x = np.random.default_rng(3).uniform(-1, 1, (2, 50_000)).astype(np.float32)
+    xt = torch_cuda.from_numpy(x).cuda()
+    src = d.render_offline(xt, 2, 512, 48000.0, mod.plugin(params)).cpu().numpy()
+    kind = d.render_offline(xt, 2, 512, 48000.0, d.Plugin.biquad(coef)).cpu().numpy()
+    for c in range(2):
+        assert np.array_equal(src[c], oracle.biquad_f32(x[c], coef, src.shape[1]))
+    check(oracle, src, x, coef, src.shape[1])
+    check(oracle, kind, x, coef, kind.shape[1])
+
+
+def test_biquad_full_hour_stereo(torch_cuda, oracle):
+    """The bench's shape: 1 h of 48 kHz stereo, two sections, against the
+    float64 cascade of the whole file (host C, a few seconds)."""
+    coef = np.array([rbj("lp", 1000.0, 0.7071), rbj("peq", 250.0, 1.5, gain_db=4.0)], np.float32)
+    L = 48_000 * 3600
+    g = torch_cuda.Generator(device="cuda").manual_seed(11)
+    x = (torch_cuda.rand((2, L), device="cuda", generator=g) * 2 - 1) * 0.1
+    got = d.render_offline(x, 2, 512, 48000.0, d.Plugin.biquad(coef))
+    torch_cuda.cuda.synchronize()
+    xh = x.cpu().numpy()
+    del x
+    for c in range(2):
+        y = got[c].cpu().numpy()
+        y64, lmax = oracle.biquad_f64(xh[c], coef, y.size)
+        bound = oracle.biquad_error_bound(coef, lmax)
+        err = float(np.max(np.abs(y.astype(np.float64) - y64)))
+        assert err <= bound, (c, err, bound)
+        del y64, y

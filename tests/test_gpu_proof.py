@@ -292,6 +292,29 @@ def test_evicted_table_outlives_a_captured_graph(torch_cuda):
     assert bool((out == 0.125).all())
 
 
+def test_evicted_tables_are_freed_after_their_last_use(torch_cuda):
+    """A Parameters sweep over a TABLE-class plugin, ten times more sets than
+    the class cache keeps: every evicted table is freed once the calls that
+    read it have passed (an event per call and stream), so the module's
+    device memory stays flat; only a table a captured graph used is kept
+    (test_evicted_table_outlives_a_captured_graph)."""
+    torch = torch_cuda
+    mod = load("dc_level")
+    p0 = struct.pack("<f", 0.5)
+    mod.initialize_state(p0, 2, 48000.0)
+    x = torch.zeros((2, 512 * 4), device="cuda")
+    most = 0
+    for i in range(40):
+        v = 0.01 * (i + 1)
+        p = struct.pack("<f", v)
+        y = d.render_offline(x, 2, 512, 48000.0, mod.plugin(p, "dc_level"))
+        assert bool((y == torch.tensor(v, dtype=torch.float32)).all())
+        most = max(most, mod.retired_tables())
+    torch.cuda.synchronize()
+    assert mod.retired_tables() == 0
+    assert most <= 8, most
+
+
 def test_verify_class_reports_and_catches_a_wrong_class(torch_cuda):
     """DSP_EXEC_VERIFY_CLASS, the second line of defence: a proven class is
     checked against the callback on four blocks of the call's own input

@@ -177,3 +177,29 @@ def test_constructs_outside_the_model(case):
         assert f["reads_block"]
     if case != "f64":
         assert not f["gain_form"]
+
+
+def test_state_written_through_a_pure_calls_pointer():
+    """a pointer a pure call returns (llvm.ptrmask, from
+    __builtin_align_down) keeps the origin of its argument -- a State store
+    through it is a State write (no parallel blocks), or the analysis stops;
+    either way the blocks are not taken as independent."""
+    src = ("#include \"plugin_header.h\"\n"
+           "struct Parameters { FLOAT_PARAM(0.0f, 1.0f) g; };\nstruct State { float z[8]; };\n"
+           "Parameters default_parameters() { Parameters p = {0.5f}; return p; }\n"
+           "State initialize_state(const Parameters &p, const unsigned C, const float sr, void *ctx) "
+           "{ State s = {}; return s; }\n"
+           "void audio_callback(const Parameters &p, State &st, float **out, const u32 C, const u32 B, "
+           "const real32 sr) {\n"
+           "    float *q = __builtin_align_down(&st.z[5], 16);\n"
+           "    q[0] += out[0][0];\n"
+           "    for (u32 s = 0; s < B; ++s) out[0][s] *= p.g + q[1];\n}\n")
+    f = dm.analyze_source(src)
+    assert (not f["analyzed"]) or f["writes_state"], f
+
+
+def test_no_fixpoint_means_no_facts():
+    """The analysis reports `analyzed` only when its dataflow settled; the
+    stock and test plugins all settle (above)."""
+    f = facts_of(os.path.join(PLUG, "state_shaper.cpp"))
+    assert f["analyzed"] and f["why"] != "no fixpoint after 64 passes"

@@ -28,13 +28,18 @@ LIB = os.environ.get("DSPBENCH_LIB", os.path.join(ROOT, "dsp-bench_amd", "libdsp
 OUT = os.environ.get("DSPB_MODULES_DIR", os.path.join(ROOT, "dsp-bench_amd", "modules"))
 
 
+# this repository's own example plugins (no reference needed)
+OWN = [os.path.join(ROOT, "dsp-bench_amd", "plugins", "biquad.cpp")]
+
+
 def main():
     ref = sys.argv[1] if len(sys.argv) > 1 else "/root/reference"
     import dspbench.module as m
     out = OUT
     os.makedirs(out, exist_ok=True)
-    for p in PLUGINS:
-        src = os.path.join(ref, p + ".cpp")
+    srcs = [os.path.join(ref, p + ".cpp") for p in PLUGINS] if os.path.isdir(os.path.join(ref, "build")) else []
+    for src in srcs + OWN:
+        p = os.path.splitext(src)[0]
         dst = os.path.join(out, f"mod_{os.path.basename(p)}.co")
         # the driver kernels (csrc/module.cpp) are compiled into every module:
         # rebuild when the library is newer too
