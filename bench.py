@@ -383,6 +383,29 @@ def bench_ir(args, dev, world, rank):
         print(json.dumps(line), flush=True)
 
 
+GATHER_TIMEOUT_RC = 3  # the process's exit status when the gather pass timed out
+
+
+def start_gather_watchdog(seconds: float, rank: int, emit, exit_fn=None):
+    """A gather that never completes (a peer lost, a transport hang) must not
+    take the measured line with it, nor pass for a good run: after `seconds`
+    the rank prints the line with the error (rank 0; `emit`) and leaves with
+    GATHER_TIMEOUT_RC, so the launcher and the driver see a failed run.
+    Returns the timer (cancel() it when the gather finishes)."""
+    import threading
+    exit_fn = exit_fn or os._exit
+
+    def _expired():
+        print(f"rank {rank}: the gather pass exceeded {seconds} s", file=sys.stderr, flush=True)
+        emit(None, f"timed out after {seconds} s")
+        sys.stdout.flush()
+        exit_fn(GATHER_TIMEOUT_RC)
+    dog = threading.Timer(seconds, _expired)
+    dog.daemon = True
+    dog.start()
+    return dog
+
+
 def rank_launch_cmd(n: int, argv: list[str]) -> list[str]:
     """`bench.py --gpus N` started outside a launcher: the N ranks come from
     torch.distributed.run in a child process (one process per GPU, rendezvous
@@ -928,18 +951,9 @@ def main():
         print(json.dumps(line), flush=True)
 
     if gather_pending:
-        # a watchdog: a gather that never completes (a peer lost, a transport
-        # hang) must not take the measured line with it -- every rank stops
-        # after --gather-timeout s, rank 0 printing the line with the error
-        import threading
-
-        def _expired():
-            print(f"rank {rank}: the gather pass exceeded {args.gather_timeout} s", file=sys.stderr, flush=True)
-            emit(None, f"timed out after {args.gather_timeout} s")
-            os._exit(0)
-        dog = threading.Timer(args.gather_timeout, _expired)
-        dog.daemon = True
-        dog.start()
+        # every rank stops after --gather-timeout s, rank 0 printing the line
+        # with the error, all with a non-zero status
+        dog = start_gather_watchdog(args.gather_timeout, rank, emit)
         try:
             comm = d.shard.TorchComm(device=local) if rehearsal else d.shard.RcclComm.from_torch(device=local)
             Ctot = world if wl == "ch96k" else CH

@@ -1294,7 +1294,12 @@ int dsp_render_loop(const float *const *in, uint32_t in_channels, uint64_t L, ui
     SampleMap map;
     int st = plugin_map(plugin, B, g.dev, s, &map, sr, ex ? ex->flags : 0);
     if (st) return st;
-    if ((st = specialize_generic(&map, C, B, s, ex, false, &hold))) return st;
+    // DSP_EXEC_VERIFY_CLASS: loop mode renders with the callback on every
+    // block (as an in-place call does) rather than a class it would not check
+    const bool verify = ex && (ex->flags & DSP_EXEC_VERIFY_CLASS);
+    const MapKind before = map.kind;
+    if ((st = specialize_generic(&map, C, B, s, ex, verify, &hold))) return st;
+    set_result(ex, before == MapKind::Generic && map.kind != MapKind::Generic ? DSP_RESULT_CLASS : 0u);
     if ((st = ensure_ramp_table(map, s))) return st;
     const uint32_t in_ch = std::min(in_channels, C);  // channels_to_write (audio.cpp:66)
     auto wrap = [&](const float *const *src, float *const *dst, uint32_t nc, const SampleMap &m) -> int {

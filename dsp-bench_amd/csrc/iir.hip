@@ -123,7 +123,7 @@ __device__ __forceinline__ void matvec(const float *m, const float (&v)[D], floa
     }
 }
 
-template <int S>
+template <int S, bool kChain>
 __global__ __launch_bounds__(256) void biquad_scan_kernel(BiquadArgs A) {
     constexpr int D = 2 * S;
     __shared__ float lds[kIirWaves][64 * kIirLdsStride];
@@ -238,7 +238,7 @@ __global__ __launch_bounds__(256) void biquad_scan_kernel(BiquadArgs A) {
         return true;
     };
     publish(A.aggw, agg);
-    if (A.window) {
+    if constexpr (!kChain) {
         // a filter whose transition decays: S_in = sum_{k < W} M^(64 T k)
         // agg_(i-1-k), every older tile's weight being below 2^-48 (the host
         // picked W).  Aggregates only, summed in a fixed order: no chain of
@@ -369,11 +369,17 @@ int launch_biquad(const BiquadArgs &A, uint32_t sections, hipStream_t s) {
     if (waves == 0) return DSP_OK;
     const uint64_t groups = (waves + kIirWaves - 1) / kIirWaves;
     if (groups > 0x7fffffffull || A.C == 0 || A.C > (uint32_t)kMaxChannels) return DSP_ERR_INVALID;
-    switch (sections) {
-    case 1: hipLaunchKernelGGL(biquad_scan_kernel<1>, dim3((uint32_t)groups), dim3(256), 0, s, A); break;
-    case 2: hipLaunchKernelGGL(biquad_scan_kernel<2>, dim3((uint32_t)groups), dim3(256), 0, s, A); break;
-    case 3: hipLaunchKernelGGL(biquad_scan_kernel<3>, dim3((uint32_t)groups), dim3(256), 0, s, A); break;
-    case 4: hipLaunchKernelGGL(biquad_scan_kernel<4>, dim3((uint32_t)groups), dim3(256), 0, s, A); break;
+    const dim3 grid((uint32_t)groups), blk(256);
+    const bool chain = A.window == 0;
+    switch (sections * 2 + (chain ? 1 : 0)) {
+    case 2: hipLaunchKernelGGL((biquad_scan_kernel<1, false>), grid, blk, 0, s, A); break;
+    case 3: hipLaunchKernelGGL((biquad_scan_kernel<1, true>), grid, blk, 0, s, A); break;
+    case 4: hipLaunchKernelGGL((biquad_scan_kernel<2, false>), grid, blk, 0, s, A); break;
+    case 5: hipLaunchKernelGGL((biquad_scan_kernel<2, true>), grid, blk, 0, s, A); break;
+    case 6: hipLaunchKernelGGL((biquad_scan_kernel<3, false>), grid, blk, 0, s, A); break;
+    case 7: hipLaunchKernelGGL((biquad_scan_kernel<3, true>), grid, blk, 0, s, A); break;
+    case 8: hipLaunchKernelGGL((biquad_scan_kernel<4, false>), grid, blk, 0, s, A); break;
+    case 9: hipLaunchKernelGGL((biquad_scan_kernel<4, true>), grid, blk, 0, s, A); break;
     default: return DSP_ERR_INVALID;
     }
     DSPB_HIP(hipGetLastError());

@@ -124,6 +124,7 @@ int invalid(const char *msg) {
 int run(const Source &src, uint32_t C, uint32_t B, float sr, const dsp_plugin *plugin, bool stft, uint32_t N,
         uint32_t H, int32_t window, uint32_t K, float *const *out, float *const *mag, uint64_t ld, uint64_t chunk,
         const dsp_exec *ex) {
+    if (ex && ex->result) *ex->result = 0;  // the chunks' DSP_RESULT_* bits are OR-ed in
     if (B == 0 || C == 0) return B == 0 ? invalid("block size B must be > 0") : DSP_OK;
     if (!out) return invalid("out is NULL");
     for (uint32_t c = 0; c < C; ++c)
@@ -274,6 +275,8 @@ int run(const Source &src, uint32_t C, uint32_t B, float sr, const dsp_plugin *p
         e.flags = ex ? (ex->flags & DSP_EXEC_METHOD_FLAGS) : 0;
         e.stream = cs;
         e.sample_offset = goff + c.start;
+        uint32_t chunk_res = 0;  // DSP_RESULT_* of this chunk, OR-ed into the caller's
+        e.result = &chunk_res;
         std::vector<const float *> rin(Cin);
         std::vector<float *> rout(C), rmag(C);
         if (Cin && src.wav()) {
@@ -299,6 +302,7 @@ int run(const Source &src, uint32_t C, uint32_t B, float sr, const dsp_plugin *p
         else
             st = dsp_render_offline(rin.data(), Cin, nin, rout.data(), C, B, sr, plugin, &e);
         if (st) return st;
+        if (ex && ex->result) *ex->result |= chunk_res;
         PL_HIP(hipEventRecord(s.comp_done, cs));
         // ---- download the owned rows
         const uint64_t rlen = (c.start + c.owned >= L) ? Lpad - c.start : c.owned;

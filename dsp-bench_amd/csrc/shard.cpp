@@ -628,6 +628,7 @@ int dsp_render_stft_sharded(const float *const *in, uint32_t in_channels, uint64
                             const dsp_plugin *plugin, uint32_t N, uint32_t H, int32_t window, uint32_t K,
                             const dsp_shard *sh, uint64_t chunk, dsp_comm *comm, uint32_t root,
                             float *const *all_out, float *const *all_mag, const dsp_exec *ex) {
+    if (ex && ex->result) *ex->result = 0;  // the chunks' DSP_RESULT_* bits are OR-ed in
     if (!sh || B == 0 || H == 0 || N < H) return invalid("dsp_render_stft_sharded: bad arguments");
     if (ex && (ex->flags & DSP_EXEC_HOST_BUFFERS)) return invalid("dsp_render_stft_sharded: device buffers only");
     if (in_channels > sh->channels) return invalid("in_channels %u > the shard's %u channels", in_channels, sh->channels);
@@ -717,12 +718,15 @@ int dsp_render_stft_sharded(const float *const *in, uint32_t in_channels, uint64
             e.flags = ex ? (ex->flags & DSP_EXEC_METHOD_FLAGS) : 0;
             e.stream = s;
             e.sample_offset = goff0 + c.start;
+            uint32_t chunk_res = 0;  // DSP_RESULT_* of this chunk, OR-ed into the caller's
+            e.result = &chunk_res;
             const uint64_t Fc = frames_of((Lc + B - 1) / B * B, N, H);
             if (Fc > c.frames && c.frames) return invalid("chunk plan: %llu frames computed, %llu owned",
                                                           (unsigned long long)Fc, (unsigned long long)c.frames);
             int st = dsp_render_stft(cin.data(), in_channels, Lc, cout.data(), nrow, B, sr, plugin, N, H, window, K,
                                      cmag.data(), ld, &e);
             if (st) return st;
+            if (ex && ex->result) *ex->result |= chunk_res;
         }
         if (!gather) continue;
         // gather step t to the root on the comm stream, behind its compute

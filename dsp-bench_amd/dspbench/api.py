@@ -153,8 +153,9 @@ _tls = threading.local()
 
 
 def last_result() -> int:
-    """dsp_exec.result of this thread's last render_offline / render_stft
-    (DSP_RESULT_CLASS / _VERIFIED / _RERENDERED bits)."""
+    """dsp_exec.result of this thread's last render_offline / render_stft /
+    render_loop / render_stft_host (DSP_RESULT_CLASS / _VERIFIED / _RERENDERED
+    bits; the chunked driver ORs its chunks' bits)."""
     return getattr(_tls, "result", 0)
 
 
@@ -198,11 +199,13 @@ def render_loop(file, C_out: int, B: int, nblocks: int, sr: float, plugin: Plugi
     ex = _exec(oref, sample_offset, stream)
     ps = plugin.as_struct() if plugin is not None else None
     ex.flags |= plugin.exec_flags if plugin is not None else 0
+    res = _track(ex)
     cur = C.c_uint64()
     st = L.lib().dsp_render_loop(chan_table(in_ptrs) if in_ptrs else None, len(in_ptrs), L_, cursor,
                                  chan_table(out_ptrs), C_out, B, nblocks, sr,
                                  C.byref(ps) if ps is not None else None, C.byref(cur), C.byref(ex))
     check(st, "dsp_render_loop")
+    _tls.result = res.value
     return out[:, : nblocks * B], cur.value
 
 
@@ -275,12 +278,14 @@ def render_stft_host(x, C_out: int, B: int, sr: float, plugin: Plugin | None, st
     ex = dsp_exec(device, 0, C.c_void_p(stream) if stream else None, sample_offset)
     ps = plugin.as_struct() if plugin is not None else None
     ex.flags |= plugin.exec_flags if plugin is not None else 0
+    res = _track(ex)
     st = L.lib().dsp_render_stft_host(chan_table(in_ptrs) if in_ptrs else None, len(in_ptrs), L_,
                                       chan_table([ptr(out, c) for c in range(C_out)]), C_out, B, sr,
                                       C.byref(ps) if ps is not None else None, N, H, window, K,
                                       chan_table([ptr(mag, c) for c in range(C_out)]) if stft else None, K, chunk,
                                       C.byref(ex))
     check(st, "dsp_render_stft_host")
+    _tls.result = res.value
     return out[:, :Lp], (mag[:, :F] if stft else None)
 
 

@@ -111,7 +111,11 @@ typedef struct dsp_plugin {
                                       stream synchronisation (dsp_render_offline / dsp_render_stft).
                                       A call whose output rows overlap its input rows (in place)
                                       runs the callback on every block instead: the check and a
-                                      re-render need the input after the render */
+                                      re-render need the input after the render.  Honoured by
+                                      dsp_render_offline and dsp_render_stft, and per chunk by the
+                                      chunked (dsp_render_stft_host / _wav) and sharded drivers,
+                                      whose result ORs their chunks' bits; dsp_render_loop with
+                                      the flag runs the callback on every block (result 0) */
 /* the flags that choose how a call computes (not where its buffers live):
  * the chunked and sharded drivers pass them on to every chunk */
 #define DSP_EXEC_METHOD_FLAGS (DSP_EXEC_FIR_DIRECT | DSP_EXEC_NO_SPECIALIZE | DSP_EXEC_VERIFY_CLASS)

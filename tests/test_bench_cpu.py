@@ -73,3 +73,32 @@ def test_world_mismatch_exits_nonzero():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4"], env=env,
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 2 and "WORLD_SIZE=2" in r.stderr
+
+
+def test_gather_watchdog_prints_the_line_and_fails(bench):
+    """A gather pass that never finishes: the watchdog prints the line (with
+    the error) and exits with a non-zero status, so a hung gather shows in
+    the run's rc."""
+    import threading
+    done = threading.Event()
+    got = {}
+
+    def emit(ms, err):
+        got["line"] = (ms, err)
+
+    def fake_exit(rc):
+        got["rc"] = rc
+        done.set()
+    bench.start_gather_watchdog(0.05, 0, emit, exit_fn=fake_exit)
+    assert done.wait(5.0)
+    assert got["rc"] == bench.GATHER_TIMEOUT_RC != 0
+    assert got["line"][0] is None and "timed out" in got["line"][1]
+
+
+def test_gather_watchdog_cancelled_in_time(bench):
+    called = []
+    dog = bench.start_gather_watchdog(0.5, 0, lambda *a: called.append(a), exit_fn=lambda rc: called.append(rc))
+    dog.cancel()
+    import time
+    time.sleep(0.7)
+    assert called == []

@@ -428,3 +428,40 @@ def test_arena_overflow_leaves_room_for_later_allocations(torch_cuda):
     assert e.value.status == d._lib.DSP_ERR_NOMEM
     big, small = struct.unpack("<QQ", mod.read_state())
     assert big == 0 and small != 0
+
+
+@pytest.mark.gpu
+def test_fast_math_divergence_is_bounded(torch_cuda, oracle):
+    """The reference JIT compiles plugins with -Ofast -ffast-math
+    (compiler.cpp:507-515); the product's module compiles IEEE (-O3
+    -ffp-contract=off).  tests/plugins/fastmath_sum.cpp's four-term sum over a
+    parameter is what fast-math rewrites (reassociation, a reciprocal
+    multiply): the GPU render equals the IEEE float32 semantics bit for bit,
+    and the -Ofast CPU build (oracle/_ref/libplug_fastmath_sum.so) differs from
+    it in a share of the samples, by at most 8 u (sum |terms|) / |div|, u =
+    2^-24 (measured 4.34 u on this input; INTEGRATION.md "Fast math")."""
+    path = os.path.join(os.path.dirname(HERE), "tests", "plugins", "fastmath_sum.cpp")
+    if not os.path.exists(os.path.join(REF, "libplug_fastmath_sum.so")):
+        pytest.skip("oracle/_ref not built")
+    mod = d.module.Module(d.module.compile_source(open(path).read(), "fastmath_sum.cpp"))
+    params = mod.default_parameters()
+    mod.initialize_state(params, 2, 48000.0)
+    x = np.random.default_rng(1).uniform(-1, 1, (2, 100_000)).astype(np.float32)
+    got = d.render_offline(torch_cuda.from_numpy(x).cuda(), 2, 512, 48000.0, mod.plugin(params)).cpu().numpy()
+    n = got.shape[1]
+    xp = np.zeros((2, n), np.float32)
+    xp[:, :x.shape[1]] = x
+    blocks = xp.reshape(2, -1, 512)
+    lag = [np.zeros_like(blocks) for _ in range(4)]
+    lag[0] = blocks
+    for k in (1, 2, 3):
+        lag[k][:, :, k:] = blocks[:, :, :-k]
+    div = np.float32(struct.unpack("<f", params)[0])
+    ieee = ((((lag[0] + lag[1]) + lag[2]) + lag[3]) / div).reshape(2, n)
+    mag = ((np.abs(lag[0]) + np.abs(lag[1]) + np.abs(lag[2]) + np.abs(lag[3])) / float(div)).reshape(2, n)
+    assert np.array_equal(got, ieee)
+    ref = oracle.RefPlugin("fastmath_sum", 2, 48000.0, prefix="libplug_")
+    cpu = oracle.render_offline([x[0], x[1]], 2, 512, 48000.0, ref.as_oracle())
+    diff = np.abs(cpu.astype(np.float64) - got)
+    assert 0.0 < float(np.mean(cpu != got)) < 1.0        # fast-math moved some samples, not all
+    assert float(np.max(diff / np.maximum(mag, 1e-30))) <= 8 * 2.0 ** -24

@@ -368,3 +368,31 @@ def test_verify_class_reports_and_catches_a_wrong_class(torch_cuda):
     out, mag = d.render_stft(xg, 2, B, 48000.0, mod.plugin(params, "gul", verify=True), window=d.DSP_WIN_HANN)
     assert last_result() == L.DSP_RESULT_CLASS | L.DSP_RESULT_RERENDERED
     assert np.array_equal(out.cpu().numpy(), want)
+
+
+def test_verify_class_result_through_every_driver(torch_cuda):
+    """DSP_EXEC_VERIFY_CLASS reported by the chunked driver (the
+    chunks' bits OR-ed into the caller's result) and by loop mode (which then
+    runs the callback on every block: result 0, the plugin's rows)."""
+    torch = torch_cuda
+    import dspbench._lib as L
+    from dspbench.api import last_result
+    mods = os.path.join(os.path.dirname(HERE), "dsp-bench_amd", "modules")
+    if not os.path.exists(os.path.join(mods, "mod_gain_test.co")):
+        pytest.skip("modules not built")
+    with open(os.path.join(mods, "mod_gain_test.co"), "rb") as f:
+        gmod = d.module.Module(f.read())
+    gp = gmod.default_parameters()
+    gmod.initialize_state(gp, 2, 48000.0)
+    g = np.float32(struct.unpack("<f", gp[:4])[0])
+    xh = np.random.default_rng(4).uniform(-1, 1, (2, 512 * 300 + 11)).astype(np.float32)
+    out, _ = d.render_stft_host(xh, 2, 512, 48000.0, gmod.plugin(gp, "gain_test", verify=True), stft=True,
+                                chunk=1 << 16)
+    assert last_result() == L.DSP_RESULT_CLASS | L.DSP_RESULT_VERIFIED
+    assert np.array_equal(out[:, :xh.shape[1]], xh * g)
+    x = torch.from_numpy(xh[:, :5000]).cuda()
+    y, _ = d.render_loop(x, 2, 512, 30, 48000.0, gmod.plugin(gp, "gain_test", verify=True), cursor=100)
+    assert last_result() == 0
+    y2, _ = d.render_loop(x, 2, 512, 30, 48000.0, gmod.plugin(gp, "gain_test"), cursor=100)
+    assert last_result() == L.DSP_RESULT_CLASS
+    assert torch.equal(y, y2)
