@@ -298,15 +298,9 @@ static bool g_timing = false;
 // launch cost more than the records themselves
 static std::map<int, std::vector<hipEvent_t>> g_event_pool;
 
-#ifdef DSPB_AB_BUILD
-// A/B and ablation options of stft8192_pk_kernel (stft_pk.hpp kPk* bits),
-// only in the tools build (make ab -> build/ab/libdspbench_ab.so).  Thread
-// local: a thread's A/B switch never changes another thread's kernel.
-static thread_local int g_pk_ab_opt = 0;
-static int pk_options() { return g_pk_ab_opt; }
-#else
-static int pk_options() { return 0; }
-#endif
+// A/B and ablation options of stft8192_pk_kernel: 0 in the product library
+// (the tools build's stft_pk_ab.hip sets them per thread)
+static int pk_options() { return stft_pk_ab_options(); }
 
 // a closed-form IR ramp (plugin_map) leaves the block table unbuilt; every
 // fused path but stft_pk's PER path reads it
@@ -1110,13 +1104,6 @@ extern "C" {
 int dsp_abi_version(void) { return DSPBENCH_ABI_VERSION; }
 
 
-#ifdef DSPB_AB_BUILD
-int dsp_stft_pk_ab_options(int opt) {
-    const int old = g_pk_ab_opt;
-    if (opt >= 0 && opt <= 0x3fffff) g_pk_ab_opt = opt;
-    return old;
-}
-#endif
 
 void dsp_kernel_timing_enable(int on) {
     std::lock_guard<std::mutex> lk(g_mu);

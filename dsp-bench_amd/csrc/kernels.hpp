@@ -143,6 +143,7 @@ int launch_wav_decode(const uint8_t *payload, uint32_t C, uint16_t bits, bool is
 int launch_wav_encode(uint8_t *payload, uint32_t C, uint16_t bits, bool is_float, uint64_t frames,
                       const ChanOut &in, hipStream_t s);
 bool stft8192_pk_per_path(const Stft8kArgs &A, bool fused);
+int stft_pk_ab_options();  // A/B option bits of this thread: 0 unless the tools build (stft_pk_ab.hip) set them
 int launch_stft8192_pk(const Stft8kArgs &A, uint32_t C, bool fused, int opt, hipStream_t s);
 int launch_fft_generic(const GenericFftArgs &A, uint64_t transforms, uint32_t C, hipStream_t s);
 int launch_gain(const float *in, float *out, float g, uint64_t n, hipStream_t s);

@@ -99,14 +99,17 @@ struct Resources {
         if (compute_used) (void)hipStreamSynchronize(compute);
         if (down) (void)hipStreamSynchronize(down);
         (void)hipGetLastError();
+        // downloads that never landed (SdmaDownloader::poisoned): the engine
+        // may still read the device rows and write the pinned ones -- keep both
+        const bool keep = dl.poisoned();
         for (Slot &s : slots) {
             if (s.d_up) (void)hipFree(s.d_up);
             if (s.d_in) (void)hipFree(s.d_in);
-            if (s.d_out) (void)hipFree(s.d_out);
-            if (s.d_mag) (void)hipFree(s.d_mag);
+            if (s.d_out && !keep) (void)hipFree(s.d_out);
+            if (s.d_mag && !keep) (void)hipFree(s.d_mag);
             if (s.h_up) (void)hipHostFree(s.h_up);
-            if (s.h_out) (void)hipHostFree(s.h_out);
-            if (s.h_mag) (void)hipHostFree(s.h_mag);
+            if (s.h_out && !keep) (void)hipHostFree(s.h_out);
+            if (s.h_mag && !keep) (void)hipHostFree(s.h_mag);
             for (hipEvent_t e : {s.up_done, s.comp_done, s.down_done})
                 if (e) (void)hipEventDestroy(e);
         }

@@ -175,12 +175,8 @@ __global__ __launch_bounds__(256) void ew_vec_kernel(const float *a, const float
     for (int u = 0; u < kVecU; ++u) {
         const uint64_t q = q0 + 256u * (uint32_t)u;
         if (q >= n4) continue;
-        if constexpr (OP == Ew::Set)  // a pure write stream: plain stores (DSPB_SET_NT: A/B)
-#ifdef DSPB_SET_NT
-            __builtin_nontemporal_store(f4nt{r[u].x, r[u].y, r[u].z, r[u].w}, reinterpret_cast<f4nt *>(out) + q);
-#else
+        if constexpr (OP == Ew::Set)  // a pure write stream: plain stores
             reinterpret_cast<float4 *>(out)[q] = r[u];
-#endif
         else
             __builtin_nontemporal_store(f4nt{r[u].x, r[u].y, r[u].z, r[u].w}, reinterpret_cast<f4nt *>(out) + q);
     }

@@ -253,8 +253,11 @@ void SdmaDownloader::run() {
             while (h.signal_wait_scacquire(sig, HSA_SIGNAL_CONDITION_LT, want, 1000000ull, HSA_WAIT_STATE_BLOCKED) >=
                    want) {
                 if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(kCopyTimeoutS)) {
-                    set_last_error("SDMA download: copies did not land within %d s", kCopyTimeoutS);
+                    set_last_error("SDMA download: copies did not land within %d s (their buffers are kept: "
+                                   "the engine may still write them)", kCopyTimeoutS);
                     if (!st) st = DSP_ERR_HIP;
+                    std::lock_guard<std::mutex> g(mu_);
+                    poisoned_ = true;
                     break;
                 }
             }
@@ -269,7 +272,13 @@ void SdmaDownloader::run() {
         }
         cv_.notify_all();
     }
-    if (sig.handle) h.signal_destroy(sig);
+    // a copy still in flight may decrement the signal: keep it then (leaked)
+    bool keep = false;
+    {
+        std::lock_guard<std::mutex> g(mu_);
+        keep = poisoned_;
+    }
+    if (sig.handle && !keep) h.signal_destroy(sig);
 }
 
 }  // namespace dspb

@@ -45,6 +45,13 @@ public:
     int wait_slot(int slot);
     // drain and stop the worker; the first error of any copy
     int finish();
+    // a copy did not land within the bounded wait: the engine may still
+    // write the destinations and read the sources, so their owners must keep
+    // them (the worker keeps its signal for the same reason)
+    bool poisoned() {
+        std::lock_guard<std::mutex> g(mu_);
+        return poisoned_;
+    }
 
 private:
     struct Job {
@@ -59,7 +66,7 @@ private:
     std::condition_variable cv_;
     std::deque<Job> q_;
     std::vector<uint64_t> submitted_, landed_;
-    bool stop_ = false, started_ = false;
+    bool stop_ = false, started_ = false, poisoned_ = false;
     int err_ = 0;
     std::string msg_;  // the worker's error text, re-raised on the caller's thread
 };

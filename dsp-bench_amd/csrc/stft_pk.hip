@@ -56,9 +56,10 @@ int launch_stft8192_pk(const Stft8kArgs &A, uint32_t C, bool fused, int opt, hip
     if (fused && A.map.kind == MapKind::Ramp && pow2 && winc) {
         // period of the block table in units of 128 samples
         const uint32_t per = A.map.B <= 128u ? 1u : A.map.B / 128u;
-#ifdef DSPB_AB_BUILD
-        if (per == 4 && opt) return launch_pk_ab(A, fused, opt, grid, stream);  // A/B at the headline shape
-#endif
+        if (per == 4 && opt) {  // A/B at the headline shape (the tools build only: stft_pk_ab.hip)
+            int st = DSP_OK;
+            if (stft_pk_ab_dispatch(A, C, fused, opt, grid, stream, &st)) return st;
+        }
 #define DSPB_PK_PER(p) \
     hipLaunchKernelGGL((stft8192_pk_kernel<kSrcRender, kKHalf, MapKind::Ramp, true, true, p, kPkPerOpt>), grid_per, \
                        dim3(64 * kPkPerWpb), 0, stream, A)
@@ -77,14 +78,18 @@ int launch_stft8192_pk(const Stft8kArgs &A, uint32_t C, bool fused, int opt, hip
         DSPB_HIP(hipGetLastError());
         return DSP_OK;
     }
-#ifdef DSPB_AB_BUILD
-    if (!fused && winc && (opt & kPkMemPf)) return launch_mem_pf(A, C, stream);
-    if (!fused && winc && (opt & kPkMemHop)) return launch_mem_hop(A, C, stream);
-    if (!fused && winc && (opt & kPkMemAos)) return launch_pk_ab(A, fused, opt, grid, stream);
-#else
-    (void)opt;  // the A/B options exist only in the tools build (make ab)
-#endif
+    if (opt && !fused && winc) {  // memory-source A/B variants (the tools build only)
+        int st = DSP_OK;
+        if (stft_pk_ab_dispatch(A, C, fused, opt, grid, stream, &st)) return st;
+    }
     return launch_pk_paths(A, fused, km, pow2, winc, grid, stream);
 }
+
+// The product library has no A/B variants: these weak definitions stand
+// unless the tools build (make ab) links stft_pk_ab.hip, which defines both.
+__attribute__((weak)) bool stft_pk_ab_dispatch(const Stft8kArgs &, uint32_t, bool, int, dim3, hipStream_t, int *) {
+    return false;
+}
+__attribute__((weak)) int stft_pk_ab_options() { return 0; }
 
 }  // namespace dspb

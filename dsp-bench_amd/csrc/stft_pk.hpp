@@ -67,10 +67,7 @@ constexpr int kPkDefaultOpt = kPkNoBarDft | kPkNoBarTw | kPkNoBarSplit;
 // 0.8-2.2% faster there, but 1-2% slower for the paths that read a signal
 // (memory, gain), whose four-frame workgroups share their hops in L2
 // (profiles/r02_w1_ab.txt)
-#ifndef DSPB_PK_PER_EXTRA
-#define DSPB_PK_PER_EXTRA 0  // extra option bits of the PER kernels (A/B builds)
-#endif
-constexpr int kPkPerOpt = kPkDefaultOpt | kPkW1 | DSPB_PK_PER_EXTRA;
+constexpr int kPkPerOpt = kPkDefaultOpt | kPkW1;
 
 typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));  // a row is only dword-aligned
 typedef float f4a __attribute__((ext_vector_type(4)));               // 16-byte aligned
@@ -561,8 +558,9 @@ void stft8192_pk_kernel(Stft8kArgs A) {
 
 // the launches of stft_pk_paths.hip / stft_pk_ab.hip (DSP_OK or a status)
 int launch_pk_paths(const Stft8kArgs &A, bool fused, int km, bool pow2, bool winc, dim3 grid, hipStream_t s);
-int launch_pk_ab(const Stft8kArgs &A, bool fused, int opt, dim3 grid, hipStream_t s);
-int launch_mem_pf(const Stft8kArgs &A, uint32_t C, hipStream_t s);
-int launch_mem_hop(const Stft8kArgs &A, uint32_t C, hipStream_t s);
+// the A/B and ablation variants (tools build, stft_pk_ab.hip): launches the
+// variant `opt` selects and returns true, or false when it has none for A
+bool stft_pk_ab_dispatch(const Stft8kArgs &A, uint32_t C, bool fused, int opt, dim3 grid, hipStream_t s, int *st);
+
 
 }  // namespace dspb

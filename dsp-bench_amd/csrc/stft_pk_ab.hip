@@ -181,7 +181,7 @@ void stft8192_mem_hop_kernel(Stft8kArgs A) {
     split_y2<kKHalf, false>(Y2, A.mag.p[ch] + (f0 + wave) * A.ld, A.K, A.tw, lane, lds);
 }
 
-int launch_mem_hop(const Stft8kArgs &A, uint32_t C, hipStream_t stream) {
+static int launch_mem_hop(const Stft8kArgs &A, uint32_t C, hipStream_t stream) {
     // H = 4096, whole frames, 4097 bins, 16-byte rows (the kernel's addressing)
     if (A.H != 4096u || A.valid < 8192u || A.K != 4097u || !A.wbase || A.in_ch < C) return DSP_ERR_INVALID;
     for (uint32_t c = 0; c < C; ++c)
@@ -192,7 +192,7 @@ int launch_mem_hop(const Stft8kArgs &A, uint32_t C, hipStream_t stream) {
     return DSP_OK;
 }
 
-int launch_mem_pf(const Stft8kArgs &A, uint32_t C, hipStream_t stream) {
+static int launch_mem_pf(const Stft8kArgs &A, uint32_t C, hipStream_t stream) {
     // H = 4096 and whole frames only (the kernel's addressing)
     if (A.H != 4096u || A.valid < 8192u || A.K != 4097u || !A.wbase) return DSP_ERR_INVALID;
     int dev = 0, cus = 0;
@@ -205,7 +205,7 @@ int launch_mem_pf(const Stft8kArgs &A, uint32_t C, hipStream_t stream) {
     return DSP_OK;
 }
 
-int launch_pk_ab(const Stft8kArgs &A, bool fused, int opt, dim3 grid_default, hipStream_t stream) {
+static int launch_pk_ab(const Stft8kArgs &A, bool fused, int opt, dim3 grid_default, hipStream_t stream) {
     // the variants below are four-wave workgroups; grid_default is sized for kPkWpb
     const dim3 grid((grid_default.x * kPkWpb + 3) / 4, grid_default.y);
     if (!fused) {  // kPkMemAos
@@ -290,4 +290,29 @@ int launch_pk_ab(const Stft8kArgs &A, bool fused, int opt, dim3 grid_default, hi
     return DSP_OK;
 }
 
+// the product's weak hooks (stft_pk.hip), defined here for the tools build
+bool stft_pk_ab_dispatch(const Stft8kArgs &A, uint32_t C, bool fused, int opt, dim3 grid, hipStream_t stream,
+                         int *st) {
+    if (fused) {
+        *st = launch_pk_ab(A, fused, opt, grid, stream);
+        return true;
+    }
+    if (opt & kPkMemPf) *st = launch_mem_pf(A, C, stream);
+    else if (opt & kPkMemHop) *st = launch_mem_hop(A, C, stream);
+    else if (opt & kPkMemAos) *st = launch_pk_ab(A, fused, opt, grid, stream);
+    else return false;
+    return true;
+}
+
+// A/B and ablation options of stft8192_pk_kernel (stft_pk.hpp kPk* bits),
+// thread local: a thread's A/B switch never changes another thread's kernel
+static thread_local int g_pk_ab_opt = 0;
+int stft_pk_ab_options() { return g_pk_ab_opt; }
+
 }  // namespace dspb
+
+extern "C" int dsp_stft_pk_ab_options(int opt) {
+    const int old = dspb::g_pk_ab_opt;
+    if (opt >= 0 && opt <= 0x3fffff) dspb::g_pk_ab_opt = opt;
+    return old;
+}
