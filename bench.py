@@ -92,9 +92,12 @@ def parse():
     ap.add_argument("--sections", type=int, default=1, choices=[1, 2, 3, 4],
                     help="biquad: sections in the cascade (1 = plugins/biquad.cpp's low-pass; more add RBJ "
                          "peaking / high-pass sections)")
-    ap.add_argument("--plugin", default=None, choices=["gain_test", "IR_test", "static_gain_plugin"],
+    ap.add_argument("--plugin", default=None,
+                    choices=["gain_test", "IR_test", "static_gain_plugin", "balance", "fade_in"],
                     help="generic / generic_stft: the reference plugin source (default gain_test / IR_test; "
-                         "static_gain_plugin = test/static_gain_plugin.cpp, a State the callback only reads)")
+                         "static_gain_plugin = test/static_gain_plugin.cpp, a State the callback only reads; "
+                         "balance / fade_in = tests/plugins/*.cpp, per-channel / per-position gains: the "
+                         "gain-table class)")
     ap.add_argument("--ir-plugin", default="source", choices=["source", "enum"],
                     help="headline / ch96k: source = the reference's IR_test.cpp compiled unchanged for gfx950 "
                          "(dsp-bench_amd/modules/mod_IR_test.co) and dispatched through its probed block class "
@@ -130,6 +133,8 @@ def source_plugin_name(pname: str, block_class: str) -> str:
     return (f"{pname}.cpp (DSP_PLUGIN_GENERIC, compiled unchanged from the reference source; block class "
             f"{block_class}: " + {"table": "its own callback's block, tiled, in the fused kernel",
                                   "gain": "the gain its callback gives, in the gain map",
+                                  "gain_table": "the per-(channel, position) gains its callback gives, in the "
+                                                "gain-table map",
                                   "callback": "the callback on every block"}[block_class] + ")")
 
 
@@ -629,7 +634,7 @@ def main():
                             "the render is extra traffic, not counted)")
             else:
                 kname = (f"{KERNEL}<render> (fused render + window + FFT + |X|; the render is the plugin's own "
-                         f"{'callback block, tiled' if block_class == 'table' else 'gain'})")
+                         f"{'callback block, tiled' if block_class == 'table' else block_class.replace('_', ' ')})")
                 alg_desc = ("fused: C*F*(4H + 4K) B (render write + |X| write; the plugin ignores its input)"
                             if block_class == "table" else
                             "fused gain: C*F*(4H + 4H + 4K) B (file read + render write + |X| write)")
@@ -886,6 +891,9 @@ def main():
                 "frames_per_gpu": CH * F if mag is not None else 0,
                 "sharding": ("one 96 kHz channel per GPU (a world-channel file, dsp_shard_plan CHANNELS, "
                              "dsp_render_stft_sharded), no data-path collective" if wl == "ch96k" else
+                             "one independent file per GPU (a stateful plugin's state crosses time chunks: it "
+                             "shards by channel or by file, never by time), no data-path collective"
+                             if wl in ("biquad", "biquad_src", "sine_src") else
                              "time-chunk per GPU, 4096-sample halo, no data-path collective"),
                 "render_gather_ms": None if gather_ms is None else round(gather_ms, 3),
                 "render_gather_error": gather_err,

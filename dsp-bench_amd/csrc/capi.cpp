@@ -66,7 +66,7 @@ struct IirTab {  // a biquad cascade's coefficients + state-transition powers (b
 // calls on one stream run in order, so a launch only meets words tagged with
 // its own epoch (zeroed at allocation; epochs run 1 .. 2^32 - 1)
 struct IirWork {
-    uint64_t *aggw = nullptr, *inclw = nullptr;  // cap * 8 words each, one allocation
+    uint64_t *aggw = nullptr, *inclw = nullptr;  // cap * 16 words each, one allocation
     uint64_t cap = 0;
     uint64_t epoch = 0;
 };
@@ -453,6 +453,8 @@ static bool ramp_closed_form(float gain, float step, uint32_t B) {
     return ok;
 }
 
+constexpr uint32_t kIirPairSections = 2;  // cascades of >= this many sections: channel pairs per wave
+
 // DSP_PLUGIN_BIQUAD (iir.hip): the cascade's zero-input state transition over
 // T = biquad_lane_samples() samples, M (D x D, D = 2 S, state = (y1, y2) per
 // section; section k's x history is section k-1's y history), simulated in
@@ -533,8 +535,8 @@ static uint32_t biquad_tables(const float *cf, uint32_t S, std::vector<float> &h
 
 // takes the stream's workspace for one launch (a fresh epoch) and launches,
 // under one lock: launches on a stream are enqueued in epoch order
-static int iir_launch(int dev, hipStream_t s, BiquadArgs *A, uint32_t sections) {
-    const uint64_t tiles = (uint64_t)A->C * A->ntiles_ch;
+static int iir_launch(int dev, hipStream_t s, BiquadArgs *A, uint32_t sections, uint32_t nch) {
+    const uint64_t tiles = (uint64_t)(A->C / nch) * A->ntiles_ch;
     {   // every launch takes a fresh epoch: a graph replay would reuse it
         hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
         if (hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) {
@@ -568,12 +570,12 @@ static int iir_launch(int dev, hipStream_t s, BiquadArgs *A, uint32_t sections) 
             w = IirWork{};
         }
         const uint64_t cap = std::max<uint64_t>(tiles, 1024);
-        const size_t bytes = 2 * cap * 8 * sizeof(uint64_t);
+        const size_t bytes = 2 * cap * 16 * sizeof(uint64_t);  // 16 words: a channel pair's 2 x 8
         void *p = nullptr;
         DSPB_HIP(hipMalloc(&p, bytes));
         DSPB_HIP(hipMemsetAsync(p, 0, bytes, s));
         w.aggw = (uint64_t *)p;
-        w.inclw = w.aggw + cap * 8;
+        w.inclw = w.aggw + cap * 16;
         w.cap = cap;
     }
     A->aggw = w.aggw;
@@ -581,7 +583,7 @@ static int iir_launch(int dev, hipStream_t s, BiquadArgs *A, uint32_t sections) 
     A->err = r.iir_err_dev;
     w.epoch = w.epoch % 0xffffffffull + 1;
     A->epoch = w.epoch;
-    if (int st = launch_biquad(*A, sections, s)) return st;
+    if (int st = launch_biquad(*A, sections, nch, s)) return st;
     return DSP_OK;
 }
 
@@ -786,6 +788,10 @@ static int specialize_generic(SampleMap *m, uint32_t C, uint32_t B, hipStream_t 
     } else if (sp.kind == kSpecGain) {
         m->kind = MapKind::Gain;
         m->a = sp.gain;
+    } else if (sp.kind == kSpecGainTable) {
+        m->kind = MapKind::GainTable;  // value = x * table[c B + (global sample) mod B]
+        m->table = sp.table;
+        m->closed = 0;
     }
     return DSP_OK;
 }
@@ -898,28 +904,37 @@ static int render_device(const float *const *in, uint32_t in_ch, uint64_t L, flo
         int dev = 0;
         DSPB_HIP(hipGetDevice(&dev));
         const uint32_t S = map.sections, D = 2 * S;
+        // channel pairs in one wavefront (packed math) from kIirPairSections
+        // sections on; an odd last channel on its own
+        const bool pairs = S >= kIirPairSections;
         for (uint32_t c0 = 0; c0 < C; c0 += kMaxChannels) {
             const uint32_t cn = (C - c0) < (uint32_t)kMaxChannels ? (C - c0) : kMaxChannels;
-            BiquadArgs A{};
-            A.in_aligned16 = A.out_aligned16 = 1;
-            for (uint32_t j = 0; j < cn; ++j) {
-                A.out.p[j] = out[c0 + j];
-                A.out_aligned16 &= aligned(out[c0 + j], 16) ? 1u : 0u;
-                if (c0 + j < in_ch) {
-                    A.in.p[j] = in[c0 + j];
-                    A.in_ch = j + 1;
-                    A.in_aligned16 &= aligned(in[c0 + j], 16) ? 1u : 0u;
+            const uint32_t np = pairs ? cn & ~1u : 0;
+            for (int part = 0; part < 2; ++part) {
+                const uint32_t first = part ? np : 0, count = part ? cn - np : np, nch = part ? 1 : 2;
+                if (!count) continue;
+                BiquadArgs A{};
+                A.in_aligned16 = A.out_aligned16 = 1;
+                for (uint32_t j = 0; j < count; ++j) {
+                    const uint32_t c = c0 + first + j;
+                    A.out.p[j] = out[c];
+                    A.out_aligned16 &= aligned(out[c], 16) ? 1u : 0u;
+                    if (c < in_ch) {
+                        A.in.p[j] = in[c];
+                        A.in_ch = j + 1;
+                        A.in_aligned16 &= aligned(in[c], 16) ? 1u : 0u;
+                    }
                 }
+                A.L = L;
+                A.Ly = end;
+                A.C = count;
+                A.ntiles_ch = biquad_tiles(end);
+                A.coef = map.iir_tab;
+                A.Q = map.iir_tab + 20;
+                A.P = A.Q + (size_t)65 * D * D;
+                A.window = map.iir_window;
+                if (int st = iir_launch(dev, s, &A, S, nch)) return st;
             }
-            A.L = L;
-            A.Ly = end;
-            A.C = cn;
-            A.ntiles_ch = biquad_tiles(end);
-            A.coef = map.iir_tab;
-            A.Q = map.iir_tab + 20;
-            A.P = A.Q + (size_t)65 * D * D;
-            A.window = map.iir_window;
-            if (int st = iir_launch(dev, s, &A, S)) return st;
         }
         return DSP_OK;
     }
@@ -997,6 +1012,7 @@ static int render_device(const float *const *in, uint32_t in_ch, uint64_t L, flo
         A.start = start;
         A.end = end;
         A.map = map;
+        if (map.kind == MapKind::GainTable) A.map.table += (uint64_t)c0 * map.B;  // this group's rows
         A.goff = goff;
         int st = launch_render(A, cn, vec, s);
         if (st) return st;
@@ -1304,12 +1320,14 @@ int dsp_render_loop(const float *const *in, uint32_t in_channels, uint64_t L, ui
             A.start = 0;
             A.end = Lr;
             A.map = m;
+            if (m.kind == MapKind::GainTable) A.map.table += (uint64_t)c0 * m.B;  // this group's rows
             A.goff = goff_of(ex);
             if (int e = launch_render_wrap(A, cn, cursor, s)) return e;
         }
         return DSP_OK;
     };
-    if (map.kind == MapKind::Noop || map.kind == MapKind::Gain || map.kind == MapKind::Ramp)
+    if (map.kind == MapKind::Noop || map.kind == MapKind::Gain || map.kind == MapKind::Ramp ||
+        map.kind == MapKind::GainTable)
         return (st = wrap(in, out, C, map)) ? st : finish(ex);
     // FIR / GENERIC: the wrapped file is materialised (the plugin's block
     // stream), then rendered as a one-shot file of nblocks B samples
@@ -1467,6 +1485,7 @@ int dsp_render_stft(const float *const *in, uint32_t in_channels, uint64_t L,
             A.scale = (float)(1.0 / std::sqrt((double)N));
             if ((st = set_wincomp(g.dev, s, window, &A))) return st;
             A.map = map;
+            if (map.kind == MapKind::GainTable) A.map.table += (uint64_t)c0 * map.B;  // this group's rows
             A.goff = goff;
             // the PER kernel also renders the tail no frame owns
             if (stft8192_pk_per_path(A, true)) A.tail_end = Lr, tail_in_kernel = true;

@@ -20,8 +20,9 @@ struct ChanOut {
 
 // Per-sample plugin maps that the render / fused kernels specialise on.
 // `table` is the IR_test ramp (B floats) computed on the device by
-// ramp_table_kernel; the others use the scalar `a`.
-enum class MapKind : int { Noop = 0, Gain = 1, Ramp = 3, Fir = 4, Generic = 5, Biquad = 6 };
+// ramp_table_kernel, or (GainTable) C rows of B gains, a GENERIC plugin's
+// per-(channel, position) gains; Gain uses the scalar `a`.
+enum class MapKind : int { Noop = 0, Gain = 1, Ramp = 3, Fir = 4, Generic = 5, Biquad = 6, GainTable = 7 };
 
 struct SampleMap {
     MapKind kind;
@@ -69,6 +70,8 @@ __device__ __forceinline__ float apply_map(const SampleMap &m, float base, uint6
         return base * m.a;  // single fp32 multiply: bit-exact vs gain_test
     case MapKind::Ramp:
         return m.closed ? ramp_value(m, block_pos(m, gi)) : m.table[block_pos(m, gi)];
+    case MapKind::GainTable:  // `table` is this channel's row of B gains: one fp32 multiply
+        return base * m.table[block_pos(m, gi)];
     default:
         return base;
     }

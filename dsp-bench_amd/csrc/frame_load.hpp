@@ -5,6 +5,8 @@
 // at local sample fs, where x is the signal after the plugin's sample map:
 //   Ramp (IR_test, ref build/IR_test.cpp:40-60): table[(global sample) mod B]
 //   Gain / Noop: the input (zero past EOF or for missing channels) * gain.
+//   GainTable: the input * G[ch][(global sample) mod B] (a GENERIC plugin's
+//   per-(channel, position) gains, module.cpp kSpecGainTable).
 #pragma once
 #include "fft_soa.hpp"
 
@@ -12,7 +14,7 @@ namespace dspb {
 
 template <MapKind MK, bool POW2>
 __device__ __forceinline__ void s_render_frame(const Stft8kArgs &A, const float *x, uint64_t fs,
-                                               uint32_t lane, cx (&v)[64]) {
+                                               uint32_t lane, cx (&v)[64], uint32_t ch = 0) {
     const uint64_t gbase = A.goff + fs;
     if constexpr (MK == MapKind::Ramp) {
         const float *T = A.map.table;
@@ -52,6 +54,28 @@ __device__ __forceinline__ void s_render_frame(const Stft8kArgs &A, const float 
         if constexpr (MK == MapKind::Gain) {
 #pragma unroll
             for (int b = 0; b < 64; ++b) v[b] = cx{v[b].r * A.map.a, v[b].i * A.map.a};
+        }
+        if constexpr (MK == MapKind::GainTable) {  // x * G[ch][(global sample) mod B]
+            const float *T = A.map.table + (uint64_t)ch * A.map.B;
+            if constexpr (POW2) {
+                const uint32_t p0 = (uint32_t)gbase + 2u * lane;
+#pragma unroll
+                for (int b = 0; b < 64; ++b) {
+                    const v2f t =
+                        *reinterpret_cast<const v2f *>(T + ((p0 + 128u * (uint32_t)b) & A.map.b_mask));
+                    v[b] = cx{v[b].r * t.x, v[b].i * t.y};
+                }
+            } else {
+                const uint32_t Bn = A.map.B;
+                uint32_t p = (uint32_t)((gbase + 2u * lane) % Bn);
+#pragma unroll
+                for (int b = 0; b < 64; ++b) {
+                    const uint32_t q = (p + 1 == Bn) ? 0u : p + 1;
+                    v[b] = cx{v[b].r * T[p], v[b].i * T[q]};
+                    p += 128u;
+                    while (p >= Bn) p -= Bn;
+                }
+            }
         }
     }
 }

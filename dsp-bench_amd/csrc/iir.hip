@@ -58,19 +58,48 @@ constexpr int kIirLdsStride = kIirT + 1;  // floats per lane chunk in LDS (confl
 constexpr uint32_t kSpinLimit = 1u << 16;  // s_sleep rounds before a wait gives up (legit waits: a few)
 typedef float f4 __attribute__((ext_vector_type(4)));
 
-template <int S>
+// a lane's values for NCH channels at once: float (one channel per wave) or
+// a VGPR pair (a channel pair per wave: every section step one v_pk_fma_f32)
+template <int NCH> struct Lanes;
+template <> struct Lanes<1> {
+    typedef float V;
+    static __device__ __forceinline__ V splat(float x) { return x; }
+    static __device__ __forceinline__ V fma(V a, V b, V c) { return __builtin_fmaf(a, b, c); }
+    static __device__ __forceinline__ float get(V v, int) { return v; }
+    static __device__ __forceinline__ void set(V &v, int, float x) { v = x; }
+    static __device__ __forceinline__ V shfl_up(V v, uint32_t d) { return __shfl_up(v, d); }
+    static __device__ __forceinline__ V shfl(V v, int l) { return __shfl(v, l); }
+    static __device__ __forceinline__ V shfl_xor(V v, int m) { return __shfl_xor(v, m); }
+};
+template <> struct Lanes<2> {
+    typedef v2f V;
+    static __device__ __forceinline__ V splat(float x) { return V{x, x}; }
+    static __device__ __forceinline__ V fma(V a, V b, V c) { return __builtin_elementwise_fma(a, b, c); }
+    static __device__ __forceinline__ float get(V v, int k) { return k ? v.y : v.x; }
+    static __device__ __forceinline__ void set(V &v, int k, float x) {
+        if (k) v.y = x;
+        else v.x = x;
+    }
+    static __device__ __forceinline__ V shfl_up(V v, uint32_t d) { return V{__shfl_up(v.x, d), __shfl_up(v.y, d)}; }
+    static __device__ __forceinline__ V shfl(V v, int l) { return V{__shfl(v.x, l), __shfl(v.y, l)}; }
+    static __device__ __forceinline__ V shfl_xor(V v, int m) { return V{__shfl_xor(v.x, m), __shfl_xor(v.y, m)}; }
+};
+
+template <int S, int NCH>
 struct Cascade {
     static constexpr int D = 2 * S;
-    float b0[S], b1[S], b2[S], na1[S], na2[S];
+    typedef Lanes<NCH> LN;
+    typedef typename LN::V V;
+    V b0[S], b1[S], b2[S], na1[S], na2[S];
 
     __device__ explicit Cascade(const float *cf) {
 #pragma unroll
         for (int k = 0; k < S; ++k) {
-            b0[k] = cf[5 * k];
-            b1[k] = cf[5 * k + 1];
-            b2[k] = cf[5 * k + 2];
-            na1[k] = -cf[5 * k + 3];
-            na2[k] = -cf[5 * k + 4];
+            b0[k] = LN::splat(cf[5 * k]);
+            b1[k] = LN::splat(cf[5 * k + 1]);
+            b2[k] = LN::splat(cf[5 * k + 2]);
+            na1[k] = LN::splat(-cf[5 * k + 3]);
+            na2[k] = LN::splat(-cf[5 * k + 4]);
         }
     }
 
@@ -79,8 +108,8 @@ struct Cascade {
     // history is (xh1, xh2).  st ends as the state after x[T-1].  kWrite:
     // x[n] becomes the last section's output.
     template <bool kWrite>
-    __device__ __forceinline__ void run(float (&x)[kIirT], float xh1, float xh2, float (&st)[D]) const {
-        float X1[S], X2[S], Y1[S], Y2[S];
+    __device__ __forceinline__ void run(V (&x)[kIirT], V xh1, V xh2, V (&st)[D]) const {
+        V X1[S], X2[S], Y1[S], Y2[S];
 #pragma unroll
         for (int k = 0; k < S; ++k) {
             Y1[k] = st[2 * k];
@@ -90,11 +119,11 @@ struct Cascade {
         }
 #pragma unroll
         for (int n = 0; n < kIirT; ++n) {
-            float v = x[n];
+            V v = x[n];
 #pragma unroll
             for (int k = 0; k < S; ++k) {
-                const float acc = __builtin_fmaf(b2[k], X2[k], __builtin_fmaf(b1[k], X1[k], b0[k] * v));
-                const float y = __builtin_fmaf(na1[k], Y1[k], __builtin_fmaf(na2[k], Y2[k], acc));
+                const V acc = LN::fma(b2[k], X2[k], LN::fma(b1[k], X1[k], b0[k] * v));
+                const V y = LN::fma(na1[k], Y1[k], LN::fma(na2[k], Y2[k], acc));
                 X2[k] = X1[k];
                 X1[k] = v;
                 Y2[k] = Y1[k];
@@ -112,20 +141,27 @@ struct Cascade {
 };
 
 // r = m v for a D x D row-major matrix in memory
-template <int D>
-__device__ __forceinline__ void matvec(const float *m, const float (&v)[D], float (&r)[D]) {
+template <int D, int NCH>
+__device__ __forceinline__ void matvec(const float *m, const typename Lanes<NCH>::V (&v)[D],
+                                       typename Lanes<NCH>::V (&r)[D]) {
+    typedef Lanes<NCH> LN;
 #pragma unroll
     for (int i = 0; i < D; ++i) {
-        float a = 0.f;
+        typename LN::V a = LN::splat(0.f);
 #pragma unroll
-        for (int j = 0; j < D; ++j) a = __builtin_fmaf(m[i * D + j], v[j], a);
+        for (int j = 0; j < D; ++j) a = LN::fma(LN::splat(m[i * D + j]), v[j], a);
         r[i] = a;
     }
 }
 
-template <int S, bool kChain>
+// NCH = 2: a wavefront owns the same 2048 samples of a channel pair (lane
+// values are VGPR pairs, every recurrence step a packed FMA: half the VALU
+// of two single-channel tiles); the tile's words hold both channels' states
+template <int S, bool kChain, int NCH>
 __global__ __launch_bounds__(256) void biquad_scan_kernel(BiquadArgs A) {
     constexpr int D = 2 * S;
+    typedef Lanes<NCH> LN;
+    typedef typename LN::V V;
     __shared__ float lds[kIirWaves][64 * kIirLdsStride];
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     float *buf = lds[wave];
@@ -133,98 +169,111 @@ __global__ __launch_bounds__(256) void biquad_scan_kernel(BiquadArgs A) {
     // tile g = the wave's place in launch order: workgroups are dispatched in
     // increasing id, so a tile's predecessors belong to waves already running
     // or done (the waits are bounded anyway)
+    const uint32_t U = A.C / NCH;  // channel units (pairs) of the launch
     const uint64_t g = (uint64_t)blockIdx.x * kIirWaves + wave;
-    if (g >= (uint64_t)A.C * A.ntiles_ch) return;
-    const uint32_t c = (uint32_t)(g % A.C);
-    const uint64_t ti = g / A.C;
+    if (g >= (uint64_t)U * A.ntiles_ch) return;
+    const uint32_t u = (uint32_t)(g % U);
+    const uint64_t ti = g / U;
     const uint64_t base = ti * kIirTile;  // first sample of the tile in the channel
-    const float *x = c < A.in_ch ? A.in.p[c] : nullptr;
-    const uint64_t lim = (x && A.L > base) ? A.L - base : 0;  // file samples in or after the tile
 
-    // 1. stage: 16-byte loads, element e of the tile -> LDS lane chunk e / T
-    if (lim >= (uint64_t)kIirTile && A.in_aligned16) {
-        const f4 *x4 = reinterpret_cast<const f4 *>(x + base);
-        f4 v[kIirTile / 256];
+    // 1. stage each channel of the unit through LDS: 16-byte loads, element e
+    // of the tile -> lane chunk e / T, then into the lane's registers
+    V xr[kIirT], h1 = LN::splat(0.f), h2 = LN::splat(0.f);
 #pragma unroll
-        for (int k = 0; k < kIirTile / 256; ++k) v[k] = __builtin_nontemporal_load(x4 + k * 64 + lane);
+    for (int ch = 0; ch < NCH; ++ch) {
+        const uint32_t c = u * NCH + (uint32_t)ch;
+        const float *x = c < A.in_ch ? A.in.p[c] : nullptr;
+        const uint64_t lim = (x && A.L > base) ? A.L - base : 0;  // file samples in or after the tile
+        if (lim >= (uint64_t)kIirTile && A.in_aligned16) {
+            const f4 *x4 = reinterpret_cast<const f4 *>(x + base);
+            f4 v[kIirTile / 256];
 #pragma unroll
-        for (int k = 0; k < kIirTile / 256; ++k) {
-            const uint32_t e = k * 256 + lane * 4;
-            float *d = buf + (e / kIirT) * kIirLdsStride + e % kIirT;
-            d[0] = v[k].x, d[1] = v[k].y, d[2] = v[k].z, d[3] = v[k].w;
+            for (int k = 0; k < kIirTile / 256; ++k) v[k] = __builtin_nontemporal_load(x4 + k * 64 + lane);
+#pragma unroll
+            for (int k = 0; k < kIirTile / 256; ++k) {
+                const uint32_t e = k * 256 + lane * 4;
+                float *d = buf + (e / kIirT) * kIirLdsStride + e % kIirT;
+                d[0] = v[k].x, d[1] = v[k].y, d[2] = v[k].z, d[3] = v[k].w;
+            }
+        } else {
+            for (uint32_t e = lane; e < (uint32_t)kIirTile; e += 64)
+                buf[(e / kIirT) * kIirLdsStride + e % kIirT] = e < lim ? x[base + e] : 0.f;
         }
-    } else {
-        for (uint32_t e = lane; e < (uint32_t)kIirTile; e += 64)
-            buf[(e / kIirT) * kIirLdsStride + e % kIirT] = e < lim ? x[base + e] : 0.f;
-    }
-    // section 1's x history at the tile start: the file's two samples before it
-    float h1 = 0.f, h2 = 0.f;
-    if (lane == 0 && x) {
-        if (base >= 1 && base - 1 < A.L) h1 = x[base - 1];
-        if (base >= 2 && base - 2 < A.L) h2 = x[base - 2];
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    float xr[kIirT];
+        // section 1's x history at the tile start: the file's two samples before it
+        float a1 = 0.f, a2 = 0.f;
+        if (lane == 0 && x) {
+            if (base >= 1 && base - 1 < A.L) a1 = x[base - 1];
+            if (base >= 2 && base - 2 < A.L) a2 = x[base - 2];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
-    for (int n = 0; n < kIirT; ++n) xr[n] = buf[lane * kIirLdsStride + n];
-    if (lane > 0) {
-        h1 = buf[(lane - 1) * kIirLdsStride + kIirT - 1];
-        h2 = buf[(lane - 1) * kIirLdsStride + kIirT - 2];
+        for (int n = 0; n < kIirT; ++n) LN::set(xr[n], ch, buf[lane * kIirLdsStride + n]);
+        if (lane > 0) {
+            a1 = buf[(lane - 1) * kIirLdsStride + kIirT - 1];
+            a2 = buf[(lane - 1) * kIirLdsStride + kIirT - 2];
+        }
+        LN::set(h1, ch, a1);
+        LN::set(h2, ch, a2);
+        // (the next channel overwrites the tile: LDS ops of a wave complete in order)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
 
     // pass 1: from state 0
-    const Cascade<S> cs(A.coef);
-    float E[D];
+    const Cascade<S, NCH> cs(A.coef);
+    V E[D];
 #pragma unroll
-    for (int r = 0; r < D; ++r) E[r] = 0.f;
+    for (int r = 0; r < D; ++r) E[r] = LN::splat(0.f);
     cs.template run<false>(xr, h1, h2, E);
 
     // 2. scan over the lanes: E_l = sum_{m <= l} M^(T (l - m)) e_m
 #pragma unroll
     for (int j = 0; j < 6; ++j) {
         const uint32_t d = 1u << j;
-        float t[D], r[D];
+        V t[D], r[D];
 #pragma unroll
-        for (int q = 0; q < D; ++q) t[q] = __shfl_up(E[q], d);
-        matvec<D>(A.Q + (size_t)d * D * D, t, r);
+        for (int q = 0; q < D; ++q) t[q] = LN::shfl_up(E[q], d);
+        matvec<D, NCH>(A.Q + (size_t)d * D * D, t, r);
         if (lane >= d) {
 #pragma unroll
             for (int q = 0; q < D; ++q) E[q] += r[q];
         }
     }
-    float agg[D];
+    V agg[D];
 #pragma unroll
-    for (int q = 0; q < D; ++q) agg[q] = __shfl(E[q], 63);
+    for (int q = 0; q < D; ++q) agg[q] = LN::shfl(E[q], 63);
 
     // 3. the state entering the tile.  A tile's aggregate (and, in the
-    // chained mode, its inclusive state) is published as D self-validating
+    // chained mode, its inclusive state) is published as NCH D self-validating
     // 64-bit words (launch tag << 32 | float bits), each one relaxed atomic
-    // store at device scope: a reader takes a value only when all D words
+    // store at device scope: a reader takes a value only when all its words
     // carry this launch's tag -- no flag, so no release / acquire (no L2
     // write-back or invalidate) on either side
-    float Sin[D];
+    constexpr int NW = NCH * D;  // words per tile
+    V Sin[D];
 #pragma unroll
-    for (int q = 0; q < D; ++q) Sin[q] = 0.f;
+    for (int q = 0; q < D; ++q) Sin[q] = LN::splat(0.f);
     const uint64_t tag = A.epoch << 32;
-    auto publish = [&](uint64_t *words, const float (&v)[D]) {
+    auto publish = [&](uint64_t *words, const V (&v)[D]) {
         float mine = 0.f;
 #pragma unroll
-        for (int q = 0; q < D; ++q) mine = lane == (uint32_t)q ? v[q] : mine;
-        if (lane < (uint32_t)D)
-            __hip_atomic_store(words + g * D + lane, tag | __float_as_uint(mine), __ATOMIC_RELAXED,
+        for (int w = 0; w < NW; ++w) mine = lane == (uint32_t)w ? LN::get(v[w / NCH], w % NCH) : mine;
+        if (lane < (uint32_t)NW)
+            __hip_atomic_store(words + g * NW + lane, tag | __float_as_uint(mine), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
     };
-    // the D words of tile gj: true when all carry this launch's tag
-    auto fetch = [&](const uint64_t *words, uint64_t gj, float (&v)[D]) {
+    // the words of tile gj: true when all carry this launch's tag
+    auto fetch = [&](const uint64_t *words, uint64_t gj, V (&v)[D]) {
         bool ok = true;
 #pragma unroll
-        for (int q = 0; q < D; ++q) {
-            const uint64_t w = __hip_atomic_load(const_cast<uint64_t *>(words) + gj * D + q, __ATOMIC_RELAXED,
+        for (int w = 0; w < NW; ++w) {
+            const uint64_t t = __hip_atomic_load(const_cast<uint64_t *>(words) + gj * NW + w, __ATOMIC_RELAXED,
                                                  __HIP_MEMORY_SCOPE_AGENT);
-            ok = ok && (w & 0xffffffff00000000ull) == tag;
-            v[q] = __uint_as_float((uint32_t)w);
+            ok = ok && (t & 0xffffffff00000000ull) == tag;
+            LN::set(v[w / NCH], w % NCH, __uint_as_float((uint32_t)t));
         }
         return ok;
     };
@@ -246,20 +295,20 @@ __global__ __launch_bounds__(256) void biquad_scan_kernel(BiquadArgs A) {
         for (uint32_t k0 = 0; k0 < A.window && (uint64_t)k0 < ti; k0 += 64) {
             const uint32_t k = k0 + lane;
             const bool valid = k < A.window && (uint64_t)k < ti;
-            const uint64_t gj = valid ? (ti - 1 - k) * A.C + c : 0;
-            float v[D], w[D];
+            const uint64_t gj = valid ? (ti - 1 - k) * U + u : 0;
+            V v[D], w[D];
             for (;;) {
                 const bool ok = !valid || fetch(A.aggw, gj, v);
                 if (__ballot(!ok) == 0 || give_up()) break;
             }
 #pragma unroll
-            for (int q = 0; q < D; ++q) v[q] = valid ? v[q] : 0.f;
-            matvec<D>(A.P + (size_t)(valid ? k : 0) * D * D, v, w);
+            for (int q = 0; q < D; ++q) v[q] = valid ? v[q] : LN::splat(0.f);
+            matvec<D, NCH>(A.P + (size_t)(valid ? k : 0) * D * D, v, w);
 #pragma unroll
             for (int q = 0; q < D; ++q) {
-                float a = w[q];
+                V a = w[q];
 #pragma unroll
-                for (int o = 32; o >= 1; o >>= 1) a += __shfl_xor(a, o);
+                for (int o = 32; o >= 1; o >>= 1) a += LN::shfl_xor(a, o);
                 Sin[q] += a;
             }
         }
@@ -273,11 +322,11 @@ __global__ __launch_bounds__(256) void biquad_scan_kernel(BiquadArgs A) {
         int64_t jbase = (int64_t)ti - 1;
         while (jbase >= 0) {
             const int64_t jj = jbase - (int64_t)lane;
-            const uint64_t gj = jj >= 0 ? (uint64_t)jj * A.C + c : 0;
-            float v[D], w[D];
+            const uint64_t gj = jj >= 0 ? (uint64_t)jj * U + u : 0;
+            V v[D], w[D];
             uint32_t state = 2;  // before the channel's first tile: an inclusive zero
 #pragma unroll
-            for (int q = 0; q < D; ++q) v[q] = 0.f;
+            for (int q = 0; q < D; ++q) v[q] = LN::splat(0.f);
             if (jj >= 0) state = fetch(A.inclw, gj, v) ? 2u : fetch(A.aggw, gj, v) ? 1u : 0u;
             const uint64_t incl = __ballot(state == 2);
             const uint64_t ready = __ballot(state != 0);
@@ -288,20 +337,20 @@ __global__ __launch_bounds__(256) void biquad_scan_kernel(BiquadArgs A) {
                 continue;
             }
 #pragma unroll
-            for (int q = 0; q < D; ++q) v[q] = (lane <= first && jj >= 0) ? v[q] : 0.f;
-            matvec<D>(A.P + (size_t)lane * D * D, v, w);  // M^(64 T lane) v
+            for (int q = 0; q < D; ++q) v[q] = (lane <= first && jj >= 0) ? v[q] : LN::splat(0.f);
+            matvec<D, NCH>(A.P + (size_t)lane * D * D, v, w);  // M^(64 T lane) v
 #pragma unroll
             for (int q = 0; q < D; ++q) {
-                float a = w[q];
+                V a = w[q];
 #pragma unroll
-                for (int o = 32; o >= 1; o >>= 1) a += __shfl_xor(a, o);
+                for (int o = 32; o >= 1; o >>= 1) a += LN::shfl_xor(a, o);
                 w[q] = a;
             }
 #pragma unroll
             for (int q = 0; q < D; ++q) {
-                float a = Sin[q];
+                V a = Sin[q];
 #pragma unroll
-                for (int j = 0; j < D; ++j) a = __builtin_fmaf(mult[q * D + j], w[j], a);
+                for (int j = 0; j < D; ++j) a = LN::fma(LN::splat(mult[q * D + j]), w[j], a);
                 Sin[q] = a;
             }
             if (first < 64) break;
@@ -321,73 +370,88 @@ __global__ __launch_bounds__(256) void biquad_scan_kernel(BiquadArgs A) {
             for (int q = 0; q < D * D; ++q) mult[q] = nm[q];
             jbase -= 64;
         }
-        float inc[D], r[D];  // agg + M^(64 T) S_in
-        matvec<D>(A.P + (size_t)D * D, Sin, r);
+        V inc[D], r[D];  // agg + M^(64 T) S_in
+        matvec<D, NCH>(A.P + (size_t)D * D, Sin, r);
 #pragma unroll
         for (int q = 0; q < D; ++q) inc[q] = agg[q] + r[q];
         publish(A.inclw, inc);
     }
 
     // 4. lane l from E_(l-1) + M^(T l) S_in, over its own samples
-    float s0[D];
+    V s0[D];
     {
-        float r[D];
-        matvec<D>(A.Q + (size_t)lane * D * D, Sin, r);
+        V r[D];
+        matvec<D, NCH>(A.Q + (size_t)lane * D * D, Sin, r);
 #pragma unroll
         for (int q = 0; q < D; ++q) {
-            const float prev = __shfl_up(E[q], 1);
-            s0[q] = (lane ? prev : 0.f) + r[q];
+            const V prev = LN::shfl_up(E[q], 1);
+            s0[q] = (lane ? prev : LN::splat(0.f)) + r[q];
         }
     }
     cs.template run<true>(xr, h1, h2, s0);
-#pragma unroll
-    for (int n = 0; n < kIirT; ++n) buf[lane * kIirLdsStride + n] = xr[n];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    float *y = A.out.p[c];
     const uint64_t ny = A.Ly > base ? A.Ly - base : 0;
-    if (ny >= (uint64_t)kIirTile && A.out_aligned16) {
-        f4 *y4 = reinterpret_cast<f4 *>(y + base);
 #pragma unroll
-        for (int k = 0; k < kIirTile / 256; ++k) {
-            const uint32_t e = k * 256 + lane * 4;
-            const float *s = buf + (e / kIirT) * kIirLdsStride + e % kIirT;
-            __builtin_nontemporal_store(f4{s[0], s[1], s[2], s[3]}, y4 + k * 64 + lane);
+    for (int ch = 0; ch < NCH; ++ch) {
+#pragma unroll
+        for (int n = 0; n < kIirT; ++n) buf[lane * kIirLdsStride + n] = LN::get(xr[n], ch);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        float *y = A.out.p[u * NCH + (uint32_t)ch];
+        if (ny >= (uint64_t)kIirTile && A.out_aligned16) {
+            f4 *y4 = reinterpret_cast<f4 *>(y + base);
+#pragma unroll
+            for (int k = 0; k < kIirTile / 256; ++k) {
+                const uint32_t e = k * 256 + lane * 4;
+                const float *sp = buf + (e / kIirT) * kIirLdsStride + e % kIirT;
+                __builtin_nontemporal_store(f4{sp[0], sp[1], sp[2], sp[3]}, y4 + k * 64 + lane);
+            }
+        } else {
+            for (uint32_t e = lane; e < (uint32_t)kIirTile && e < ny; e += 64)
+                y[base + e] = buf[(e / kIirT) * kIirLdsStride + e % kIirT];
         }
-    } else {
-        for (uint32_t e = lane; e < (uint32_t)kIirTile && e < ny; e += 64)
-            y[base + e] = buf[(e / kIirT) * kIirLdsStride + e % kIirT];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
 }
 
 uint64_t biquad_tiles(uint64_t Ly) { return (Ly + kIirTile - 1) / kIirTile; }
 uint32_t biquad_lane_samples() { return kIirT; }
 
-int launch_biquad(const BiquadArgs &A, uint32_t sections, hipStream_t s) {
-    const uint64_t waves = (uint64_t)A.C * A.ntiles_ch;
+int launch_biquad(const BiquadArgs &A, uint32_t sections, uint32_t nch, hipStream_t s) {
+    if (nch != 1 && nch != 2) return DSP_ERR_INVALID;
+    if (A.C == 0 || A.C % nch || A.C > (uint32_t)kMaxChannels) return DSP_ERR_INVALID;
+    const uint64_t waves = (uint64_t)(A.C / nch) * A.ntiles_ch;
     if (waves == 0) return DSP_OK;
     const uint64_t groups = (waves + kIirWaves - 1) / kIirWaves;
-    if (groups > 0x7fffffffull || A.C == 0 || A.C > (uint32_t)kMaxChannels) return DSP_ERR_INVALID;
+    if (groups > 0x7fffffffull) return DSP_ERR_INVALID;
     const dim3 grid((uint32_t)groups), blk(256);
     const bool chain = A.window == 0;
-    switch (sections * 2 + (chain ? 1 : 0)) {
-    case 2: hipLaunchKernelGGL((biquad_scan_kernel<1, false>), grid, blk, 0, s, A); break;
-    case 3: hipLaunchKernelGGL((biquad_scan_kernel<1, true>), grid, blk, 0, s, A); break;
-    case 4: hipLaunchKernelGGL((biquad_scan_kernel<2, false>), grid, blk, 0, s, A); break;
-    case 5: hipLaunchKernelGGL((biquad_scan_kernel<2, true>), grid, blk, 0, s, A); break;
-    case 6: hipLaunchKernelGGL((biquad_scan_kernel<3, false>), grid, blk, 0, s, A); break;
-    case 7: hipLaunchKernelGGL((biquad_scan_kernel<3, true>), grid, blk, 0, s, A); break;
-    case 8: hipLaunchKernelGGL((biquad_scan_kernel<4, false>), grid, blk, 0, s, A); break;
-    case 9: hipLaunchKernelGGL((biquad_scan_kernel<4, true>), grid, blk, 0, s, A); break;
+#define DSPB_BQ(SS, CH, NC) hipLaunchKernelGGL((biquad_scan_kernel<SS, CH, NC>), grid, blk, 0, s, A)
+    switch ((sections * 2 + (chain ? 1 : 0)) * 2 + (nch - 1)) {
+    case 4: DSPB_BQ(1, false, 1); break;
+    case 5: DSPB_BQ(1, false, 2); break;
+    case 6: DSPB_BQ(1, true, 1); break;
+    case 7: DSPB_BQ(1, true, 2); break;
+    case 8: DSPB_BQ(2, false, 1); break;
+    case 9: DSPB_BQ(2, false, 2); break;
+    case 10: DSPB_BQ(2, true, 1); break;
+    case 11: DSPB_BQ(2, true, 2); break;
+    case 12: DSPB_BQ(3, false, 1); break;
+    case 13: DSPB_BQ(3, false, 2); break;
+    case 14: DSPB_BQ(3, true, 1); break;
+    case 15: DSPB_BQ(3, true, 2); break;
+    case 16: DSPB_BQ(4, false, 1); break;
+    case 17: DSPB_BQ(4, false, 2); break;
+    case 18: DSPB_BQ(4, true, 1); break;
+    case 19: DSPB_BQ(4, true, 2); break;
     default: return DSP_ERR_INVALID;
     }
+#undef DSPB_BQ
     DSPB_HIP(hipGetLastError());
     return DSP_OK;
 }
 
-uint64_t biquad_waves_launched(uint64_t C, uint64_t ntiles_ch) {
-    return (C * ntiles_ch + kIirWaves - 1) / kIirWaves * kIirWaves;
-}
 
 }  // namespace dspb

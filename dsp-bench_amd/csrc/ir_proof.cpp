@@ -65,6 +65,7 @@ struct Val {
 struct Inst {
     std::string res, op, text;      // result (or ""), opcode, operand text after the opcode
     std::vector<std::string> parts; // `text` split at top-level commas
+    int blk = 0;                    // its basic block (Analysis::blk_name)
 };
 
 bool ident_char(char c) {
@@ -176,6 +177,7 @@ struct Analysis {
     uint32_t loc_data = 0, sta_data = 0;
     Facts f;
     std::string fail;
+    std::vector<std::string> blk_name;  // "%label" per basic block; block 0 is the entry
 
     explicit Analysis(const Module &m) : M(m) {}
 
@@ -370,7 +372,8 @@ struct Analysis {
                     if (dst.org & O_STA) { f.writes_state = true; sta_data |= v.data | dst.data; }
                     if (dst.org & O_LOC) loc_data |= v.data | dst.data;
                 }
-                if (final_pass && (dst.org & O_BUF)) gain_breakers.insert("a memcpy into the block");
+                if (final_pass && (dst.org & O_BUF)) gain_breakers.insert("a memcpy into the block"),
+                    table_breakers.insert("a memcpy into the block");
                 return false;
             }
             if (starts_with(callee, "@llvm.memset")) {
@@ -383,7 +386,8 @@ struct Analysis {
                     if (dst.org & O_STA) { f.writes_state = true; sta_data |= v.data | dst.data; }
                     if (dst.org & O_LOC) loc_data |= v.data | dst.data;
                 }
-                if (final_pass && (dst.org & O_BUF)) gain_breakers.insert("a memset of the block");
+                if (final_pass && (dst.org & O_BUF)) gain_breakers.insert("a memset of the block"),
+                    table_breakers.insert("a memset of the block");
                 return false;
             }
             static const char *kIgnore[] = {"@llvm.lifetime.", "@llvm.assume", "@llvm.experimental.noalias.scope.decl",
@@ -430,8 +434,234 @@ struct Analysis {
         return cur.org != before.org || cur.data != before.data;
     }
 
-    std::set<std::string> gain_breakers;
+    std::set<std::string> gain_breakers, table_breakers;
     std::map<std::string, std::string> canon_memo;
+
+    // ---- the gain-table form: at most one store per block element --------
+    // The control flow graph from the terminators' `label %x` operands, its
+    // dominators and natural loops; a loop's canonical induction variable
+    // (phi [0, outside], [iv + 1, inside] in its header) takes distinct
+    // values in one run of the loop.  A store whose address is (channel,
+    // sample) = (a constant or a loop's IV, a loop's IV), inside exactly the
+    // loops whose IVs its address uses, hits each element at most once; two
+    // store instructions must name different constant channels.
+    struct Loop {
+        int header;
+        std::vector<bool> body;
+    };
+    std::vector<std::vector<int>> succ_;
+    std::vector<Loop> loops_;
+
+    static std::vector<std::string> labels_in(const std::string &t) {
+        std::vector<std::string> out;
+        for (size_t i = t.find("label %"); i != std::string::npos; i = t.find("label %", i + 1)) {
+            size_t j = i + 7;
+            while (j < t.size() && ident_char(t[j])) ++j;
+            out.push_back(t.substr(i + 6, j - i - 6));
+        }
+        return out;
+    }
+
+    bool build_loops(std::string *why) {
+        const int n = (int)blk_name.size();
+        std::map<std::string, int> id;
+        for (int b = 0; b < n; ++b)
+            if (!blk_name[b].empty()) id[blk_name[b]] = b;
+        succ_.assign(n, {});
+        std::vector<std::vector<int>> pred(n);
+        for (const Inst &I : body) {
+            if (I.op != "br" && I.op != "switch" && I.op != "indirectbr" && I.op != "callbr") continue;
+            for (const auto &l : labels_in(I.text)) {
+                auto it = id.find(l);
+                if (it == id.end()) return *why = "a branch to an unknown block " + l, false;
+                succ_[I.blk].push_back(it->second);
+                pred[it->second].push_back(I.blk);
+            }
+        }
+        // dominators, iteratively (a few hundred blocks at most)
+        std::vector<std::vector<bool>> dom(n, std::vector<bool>(n, true));
+        dom[0].assign(n, false);
+        dom[0][0] = true;
+        for (bool changed = true; changed;) {
+            changed = false;
+            for (int b = 1; b < n; ++b) {
+                std::vector<bool> d(n, pred[b].empty() ? false : true);
+                for (int p : pred[b])
+                    for (int k = 0; k < n; ++k) d[k] = d[k] && dom[p][k];
+                d[b] = true;
+                if (d != dom[b]) dom[b] = d, changed = true;
+            }
+        }
+        // natural loops of the back edges t -> h (h dominates t), one per header
+        std::map<int, int> by_header;
+        for (int t = 0; t < n; ++t)
+            for (int h : succ_[t]) {
+                if (!dom[t][h]) continue;
+                auto it = by_header.find(h);
+                if (it == by_header.end()) {
+                    by_header[h] = (int)loops_.size();
+                    loops_.push_back(Loop{h, std::vector<bool>(n, false)});
+                    it = by_header.find(h);
+                }
+                std::vector<bool> &in = loops_[it->second].body;
+                in[h] = true;
+                std::vector<int> work;
+                if (!in[t]) in[t] = true, work.push_back(t);
+                while (!work.empty()) {
+                    const int b = work.back();
+                    work.pop_back();
+                    for (int p : pred[b])
+                        if (!in[p]) in[p] = true, work.push_back(p);
+                }
+            }
+        return true;
+    }
+
+    // the loop whose canonical IV `tok` is (through zext / sext), or -1
+    int iv_loop(std::string tok) const {
+        for (int hop = 0; hop < 2; ++hop) {
+            auto d = def.find(tok);
+            if (d == def.end()) return -1;
+            const Inst &I = *d->second;
+            if (I.op == "zext" || I.op == "sext") {
+                tok = first_value(I.text, M);
+                continue;
+            }
+            if (I.op != "phi") return -1;
+            int li = -1;
+            for (size_t k = 0; k < loops_.size(); ++k)
+                if (loops_[k].header == I.blk) li = (int)k;
+            if (li < 0) return -1;
+            // [ value, %block ], ...: 0 from outside the loop, tok + 1 from inside
+            bool zero_in = false, step_in = false;
+            const size_t lb = I.text.find('[');
+            if (lb == std::string::npos) return -1;
+            for (const auto &pp : split_top(I.text.substr(lb))) {
+                const size_t a = pp.find('['), b = pp.rfind(']');
+                if (a == std::string::npos || b == std::string::npos || b <= a) return -1;
+                const auto two = split_top(pp.substr(a + 1, b - a - 1));
+                if (two.size() != 2) return -1;
+                int from = -1;
+                for (size_t q = 0; q < blk_name.size(); ++q)
+                    if (blk_name[q] == two[1]) from = (int)q;
+                if (from < 0) return -1;
+                if (!loops_[li].body[from]) {
+                    if (two[0] != "0" || zero_in) return -1;
+                    zero_in = true;
+                } else {
+                    auto n = def.find(two[0]);
+                    if (n == def.end() || n->second->op != "add" || n->second->parts.size() != 2) return -1;
+                    const std::string x0 = first_value(n->second->parts[0], M);
+                    const std::string one = trim(n->second->parts[1]);
+                    if (x0 != tok || one != "1") return -1;
+                    step_in = true;
+                }
+            }
+            return zero_in && step_in ? li : -1;
+        }
+        return -1;
+    }
+
+    void check_gain_table() {
+        std::string why;
+        auto refuse = [&](const std::string &w) {
+            if (why.empty()) why = w;
+        };
+        if (!table_breakers.empty()) refuse(*table_breakers.begin());
+        if (why.empty() && !build_loops(&why)) {}
+        struct StoreAt {
+            int chan_const = -1, chan_loop = -1, samp_loop = -1;
+        };
+        std::vector<StoreAt> seen;
+        for (const Inst &I : body) {
+            if (!why.empty()) break;
+            if (I.op != "store" || I.parts.size() < 2) continue;
+            const std::string ptr = first_value(I.parts[1], M);
+            if (!(get(ptr).org & O_BUF)) continue;
+            if (!starts_with(I.parts[0], "float ")) { refuse("a block store that is not one float"); break; }
+            // the value: x * G with x loaded from this address, G free of samples
+            const std::string v = first_value(I.parts[0], M);
+            auto d = def.find(v);
+            if (v.empty() || d == def.end() || d->second->op != "fmul" || d->second->parts.size() != 2) {
+                refuse("a block store that is not a product");
+                break;
+            }
+            std::string g_tok;
+            bool have_x = false;
+            for (int k = 0; k < 2; ++k) {
+                const std::string t = first_value(d->second->parts[k], M);
+                auto ld = def.find(t);
+                if (!have_x && !t.empty() && ld != def.end() && ld->second->op == "load" &&
+                    ld->second->parts.size() >= 2 && first_value(ld->second->parts[1], M) == ptr) {
+                    have_x = true;
+                    g_tok = first_value(d->second->parts[1 - k], M);
+                }
+            }
+            if (!have_x) { refuse("a block store of a product that is not x * G at its own address"); break; }
+            if (!g_tok.empty() && (get(g_tok).data & (D_IN | D_ADDR))) { refuse("a gain that depends on a sample"); break; }
+            // the address: getelementptr float, (load of the channel's pointer), sample index
+            auto gp = def.find(ptr);
+            if (gp == def.end() || gp->second->op != "getelementptr" || gp->second->parts.size() != 3 ||
+                trim(gp->second->parts[0]) != "float") {
+                refuse("a block address that is not row[index]");
+                break;
+            }
+            StoreAt sa;
+            sa.samp_loop = iv_loop(first_value(gp->second->parts[2], M));
+            if (sa.samp_loop < 0) { refuse("a sample index that is not a loop's induction variable"); break; }
+            const std::string row = first_value(gp->second->parts[1], M);
+            auto rl = def.find(row);
+            if (rl == def.end() || rl->second->op != "load" || rl->second->parts.size() < 2) {
+                refuse("a row pointer not read from the pointer table");
+                break;
+            }
+            const std::string tp = first_value(rl->second->parts[1], M);
+            if (args.size() == 6 && tp == args[2]) {
+                sa.chan_const = 0;
+            } else {
+                auto tg = def.find(tp);
+                if (tg == def.end() || tg->second->op != "getelementptr" || tg->second->parts.size() != 3 ||
+                    first_value(tg->second->parts[1], M) != args[2]) {
+                    refuse("a row pointer not read from the pointer table");
+                    break;
+                }
+                const std::string et = trim(tg->second->parts[0]);
+                std::string ix = trim(tg->second->parts[2]);
+                const size_t sp = ix.find(' ');
+                const std::string ixv = sp == std::string::npos ? ix : trim(ix.substr(sp + 1));
+                char *end = nullptr;
+                const long long k = std::strtoll(ixv.c_str(), &end, 10);
+                if (end && *end == 0 && !ixv.empty() && ixv[0] != '%') {
+                    const long long esz = et == "ptr" ? 8 : et == "i8" ? 1 : 0;
+                    if (!esz || k < 0 || (k * (esz) % 8) != 0) { refuse("an unparsed channel index"); break; }
+                    sa.chan_const = (int)(k * esz / 8);
+                } else if (et == "ptr") {
+                    sa.chan_loop = iv_loop(first_value(ix, M));
+                    if (sa.chan_loop < 0) { refuse("a channel index that is not a loop's induction variable"); break; }
+                } else {
+                    refuse("an unparsed channel index");
+                    break;
+                }
+            }
+            if (sa.chan_loop == sa.samp_loop) { refuse("channel and sample from one loop"); break; }
+            // inside exactly the loops its address uses
+            for (size_t li = 0; li < loops_.size(); ++li) {
+                const bool in = loops_[li].body[I.blk];
+                const bool used = (int)li == sa.samp_loop || (int)li == sa.chan_loop;
+                if (in != used) {
+                    refuse(in ? "a block store inside a loop its address does not use"
+                              : "a block store outside its index's loop");
+                    break;
+                }
+            }
+            for (const StoreAt &o : seen)
+                if (o.chan_loop >= 0 || sa.chan_loop >= 0 || o.chan_const == sa.chan_const)
+                    refuse("two block stores that may hit one element");
+            seen.push_back(sa);
+        }
+        f.gain_table_form = why.empty() && !f.input_control;
+        if (!f.gain_table_form) f.table_why = why.empty() ? "the stored samples depend on a sample" : why;
+    }
 
     // canonical text of a call-invariant value (an operand part or a token)
     std::string canon_tok(const std::string &tok, int depth) {
@@ -629,6 +859,7 @@ Facts analyze(const std::string &ir, const char *fn) {
     const std::string want = std::string("@") + fn + "(";
     bool inside = false;
     std::string pending;  // a switch spanning lines
+    A.blk_name.push_back("");  // the entry block (no label)
     while (std::getline(in, line)) {
         if (!inside) {
             if (starts_with(line, "define ") && line.find(want) != std::string::npos) {
@@ -659,7 +890,10 @@ Facts analyze(const std::string &ir, const char *fn) {
             pending = s;
             continue;
         }
-        if (s.back() == ':' && s.find(' ') == std::string::npos) continue;  // a block label
+        if (s.back() == ':' && s.find(' ') == std::string::npos) {  // a block label
+            A.blk_name.push_back("%" + s.substr(0, s.size() - 1));
+            continue;
+        }
         Inst I;
         std::string rest = s;
         if (s[0] == '%') {
@@ -691,6 +925,7 @@ Facts analyze(const std::string &ir, const char *fn) {
         }
         I.text = tail;
         I.parts = split_top(tail);
+        I.blk = (int)A.blk_name.size() - 1;
         A.body.push_back(I);
     }
     if (!inside) {
@@ -725,6 +960,7 @@ Facts analyze(const std::string &ir, const char *fn) {
     }
     A.f.analyzed = true;
     A.check_gain();
+    A.check_gain_table();
     if (A.f.input_control && A.f.gain_form) {
         A.f.gain_form = false;
         A.f.why = "not a gain: which samples are stored depends on a sample (a branch or an address)";
@@ -855,6 +1091,8 @@ std::string encode(const Facts &f) {
     s += "gain_src=" + std::string(f.gain_src ? 1 : 0, f.gain_src) + "\n";
     s += "gain_off=" + std::to_string(f.gain_off) + "\n";
     s += "gain_bits=" + std::to_string(f.gain_bits) + "\n";
+    s += "gain_table_form=" + std::to_string(f.gain_table_form) + "\n";
+    s += "table_why=" + clean(f.table_why.substr(0, 256)) + "\n";
     s += "why=" + clean(f.why.substr(0, 512)) + "\n";
     return s;
 }
@@ -878,6 +1116,8 @@ bool decode(const std::string &s, Facts *f) {
         else if (k == "gain_src") f->gain_src = v.empty() ? 0 : v[0];
         else if (k == "gain_off") f->gain_off = (uint32_t)std::strtoul(v.c_str(), nullptr, 10);
         else if (k == "gain_bits") f->gain_bits = (uint32_t)std::strtoul(v.c_str(), nullptr, 10);
+        else if (k == "gain_table_form") f->gain_table_form = v == "1";
+        else if (k == "table_why") f->table_why = v;
         else if (k == "why") f->why = v;
     }
     return have_analyzed;

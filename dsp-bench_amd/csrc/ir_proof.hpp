@@ -32,6 +32,15 @@ struct Facts {
     // sample-rate argument -- so that its value is known without the callback
     char gain_src = 0;
     uint32_t gain_off = 0, gain_bits = 0;
+    // every block store is fl(x G) at the address x was loaded from, G free
+    // of any sample (it may vary with the channel, the position, Parameters,
+    // a State the callback only reads), and each element is stored at most
+    // once: the store addresses are (a constant channel or a loop's induction
+    // variable, a loop's induction variable), each store inside exactly the
+    // loops its address uses, different store instructions on different
+    // constant channels (the CFG's natural loops, ir_proof.cpp)
+    bool gain_table_form = false;
+    std::string table_why;      // why not gain_table_form
     std::string why;            // the first construct that ended the analysis, or why a
                                 // property does not hold
 };

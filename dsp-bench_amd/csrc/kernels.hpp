@@ -75,11 +75,12 @@ int module_ir(::dsp_module *m, const void *params, uint32_t params_size, float *
               uint32_t n, float sr, hipStream_t s);
 // a stateless plugin's block class for (Parameters, C, B, sr), probed once
 // through its own callback and cached in the module (module.cpp)
-enum { kSpecNone = 0, kSpecTable = 1, kSpecGain = 2 };
+enum { kSpecNone = 0, kSpecTable = 1, kSpecGain = 2, kSpecGainTable = 3 };
 struct ModuleSpec {
     int kind = kSpecNone;
     float gain = 1.f;             // kSpecGain: y = gain x
-    const float *table = nullptr; // kSpecTable: the block every block renders (B floats, every channel)
+    const float *table = nullptr; // kSpecTable: the block every block renders (B floats, every channel);
+                                  // kSpecGainTable: C rows of B gains, y = x * G[c][position]
     // kSpecTable: the block is an f64 ramp rounded to f32, table[i] =
     // (float)fma(-i, rs, rg0) for every i < B, checked bit for bit on the host
     // (the fused kernels then evaluate it instead of loading the table)
@@ -126,15 +127,15 @@ struct BiquadArgs {
     const float *Q;        // 65 D x D: M^(T l)
     const float *P;        // 257 D x D: M^(64 T k)
     uint32_t window;       // W: S_in from the W previous tiles' aggregates (0: inclusive look-back)
-    uint64_t *aggw, *inclw;  // per tile, D words: epoch << 32 | float bits (aggregate, inclusive)
+    uint64_t *aggw, *inclw;  // per tile, nch D words: epoch << 32 | float bits (aggregate, inclusive)
     uint64_t epoch;        // distinct per launch on one workspace (32 bits used)
     uint32_t *err;         // host-mapped: set when a look-back gives up
     uint32_t in_aligned16, out_aligned16;
 };
 uint64_t biquad_tiles(uint64_t Ly);
 uint32_t biquad_lane_samples();
-uint64_t biquad_waves_launched(uint64_t C, uint64_t ntiles_ch);
-int launch_biquad(const BiquadArgs &A, uint32_t sections, hipStream_t s);
+// nch = 2: one wavefront per tile of a channel pair (C even), packed math
+int launch_biquad(const BiquadArgs &A, uint32_t sections, uint32_t nch, hipStream_t s);
 int launch_minmax(const float *x, uint64_t n, uint32_t P, float *vmax, float *vmin, hipStream_t s);
 int launch_spectro(const float *mag, uint64_t F, uint32_t K, uint64_t ld, uint32_t P, float *out,
                    hipStream_t s);

@@ -890,8 +890,10 @@ int dsp_module_block_class(dsp_module *m, const void *params, uint32_t params_si
     int cur = -1;
     if (hipGetDevice(&cur) == hipSuccess && prev >= 0 && prev != cur) (void)hipSetDevice(prev);
     if (st) return st;
-    *block_class = r.kind == dspb::kSpecTable ? DSP_BLOCK_TABLE : r.kind == dspb::kSpecGain ? DSP_BLOCK_GAIN
-                                                                                              : DSP_BLOCK_CALLBACK;
+    *block_class = r.kind == dspb::kSpecTable ? DSP_BLOCK_TABLE
+                   : r.kind == dspb::kSpecGain ? DSP_BLOCK_GAIN
+                   : r.kind == dspb::kSpecGainTable ? DSP_BLOCK_GAIN_TABLE
+                                                   : DSP_BLOCK_CALLBACK;
     if (gain) *gain = r.gain;
     return DSP_OK;
 }
@@ -1120,6 +1122,8 @@ static void facts_out(const dspb::irp::Facts &f, bool present, dsp_callback_fact
     o->gain_offset = f.gain_off;
     std::memcpy(&o->gain_constant, &f.gain_bits, 4);
     std::strncpy(o->why, f.why.c_str(), sizeof o->why - 1);
+    o->gain_table_form = f.gain_table_form;
+    std::strncpy(o->table_why, f.table_why.c_str(), sizeof o->table_why - 1);
 }
 
 int dsp_module_facts(const dsp_module *m, dsp_callback_facts *out) {
@@ -1520,7 +1524,8 @@ int module_specialize(dsp_module *m, const void *params, uint32_t params_size, u
     const dspb::irp::Facts &F = m->facts;
     const bool may_table = m->has_facts && F.analyzed && !F.writes_state && !F.reads_block;
     const bool may_gain = m->has_facts && F.analyzed && !F.writes_state && F.gain_form && !F.input_control;
-    if (!may_table && !may_gain) return DSP_OK;  // the callback on every block
+    const bool may_gtab = m->has_facts && F.analyzed && !F.writes_state && F.gain_table_form && !F.input_control;
+    if (!may_table && !may_gain && !may_gtab) return DSP_OK;  // the callback on every block
     if (params_size != m->params_size || (!params && params_size)) return DSP_OK;  // module_render reports it
     if (int st = check_device(m)) return st;
     std::lock_guard<std::mutex> lk(m->mu);
@@ -1600,6 +1605,12 @@ int module_specialize(dsp_module *m, const void *params, uint32_t params_size, u
     bool gain = !table && may_gain && have_ge && std::isfinite(g);
     for (uint64_t i = 4 * n; i < 5 * n && gain; ++i) gain = same_bits(r[i], g);  // ones -> g, every element
     for (uint64_t i = 0; i < kProbes * n && gain; ++i) gain = same_bits(r[i], h[i] * g);
+    // a gain table (IR: every store x G at x's address, G free of samples,
+    // each element stored at most once): G[c][s] is what the probe of ones
+    // renders (fl(1 G) = G; 1 where nothing is stored), and every probe must
+    // render fl(x G) element by element
+    bool gtab = !table && !gain && may_gtab;
+    for (uint64_t i = 0; i < kProbes * n && gtab; ++i) gtab = same_bits(r[i], h[i] * r[4 * n + i % n]);
     if (table) {
         float *t = nullptr;
         MOD_HIP(hipMalloc(&t, sizeof(float) * B));
@@ -1610,6 +1621,12 @@ int module_specialize(dsp_module *m, const void *params, uint32_t params_size, u
     } else if (gain) {
         res.kind = kSpecGain;
         res.gain = g;
+    } else if (gtab) {
+        float *t = nullptr;
+        MOD_HIP(hipMalloc(&t, sizeof(float) * n));
+        MOD_HIP(hipMemcpyAsync(t, d + 4 * n, sizeof(float) * n, hipMemcpyDeviceToDevice, s));
+        res.kind = kSpecGainTable;
+        res.table = t;
     }
     // an evicted entry's table is retired, not freed: a call (this thread's
     // or another's) or a captured graph may still read it (spec_reap)

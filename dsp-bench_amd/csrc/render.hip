@@ -37,8 +37,18 @@ __global__ void ramp_table_kernel(float *table, uint32_t B, float gain, float st
 }
 
 
+// the launch's map as kernel K applies it to channel c of the launch (a
+// gain table: that channel's row of C x B gains)
 template <MapKind K>
-__device__ __forceinline__ float4 render4(const RenderArgs &A, const float *x, uint64_t i) {
+__device__ __forceinline__ SampleMap map_for(const SampleMap &a, uint32_t c) {
+    SampleMap m = a;
+    m.kind = K;
+    if constexpr (K == MapKind::GainTable) m.table += (uint64_t)c * m.B;
+    return m;
+}
+
+template <MapKind K>
+__device__ __forceinline__ float4 render4(const RenderArgs &A, const float *x, uint64_t i, uint32_t c) {
     float4 b = make_float4(0.f, 0.f, 0.f, 0.f);
     if (K != MapKind::Ramp && x != nullptr) {
         if (i + 4 <= A.L) {
@@ -50,8 +60,7 @@ __device__ __forceinline__ float4 render4(const RenderArgs &A, const float *x, u
         }
     }
     if (K == MapKind::Noop) return b;
-    SampleMap m = A.map;
-    m.kind = K;
+    const SampleMap m = map_for<K>(A.map, c);
     const uint64_t g = A.goff + i;
     return make_float4(apply_map(m, b.x, g), apply_map(m, b.y, g + 1),
                        apply_map(m, b.z, g + 2), apply_map(m, b.w, g + 3));
@@ -76,7 +85,7 @@ __global__ __launch_bounds__(256) void render_vec_kernel(RenderArgs A) {
 #pragma unroll
     for (int u = 0; u < kVecU; ++u) {
         const uint64_t q = q0 + 256u * (uint32_t)u;
-        if (q < n4) r[u] = render4<K>(A, x, A.start + 4 * q);
+        if (q < n4) r[u] = render4<K>(A, x, A.start + 4 * q, c);
     }
 #pragma unroll
     for (int u = 0; u < kVecU; ++u) {
@@ -89,8 +98,7 @@ __global__ __launch_bounds__(256) void render_vec_kernel(RenderArgs A) {
     if (blockIdx.x == 0 && threadIdx.x < ((A.end - A.start) & 3)) {
         const uint64_t i = A.start + 4 * n4 + threadIdx.x;
         const float b = (K != MapKind::Ramp && x != nullptr && i < A.L) ? x[i] : 0.f;
-        SampleMap m = A.map;
-        m.kind = K;
+        const SampleMap m = map_for<K>(A.map, c);
         o[i] = apply_map(m, b, A.goff + i);
     }
 }
@@ -102,8 +110,7 @@ __global__ __launch_bounds__(256) void render_scalar_kernel(RenderArgs A) {
     const float *x = (c < A.in_ch) ? A.in.p[c] : nullptr;
     float *o = A.out.p[c];
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    SampleMap m = A.map;
-    m.kind = K;
+    const SampleMap m = map_for<K>(A.map, c);
     for (uint64_t i = A.start + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < A.end;
          i += stride) {
         const float b = (K != MapKind::Ramp && x != nullptr && i < A.L) ? x[i] : 0.f;
@@ -217,8 +224,7 @@ __global__ __launch_bounds__(256) void render_wrap_kernel(RenderArgs A, uint64_t
     const uint64_t L = A.L;
     uint64_t j = (K == MapKind::Ramp || x == nullptr) ? 0 : (cursor + i0) % L;
     const uint64_t dj = (K == MapKind::Ramp || x == nullptr) ? 0 : stride % L;
-    SampleMap m = A.map;
-    m.kind = K;
+    const SampleMap m = map_for<K>(A.map, c);
     for (uint64_t i = i0; i < A.end; i += stride) {
         const float b = (K != MapKind::Ramp && x != nullptr) ? x[j] : 0.f;
         o[i] = apply_map(m, b, A.goff + i);
@@ -242,8 +248,7 @@ __global__ __launch_bounds__(256) void render_wrap_vec_kernel(RenderArgs A, uint
     const uint64_t q0 = (uint64_t)blockIdx.x * (256u * kVecU) + threadIdx.x;
     const uint64_t L = A.L;
     const bool rd = K != MapKind::Ramp && x != nullptr;
-    SampleMap m = A.map;
-    m.kind = K;
+    const SampleMap m = map_for<K>(A.map, c);
     // the block's first file index is wave-uniform (one scalar modulo per
     // wave); lanes add 4 t < 1024 and wrap by compare when L > 1024
     uint64_t j = 0;
@@ -312,6 +317,9 @@ int launch_render_wrap(const RenderArgs &A, uint32_t C, uint64_t cursor, hipStre
         case MapKind::Noop: hipLaunchKernelGGL(render_wrap_vec_kernel<MapKind::Noop>, vgrid, dim3(256), 0, s, A, cursor); break;
         case MapKind::Gain: hipLaunchKernelGGL(render_wrap_vec_kernel<MapKind::Gain>, vgrid, dim3(256), 0, s, A, cursor); break;
         case MapKind::Ramp: hipLaunchKernelGGL(render_wrap_vec_kernel<MapKind::Ramp>, vgrid, dim3(256), 0, s, A, cursor); break;
+        case MapKind::GainTable:
+            hipLaunchKernelGGL(render_wrap_vec_kernel<MapKind::GainTable>, vgrid, dim3(256), 0, s, A, cursor);
+            break;
         default: return DSP_ERR_INVALID;
         }
         DSPB_HIP(hipGetLastError());
@@ -325,6 +333,7 @@ int launch_render_wrap(const RenderArgs &A, uint32_t C, uint64_t cursor, hipStre
     case MapKind::Noop: hipLaunchKernelGGL(render_wrap_kernel<MapKind::Noop>, grid, block, 0, s, A, cursor); break;
     case MapKind::Gain: hipLaunchKernelGGL(render_wrap_kernel<MapKind::Gain>, grid, block, 0, s, A, cursor); break;
     case MapKind::Ramp: hipLaunchKernelGGL(render_wrap_kernel<MapKind::Ramp>, grid, block, 0, s, A, cursor); break;
+    case MapKind::GainTable: hipLaunchKernelGGL(render_wrap_kernel<MapKind::GainTable>, grid, block, 0, s, A, cursor); break;
     default: return DSP_ERR_INVALID;
     }
     DSPB_HIP(hipGetLastError());
@@ -361,6 +370,7 @@ int launch_render(const RenderArgs &A, uint32_t C, bool vec, hipStream_t s) {
         DSPB_RENDER_CASE(MapKind::Noop)
         DSPB_RENDER_CASE(MapKind::Gain)
         DSPB_RENDER_CASE(MapKind::Ramp)
+        DSPB_RENDER_CASE(MapKind::GainTable)
     default:
         return DSP_ERR_INVALID;
     }

@@ -428,7 +428,7 @@ void stft8192_pk_kernel(Stft8kArgs A) {
             if (A.map.B >= 4u && A.map.B <= 4096u) lds_table_frame(A, lds, fs, lane, v);
             else s_render_frame<MK, POW2>(A, x, fs, lane, v);
         } else {
-            s_render_frame<MK, POW2>(A, x, fs, lane, v);
+            s_render_frame<MK, POW2>(A, x, fs, lane, v, ch);
         }
         float *o = A.out.p[ch] + fs;
         constexpr bool NT = !(OPT & kPkRenderCached);

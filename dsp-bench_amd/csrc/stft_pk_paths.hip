@@ -36,6 +36,14 @@ int launch_pk_paths(const Stft8kArgs &A, bool fused, int km, bool pow2, bool win
                 hipLaunchKernelGGL((stft8192_pk_kernel<kSrcRender, kKHalf, MapKind::Ramp, false, true>), grid,
                                    dim3(64 * kPkWpb), 0, stream, A);
             break;
+        case MapKind::GainTable:
+            if (pow2)
+                hipLaunchKernelGGL((stft8192_pk_kernel<kSrcRender, kKHalf, MapKind::GainTable, true, true>), grid,
+                                   dim3(64 * kPkWpb), 0, stream, A);
+            else
+                hipLaunchKernelGGL((stft8192_pk_kernel<kSrcRender, kKHalf, MapKind::GainTable, false, true>), grid,
+                                   dim3(64 * kPkWpb), 0, stream, A);
+            break;
         default: return DSP_ERR_INVALID;
         }
     } else if (fused) {
@@ -45,6 +53,10 @@ int launch_pk_paths(const Stft8kArgs &A, bool fused, int km, bool pow2, bool win
         case MapKind::Ramp:
             if (pow2) launch_pk_km<kSrcRender, MapKind::Ramp, true, false>(km, grid, stream, A);
             else launch_pk_km<kSrcRender, MapKind::Ramp, false, false>(km, grid, stream, A);
+            break;
+        case MapKind::GainTable:
+            if (pow2) launch_pk_km<kSrcRender, MapKind::GainTable, true, false>(km, grid, stream, A);
+            else launch_pk_km<kSrcRender, MapKind::GainTable, false, false>(km, grid, stream, A);
             break;
         default: return DSP_ERR_INVALID;
         }

@@ -37,7 +37,7 @@ DSP_EXEC_VERIFY_CLASS = 0x10
 DSP_RESULT_CLASS = 0x1
 DSP_RESULT_VERIFIED = 0x2
 DSP_RESULT_RERENDERED = 0x4
-DSP_BLOCK_CALLBACK, DSP_BLOCK_TABLE, DSP_BLOCK_GAIN = 0, 1, 2
+DSP_BLOCK_CALLBACK, DSP_BLOCK_TABLE, DSP_BLOCK_GAIN, DSP_BLOCK_GAIN_TABLE = 0, 1, 2, 3
 
 
 class DspError(RuntimeError):
@@ -96,7 +96,8 @@ class dsp_callback_facts(C.Structure):  # module.h
     _fields_ = [("present", C.c_int32), ("analyzed", C.c_int32), ("reads_block", C.c_int32),
                 ("writes_state", C.c_int32), ("input_control", C.c_int32), ("gain_form", C.c_int32),
                 ("gain_source", C.c_int32), ("gain_offset", C.c_uint32), ("gain_constant", C.c_float),
-                ("gain", C.c_char * 128), ("why", C.c_char * 256)]
+                ("gain", C.c_char * 128), ("why", C.c_char * 256), ("gain_table_form", C.c_int32),
+                ("table_why", C.c_char * 128)]
 
     def as_dict(self) -> dict:
         return {"present": bool(self.present), "analyzed": bool(self.analyzed),
@@ -104,7 +105,9 @@ class dsp_callback_facts(C.Structure):  # module.h
                 "input_control": bool(self.input_control), "gain_form": bool(self.gain_form),
                 "gain_source": chr(self.gain_source) if self.gain_source else "",
                 "gain_offset": int(self.gain_offset), "gain_constant": float(self.gain_constant),
-                "gain": self.gain.decode(errors="replace"), "why": self.why.decode(errors="replace")}
+                "gain": self.gain.decode(errors="replace"), "why": self.why.decode(errors="replace"),
+                "gain_table_form": bool(self.gain_table_form),
+                "table_why": self.table_why.decode(errors="replace")}
 
 
 # name -> (restype, argtypes)
@@ -194,7 +197,7 @@ _OPTIONAL_SIGS = {
 _lib: C.CDLL | None = None
 
 
-ABI_VERSION = 2  # include/dspbench/dspbench.h DSPBENCH_ABI_VERSION this binding is written against
+ABI_VERSION = 3  # include/dspbench/dspbench.h DSPBENCH_ABI_VERSION this binding is written against
 
 
 def lib() -> C.CDLL:

@@ -249,7 +249,7 @@ class Module:
         return n.value
 
     def block_class(self, params: bytes, channels: int, block: int, sample_rate: float, stream=None):
-        """(class, gain): "table" | "gain" | "callback" (dsp_module_block_class),
+        """(class, gain): "table" | "gain" | "gain_table" | "callback" (dsp_module_block_class),
         probing the plugin's callback on the current device if not known yet."""
         import torch
         buf = C.create_string_buffer(bytes(params), max(1, len(params)))
@@ -258,4 +258,5 @@ class Module:
         ex = L.dsp_exec(-1, 0, C.c_void_p(st), 0)
         check(L.lib().dsp_module_block_class(self.handle, buf, len(params), channels, block, sample_rate,
                                              C.byref(cls), C.byref(g), C.byref(ex)), "dsp_module_block_class")
-        return {L.DSP_BLOCK_TABLE: "table", L.DSP_BLOCK_GAIN: "gain"}.get(cls.value, "callback"), g.value
+        return {L.DSP_BLOCK_TABLE: "table", L.DSP_BLOCK_GAIN: "gain",
+                L.DSP_BLOCK_GAIN_TABLE: "gain_table"}.get(cls.value, "callback"), g.value

@@ -47,7 +47,7 @@ extern "C" {
  * selects the direct form), the transport / gather-plan entry points and the
  * dsp_comm layout of shard.h, dsp_callback_facts and the fact-gated block
  * classes of module.h.  A binding written against 1 must not assume those. */
-#define DSPBENCH_ABI_VERSION 2
+#define DSPBENCH_ABI_VERSION 3
 
 enum dsp_status {
     DSP_OK = 0,

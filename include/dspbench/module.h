@@ -185,7 +185,7 @@ int dsp_param_denormalize(const dsp_param_desc *p, const int64_t *enum_values, f
  * synchronises its stream once.  Anything else, including every code object
  * without facts, runs the callback on every block, as does
  * DSP_EXEC_NO_SPECIALIZE (dspbench.h). */
-enum dsp_block_class { DSP_BLOCK_CALLBACK = 0, DSP_BLOCK_TABLE = 1, DSP_BLOCK_GAIN = 2 };
+enum dsp_block_class { DSP_BLOCK_CALLBACK = 0, DSP_BLOCK_TABLE = 1, DSP_BLOCK_GAIN = 2, DSP_BLOCK_GAIN_TABLE = 3 };
 
 /* The block class of `params` for C channels of B-sample blocks at sample
  * rate sr (probing on ex->stream if not known yet); *gain receives g for
@@ -225,6 +225,12 @@ typedef struct dsp_callback_facts {
     float gain_constant;
     char gain[128];        /* g as the analysis wrote it (diagnostics) */
     char why[256];         /* why the analysis stopped, or why a property fails */
+    int32_t gain_table_form; /* (ABI 3) every block store is x * G at x's address, G free of any
+                              sample (it may vary with channel and position), and no element
+                              is stored twice: the IR's loops (the CFG's natural loops and
+                              their induction variables) give every store the address
+                              (constant or loop channel, loop sample) */
+    char table_why[128];   /* (ABI 3) why not gain_table_form */
 } dsp_callback_facts;
 
 /* The facts of a loaded module (present = 0 for a code object without). */

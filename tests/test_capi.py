@@ -52,7 +52,7 @@ def test_library_exports_every_declared_symbol(header):
 
 def test_abi_and_status_strings():
     L = d.lib()
-    assert L.dsp_abi_version() == 2  # dspbench.h DSPBENCH_ABI_VERSION (bumped in round 4)
+    assert L.dsp_abi_version() == 3  # dspbench.h DSPBENCH_ABI_VERSION (bumped in round 5: facts.gain_table_form)
     for s, txt in [(0, b"ok"), (-1, b"invalid argument"), (-2, b"HIP runtime error"),
                    (-3, b"unsupported"), (-4, b"out of device memory"), (-5, b"no device"),
                    (-99, b"unknown status")]:

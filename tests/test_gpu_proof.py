@@ -93,10 +93,10 @@ EXPECT = {
     "exact_value_branch": ("callback", True),
     "gain_until_loud": ("callback", True),
     "static_counter": ("callback", False),
-    "fade_in": ("callback", True),
-    "balance": ("callback", True),
+    "fade_in": ("gain_table", True),      # x * G[position] (round 5: the gain-table class)
+    "balance": ("gain_table", True),      # x * G[channel]
     "gain_twice": ("callback", True),
-    "half_block": ("callback", True),
+    "half_block": ("gain_table", True),   # x * g on half the block, x elsewhere
     "state_shaper": ("callback", True),
     "dc_level": ("table", True),
 }
@@ -148,7 +148,8 @@ def test_static_counter_runs_in_order_across_calls(torch_cuda):
     assert np.array_equal(b, semantics("static_counter", blocks(x, 2, B), params, call0=nb))
 
 
-@pytest.mark.parametrize("name", ["clip_beyond_2000", "state_shaper", "dc_level", "gain_until_loud"])
+@pytest.mark.parametrize("name", ["clip_beyond_2000", "state_shaper", "dc_level", "gain_until_loud", "balance",
+                                  "fade_in", "half_block"])
 def test_render_stft_of_proof_plugins(torch_cuda, oracle, name):
     """render + STFT through the same dispatch: the render bit for bit, the
     spectra within 1e-6 of the peak of float64."""
@@ -187,15 +188,17 @@ def test_gain_twice_is_a_gain_only_when_g_squared_is_g(torch_cuda):
 
 def test_half_block_gain_is_refused_unless_it_is_the_identity(torch_cuda):
     """half_block.cpp stores x * g (the IR's gain form) on the first half of
-    each block only: the probe of ones sees 1 in the second half, so the
+    each block only: the probe of ones sees 1 in the second half, so the gain
     class is refused for g = 0.5 and g = 0 and taken for g = 1, where the
-    callback is the identity."""
+    callback is the identity.  Each element is stored at most once (the IR's
+    loops), so g = 0.5 and 0 take the gain-table class: G = g on the first
+    half, 1 on the second (round 5) -- the same rows either way."""
     torch = torch_cuda
     mod = load("half_block")
     mod.initialize_state(mod.default_parameters(), 2, 48000.0)
     assert mod.facts["gain_form"]
     x = torch.from_numpy(make_input(512 * 9 + 5)).cuda()
-    for g, cls in ((0.5, "callback"), (0.0, "callback"), (1.0, "gain")):
+    for g, cls in ((0.5, "gain_table"), (0.0, "gain_table"), (1.0, "gain")):
         params = struct.pack("<f", g)
         assert mod.block_class(params, 2, 512, 48000.0)[0] == cls, g
         got = d.render_offline(x, 2, 512, 48000.0, mod.plugin(params, "half_block")).cpu().numpy()
@@ -395,4 +398,42 @@ def test_verify_class_result_through_every_driver(torch_cuda):
     assert last_result() == 0
     y2, _ = d.render_loop(x, 2, 512, 30, 48000.0, gmod.plugin(gp, "gain_test"), cursor=100)
     assert last_result() == L.DSP_RESULT_CLASS
+    assert torch.equal(y, y2)
+
+
+@pytest.mark.parametrize("name", ["balance", "fade_in", "half_block"])
+def test_gain_table_class_in_every_path(torch_cuda, oracle, name):
+    """The gain-table class (round 5): per-(channel, position) gains proven
+    from the IR (each element stored at most once, x G at x's address, G free
+    of samples) and pinned by the probe of ones.  The fused render + STFT,
+    the two-pass path (an odd sample offset), loop mode and VERIFY_CLASS all
+    render the callback's rows bit for bit; the spectra are within 1e-6 of
+    the peak of float64."""
+    torch = torch_cuda
+    import dspbench._lib as L
+    from dspbench.api import last_result
+    mod = load(name)
+    params = mod.default_parameters()
+    mod.initialize_state(params, 2, 48000.0)
+    assert mod.facts["gain_table_form"], mod.facts
+    B, L_ = 512, 8192 * 9 + 700
+    x = make_input(L_, seed=21)
+    want = semantics(name, blocks(x, 2, B), params)
+    xg = torch.from_numpy(x).cuda()
+    out, mag = d.render_stft(xg, 2, B, 48000.0, mod.plugin(params, name, verify=True), window=d.DSP_WIN_HANN)
+    assert last_result() == L.DSP_RESULT_CLASS | L.DSP_RESULT_VERIFIED
+    assert np.array_equal(out.cpu().numpy(), want)
+    for c in range(2):
+        m64 = oracle.np_stft_mag(want[c], 8192, 4096, d.DSP_WIN_HANN, 4097)
+        mm = mag[c].cpu().numpy().astype(np.float64)
+        peak = np.maximum(m64.max(axis=1), 1e-30)
+        assert float(np.max(np.abs(mm - m64).max(axis=1) / peak)) <= PEAK_REL_TOL
+    # a channel the file lacks, three channels (balance: C > 1 scales channel 1 only)
+    x1 = make_input(L_, C=1, seed=22)
+    got3 = d.render_offline(torch.from_numpy(x1).cuda(), 3, B, 48000.0, mod.plugin(params, name)).cpu().numpy()
+    assert np.array_equal(got3, semantics(name, blocks(x1, 3, B), params))
+    # loop mode: the wrap kernels with the same gains
+    y, _ = d.render_loop(xg, 2, B, 40, 48000.0, mod.plugin(params, name), cursor=333)
+    assert last_result() == L.DSP_RESULT_CLASS
+    y2, _ = d.render_loop(xg, 2, B, 40, 48000.0, mod.plugin(params, name, specialize=False), cursor=333)
     assert torch.equal(y, y2)

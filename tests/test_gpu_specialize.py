@@ -309,3 +309,29 @@ def test_new_parameters_are_probed_again(torch_cuda):
         got = d.render_offline(x, 2, 512, 48000.0, mod.plugin(params, "gain_test"))
         want = d.render_offline(x, 2, 512, 48000.0, d.Plugin.gain_test(g))
         assert torch.equal(got, want)
+
+
+@pytest.mark.parametrize("name", sorted(k for k, v in EXPECTED.items() if v != "callback"))
+def test_shipped_object_confirms_the_class(torch_cuda, name):
+    """The classes come from the callback's -O2 analysis IR; the module that
+    runs is the -O3 object.  Both compile the same source with
+    the same IEEE options, and the shipped object's own callback confirms the
+    class on the call's input: DSP_EXEC_VERIFY_CLASS runs it on four blocks of
+    each render and compares bit for bit (VERIFIED, never RERENDERED) --
+    through render_offline, render_stft and the chunked host driver."""
+    if not have(name):
+        pytest.skip("modules / oracle/_ref not built")
+    import dspbench._lib as L
+    from dspbench.api import last_result
+    mod = load(name)
+    params = mod.default_parameters()
+    mod.initialize_state(params, 2, 48000.0)
+    ok = L.DSP_RESULT_CLASS | L.DSP_RESULT_VERIFIED
+    x = np.random.default_rng(31).uniform(-1, 1, (2, 512 * 200 + 77)).astype(np.float32)
+    xg = torch_cuda.from_numpy(x).cuda()
+    d.render_offline(xg, 2, 512, 48000.0, mod.plugin(params, name, verify=True))
+    assert last_result() == ok
+    d.render_stft(xg, 2, 512, 48000.0, mod.plugin(params, name, verify=True))
+    assert last_result() == ok
+    d.render_stft_host(x, 2, 512, 48000.0, mod.plugin(params, name, verify=True), chunk=1 << 15)
+    assert last_result() == ok

@@ -72,6 +72,45 @@ TEST = {
 }
 
 
+# the gain-table form (round 5): every element stored at most once as x * G
+GAIN_TABLE = {"balance.cpp": True, "fade_in.cpp": True, "half_block.cpp": True, "gain_twice.cpp": False,
+              "clip_beyond_2000.cpp": False, "exact_value_branch.cpp": False, "gain_until_loud.cpp": False,
+              "state_shaper.cpp": False, "dc_level.cpp": False}
+
+
+@pytest.mark.parametrize("name", sorted(GAIN_TABLE))
+def test_gain_table_form_of_test_plugins(name):
+    f = facts_of(os.path.join(PLUG, name))
+    assert f["gain_table_form"] == GAIN_TABLE[name], (name, f)
+    if not f["gain_table_form"]:
+        assert f["table_why"], f
+
+
+# bodies that store each element at most once as x * G (True), or not / not
+# provably (False): the refusals are the cases a probe of ones cannot see
+GT_SNIPPETS = {
+    "pan_by_channel_loop": ("for (u32 c = 0; c < C; ++c) for (u32 s = 0; s < B; ++s) "
+                            "out[c][s] *= (c == 0 ? p.g : 1.0f - p.g);", True),
+    "window_shape": ("for (u32 s = 0; s < B; ++s) { const float w = 0.5f - 0.5f * cosf(6.2831853f * s / B); "
+                     "for (u32 c = 0; c < C; ++c) out[c][s] *= w; }", True),
+    "repeat_loop": ("for (int r = 0; r < 2; ++r) for (u32 s = 0; s < B; ++s) out[0][s] *= p.g;", False),
+    "same_channel_twice": ("for (u32 s = 0; s < B; ++s) out[0][s] *= p.g; "
+                           "for (u32 s = 0; s < B; ++s) out[0][s] *= 0.5f;", False),
+    "loop_and_const_channel": ("for (u32 c = 0; c < C; ++c) for (u32 s = 0; s < B; ++s) out[c][s] *= p.g; "
+                               "out[0][0] *= 2.0f;", False),
+    "shifted_index": ("for (u32 s = 0; s + 1 < B; ++s) out[0][s + 1] *= p.g;", False),
+    "gain_from_a_sample": ("for (u32 s = 0; s < B; ++s) out[0][s] *= out[1][0];", False),
+    "channel_from_sample_loop": ("for (u32 s = 0; s < B && s < C; ++s) out[s][s] *= p.g;", False),
+}
+
+
+@pytest.mark.parametrize("case", sorted(GT_SNIPPETS))
+def test_gain_table_constructs(case):
+    body, want = GT_SNIPPETS[case]
+    f = dm.analyze_source(snippet("", body))
+    assert f["gain_table_form"] == want, f
+
+
 @pytest.mark.parametrize("name", sorted(TEST))
 def test_test_plugin_facts(name):
     f = facts_of(os.path.join(PLUG, name))

@@ -29,7 +29,9 @@ OUT = os.environ.get("DSPB_MODULES_DIR", os.path.join(ROOT, "dsp-bench_amd", "mo
 
 
 # this repository's own example plugins (no reference needed)
-OWN = [os.path.join(ROOT, "dsp-bench_amd", "plugins", "biquad.cpp")]
+OWN = [os.path.join(ROOT, "dsp-bench_amd", "plugins", "biquad.cpp"),
+       # test plugins the bench times (the gain-table class: per-channel / per-position gains)
+       os.path.join(ROOT, "tests", "plugins", "balance.cpp"), os.path.join(ROOT, "tests", "plugins", "fade_in.cpp")]
 
 
 def main():
