@@ -112,4 +112,35 @@ __device__ __forceinline__ void lds_table_frame(const Stft8kArgs &A, float *lds,
     }
 }
 
+// the gain table's row of this channel (pow2 B, 4 <= B <= 4096) staged in the
+// wave's LDS tile like lds_table_frame, then x * G[(global sample) mod B]:
+// two coalesced float4 loads per lane at B = 512 instead of 64 scattered
+// 8-byte gathers beside the frame's own loads
+__device__ __forceinline__ void lds_gain_table_frame(const Stft8kArgs &A, float *lds, const float *x, uint64_t fs,
+                                                     uint32_t lane, cx (&v)[64], uint32_t ch) {
+    const uint32_t q4 = A.map.B >> 2;  // float4s in the row
+    const float4 *T4 = reinterpret_cast<const float4 *>(A.map.table + (uint64_t)ch * A.map.B);
+    for (uint32_t g = 0; 256u * g < q4; ++g) {
+        float4 t4[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t i = lane + 64u * (4u * g + (uint32_t)u);
+            t4[u] = T4[i < q4 ? i : 0u];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t i = lane + 64u * (4u * g + (uint32_t)u);
+            if (i < q4) reinterpret_cast<float4 *>(lds)[i] = t4[u];
+        }
+    }
+    s_render_frame<MapKind::Noop, true>(A, x, fs, lane, v);
+    lds_fence();
+    const uint32_t p0 = (uint32_t)(A.goff + fs) + 2u * lane;
+#pragma unroll
+    for (int b = 0; b < 64; ++b) {
+        const v2f t = *reinterpret_cast<const v2f *>(lds + ((p0 + 128u * (uint32_t)b) & A.map.b_mask));
+        v[b] = cx{v[b].r * t.x, v[b].i * t.y};
+    }
+}
+
 }  // namespace dspb

@@ -112,7 +112,8 @@ std::vector<std::string> split_top(const std::string &s) {
 }
 
 struct Module {
-    std::set<std::string> types;                       // %named types
+    std::set<std::string> types;                       // %named types (numbered ones too: %0 = type ...)
+    std::set<std::string> locals;                      // the analysed function's arguments and results
     std::map<std::string, bool> global_const;          // @global -> constant
     std::map<std::string, std::string> fn_attrs;       // @function -> its attribute groups' text
     std::map<std::string, std::string> attr_groups;    // #N -> text
@@ -135,7 +136,11 @@ std::vector<std::string> values_in(const std::string &s, const Module &M) {
         }
         const std::string tok = s.substr(i, j - i);
         const bool is_label = i >= 6 && s.compare(i - 6, 6, "label ") == 0;
-        if (tok.size() > 1 && !is_label && !(s[i] == '%' && M.types.count(tok))) v.push_back(tok);
+        // a numbered type (%0 = type ...) and a numbered value (%0, an
+        // unnamed argument) share their spelling: a token the function
+        // defines is taken as the value (at worst an extra dependence)
+        const bool is_type = s[i] == '%' && M.types.count(tok) && !M.locals.count(tok);
+        if (tok.size() > 1 && !is_label && !is_type) v.push_back(tok);
         i = j - 1;
     }
     return v;
@@ -490,6 +495,31 @@ struct Analysis {
                     for (int k = 0; k < n; ++k) d[k] = d[k] && dom[p][k];
                 d[b] = true;
                 if (d != dom[b]) dom[b] = d, changed = true;
+            }
+        }
+        // every cycle must be a natural loop: without the back edges (t -> h,
+        // h dominating t) the graph is acyclic, else the control flow is
+        // irreducible and a block could run more than once per iteration of
+        // the loops found below
+        {
+            std::vector<int> color(n, 0);  // 0 new, 1 on the stack, 2 done
+            std::vector<std::pair<int, size_t>> st;
+            for (int r = 0; r < n; ++r) {
+                if (color[r]) continue;
+                st.push_back({r, 0});
+                color[r] = 1;
+                while (!st.empty()) {
+                    auto &[b, k] = st.back();
+                    if (k == succ_[b].size()) {
+                        color[b] = 2;
+                        st.pop_back();
+                        continue;
+                    }
+                    const int t = succ_[b][k++];
+                    if (dom[b][t]) continue;  // a back edge
+                    if (color[t] == 1) return *why = "irreducible control flow", false;
+                    if (!color[t]) color[t] = 1, st.push_back({t, 0});
+                }
             }
         }
         // natural loops of the back edges t -> h (h dominates t), one per header
@@ -872,8 +902,16 @@ Facts analyze(const std::string &ir, const char *fn) {
                     else if (line[k] == ')' && --depth == 0) break;
                 }
                 for (const auto &p : split_top(line.substr(open + 1, k - open - 1))) {
-                    const auto v = values_in(p, M);
-                    A.args.push_back(v.empty() ? std::string() : v.back());
+                    // the parameter's name: its last %token (the type before it
+                    // may itself be a %type)
+                    const size_t at = p.rfind('%');
+                    std::string name;
+                    if (at != std::string::npos) {
+                        size_t e = at + 1;
+                        while (e < p.size() && ident_char(p[e])) ++e;
+                        name = p.substr(at, e - at);
+                    }
+                    A.args.push_back(name.size() > 1 ? name : std::string());
                 }
             }
             continue;
@@ -912,7 +950,7 @@ Facts analyze(const std::string &ir, const char *fn) {
         tail = trim(tail);
         // fast-math and wrap flags before the operands
         static const std::set<std::string> kFlags = {"nnan", "ninf", "nsz", "arcp", "contract", "afn", "reassoc",
-                                                     "fast", "nuw", "nsw", "exact", "disjoint", "nneg", "samesign",
+                                                     "fast", "nuw", "nsw", "nusw", "exact", "disjoint", "nneg", "samesign",
                                                      "volatile", "inbounds", "inrange"};
         for (;;) {
             const size_t sp = tail.find(' ');
@@ -936,6 +974,15 @@ Facts analyze(const std::string &ir, const char *fn) {
         A.f.why = "the analysis kernel does not have six parameters";
         return A.f;
     }
+    for (const auto &a : A.args)
+        if (a.empty()) {
+            A.f.why = "unparsed parameters of the analysis kernel";
+            return A.f;
+        }
+    // the function's own names: a numbered value shadows a numbered type
+    for (const auto &a : A.args) M.locals.insert(a);
+    for (const Inst &I : A.body)
+        if (!I.res.empty()) M.locals.insert(I.res);
     for (const Inst &I : A.body)
         if (!I.res.empty()) A.def[I.res] = &I;
     A.val[A.args[0]].org = O_PRM;

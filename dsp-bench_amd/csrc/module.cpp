@@ -690,6 +690,12 @@ dspb::irp::Facts analyze_source(const char *source) {
         f.why = "the analysis compile failed: " + log.substr(0, 300);
         return f;
     }
+    if (const char *dump = std::getenv("DSPB_PROOF_IR")) {  // diagnostics: the IR the analysis reads
+        if (FILE *fp = std::fopen(dump, "w")) {
+            std::fwrite(ir.data(), 1, ir.size(), fp);
+            std::fclose(fp);
+        }
+    }
     return dspb::irp::analyze(ir, "dspb_proof");
 }
 

@@ -427,6 +427,9 @@ void stft8192_pk_kernel(Stft8kArgs A) {
         if constexpr (MK == MapKind::Ramp && POW2) {
             if (A.map.B >= 4u && A.map.B <= 4096u) lds_table_frame(A, lds, fs, lane, v);
             else s_render_frame<MK, POW2>(A, x, fs, lane, v);
+        } else if constexpr (MK == MapKind::GainTable && POW2) {
+            if (A.map.B >= 4u && A.map.B <= 4096u) lds_gain_table_frame(A, lds, x, fs, lane, v, ch);
+            else s_render_frame<MK, POW2>(A, x, fs, lane, v, ch);
         } else {
             s_render_frame<MK, POW2>(A, x, fs, lane, v, ch);
         }

@@ -402,7 +402,8 @@ def test_verify_class_result_through_every_driver(torch_cuda):
 
 
 @pytest.mark.parametrize("name", ["balance", "fade_in", "half_block"])
-def test_gain_table_class_in_every_path(torch_cuda, oracle, name):
+@pytest.mark.parametrize("B", [512, 384, 2048])
+def test_gain_table_class_in_every_path(torch_cuda, oracle, name, B):
     """The gain-table class (round 5): per-(channel, position) gains proven
     from the IR (each element stored at most once, x G at x's address, G free
     of samples) and pinned by the probe of ones.  The fused render + STFT,
@@ -416,7 +417,7 @@ def test_gain_table_class_in_every_path(torch_cuda, oracle, name):
     params = mod.default_parameters()
     mod.initialize_state(params, 2, 48000.0)
     assert mod.facts["gain_table_form"], mod.facts
-    B, L_ = 512, 8192 * 9 + 700
+    L_ = 8192 * 9 + 700
     x = make_input(L_, seed=21)
     want = semantics(name, blocks(x, 2, B), params)
     xg = torch.from_numpy(x).cuda()

@@ -101,6 +101,9 @@ GT_SNIPPETS = {
     "shifted_index": ("for (u32 s = 0; s + 1 < B; ++s) out[0][s + 1] *= p.g;", False),
     "gain_from_a_sample": ("for (u32 s = 0; s < B; ++s) out[0][s] *= out[1][0];", False),
     "channel_from_sample_loop": ("for (u32 s = 0; s < B && s < C; ++s) out[s][s] *= p.g;", False),
+    # a cycle entered in its middle (no natural loop): refused whatever the index
+    "irreducible_goto": ("u32 s = 0; if (C > 1) goto mid; top: out[0][s] *= p.g; mid: ++s; if (s < B) goto top;",
+                         False),
 }
 
 
@@ -242,3 +245,28 @@ def test_no_fixpoint_means_no_facts():
     stock and test plugins all settle (above)."""
     f = facts_of(os.path.join(PLUG, "state_shaper.cpp"))
     assert f["analyzed"] and f["why"] != "no fixpoint after 64 passes"
+
+
+def test_numbered_types_do_not_hide_the_arguments():
+    """A callback calling double-precision sin links device-library
+    declarations that bring numbered types (%0 = type ...) into the module,
+    spelled like the analysis kernel's unnamed arguments %0 (Parameters) and
+    %1 (State).  The arguments must still be recognised: a State write is
+    seen, and an input-free tone stays a table candidate (round 5: the
+    Parameters / State pointers had lost their origins in such modules)."""
+    def src(body):
+        return ("#include \"plugin_header.h\"\n"
+                "struct Parameters { FLOAT_PARAM(20.0f, 2000.0f) f; };\nstruct State { float phase; };\n"
+                "Parameters default_parameters() { Parameters p = {375.0f}; return p; }\n"
+                "State initialize_state(const Parameters &p, const unsigned C, const float sr, void *ctx) "
+                "{ State s = {}; return s; }\n"
+                "void audio_callback(const Parameters &p, State &st, float **out, const u32 C, const u32 B, "
+                "const real32 sr) {\n" + body + "\n}\n")
+    tone = ("for (u32 s = 0; s < B; ++s) { const float v = (float)sin(2.0 * 3.14159265358979 * (double)p.f * "
+            "(double)s / (double)sr); for (u32 c = 0; c < C; ++c) out[c][s] = v; }")
+    f = dm.analyze_source(src(tone))
+    assert f["analyzed"] and not f["reads_block"] and not f["writes_state"], f
+    osc = ("for (u32 s = 0; s < B; ++s) { const float v = (float)sin((double)st.phase); st.phase += p.f / sr; "
+           "for (u32 c = 0; c < C; ++c) out[c][s] = v; }")
+    f = dm.analyze_source(src(osc))
+    assert (not f["analyzed"]) or f["writes_state"], f
