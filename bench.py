@@ -129,8 +129,14 @@ def source_plugin(d, pname: str, C: int, B: int, sr: int, specialize: bool = Tru
     return gmod, gplug, block_class
 
 
+# plugin sources of this repository (tests/plugins/, dsp-bench_amd/plugins/), not the reference's
+OWN_PLUGINS = {"balance": "tests/plugins", "fade_in": "tests/plugins", "biquad": "dsp-bench_amd/plugins"}
+
+
 def source_plugin_name(pname: str, block_class: str) -> str:
-    return (f"{pname}.cpp (DSP_PLUGIN_GENERIC, compiled unchanged from the reference source; block class "
+    origin = (f"this repository's {OWN_PLUGINS[pname]}/{pname}.cpp" if pname in OWN_PLUGINS
+              else "the reference source")
+    return (f"{pname}.cpp (DSP_PLUGIN_GENERIC, compiled unchanged from {origin}; block class "
             f"{block_class}: " + {"table": "its own callback's block, tiled, in the fused kernel",
                                   "gain": "the gain its callback gives, in the gain map",
                                   "gain_table": "the per-(channel, position) gains its callback gives, in the "
