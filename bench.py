@@ -193,7 +193,20 @@ PK_INST = {
     "ch96k": "stft8192_pk_kernel<1, 0, (dspb::MapKind)3, true, true, 4, 65543, 2>",
     "gain_stft": "stft8192_pk_kernel<1, 0, (dspb::MapKind)1, true, true, 0, 7, 2>",
     "stft96k": "stft8192_pk_kernel<0, 0, (dspb::MapKind)0, true, true, 0, 7, 2>",
+    # generic_stft by block class (the gain-table plugins balance.cpp / fade_in.cpp)
+    "generic_stft_gain_table": "stft8192_pk_kernel<1, 0, (dspb::MapKind)7, true, true, 0, 7, 2>",
+    # the biquad kind at one section (one channel per tile)
+    "biquad_1": "biquad_scan_kernel<1, false, 1>",
 }
+
+
+def pmc_key(wl: str, block_class, sections: int) -> str:
+    """The PK_INST / profiles/r*_pmc_<key>.json key of a bench command."""
+    if wl == "generic_stft":
+        return f"generic_stft_{block_class}"
+    if wl == "biquad":
+        return f"biquad_{sections}"
+    return wl
 
 
 def pmc_traffic(workload: str, alg_bytes: float):
@@ -852,7 +865,7 @@ def main():
                          "(profiles/r03_d2h_probe.txt)"}
         del pay, h_out, h_mag
 
-    traffic, traffic_src, traffic_inst = pmc_traffic(wl, bytes_per_launch)
+    traffic, traffic_src, traffic_inst = pmc_traffic(pmc_key(wl, block_class, args.sections), bytes_per_launch)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and wl == "headline":
