@@ -106,13 +106,16 @@ def parse():
     ap.add_argument("--mag-ld", type=int, default=None,
                     help="headline / gain_stft / stft96k / generic_stft: row stride of the spectra in floats "
                          "(default K = 4097, rows packed); the K bins written per row are the same")
+    ap.add_argument("--serial-state", action="store_true",
+                    help="biquad_src / sine_src: the serial chain (DSP_EXEC_SERIAL_STATE, one lane) instead of "
+                         "speculative segments (module.h dsp_state_spec_info)")
     ap.add_argument("--no-specialize", action="store_true",
                     help="generic / generic_stft: run the plugin's callback on every block "
                          "(DSP_EXEC_NO_SPECIALIZE) instead of its probed block class")
     return ap.parse_args()
 
 
-def source_plugin(d, pname: str, C: int, B: int, sr: int, specialize: bool = True):
+def source_plugin(d, pname: str, C: int, B: int, sr: int, specialize: bool = True, serial_state: bool = False):
     """A reference plugin source compiled unchanged by the product's plugin
     compiler (hiprtc -> gfx950, dsp-bench_amd/modules/mod_<pname>.co, built by
     tools/make_plugin_modules.py) as a DSP_PLUGIN_GENERIC plugin with its
@@ -124,7 +127,7 @@ def source_plugin(d, pname: str, C: int, B: int, sr: int, specialize: bool = Tru
         gmod = d.module.Module(f.read())
     gparams = gmod.default_parameters()
     gmod.initialize_state(gparams, C, float(sr))
-    gplug = gmod.plugin(gparams, pname, specialize=specialize)
+    gplug = gmod.plugin(gparams, pname, specialize=specialize, serial_state=serial_state)
     block_class = "callback" if not specialize else gmod.block_class(gparams, C, B, float(sr))[0]
     return gmod, gplug, block_class
 
@@ -498,8 +501,8 @@ def main():
     # cfg 5 shards by channel (one 96 kHz channel per GPU), the rest by time
     CH = 1 if wl == "ch96k" else globals()["CH"]
     minutes = args.minutes if wl not in ("gain10min", "fir1024") or args.minutes != 60.0 else 10.0
-    if wl in ("biquad_src", "sine_src") and args.minutes == 60.0:
-        minutes = 1.0  # the serial chain: ~10 Msamples/s
+    if (wl == "sine_src" or (wl == "biquad_src" and args.serial_state)) and args.minutes == 60.0:
+        minutes = 1.0  # the serial chain: ~10 Msamples/s (sine_test's phase never forgets: serial)
     L = int(round(minutes * 60 * sr))
     L -= L % HOP  # whole hops per rank (HOP is a multiple of B)
     # the file is world * L samples long; rank r owns [r L, (r+1) L) and
@@ -675,14 +678,18 @@ def main():
         alg_desc = "C*L*(4 + 4) B (each input sample read once + each output sample written once)"
     elif wl in ("biquad_src", "sine_src"):
         pname = "biquad" if wl == "biquad_src" else "sine_test"
-        gmod, gplug, block_class = source_plugin(d, pname, CH, B, sr)
-        plug_name = (f"{pname}.cpp compiled unchanged (DSP_PLUGIN_GENERIC; its callback writes its State: "
-                     "the serial chain, one lane)")
+        gmod, gplug, block_class = source_plugin(d, pname, CH, B, sr, serial_state=args.serial_state)
+        plug_name = (f"{pname}.cpp compiled unchanged (DSP_PLUGIN_GENERIC; its callback writes its State: " +
+                     ("the serial chain, one lane)" if args.serial_state else
+                      "speculative segments checked bit for bit against the State chain, serial where they "
+                      "differ)"))
 
         def step():
             d.render_offline(x, CH, B, float(sr), gplug, out=out)
         workload = f"{pname}.cpp via the generic plugin driver (B=512), {minutes:g} min of 48 kHz stereo per GPU"
-        kname = "dspb_render_st_c2b512 (generic driver: one chain through the State, LDS double buffer)"
+        kname = ("dspb_render_st_c2b512 (generic driver: one chain through the State, LDS double buffer)"
+                 if args.serial_state else
+                 "dspb_seg_c2b512 + dspb_seg_check + dspb_seg_walk (speculative segments, DESIGN 4.6)")
         alg_desc = "C*L*(4 + 4) B (read + write)" if pname == "biquad" else "C*L*4 B (write; the input is ignored)"
     elif wl in ("wav16enc", "wav24enc"):
         # SURVEY 8(f) row 1, the writer: planar float -> interleaved PCM
@@ -866,6 +873,8 @@ def main():
         del pay, h_out, h_mag
 
     traffic, traffic_src, traffic_inst = pmc_traffic(pmc_key(wl, block_class, args.sections), bytes_per_launch)
+    # the last timed render of a State-writing source plugin (module.h dsp_state_spec_info)
+    state_segments = gmod.state_spec() if wl in ("biquad_src", "sine_src") else None
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and wl == "headline":
@@ -902,6 +911,7 @@ def main():
                 "workload": workload,
                 "plugin": plug_name,
                 "block_class": block_class,
+                "state_segments": state_segments,
                 "mag_row_stride": LD if mag is not None else None,
                 "timed_launches_per_call": launches_per_call,
                 "ir_plugin": (None if wl not in ("headline", "ch96k") else
@@ -966,7 +976,11 @@ def main():
                             "the read + write stream (render_vec_kernel)" if wl == "generic" else
                             "the read + write stream and the two recurrence passes (DESIGN 4.7)" if wl == "biquad" else
                             "the serial chain: one lane runs the callback block after block (a State written "
-                            "every block); DESIGN 4.6" if wl in ("biquad_src", "sine_src") else
+                            "every block); DESIGN 4.6" if wl in ("biquad_src", "sine_src") and
+                            (args.serial_state or not (state_segments or {}).get("used")) else
+                            "segments: one lane per segment runs the callback block after block, 16 lanes per "
+                            "64 KB workgroup round (the LDS-blocks driver's capacity); DESIGN 4.6"
+                            if wl in ("biquad_src", "sine_src") else
                             "the render (LDS-capacity-bound callbacks) then the power-capped memory STFT, "
                             "serial: DESIGN 4.6, profiles/r02_generic_stft_schedules.txt"
                             if wl == "generic_stft" and block_class == "callback" else

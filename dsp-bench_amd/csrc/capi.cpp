@@ -732,6 +732,7 @@ static int plugin_map(const dsp_plugin *p, uint32_t B, int dev, hipStream_t s, S
         m->module = const_cast<void *>(p->module);
         m->gparams = p->params;
         m->gparams_size = p->params_size;
+        m->gflags = flags;
         return DSP_OK;
     default:
         return invalid("unknown plugin kind %d", p->kind);
@@ -897,7 +898,7 @@ static int render_device(const float *const *in, uint32_t in_ch, uint64_t L, flo
     if (map.kind == MapKind::Generic) {
         if (start != 0) return invalid("GENERIC render: the fused tail path does not apply");
         return module_render((::dsp_module *)map.module, map.gparams, map.gparams_size, in, in_ch, L, out, C, B,
-                             map.sr, goff, s);
+                             map.sr, goff, s, map.gflags);
     }
     if (map.kind == MapKind::Biquad) {  // the cascade from zero state at the start of the file
         if (start != 0 || goff != 0) return invalid("BIQUAD render: whole files only (sample_offset 0)");
@@ -1104,7 +1105,7 @@ static int generic_render_stft(const float *const *in, uint32_t in_ch, uint64_t 
                                float *const *mag, uint64_t ld, uint64_t goff, int dev, hipStream_t s) {
     const uint64_t Lr = (L + B - 1) / B * B;
     int st = module_render((::dsp_module *)map.module, map.gparams, map.gparams_size, in, in_ch, L, out, C, B,
-                           map.sr, goff, s);
+                           map.sr, goff, s, map.gflags);
     return st ? st : stft_device(out, C, Lr, N, H, window, K, mag, ld, dev, s);
 }
 

@@ -44,6 +44,7 @@ struct SampleMap {
     const void *gparams; // Generic: host Parameters blob
     uint32_t gparams_size;
     float sr;            // sample rate handed to the callback (Generic)
+    uint32_t gflags;     // Generic: the call's DSP_EXEC_* method flags (DSP_EXEC_SERIAL_STATE)
     // Ramp: table[i] = (float)(gain - i step) in closed form when the host
     // verified that IR_test's sequential f64 recurrence is exact for these
     // parameters and this B (capi.cpp ramp_closed_form); the table is then

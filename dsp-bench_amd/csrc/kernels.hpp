@@ -68,7 +68,7 @@ int launch_render(const RenderArgs &A, uint32_t C, bool vec, hipStream_t s);
 int launch_render_wrap(const RenderArgs &A, uint32_t C, uint64_t cursor, hipStream_t s);
 int module_render(::dsp_module *m, const void *params, uint32_t params_size, const float *const *in,
                   uint32_t in_ch, uint64_t L, float *const *out, uint32_t C, uint32_t B, float sr,
-                  uint64_t goff, hipStream_t s);
+                  uint64_t goff, hipStream_t s, uint32_t flags);
 int module_callback_once(::dsp_module *m, const void *params, uint32_t params_size, float *const *bufs, uint32_t C,
                          uint32_t B, float sr, hipStream_t s);
 int module_ir(::dsp_module *m, const void *params, uint32_t params_size, float *const *bufs, uint32_t C,

@@ -60,6 +60,15 @@ constexpr LdsShape kLdsShapes[7] = {{"dspb_render_lds", 0, 0},         {"dspb_re
 // the stateful LDS path's kernels: dspb_render covers every other shape
 constexpr LdsShape kStShapes[4] = {{"dspb_render_st_c2b512", 2, 512}, {"dspb_render_st_c2b256", 2, 256},
                                    {"dspb_render_st_c1", 1, 0}, {"dspb_render_st_c2", 2, 0}};
+// speculative segments of a stateful render (kDriver dspb_segments): pass 1 /
+// rerun kernels, most specific first, and the walk's
+constexpr LdsShape kSegShapes[4] = {{"dspb_seg_c2b512", 2, 512}, {"dspb_seg_c1", 1, 0}, {"dspb_seg_c2", 2, 0},
+                                    {"dspb_seg", 0, 0}};
+constexpr LdsShape kWalkShapes[2] = {{"dspb_seg_walk_c2b512", 2, 512}, {"dspb_seg_walk_any", 0, 0}};
+constexpr uint32_t kSegMaxState = 1024;   // bytes of State a lane copies (the walk keeps one in LDS)
+constexpr uint32_t kSegWarm0 = 4;         // blocks of warm-up of a first render
+constexpr uint32_t kSegWarmMax = 256;     // beyond this, the module renders its chain serially
+constexpr uint32_t kSegMinBlocks = 4;     // blocks per segment at least
 
 // Host mirror of the driver's argument block (same layout on both sides).
 struct RenderArgsG {
@@ -78,6 +87,21 @@ struct RenderArgsG {
     unsigned lds_nb;      // stateless LDS path: blocks per workgroup round
     unsigned lds_stride;  // stateless LDS path: floats per block in LDS (C B + 1)
     unsigned par;         // blocks render independently (dsp_module: par), in parallel
+};
+// Host mirror of kDriver's dspb_seg_args.
+struct SegArgsG {
+    RenderArgsG R;
+    void *st_blk;
+    void *st_end;
+    unsigned *list;
+    unsigned *count;
+    unsigned char *flags;
+    unsigned *stats;
+    unsigned long long seg;
+    unsigned K;
+    unsigned warm;
+    unsigned mode;
+    unsigned pass;
 };
 
 const char *kDriver = R"DSPB(
@@ -502,6 +526,379 @@ DSPB_ST_KERNEL(dspb_render_st_c2b256, 2, 256)
 DSPB_ST_KERNEL(dspb_render_st_c1, 1, 0)
 DSPB_ST_KERNEL(dspb_render_st_c2, 2, 0)
 
+// ---- a State the callback writes: speculative segments (module_render_seg)
+// The file's blocks are cut into K segments of `seg` blocks.  Pass 1 runs
+// every segment at once, one lane each, from the live State after `warm`
+// blocks of warm-up on the blocks before it (their output discarded), and
+// records the State it rendered each kept block from (st_blk, one per block
+// of the file) and the State it ended with (st_end).  The callback is a
+// function of (Parameters, State, block) -- the analysis proved it writes no
+// other memory -- so a segment whose first block's State equals, bit for bit,
+// the true State there rendered exactly what the serial chain renders;
+// segment 0 starts from the live State itself, and by induction every segment
+// k whose st_blk at its first block equals st_end[k - 1] is exact when
+// segment k - 1 is.  A check lists the others (and hands each its
+// predecessor's st_end), a rerun pass renders the listed segments again from
+// those States, in parallel, each only until its State meets the one
+// recorded at a block boundary (from there on the recorded blocks were
+// rendered from the same bits); after the last check one workgroup walks the
+// segments in order and reruns serially, with the same early stop, whatever
+// still differs, so the result is the serial chain's whatever the plugin
+// does.  Filters forget their State: their trajectories from different States
+// meet bit for bit within a few hundred samples, and one pass suffices.
+struct dspb_seg_args {
+    dspb_render_args R;
+    State *st_blk;          // [nblocks] the State each block was rendered from
+    State *st_end;          // [K] the State each segment ended with
+    unsigned *list;         // segments to rerun (check -> rerun)
+    unsigned *count;        // how many
+    unsigned char *flags;   // the last check: 1 = differed
+    unsigned *stats;        // per check: segments that differed; [3]: serial reruns of the walk
+    unsigned long long seg; // blocks per segment
+    unsigned K;             // segments
+    unsigned warm;          // pass 1: warm-up blocks
+    unsigned mode;          // segments: 0 = pass 1 (every segment), 1 = rerun the listed ones;
+                            // check: 1 = list the differing ones for a rerun (0: flag only)
+    unsigned pass;          // the check's stats slot
+};
+__device__ static bool dspb_same_state(const State *a, const State *b) {
+    bool same = true;
+    if constexpr (sizeof(State) % 4 == 0 && alignof(State) >= 4) {
+        const unsigned *x = (const unsigned *)a, *y = (const unsigned *)b;
+        for (unsigned i = 0; i < sizeof(State) / 4; ++i) same = same && x[i] == y[i];
+    } else {
+        const unsigned char *x = (const unsigned char *)a, *y = (const unsigned char *)b;
+        for (unsigned i = 0; i < sizeof(State); ++i) same = same && x[i] == y[i];
+    }
+    return same;
+}
+// lane t's segment: its index (~0u: none), first block rendered (warm-up
+// included), warm-up blocks, blocks rendered
+__device__ static unsigned dspb_seg_lane(const dspb_seg_args &G, unsigned base, unsigned t, unsigned nseg,
+                                         unsigned *s_first, unsigned *s_warm, unsigned *s_len) {
+    const dspb_render_args &A = G.R;
+    unsigned k = 0xffffffffu, f = 0, w = 0, len = 0;
+    if (base + t < nseg) {
+        k = G.mode ? G.list[base + t] : base + t;
+        const unsigned long long b0 = (unsigned long long)k * G.seg;
+        const unsigned long long b1 = b0 + G.seg < A.nblocks ? b0 + G.seg : A.nblocks;
+        w = (G.mode || k == 0) ? 0u : (unsigned)(G.warm < b0 ? G.warm : b0);
+        f = (unsigned)(b0 - w);
+        len = w + (unsigned)(b1 - b0);
+    }
+    s_first[t] = f;
+    s_warm[t] = w;
+    s_len[t] = len;
+    return k;
+}
+// a lane about to render block b in its round r (w: its warm-up blocks):
+// pass 1 records the State a kept block is rendered from; a rerun stops
+// (false) where its State meets the one recorded there
+__device__ static bool dspb_seg_block(const dspb_seg_args &G, unsigned long long b, unsigned r, unsigned w,
+                                      State &st) {
+    if (r < w) return true;  // warm-up: nothing kept
+    if (G.mode && r > 0 && dspb_same_state(&st, &G.st_blk[b])) return false;
+    __builtin_memcpy((void *)&G.st_blk[b], (const void *)&st, sizeof(State));
+    return true;
+}
+// pass 1 / rerun, any shape: lane t of wave 0 runs segment k_t, rounds of one
+// block per lane staged in LDS by all 256 threads (render_audio's copy: zeros
+// past EOF and for the channels the file lacks), kept blocks copied out after
+// the callbacks.  CC / BB constants as in the LDS-blocks path.
+template <unsigned CC, unsigned BB>
+__device__ static void dspb_segments(const dspb_seg_args &G) {
+    extern __shared__ float dspb_lbuf[];
+    __shared__ unsigned s_first[64], s_warm[64], s_len[64];
+    const dspb_render_args &A = G.R;
+    const unsigned C = CC ? CC : A.C, B = BB ? BB : A.B, CB = C * B, NB = A.lds_nb, SB = A.lds_stride;
+    const unsigned t = threadIdx.x, nt = blockDim.x;
+    const unsigned base = blockIdx.x * NB;
+    const unsigned nseg = G.mode ? *(volatile unsigned *)G.count : G.K;
+    if (base >= nseg) return;  // the same for the whole workgroup
+    unsigned k = 0xffffffffu;
+    if (t < NB) k = dspb_seg_lane(G, base, t, nseg, s_first, s_warm, s_len);
+    __syncthreads();
+    unsigned rounds = 0;
+    for (unsigned i = 0; i < NB; ++i) rounds = s_len[i] > rounds ? s_len[i] : rounds;
+    Parameters prm = dspb_from_global<Parameters>(A.P);
+    State st;
+    bool stopped = false;
+    if (k != 0xffffffffu)
+        __builtin_memcpy((void *)&st, G.mode ? (const void *)&G.st_blk[(unsigned long long)k * G.seg] : A.S,
+                         sizeof(State));
+    for (unsigned r = 0; r < rounds; ++r) {
+        for (unsigned j = t; j < NB * CB; j += nt) {
+            const unsigned i = j / CB, e = j - i * CB, c = e / B, s = e - c * B;
+            if (r < s_len[i]) {
+                const unsigned long long gi = (unsigned long long)(s_first[i] + r) * B + s;
+                dspb_lbuf[i * SB + e] = (c < A.in_ch && gi < A.L) ? ((const dspb_gfloat *)A.in[c])[gi] : 0.0f;
+            }
+        }
+        __syncthreads();
+        if (k != 0xffffffffu && r < s_len[t]) {
+            if (dspb_seg_block(G, (unsigned long long)s_first[t] + r, r, s_warm[t], st)) {
+                float *blk = dspb_lbuf + t * SB;
+                float *ptrs[CC ? CC : 16];
+                for (unsigned c = 0; c < C; ++c) ptrs[c] = blk + c * B;
+                audio_callback(prm, st, ptrs, C, B, A.sr);
+            } else {
+                s_len[t] = r;  // met the recorded chain: the rest stands
+                stopped = true;
+            }
+        }
+        __syncthreads();
+        for (unsigned j = t; j < NB * CB; j += nt) {
+            const unsigned i = j / CB, e = j - i * CB, c = e / B, s = e - c * B;
+            if (r >= s_warm[i] && r < s_len[i])
+                ((dspb_gfloat *)A.out[c])[(unsigned long long)(s_first[i] + r) * B + s] = dspb_lbuf[i * SB + e];
+        }
+        __syncthreads();
+        rounds = 0;
+        for (unsigned i = 0; i < NB; ++i) rounds = s_len[i] > rounds ? s_len[i] : rounds;
+    }
+    if (k != 0xffffffffu && !stopped) __builtin_memcpy((void *)&G.st_end[k], (const void *)&st, sizeof(State));
+}
+// the same for a constant shape (C, B, 4 | B), software pipelined: round r +
+// 1's blocks are in flight into registers (16-byte loads, all issued at once)
+// while round r's callbacks run; blocks at a stride of C B + 2 floats (float2
+// LDS moves; the 16 callback lanes on distinct banks), as dspb_stateless_lds_pf
+template <unsigned CC, unsigned BB>
+__device__ static void dspb_segments_pf(const dspb_seg_args &G) {
+    extern __shared__ float dspb_lbuf[];
+    __shared__ unsigned s_first[64], s_warm[64], s_len[64];
+    constexpr unsigned C = CC, B = BB, CB = C * B, SB = CB + 2u, NB = dspb_lds_nb(SB);
+    // per channel: NB rows of B / 4 float4, PV of them per thread
+    constexpr unsigned R4 = B / 4u, T4 = NB * R4, PV = (T4 + 255u) / 256u;
+    static_assert(NB <= 64 && B % 4 == 0, "one wave runs a round's callbacks");
+    typedef __attribute__((address_space(1))) float4 gfloat4;
+    const dspb_render_args &A = G.R;
+    const unsigned t = threadIdx.x;
+    const unsigned base = blockIdx.x * NB;
+    const unsigned nseg = G.mode ? *(volatile unsigned *)G.count : G.K;
+    if (base >= nseg) return;  // the same for the whole workgroup
+    unsigned k = 0xffffffffu;
+    if (t < NB) k = dspb_seg_lane(G, base, t, nseg, s_first, s_warm, s_len);
+    __syncthreads();
+    unsigned rounds = 0;
+    for (unsigned i = 0; i < NB; ++i) rounds = s_len[i] > rounds ? s_len[i] : rounds;
+    // the channels' rows as uniform values (the channel of every access below
+    // is a constant, so none of them is an indexed load of the argument block)
+    const dspb_gfloat *xin[C];
+    dspb_gfloat *xout[C];
+    bool aligned_in = true, aligned_out = true;
+#pragma unroll
+    for (unsigned c = 0; c < C; ++c) {
+        xin[c] = (const dspb_gfloat *)A.in[c < A.in_ch ? c : 0];
+        xout[c] = (dspb_gfloat *)A.out[c];
+        if (c < A.in_ch) aligned_in = aligned_in && !(((unsigned long long)A.in[c]) & 15);
+        aligned_out = aligned_out && !(((unsigned long long)A.out[c]) & 15);
+    }
+    Parameters prm = dspb_from_global<Parameters>(A.P);
+    State st;
+    bool stopped = false;
+    if (k != 0xffffffffu)
+        __builtin_memcpy((void *)&st, G.mode ? (const void *)&G.st_blk[(unsigned long long)k * G.seg] : A.S,
+                         sizeof(State));
+    float4 pf[C][PV];
+    auto load = [&](unsigned r) {
+#pragma unroll
+        for (unsigned c = 0; c < C; ++c) {
+#pragma unroll
+            for (unsigned v = 0; v < PV; ++v) {
+                const unsigned q = t + 256u * v, i = q / R4, s = (q - i * R4) * 4u;
+                float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
+                if ((T4 % 256u == 0 || q < T4) && r < s_len[i] && c < A.in_ch) {
+                    const unsigned long long gi = (unsigned long long)(s_first[i] + r) * B + s;
+                    if (aligned_in && gi + 4 <= A.L) {
+                        x = *(const gfloat4 *)(xin[c] + gi);
+                    } else {
+                        x.x = gi < A.L ? xin[c][gi] : 0.f;
+                        x.y = gi + 1 < A.L ? xin[c][gi + 1] : 0.f;
+                        x.z = gi + 2 < A.L ? xin[c][gi + 2] : 0.f;
+                        x.w = gi + 3 < A.L ? xin[c][gi + 3] : 0.f;
+                    }
+                }
+                pf[c][v] = x;
+            }
+        }
+    };
+    if (rounds) load(0);
+    for (unsigned r = 0; r < rounds; ++r) {
+#pragma unroll
+        for (unsigned c = 0; c < C; ++c) {
+#pragma unroll
+            for (unsigned v = 0; v < PV; ++v) {
+                const unsigned q = t + 256u * v, i = q / R4, s = (q - i * R4) * 4u;
+                if ((T4 % 256u == 0 || q < T4) && r < s_len[i]) {
+                    float2 *d = (float2 *)(dspb_lbuf + i * SB + c * B + s);
+                    d[0] = make_float2(pf[c][v].x, pf[c][v].y);
+                    d[1] = make_float2(pf[c][v].z, pf[c][v].w);
+                }
+            }
+        }
+        __syncthreads();
+        if (r + 1 < rounds) load(r + 1);  // in flight while the callbacks run
+        if (k != 0xffffffffu && r < s_len[t]) {
+            if (dspb_seg_block(G, (unsigned long long)s_first[t] + r, r, s_warm[t], st)) {
+                float *blk = dspb_lbuf + t * SB;
+                float *ptrs[C];
+                for (unsigned c = 0; c < C; ++c) ptrs[c] = blk + c * B;
+                audio_callback(prm, st, ptrs, C, B, A.sr);
+            } else {
+                s_len[t] = r;  // met the recorded chain: the rest stands
+                stopped = true;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (unsigned c = 0; c < C; ++c) {
+#pragma unroll
+            for (unsigned v = 0; v < PV; ++v) {
+                const unsigned q = t + 256u * v, i = q / R4, s = (q - i * R4) * 4u;
+                if ((T4 % 256u == 0 || q < T4) && r >= s_warm[i] && r < s_len[i]) {
+                    const unsigned long long gi = (unsigned long long)(s_first[i] + r) * B + s;
+                    const float2 *d = (const float2 *)(dspb_lbuf + i * SB + c * B + s);
+                    const float2 lo = d[0], hi = d[1];
+                    if (aligned_out) {
+                        *(gfloat4 *)(xout[c] + gi) = make_float4(lo.x, lo.y, hi.x, hi.y);
+                    } else {
+                        xout[c][gi] = lo.x, xout[c][gi + 1] = lo.y, xout[c][gi + 2] = hi.x, xout[c][gi + 3] = hi.y;
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        rounds = 0;
+        for (unsigned i = 0; i < NB; ++i) rounds = s_len[i] > rounds ? s_len[i] : rounds;
+    }
+    if (k != 0xffffffffu && !stopped) __builtin_memcpy((void *)&G.st_end[k], (const void *)&st, sizeof(State));
+}
+#define DSPB_SEG_KERNEL(name, CC, BB)                                                  \
+    extern "C" __global__ __launch_bounds__(256) void name(dspb_seg_args G) { dspb_segments<CC, BB>(G); }
+#define DSPB_SEG_PF_KERNEL(name, CC, BB)                                               \
+    extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) void name(  \
+        dspb_seg_args G) { dspb_segments_pf<CC, BB>(G); }
+DSPB_SEG_PF_KERNEL(dspb_seg_c2b512, 2, 512)
+DSPB_SEG_KERNEL(dspb_seg_c1, 1, 0)
+DSPB_SEG_KERNEL(dspb_seg_c2, 2, 0)
+DSPB_SEG_KERNEL(dspb_seg, 0, 0)
+// segment k (k >= 1) rendered its first block from st_blk[k seg]; the true
+// State there is st_end[k - 1] if segment k - 1 is exact: flag the segments
+// where the two differ and, when a rerun follows, list them and give each
+// the State to start again from
+extern "C" __global__ void dspb_seg_check(dspb_seg_args G) {
+    const unsigned k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= G.K) return;
+    if (k == 0) {
+        G.flags[0] = 0;
+        return;
+    }
+    State *first = &G.st_blk[(unsigned long long)k * G.seg];
+    const bool same = dspb_same_state(first, &G.st_end[k - 1]);
+    G.flags[k] = same ? 0 : 1;
+    if (!same) {
+        atomicAdd(&G.stats[G.pass], 1u);
+        if (G.mode) {
+            __builtin_memcpy((void *)first, (const void *)&G.st_end[k - 1], sizeof(State));
+            G.list[atomicAdd(G.count, 1u)] = k;
+        }
+    }
+}
+// the walk: one workgroup, segments in order; a segment is looked at when the
+// last check flagged it or its predecessor's final State changed here; one
+// whose first block's State differs is rendered serially from its
+// predecessor's final State (thread 0 runs the callback on an LDS double
+// buffer, the other waves stage blocks in and out, as dspb_stateful_lds)
+// until its State meets the recorded one.  Then the live State = the last
+// segment's final State.
+template <unsigned CC, unsigned NB_>
+__device__ static void dspb_seg_walk(const dspb_seg_args &G) {
+    extern __shared__ float dspb_lbuf[];
+    __shared__ unsigned s_next;
+    __shared__ int s_bad, s_stop;
+    __shared__ unsigned long long s_prev[(sizeof(State) + 7) / 8];  // the predecessor's final State
+    const dspb_render_args &A = G.R;
+    const unsigned B = NB_ ? NB_ : A.B, C = CC ? CC : A.C, CB = C * B, t = threadIdx.x, nt = blockDim.x;
+    float *buf0 = dspb_lbuf, *buf1 = dspb_lbuf + CB;
+    Parameters prm = dspb_from_global<Parameters>(A.P);
+    State local;
+    bool prev_ended = false;  // s_prev holds a final State the walk rendered
+    unsigned reruns = 0;
+    for (unsigned k = 1; k < G.K; ++k) {
+        if (!prev_ended) {  // the next flagged segment at or after k
+            unsigned found = G.K;
+            for (unsigned c0 = k; c0 < G.K && found == G.K; c0 += nt) {
+                if (t == 0) s_next = G.K;
+                __syncthreads();
+                if (c0 + t < G.K && G.flags[c0 + t]) atomicMin(&s_next, c0 + t);
+                __syncthreads();
+                found = s_next;
+                __syncthreads();
+            }
+            if (found >= G.K) break;
+            k = found;
+            for (unsigned i = t; i < sizeof(State); i += nt)
+                ((unsigned char *)s_prev)[i] = ((const unsigned char *)&G.st_end[k - 1])[i];
+        }
+        const unsigned long long b0 = (unsigned long long)k * G.seg;
+        const unsigned long long b1 = b0 + G.seg < A.nblocks ? b0 + G.seg : A.nblocks;
+        if (t == 0) s_bad = 0;
+        __syncthreads();
+        for (unsigned i = t; i < sizeof(State); i += nt)
+            if (((const unsigned char *)s_prev)[i] != ((const unsigned char *)&G.st_blk[b0])[i]) s_bad = 1;
+        __syncthreads();
+        prev_ended = false;
+        if (s_bad) {
+            ++reruns;
+            __builtin_memcpy((void *)&local, (const void *)s_prev, sizeof(State));
+            dspb_stage_in(A, b0, buf0, t, nt);
+            __syncthreads();
+            unsigned long long b = b0;
+            bool ended = true;
+            for (; b < b1; ++b) {
+                float *cur = ((b - b0) & 1) ? buf1 : buf0, *oth = ((b - b0) & 1) ? buf0 : buf1;
+                if (t == 0) {  // does the chain meet the recorded one here?
+                    s_stop = (b > b0 && dspb_same_state(&local, &G.st_blk[b])) ? 1 : 0;
+                    if (!s_stop) __builtin_memcpy((void *)&G.st_blk[b], (const void *)&local, sizeof(State));
+                }
+                __syncthreads();
+                if (s_stop) {
+                    ended = false;
+                    break;
+                }
+                if (t == 0) {
+                    float *ptrs[CC ? CC : 16];
+                    for (unsigned c = 0; c < C; ++c) ptrs[c] = cur + c * B;
+                    audio_callback(prm, local, ptrs, C, B, A.sr);
+                } else if (t >= 64) {
+                    if (b > b0) dspb_stage_out(A, b - 1, oth, t - 64, nt - 64);
+                    if (b + 1 < b1) dspb_stage_in(A, b + 1, oth, t - 64, nt - 64);
+                }
+                __syncthreads();
+            }
+            // the last block rendered here
+            dspb_stage_out(A, b - 1, ((b - 1 - b0) & 1) ? buf1 : buf0, t, nt);
+            if (ended && t == 0) {
+                __builtin_memcpy((void *)s_prev, (const void *)&local, sizeof(State));
+                __builtin_memcpy((void *)&G.st_end[k], (const void *)&local, sizeof(State));
+            }
+            prev_ended = ended;
+            __syncthreads();
+        }
+    }
+    __syncthreads();
+    if (t == 0) G.stats[3] = reruns;
+    // the live State: the last segment's final State (s_prev when the walk
+    // rendered it to its end, else st_end as pass 1 / a rerun left it)
+    const unsigned char *last = prev_ended ? (const unsigned char *)s_prev
+                                           : (const unsigned char *)&G.st_end[G.K - 1];
+    for (unsigned i = t; i < sizeof(State); i += nt) ((unsigned char *)A.S)[i] = last[i];
+}
+#define DSPB_WALK_KERNEL(name, CC, BB)                                                 \
+    extern "C" __global__ __launch_bounds__(256) void name(dspb_seg_args G) { dspb_seg_walk<CC, BB>(G); }
+DSPB_WALK_KERNEL(dspb_seg_walk_c2b512, 2, 512)
+DSPB_WALK_KERNEL(dspb_seg_walk_any, 0, 0)
+
 // compute_IR (plugin.cpp:17-58): the callback once, on buffers as they are
 extern "C" __global__ void dspb_callback(dspb_render_args A) {
     float *ptrs[16];
@@ -532,6 +929,32 @@ struct dsp_module {
     // existed): [0] any (C, B), then the instantiations of kLdsShapes
     hipFunction_t f_render_lds[7] = {};
     hipFunction_t f_render_st[4] = {};  // kStShapes (NULL: dspb_render)
+    // speculative segments (kSegShapes, the check, kWalkShapes; NULL in code
+    // objects compiled before them: the serial chain)
+    hipFunction_t f_seg[4] = {}, f_seg_check = nullptr, f_seg_walk[2] = {};
+    struct SegWork {
+        void *blk = nullptr;           // [cap_blk] States: st_blk
+        void *end = nullptr;           // [cap] States: st_end
+        uint64_t cap_blk = 0;
+        unsigned *list = nullptr;      // [cap]
+        unsigned char *flags = nullptr;  // [cap]
+        unsigned *words = nullptr;     // [0] count, [4..8) stats
+        uint32_t cap = 0;
+        // the counters of the last two speculative renders: pinned copies
+        // [2][4], each behind an event, read back without waiting by a later
+        // call (what the module learns) or waiting by dsp_module_state_spec
+        unsigned *h_stats = nullptr;
+        hipEvent_t ev[2] = {};
+        bool pending[2] = {};
+        uint64_t seq[2] = {};
+        dsp_state_spec_info info[2] = {};
+        uint64_t calls = 0;
+        dsp_state_spec_info last{};    // the newest render whose counters were read
+        bool serial = false;           // the module's last State-writing render was the serial chain
+        uint32_t warm = 0;             // learned warm-up for `params` (0: not yet)
+        bool off = false;              // learned: the chain does not forget its State
+        std::vector<unsigned char> params;
+    } seg;
     hipFunction_t f_sizes = nullptr, f_defaults = nullptr, f_init = nullptr, f_render = nullptr,
                   f_callback = nullptr;
     uint32_t params_size = 0, state_size = 0;
@@ -582,6 +1005,7 @@ struct dsp_module {
 namespace dspb {
 void set_last_error(const char *fmt, ...);
 int hip_fail(hipError_t e, const char *what);
+int module_seg_collect(dsp_module *m, bool wait);
 }  // namespace dspb
 using dspb::set_last_error;
 
@@ -816,12 +1240,16 @@ int dsp_module_load(const void *code, uint64_t code_size, int device, dsp_module
             m->f_render_lds[i] = nullptr;
         }
     }
-    for (int i = 0; i < 4; ++i) {
-        if (hipModuleGetFunction(&m->f_render_st[i], m->mod, kStShapes[i].name) != hipSuccess) {
+    auto optional = [&](hipFunction_t *f, const char *name) {
+        if (hipModuleGetFunction(f, m->mod, name) != hipSuccess) {
             (void)hipGetLastError();
-            m->f_render_st[i] = nullptr;
+            *f = nullptr;
         }
-    }
+    };
+    for (int i = 0; i < 4; ++i) optional(&m->f_render_st[i], kStShapes[i].name);
+    for (int i = 0; i < 4; ++i) optional(&m->f_seg[i], kSegShapes[i].name);
+    for (int i = 0; i < 2; ++i) optional(&m->f_seg_walk[i], kWalkShapes[i].name);
+    optional(&m->f_seg_check, "dspb_seg_check");
     unsigned *d_o = nullptr;
     if ((e = hipMalloc(&d_o, 4 * sizeof(unsigned))) != hipSuccess) return fail(dspb::hip_fail(e, "hipMalloc"));
     void *args[] = {&d_o};
@@ -869,12 +1297,15 @@ void dsp_module_destroy(dsp_module *m) {
             (void)hipFree(u->table);
             for (auto &kv : u->ev) (void)hipEventDestroy(kv.second);
         }
-        for (hipEvent_t e : {m->upload_ev, m->use_ev})
+        for (hipEvent_t e : {m->upload_ev, m->use_ev, m->seg.ev[0], m->seg.ev[1]})
             if (e) {
                 (void)hipEventSynchronize(e);
                 (void)hipEventDestroy(e);
             }
         if (m->h_params) (void)hipHostFree(m->h_params);
+        if (m->seg.h_stats) (void)hipHostFree(m->seg.h_stats);
+        for (void *p : {m->seg.blk, m->seg.end, (void *)m->seg.list, (void *)m->seg.flags, (void *)m->seg.words})
+            if (p) (void)hipFree(p);
         if (m->mod) (void)hipModuleUnload(m->mod);
         if (prev >= 0 && prev != m->device) (void)hipSetDevice(prev);
     }
@@ -907,6 +1338,18 @@ int dsp_module_block_class(dsp_module *m, const void *params, uint32_t params_si
 int dsp_module_retired_tables(dsp_module *m, uint64_t *n) {
     if (!m || !n) return DSP_ERR_INVALID;
     *n = dspb::module_spec_retired(m);
+    return DSP_OK;
+}
+
+int dsp_module_state_spec(dsp_module *m, dsp_state_spec_info *out) {
+    if (!m || !out) {
+        set_last_error("dsp_module_state_spec: NULL argument");
+        return DSP_ERR_INVALID;
+    }
+    std::lock_guard<std::mutex> lk(m->mu);
+    if (int st = dspb::module_seg_collect(m, true)) return st;
+    *out = m->seg.serial ? dsp_state_spec_info{} : m->seg.last;
+    out->disabled = m->seg.off ? 1 : 0;
     return DSP_OK;
 }
 
@@ -1229,10 +1672,153 @@ static int check_device(const dsp_module *m) {
     return DSP_OK;
 }
 
+// The last speculative render's counters (pinned copy, behind an event):
+// into m->seg.last, and what they teach about the current Parameters -- a
+// pass where more than 1/8 of the segments started from a State that was not
+// the true one asks for a longer warm-up (x4; x16 when half of them still
+// differed after both reruns: the trajectories do not meet within a
+// segment), and past kSegWarmMax the chain is rendered serially.  wait =
+// false reads them only if they have landed (a render never waits for them).
+int module_seg_collect(dsp_module *m, bool wait) {
+    auto &W = m->seg;
+    for (int pass = 0; pass < 2; ++pass) {
+        // the older slot first
+        const int i = (W.pending[0] && W.pending[1]) ? (W.seq[0] < W.seq[1] ? pass : 1 - pass) : pass;
+        if (!W.pending[i]) continue;
+        if (wait) MOD_HIP(hipEventSynchronize(W.ev[i]));
+        else if (hipEventQuery(W.ev[i]) != hipSuccess) {
+            (void)hipGetLastError();
+            continue;
+        }
+        W.pending[i] = false;
+        dsp_state_spec_info &r = W.info[i];
+        const unsigned *h = W.h_stats + 4 * i;
+        for (int j = 0; j < 3; ++j) r.differed[j] = h[j];
+        r.serial_reruns = h[3];
+        if (W.seq[i] == W.calls) W.last = r;
+        // learn only from renders made with the warm-up now in force, and
+        // only from the segments whose warm-up began after block 0 (those
+        // before start from the true State)
+        const uint64_t early = std::min<uint64_t>(r.segments - 1, r.warmup_blocks / r.blocks_per_segment);
+        const uint64_t guessed = r.segments - 1 - early;
+        if (r.warmup_blocks == W.warm && !W.off && guessed && r.differed[0] * 8ull > guessed) {
+            const uint32_t grow = r.differed[2] * 2ull > guessed ? 16u : 4u;
+            if (W.warm >= kSegWarmMax) W.off = true;
+            else W.warm = std::min<uint32_t>(W.warm * grow, kSegWarmMax);
+        }
+    }
+    return DSP_OK;
+}
+
+// rows [in[c], in[c] + L) and [out[c'], out[c'] + Lr) share an element
+static bool module_rows_overlap(const float *const *in, uint32_t in_ch, uint64_t L, const float *const *out,
+                                uint32_t C, uint64_t Lr) {
+    for (uint32_t a = 0; a < in_ch; ++a)
+        for (uint32_t b = 0; b < C; ++b)
+            if (in[a] < out[b] + Lr && out[b] < in[a] + L) return true;
+    return false;
+}
+
+// A State-writing callback over the whole file as speculative segments
+// (kDriver dspb_segments); returns 1 (nothing launched) when the shape does
+// not fit them -- the caller renders the serial chain.
+static int module_render_seg(dsp_module *m, RenderArgsG &A, hipStream_t s) {
+    const uint32_t C = A.C, B = A.B;
+    if (2ull * C * B * sizeof(float) > kStagedLdsBytes) return 1;  // the walk's double buffer
+    hipFunction_t f = nullptr, fw = nullptr;
+    int fi = -1;
+    for (int i = 0; i < 4 && !f; ++i)
+        if (m->f_seg[i] && (!kSegShapes[i].C || kSegShapes[i].C == C) && (!kSegShapes[i].B || kSegShapes[i].B == B))
+            f = m->f_seg[fi = i];
+    // the constant-shape kernel (dspb_segments_pf) strides blocks by C B + 2
+    const uint64_t stride = (uint64_t)C * B + (fi == 0 ? 2 : 1);
+    const uint64_t nb = std::min<uint64_t>(64, kLdsRoundBytes / (stride * sizeof(float)) / 4 * 4);
+    if (nb < 4) return 1;
+    for (int i = 0; i < 2 && !fw; ++i)
+        if (m->f_seg_walk[i] && (!kWalkShapes[i].C || kWalkShapes[i].C == C) &&
+            (!kWalkShapes[i].B || kWalkShapes[i].B == B))
+            fw = m->f_seg_walk[i];
+    if (!f || !fw || !m->f_seg_check) return 1;
+    auto &W = m->seg;
+    // segments: as many as the chip runs lanes at once (two workgroups per
+    // CU, nb lanes each), kSegMinBlocks blocks at least
+    const uint64_t lanes = kLdsWgPerCu * (uint64_t)m->cus * nb;
+    const uint64_t seg = std::max<uint64_t>((A.nblocks + lanes - 1) / lanes, kSegMinBlocks);
+    const uint64_t K = (A.nblocks + seg - 1) / seg;
+    // (block indices in 32 bits; one recorded State per block, at most 8 GB of them)
+    if (K < 2 || A.nblocks >= (1ull << 32) || A.nblocks * m->state_size > (8ull << 30)) return 1;
+    if (K > W.cap || A.nblocks > W.cap_blk) {
+        if (int st = wait_uses(m)) return st;
+        for (void *p : {W.blk, W.end, (void *)W.list, (void *)W.flags}) if (p) (void)hipFree(p);
+        W.blk = W.end = nullptr, W.list = nullptr, W.flags = nullptr, W.cap = 0, W.cap_blk = 0;
+        const uint32_t cap = (uint32_t)std::max<uint64_t>(K, 1024);
+        const uint64_t cap_blk = std::max<uint64_t>(A.nblocks, 4096);
+        MOD_HIP(hipMalloc(&W.blk, cap_blk * m->state_size));
+        MOD_HIP(hipMalloc(&W.end, (uint64_t)cap * m->state_size));
+        MOD_HIP(hipMalloc(&W.list, cap * sizeof(unsigned)));
+        MOD_HIP(hipMalloc(&W.flags, cap));
+        W.cap = cap;
+        W.cap_blk = cap_blk;
+    }
+    if (!W.words) {
+        MOD_HIP(hipMalloc(&W.words, 16 * sizeof(unsigned)));
+        MOD_HIP(hipHostMalloc(&W.h_stats, 8 * sizeof(unsigned), hipHostMallocDefault));
+        for (hipEvent_t &e : W.ev) MOD_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    // the slot this call fills: the one of the render two calls back, whose
+    // counters have landed by now in a stream of back-to-back calls
+    const int slot = W.seq[0] <= W.seq[1] ? 0 : 1;
+    if (W.pending[slot]) {
+        MOD_HIP(hipEventSynchronize(W.ev[slot]));
+        if (int st = module_seg_collect(m, false)) return st;
+    }
+    SegArgsG G{};
+    G.R = A;
+    G.R.lds_nb = (unsigned)nb;
+    G.R.lds_stride = (unsigned)stride;
+    G.st_blk = W.blk;
+    G.st_end = W.end;
+    G.list = W.list;
+    G.count = W.words;
+    G.flags = W.flags;
+    G.stats = W.words + 4;
+    G.seg = seg;
+    G.K = (unsigned)K;
+    G.warm = W.warm;
+    void *args[] = {&G};
+    const unsigned lds = (unsigned)(nb * stride * sizeof(float));
+    const unsigned gseg = (unsigned)((K + nb - 1) / nb), gchk = (unsigned)((K + 255) / 256);
+    MOD_HIP(hipMemsetAsync(W.words, 0, 16 * sizeof(unsigned), s));
+    G.mode = 0;
+    MOD_HIP(hipModuleLaunchKernel(f, gseg, 1, 1, 256, 1, 1, lds, s, args, nullptr));
+    for (unsigned p = 0; p < 3; ++p) {  // check, rerun, check, rerun, check (flags only)
+        G.pass = p;
+        G.mode = p < 2 ? 1 : 0;  // the check lists the segments for a rerun; the last one only flags them
+        MOD_HIP(hipMemsetAsync(W.words, 0, sizeof(unsigned), s));
+        MOD_HIP(hipModuleLaunchKernel(m->f_seg_check, gchk, 1, 1, 256, 1, 1, 0, s, args, nullptr));
+        if (p == 2) break;
+        MOD_HIP(hipModuleLaunchKernel(f, gseg, 1, 1, 256, 1, 1, lds, s, args, nullptr));
+    }
+    MOD_HIP(hipModuleLaunchKernel(fw, 1, 1, 1, 256, 1, 1, (unsigned)(2ull * C * B * sizeof(float)), s, args,
+                                  nullptr));
+    MOD_HIP(hipMemcpyAsync(W.h_stats + 4 * slot, W.words + 4, 4 * sizeof(unsigned), hipMemcpyDeviceToHost, s));
+    MOD_HIP(hipEventRecord(W.ev[slot], s));
+    W.pending[slot] = true;
+    W.seq[slot] = ++W.calls;
+    dsp_state_spec_info &r = W.info[slot];
+    r = dsp_state_spec_info{};
+    r.used = 1;
+    r.segments = (uint32_t)K;
+    r.blocks_per_segment = (uint32_t)seg;
+    r.warmup_blocks = W.warm;
+    MOD_HIP(hipEventRecord(m->use_ev, s));
+    return DSP_OK;
+}
+
 // dsp_render_offline / dsp_render_stft with DSP_PLUGIN_GENERIC (device buffers)
 int module_render(dsp_module *m, const void *params, uint32_t params_size, const float *const *in,
                   uint32_t in_ch, uint64_t L, float *const *out, uint32_t C, uint32_t B, float sr,
-                  uint64_t goff, hipStream_t s) {
+                  uint64_t goff, hipStream_t s, uint32_t flags) {
     if (!m || !m->initialized) {
         set_last_error("GENERIC plugin: module not loaded / initialize_state not run");
         return DSP_ERR_INVALID;
@@ -1315,6 +1901,27 @@ int module_render(dsp_module *m, const void *params, uint32_t params_size, const
         const uint64_t g = (A.nblocks + 63) / 64;
         grid = (unsigned)(g < 65535 ? g : 65535);
     }
+    // a State the callback writes, and no other memory (the analysis), a
+    // State a lane can copy, rows apart: speculative segments, the serial
+    // chain's bits (module_render_seg)
+    if (!par && !(flags & DSP_EXEC_SERIAL_STATE) && m->has_facts && m->facts.analyzed && m->facts.writes_state &&
+        m->state_size > 0 && m->state_size <= kSegMaxState &&
+        !module_rows_overlap(in, in_ch, L, out, C, A.nblocks * B)) {
+        auto &W = m->seg;
+        if (int st = module_seg_collect(m, false)) return st;
+        const unsigned char *pb = (const unsigned char *)params;
+        if (!W.warm || W.params.size() != params_size || (params_size && std::memcmp(W.params.data(), pb, params_size))) {
+            W.params.assign(pb, pb + params_size);  // new Parameters: learn again
+            W.warm = kSegWarm0;
+            W.off = false;
+        }
+        if (!W.off) {
+            const int st = module_render_seg(m, A, s);
+            W.serial = st > 0;
+            if (st <= 0) return st;
+        }
+    }
+    if (!par) m->seg.serial = true;
     hipFunction_t f = m->f_render;
     if (!par && 2ull * C * B * sizeof(float) <= kStagedLdsBytes) {
         // stateful: 4 waves, the block double-buffer in LDS (the callback's

@@ -34,6 +34,7 @@ DSP_EXEC_SYNC = 0x2
 DSP_EXEC_FIR_DIRECT = 0x4
 DSP_EXEC_NO_SPECIALIZE = 0x8
 DSP_EXEC_VERIFY_CLASS = 0x10
+DSP_EXEC_SERIAL_STATE = 0x20
 DSP_RESULT_CLASS = 0x1
 DSP_RESULT_VERIFIED = 0x2
 DSP_RESULT_RERENDERED = 0x4
@@ -110,6 +111,17 @@ class dsp_callback_facts(C.Structure):  # module.h
                 "table_why": self.table_why.decode(errors="replace")}
 
 
+class dsp_state_spec_info(C.Structure):  # module.h
+    _fields_ = [("used", C.c_int32), ("disabled", C.c_int32), ("segments", C.c_uint32),
+                ("blocks_per_segment", C.c_uint32), ("warmup_blocks", C.c_uint32), ("differed", C.c_uint32 * 3),
+                ("serial_reruns", C.c_uint32)]
+
+    def as_dict(self) -> dict:
+        return {"used": bool(self.used), "disabled": bool(self.disabled), "segments": int(self.segments),
+                "blocks_per_segment": int(self.blocks_per_segment), "warmup_blocks": int(self.warmup_blocks),
+                "differed": [int(v) for v in self.differed], "serial_reruns": int(self.serial_reruns)}
+
+
 # name -> (restype, argtypes)
 _SIGS = {
     "dsp_abi_version": (C.c_int, []),
@@ -161,6 +173,7 @@ _SIGS = {
     "dsp_module_block_class": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_float,
                                          C.POINTER(C.c_int32), C.POINTER(C.c_float), C.POINTER(dsp_exec)]),
     "dsp_module_facts": (C.c_int, [C.c_void_p, C.POINTER(dsp_callback_facts)]),
+    "dsp_module_state_spec": (C.c_int, [C.c_void_p, C.POINTER(dsp_state_spec_info)]),
     "dsp_plugin_analyze": (C.c_int, [C.c_char_p, C.POINTER(dsp_callback_facts)]),
     "dsp_code_facts": (C.c_int, [C.c_void_p, C.c_uint64, C.POINTER(dsp_callback_facts)]),
     "dsp_descriptor_from_code": (C.c_int, [C.c_void_p, C.c_uint64, C.POINTER(C.c_void_p)]),

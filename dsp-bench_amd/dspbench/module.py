@@ -230,17 +230,31 @@ class Module:
         check(L.lib().dsp_module_read_state(self.handle, buf), "dsp_module_read_state")
         return buf.raw[:self.state_size]
 
-    def plugin(self, params: bytes, name: str = "generic", specialize: bool = True, verify: bool = False):
+    def plugin(self, params: bytes, name: str = "generic", specialize: bool = True, verify: bool = False,
+               serial_state: bool = False):
         """A GENERIC plugin over this module.  specialize=False runs the
         plugin's callback on every block (DSP_EXEC_NO_SPECIALIZE); by default
         a plugin whose block class its IR proves runs as that class
         (block_class).  verify=True checks blocks of every call against the
-        callback (DSP_EXEC_VERIFY_CLASS; dspbench.api.last_result())."""
+        callback (DSP_EXEC_VERIFY_CLASS; dspbench.api.last_result()).
+        serial_state=True renders a State-writing callback as one chain
+        (DSP_EXEC_SERIAL_STATE) instead of speculative segments (state_spec)."""
         from .api import Plugin
         flags = 0 if specialize else L.DSP_EXEC_NO_SPECIALIZE
         if verify:
             flags |= L.DSP_EXEC_VERIFY_CLASS
+        if serial_state:
+            flags |= L.DSP_EXEC_SERIAL_STATE
         return Plugin(L.DSP_PLUGIN_GENERIC, bytes(params), b"", name, self, exec_flags=flags)
+
+    def state_spec(self) -> dict:
+        """The module's last render of a State-writing callback in speculative
+        segments (dsp_module_state_spec; waits for it): used, disabled,
+        segments, blocks_per_segment, warmup_blocks, differed (pass 1, rerun 1,
+        rerun 2), serial_reruns."""
+        info = L.dsp_state_spec_info()
+        check(L.lib().dsp_module_state_spec(self.handle, C.byref(info)), "dsp_module_state_spec")
+        return info.as_dict()
 
     def retired_tables(self) -> int:
         """Evicted TABLE-class blocks not freed yet (dsp_module_retired_tables)."""

@@ -116,9 +116,14 @@ typedef struct dsp_plugin {
                                       chunked (dsp_render_stft_host / _wav) and sharded drivers,
                                       whose result ORs their chunks' bits; dsp_render_loop with
                                       the flag runs the callback on every block (result 0) */
+#define DSP_EXEC_SERIAL_STATE 0x20u /* DSP_PLUGIN_GENERIC whose callback writes its State: one chain
+                                      of blocks in order on one lane, as the reference's audio thread
+                                      runs them (default: speculative segments, module.h
+                                      dsp_state_spec_info -- the same bits) */
 /* the flags that choose how a call computes (not where its buffers live):
  * the chunked and sharded drivers pass them on to every chunk */
-#define DSP_EXEC_METHOD_FLAGS (DSP_EXEC_FIR_DIRECT | DSP_EXEC_NO_SPECIALIZE | DSP_EXEC_VERIFY_CLASS)
+#define DSP_EXEC_METHOD_FLAGS \
+    (DSP_EXEC_FIR_DIRECT | DSP_EXEC_NO_SPECIALIZE | DSP_EXEC_VERIFY_CLASS | DSP_EXEC_SERIAL_STATE)
 
 /* dsp_exec.result bits (written when result is not NULL) */
 #define DSP_RESULT_CLASS 0x1u      /* a GENERIC plugin ran as its block class */

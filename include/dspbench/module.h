@@ -200,6 +200,36 @@ int dsp_module_block_class(dsp_module *m, const void *params, uint32_t params_si
  * freed yet (diagnostic; frees what can be freed first). */
 int dsp_module_retired_tables(dsp_module *m, uint64_t *n);
 
+/* ---- a State the callback writes: speculative segments -------------------
+ * The reference runs such a callback block after block (audio.cpp:160-165);
+ * one GPU lane running that chain is slower than a host core.  When the
+ * analysis proved that the callback writes no memory but its State and its
+ * block (dsp_callback_facts: analyzed, writes_state) and the State is at most
+ * 1024 bytes, dsp_render_offline / dsp_render_stft (input and output rows
+ * apart) cut the file into segments rendered at once, each from the live State
+ * after a warm-up on the blocks before it, and keep a segment's output only
+ * when the State it started from equals, bit for bit, the State the previous
+ * segment ended with; the others are rendered again from that State (two
+ * parallel passes, then serially in file order).  Output and final State are
+ * the serial chain's, bit for bit, for any such callback.  It is fast when the
+ * callback forgets its State (filters, envelopes, smoothers: trajectories
+ * from different States meet exactly within a few hundred samples); when it
+ * does not (an oscillator's phase) the call costs the serial chain plus one
+ * pass, the warm-up grows on later calls, and past 256 blocks the module
+ * renders these Parameters serially.  DSP_EXEC_SERIAL_STATE (dspbench.h)
+ * forces the serial chain. */
+typedef struct dsp_state_spec_info {
+    int32_t used;                /* the module's last State-writing render ran in segments */
+    int32_t disabled;            /* learned: serial for the current Parameters */
+    uint32_t segments;           /* K of that render */
+    uint32_t blocks_per_segment;
+    uint32_t warmup_blocks;
+    uint32_t differed[3];        /* segments whose start State differed: pass 1, rerun 1, rerun 2 */
+    uint32_t serial_reruns;      /* segments the in-order walk rendered again */
+} dsp_state_spec_info;
+/* Waits for the module's last speculative render and describes it. */
+int dsp_module_state_spec(dsp_module *m, dsp_state_spec_info *out);
+
 /* ---- what the callback does with its block (no GPU) ----------------------
  * dsp_module_compile compiles the plugin a second time into an analysis
  * kernel, dspb_proof(P, S, out, C, B, sr) { audio_callback(*P, *S, out, C, B,
