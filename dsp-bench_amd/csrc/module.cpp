@@ -561,16 +561,31 @@ struct dspb_seg_args {
                             // check: 1 = list the differing ones for a rerun (0: flag only)
     unsigned pass;          // the check's stats slot
 };
+// a State copy as whole words, fully unrolled (a private State stays in
+// registers; a memcpy this size would be lowered to a loop over it)
+__device__ static inline void dspb_copy_state(void *dst, const void *src) {
+    if constexpr (sizeof(State) % 4 == 0 && alignof(State) >= 4) {
+#pragma unroll
+        for (unsigned i = 0; i < sizeof(State) / 4; ++i) ((unsigned *)dst)[i] = ((const unsigned *)src)[i];
+    } else {
+#pragma unroll
+        for (unsigned i = 0; i < sizeof(State); ++i) ((unsigned char *)dst)[i] = ((const unsigned char *)src)[i];
+    }
+}
+// bit-for-bit equality; every word is loaded before any is compared (no
+// short circuit: one memory round trip, not one per word)
 __device__ static bool dspb_same_state(const State *a, const State *b) {
-    bool same = true;
+    unsigned d = 0;
     if constexpr (sizeof(State) % 4 == 0 && alignof(State) >= 4) {
         const unsigned *x = (const unsigned *)a, *y = (const unsigned *)b;
-        for (unsigned i = 0; i < sizeof(State) / 4; ++i) same = same && x[i] == y[i];
+#pragma unroll
+        for (unsigned i = 0; i < sizeof(State) / 4; ++i) d |= x[i] ^ y[i];
     } else {
         const unsigned char *x = (const unsigned char *)a, *y = (const unsigned char *)b;
-        for (unsigned i = 0; i < sizeof(State); ++i) same = same && x[i] == y[i];
+#pragma unroll
+        for (unsigned i = 0; i < sizeof(State); ++i) d |= (unsigned)(x[i] ^ y[i]);
     }
-    return same;
+    return d == 0;
 }
 // lane t's segment: its index (~0u: none), first block rendered (warm-up
 // included), warm-up blocks, blocks rendered
@@ -594,11 +609,12 @@ __device__ static unsigned dspb_seg_lane(const dspb_seg_args &G, unsigned base, 
 // a lane about to render block b in its round r (w: its warm-up blocks):
 // pass 1 records the State a kept block is rendered from; a rerun stops
 // (false) where its State meets the one recorded there
+template <bool kRerun>
 __device__ static bool dspb_seg_block(const dspb_seg_args &G, unsigned long long b, unsigned r, unsigned w,
                                       State &st) {
     if (r < w) return true;  // warm-up: nothing kept
-    if (G.mode && r > 0 && dspb_same_state(&st, &G.st_blk[b])) return false;
-    __builtin_memcpy((void *)&G.st_blk[b], (const void *)&st, sizeof(State));
+    if (kRerun && r > 0 && dspb_same_state(&st, &G.st_blk[b])) return false;
+    dspb_copy_state((void *)&G.st_blk[b], (const void *)&st);
     return true;
 }
 // pass 1 / rerun, any shape: lane t of wave 0 runs segment k_t, rounds of one
@@ -624,8 +640,7 @@ __device__ static void dspb_segments(const dspb_seg_args &G) {
     State st;
     bool stopped = false;
     if (k != 0xffffffffu)
-        __builtin_memcpy((void *)&st, G.mode ? (const void *)&G.st_blk[(unsigned long long)k * G.seg] : A.S,
-                         sizeof(State));
+        dspb_copy_state((void *)&st, G.mode ? (const void *)&G.st_blk[(unsigned long long)k * G.seg] : (const void *)A.S);
     for (unsigned r = 0; r < rounds; ++r) {
         for (unsigned j = t; j < NB * CB; j += nt) {
             const unsigned i = j / CB, e = j - i * CB, c = e / B, s = e - c * B;
@@ -636,7 +651,8 @@ __device__ static void dspb_segments(const dspb_seg_args &G) {
         }
         __syncthreads();
         if (k != 0xffffffffu && r < s_len[t]) {
-            if (dspb_seg_block(G, (unsigned long long)s_first[t] + r, r, s_warm[t], st)) {
+            if (G.mode ? dspb_seg_block<true>(G, (unsigned long long)s_first[t] + r, r, s_warm[t], st)
+                       : dspb_seg_block<false>(G, (unsigned long long)s_first[t] + r, r, s_warm[t], st)) {
                 float *blk = dspb_lbuf + t * SB;
                 float *ptrs[CC ? CC : 16];
                 for (unsigned c = 0; c < C; ++c) ptrs[c] = blk + c * B;
@@ -656,13 +672,13 @@ __device__ static void dspb_segments(const dspb_seg_args &G) {
         rounds = 0;
         for (unsigned i = 0; i < NB; ++i) rounds = s_len[i] > rounds ? s_len[i] : rounds;
     }
-    if (k != 0xffffffffu && !stopped) __builtin_memcpy((void *)&G.st_end[k], (const void *)&st, sizeof(State));
+    if (k != 0xffffffffu && !stopped) dspb_copy_state((void *)&G.st_end[k], (const void *)&st);
 }
 // the same for a constant shape (C, B, 4 | B), software pipelined: round r +
 // 1's blocks are in flight into registers (16-byte loads, all issued at once)
 // while round r's callbacks run; blocks at a stride of C B + 2 floats (float2
 // LDS moves; the 16 callback lanes on distinct banks), as dspb_stateless_lds_pf
-template <unsigned CC, unsigned BB>
+template <unsigned CC, unsigned BB, bool kRerun>
 __device__ static void dspb_segments_pf(const dspb_seg_args &G) {
     extern __shared__ float dspb_lbuf[];
     __shared__ unsigned s_first[64], s_warm[64], s_len[64];
@@ -674,7 +690,7 @@ __device__ static void dspb_segments_pf(const dspb_seg_args &G) {
     const dspb_render_args &A = G.R;
     const unsigned t = threadIdx.x;
     const unsigned base = blockIdx.x * NB;
-    const unsigned nseg = G.mode ? *(volatile unsigned *)G.count : G.K;
+    const unsigned nseg = kRerun ? *(volatile unsigned *)G.count : G.K;
     if (base >= nseg) return;  // the same for the whole workgroup
     unsigned k = 0xffffffffu;
     if (t < NB) k = dspb_seg_lane(G, base, t, nseg, s_first, s_warm, s_len);
@@ -697,8 +713,7 @@ __device__ static void dspb_segments_pf(const dspb_seg_args &G) {
     State st;
     bool stopped = false;
     if (k != 0xffffffffu)
-        __builtin_memcpy((void *)&st, G.mode ? (const void *)&G.st_blk[(unsigned long long)k * G.seg] : A.S,
-                         sizeof(State));
+        dspb_copy_state((void *)&st, kRerun ? (const void *)&G.st_blk[(unsigned long long)k * G.seg] : (const void *)A.S);
     float4 pf[C][PV];
     auto load = [&](unsigned r) {
 #pragma unroll
@@ -739,7 +754,7 @@ __device__ static void dspb_segments_pf(const dspb_seg_args &G) {
         __syncthreads();
         if (r + 1 < rounds) load(r + 1);  // in flight while the callbacks run
         if (k != 0xffffffffu && r < s_len[t]) {
-            if (dspb_seg_block(G, (unsigned long long)s_first[t] + r, r, s_warm[t], st)) {
+            if (dspb_seg_block<kRerun>(G, (unsigned long long)s_first[t] + r, r, s_warm[t], st)) {
                 float *blk = dspb_lbuf + t * SB;
                 float *ptrs[C];
                 for (unsigned c = 0; c < C; ++c) ptrs[c] = blk + c * B;
@@ -771,37 +786,57 @@ __device__ static void dspb_segments_pf(const dspb_seg_args &G) {
         rounds = 0;
         for (unsigned i = 0; i < NB; ++i) rounds = s_len[i] > rounds ? s_len[i] : rounds;
     }
-    if (k != 0xffffffffu && !stopped) __builtin_memcpy((void *)&G.st_end[k], (const void *)&st, sizeof(State));
+    if (k != 0xffffffffu && !stopped) dspb_copy_state((void *)&G.st_end[k], (const void *)&st);
 }
 #define DSPB_SEG_KERNEL(name, CC, BB)                                                  \
     extern "C" __global__ __launch_bounds__(256) void name(dspb_seg_args G) { dspb_segments<CC, BB>(G); }
-#define DSPB_SEG_PF_KERNEL(name, CC, BB)                                               \
+// pass 1 and the reruns as kernels of their own: pass 1 carries no
+// comparison (its registers are the callback's)
+#define DSPB_SEG_PF_KERNEL(name, CC, BB, RR)                                           \
     extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) void name(  \
-        dspb_seg_args G) { dspb_segments_pf<CC, BB>(G); }
-DSPB_SEG_PF_KERNEL(dspb_seg_c2b512, 2, 512)
+        dspb_seg_args G) { dspb_segments_pf<CC, BB, RR>(G); }
+DSPB_SEG_PF_KERNEL(dspb_seg_c2b512, 2, 512, false)
+DSPB_SEG_PF_KERNEL(dspb_seg_c2b512_rerun, 2, 512, true)
 DSPB_SEG_KERNEL(dspb_seg_c1, 1, 0)
 DSPB_SEG_KERNEL(dspb_seg_c2, 2, 0)
 DSPB_SEG_KERNEL(dspb_seg, 0, 0)
 // segment k (k >= 1) rendered its first block from st_blk[k seg]; the true
 // State there is st_end[k - 1] if segment k - 1 is exact: flag the segments
 // where the two differ and, when a rerun follows, list them and give each
-// the State to start again from
+// the State to start again from.  One wavefront per segment, its lanes over
+// the State's words; a check after a pass that found nothing to rerun
+// returns at once (nothing changed: the flags stand).
 extern "C" __global__ void dspb_seg_check(dspb_seg_args G) {
-    const unsigned k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= G.K) return;
+    if (G.pass > 0 && G.stats[G.pass - 1] == 0) return;
+    const unsigned lane = threadIdx.x & 63u;
+    const unsigned k = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (k >= G.K) return;  // the same for the whole wavefront
     if (k == 0) {
-        G.flags[0] = 0;
+        if (lane == 0) G.flags[0] = 0;
         return;
     }
     State *first = &G.st_blk[(unsigned long long)k * G.seg];
-    const bool same = dspb_same_state(first, &G.st_end[k - 1]);
-    G.flags[k] = same ? 0 : 1;
-    if (!same) {
-        atomicAdd(&G.stats[G.pass], 1u);
-        if (G.mode) {
-            __builtin_memcpy((void *)first, (const void *)&G.st_end[k - 1], sizeof(State));
-            G.list[atomicAdd(G.count, 1u)] = k;
+    const State *prev = &G.st_end[k - 1];
+    bool diff = false;
+    constexpr bool kWords = sizeof(State) % 4 == 0 && alignof(State) >= 4;
+    constexpr unsigned n = kWords ? sizeof(State) / 4 : sizeof(State);
+    if constexpr (kWords) {
+        for (unsigned i = lane; i < n; i += 64) diff = diff || ((const unsigned *)first)[i] != ((const unsigned *)prev)[i];
+    } else {
+        for (unsigned i = lane; i < n; i += 64)
+            diff = diff || ((const unsigned char *)first)[i] != ((const unsigned char *)prev)[i];
+    }
+    const bool any = __any(diff) != 0;
+    if (lane == 0) G.flags[k] = any ? 1 : 0;
+    if (!any) return;
+    if (lane == 0) atomicAdd(&G.stats[G.pass], 1u);
+    if (G.mode) {
+        if constexpr (kWords) {
+            for (unsigned i = lane; i < n; i += 64) ((unsigned *)first)[i] = ((const unsigned *)prev)[i];
+        } else {
+            for (unsigned i = lane; i < n; i += 64) ((unsigned char *)first)[i] = ((const unsigned char *)prev)[i];
         }
+        if (lane == 0) G.list[atomicAdd(G.count, 1u)] = k;
     }
 }
 // the walk: one workgroup, segments in order; a segment is looked at when the
@@ -850,7 +885,7 @@ __device__ static void dspb_seg_walk(const dspb_seg_args &G) {
         prev_ended = false;
         if (s_bad) {
             ++reruns;
-            __builtin_memcpy((void *)&local, (const void *)s_prev, sizeof(State));
+            dspb_copy_state((void *)&local, (const void *)s_prev);
             dspb_stage_in(A, b0, buf0, t, nt);
             __syncthreads();
             unsigned long long b = b0;
@@ -859,7 +894,7 @@ __device__ static void dspb_seg_walk(const dspb_seg_args &G) {
                 float *cur = ((b - b0) & 1) ? buf1 : buf0, *oth = ((b - b0) & 1) ? buf0 : buf1;
                 if (t == 0) {  // does the chain meet the recorded one here?
                     s_stop = (b > b0 && dspb_same_state(&local, &G.st_blk[b])) ? 1 : 0;
-                    if (!s_stop) __builtin_memcpy((void *)&G.st_blk[b], (const void *)&local, sizeof(State));
+                    if (!s_stop) dspb_copy_state((void *)&G.st_blk[b], (const void *)&local);
                 }
                 __syncthreads();
                 if (s_stop) {
@@ -879,8 +914,8 @@ __device__ static void dspb_seg_walk(const dspb_seg_args &G) {
             // the last block rendered here
             dspb_stage_out(A, b - 1, ((b - 1 - b0) & 1) ? buf1 : buf0, t, nt);
             if (ended && t == 0) {
-                __builtin_memcpy((void *)s_prev, (const void *)&local, sizeof(State));
-                __builtin_memcpy((void *)&G.st_end[k], (const void *)&local, sizeof(State));
+                dspb_copy_state((void *)s_prev, (const void *)&local);
+                dspb_copy_state((void *)&G.st_end[k], (const void *)&local);
             }
             prev_ended = ended;
             __syncthreads();
@@ -931,7 +966,7 @@ struct dsp_module {
     hipFunction_t f_render_st[4] = {};  // kStShapes (NULL: dspb_render)
     // speculative segments (kSegShapes, the check, kWalkShapes; NULL in code
     // objects compiled before them: the serial chain)
-    hipFunction_t f_seg[4] = {}, f_seg_check = nullptr, f_seg_walk[2] = {};
+    hipFunction_t f_seg[4] = {}, f_seg_rerun0 = nullptr, f_seg_check = nullptr, f_seg_walk[2] = {};
     struct SegWork {
         void *blk = nullptr;           // [cap_blk] States: st_blk
         void *end = nullptr;           // [cap] States: st_end
@@ -1250,6 +1285,7 @@ int dsp_module_load(const void *code, uint64_t code_size, int device, dsp_module
     for (int i = 0; i < 4; ++i) optional(&m->f_seg[i], kSegShapes[i].name);
     for (int i = 0; i < 2; ++i) optional(&m->f_seg_walk[i], kWalkShapes[i].name);
     optional(&m->f_seg_check, "dspb_seg_check");
+    optional(&m->f_seg_rerun0, "dspb_seg_c2b512_rerun");  // kSegShapes[0]'s reruns
     unsigned *d_o = nullptr;
     if ((e = hipMalloc(&d_o, 4 * sizeof(unsigned))) != hipSuccess) return fail(dspb::hip_fail(e, "hipMalloc"));
     void *args[] = {&d_o};
@@ -1738,7 +1774,8 @@ static int module_render_seg(dsp_module *m, RenderArgsG &A, hipStream_t s) {
         if (m->f_seg_walk[i] && (!kWalkShapes[i].C || kWalkShapes[i].C == C) &&
             (!kWalkShapes[i].B || kWalkShapes[i].B == B))
             fw = m->f_seg_walk[i];
-    if (!f || !fw || !m->f_seg_check) return 1;
+    if (!f || !fw || !m->f_seg_check || (fi == 0 && !m->f_seg_rerun0)) return 1;
+    hipFunction_t fr = fi == 0 ? m->f_seg_rerun0 : f;  // the reruns' kernel
     auto &W = m->seg;
     // segments: as many as the chip runs lanes at once (two workgroups per
     // CU, nb lanes each), kSegMinBlocks blocks at least
@@ -1787,17 +1824,18 @@ static int module_render_seg(dsp_module *m, RenderArgsG &A, hipStream_t s) {
     G.warm = W.warm;
     void *args[] = {&G};
     const unsigned lds = (unsigned)(nb * stride * sizeof(float));
-    const unsigned gseg = (unsigned)((K + nb - 1) / nb), gchk = (unsigned)((K + 255) / 256);
+    const unsigned gseg = (unsigned)((K + nb - 1) / nb), gchk = (unsigned)((K + 3) / 4);  // 4 segments per 256 threads
+    // words: [0, 2) the checks' list counts, [4, 8) the stats
     MOD_HIP(hipMemsetAsync(W.words, 0, 16 * sizeof(unsigned), s));
     G.mode = 0;
     MOD_HIP(hipModuleLaunchKernel(f, gseg, 1, 1, 256, 1, 1, lds, s, args, nullptr));
     for (unsigned p = 0; p < 3; ++p) {  // check, rerun, check, rerun, check (flags only)
         G.pass = p;
         G.mode = p < 2 ? 1 : 0;  // the check lists the segments for a rerun; the last one only flags them
-        MOD_HIP(hipMemsetAsync(W.words, 0, sizeof(unsigned), s));
+        G.count = W.words + (p < 2 ? p : 0);
         MOD_HIP(hipModuleLaunchKernel(m->f_seg_check, gchk, 1, 1, 256, 1, 1, 0, s, args, nullptr));
         if (p == 2) break;
-        MOD_HIP(hipModuleLaunchKernel(f, gseg, 1, 1, 256, 1, 1, lds, s, args, nullptr));
+        MOD_HIP(hipModuleLaunchKernel(fr, gseg, 1, 1, 256, 1, 1, lds, s, args, nullptr));
     }
     MOD_HIP(hipModuleLaunchKernel(fw, 1, 1, 1, 256, 1, 1, (unsigned)(2ull * C * B * sizeof(float)), s, args,
                                   nullptr));
