@@ -67,7 +67,8 @@ constexpr LdsShape kSegShapes[4] = {{"dspb_seg_c2b512", 2, 512}, {"dspb_seg_c1",
 constexpr LdsShape kWalkShapes[2] = {{"dspb_seg_walk_c2b512", 2, 512}, {"dspb_seg_walk_any", 0, 0}};
 constexpr uint32_t kSegMaxState = 1024;   // bytes of State a lane copies (the walk keeps one in LDS)
 constexpr uint32_t kSegWarm0 = 4;         // blocks of warm-up of a first render
-constexpr uint32_t kSegWarmMax = 256;     // beyond this, the module renders its chain serially
+constexpr uint32_t kSegWarmMax = 4096;    // the longest warm-up (blocks); past it, the chain is serial
+constexpr uint32_t kSegLevels = 4;        // warm-up levels a render may try (x16 each)
 constexpr uint32_t kSegMinBlocks = 4;     // blocks per segment at least
 
 // Host mirror of the driver's argument block (same layout on both sides).
@@ -95,11 +96,14 @@ struct SegArgsG {
     void *st_end;
     unsigned *list;
     unsigned *count;
+    unsigned *prev_count;
     unsigned char *flags;
     unsigned *stats;
     unsigned long long seg;
     unsigned K;
     unsigned warm;
+    unsigned prev_warm;
+    unsigned level;
     unsigned mode;
     unsigned pass;
 };
@@ -552,15 +556,32 @@ struct dspb_seg_args {
     State *st_end;          // [K] the State each segment ended with
     unsigned *list;         // segments to rerun (check -> rerun)
     unsigned *count;        // how many
+    unsigned *prev_count;   // a rerun's check: the rerun's count (0: nothing changed, skip)
     unsigned char *flags;   // the last check: 1 = differed
-    unsigned *stats;        // per check: segments that differed; [3]: serial reruns of the walk
+    unsigned *stats;        // [0, 4) segments that differed per warm-up level, [4] / [5] after
+                            // rerun 1 / 2, [7] serial reruns of the walk, [8, 12) levels run
     unsigned long long seg; // blocks per segment
     unsigned K;             // segments
     unsigned warm;          // pass 1: warm-up blocks
+    unsigned prev_warm;     // pass 1 at level > 0: the warm-up of the level before
+    unsigned level;         // pass 1 / its check: the warm-up level (~0u: a rerun's check)
     unsigned mode;          // segments: 0 = pass 1 (every segment), 1 = rerun the listed ones;
                             // check: 1 = list the differing ones for a rerun (0: flag only)
     unsigned pass;          // the check's stats slot
 };
+// pass 1 at warm-up level L > 0 (and its check) runs only when level L - 1
+// ran and more than 1/8 of the segments it guessed -- those whose warm-up
+// began after block 0 -- started from a State that was not the true one: the
+// trajectories had not met within its warm-up, so a 16x longer one is tried
+__device__ static bool dspb_seg_level_runs(const dspb_seg_args &G) {
+    if (G.level == 0) return true;
+    const volatile unsigned *st = G.stats;
+    const unsigned prev = G.level - 1;
+    if (!st[8 + prev]) return false;
+    const unsigned long long early = G.prev_warm / G.seg < G.K - 1 ? G.prev_warm / G.seg : G.K - 1;
+    const unsigned long long guessed = G.K - 1 - early;
+    return guessed && st[prev] * 8ull > guessed;
+}
 // a State copy as whole words, fully unrolled (a private State stays in
 // registers; a memcpy this size would be lowered to a loop over it)
 __device__ static inline void dspb_copy_state(void *dst, const void *src) {
@@ -629,6 +650,10 @@ __device__ static void dspb_segments(const dspb_seg_args &G) {
     const unsigned C = CC ? CC : A.C, B = BB ? BB : A.B, CB = C * B, NB = A.lds_nb, SB = A.lds_stride;
     const unsigned t = threadIdx.x, nt = blockDim.x;
     const unsigned base = blockIdx.x * NB;
+    if (!G.mode) {  // pass 1: at a warm-up level that runs; it restarts the listing
+        if (!dspb_seg_level_runs(G)) return;
+        if (G.level && blockIdx.x == 0 && t == 0) *G.count = 0;
+    }
     const unsigned nseg = G.mode ? *(volatile unsigned *)G.count : G.K;
     if (base >= nseg) return;  // the same for the whole workgroup
     unsigned k = 0xffffffffu;
@@ -690,6 +715,10 @@ __device__ static void dspb_segments_pf(const dspb_seg_args &G) {
     const dspb_render_args &A = G.R;
     const unsigned t = threadIdx.x;
     const unsigned base = blockIdx.x * NB;
+    if (!kRerun) {  // pass 1: at a warm-up level that runs; it restarts the listing
+        if (!dspb_seg_level_runs(G)) return;
+        if (G.level && blockIdx.x == 0 && t == 0) *G.count = 0;
+    }
     const unsigned nseg = kRerun ? *(volatile unsigned *)G.count : G.K;
     if (base >= nseg) return;  // the same for the whole workgroup
     unsigned k = 0xffffffffu;
@@ -807,7 +836,12 @@ DSPB_SEG_KERNEL(dspb_seg, 0, 0)
 // the State's words; a check after a pass that found nothing to rerun
 // returns at once (nothing changed: the flags stand).
 extern "C" __global__ void dspb_seg_check(dspb_seg_args G) {
-    if (G.pass > 0 && G.stats[G.pass - 1] == 0) return;
+    if (G.level != 0xffffffffu) {  // pass 1's check: where pass 1 ran
+        if (!dspb_seg_level_runs(G)) return;
+        if (blockIdx.x == 0 && threadIdx.x == 0) G.stats[8 + G.level] = 1;
+    } else if (*(volatile unsigned *)G.prev_count == 0) {
+        return;  // the rerun before rendered nothing: the flags stand
+    }
     const unsigned lane = threadIdx.x & 63u;
     const unsigned k = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     if (k >= G.K) return;  // the same for the whole wavefront
@@ -922,7 +956,7 @@ __device__ static void dspb_seg_walk(const dspb_seg_args &G) {
         }
     }
     __syncthreads();
-    if (t == 0) G.stats[3] = reruns;
+    if (t == 0) G.stats[7] = reruns;
     // the live State: the last segment's final State (s_prev when the walk
     // rendered it to its end, else st_end as pass 1 / a rerun left it)
     const unsigned char *last = prev_ended ? (const unsigned char *)s_prev
@@ -1709,12 +1743,14 @@ static int check_device(const dsp_module *m) {
 }
 
 // The last speculative render's counters (pinned copy, behind an event):
-// into m->seg.last, and what they teach about the current Parameters -- a
-// pass where more than 1/8 of the segments started from a State that was not
-// the true one asks for a longer warm-up (x4; x16 when half of them still
-// differed after both reruns: the trajectories do not meet within a
-// segment), and past kSegWarmMax the chain is rendered serially.  wait =
-// false reads them only if they have landed (a render never waits for them).
+// into m->seg.last, and what they teach about the current Parameters.  The
+// render tried warm-up levels (x16 each, on the GPU) until no more than 1/8
+// of the segments it guessed started from a State that was not the true one;
+// the level that stood is where the next render with these Parameters
+// starts.  When even the last level it could try failed (kSegWarmMax, or a
+// warm-up half the file), the chain does not forget: these Parameters render
+// serially from now on.  wait = false reads the counters only if they have
+// landed (a render never waits for them).
 int module_seg_collect(dsp_module *m, bool wait) {
     auto &W = m->seg;
     for (int pass = 0; pass < 2; ++pass) {
@@ -1728,20 +1764,26 @@ int module_seg_collect(dsp_module *m, bool wait) {
         }
         W.pending[i] = false;
         dsp_state_spec_info &r = W.info[i];
-        const unsigned *h = W.h_stats + 4 * i;
-        for (int j = 0; j < 3; ++j) r.differed[j] = h[j];
-        r.serial_reruns = h[3];
-        if (W.seq[i] == W.calls) W.last = r;
-        // learn only from renders made with the warm-up now in force, and
-        // only from the segments whose warm-up began after block 0 (those
-        // before start from the true State)
-        const uint64_t early = std::min<uint64_t>(r.segments - 1, r.warmup_blocks / r.blocks_per_segment);
-        const uint64_t guessed = r.segments - 1 - early;
-        if (r.warmup_blocks == W.warm && !W.off && guessed && r.differed[0] * 8ull > guessed) {
-            const uint32_t grow = r.differed[2] * 2ull > guessed ? 16u : 4u;
-            if (W.warm >= kSegWarmMax) W.off = true;
-            else W.warm = std::min<uint32_t>(W.warm * grow, kSegWarmMax);
+        const unsigned *h = W.h_stats + 16 * i;  // [0, 4) levels, [4] [5] reruns, [7] walk, [8, 12) levels run
+        const uint32_t first_warm = r.warmup_blocks;
+        uint32_t last = 0, warm = first_warm;
+        for (uint32_t L = 1; L < r.levels && h[8 + L]; ++L) {
+            last = L;
+            warm = std::min<uint32_t>(warm * 16, kSegWarmMax);
         }
+        r.levels = last + 1;
+        r.warmup_blocks = warm;
+        r.differed[0] = h[last];
+        r.differed[1] = h[4];
+        r.differed[2] = h[5];
+        r.serial_reruns = h[7];
+        if (W.seq[i] == W.calls) W.last = r;
+        // learn only from renders that started with the warm-up now in force
+        if (first_warm != W.warm || W.off) continue;
+        const uint64_t early = std::min<uint64_t>(r.segments - 1, warm / r.blocks_per_segment);
+        const uint64_t guessed = r.segments - 1 - early;
+        if (guessed && r.differed[0] * 8ull > guessed) W.off = true;  // the longest warm-up it could try failed
+        else W.warm = warm;
     }
     return DSP_OK;
 }
@@ -1798,8 +1840,8 @@ static int module_render_seg(dsp_module *m, RenderArgsG &A, hipStream_t s) {
         W.cap_blk = cap_blk;
     }
     if (!W.words) {
-        MOD_HIP(hipMalloc(&W.words, 16 * sizeof(unsigned)));
-        MOD_HIP(hipHostMalloc(&W.h_stats, 8 * sizeof(unsigned), hipHostMallocDefault));
+        MOD_HIP(hipMalloc(&W.words, 32 * sizeof(unsigned)));
+        MOD_HIP(hipHostMalloc(&W.h_stats, 32 * sizeof(unsigned), hipHostMallocDefault));
         for (hipEvent_t &e : W.ev) MOD_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     }
     // the slot this call fills: the one of the render two calls back, whose
@@ -1816,30 +1858,53 @@ static int module_render_seg(dsp_module *m, RenderArgsG &A, hipStream_t s) {
     G.st_blk = W.blk;
     G.st_end = W.end;
     G.list = W.list;
-    G.count = W.words;
     G.flags = W.flags;
-    G.stats = W.words + 4;
+    G.stats = W.words + 8;  // words: [0] pass 1's listing, [2] / [3] the reruns' listings
     G.seg = seg;
     G.K = (unsigned)K;
-    G.warm = W.warm;
     void *args[] = {&G};
     const unsigned lds = (unsigned)(nb * stride * sizeof(float));
     const unsigned gseg = (unsigned)((K + nb - 1) / nb), gchk = (unsigned)((K + 3) / 4);  // 4 segments per 256 threads
-    // words: [0, 2) the checks' list counts, [4, 8) the stats
-    MOD_HIP(hipMemsetAsync(W.words, 0, 16 * sizeof(unsigned), s));
-    G.mode = 0;
-    MOD_HIP(hipModuleLaunchKernel(f, gseg, 1, 1, 256, 1, 1, lds, s, args, nullptr));
-    for (unsigned p = 0; p < 3; ++p) {  // check, rerun, check, rerun, check (flags only)
-        G.pass = p;
-        G.mode = p < 2 ? 1 : 0;  // the check lists the segments for a rerun; the last one only flags them
-        G.count = W.words + (p < 2 ? p : 0);
+    MOD_HIP(hipMemsetAsync(W.words, 0, 32 * sizeof(unsigned), s));
+    // pass 1 and its check at the learnt warm-up, then at 16x longer ones
+    // while too many segments started wrong (each level decides on the GPU
+    // whether it runs: dspb_seg_level_runs)
+    uint32_t warm = W.warm, prev = 0, levels = 0;
+    G.count = W.words;
+    for (uint32_t L = 0; L < kSegLevels; ++L) {
+        if (L > 0) {
+            const uint32_t next = std::min<uint32_t>(warm * 16, kSegWarmMax);
+            if (next <= warm || 2ull * next >= A.nblocks) break;  // no longer, or as long as the file
+            prev = warm;
+            warm = next;
+        }
+        G.level = L;
+        G.warm = warm;
+        G.prev_warm = prev;
+        G.mode = 0;
+        MOD_HIP(hipModuleLaunchKernel(f, gseg, 1, 1, 256, 1, 1, lds, s, args, nullptr));
+        G.pass = L;
+        G.mode = 1;  // the check lists the differing segments for the rerun
         MOD_HIP(hipModuleLaunchKernel(m->f_seg_check, gchk, 1, 1, 256, 1, 1, 0, s, args, nullptr));
-        if (p == 2) break;
+        ++levels;
+    }
+    // two reruns of the listed segments, each checked; the last check only flags
+    G.level = 0xffffffffu;
+    unsigned *listing = W.words;
+    for (unsigned p = 0; p < 2; ++p) {
+        G.count = listing;
+        G.mode = 1;
         MOD_HIP(hipModuleLaunchKernel(fr, gseg, 1, 1, 256, 1, 1, lds, s, args, nullptr));
+        G.prev_count = listing;
+        listing = W.words + 2 + p;
+        G.count = listing;
+        G.pass = 4 + p;
+        G.mode = p == 0 ? 1 : 0;
+        MOD_HIP(hipModuleLaunchKernel(m->f_seg_check, gchk, 1, 1, 256, 1, 1, 0, s, args, nullptr));
     }
     MOD_HIP(hipModuleLaunchKernel(fw, 1, 1, 1, 256, 1, 1, (unsigned)(2ull * C * B * sizeof(float)), s, args,
                                   nullptr));
-    MOD_HIP(hipMemcpyAsync(W.h_stats + 4 * slot, W.words + 4, 4 * sizeof(unsigned), hipMemcpyDeviceToHost, s));
+    MOD_HIP(hipMemcpyAsync(W.h_stats + 16 * slot, W.words + 8, 16 * sizeof(unsigned), hipMemcpyDeviceToHost, s));
     MOD_HIP(hipEventRecord(W.ev[slot], s));
     W.pending[slot] = true;
     W.seq[slot] = ++W.calls;
@@ -1848,7 +1913,8 @@ static int module_render_seg(dsp_module *m, RenderArgsG &A, hipStream_t s) {
     r.used = 1;
     r.segments = (uint32_t)K;
     r.blocks_per_segment = (uint32_t)seg;
-    r.warmup_blocks = W.warm;
+    r.warmup_blocks = W.warm;  // the first level's; module_seg_collect names the one that stood
+    r.levels = levels;
     MOD_HIP(hipEventRecord(m->use_ev, s));
     return DSP_OK;
 }

@@ -215,17 +215,19 @@ int dsp_module_retired_tables(dsp_module *m, uint64_t *n);
  * callback forgets its State (filters, envelopes, smoothers: trajectories
  * from different States meet exactly within a few hundred samples); when it
  * does not (an oscillator's phase) the call costs the serial chain plus one
- * pass, the warm-up grows on later calls, and past 256 blocks the module
- * renders these Parameters serially.  DSP_EXEC_SERIAL_STATE (dspbench.h)
- * forces the serial chain. */
+ * pass per warm-up level tried (16x longer each, up to 4096 blocks, within
+ * the same call), and then the module renders these Parameters serially.
+ * DSP_EXEC_SERIAL_STATE (dspbench.h) forces the serial chain. */
 typedef struct dsp_state_spec_info {
     int32_t used;                /* the module's last State-writing render ran in segments */
     int32_t disabled;            /* learned: serial for the current Parameters */
     uint32_t segments;           /* K of that render */
     uint32_t blocks_per_segment;
-    uint32_t warmup_blocks;
-    uint32_t differed[3];        /* segments whose start State differed: pass 1, rerun 1, rerun 2 */
+    uint32_t warmup_blocks;      /* the warm-up of the pass 1 that stood */
+    uint32_t differed[3];        /* segments whose start State differed: that pass 1, rerun 1, rerun 2 */
     uint32_t serial_reruns;      /* segments the in-order walk rendered again */
+    uint32_t levels;             /* pass 1 runs: the learnt warm-up, then 16x longer ones while more
+                                    than 1/8 of the guessed segments started wrong (at most 4) */
 } dsp_state_spec_info;
 /* Waits for the module's last speculative render and describes it. */
 int dsp_module_state_spec(dsp_module *m, dsp_state_spec_info *out);

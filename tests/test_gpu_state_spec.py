@@ -139,7 +139,7 @@ def test_biquad_source_one_minute_bit_exact(torch_cuda):
     assert mod.facts["analyzed"] and mod.facts["writes_state"]
     spec, ser, info = both(torch_cuda, mod, params, noise(2, 48000 * 60, 1), 2, 512)
     assert_same(spec, ser)
-    assert info[0]["used"] and info[0]["segments"] > 1000
+    assert info[0]["used"] and info[0]["segments"] > 1000 and info[0]["levels"] == 1
     assert info[0]["differed"][0] * 50 < info[0]["segments"]
     assert info[0]["differed"][2] <= 2 and info[0]["serial_reruns"] <= 2
 
@@ -153,6 +153,21 @@ def test_biquad_slow_and_fast_filters(torch_cuda, cutoff, q):
     spec, ser, info = both(torch_cuda, mod, params, noise(2, 400_000 + 123, 2), 2, 512, calls=3)
     assert_same(spec, ser)
     assert all(i["used"] or i["disabled"] for i in info)
+
+
+@pytest.mark.gpu
+def test_longer_warm_up_within_one_render(torch_cuda):
+    """A 300 Hz low-pass forgets within ~4,600 samples on average (26,000 at
+    worst over 200 trials, tools/diag/biquad_state_sync.c): the first warm-up
+    (4 blocks) leaves most segments wrong, so the same render tries 64 blocks,
+    which stands; the next render starts there.  Bit-exact throughout."""
+    mod, params = biquad_module(300.0, 0.7071)
+    spec, ser, info = both(torch_cuda, mod, params, noise(2, 1_500_000, 9), 2, 512)
+    assert_same(spec, ser)
+    assert info[0]["used"] and info[0]["levels"] == 2 and info[0]["warmup_blocks"] == 64
+    guessed = info[0]["segments"] - 1 - 64 // info[0]["blocks_per_segment"]
+    assert info[0]["differed"][0] * 8 <= guessed
+    assert info[1]["used"] and info[1]["levels"] == 1 and info[1]["warmup_blocks"] == 64
 
 
 @pytest.mark.gpu
@@ -172,17 +187,22 @@ def test_one_pole_shapes(torch_cuda, C, cin, B, L):
 @pytest.mark.gpu
 def test_never_forgetting_state_is_exact_and_learned(torch_cuda):
     """A block counter in the State: every speculative segment starts wrong,
-    the walk renders them again in order (exact), and after the warm-up has
-    grown past its limit the module renders these Parameters serially."""
+    at every warm-up level the render tries (4, then 64 blocks: a 1,024-block
+    one would be more than half the file), the walk renders them again in
+    order (exact), and the module renders these Parameters serially from the
+    next call on."""
     mod = module_of(COUNTER_SRC, "counter_spec")
     params = mod.default_parameters()
     x = noise(2, 150_000, 4)
-    spec, ser, info = both(torch_cuda, mod, params, x, 2, 512, calls=4)
+    spec, ser, info = both(torch_cuda, mod, params, x, 2, 512, calls=3)
     assert_same(spec, ser)
-    # (segment 1's warm-up starts at block 0, from the true State: exact)
-    assert info[0]["used"] and info[0]["differed"][0] == info[0]["segments"] - 2
+    seg = info[0]["blocks_per_segment"]
+    # (segments whose warm-up starts at block 0 start from the true State)
+    assert info[0]["used"] and info[0]["levels"] == 2 and info[0]["warmup_blocks"] == 64
+    assert info[0]["differed"][0] == info[0]["segments"] - 1 - 64 // seg
     assert info[0]["serial_reruns"] > 0
-    assert info[-1]["disabled"] and not info[-1]["used"]
+    assert info[1]["disabled"] and not info[1]["used"]
+    assert info[2]["disabled"] and not info[2]["used"]
     # new Parameters: learnt again
     p2 = np.frombuffer(params, np.float32).copy()
     p2[0] = 0.02
