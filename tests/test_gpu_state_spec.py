@@ -270,3 +270,96 @@ def test_chunked_host_driver_carries_the_state(torch_cuda):
         out, mag = d.render_stft_host(x, 2, 512, 48000.0, mod.plugin(params, serial_state=serial), chunk=1 << 20)
         res.append((np.asarray(out), np.asarray(mag), mod.read_state()))
     assert_same([res[0]], [res[1]])
+
+
+# ---- generated State-writing plugins: whatever the callback does with its
+# State (smoothers, envelopes with input-dependent branches, saturation, a
+# counter, a padded State rewritten as a whole, a read-only arena table), the
+# segments render the serial chain's bits
+GEN_HEAD = r'''
+#include "plugin_header.h"
+struct Parameters { FLOAT_PARAM(0.0f, 1.0f) a; FLOAT_PARAM(0.0f, 1.0f) b; };
+Parameters default_parameters() { Parameters p = {0.03f, 0.3f}; return p; }
+'''
+GEN_BODIES = {
+    # two cascaded one-poles with a saturation between them, per channel
+    "sat_chain": r'''
+struct State { float z1[16], z2[16]; };
+State initialize_state(const Parameters& p, const unsigned C, const float sr, void* ctx) { State s = {}; return s; }
+void audio_callback(const Parameters& p, State& st, float** out, const u32 C, const u32 B, const real32 sr) {
+    for (u32 c = 0; c < C; ++c)
+        for (u32 s = 0; s < B; ++s) {
+            st.z1[c] += p.a * (out[c][s] - st.z1[c]);
+            const float u = 3.0f * st.z1[c];
+            const float v = u / (1.0f + (u < 0.0f ? -u : u));
+            st.z2[c] += p.b * (v - st.z2[c]);
+            out[c][s] = st.z2[c];
+        }
+}''',
+    # attack / release envelope (a branch on the sample) driving a gain
+    "env_gate": r'''
+struct State { float env; float g; };
+State initialize_state(const Parameters& p, const unsigned C, const float sr, void* ctx) { State s = {0.0f, 1.0f}; return s; }
+void audio_callback(const Parameters& p, State& st, float** out, const u32 C, const u32 B, const real32 sr) {
+    for (u32 s = 0; s < B; ++s) {
+        float m = 0.0f;
+        for (u32 c = 0; c < C; ++c) { const float x = out[c][s] < 0.0f ? -out[c][s] : out[c][s]; m = x > m ? x : m; }
+        if (m > st.env) st.env += p.b * (m - st.env); else st.env += p.a * (m - st.env);
+        const float target = st.env > 0.5f ? 0.25f : 1.0f;
+        st.g += 0.01f * (target - st.g);
+        for (u32 c = 0; c < C; ++c) out[c][s] *= st.g;
+    }
+}''',
+    # a padded State (char beside floats) assigned as a whole every block
+    "padded_whole": r'''
+struct State { char on; float y; double acc; };
+State initialize_state(const Parameters& p, const unsigned C, const float sr, void* ctx) { State s = {1, 0.0f, 0.0}; return s; }
+void audio_callback(const Parameters& p, State& st, float** out, const u32 C, const u32 B, const real32 sr) {
+    State n = st;
+    for (u32 s = 0; s < B; ++s) {
+        n.y += p.a * (out[0][s] - n.y);
+        n.acc = 0.999 * n.acc + (double)n.y;
+        for (u32 c = 0; c < C; ++c) out[c][s] = n.on ? n.y + 1e-4f * (float)n.acc : out[c][s];
+    }
+    n.on = n.acc > -1e30 ? 1 : 0;
+    st = n;
+}''',
+    # a wavetable in the arena, only read; a phase that wraps (never forgets)
+    "arena_table": r'''
+struct State { float* tab; unsigned pos; };
+State initialize_state(const Parameters& p, const unsigned C, const float sr, void* ctx) {
+    State s; s.tab = (float*)allocate_bytes(sizeof(float) * 64, ctx); s.pos = 0;
+    for (int i = 0; i < 64; ++i) s.tab[i] = (float)i / 64.0f;
+    return s;
+}
+void audio_callback(const Parameters& p, State& st, float** out, const u32 C, const u32 B, const real32 sr) {
+    for (u32 s = 0; s < B; ++s) {
+        const float t = st.tab[st.pos & 63u];
+        for (u32 c = 0; c < C; ++c) out[c][s] = out[c][s] * p.b + t;
+        st.pos += 3u;
+    }
+}''',
+    # a one-pole whose coefficient is read from a mutable-looking State field
+    # the callback also rewrites (the same value every block)
+    "self_coef": r'''
+struct State { float k; float z[16]; };
+State initialize_state(const Parameters& p, const unsigned C, const float sr, void* ctx) { State s = {}; s.k = p.a; return s; }
+void audio_callback(const Parameters& p, State& st, float** out, const u32 C, const u32 B, const real32 sr) {
+    st.k = p.a;
+    for (u32 c = 0; c < C && c < 16; ++c)
+        for (u32 s = 0; s < B; ++s) { st.z[c] = st.z[c] + st.k * (out[c][s] - st.z[c]); out[c][s] = st.z[c] - out[c][s]; }
+}''',
+}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", sorted(GEN_BODIES))
+def test_generated_plugins_match_the_serial_chain(torch_cuda, name):
+    mod = module_of(GEN_HEAD + GEN_BODIES[name], f"gen_{name}")
+    f = mod.facts
+    params = mod.default_parameters()
+    x = noise(2, 250_000 + 77, 11) * np.float32(0.8)
+    spec, ser, info = both(torch_cuda, mod, params, x, 2, 512, calls=2)
+    assert_same(spec, ser)
+    if f["analyzed"] and f["writes_state"] and mod.state_size <= 1024:
+        assert info[0]["used"] or info[0]["disabled"]
