@@ -363,3 +363,24 @@ def test_generated_plugins_match_the_serial_chain(torch_cuda, name):
     assert_same(spec, ser)
     if f["analyzed"] and f["writes_state"] and mod.state_size <= 1024:
         assert info[0]["used"] or info[0]["disabled"]
+
+
+@pytest.mark.gpu
+def test_loop_mode_through_segments(torch_cuda):
+    """dsp_render_loop (audio.cpp:100-132: the file wraps from the cursor)
+    with a State-writing plugin: the wrapped block stream through the
+    segments equals the serial chain's, cursor and State included."""
+    torch = torch_cuda
+    mod, params = biquad_module(700.0, 0.9)
+    x = torch.from_numpy(noise(2, 33_333, 12)).cuda()
+    res = []
+    for serial in (False, True):
+        mod.initialize_state(params, 2, 48000.0)
+        plug = mod.plugin(params, serial_state=serial)
+        y1, cur = d.render_loop(x, 2, 512, 700, 48000.0, plug, cursor=1234)
+        y2, cur2 = d.render_loop(x, 2, 512, 300, 48000.0, plug, cursor=cur)
+        res.append((y1.cpu().numpy(), y2.cpu().numpy(), cur, cur2, mod.read_state()))
+    a, b = res
+    assert a[2:4] == b[2:4] and a[4] == b[4]
+    for i in (0, 1):
+        assert np.array_equal(a[i].view(np.uint32), b[i].view(np.uint32))
