@@ -384,3 +384,26 @@ def test_loop_mode_through_segments(torch_cuda):
     assert a[2:4] == b[2:4] and a[4] == b[4]
     for i in (0, 1):
         assert np.array_equal(a[i].view(np.uint32), b[i].view(np.uint32))
+
+
+@pytest.mark.gpu
+def test_biquad_source_full_hour_bit_exact(torch_cuda):
+    """The bench's full size: 1 h of 48 kHz stereo through plugins/biquad.cpp
+    compiled unchanged, segments against the serial chain (≈10 s on one lane),
+    compared on the device bit for bit, final State included."""
+    torch = torch_cuda
+    mod, params = biquad_module()
+    L = 48000 * 3600
+    g = torch.Generator(device="cuda").manual_seed(13)
+    x = torch.rand((2, L), device="cuda", generator=g) * 2 - 1
+    outs = []
+    for serial in (False, True):
+        mod.initialize_state(params, 2, 48000.0)
+        y = d.render_offline(x, 2, 512, 48000.0, mod.plugin(params, serial_state=serial))
+        torch.cuda.synchronize()
+        outs.append((y, mod.read_state()))
+        if not serial:
+            info = mod.state_spec()
+    assert info["used"] and info["segments"] > 8000
+    assert outs[0][1] == outs[1][1]
+    assert torch.equal(outs[0][0].view(torch.int32), outs[1][0].view(torch.int32))
