@@ -608,6 +608,12 @@ __device__ static bool dspb_same_state(const State *a, const State *b) {
     }
     return d == 0;
 }
+// lanes (blocks in LDS) per workgroup of the segment kernels: as many as the
+// round's LDS holds (the host computes the same: module_render_seg)
+constexpr unsigned dspb_seg_nb(unsigned SB) {
+    const unsigned v = DSPB_LDS_ROUND_BYTES / (SB * 4u);
+    return v < 64u ? v : 64u;
+}
 // lane t's segment: its index (~0u: none), first block rendered (warm-up
 // included), warm-up blocks, blocks rendered
 __device__ static unsigned dspb_seg_lane(const dspb_seg_args &G, unsigned base, unsigned t, unsigned nseg,
@@ -707,7 +713,7 @@ template <unsigned CC, unsigned BB, bool kRerun>
 __device__ static void dspb_segments_pf(const dspb_seg_args &G) {
     extern __shared__ float dspb_lbuf[];
     __shared__ unsigned s_first[64], s_warm[64], s_len[64];
-    constexpr unsigned C = CC, B = BB, CB = C * B, SB = CB + 2u, NB = dspb_lds_nb(SB);
+    constexpr unsigned C = CC, B = BB, CB = C * B, SB = CB + 2u, NB = dspb_seg_nb(SB);
     // per channel: NB rows of B / 4 float4, PV of them per thread
     constexpr unsigned R4 = B / 4u, T4 = NB * R4, PV = (T4 + 255u) / 256u;
     static_assert(NB <= 64 && B % 4 == 0, "one wave runs a round's callbacks");
@@ -1810,7 +1816,8 @@ static int module_render_seg(dsp_module *m, RenderArgsG &A, hipStream_t s) {
             f = m->f_seg[fi = i];
     // the constant-shape kernel (dspb_segments_pf) strides blocks by C B + 2
     const uint64_t stride = (uint64_t)C * B + (fi == 0 ? 2 : 1);
-    const uint64_t nb = std::min<uint64_t>(64, kLdsRoundBytes / (stride * sizeof(float)) / 4 * 4);
+    // lanes per workgroup (kDriver dspb_seg_nb: the same formula)
+    const uint64_t nb = std::min<uint64_t>(64, kLdsRoundBytes / (stride * sizeof(float)));
     if (nb < 4) return 1;
     for (int i = 0; i < 2 && !fw; ++i)
         if (m->f_seg_walk[i] && (!kWalkShapes[i].C || kWalkShapes[i].C == C) &&
