@@ -364,10 +364,17 @@ __device__ static void dspb_stateless_lds(const dspb_render_args &A) {
         __syncthreads();
     }
 }
-// blocks per round of the LDS-blocks path at a block stride of SB floats
-// (the host computes the same: module.cpp lds_round)
+// blocks per round of the LDS-blocks path at a block stride of SB floats, a
+// multiple of 4 (18 blocks of stereo B = 512 instead of 16 made the
+// stateless rounds 1-6% slower, profiles/r05_lds_nb_ab.txt), and lanes of
+// the segment kernels: as many as the round's LDS holds (18 instead of 16:
+// 15% faster).  The host computes the same (module_render, module_render_seg)
 constexpr unsigned dspb_lds_nb(unsigned SB) {
     const unsigned v = DSPB_LDS_ROUND_BYTES / (SB * 4u) / 4u * 4u;
+    return v < 64u ? v : 64u;
+}
+constexpr unsigned dspb_seg_nb(unsigned SB) {
+    const unsigned v = DSPB_LDS_ROUND_BYTES / (SB * 4u);
     return v < 64u ? v : 64u;
 }
 // the LDS-blocks path for a constant shape (C, B, 4 | B), software
@@ -607,12 +614,6 @@ __device__ static bool dspb_same_state(const State *a, const State *b) {
         for (unsigned i = 0; i < sizeof(State); ++i) d |= (unsigned)(x[i] ^ y[i]);
     }
     return d == 0;
-}
-// lanes (blocks in LDS) per workgroup of the segment kernels: as many as the
-// round's LDS holds (the host computes the same: module_render_seg)
-constexpr unsigned dspb_seg_nb(unsigned SB) {
-    const unsigned v = DSPB_LDS_ROUND_BYTES / (SB * 4u);
-    return v < 64u ? v : 64u;
 }
 // lane t's segment: its index (~0u: none), first block rendered (warm-up
 // included), warm-up blocks, blocks rendered
