@@ -108,880 +108,8 @@ struct SegArgsG {
     unsigned pass;
 };
 
-const char *kDriver = R"DSPB(
-struct dspb_render_args {
-    void *P;
-    void *S;
-    float *in[16];
-    float *out[16];
-    unsigned long long L;
-    unsigned long long nblocks;
-    unsigned long long block0;
-    unsigned in_ch;
-    unsigned C;
-    unsigned B;
-    float sr;
-    unsigned lds;
-    unsigned lds_nb;
-    unsigned lds_stride;
-    unsigned par;
-};
-extern "C" __global__ void dspb_sizes(unsigned *o) {
-    o[0] = sizeof(Parameters);
-    o[1] = sizeof(State);
-    o[2] = __is_empty(State) ? 1u : 0u;
-}
-extern "C" __global__ void dspb_defaults(Parameters *p) { *p = default_parameters(); }
-// non-const lvalues, as the reference's generated wrappers pass them
-// (compiler.cpp:1181-1203): plugins may take Parameters& or const Parameters&
-extern "C" __global__ void dspb_init(Parameters *p, State *s, unsigned C, float sr, dspb_arena *a) {
-    *s = initialize_state(*p, C, sr, (void *)a);
-}
-// one block: the render_audio body (audio.cpp:13-175), one-shot
-__device__ static void dspb_block(const dspb_render_args &A, unsigned long long b, State &st) {
-    float *ptrs[16];
-    const unsigned long long s0 = (A.block0 + b) * A.B;  // global sample of the block
-    for (unsigned c = 0; c < A.C; ++c) {
-        ptrs[c] = A.out[c] + b * A.B;
-        for (unsigned s = 0; s < A.B; ++s) {
-            const unsigned long long i = b * A.B + s;
-            ptrs[c][s] = (c < A.in_ch && i < A.L) ? A.in[c][i] : 0.0f;
-        }
-    }
-    (void)s0;
-    audio_callback(*(Parameters *)A.P, st, ptrs, A.C, A.B, A.sr);
-}
-// render_audio's copy of block b into a staging buffer (zero past EOF and
-// for the channels the file lacks), element j of every (n0 + k*nt) stride
-__device__ static void dspb_stage_in(const dspb_render_args &A, unsigned long long b, float *buf, unsigned j0,
-                                     unsigned nt) {
-    const unsigned CB = A.C * A.B;
-    for (unsigned j = j0; j < CB; j += nt) {
-        const unsigned c = j / A.B, s = j - c * A.B;
-        const unsigned long long i = b * A.B + s;
-        buf[j] = (c < A.in_ch && i < A.L) ? A.in[c][i] : 0.0f;
-    }
-}
-__device__ static void dspb_stage_out(const dspb_render_args &A, unsigned long long b, const float *buf,
-                                      unsigned j0, unsigned nt) {
-    const unsigned CB = A.C * A.B;
-    for (unsigned j = j0; j < CB; j += nt) {
-        const unsigned c = j / A.B, s = j - c * A.B;
-        A.out[c][b * A.B + s] = buf[j];
-    }
-}
-typedef __attribute__((address_space(1))) float dspb_gfloat;
-// the Parameters / State blobs, read through a global-address-space pointer:
-// a copy the compiler forwards to the source then reads global memory, which
-// the callback's LDS stores cannot alias -- so a field the callback reads
-// every sample (gain_test's gain, IR_test's step) stays in a register
-// instead of being reloaded through a flat pointer after every store
-template <class T> __device__ static inline T dspb_from_global(const void *p) {
-    return *(const __attribute__((address_space(1))) T *)p;
-}
-// the State of a parallel render: empty, or one the callback never writes
-// (dsp_module_facts: proven from the callback's IR, with no global memory
-// written).  Each lane calls the
-// callback with a private copy when the State is small (its fields then stay
-// in registers), else with the shared blob itself (read only).
-template <bool kSmall = (sizeof(State) <= 256)> struct dspb_ro_state {
-    State s;
-    __device__ explicit dspb_ro_state(const void *p) : s(dspb_from_global<State>(p)) {}
-    __device__ State &get() { return s; }
-};
-template <> struct dspb_ro_state<false> {
-    State *s;
-    __device__ explicit dspb_ro_state(const void *p) : s((State *)p) {}
-    __device__ State &get() { return *s; }
-};
-// a generic pointer the compiler can prove is global memory (global_load /
-// global_store in the inlined callback, not flat ops that also wait on LDS)
-__device__ static inline float *dspb_global(float *p) { return (float *)(dspb_gfloat *)p; }
-// no state: one wavefront renders 64 consecutive blocks. render_audio's copy
-// (audio.cpp:13-175: the file at the cursor, zeros past EOF and for the
-// channels the file lacks) runs first for all 64 blocks at once, coalesced
-// per channel, four loads in flight per lane before their stores (in == out
-// is allowed: every element is stored where it was loaded). Then lane t runs
-// the callback in place on block t. CC > 0 makes the channel count a
-// constant, so the callback's channel loops unroll and its pointer table
-// lives in registers instead of scratch.
-template <unsigned CC>
-__device__ static void dspb_stateless(const dspb_render_args &A) {
-    dspb_ro_state<> local(A.S);
-    // a private copy: the callback's stores cannot alias it, so its fields
-    // stay in registers instead of being reloaded after every store
-    Parameters prm = dspb_from_global<Parameters>(A.P);
-    const unsigned C = CC ? CC : A.C, t = threadIdx.x;
-    for (unsigned long long b0 = (unsigned long long)blockIdx.x * 64; b0 < A.nblocks;
-         b0 += (unsigned long long)gridDim.x * 64) {
-        const unsigned long long nb = A.nblocks - b0 < 64 ? A.nblocks - b0 : 64;
-        const unsigned long long i0 = b0 * A.B, n = nb * A.B;
-        const unsigned long long lim = A.L > i0 ? A.L - i0 : 0;  // file samples left at i0
-        for (unsigned c = 0; c < C; ++c) {
-            dspb_gfloat *o = (dspb_gfloat *)A.out[c] + i0;
-            const dspb_gfloat *x = (const dspb_gfloat *)A.in[c < A.in_ch ? c : 0] + i0;
-            const unsigned long long m = c < A.in_ch ? (lim < n ? lim : n) : 0;  // copied, the rest zeroed
-            unsigned long long j = t;
-            for (; j + 192 < m; j += 256) {
-                const float v0 = x[j], v1 = x[j + 64], v2 = x[j + 128], v3 = x[j + 192];
-                o[j] = v0;
-                o[j + 64] = v1;
-                o[j + 128] = v2;
-                o[j + 192] = v3;
-            }
-            for (; j < m; j += 64) o[j] = x[j];
-            for (j = m + ((t - m) & 63); j < n; j += 64) o[j] = 0.0f;
-        }
-        __syncthreads();  // the wave's copies are visible to every lane
-        if (t < nb) {
-            float *ptrs[CC ? CC : 16];
-            for (unsigned c = 0; c < C; ++c) ptrs[c] = dspb_global(A.out[c] + (i0 + (unsigned long long)t * A.B));
-            audio_callback(prm, local.get(), ptrs, C, A.B, A.sr);
-        }
-        __syncthreads();
-    }
-}
-// stateful, in order: thread 0 runs the callback on block b in LDS while
-// waves 1.. write block b - 1 out and stage block b + 1 in the other half of
-// the double buffer (the same elements per thread, so no element is
-// overwritten before it is written out). Thread 0 keeps Parameters and a
-// small State in private copies (written back at the end): the callback's
-// LDS stores cannot alias them, so they stay in registers. CC as above.
-template <unsigned CC, unsigned NB = 0>
-__device__ static void dspb_stateful_lds(const dspb_render_args &A) {
-    extern __shared__ float dspb_lbuf[];
-    const unsigned B = NB ? NB : A.B;
-    const unsigned C = CC ? CC : A.C, CB = C * B, t = threadIdx.x, nt = blockDim.x;
-    float *buf0 = dspb_lbuf, *buf1 = dspb_lbuf + CB;
-    dspb_stage_in(A, 0, buf0, t, nt);
-    __syncthreads();
-    constexpr bool kLocal = sizeof(State) <= 256;
-    State *gst = (State *)A.S;
-    // copies made by every thread (a few hundred bytes at most), used by
-    // thread 0; the blobs are plain bytes to the host, as in the reference
-    Parameters prm = dspb_from_global<Parameters>(A.P);
-    State local = *gst;
-    for (unsigned long long b = 0; b < A.nblocks; ++b) {
-        float *cur = (b & 1) ? buf1 : buf0, *oth = (b & 1) ? buf0 : buf1;
-        if (t == 0) {
-            float *ptrs[CC ? CC : 16];
-            for (unsigned c = 0; c < C; ++c) ptrs[c] = cur + c * B;
-            if constexpr (kLocal) audio_callback(prm, local, ptrs, C, B, A.sr);
-            else audio_callback(prm, *gst, ptrs, C, B, A.sr);
-        } else if (t >= 64) {
-            if (b > 0) dspb_stage_out(A, b - 1, oth, t - 64, nt - 64);
-            if (b + 1 < A.nblocks) dspb_stage_in(A, b + 1, oth, t - 64, nt - 64);
-        }
-        __syncthreads();
-    }
-    if constexpr (kLocal) {
-        if (t == 0) __builtin_memcpy((void *)gst, (const void *)&local, sizeof(State));
-    }
-    dspb_stage_out(A, A.nblocks - 1, (A.nblocks - 1) & 1 ? buf1 : buf0, t, nt);
-}
-// no state, LDS blocks: a workgroup renders lds_nb consecutive blocks per
-// round.  render_audio's copy (audio.cpp:13-175: the file at the cursor,
-// zeros past EOF and for the channels the file lacks) stages them into LDS
-// with all 256 threads, coalesced per channel; then the lanes of wave 0 run
-// the callback on one block each, in LDS (a block's rows at a stride of
-// C B + 1 floats: the lanes of one ds_read hit different banks); then all
-// threads copy the blocks out, coalesced.  The
-// callback's sample loop addresses one LDS base at constant offsets when C
-// and B are constants (CC, BB), so its loads run ahead of its stores.  Two
-// workgroups per CU: one stages while the other runs callbacks.
-template <unsigned CC, unsigned BB>
-__device__ static void dspb_stateless_lds(const dspb_render_args &A) {
-    extern __shared__ float dspb_lbuf[];
-    dspb_ro_state<> local(A.S);
-    Parameters prm = dspb_from_global<Parameters>(A.P);
-    const unsigned C = CC ? CC : A.C, B = BB ? BB : A.B, NB = A.lds_nb, SB = A.lds_stride;
-    const unsigned t = threadIdx.x, nt = blockDim.x;
-    for (unsigned long long b0 = (unsigned long long)blockIdx.x * NB; b0 < A.nblocks;
-         b0 += (unsigned long long)gridDim.x * NB) {
-        const unsigned nb = (unsigned)(A.nblocks - b0 < NB ? A.nblocks - b0 : NB);
-        const unsigned long long i0 = b0 * B;
-        const unsigned long long lim = A.L > i0 ? A.L - i0 : 0;  // file samples left at i0
-        const unsigned n = nb * B;
-        for (unsigned c = 0; c < C; ++c) {
-            const dspb_gfloat *x = (const dspb_gfloat *)A.in[c < A.in_ch ? c : 0] + i0;
-            const unsigned long long m = c < A.in_ch ? lim : 0;
-            float *row = dspb_lbuf + c * B;
-            if (m >= n && (B & 3) == 0 && (((unsigned long long)x) & 15) == 0) {
-                // the whole round is inside the file: 16-byte loads, two in
-                // flight per thread (a float4 never crosses a block: 4 | B)
-                const __attribute__((address_space(1))) float4 *x4 =
-                    (const __attribute__((address_space(1))) float4 *)x;
-                unsigned j = 4 * t;
-                for (; j + 4 * nt < n; j += 8 * nt) {
-                    const float4 v0 = x4[j / 4], v1 = x4[(j + 4 * nt) / 4];
-                    unsigned q = j / B;
-                    float *d = row + q * SB + (j - q * B);
-                    d[0] = v0.x, d[1] = v0.y, d[2] = v0.z, d[3] = v0.w;
-                    q = (j + 4 * nt) / B;
-                    d = row + q * SB + (j + 4 * nt - q * B);
-                    d[0] = v1.x, d[1] = v1.y, d[2] = v1.z, d[3] = v1.w;
-                }
-                for (; j < n; j += 4 * nt) {
-                    const float4 v0 = x4[j / 4];
-                    const unsigned q = j / B;
-                    float *d = row + q * SB + (j - q * B);
-                    d[0] = v0.x, d[1] = v0.y, d[2] = v0.z, d[3] = v0.w;
-                }
-            } else {  // EOF in the round, or no file channel: zeros past it
-                for (unsigned j = t; j < n; j += nt) {
-                    const unsigned q = j / B;
-                    row[q * SB + (j - q * B)] = j < m ? x[j] : 0.0f;
-                }
-            }
-        }
-        __syncthreads();
-        // one wave, one block per lane (an LDS instruction costs its cycles
-        // whatever the active lanes, so the callbacks share as few as possible)
-        if (t < nb) {
-            float *blk = dspb_lbuf + t * SB;
-            float *ptrs[CC ? CC : 16];
-            for (unsigned c = 0; c < C; ++c) ptrs[c] = blk + c * B;
-            audio_callback(prm, local.get(), ptrs, C, B, A.sr);
-        }
-        __syncthreads();
-        for (unsigned c = 0; c < C; ++c) {
-            dspb_gfloat *o = (dspb_gfloat *)A.out[c] + i0;
-            const float *row = dspb_lbuf + c * B;
-            if ((B & 3) == 0 && (((unsigned long long)o) & 15) == 0) {
-                __attribute__((address_space(1))) float4 *o4 = (__attribute__((address_space(1))) float4 *)o;
-                for (unsigned j = 4 * t; j < n; j += 4 * nt) {
-                    const unsigned q = j / B;
-                    const float *d = row + q * SB + (j - q * B);
-                    o4[j / 4] = make_float4(d[0], d[1], d[2], d[3]);
-                }
-            } else {
-                for (unsigned j = t; j < n; j += nt) {
-                    const unsigned q = j / B;
-                    o[j] = row[q * SB + (j - q * B)];
-                }
-            }
-        }
-        __syncthreads();
-    }
-}
-// blocks per round of the LDS-blocks path at a block stride of SB floats, a
-// multiple of 4 (18 blocks of stereo B = 512 instead of 16 made the
-// stateless rounds 1-6% slower, profiles/r05_lds_nb_ab.txt), and lanes of
-// the segment kernels: as many as the round's LDS holds (18 instead of 16:
-// 15% faster).  The host computes the same (module_render, module_render_seg)
-constexpr unsigned dspb_lds_nb(unsigned SB) {
-    const unsigned v = DSPB_LDS_ROUND_BYTES / (SB * 4u) / 4u * 4u;
-    return v < 64u ? v : 64u;
-}
-constexpr unsigned dspb_seg_nb(unsigned SB) {
-    const unsigned v = DSPB_LDS_ROUND_BYTES / (SB * 4u);
-    return v < 64u ? v : 64u;
-}
-// the LDS-blocks path for a constant shape (C, B, 4 | B), software
-// pipelined over the workgroup's rounds: a persistent grid of two
-// workgroups per CU walks the file, and while round r's callbacks run in LDS,
-// the next round's file samples are already in flight into registers (16-byte
-// loads, all issued at once), so a round costs its callbacks and one copy
-// out, not a chain of dependent HBM loads.  Rounds the file does not cover
-// completely (EOF, the ragged last round) or an unaligned file take
-// render_audio's copy with zeros instead.  Block rows at a stride of C B + 2
-// floats: 8-byte aligned (the copies move float2 pairs through LDS, 16-byte
-// rows to and from HBM) and conflict-free for the 16 callback lanes of a
-// stereo B = 512 round.
-template <unsigned CC, unsigned BB>
-__device__ static void dspb_stateless_lds_pf(const dspb_render_args &A) {
-    extern __shared__ float dspb_lbuf[];
-    constexpr unsigned C = CC, B = BB, SB = C * B + 2u, NB = dspb_lds_nb(SB);
-    constexpr unsigned N4 = NB * B / 4u, PT = (N4 + 255u) / 256u;  // float4 per channel per round / per thread
-    static_assert(NB <= 64 && B % 4 == 0, "one wave runs a round's callbacks");
-    typedef __attribute__((address_space(1))) float4 gfloat4;
-    dspb_ro_state<> local(A.S);
-    Parameters prm = dspb_from_global<Parameters>(A.P);
-    const unsigned t = threadIdx.x, lane = t & 63u;
-    const unsigned long long stride = (unsigned long long)gridDim.x * NB;
-    bool aligned_in = true;
-    for (unsigned c = 0; c < C && c < A.in_ch; ++c) aligned_in = aligned_in && !(((unsigned long long)A.in[c]) & 15);
-    auto full = [&](unsigned long long b0) {
-        return b0 + NB <= A.nblocks && (A.in_ch == 0 || ((b0 + NB) * B <= A.L && aligned_in));
-    };
-    float4 pf[C][PT];
-    auto load = [&](unsigned long long b0) {
-#pragma unroll
-        for (unsigned c = 0; c < C; ++c) {
-            const gfloat4 *x4 = (const gfloat4 *)(A.in[c < A.in_ch ? c : 0] + b0 * B);
-#pragma unroll
-            for (unsigned k = 0; k < PT; ++k) {
-                const unsigned i = t + 256u * k;
-                if (c < A.in_ch && (N4 % 256u == 0 || i < N4)) {
-                    const float4 v = x4[i];
-                    pf[c][k] = v;
-                } else {
-                    pf[c][k] = make_float4(0.f, 0.f, 0.f, 0.f);
-                }
-            }
-        }
-    };
-    unsigned long long b0 = (unsigned long long)blockIdx.x * NB;
-    bool have = b0 < A.nblocks && full(b0);
-    if (have) load(b0);
-    for (; b0 < A.nblocks; b0 += stride) {
-        const unsigned nb = (unsigned)(A.nblocks - b0 < NB ? A.nblocks - b0 : NB);
-        const unsigned long long i0 = b0 * B;
-        const unsigned n = nb * B;
-        if (have) {
-#pragma unroll
-            for (unsigned c = 0; c < C; ++c) {
-#pragma unroll
-                for (unsigned k = 0; k < PT; ++k) {
-                    const unsigned j = 4u * (t + 256u * k);
-                    if (N4 % 256u == 0 || j < 4u * N4) {
-                        float2 *d = (float2 *)(dspb_lbuf + (j / B) * SB + c * B + j % B);
-                        d[0] = make_float2(pf[c][k].x, pf[c][k].y);
-                        d[1] = make_float2(pf[c][k].z, pf[c][k].w);
-                    }
-                }
-            }
-        } else {  // render_audio's copy with zeros past EOF and for missing channels
-            const unsigned long long lim = A.L > i0 ? A.L - i0 : 0;
-            for (unsigned c = 0; c < C; ++c) {
-                const dspb_gfloat *x = (const dspb_gfloat *)A.in[c < A.in_ch ? c : 0] + i0;
-                const unsigned long long m = c < A.in_ch ? lim : 0;
-                for (unsigned j = t; j < n; j += 256u) dspb_lbuf[(j / B) * SB + c * B + j % B] = j < m ? x[j] : 0.0f;
-            }
-        }
-        __syncthreads();
-        // the next round's loads fly while this round's callbacks run
-        have = b0 + stride < A.nblocks && full(b0 + stride);
-        if (have) load(b0 + stride);
-        // one wave, one block per lane: an LDS instruction costs its cycles
-        // whatever the active lanes, so the callbacks share as few as possible
-        if (t < nb) {
-            float *blk = dspb_lbuf + lane * SB;
-            float *ptrs[C];
-            for (unsigned c = 0; c < C; ++c) ptrs[c] = blk + c * B;
-            audio_callback(prm, local.get(), ptrs, C, B, A.sr);
-        }
-        __syncthreads();
-        for (unsigned c = 0; c < C; ++c) {
-            if ((((unsigned long long)A.out[c]) & 15) == 0) {
-                gfloat4 *o4 = (gfloat4 *)(A.out[c] + i0);
-#pragma unroll 4
-                for (unsigned j = 4u * t; j < n; j += 1024u) {
-                    const float2 *d = (const float2 *)(dspb_lbuf + (j / B) * SB + c * B + j % B);
-                    const float2 lo = d[0], hi = d[1];
-                    o4[j / 4u] = make_float4(lo.x, lo.y, hi.x, hi.y);
-                }
-            } else {
-                dspb_gfloat *o = (dspb_gfloat *)A.out[c] + i0;
-                for (unsigned j = t; j < n; j += 256u) o[j] = dspb_lbuf[(j / B) * SB + c * B + j % B];
-            }
-        }
-        __syncthreads();
-    }
-}
-// the LDS-blocks path: four waves, two workgroups per CU, one kernel per
-// (C, B) instantiation (the host picks it).  Kept apart, each kernel's
-// register budget is its own: with all instantiations behind one dispatch the
-// scheduler held the callback to one LDS round trip per sample pair (a ds_read
-// waited on the previous ds_write) to keep the whole kernel under 64 VGPRs.
-// Constant shapes with 4 | B take the pipelined rounds (dspb_stateless_lds_pf).
-#define DSPB_LDS_KERNEL(name, CC, BB)                                                  \
-    extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) void name(  \
-        dspb_render_args A) {                                                          \
-        if (A.par) {                                                                   \
-            if constexpr (CC > 0 && BB > 0 && BB % 4 == 0) dspb_stateless_lds_pf<CC, BB>(A); \
-            else dspb_stateless_lds<CC, BB>(A);                                        \
-        }                                                                              \
-    }
-DSPB_LDS_KERNEL(dspb_render_lds_c2b512, 2, 512)
-DSPB_LDS_KERNEL(dspb_render_lds_c2b256, 2, 256)
-DSPB_LDS_KERNEL(dspb_render_lds_c2b1024, 2, 1024)
-DSPB_LDS_KERNEL(dspb_render_lds_c1b512, 1, 512)
-DSPB_LDS_KERNEL(dspb_render_lds_c1, 1, 0)
-DSPB_LDS_KERNEL(dspb_render_lds_c2, 2, 0)
-DSPB_LDS_KERNEL(dspb_render_lds, 0, 0)
-extern "C" __global__ void dspb_render(dspb_render_args A) {
-    extern __shared__ float dspb_lbuf[];
-    if (A.par) {
-        if (A.C == 1) dspb_stateless<1>(A);
-        else if (A.C == 2) dspb_stateless<2>(A);
-        else dspb_stateless<0>(A);
-    } else if (!A.lds) {  // stateful, blocks too large for LDS: in order, one thread
-        if (blockIdx.x == 0 && threadIdx.x == 0) {
-            State &st = *(State *)A.S;
-            for (unsigned long long b = 0; b < A.nblocks; ++b) dspb_block(A, b, st);
-        }
-    } else if (blockIdx.x == 0) {
-        // B = 512 stereo as constants too: the callback's sample loop then
-        // addresses one LDS base at constant offsets, so its loads can run
-        // ahead of its stores instead of waiting a round trip per sample
-        // (512: the render configs; 256: BASELINE configs[0], the reference
-        // device's forced stereo)
-        if (A.C == 2 && A.B == 512) dspb_stateful_lds<2, 512>(A);
-        else if (A.C == 2 && A.B == 256) dspb_stateful_lds<2, 256>(A);
-        else if (A.C == 1) dspb_stateful_lds<1>(A);
-        else if (A.C == 2) dspb_stateful_lds<2>(A);
-        else dspb_stateful_lds<0>(A);
-    }
-}
-// the stateful LDS path's common shapes as kernels of their own (as the
-// LDS-blocks kernels above: a register budget of their own, so the callback's
-// LDS loads can run ahead of its stores)
-#define DSPB_ST_KERNEL(name, CC, BB)                                                   \
-    extern "C" __global__ void name(dspb_render_args A) {                              \
-        extern __shared__ float dspb_lbuf[];                                           \
-        if (!A.par && blockIdx.x == 0) dspb_stateful_lds<CC, BB>(A);                   \
-    }
-DSPB_ST_KERNEL(dspb_render_st_c2b512, 2, 512)
-DSPB_ST_KERNEL(dspb_render_st_c2b256, 2, 256)
-DSPB_ST_KERNEL(dspb_render_st_c1, 1, 0)
-DSPB_ST_KERNEL(dspb_render_st_c2, 2, 0)
-
-// ---- a State the callback writes: speculative segments (module_render_seg)
-// The file's blocks are cut into K segments of `seg` blocks.  Pass 1 runs
-// every segment at once, one lane each, from the live State after `warm`
-// blocks of warm-up on the blocks before it (their output discarded), and
-// records the State it rendered each kept block from (st_blk, one per block
-// of the file) and the State it ended with (st_end).  The callback is a
-// function of (Parameters, State, block) -- the analysis proved it writes no
-// other memory -- so a segment whose first block's State equals, bit for bit,
-// the true State there rendered exactly what the serial chain renders;
-// segment 0 starts from the live State itself, and by induction every segment
-// k whose st_blk at its first block equals st_end[k - 1] is exact when
-// segment k - 1 is.  A check lists the others (and hands each its
-// predecessor's st_end), a rerun pass renders the listed segments again from
-// those States, in parallel, each only until its State meets the one
-// recorded at a block boundary (from there on the recorded blocks were
-// rendered from the same bits); after the last check one workgroup walks the
-// segments in order and reruns serially, with the same early stop, whatever
-// still differs, so the result is the serial chain's whatever the plugin
-// does.  Filters forget their State: their trajectories from different States
-// meet bit for bit within a few hundred samples, and one pass suffices.
-struct dspb_seg_args {
-    dspb_render_args R;
-    State *st_blk;          // [nblocks] the State each block was rendered from
-    State *st_end;          // [K] the State each segment ended with
-    unsigned *list;         // segments to rerun (check -> rerun)
-    unsigned *count;        // how many
-    unsigned *prev_count;   // a rerun's check: the rerun's count (0: nothing changed, skip)
-    unsigned char *flags;   // the last check: 1 = differed
-    unsigned *stats;        // [0, 4) segments that differed per warm-up level, [4] / [5] after
-                            // rerun 1 / 2, [7] serial reruns of the walk, [8, 12) levels run
-    unsigned long long seg; // blocks per segment
-    unsigned K;             // segments
-    unsigned warm;          // pass 1: warm-up blocks
-    unsigned prev_warm;     // pass 1 at level > 0: the warm-up of the level before
-    unsigned level;         // pass 1 / its check: the warm-up level (~0u: a rerun's check)
-    unsigned mode;          // segments: 0 = pass 1 (every segment), 1 = rerun the listed ones;
-                            // check: 1 = list the differing ones for a rerun (0: flag only)
-    unsigned pass;          // the check's stats slot
-};
-// pass 1 at warm-up level L > 0 (and its check) runs only when level L - 1
-// ran and more than 1/8 of the segments it guessed -- those whose warm-up
-// began after block 0 -- started from a State that was not the true one: the
-// trajectories had not met within its warm-up, so a 16x longer one is tried
-__device__ static bool dspb_seg_level_runs(const dspb_seg_args &G) {
-    if (G.level == 0) return true;
-    const volatile unsigned *st = G.stats;
-    const unsigned prev = G.level - 1;
-    if (!st[8 + prev]) return false;
-    const unsigned long long early = G.prev_warm / G.seg < G.K - 1 ? G.prev_warm / G.seg : G.K - 1;
-    const unsigned long long guessed = G.K - 1 - early;
-    return guessed && st[prev] * 8ull > guessed;
-}
-// a State copy as whole words, fully unrolled (a private State stays in
-// registers; a memcpy this size would be lowered to a loop over it)
-__device__ static inline void dspb_copy_state(void *dst, const void *src) {
-    if constexpr (sizeof(State) % 4 == 0 && alignof(State) >= 4) {
-#pragma unroll
-        for (unsigned i = 0; i < sizeof(State) / 4; ++i) ((unsigned *)dst)[i] = ((const unsigned *)src)[i];
-    } else {
-#pragma unroll
-        for (unsigned i = 0; i < sizeof(State); ++i) ((unsigned char *)dst)[i] = ((const unsigned char *)src)[i];
-    }
-}
-// bit-for-bit equality; every word is loaded before any is compared (no
-// short circuit: one memory round trip, not one per word)
-__device__ static bool dspb_same_state(const State *a, const State *b) {
-    unsigned d = 0;
-    if constexpr (sizeof(State) % 4 == 0 && alignof(State) >= 4) {
-        const unsigned *x = (const unsigned *)a, *y = (const unsigned *)b;
-#pragma unroll
-        for (unsigned i = 0; i < sizeof(State) / 4; ++i) d |= x[i] ^ y[i];
-    } else {
-        const unsigned char *x = (const unsigned char *)a, *y = (const unsigned char *)b;
-#pragma unroll
-        for (unsigned i = 0; i < sizeof(State); ++i) d |= (unsigned)(x[i] ^ y[i]);
-    }
-    return d == 0;
-}
-// lane t's segment: its index (~0u: none), first block rendered (warm-up
-// included), warm-up blocks, blocks rendered
-__device__ static unsigned dspb_seg_lane(const dspb_seg_args &G, unsigned base, unsigned t, unsigned nseg,
-                                         unsigned *s_first, unsigned *s_warm, unsigned *s_len) {
-    const dspb_render_args &A = G.R;
-    unsigned k = 0xffffffffu, f = 0, w = 0, len = 0;
-    if (base + t < nseg) {
-        k = G.mode ? G.list[base + t] : base + t;
-        const unsigned long long b0 = (unsigned long long)k * G.seg;
-        const unsigned long long b1 = b0 + G.seg < A.nblocks ? b0 + G.seg : A.nblocks;
-        w = (G.mode || k == 0) ? 0u : (unsigned)(G.warm < b0 ? G.warm : b0);
-        f = (unsigned)(b0 - w);
-        len = w + (unsigned)(b1 - b0);
-    }
-    s_first[t] = f;
-    s_warm[t] = w;
-    s_len[t] = len;
-    return k;
-}
-// a lane about to render block b in its round r (w: its warm-up blocks):
-// pass 1 records the State a kept block is rendered from; a rerun stops
-// (false) where its State meets the one recorded there
-template <bool kRerun>
-__device__ static bool dspb_seg_block(const dspb_seg_args &G, unsigned long long b, unsigned r, unsigned w,
-                                      State &st) {
-    if (r < w) return true;  // warm-up: nothing kept
-    if (kRerun && r > 0 && dspb_same_state(&st, &G.st_blk[b])) return false;
-    dspb_copy_state((void *)&G.st_blk[b], (const void *)&st);
-    return true;
-}
-// pass 1 / rerun, any shape: lane t of wave 0 runs segment k_t, rounds of one
-// block per lane staged in LDS by all 256 threads (render_audio's copy: zeros
-// past EOF and for the channels the file lacks), kept blocks copied out after
-// the callbacks.  CC / BB constants as in the LDS-blocks path.
-template <unsigned CC, unsigned BB>
-__device__ static void dspb_segments(const dspb_seg_args &G) {
-    extern __shared__ float dspb_lbuf[];
-    __shared__ unsigned s_first[64], s_warm[64], s_len[64];
-    const dspb_render_args &A = G.R;
-    const unsigned C = CC ? CC : A.C, B = BB ? BB : A.B, CB = C * B, NB = A.lds_nb, SB = A.lds_stride;
-    const unsigned t = threadIdx.x, nt = blockDim.x;
-    const unsigned base = blockIdx.x * NB;
-    if (!G.mode) {  // pass 1: at a warm-up level that runs; it restarts the listing
-        if (!dspb_seg_level_runs(G)) return;
-        if (G.level && blockIdx.x == 0 && t == 0) *G.count = 0;
-    }
-    const unsigned nseg = G.mode ? *(volatile unsigned *)G.count : G.K;
-    if (base >= nseg) return;  // the same for the whole workgroup
-    unsigned k = 0xffffffffu;
-    if (t < NB) k = dspb_seg_lane(G, base, t, nseg, s_first, s_warm, s_len);
-    __syncthreads();
-    unsigned rounds = 0;
-    for (unsigned i = 0; i < NB; ++i) rounds = s_len[i] > rounds ? s_len[i] : rounds;
-    Parameters prm = dspb_from_global<Parameters>(A.P);
-    State st;
-    bool stopped = false;
-    if (k != 0xffffffffu)
-        dspb_copy_state((void *)&st, G.mode ? (const void *)&G.st_blk[(unsigned long long)k * G.seg] : (const void *)A.S);
-    for (unsigned r = 0; r < rounds; ++r) {
-        for (unsigned j = t; j < NB * CB; j += nt) {
-            const unsigned i = j / CB, e = j - i * CB, c = e / B, s = e - c * B;
-            if (r < s_len[i]) {
-                const unsigned long long gi = (unsigned long long)(s_first[i] + r) * B + s;
-                dspb_lbuf[i * SB + e] = (c < A.in_ch && gi < A.L) ? ((const dspb_gfloat *)A.in[c])[gi] : 0.0f;
-            }
-        }
-        __syncthreads();
-        if (k != 0xffffffffu && r < s_len[t]) {
-            if (G.mode ? dspb_seg_block<true>(G, (unsigned long long)s_first[t] + r, r, s_warm[t], st)
-                       : dspb_seg_block<false>(G, (unsigned long long)s_first[t] + r, r, s_warm[t], st)) {
-                float *blk = dspb_lbuf + t * SB;
-                float *ptrs[CC ? CC : 16];
-                for (unsigned c = 0; c < C; ++c) ptrs[c] = blk + c * B;
-                audio_callback(prm, st, ptrs, C, B, A.sr);
-            } else {
-                s_len[t] = r;  // met the recorded chain: the rest stands
-                stopped = true;
-            }
-        }
-        __syncthreads();
-        for (unsigned j = t; j < NB * CB; j += nt) {
-            const unsigned i = j / CB, e = j - i * CB, c = e / B, s = e - c * B;
-            if (r >= s_warm[i] && r < s_len[i])
-                ((dspb_gfloat *)A.out[c])[(unsigned long long)(s_first[i] + r) * B + s] = dspb_lbuf[i * SB + e];
-        }
-        __syncthreads();
-        rounds = 0;
-        for (unsigned i = 0; i < NB; ++i) rounds = s_len[i] > rounds ? s_len[i] : rounds;
-    }
-    if (k != 0xffffffffu && !stopped) dspb_copy_state((void *)&G.st_end[k], (const void *)&st);
-}
-// the same for a constant shape (C, B, 4 | B), software pipelined: round r +
-// 1's blocks are in flight into registers (16-byte loads, all issued at once)
-// while round r's callbacks run; blocks at a stride of C B + 2 floats (float2
-// LDS moves; the 16 callback lanes on distinct banks), as dspb_stateless_lds_pf
-template <unsigned CC, unsigned BB, bool kRerun>
-__device__ static void dspb_segments_pf(const dspb_seg_args &G) {
-    extern __shared__ float dspb_lbuf[];
-    __shared__ unsigned s_first[64], s_warm[64], s_len[64];
-    constexpr unsigned C = CC, B = BB, CB = C * B, SB = CB + 2u, NB = dspb_seg_nb(SB);
-    // per channel: NB rows of B / 4 float4, PV of them per thread
-    constexpr unsigned R4 = B / 4u, T4 = NB * R4, PV = (T4 + 255u) / 256u;
-    static_assert(NB <= 64 && B % 4 == 0, "one wave runs a round's callbacks");
-    typedef __attribute__((address_space(1))) float4 gfloat4;
-    const dspb_render_args &A = G.R;
-    const unsigned t = threadIdx.x;
-    const unsigned base = blockIdx.x * NB;
-    if (!kRerun) {  // pass 1: at a warm-up level that runs; it restarts the listing
-        if (!dspb_seg_level_runs(G)) return;
-        if (G.level && blockIdx.x == 0 && t == 0) *G.count = 0;
-    }
-    const unsigned nseg = kRerun ? *(volatile unsigned *)G.count : G.K;
-    if (base >= nseg) return;  // the same for the whole workgroup
-    unsigned k = 0xffffffffu;
-    if (t < NB) k = dspb_seg_lane(G, base, t, nseg, s_first, s_warm, s_len);
-    __syncthreads();
-    unsigned rounds = 0;
-    for (unsigned i = 0; i < NB; ++i) rounds = s_len[i] > rounds ? s_len[i] : rounds;
-    // the channels' rows as uniform values (the channel of every access below
-    // is a constant, so none of them is an indexed load of the argument block)
-    const dspb_gfloat *xin[C];
-    dspb_gfloat *xout[C];
-    bool aligned_in = true, aligned_out = true;
-#pragma unroll
-    for (unsigned c = 0; c < C; ++c) {
-        xin[c] = (const dspb_gfloat *)A.in[c < A.in_ch ? c : 0];
-        xout[c] = (dspb_gfloat *)A.out[c];
-        if (c < A.in_ch) aligned_in = aligned_in && !(((unsigned long long)A.in[c]) & 15);
-        aligned_out = aligned_out && !(((unsigned long long)A.out[c]) & 15);
-    }
-    Parameters prm = dspb_from_global<Parameters>(A.P);
-    State st;
-    bool stopped = false;
-    if (k != 0xffffffffu)
-        dspb_copy_state((void *)&st, kRerun ? (const void *)&G.st_blk[(unsigned long long)k * G.seg] : (const void *)A.S);
-    float4 pf[C][PV];
-    auto load = [&](unsigned r) {
-#pragma unroll
-        for (unsigned c = 0; c < C; ++c) {
-#pragma unroll
-            for (unsigned v = 0; v < PV; ++v) {
-                const unsigned q = t + 256u * v, i = q / R4, s = (q - i * R4) * 4u;
-                float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
-                if ((T4 % 256u == 0 || q < T4) && r < s_len[i] && c < A.in_ch) {
-                    const unsigned long long gi = (unsigned long long)(s_first[i] + r) * B + s;
-                    if (aligned_in && gi + 4 <= A.L) {
-                        x = *(const gfloat4 *)(xin[c] + gi);
-                    } else {
-                        x.x = gi < A.L ? xin[c][gi] : 0.f;
-                        x.y = gi + 1 < A.L ? xin[c][gi + 1] : 0.f;
-                        x.z = gi + 2 < A.L ? xin[c][gi + 2] : 0.f;
-                        x.w = gi + 3 < A.L ? xin[c][gi + 3] : 0.f;
-                    }
-                }
-                pf[c][v] = x;
-            }
-        }
-    };
-    if (rounds) load(0);
-    for (unsigned r = 0; r < rounds; ++r) {
-#pragma unroll
-        for (unsigned c = 0; c < C; ++c) {
-#pragma unroll
-            for (unsigned v = 0; v < PV; ++v) {
-                const unsigned q = t + 256u * v, i = q / R4, s = (q - i * R4) * 4u;
-                if ((T4 % 256u == 0 || q < T4) && r < s_len[i]) {
-                    float2 *d = (float2 *)(dspb_lbuf + i * SB + c * B + s);
-                    d[0] = make_float2(pf[c][v].x, pf[c][v].y);
-                    d[1] = make_float2(pf[c][v].z, pf[c][v].w);
-                }
-            }
-        }
-        __syncthreads();
-        if (r + 1 < rounds) load(r + 1);  // in flight while the callbacks run
-        if (k != 0xffffffffu && r < s_len[t]) {
-            if (dspb_seg_block<kRerun>(G, (unsigned long long)s_first[t] + r, r, s_warm[t], st)) {
-                float *blk = dspb_lbuf + t * SB;
-                float *ptrs[C];
-                for (unsigned c = 0; c < C; ++c) ptrs[c] = blk + c * B;
-                audio_callback(prm, st, ptrs, C, B, A.sr);
-            } else {
-                s_len[t] = r;  // met the recorded chain: the rest stands
-                stopped = true;
-            }
-        }
-        __syncthreads();
-#pragma unroll
-        for (unsigned c = 0; c < C; ++c) {
-#pragma unroll
-            for (unsigned v = 0; v < PV; ++v) {
-                const unsigned q = t + 256u * v, i = q / R4, s = (q - i * R4) * 4u;
-                if ((T4 % 256u == 0 || q < T4) && r >= s_warm[i] && r < s_len[i]) {
-                    const unsigned long long gi = (unsigned long long)(s_first[i] + r) * B + s;
-                    const float2 *d = (const float2 *)(dspb_lbuf + i * SB + c * B + s);
-                    const float2 lo = d[0], hi = d[1];
-                    if (aligned_out) {
-                        *(gfloat4 *)(xout[c] + gi) = make_float4(lo.x, lo.y, hi.x, hi.y);
-                    } else {
-                        xout[c][gi] = lo.x, xout[c][gi + 1] = lo.y, xout[c][gi + 2] = hi.x, xout[c][gi + 3] = hi.y;
-                    }
-                }
-            }
-        }
-        __syncthreads();
-        rounds = 0;
-        for (unsigned i = 0; i < NB; ++i) rounds = s_len[i] > rounds ? s_len[i] : rounds;
-    }
-    if (k != 0xffffffffu && !stopped) dspb_copy_state((void *)&G.st_end[k], (const void *)&st);
-}
-#define DSPB_SEG_KERNEL(name, CC, BB)                                                  \
-    extern "C" __global__ __launch_bounds__(256) void name(dspb_seg_args G) { dspb_segments<CC, BB>(G); }
-// pass 1 and the reruns as kernels of their own: pass 1 carries no
-// comparison (its registers are the callback's)
-#define DSPB_SEG_PF_KERNEL(name, CC, BB, RR)                                           \
-    extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) void name(  \
-        dspb_seg_args G) { dspb_segments_pf<CC, BB, RR>(G); }
-DSPB_SEG_PF_KERNEL(dspb_seg_c2b512, 2, 512, false)
-DSPB_SEG_PF_KERNEL(dspb_seg_c2b512_rerun, 2, 512, true)
-DSPB_SEG_KERNEL(dspb_seg_c1, 1, 0)
-DSPB_SEG_KERNEL(dspb_seg_c2, 2, 0)
-DSPB_SEG_KERNEL(dspb_seg, 0, 0)
-// segment k (k >= 1) rendered its first block from st_blk[k seg]; the true
-// State there is st_end[k - 1] if segment k - 1 is exact: flag the segments
-// where the two differ and, when a rerun follows, list them and give each
-// the State to start again from.  One wavefront per segment, its lanes over
-// the State's words; a check after a pass that found nothing to rerun
-// returns at once (nothing changed: the flags stand).
-extern "C" __global__ void dspb_seg_check(dspb_seg_args G) {
-    if (G.level != 0xffffffffu) {  // pass 1's check: where pass 1 ran
-        if (!dspb_seg_level_runs(G)) return;
-        if (blockIdx.x == 0 && threadIdx.x == 0) G.stats[8 + G.level] = 1;
-    } else if (*(volatile unsigned *)G.prev_count == 0) {
-        return;  // the rerun before rendered nothing: the flags stand
-    }
-    const unsigned lane = threadIdx.x & 63u;
-    const unsigned k = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    if (k >= G.K) return;  // the same for the whole wavefront
-    if (k == 0) {
-        if (lane == 0) G.flags[0] = 0;
-        return;
-    }
-    State *first = &G.st_blk[(unsigned long long)k * G.seg];
-    const State *prev = &G.st_end[k - 1];
-    bool diff = false;
-    constexpr bool kWords = sizeof(State) % 4 == 0 && alignof(State) >= 4;
-    constexpr unsigned n = kWords ? sizeof(State) / 4 : sizeof(State);
-    if constexpr (kWords) {
-        for (unsigned i = lane; i < n; i += 64) diff = diff || ((const unsigned *)first)[i] != ((const unsigned *)prev)[i];
-    } else {
-        for (unsigned i = lane; i < n; i += 64)
-            diff = diff || ((const unsigned char *)first)[i] != ((const unsigned char *)prev)[i];
-    }
-    const bool any = __any(diff) != 0;
-    if (lane == 0) G.flags[k] = any ? 1 : 0;
-    if (!any) return;
-    if (lane == 0) atomicAdd(&G.stats[G.pass], 1u);
-    if (G.mode) {
-        if constexpr (kWords) {
-            for (unsigned i = lane; i < n; i += 64) ((unsigned *)first)[i] = ((const unsigned *)prev)[i];
-        } else {
-            for (unsigned i = lane; i < n; i += 64) ((unsigned char *)first)[i] = ((const unsigned char *)prev)[i];
-        }
-        if (lane == 0) G.list[atomicAdd(G.count, 1u)] = k;
-    }
-}
-// the walk: one workgroup, segments in order; a segment is looked at when the
-// last check flagged it or its predecessor's final State changed here; one
-// whose first block's State differs is rendered serially from its
-// predecessor's final State (thread 0 runs the callback on an LDS double
-// buffer, the other waves stage blocks in and out, as dspb_stateful_lds)
-// until its State meets the recorded one.  Then the live State = the last
-// segment's final State.
-template <unsigned CC, unsigned NB_>
-__device__ static void dspb_seg_walk(const dspb_seg_args &G) {
-    extern __shared__ float dspb_lbuf[];
-    __shared__ unsigned s_next;
-    __shared__ int s_bad, s_stop;
-    __shared__ unsigned long long s_prev[(sizeof(State) + 7) / 8];  // the predecessor's final State
-    const dspb_render_args &A = G.R;
-    const unsigned B = NB_ ? NB_ : A.B, C = CC ? CC : A.C, CB = C * B, t = threadIdx.x, nt = blockDim.x;
-    float *buf0 = dspb_lbuf, *buf1 = dspb_lbuf + CB;
-    Parameters prm = dspb_from_global<Parameters>(A.P);
-    State local;
-    bool prev_ended = false;  // s_prev holds a final State the walk rendered
-    unsigned reruns = 0;
-    for (unsigned k = 1; k < G.K; ++k) {
-        if (!prev_ended) {  // the next flagged segment at or after k
-            unsigned found = G.K;
-            for (unsigned c0 = k; c0 < G.K && found == G.K; c0 += nt) {
-                if (t == 0) s_next = G.K;
-                __syncthreads();
-                if (c0 + t < G.K && G.flags[c0 + t]) atomicMin(&s_next, c0 + t);
-                __syncthreads();
-                found = s_next;
-                __syncthreads();
-            }
-            if (found >= G.K) break;
-            k = found;
-            for (unsigned i = t; i < sizeof(State); i += nt)
-                ((unsigned char *)s_prev)[i] = ((const unsigned char *)&G.st_end[k - 1])[i];
-        }
-        const unsigned long long b0 = (unsigned long long)k * G.seg;
-        const unsigned long long b1 = b0 + G.seg < A.nblocks ? b0 + G.seg : A.nblocks;
-        if (t == 0) s_bad = 0;
-        __syncthreads();
-        for (unsigned i = t; i < sizeof(State); i += nt)
-            if (((const unsigned char *)s_prev)[i] != ((const unsigned char *)&G.st_blk[b0])[i]) s_bad = 1;
-        __syncthreads();
-        prev_ended = false;
-        if (s_bad) {
-            ++reruns;
-            dspb_copy_state((void *)&local, (const void *)s_prev);
-            dspb_stage_in(A, b0, buf0, t, nt);
-            __syncthreads();
-            unsigned long long b = b0;
-            bool ended = true;
-            for (; b < b1; ++b) {
-                float *cur = ((b - b0) & 1) ? buf1 : buf0, *oth = ((b - b0) & 1) ? buf0 : buf1;
-                if (t == 0) {  // does the chain meet the recorded one here?
-                    s_stop = (b > b0 && dspb_same_state(&local, &G.st_blk[b])) ? 1 : 0;
-                    if (!s_stop) dspb_copy_state((void *)&G.st_blk[b], (const void *)&local);
-                }
-                __syncthreads();
-                if (s_stop) {
-                    ended = false;
-                    break;
-                }
-                if (t == 0) {
-                    float *ptrs[CC ? CC : 16];
-                    for (unsigned c = 0; c < C; ++c) ptrs[c] = cur + c * B;
-                    audio_callback(prm, local, ptrs, C, B, A.sr);
-                } else if (t >= 64) {
-                    if (b > b0) dspb_stage_out(A, b - 1, oth, t - 64, nt - 64);
-                    if (b + 1 < b1) dspb_stage_in(A, b + 1, oth, t - 64, nt - 64);
-                }
-                __syncthreads();
-            }
-            // the last block rendered here
-            dspb_stage_out(A, b - 1, ((b - 1 - b0) & 1) ? buf1 : buf0, t, nt);
-            if (ended && t == 0) {
-                dspb_copy_state((void *)s_prev, (const void *)&local);
-                dspb_copy_state((void *)&G.st_end[k], (const void *)&local);
-            }
-            prev_ended = ended;
-            __syncthreads();
-        }
-    }
-    __syncthreads();
-    if (t == 0) G.stats[7] = reruns;
-    // the live State: the last segment's final State (s_prev when the walk
-    // rendered it to its end, else st_end as pass 1 / a rerun left it)
-    const unsigned char *last = prev_ended ? (const unsigned char *)s_prev
-                                           : (const unsigned char *)&G.st_end[G.K - 1];
-    for (unsigned i = t; i < sizeof(State); i += nt) ((unsigned char *)A.S)[i] = last[i];
-}
-#define DSPB_WALK_KERNEL(name, CC, BB)                                                 \
-    extern "C" __global__ __launch_bounds__(256) void name(dspb_seg_args G) { dspb_seg_walk<CC, BB>(G); }
-DSPB_WALK_KERNEL(dspb_seg_walk_c2b512, 2, 512)
-DSPB_WALK_KERNEL(dspb_seg_walk_any, 0, 0)
-
-// compute_IR (plugin.cpp:17-58): the callback once, on buffers as they are
-extern "C" __global__ void dspb_callback(dspb_render_args A) {
-    float *ptrs[16];
-    for (unsigned c = 0; c < A.C; ++c) ptrs[c] = A.out[c];
-    audio_callback(*(Parameters *)A.P, *(State *)A.S, ptrs, A.C, A.B, A.sr);
-}
-)DSPB";
+// kDriver: the driver kernels (csrc/plugin_driver.inl, plugin_driver_seg.inl), as one string
+#include "plugin_driver_src.inc"
 
 struct ArenaHost {  // mirror of dspb_arena
     char *base;

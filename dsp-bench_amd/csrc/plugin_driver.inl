@@ -1,0 +1,435 @@
+// plugin_driver.inl -- the driver kernels compiled into every plugin module
+// (csrc/module.cpp dsp_module_compile: after the plugin source and its
+// descriptor, in one hiprtc translation unit for gfx950).  A source fragment,
+// not a translation unit of the library: it uses the plugin's Parameters,
+// State and audio_callback.  Embedded as a string by the Makefile
+// (build/gen/plugin_driver_src.inc); the host mirrors of its argument blocks
+// are module.cpp's RenderArgsG / SegArgsG.
+struct dspb_render_args {
+    void *P;
+    void *S;
+    float *in[16];
+    float *out[16];
+    unsigned long long L;
+    unsigned long long nblocks;
+    unsigned long long block0;
+    unsigned in_ch;
+    unsigned C;
+    unsigned B;
+    float sr;
+    unsigned lds;
+    unsigned lds_nb;
+    unsigned lds_stride;
+    unsigned par;
+};
+extern "C" __global__ void dspb_sizes(unsigned *o) {
+    o[0] = sizeof(Parameters);
+    o[1] = sizeof(State);
+    o[2] = __is_empty(State) ? 1u : 0u;
+}
+extern "C" __global__ void dspb_defaults(Parameters *p) { *p = default_parameters(); }
+// non-const lvalues, as the reference's generated wrappers pass them
+// (compiler.cpp:1181-1203): plugins may take Parameters& or const Parameters&
+extern "C" __global__ void dspb_init(Parameters *p, State *s, unsigned C, float sr, dspb_arena *a) {
+    *s = initialize_state(*p, C, sr, (void *)a);
+}
+// one block: the render_audio body (audio.cpp:13-175), one-shot
+__device__ static void dspb_block(const dspb_render_args &A, unsigned long long b, State &st) {
+    float *ptrs[16];
+    const unsigned long long s0 = (A.block0 + b) * A.B;  // global sample of the block
+    for (unsigned c = 0; c < A.C; ++c) {
+        ptrs[c] = A.out[c] + b * A.B;
+        for (unsigned s = 0; s < A.B; ++s) {
+            const unsigned long long i = b * A.B + s;
+            ptrs[c][s] = (c < A.in_ch && i < A.L) ? A.in[c][i] : 0.0f;
+        }
+    }
+    (void)s0;
+    audio_callback(*(Parameters *)A.P, st, ptrs, A.C, A.B, A.sr);
+}
+// render_audio's copy of block b into a staging buffer (zero past EOF and
+// for the channels the file lacks), element j of every (n0 + k*nt) stride
+__device__ static void dspb_stage_in(const dspb_render_args &A, unsigned long long b, float *buf, unsigned j0,
+                                     unsigned nt) {
+    const unsigned CB = A.C * A.B;
+    for (unsigned j = j0; j < CB; j += nt) {
+        const unsigned c = j / A.B, s = j - c * A.B;
+        const unsigned long long i = b * A.B + s;
+        buf[j] = (c < A.in_ch && i < A.L) ? A.in[c][i] : 0.0f;
+    }
+}
+__device__ static void dspb_stage_out(const dspb_render_args &A, unsigned long long b, const float *buf,
+                                      unsigned j0, unsigned nt) {
+    const unsigned CB = A.C * A.B;
+    for (unsigned j = j0; j < CB; j += nt) {
+        const unsigned c = j / A.B, s = j - c * A.B;
+        A.out[c][b * A.B + s] = buf[j];
+    }
+}
+typedef __attribute__((address_space(1))) float dspb_gfloat;
+// the Parameters / State blobs, read through a global-address-space pointer:
+// a copy the compiler forwards to the source then reads global memory, which
+// the callback's LDS stores cannot alias -- so a field the callback reads
+// every sample (gain_test's gain, IR_test's step) stays in a register
+// instead of being reloaded through a flat pointer after every store
+template <class T> __device__ static inline T dspb_from_global(const void *p) {
+    return *(const __attribute__((address_space(1))) T *)p;
+}
+// the State of a parallel render: empty, or one the callback never writes
+// (dsp_module_facts: proven from the callback's IR, with no global memory
+// written).  Each lane calls the
+// callback with a private copy when the State is small (its fields then stay
+// in registers), else with the shared blob itself (read only).
+template <bool kSmall = (sizeof(State) <= 256)> struct dspb_ro_state {
+    State s;
+    __device__ explicit dspb_ro_state(const void *p) : s(dspb_from_global<State>(p)) {}
+    __device__ State &get() { return s; }
+};
+template <> struct dspb_ro_state<false> {
+    State *s;
+    __device__ explicit dspb_ro_state(const void *p) : s((State *)p) {}
+    __device__ State &get() { return *s; }
+};
+// a generic pointer the compiler can prove is global memory (global_load /
+// global_store in the inlined callback, not flat ops that also wait on LDS)
+__device__ static inline float *dspb_global(float *p) { return (float *)(dspb_gfloat *)p; }
+// no state: one wavefront renders 64 consecutive blocks. render_audio's copy
+// (audio.cpp:13-175: the file at the cursor, zeros past EOF and for the
+// channels the file lacks) runs first for all 64 blocks at once, coalesced
+// per channel, four loads in flight per lane before their stores (in == out
+// is allowed: every element is stored where it was loaded). Then lane t runs
+// the callback in place on block t. CC > 0 makes the channel count a
+// constant, so the callback's channel loops unroll and its pointer table
+// lives in registers instead of scratch.
+template <unsigned CC>
+__device__ static void dspb_stateless(const dspb_render_args &A) {
+    dspb_ro_state<> local(A.S);
+    // a private copy: the callback's stores cannot alias it, so its fields
+    // stay in registers instead of being reloaded after every store
+    Parameters prm = dspb_from_global<Parameters>(A.P);
+    const unsigned C = CC ? CC : A.C, t = threadIdx.x;
+    for (unsigned long long b0 = (unsigned long long)blockIdx.x * 64; b0 < A.nblocks;
+         b0 += (unsigned long long)gridDim.x * 64) {
+        const unsigned long long nb = A.nblocks - b0 < 64 ? A.nblocks - b0 : 64;
+        const unsigned long long i0 = b0 * A.B, n = nb * A.B;
+        const unsigned long long lim = A.L > i0 ? A.L - i0 : 0;  // file samples left at i0
+        for (unsigned c = 0; c < C; ++c) {
+            dspb_gfloat *o = (dspb_gfloat *)A.out[c] + i0;
+            const dspb_gfloat *x = (const dspb_gfloat *)A.in[c < A.in_ch ? c : 0] + i0;
+            const unsigned long long m = c < A.in_ch ? (lim < n ? lim : n) : 0;  // copied, the rest zeroed
+            unsigned long long j = t;
+            for (; j + 192 < m; j += 256) {
+                const float v0 = x[j], v1 = x[j + 64], v2 = x[j + 128], v3 = x[j + 192];
+                o[j] = v0;
+                o[j + 64] = v1;
+                o[j + 128] = v2;
+                o[j + 192] = v3;
+            }
+            for (; j < m; j += 64) o[j] = x[j];
+            for (j = m + ((t - m) & 63); j < n; j += 64) o[j] = 0.0f;
+        }
+        __syncthreads();  // the wave's copies are visible to every lane
+        if (t < nb) {
+            float *ptrs[CC ? CC : 16];
+            for (unsigned c = 0; c < C; ++c) ptrs[c] = dspb_global(A.out[c] + (i0 + (unsigned long long)t * A.B));
+            audio_callback(prm, local.get(), ptrs, C, A.B, A.sr);
+        }
+        __syncthreads();
+    }
+}
+// stateful, in order: thread 0 runs the callback on block b in LDS while
+// waves 1.. write block b - 1 out and stage block b + 1 in the other half of
+// the double buffer (the same elements per thread, so no element is
+// overwritten before it is written out). Thread 0 keeps Parameters and a
+// small State in private copies (written back at the end): the callback's
+// LDS stores cannot alias them, so they stay in registers. CC as above.
+template <unsigned CC, unsigned NB = 0>
+__device__ static void dspb_stateful_lds(const dspb_render_args &A) {
+    extern __shared__ float dspb_lbuf[];
+    const unsigned B = NB ? NB : A.B;
+    const unsigned C = CC ? CC : A.C, CB = C * B, t = threadIdx.x, nt = blockDim.x;
+    float *buf0 = dspb_lbuf, *buf1 = dspb_lbuf + CB;
+    dspb_stage_in(A, 0, buf0, t, nt);
+    __syncthreads();
+    constexpr bool kLocal = sizeof(State) <= 256;
+    State *gst = (State *)A.S;
+    // copies made by every thread (a few hundred bytes at most), used by
+    // thread 0; the blobs are plain bytes to the host, as in the reference
+    Parameters prm = dspb_from_global<Parameters>(A.P);
+    State local = *gst;
+    for (unsigned long long b = 0; b < A.nblocks; ++b) {
+        float *cur = (b & 1) ? buf1 : buf0, *oth = (b & 1) ? buf0 : buf1;
+        if (t == 0) {
+            float *ptrs[CC ? CC : 16];
+            for (unsigned c = 0; c < C; ++c) ptrs[c] = cur + c * B;
+            if constexpr (kLocal) audio_callback(prm, local, ptrs, C, B, A.sr);
+            else audio_callback(prm, *gst, ptrs, C, B, A.sr);
+        } else if (t >= 64) {
+            if (b > 0) dspb_stage_out(A, b - 1, oth, t - 64, nt - 64);
+            if (b + 1 < A.nblocks) dspb_stage_in(A, b + 1, oth, t - 64, nt - 64);
+        }
+        __syncthreads();
+    }
+    if constexpr (kLocal) {
+        if (t == 0) __builtin_memcpy((void *)gst, (const void *)&local, sizeof(State));
+    }
+    dspb_stage_out(A, A.nblocks - 1, (A.nblocks - 1) & 1 ? buf1 : buf0, t, nt);
+}
+// no state, LDS blocks: a workgroup renders lds_nb consecutive blocks per
+// round.  render_audio's copy (audio.cpp:13-175: the file at the cursor,
+// zeros past EOF and for the channels the file lacks) stages them into LDS
+// with all 256 threads, coalesced per channel; then the lanes of wave 0 run
+// the callback on one block each, in LDS (a block's rows at a stride of
+// C B + 1 floats: the lanes of one ds_read hit different banks); then all
+// threads copy the blocks out, coalesced.  The
+// callback's sample loop addresses one LDS base at constant offsets when C
+// and B are constants (CC, BB), so its loads run ahead of its stores.  Two
+// workgroups per CU: one stages while the other runs callbacks.
+template <unsigned CC, unsigned BB>
+__device__ static void dspb_stateless_lds(const dspb_render_args &A) {
+    extern __shared__ float dspb_lbuf[];
+    dspb_ro_state<> local(A.S);
+    Parameters prm = dspb_from_global<Parameters>(A.P);
+    const unsigned C = CC ? CC : A.C, B = BB ? BB : A.B, NB = A.lds_nb, SB = A.lds_stride;
+    const unsigned t = threadIdx.x, nt = blockDim.x;
+    for (unsigned long long b0 = (unsigned long long)blockIdx.x * NB; b0 < A.nblocks;
+         b0 += (unsigned long long)gridDim.x * NB) {
+        const unsigned nb = (unsigned)(A.nblocks - b0 < NB ? A.nblocks - b0 : NB);
+        const unsigned long long i0 = b0 * B;
+        const unsigned long long lim = A.L > i0 ? A.L - i0 : 0;  // file samples left at i0
+        const unsigned n = nb * B;
+        for (unsigned c = 0; c < C; ++c) {
+            const dspb_gfloat *x = (const dspb_gfloat *)A.in[c < A.in_ch ? c : 0] + i0;
+            const unsigned long long m = c < A.in_ch ? lim : 0;
+            float *row = dspb_lbuf + c * B;
+            if (m >= n && (B & 3) == 0 && (((unsigned long long)x) & 15) == 0) {
+                // the whole round is inside the file: 16-byte loads, two in
+                // flight per thread (a float4 never crosses a block: 4 | B)
+                const __attribute__((address_space(1))) float4 *x4 =
+                    (const __attribute__((address_space(1))) float4 *)x;
+                unsigned j = 4 * t;
+                for (; j + 4 * nt < n; j += 8 * nt) {
+                    const float4 v0 = x4[j / 4], v1 = x4[(j + 4 * nt) / 4];
+                    unsigned q = j / B;
+                    float *d = row + q * SB + (j - q * B);
+                    d[0] = v0.x, d[1] = v0.y, d[2] = v0.z, d[3] = v0.w;
+                    q = (j + 4 * nt) / B;
+                    d = row + q * SB + (j + 4 * nt - q * B);
+                    d[0] = v1.x, d[1] = v1.y, d[2] = v1.z, d[3] = v1.w;
+                }
+                for (; j < n; j += 4 * nt) {
+                    const float4 v0 = x4[j / 4];
+                    const unsigned q = j / B;
+                    float *d = row + q * SB + (j - q * B);
+                    d[0] = v0.x, d[1] = v0.y, d[2] = v0.z, d[3] = v0.w;
+                }
+            } else {  // EOF in the round, or no file channel: zeros past it
+                for (unsigned j = t; j < n; j += nt) {
+                    const unsigned q = j / B;
+                    row[q * SB + (j - q * B)] = j < m ? x[j] : 0.0f;
+                }
+            }
+        }
+        __syncthreads();
+        // one wave, one block per lane (an LDS instruction costs its cycles
+        // whatever the active lanes, so the callbacks share as few as possible)
+        if (t < nb) {
+            float *blk = dspb_lbuf + t * SB;
+            float *ptrs[CC ? CC : 16];
+            for (unsigned c = 0; c < C; ++c) ptrs[c] = blk + c * B;
+            audio_callback(prm, local.get(), ptrs, C, B, A.sr);
+        }
+        __syncthreads();
+        for (unsigned c = 0; c < C; ++c) {
+            dspb_gfloat *o = (dspb_gfloat *)A.out[c] + i0;
+            const float *row = dspb_lbuf + c * B;
+            if ((B & 3) == 0 && (((unsigned long long)o) & 15) == 0) {
+                __attribute__((address_space(1))) float4 *o4 = (__attribute__((address_space(1))) float4 *)o;
+                for (unsigned j = 4 * t; j < n; j += 4 * nt) {
+                    const unsigned q = j / B;
+                    const float *d = row + q * SB + (j - q * B);
+                    o4[j / 4] = make_float4(d[0], d[1], d[2], d[3]);
+                }
+            } else {
+                for (unsigned j = t; j < n; j += nt) {
+                    const unsigned q = j / B;
+                    o[j] = row[q * SB + (j - q * B)];
+                }
+            }
+        }
+        __syncthreads();
+    }
+}
+// blocks per round of the LDS-blocks path at a block stride of SB floats, a
+// multiple of 4 (18 blocks of stereo B = 512 instead of 16 made the
+// stateless rounds 1-6% slower, profiles/r05_lds_nb_ab.txt), and lanes of
+// the segment kernels: as many as the round's LDS holds (18 instead of 16:
+// 15% faster).  The host computes the same (module_render, module_render_seg)
+constexpr unsigned dspb_lds_nb(unsigned SB) {
+    const unsigned v = DSPB_LDS_ROUND_BYTES / (SB * 4u) / 4u * 4u;
+    return v < 64u ? v : 64u;
+}
+constexpr unsigned dspb_seg_nb(unsigned SB) {
+    const unsigned v = DSPB_LDS_ROUND_BYTES / (SB * 4u);
+    return v < 64u ? v : 64u;
+}
+// the LDS-blocks path for a constant shape (C, B, 4 | B), software
+// pipelined over the workgroup's rounds: a persistent grid of two
+// workgroups per CU walks the file, and while round r's callbacks run in LDS,
+// the next round's file samples are already in flight into registers (16-byte
+// loads, all issued at once), so a round costs its callbacks and one copy
+// out, not a chain of dependent HBM loads.  Rounds the file does not cover
+// completely (EOF, the ragged last round) or an unaligned file take
+// render_audio's copy with zeros instead.  Block rows at a stride of C B + 2
+// floats: 8-byte aligned (the copies move float2 pairs through LDS, 16-byte
+// rows to and from HBM) and conflict-free for the 16 callback lanes of a
+// stereo B = 512 round.
+template <unsigned CC, unsigned BB>
+__device__ static void dspb_stateless_lds_pf(const dspb_render_args &A) {
+    extern __shared__ float dspb_lbuf[];
+    constexpr unsigned C = CC, B = BB, SB = C * B + 2u, NB = dspb_lds_nb(SB);
+    constexpr unsigned N4 = NB * B / 4u, PT = (N4 + 255u) / 256u;  // float4 per channel per round / per thread
+    static_assert(NB <= 64 && B % 4 == 0, "one wave runs a round's callbacks");
+    typedef __attribute__((address_space(1))) float4 gfloat4;
+    dspb_ro_state<> local(A.S);
+    Parameters prm = dspb_from_global<Parameters>(A.P);
+    const unsigned t = threadIdx.x, lane = t & 63u;
+    const unsigned long long stride = (unsigned long long)gridDim.x * NB;
+    bool aligned_in = true;
+    for (unsigned c = 0; c < C && c < A.in_ch; ++c) aligned_in = aligned_in && !(((unsigned long long)A.in[c]) & 15);
+    auto full = [&](unsigned long long b0) {
+        return b0 + NB <= A.nblocks && (A.in_ch == 0 || ((b0 + NB) * B <= A.L && aligned_in));
+    };
+    float4 pf[C][PT];
+    auto load = [&](unsigned long long b0) {
+#pragma unroll
+        for (unsigned c = 0; c < C; ++c) {
+            const gfloat4 *x4 = (const gfloat4 *)(A.in[c < A.in_ch ? c : 0] + b0 * B);
+#pragma unroll
+            for (unsigned k = 0; k < PT; ++k) {
+                const unsigned i = t + 256u * k;
+                if (c < A.in_ch && (N4 % 256u == 0 || i < N4)) {
+                    const float4 v = x4[i];
+                    pf[c][k] = v;
+                } else {
+                    pf[c][k] = make_float4(0.f, 0.f, 0.f, 0.f);
+                }
+            }
+        }
+    };
+    unsigned long long b0 = (unsigned long long)blockIdx.x * NB;
+    bool have = b0 < A.nblocks && full(b0);
+    if (have) load(b0);
+    for (; b0 < A.nblocks; b0 += stride) {
+        const unsigned nb = (unsigned)(A.nblocks - b0 < NB ? A.nblocks - b0 : NB);
+        const unsigned long long i0 = b0 * B;
+        const unsigned n = nb * B;
+        if (have) {
+#pragma unroll
+            for (unsigned c = 0; c < C; ++c) {
+#pragma unroll
+                for (unsigned k = 0; k < PT; ++k) {
+                    const unsigned j = 4u * (t + 256u * k);
+                    if (N4 % 256u == 0 || j < 4u * N4) {
+                        float2 *d = (float2 *)(dspb_lbuf + (j / B) * SB + c * B + j % B);
+                        d[0] = make_float2(pf[c][k].x, pf[c][k].y);
+                        d[1] = make_float2(pf[c][k].z, pf[c][k].w);
+                    }
+                }
+            }
+        } else {  // render_audio's copy with zeros past EOF and for missing channels
+            const unsigned long long lim = A.L > i0 ? A.L - i0 : 0;
+            for (unsigned c = 0; c < C; ++c) {
+                const dspb_gfloat *x = (const dspb_gfloat *)A.in[c < A.in_ch ? c : 0] + i0;
+                const unsigned long long m = c < A.in_ch ? lim : 0;
+                for (unsigned j = t; j < n; j += 256u) dspb_lbuf[(j / B) * SB + c * B + j % B] = j < m ? x[j] : 0.0f;
+            }
+        }
+        __syncthreads();
+        // the next round's loads fly while this round's callbacks run
+        have = b0 + stride < A.nblocks && full(b0 + stride);
+        if (have) load(b0 + stride);
+        // one wave, one block per lane: an LDS instruction costs its cycles
+        // whatever the active lanes, so the callbacks share as few as possible
+        if (t < nb) {
+            float *blk = dspb_lbuf + lane * SB;
+            float *ptrs[C];
+            for (unsigned c = 0; c < C; ++c) ptrs[c] = blk + c * B;
+            audio_callback(prm, local.get(), ptrs, C, B, A.sr);
+        }
+        __syncthreads();
+        for (unsigned c = 0; c < C; ++c) {
+            if ((((unsigned long long)A.out[c]) & 15) == 0) {
+                gfloat4 *o4 = (gfloat4 *)(A.out[c] + i0);
+#pragma unroll 4
+                for (unsigned j = 4u * t; j < n; j += 1024u) {
+                    const float2 *d = (const float2 *)(dspb_lbuf + (j / B) * SB + c * B + j % B);
+                    const float2 lo = d[0], hi = d[1];
+                    o4[j / 4u] = make_float4(lo.x, lo.y, hi.x, hi.y);
+                }
+            } else {
+                dspb_gfloat *o = (dspb_gfloat *)A.out[c] + i0;
+                for (unsigned j = t; j < n; j += 256u) o[j] = dspb_lbuf[(j / B) * SB + c * B + j % B];
+            }
+        }
+        __syncthreads();
+    }
+}
+// the LDS-blocks path: four waves, two workgroups per CU, one kernel per
+// (C, B) instantiation (the host picks it).  Kept apart, each kernel's
+// register budget is its own: with all instantiations behind one dispatch the
+// scheduler held the callback to one LDS round trip per sample pair (a ds_read
+// waited on the previous ds_write) to keep the whole kernel under 64 VGPRs.
+// Constant shapes with 4 | B take the pipelined rounds (dspb_stateless_lds_pf).
+#define DSPB_LDS_KERNEL(name, CC, BB)                                                  \
+    extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) void name(  \
+        dspb_render_args A) {                                                          \
+        if (A.par) {                                                                   \
+            if constexpr (CC > 0 && BB > 0 && BB % 4 == 0) dspb_stateless_lds_pf<CC, BB>(A); \
+            else dspb_stateless_lds<CC, BB>(A);                                        \
+        }                                                                              \
+    }
+DSPB_LDS_KERNEL(dspb_render_lds_c2b512, 2, 512)
+DSPB_LDS_KERNEL(dspb_render_lds_c2b256, 2, 256)
+DSPB_LDS_KERNEL(dspb_render_lds_c2b1024, 2, 1024)
+DSPB_LDS_KERNEL(dspb_render_lds_c1b512, 1, 512)
+DSPB_LDS_KERNEL(dspb_render_lds_c1, 1, 0)
+DSPB_LDS_KERNEL(dspb_render_lds_c2, 2, 0)
+DSPB_LDS_KERNEL(dspb_render_lds, 0, 0)
+extern "C" __global__ void dspb_render(dspb_render_args A) {
+    extern __shared__ float dspb_lbuf[];
+    if (A.par) {
+        if (A.C == 1) dspb_stateless<1>(A);
+        else if (A.C == 2) dspb_stateless<2>(A);
+        else dspb_stateless<0>(A);
+    } else if (!A.lds) {  // stateful, blocks too large for LDS: in order, one thread
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            State &st = *(State *)A.S;
+            for (unsigned long long b = 0; b < A.nblocks; ++b) dspb_block(A, b, st);
+        }
+    } else if (blockIdx.x == 0) {
+        // B = 512 stereo as constants too: the callback's sample loop then
+        // addresses one LDS base at constant offsets, so its loads can run
+        // ahead of its stores instead of waiting a round trip per sample
+        // (512: the render configs; 256: BASELINE configs[0], the reference
+        // device's forced stereo)
+        if (A.C == 2 && A.B == 512) dspb_stateful_lds<2, 512>(A);
+        else if (A.C == 2 && A.B == 256) dspb_stateful_lds<2, 256>(A);
+        else if (A.C == 1) dspb_stateful_lds<1>(A);
+        else if (A.C == 2) dspb_stateful_lds<2>(A);
+        else dspb_stateful_lds<0>(A);
+    }
+}
+// the stateful LDS path's common shapes as kernels of their own (as the
+// LDS-blocks kernels above: a register budget of their own, so the callback's
+// LDS loads can run ahead of its stores)
+#define DSPB_ST_KERNEL(name, CC, BB)                                                   \
+    extern "C" __global__ void name(dspb_render_args A) {                              \
+        extern __shared__ float dspb_lbuf[];                                           \
+        if (!A.par && blockIdx.x == 0) dspb_stateful_lds<CC, BB>(A);                   \
+    }
+DSPB_ST_KERNEL(dspb_render_st_c2b512, 2, 512)
+DSPB_ST_KERNEL(dspb_render_st_c2b256, 2, 256)
+DSPB_ST_KERNEL(dspb_render_st_c1, 1, 0)
+DSPB_ST_KERNEL(dspb_render_st_c2, 2, 0)
+
