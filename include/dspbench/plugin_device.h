@@ -151,9 +151,12 @@ static inline void phasor_32_array(real32 *out, real32 ampl, real32 freq, i32 n,
 }
 static inline void random_uniform_32_array(real32 *out, i32 n, void *rng) { (void)out; (void)n; (void)rng; }
 
+/* ippsCopy_32f (dsp.cpp:171-173) copies between vectors that do not overlap
+   (overlapping ones are ippsMove's): a forward copy, with no comparison of
+   the two addresses -- one would keep the callback's IR analysis from
+   concluding anything (a block address compared) */
 static inline void copy_array(real32 *in, real32 *out, i32 n) {
-    if (out < in) for (i32 i = 0; i < n; ++i) out[i] = in[i];
-    else for (i32 i = n - 1; i >= 0; --i) out[i] = in[i];
+    for (i32 i = 0; i < n; ++i) out[i] = in[i];
 }
 static inline void set_array(real32 v, real32 *out, i32 n) { for (i32 i = 0; i < n; ++i) out[i] = v; }
 static inline void zero_array(real32 *out, i32 n) { for (i32 i = 0; i < n; ++i) out[i] = 0.0f; }

@@ -339,6 +339,21 @@ void audio_callback(const Parameters& p, State& st, float** out, const u32 C, co
         st.pos += 3u;
     }
 }''',
+    # the plugin services on the block (copy_array, gain_ip_32_array): the
+    # block's last 64 samples held in the State and played at the start of the
+    # next block (forgets after one block)
+    "service_copy": r'''
+struct State { float prev[2][64]; };
+State initialize_state(const Parameters& p, const unsigned C, const float sr, void* ctx) { State s = {}; return s; }
+void audio_callback(const Parameters& p, State& st, float** out, const u32 C, const u32 B, const real32 sr) {
+    for (u32 c = 0; c < C && c < 2; ++c) {
+        float t[64];
+        copy_array(out[c] + (B - 64), t, 64);
+        gain_ip_32_array(out[c] + 64, p.b, B - 64);
+        copy_array(st.prev[c], out[c], 64);
+        copy_array(t, st.prev[c], 64);
+    }
+}''',
     # a one-pole whose coefficient is read from a mutable-looking State field
     # the callback also rewrites (the same value every block)
     "self_coef": r'''
