@@ -968,10 +968,14 @@ static int module_render_seg(dsp_module *m, RenderArgsG &A, hipStream_t s) {
         W.blk = W.end = nullptr, W.list = nullptr, W.flags = nullptr, W.cap = 0, W.cap_blk = 0;
         const uint32_t cap = (uint32_t)std::max<uint64_t>(K, 1024);
         const uint64_t cap_blk = std::max<uint64_t>(A.nblocks, 4096);
-        MOD_HIP(hipMalloc(&W.blk, cap_blk * m->state_size));
-        MOD_HIP(hipMalloc(&W.end, (uint64_t)cap * m->state_size));
-        MOD_HIP(hipMalloc(&W.list, cap * sizeof(unsigned)));
-        MOD_HIP(hipMalloc(&W.flags, cap));
+        if (hipMalloc(&W.blk, cap_blk * m->state_size) != hipSuccess ||
+            hipMalloc(&W.end, (uint64_t)cap * m->state_size) != hipSuccess ||
+            hipMalloc(&W.list, cap * sizeof(unsigned)) != hipSuccess || hipMalloc(&W.flags, cap) != hipSuccess) {
+            (void)hipGetLastError();  // no room for the records: the serial chain renders this call
+            for (void *p : {W.blk, W.end, (void *)W.list, (void *)W.flags}) if (p) (void)hipFree(p);
+            W.blk = W.end = nullptr, W.list = nullptr, W.flags = nullptr;
+            return 1;
+        }
         W.cap = cap;
         W.cap_blk = cap_blk;
     }
