@@ -978,8 +978,9 @@ def main():
                             "the serial chain: one lane runs the callback block after block (a State written "
                             "every block); DESIGN 4.6" if wl in ("biquad_src", "sine_src") and
                             (args.serial_state or not (state_segments or {}).get("used")) else
-                            "segments: one lane per segment runs the callback block after block, 16 lanes per "
-                            "64 KB workgroup round (the LDS-blocks driver's capacity); DESIGN 4.6"
+                            "segments: one lane per segment runs the callback's own chain block after block; "
+                            "the lanes are the blocks LDS holds (18 per 76 KB workgroup, 36 per CU), so the rounds "
+                            "(blocks per segment + warm-up) bound it; DESIGN 4.6"
                             if wl in ("biquad_src", "sine_src") else
                             "the render (LDS-capacity-bound callbacks) then the power-capped memory STFT, "
                             "serial: DESIGN 4.6, profiles/r02_generic_stft_schedules.txt"
