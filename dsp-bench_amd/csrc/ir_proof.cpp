@@ -558,6 +558,9 @@ struct Analysis {
                 continue;
             }
             if (I.op != "phi") return -1;
+            // an i8 / i16 counter can wrap inside one run of its loop (distinct
+            // values only up to 2^N iterations): i32 and i64 only
+            if (!starts_with(I.text, "i32 ") && !starts_with(I.text, "i64 ")) return -1;
             int li = -1;
             for (size_t k = 0; k < loops_.size(); ++k)
                 if (loops_[k].header == I.blk) li = (int)k;

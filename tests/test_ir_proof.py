@@ -104,6 +104,10 @@ GT_SNIPPETS = {
     # a cycle entered in its middle (no natural loop): refused whatever the index
     "irreducible_goto": ("u32 s = 0; if (C > 1) goto mid; top: out[0][s] *= p.g; mid: ++s; if (s < B) goto top;",
                          False),
+    # an 8-bit index wraps within one run of its loop (B > 256 stores an
+    # element twice): only i32 / i64 counters are induction variables
+    "wrapping_u8_index": ("unsigned char i = 0; for (u32 n = 0; n < B; ++n, ++i) out[0][i] *= p.g;", False),
+    "u32_index_same_loop": ("unsigned i = 0; for (u32 n = 0; n < B; ++n, ++i) out[0][i] *= p.g;", True),
 }
 
 
