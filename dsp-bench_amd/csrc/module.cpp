@@ -888,9 +888,9 @@ static int check_device(const dsp_module *m) {
 // landed (a render never waits for them).
 int module_seg_collect(dsp_module *m, bool wait) {
     auto &W = m->seg;
+    const int older = W.seq[0] < W.seq[1] ? 0 : 1;  // the older slot first
     for (int pass = 0; pass < 2; ++pass) {
-        // the older slot first
-        const int i = (W.pending[0] && W.pending[1]) ? (W.seq[0] < W.seq[1] ? pass : 1 - pass) : pass;
+        const int i = pass == 0 ? older : 1 - older;
         if (!W.pending[i]) continue;
         if (wait) MOD_HIP(hipEventSynchronize(W.ev[i]));
         else if (hipEventQuery(W.ev[i]) != hipSuccess) {

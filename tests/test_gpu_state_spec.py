@@ -422,3 +422,27 @@ def test_biquad_source_full_hour_bit_exact(torch_cuda):
     assert info["used"] and info["segments"] > 8000
     assert outs[0][1] == outs[1][1]
     assert torch.equal(outs[0][0].view(torch.int32), outs[1][0].view(torch.int32))
+
+
+@pytest.mark.gpu
+def test_state_spec_names_the_last_render(torch_cuda):
+    """Renders made back to back without reading the counters in between:
+    dsp_module_state_spec describes the last one (the counters of the two
+    newest renders are read oldest first; the newest was once skipped when
+    the older sat in the second slot)."""
+    torch = torch_cuda
+    mod, params = biquad_module()
+    mod.initialize_state(params, 2, 48000.0)
+    plug = mod.plugin(params)
+    xa = torch.from_numpy(noise(2, 200_000, 14)).cuda()
+    xb = torch.from_numpy(noise(2, 900_000, 15)).cuda()
+    for x in (xa, xa, xb):
+        d.render_offline(x, 2, 512, 48000.0, plug)
+    info = mod.state_spec()
+    nb = (900_000 + 511) // 512
+    assert info["used"] and info["segments"] == (nb + info["blocks_per_segment"] - 1) // info["blocks_per_segment"]
+    for x in (xb, xa):
+        d.render_offline(x, 2, 512, 48000.0, plug)
+    info = mod.state_spec()
+    nb = (200_000 + 511) // 512
+    assert info["segments"] == (nb + info["blocks_per_segment"] - 1) // info["blocks_per_segment"]
