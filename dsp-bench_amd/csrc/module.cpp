@@ -62,8 +62,16 @@ constexpr LdsShape kStShapes[4] = {{"dspb_render_st_c2b512", 2, 512}, {"dspb_ren
                                    {"dspb_render_st_c1", 1, 0}, {"dspb_render_st_c2", 2, 0}};
 // speculative segments of a stateful render (kDriver dspb_segments): pass 1 /
 // rerun kernels, most specific first, and the walk's
-constexpr LdsShape kSegShapes[4] = {{"dspb_seg_c2b512", 2, 512}, {"dspb_seg_c1", 1, 0}, {"dspb_seg_c2", 2, 0},
-                                    {"dspb_seg", 0, 0}};
+// (pass 1, its reruns; pipelined: blocks at a stride of C B + 2 and 4 | B)
+struct SegShape {
+    const char *name, *rerun;
+    uint32_t C, B;
+    bool pf;
+};
+constexpr SegShape kSegShapes[4] = {{"dspb_seg_c2b512", "dspb_seg_c2b512_rerun", 2, 512, true},
+                                    {"dspb_seg_c2", "dspb_seg_c2_rerun", 2, 0, true},
+                                    {"dspb_seg_c1", "dspb_seg_c1_rerun", 1, 0, true},
+                                    {"dspb_seg", nullptr, 0, 0, false}};
 constexpr LdsShape kWalkShapes[2] = {{"dspb_seg_walk_c2b512", 2, 512}, {"dspb_seg_walk_any", 0, 0}};
 constexpr uint32_t kSegMaxState = 1024;   // bytes of State a lane copies (the walk keeps one in LDS)
 constexpr uint32_t kSegWarm0 = 4;         // blocks of warm-up of a first render
@@ -135,7 +143,7 @@ struct dsp_module {
     hipFunction_t f_render_st[4] = {};  // kStShapes (NULL: dspb_render)
     // speculative segments (kSegShapes, the check, kWalkShapes; NULL in code
     // objects compiled before them: the serial chain)
-    hipFunction_t f_seg[4] = {}, f_seg_rerun0 = nullptr, f_seg_check = nullptr, f_seg_walk[2] = {};
+    hipFunction_t f_seg[4] = {}, f_seg_rerun[4] = {}, f_seg_check = nullptr, f_seg_walk[2] = {};
     struct SegWork {
         void *blk = nullptr;           // [cap_blk] States: st_blk
         void *end = nullptr;           // [cap] States: st_end
@@ -451,10 +459,12 @@ int dsp_module_load(const void *code, uint64_t code_size, int device, dsp_module
         }
     };
     for (int i = 0; i < 4; ++i) optional(&m->f_render_st[i], kStShapes[i].name);
-    for (int i = 0; i < 4; ++i) optional(&m->f_seg[i], kSegShapes[i].name);
+    for (int i = 0; i < 4; ++i) {
+        optional(&m->f_seg[i], kSegShapes[i].name);
+        if (kSegShapes[i].rerun) optional(&m->f_seg_rerun[i], kSegShapes[i].rerun);
+    }
     for (int i = 0; i < 2; ++i) optional(&m->f_seg_walk[i], kWalkShapes[i].name);
     optional(&m->f_seg_check, "dspb_seg_check");
-    optional(&m->f_seg_rerun0, "dspb_seg_c2b512_rerun");  // kSegShapes[0]'s reruns
     unsigned *d_o = nullptr;
     if ((e = hipMalloc(&d_o, 4 * sizeof(unsigned))) != hipSuccess) return fail(dspb::hip_fail(e, "hipMalloc"));
     void *args[] = {&d_o};
@@ -940,11 +950,15 @@ static int module_render_seg(dsp_module *m, RenderArgsG &A, hipStream_t s) {
     if (2ull * C * B * sizeof(float) > kStagedLdsBytes) return 1;  // the walk's double buffer
     hipFunction_t f = nullptr, fw = nullptr;
     int fi = -1;
-    for (int i = 0; i < 4 && !f; ++i)
-        if (m->f_seg[i] && (!kSegShapes[i].C || kSegShapes[i].C == C) && (!kSegShapes[i].B || kSegShapes[i].B == B))
-            f = m->f_seg[fi = i];
-    // the constant-shape kernel (dspb_segments_pf) strides blocks by C B + 2
-    const uint64_t stride = (uint64_t)C * B + (fi == 0 ? 2 : 1);
+    for (int i = 0; i < 4 && !f; ++i) {
+        const SegShape &sh = kSegShapes[i];
+        if (!m->f_seg[i] || (sh.C && sh.C != C) || (sh.B && sh.B != B) || (sh.pf && B % 4)) continue;
+        if (sh.rerun && !m->f_seg_rerun[i]) continue;
+        f = m->f_seg[fi = i];
+    }
+    if (!f) return 1;
+    // the pipelined kernels (dspb_segments_pf) stride blocks by C B + 2
+    const uint64_t stride = (uint64_t)C * B + (kSegShapes[fi].pf ? 2 : 1);
     // lanes per workgroup (kDriver dspb_seg_nb: the same formula)
     const uint64_t nb = std::min<uint64_t>(64, kLdsRoundBytes / (stride * sizeof(float)));
     if (nb < 4) return 1;
@@ -952,8 +966,8 @@ static int module_render_seg(dsp_module *m, RenderArgsG &A, hipStream_t s) {
         if (m->f_seg_walk[i] && (!kWalkShapes[i].C || kWalkShapes[i].C == C) &&
             (!kWalkShapes[i].B || kWalkShapes[i].B == B))
             fw = m->f_seg_walk[i];
-    if (!f || !fw || !m->f_seg_check || (fi == 0 && !m->f_seg_rerun0)) return 1;
-    hipFunction_t fr = fi == 0 ? m->f_seg_rerun0 : f;  // the reruns' kernel
+    if (!fw || !m->f_seg_check) return 1;
+    hipFunction_t fr = kSegShapes[fi].rerun ? m->f_seg_rerun[fi] : f;  // the reruns' kernel
     auto &W = m->seg;
     // segments: as many as the chip runs lanes at once (two workgroups per
     // CU, nb lanes each), kSegMinBlocks blocks at least

@@ -171,18 +171,25 @@ __device__ static void dspb_segments(const dspb_seg_args &G) {
     }
     if (k != 0xffffffffu && !stopped) dspb_copy_state((void *)&G.st_end[k], (const void *)&st);
 }
-// the same for a constant shape (C, B, 4 | B), software pipelined: round r +
-// 1's blocks are in flight into registers (16-byte loads, all issued at once)
-// while round r's callbacks run; blocks at a stride of C B + 2 floats (float2
-// LDS moves; the 16 callback lanes on distinct banks), as dspb_stateless_lds_pf
+// the same for a constant channel count and 4 | B, software pipelined: round
+// r + 1's blocks are in flight into registers (16-byte loads, all issued at
+// once) while round r's callbacks run; blocks at a stride of C B + 2 floats
+// (float2 LDS moves; the callback lanes on distinct banks), as
+// dspb_stateless_lds_pf.  BB = 0: B from the arguments (the host checks
+// 4 | B), the registers sized for the most float4 a round can hold.
 template <unsigned CC, unsigned BB, bool kRerun>
 __device__ static void dspb_segments_pf(const dspb_seg_args &G) {
     extern __shared__ float dspb_lbuf[];
     __shared__ unsigned s_first[64], s_warm[64], s_len[64];
-    constexpr unsigned C = CC, B = BB, CB = C * B, SB = CB + 2u, NB = dspb_seg_nb(SB);
-    // per channel: NB rows of B / 4 float4, PV of them per thread
-    constexpr unsigned R4 = B / 4u, T4 = NB * R4, PV = (T4 + 255u) / 256u;
-    static_assert(NB <= 64 && B % 4 == 0, "one wave runs a round's callbacks");
+    constexpr unsigned C = CC;
+    const unsigned B = BB ? BB : G.R.B, CB = C * B, SB = CB + 2u, NB = BB ? dspb_seg_nb(CC * BB + 2u) : G.R.lds_nb;
+    // per channel: NB rows of B / 4 float4, at most PV of them per thread
+    // (a round holds fewer than DSPB_LDS_ROUND_BYTES / (16 C) float4 per channel)
+    const unsigned R4 = B / 4u, T4 = NB * R4;
+    constexpr unsigned PV = BB ? (dspb_seg_nb(CC * BB + 2u) * (BB / 4u) + 255u) / 256u
+                               : (DSPB_LDS_ROUND_BYTES / (16u * CC) + 255u) / 256u;
+    constexpr bool kFull = BB && (dspb_seg_nb(CC * BB + 2u) * (BB / 4u)) % 256u == 0;
+    static_assert(!BB || (dspb_seg_nb(CC * BB + 2u) <= 64 && BB % 4 == 0), "one wave runs a round's callbacks");
     typedef __attribute__((address_space(1))) float4 gfloat4;
     const dspb_render_args &A = G.R;
     const unsigned t = threadIdx.x;
@@ -215,15 +222,19 @@ __device__ static void dspb_segments_pf(const dspb_seg_args &G) {
     bool stopped = false;
     if (k != 0xffffffffu)
         dspb_copy_state((void *)&st, kRerun ? (const void *)&G.st_blk[(unsigned long long)k * G.seg] : (const void *)A.S);
-    float4 pf[C][PV];
-    auto load = [&](unsigned r) {
+    // a constant B prefetches a whole round (PB = PV) while the callbacks run;
+    // a runtime B stages in batches of 4 float4 per channel at the round's
+    // start (a whole round's registers would spill)
+    constexpr unsigned PB = BB ? PV : 4u;
+    float4 pf[C][PB];
+    auto load = [&](unsigned r, unsigned v0) {
 #pragma unroll
         for (unsigned c = 0; c < C; ++c) {
 #pragma unroll
-            for (unsigned v = 0; v < PV; ++v) {
-                const unsigned q = t + 256u * v, i = q / R4, s = (q - i * R4) * 4u;
+            for (unsigned v = 0; v < PB; ++v) {
+                const unsigned q = t + 256u * (v0 + v), i = q / R4, s = (q - i * R4) * 4u;
                 float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
-                if ((T4 % 256u == 0 || q < T4) && r < s_len[i] && c < A.in_ch) {
+                if ((kFull || q < T4) && r < s_len[i] && c < A.in_ch) {
                     const unsigned long long gi = (unsigned long long)(s_first[i] + r) * B + s;
                     if (aligned_in && gi + 4 <= A.L) {
                         x = *(const gfloat4 *)(xin[c] + gi);
@@ -238,22 +249,32 @@ __device__ static void dspb_segments_pf(const dspb_seg_args &G) {
             }
         }
     };
-    if (rounds) load(0);
-    for (unsigned r = 0; r < rounds; ++r) {
+    auto put = [&](unsigned r, unsigned v0) {
 #pragma unroll
         for (unsigned c = 0; c < C; ++c) {
 #pragma unroll
-            for (unsigned v = 0; v < PV; ++v) {
-                const unsigned q = t + 256u * v, i = q / R4, s = (q - i * R4) * 4u;
-                if ((T4 % 256u == 0 || q < T4) && r < s_len[i]) {
+            for (unsigned v = 0; v < PB; ++v) {
+                const unsigned q = t + 256u * (v0 + v), i = q / R4, s = (q - i * R4) * 4u;
+                if ((kFull || q < T4) && r < s_len[i]) {
                     float2 *d = (float2 *)(dspb_lbuf + i * SB + c * B + s);
                     d[0] = make_float2(pf[c][v].x, pf[c][v].y);
                     d[1] = make_float2(pf[c][v].z, pf[c][v].w);
                 }
             }
         }
+    };
+    if (BB && rounds) load(0, 0);
+    for (unsigned r = 0; r < rounds; ++r) {
+        if constexpr (BB != 0) {
+            put(r, 0);
+        } else {
+            for (unsigned v0 = 0; v0 < PV; v0 += PB) {
+                load(r, v0);
+                put(r, v0);
+            }
+        }
         __syncthreads();
-        if (r + 1 < rounds) load(r + 1);  // in flight while the callbacks run
+        if (BB && r + 1 < rounds) load(r + 1, 0);  // in flight while the callbacks run
         if (k != 0xffffffffu && r < s_len[t]) {
             if (dspb_seg_block<kRerun>(G, (unsigned long long)s_first[t] + r, r, s_warm[t], st)) {
                 float *blk = dspb_lbuf + t * SB;
@@ -271,7 +292,7 @@ __device__ static void dspb_segments_pf(const dspb_seg_args &G) {
 #pragma unroll
             for (unsigned v = 0; v < PV; ++v) {
                 const unsigned q = t + 256u * v, i = q / R4, s = (q - i * R4) * 4u;
-                if ((T4 % 256u == 0 || q < T4) && r >= s_warm[i] && r < s_len[i]) {
+                if ((kFull || q < T4) && r >= s_warm[i] && r < s_len[i]) {
                     const unsigned long long gi = (unsigned long long)(s_first[i] + r) * B + s;
                     const float2 *d = (const float2 *)(dspb_lbuf + i * SB + c * B + s);
                     const float2 lo = d[0], hi = d[1];
@@ -293,13 +314,18 @@ __device__ static void dspb_segments_pf(const dspb_seg_args &G) {
     extern "C" __global__ __launch_bounds__(256) void name(dspb_seg_args G) { dspb_segments<CC, BB>(G); }
 // pass 1 and the reruns as kernels of their own: pass 1 carries no
 // comparison (its registers are the callback's)
+// pass 1 at two waves per SIMD: both workgroups of a CU resident (their LDS
+// rounds are what the lanes are); a rerun renders few segments, each until
+// its chain meets the recorded one, and may take the registers of one
 #define DSPB_SEG_PF_KERNEL(name, CC, BB, RR)                                           \
-    extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) void name(  \
+    extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RR ? 1 : 2, 2))) void name(  \
         dspb_seg_args G) { dspb_segments_pf<CC, BB, RR>(G); }
 DSPB_SEG_PF_KERNEL(dspb_seg_c2b512, 2, 512, false)
 DSPB_SEG_PF_KERNEL(dspb_seg_c2b512_rerun, 2, 512, true)
-DSPB_SEG_KERNEL(dspb_seg_c1, 1, 0)
-DSPB_SEG_KERNEL(dspb_seg_c2, 2, 0)
+DSPB_SEG_PF_KERNEL(dspb_seg_c2, 2, 0, false)
+DSPB_SEG_PF_KERNEL(dspb_seg_c2_rerun, 2, 0, true)
+DSPB_SEG_PF_KERNEL(dspb_seg_c1, 1, 0, false)
+DSPB_SEG_PF_KERNEL(dspb_seg_c1_rerun, 1, 0, true)
 DSPB_SEG_KERNEL(dspb_seg, 0, 0)
 // segment k (k >= 1) rendered its first block from st_blk[k seg]; the true
 // State there is st_end[k - 1] if segment k - 1 is exact: flag the segments
