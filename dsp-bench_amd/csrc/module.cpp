@@ -68,9 +68,10 @@ struct SegShape {
     uint32_t C, B;
     bool pf;
 };
-constexpr SegShape kSegShapes[4] = {{"dspb_seg_c2b512", "dspb_seg_c2b512_rerun", 2, 512, true},
+constexpr SegShape kSegShapes[5] = {{"dspb_seg_c2b512", "dspb_seg_c2b512_rerun", 2, 512, true},
                                     {"dspb_seg_c2", "dspb_seg_c2_rerun", 2, 0, true},
                                     {"dspb_seg_c1", "dspb_seg_c1_rerun", 1, 0, true},
+                                    {"dspb_seg_c4", "dspb_seg_c4_rerun", 4, 0, true},
                                     {"dspb_seg", nullptr, 0, 0, false}};
 constexpr LdsShape kWalkShapes[2] = {{"dspb_seg_walk_c2b512", 2, 512}, {"dspb_seg_walk_any", 0, 0}};
 constexpr uint32_t kSegMaxState = 1024;   // bytes of State a lane copies (the walk keeps one in LDS)
@@ -143,7 +144,7 @@ struct dsp_module {
     hipFunction_t f_render_st[4] = {};  // kStShapes (NULL: dspb_render)
     // speculative segments (kSegShapes, the check, kWalkShapes; NULL in code
     // objects compiled before them: the serial chain)
-    hipFunction_t f_seg[4] = {}, f_seg_rerun[4] = {}, f_seg_check = nullptr, f_seg_walk[2] = {};
+    hipFunction_t f_seg[5] = {}, f_seg_rerun[5] = {}, f_seg_check = nullptr, f_seg_walk[2] = {};
     struct SegWork {
         void *blk = nullptr;           // [cap_blk] States: st_blk
         void *end = nullptr;           // [cap] States: st_end
@@ -459,7 +460,7 @@ int dsp_module_load(const void *code, uint64_t code_size, int device, dsp_module
         }
     };
     for (int i = 0; i < 4; ++i) optional(&m->f_render_st[i], kStShapes[i].name);
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < 5; ++i) {
         optional(&m->f_seg[i], kSegShapes[i].name);
         if (kSegShapes[i].rerun) optional(&m->f_seg_rerun[i], kSegShapes[i].rerun);
     }
@@ -950,7 +951,7 @@ static int module_render_seg(dsp_module *m, RenderArgsG &A, hipStream_t s) {
     if (2ull * C * B * sizeof(float) > kStagedLdsBytes) return 1;  // the walk's double buffer
     hipFunction_t f = nullptr, fw = nullptr;
     int fi = -1;
-    for (int i = 0; i < 4 && !f; ++i) {
+    for (int i = 0; i < 5 && !f; ++i) {
         const SegShape &sh = kSegShapes[i];
         if (!m->f_seg[i] || (sh.C && sh.C != C) || (sh.B && sh.B != B) || (sh.pf && B % 4)) continue;
         if (sh.rerun && !m->f_seg_rerun[i]) continue;

@@ -138,13 +138,38 @@ __device__ static void dspb_segments(const dspb_seg_args &G) {
     bool stopped = false;
     if (k != 0xffffffffu)
         dspb_copy_state((void *)&st, G.mode ? (const void *)&G.st_blk[(unsigned long long)k * G.seg] : (const void *)A.S);
+    // the channels' rows in LDS (an access by a lane-dependent channel reads
+    // them there, not from the argument block in memory)
+    __shared__ const float *s_in[16];
+    __shared__ float *s_out[16];
+    if (t < C) {
+        s_in[t] = t < A.in_ch ? A.in[t] : nullptr;
+        s_out[t] = A.out[t];
+    }
+    __syncthreads();
+    const unsigned NE = NB * CB;
     for (unsigned r = 0; r < rounds; ++r) {
-        for (unsigned j = t; j < NB * CB; j += nt) {
-            const unsigned i = j / CB, e = j - i * CB, c = e / B, s = e - c * B;
-            if (r < s_len[i]) {
-                const unsigned long long gi = (unsigned long long)(s_first[i] + r) * B + s;
-                dspb_lbuf[i * SB + e] = (c < A.in_ch && gi < A.L) ? ((const dspb_gfloat *)A.in[c])[gi] : 0.0f;
+        // render_audio's copy in batches of 8 loads in flight per thread
+        for (unsigned j0 = t; j0 < NE; j0 += 8 * nt) {
+            float v[8];
+            unsigned dst[8];
+#pragma unroll
+            for (unsigned u = 0; u < 8; ++u) {
+                const unsigned j = j0 + u * nt;
+                v[u] = 0.0f;
+                dst[u] = 0xffffffffu;
+                if (j < NE) {
+                    const unsigned i = j / CB, e = j - i * CB, c = e / B, s = e - c * B;
+                    if (r < s_len[i]) {
+                        const unsigned long long gi = (unsigned long long)(s_first[i] + r) * B + s;
+                        if (s_in[c] && gi < A.L) v[u] = ((const dspb_gfloat *)s_in[c])[gi];
+                        dst[u] = i * SB + e;
+                    }
+                }
             }
+#pragma unroll
+            for (unsigned u = 0; u < 8; ++u)
+                if (dst[u] != 0xffffffffu) dspb_lbuf[dst[u]] = v[u];
         }
         __syncthreads();
         if (k != 0xffffffffu && r < s_len[t]) {
@@ -160,10 +185,10 @@ __device__ static void dspb_segments(const dspb_seg_args &G) {
             }
         }
         __syncthreads();
-        for (unsigned j = t; j < NB * CB; j += nt) {
+        for (unsigned j = t; j < NE; j += nt) {
             const unsigned i = j / CB, e = j - i * CB, c = e / B, s = e - c * B;
             if (r >= s_warm[i] && r < s_len[i])
-                ((dspb_gfloat *)A.out[c])[(unsigned long long)(s_first[i] + r) * B + s] = dspb_lbuf[i * SB + e];
+                ((dspb_gfloat *)s_out[c])[(unsigned long long)(s_first[i] + r) * B + s] = dspb_lbuf[i * SB + e];
         }
         __syncthreads();
         rounds = 0;
@@ -326,6 +351,8 @@ DSPB_SEG_PF_KERNEL(dspb_seg_c2, 2, 0, false)
 DSPB_SEG_PF_KERNEL(dspb_seg_c2_rerun, 2, 0, true)
 DSPB_SEG_PF_KERNEL(dspb_seg_c1, 1, 0, false)
 DSPB_SEG_PF_KERNEL(dspb_seg_c1_rerun, 1, 0, true)
+DSPB_SEG_PF_KERNEL(dspb_seg_c4, 4, 0, false)
+DSPB_SEG_PF_KERNEL(dspb_seg_c4_rerun, 4, 0, true)
 DSPB_SEG_KERNEL(dspb_seg, 0, 0)
 // segment k (k >= 1) rendered its first block from st_blk[k seg]; the true
 // State there is st_end[k - 1] if segment k - 1 is exact: flag the segments
