@@ -117,7 +117,8 @@ struct SegArgsG {
     unsigned pass;
 };
 
-// kDriver: the driver kernels (csrc/plugin_driver.inl, plugin_driver_seg.inl), as one string
+// kDriver / kSegDriver: the driver kernels (csrc/plugin_driver.inl) and the
+// speculative-segment kernels (csrc/plugin_driver_seg.inl), as strings
 #include "plugin_driver_src.inc"
 
 struct ArenaHost {  // mirror of dspb_arena
@@ -358,6 +359,9 @@ int dsp_module_compile(const char *source, const char *name, void **code, uint64
     tu += "extern \"C\" __attribute__((used, visibility(\"default\"))) __device__ const unsigned char "
           "dspb_callback_facts[] = {" + dspb::desc::hex_literal(dspb::irp::encode(facts)) + "};\n";
     tu += kDriver;
+    // the segment kernels only where they can run: a callback the analysis
+    // bounded that writes its State (the loader treats them as optional)
+    if (facts.analyzed && facts.writes_state) tu += kSegDriver;
     std::vector<const char *> hdrs = {kPluginDeviceSrc, source}, hnames = {"plugin_header.h", "dspb_plugin_source.cpp"};
     hiprtcProgram prog;
     if (hiprtcCreateProgram(&prog, tu.c_str(), name ? name : "plugin.cpp", (int)hdrs.size(), hdrs.data(),
