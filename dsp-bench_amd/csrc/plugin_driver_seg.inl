@@ -492,10 +492,3 @@ __device__ static void dspb_seg_walk(const dspb_seg_args &G) {
     extern "C" __global__ __launch_bounds__(256) void name(dspb_seg_args G) { dspb_seg_walk<CC, BB>(G); }
 DSPB_WALK_KERNEL(dspb_seg_walk_c2b512, 2, 512)
 DSPB_WALK_KERNEL(dspb_seg_walk_any, 0, 0)
-
-// compute_IR (plugin.cpp:17-58): the callback once, on buffers as they are
-extern "C" __global__ void dspb_callback(dspb_render_args A) {
-    float *ptrs[16];
-    for (unsigned c = 0; c < A.C; ++c) ptrs[c] = A.out[c];
-    audio_callback(*(Parameters *)A.P, *(State *)A.S, ptrs, A.C, A.B, A.sr);
-}

@@ -465,3 +465,22 @@ def test_fast_math_divergence_is_bounded(torch_cuda, oracle):
     diff = np.abs(cpu.astype(np.float64) - got)
     assert 0.0 < float(np.mean(cpu != got)) < 1.0        # fast-math moved some samples, not all
     assert float(np.max(diff / np.maximum(mag, 1e-30))) <= 8 * 2.0 ** -24
+
+
+def test_code_objects_carry_the_driver_kernels():
+    """(CPU) Every module carries the loader's mandatory kernels; the
+    speculative-segment kernels are compiled only into a module whose
+    callback writes its State (module.cpp dsp_module_compile)."""
+    stateless = d.module.compile_source(
+        '#include "plugin_header.h"\nstruct Parameters { FLOAT_PARAM(0.0f, 1.0f) g; };\nstruct State {};\n'
+        'Parameters default_parameters() { Parameters p = {0.5f}; return p; }\n'
+        'State initialize_state(const Parameters& p, const unsigned C, const float sr, void* ctx) { State s; return s; }\n'
+        'void audio_callback(const Parameters& p, State& st, float** out, const u32 C, const u32 B, const real32 sr) '
+        '{ for (u32 c = 0; c < C; ++c) for (u32 s = 0; s < B; ++s) out[c][s] *= p.g; }\n', "g.cpp")
+    stateful = d.module.compile_source(open(os.path.join(PLUGIN_DIR, "biquad.cpp")).read(), "biquad.cpp")
+    for code in (stateless, stateful):
+        for k in (b"dspb_sizes", b"dspb_defaults", b"dspb_init", b"dspb_render", b"dspb_callback",
+                  b"dspb_render_lds_c2b512", b"dspb_render_st_c2b512"):
+            assert k in code, k
+    for k in (b"dspb_seg_c2b512", b"dspb_seg_check", b"dspb_seg_walk_any"):
+        assert k in stateful and k not in stateless, k
