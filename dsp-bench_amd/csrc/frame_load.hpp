@@ -143,4 +143,20 @@ __device__ __forceinline__ void lds_gain_table_frame(const Stft8kArgs &A, float 
     }
 }
 
+// pow2 B <= 512: the lane's samples 2 lane + 128 b (+1) meet at most four
+// positions of the row, (p0 + 128 b) mod B depends on b mod 4 only, so the
+// lane keeps its 4 gain pairs in registers -- four 8-byte loads from a 2 KB
+// row and no LDS traffic
+__device__ __forceinline__ void reg_gain_table_frame(const Stft8kArgs &A, const float *x, uint64_t fs,
+                                                     uint32_t lane, cx (&v)[64], uint32_t ch) {
+    const float *T = A.map.table + (uint64_t)ch * A.map.B;
+    const uint32_t p0 = (uint32_t)(A.goff + fs) + 2u * lane;
+    v2f t[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) t[j] = *reinterpret_cast<const v2f *>(T + ((p0 + 128u * (uint32_t)j) & A.map.b_mask));
+    s_render_frame<MapKind::Noop, true>(A, x, fs, lane, v);
+#pragma unroll
+    for (int b = 0; b < 64; ++b) v[b] = cx{v[b].r * t[b & 3].x, v[b].i * t[b & 3].y};
+}
+
 }  // namespace dspb

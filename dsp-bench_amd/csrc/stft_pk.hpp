@@ -428,7 +428,8 @@ void stft8192_pk_kernel(Stft8kArgs A) {
             if (A.map.B >= 4u && A.map.B <= 4096u) lds_table_frame(A, lds, fs, lane, v);
             else s_render_frame<MK, POW2>(A, x, fs, lane, v);
         } else if constexpr (MK == MapKind::GainTable && POW2) {
-            if (A.map.B >= 4u && A.map.B <= 4096u) lds_gain_table_frame(A, lds, x, fs, lane, v, ch);
+            if (A.map.B >= 4u && A.map.B <= 512u) reg_gain_table_frame(A, x, fs, lane, v, ch);
+            else if (A.map.B >= 4u && A.map.B <= 4096u) lds_gain_table_frame(A, lds, x, fs, lane, v, ch);
             else s_render_frame<MK, POW2>(A, x, fs, lane, v, ch);
         } else {
             s_render_frame<MK, POW2>(A, x, fs, lane, v, ch);

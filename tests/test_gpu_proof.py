@@ -402,7 +402,7 @@ def test_verify_class_result_through_every_driver(torch_cuda):
 
 
 @pytest.mark.parametrize("name", ["balance", "fade_in", "half_block"])
-@pytest.mark.parametrize("B", [512, 384, 2048])
+@pytest.mark.parametrize("B", [512, 384, 2048, 128])
 def test_gain_table_class_in_every_path(torch_cuda, oracle, name, B):
     """The gain-table class (round 5): per-(channel, position) gains proven
     from the IR (each element stored at most once, x G at x's address, G free
