@@ -689,7 +689,10 @@ def main():
         workload = f"{pname}.cpp via the generic plugin driver (B=512), {minutes:g} min of 48 kHz stereo per GPU"
         kname = ("dspb_render_st_c2b512 (generic driver: one chain through the State, LDS double buffer)"
                  if args.serial_state else
-                 "dspb_seg_c2b512 + dspb_seg_check + dspb_seg_walk (speculative segments, DESIGN 4.6)")
+                 "dspb_seg_c2b512 + dspb_seg_check + dspb_seg_walk (speculative segments, DESIGN 4.6)"
+                 if pname == "biquad" else
+                 "dspb_seg_chain_c2b512 + dspb_seg_c2b512_rerun (a State learned never to forget: the State "
+                 "chain on one lane, then every segment from its recorded State; DESIGN 4.6)")
         alg_desc = "C*L*(4 + 4) B (read + write)" if pname == "biquad" else "C*L*4 B (write; the input is ignored)"
     elif wl in ("wav16enc", "wav24enc"):
         # SURVEY 8(f) row 1, the writer: planar float -> interleaved PCM
@@ -978,6 +981,9 @@ def main():
                             "the serial chain: one lane runs the callback block after block (a State written "
                             "every block); DESIGN 4.6" if wl in ("biquad_src", "sine_src") and
                             (args.serial_state or not (state_segments or {}).get("used")) else
+                            "the State chain: one lane runs the phase update sample after sample (dependent "
+                            "float64 adds; the callback's block arithmetic compiled away), then the segments "
+                            "in parallel; DESIGN 4.6" if (state_segments or {}).get("chain") else
                             "segments: one lane per segment runs the callback's own chain block after block; "
                             "the lanes are the blocks LDS holds (18 per 76 KB workgroup, 36 per CU), so the rounds "
                             "(blocks per segment + warm-up) bound it; DESIGN 4.6"

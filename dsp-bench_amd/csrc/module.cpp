@@ -74,6 +74,11 @@ constexpr SegShape kSegShapes[5] = {{"dspb_seg_c2b512", "dspb_seg_c2b512_rerun",
                                     {"dspb_seg_c4", "dspb_seg_c4_rerun", 4, 0, true},
                                     {"dspb_seg", nullptr, 0, 0, false}};
 constexpr LdsShape kWalkShapes[2] = {{"dspb_seg_walk_c2b512", 2, 512}, {"dspb_seg_walk_any", 0, 0}};
+// the chain kernels of a State that never forgets (kSegDriver dspb_seg_chain;
+// B = 0: any B <= kChainMaxB, the private block sized for it)
+constexpr LdsShape kChainShapes[4] = {{"dspb_seg_chain_c2b512", 2, 512}, {"dspb_seg_chain_c2", 2, 0},
+                                      {"dspb_seg_chain_c1", 1, 0}, {"dspb_seg_chain_c4", 4, 0}};
+constexpr uint32_t kChainMaxB = 4096;
 constexpr uint32_t kSegMaxState = 1024;   // bytes of State a lane copies (the walk keeps one in LDS)
 constexpr uint32_t kSegWarm0 = 4;         // blocks of warm-up of a first render
 constexpr uint32_t kSegWarmMax = 4096;    // the longest warm-up (blocks); past it, the chain is serial
@@ -115,6 +120,7 @@ struct SegArgsG {
     unsigned level;
     unsigned mode;
     unsigned pass;
+    unsigned exact;
 };
 
 // kDriver / kSegDriver: the driver kernels (csrc/plugin_driver.inl) and the
@@ -146,6 +152,11 @@ struct dsp_module {
     // speculative segments (kSegShapes, the check, kWalkShapes; NULL in code
     // objects compiled before them: the serial chain)
     hipFunction_t f_seg[5] = {}, f_seg_rerun[5] = {}, f_seg_check = nullptr, f_seg_walk[2] = {};
+    // kChainShapes and their private memory per lane: one whose compiled
+    // form kept more than a State copy there kept (part of) the block, which
+    // the State then depends on -- the serial chain renders instead
+    hipFunction_t f_seg_chain[4] = {};
+    int chain_priv[4] = {};
     struct SegWork {
         void *blk = nullptr;           // [cap_blk] States: st_blk
         void *end = nullptr;           // [cap] States: st_end
@@ -470,6 +481,15 @@ int dsp_module_load(const void *code, uint64_t code_size, int device, dsp_module
     }
     for (int i = 0; i < 2; ++i) optional(&m->f_seg_walk[i], kWalkShapes[i].name);
     optional(&m->f_seg_check, "dspb_seg_check");
+    for (int i = 0; i < 4; ++i) {
+        optional(&m->f_seg_chain[i], kChainShapes[i].name);
+        if (m->f_seg_chain[i] &&
+            hipFuncGetAttribute(&m->chain_priv[i], HIP_FUNC_ATTRIBUTE_LOCAL_SIZE_BYTES, m->f_seg_chain[i]) !=
+                hipSuccess) {
+            (void)hipGetLastError();
+            m->f_seg_chain[i] = nullptr;
+        }
+    }
     unsigned *d_o = nullptr;
     if ((e = hipMalloc(&d_o, 4 * sizeof(unsigned))) != hipSuccess) return fail(dspb::hip_fail(e, "hipMalloc"));
     void *args[] = {&d_o};
@@ -949,10 +969,19 @@ static bool module_rows_overlap(const float *const *in, uint32_t in_ch, uint64_t
 
 // A State-writing callback over the whole file as speculative segments
 // (kDriver dspb_segments); returns 1 (nothing launched) when the shape does
-// not fit them -- the caller renders the serial chain.
-static int module_render_seg(dsp_module *m, RenderArgsG &A, hipStream_t s) {
+// not fit them -- the caller renders the serial chain.  `chain` (a State
+// learned not to forget): the chain kernel records every block's State, and
+// the exact rerun renders the segments from them (dspb_seg_chain).
+static int module_render_seg(dsp_module *m, RenderArgsG &A, hipStream_t s, bool chain) {
     const uint32_t C = A.C, B = A.B;
     if (2ull * C * B * sizeof(float) > kStagedLdsBytes) return 1;  // the walk's double buffer
+    hipFunction_t fc = nullptr;
+    for (int i = 0; i < 4 && chain && !fc; ++i)
+        if (m->f_seg_chain[i] && kChainShapes[i].C == C &&
+            (kChainShapes[i].B ? kChainShapes[i].B == B : B <= kChainMaxB) &&
+            (uint64_t)m->chain_priv[i] <= (uint64_t)m->state_size + 64)
+            fc = m->f_seg_chain[i];
+    if (chain && !fc) return 1;
     hipFunction_t f = nullptr, fw = nullptr;
     int fi = -1;
     for (int i = 0; i < 5 && !f; ++i) {
@@ -1024,6 +1053,20 @@ static int module_render_seg(dsp_module *m, RenderArgsG &A, hipStream_t s) {
     void *args[] = {&G};
     const unsigned lds = (unsigned)(nb * stride * sizeof(float));
     const unsigned gseg = (unsigned)((K + nb - 1) / nb), gchk = (unsigned)((K + 3) / 4);  // 4 segments per 256 threads
+    if (chain) {
+        MOD_HIP(hipModuleLaunchKernel(fc, 1, 1, 1, 64, 1, 1, 0, s, args, nullptr));
+        G.mode = 1;
+        G.exact = 1;
+        MOD_HIP(hipModuleLaunchKernel(fr, gseg, 1, 1, 256, 1, 1, lds, s, args, nullptr));
+        W.last = dsp_state_spec_info{};
+        W.last.used = 1;
+        W.last.segments = (uint32_t)K;
+        W.last.blocks_per_segment = (uint32_t)seg;
+        W.last.chain = 1;
+        ++W.calls;  // an older speculative render's counters no longer name the last render
+        MOD_HIP(hipEventRecord(m->use_ev, s));
+        return DSP_OK;
+    }
     MOD_HIP(hipMemsetAsync(W.words, 0, 32 * sizeof(unsigned), s));
     // pass 1 and its check at the learnt warm-up, then at 16x longer ones
     // while too many segments started wrong (each level decides on the GPU
@@ -1178,11 +1221,10 @@ int module_render(dsp_module *m, const void *params, uint32_t params_size, const
             W.warm = kSegWarm0;
             W.off = false;
         }
-        if (!W.off) {
-            const int st = module_render_seg(m, A, s);
-            W.serial = st > 0;
-            if (st <= 0) return st;
-        }
+        // (learned never to forget: the State chain, then the segments exactly)
+        const int st = module_render_seg(m, A, s, W.off);
+        W.serial = st > 0;
+        if (st <= 0) return st;
     }
     if (!par) m->seg.serial = true;
     hipFunction_t f = m->f_render;

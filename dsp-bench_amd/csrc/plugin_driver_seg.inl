@@ -40,6 +40,8 @@ struct dspb_seg_args {
     unsigned mode;          // segments: 0 = pass 1 (every segment), 1 = rerun the listed ones;
                             // check: 1 = list the differing ones for a rerun (0: flag only)
     unsigned pass;          // the check's stats slot
+    unsigned exact;         // a rerun of every segment from the States the chain kernel recorded
+                            // (dspb_seg_chain): no list, no early stop
 };
 // pass 1 at warm-up level L > 0 (and its check) runs only when level L - 1
 // ran and more than 1/8 of the segments it guessed -- those whose warm-up
@@ -54,12 +56,16 @@ __device__ static bool dspb_seg_level_runs(const dspb_seg_args &G) {
     const unsigned long long guessed = G.K - 1 - early;
     return guessed && st[prev] * 8ull > guessed;
 }
+// a State's words: accesses that may alias the State's own fields (without
+// may_alias, type-based alias analysis lets the compiler take a word copy of
+// a State of doubles for unrelated memory -- and drop the callback's updates)
+typedef unsigned __attribute__((may_alias)) dspb_word;
 // a State copy as whole words, fully unrolled (a private State stays in
 // registers; a memcpy this size would be lowered to a loop over it)
 __device__ static inline void dspb_copy_state(void *dst, const void *src) {
     if constexpr (sizeof(State) % 4 == 0 && alignof(State) >= 4) {
 #pragma unroll
-        for (unsigned i = 0; i < sizeof(State) / 4; ++i) ((unsigned *)dst)[i] = ((const unsigned *)src)[i];
+        for (unsigned i = 0; i < sizeof(State) / 4; ++i) ((dspb_word *)dst)[i] = ((const dspb_word *)src)[i];
     } else {
 #pragma unroll
         for (unsigned i = 0; i < sizeof(State); ++i) ((unsigned char *)dst)[i] = ((const unsigned char *)src)[i];
@@ -70,7 +76,7 @@ __device__ static inline void dspb_copy_state(void *dst, const void *src) {
 __device__ static bool dspb_same_state(const State *a, const State *b) {
     unsigned d = 0;
     if constexpr (sizeof(State) % 4 == 0 && alignof(State) >= 4) {
-        const unsigned *x = (const unsigned *)a, *y = (const unsigned *)b;
+        const dspb_word *x = (const dspb_word *)a, *y = (const dspb_word *)b;
 #pragma unroll
         for (unsigned i = 0; i < sizeof(State) / 4; ++i) d |= x[i] ^ y[i];
     } else {
@@ -87,7 +93,7 @@ __device__ static unsigned dspb_seg_lane(const dspb_seg_args &G, unsigned base, 
     const dspb_render_args &A = G.R;
     unsigned k = 0xffffffffu, f = 0, w = 0, len = 0;
     if (base + t < nseg) {
-        k = G.mode ? G.list[base + t] : base + t;
+        k = (G.mode && !G.exact) ? G.list[base + t] : base + t;
         const unsigned long long b0 = (unsigned long long)k * G.seg;
         const unsigned long long b1 = b0 + G.seg < A.nblocks ? b0 + G.seg : A.nblocks;
         w = (G.mode || k == 0) ? 0u : (unsigned)(G.warm < b0 ? G.warm : b0);
@@ -106,6 +112,7 @@ template <bool kRerun>
 __device__ static bool dspb_seg_block(const dspb_seg_args &G, unsigned long long b, unsigned r, unsigned w,
                                       State &st) {
     if (r < w) return true;  // warm-up: nothing kept
+    if (kRerun && G.exact) return true;  // rendered from the chain's own States
     if (kRerun && r > 0 && dspb_same_state(&st, &G.st_blk[b])) return false;
     dspb_copy_state((void *)&G.st_blk[b], (const void *)&st);
     return true;
@@ -126,7 +133,7 @@ __device__ static void dspb_segments(const dspb_seg_args &G) {
         if (!dspb_seg_level_runs(G)) return;
         if (G.level && blockIdx.x == 0 && t == 0) *G.count = 0;
     }
-    const unsigned nseg = G.mode ? *(volatile unsigned *)G.count : G.K;
+    const unsigned nseg = (G.mode && !G.exact) ? *(volatile unsigned *)G.count : G.K;
     if (base >= nseg) return;  // the same for the whole workgroup
     unsigned k = 0xffffffffu;
     if (t < NB) k = dspb_seg_lane(G, base, t, nseg, s_first, s_warm, s_len);
@@ -223,7 +230,7 @@ __device__ static void dspb_segments_pf(const dspb_seg_args &G) {
         if (!dspb_seg_level_runs(G)) return;
         if (G.level && blockIdx.x == 0 && t == 0) *G.count = 0;
     }
-    const unsigned nseg = kRerun ? *(volatile unsigned *)G.count : G.K;
+    const unsigned nseg = (kRerun && !G.exact) ? *(volatile unsigned *)G.count : G.K;
     if (base >= nseg) return;  // the same for the whole workgroup
     unsigned k = 0xffffffffu;
     if (t < NB) k = dspb_seg_lane(G, base, t, nseg, s_first, s_warm, s_len);
@@ -380,7 +387,7 @@ extern "C" __global__ void dspb_seg_check(dspb_seg_args G) {
     constexpr bool kWords = sizeof(State) % 4 == 0 && alignof(State) >= 4;
     constexpr unsigned n = kWords ? sizeof(State) / 4 : sizeof(State);
     if constexpr (kWords) {
-        for (unsigned i = lane; i < n; i += 64) diff = diff || ((const unsigned *)first)[i] != ((const unsigned *)prev)[i];
+        for (unsigned i = lane; i < n; i += 64) diff = diff || ((const dspb_word *)first)[i] != ((const dspb_word *)prev)[i];
     } else {
         for (unsigned i = lane; i < n; i += 64)
             diff = diff || ((const unsigned char *)first)[i] != ((const unsigned char *)prev)[i];
@@ -391,7 +398,7 @@ extern "C" __global__ void dspb_seg_check(dspb_seg_args G) {
     if (lane == 0) atomicAdd(&G.stats[G.pass], 1u);
     if (G.mode) {
         if constexpr (kWords) {
-            for (unsigned i = lane; i < n; i += 64) ((unsigned *)first)[i] = ((const unsigned *)prev)[i];
+            for (unsigned i = lane; i < n; i += 64) ((dspb_word *)first)[i] = ((const dspb_word *)prev)[i];
         } else {
             for (unsigned i = lane; i < n; i += 64) ((unsigned char *)first)[i] = ((const unsigned char *)prev)[i];
         }
@@ -492,3 +499,49 @@ __device__ static void dspb_seg_walk(const dspb_seg_args &G) {
     extern "C" __global__ __launch_bounds__(256) void name(dspb_seg_args G) { dspb_seg_walk<CC, BB>(G); }
 DSPB_WALK_KERNEL(dspb_seg_walk_c2b512, 2, 512)
 DSPB_WALK_KERNEL(dspb_seg_walk_any, 0, 0)
+
+// ---- a State that never forgets (module_render_seg, chain) -----------------
+// An oscillator's phase never forgets where it started: no warm-up level
+// meets the true State, and the module learns to render these Parameters
+// without speculation.  The chain kernel then runs the callback on every
+// block in order on one lane and records the State each block starts from
+// (st_blk); the block it hands the callback is a private array filled from the
+// input and read by nothing afterwards, so once the callback is inlined the
+// compiler keeps only the arithmetic the State needs (a phase update, not its
+// cosine).  The exact rerun (G.exact) then renders every segment from its
+// recorded first State, in parallel -- the serial chain's bits.  The host
+// takes a chain kernel only when its private memory is smaller than the block
+// (module.cpp kChainShapes): a block the State depends on stays in scratch,
+// and such a callback renders serially as before.
+template <unsigned CC, unsigned BB>
+__device__ static void dspb_seg_chain(const dspb_seg_args &G) {
+    const dspb_render_args &A = G.R;
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    constexpr unsigned BMAX = BB ? BB : 4096u;
+    const unsigned B = BB ? BB : A.B;
+    const Parameters prm = dspb_from_global<Parameters>(A.P);
+    State st;
+    dspb_copy_state((void *)&st, (const void *)A.S);
+    for (unsigned long long b = 0; b < A.nblocks; ++b) {
+        dspb_copy_state((void *)&G.st_blk[b], (const void *)&st);
+        float blk[CC * BMAX];
+        float *ptrs[CC];
+#pragma unroll
+        for (unsigned c = 0; c < CC; ++c) {
+            ptrs[c] = blk + c * B;
+            const dspb_gfloat *x = (const dspb_gfloat *)A.in[c < A.in_ch ? c : 0];
+            for (unsigned i = 0; i < B; ++i) {
+                const unsigned long long gi = b * B + i;
+                blk[c * B + i] = (c < A.in_ch && gi < A.L) ? x[gi] : 0.0f;
+            }
+        }
+        audio_callback(prm, st, ptrs, CC, B, A.sr);
+    }
+    dspb_copy_state((void *)A.S, (const void *)&st);
+}
+#define DSPB_CHAIN_KERNEL(name, CC, BB)                                                \
+    extern "C" __global__ __launch_bounds__(64) void name(dspb_seg_args G) { dspb_seg_chain<CC, BB>(G); }
+DSPB_CHAIN_KERNEL(dspb_seg_chain_c2b512, 2, 512)
+DSPB_CHAIN_KERNEL(dspb_seg_chain_c2, 2, 0)
+DSPB_CHAIN_KERNEL(dspb_seg_chain_c1, 1, 0)
+DSPB_CHAIN_KERNEL(dspb_seg_chain_c4, 4, 0)

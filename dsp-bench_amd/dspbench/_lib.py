@@ -114,13 +114,13 @@ class dsp_callback_facts(C.Structure):  # module.h
 class dsp_state_spec_info(C.Structure):  # module.h
     _fields_ = [("used", C.c_int32), ("disabled", C.c_int32), ("segments", C.c_uint32),
                 ("blocks_per_segment", C.c_uint32), ("warmup_blocks", C.c_uint32), ("differed", C.c_uint32 * 3),
-                ("serial_reruns", C.c_uint32), ("levels", C.c_uint32)]
+                ("serial_reruns", C.c_uint32), ("levels", C.c_uint32), ("chain", C.c_int32)]
 
     def as_dict(self) -> dict:
         return {"used": bool(self.used), "disabled": bool(self.disabled), "segments": int(self.segments),
                 "blocks_per_segment": int(self.blocks_per_segment), "warmup_blocks": int(self.warmup_blocks),
                 "differed": [int(v) for v in self.differed], "serial_reruns": int(self.serial_reruns),
-                "levels": int(self.levels)}
+                "levels": int(self.levels), "chain": bool(self.chain)}
 
 
 # name -> (restype, argtypes)

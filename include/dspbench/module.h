@@ -216,7 +216,12 @@ int dsp_module_retired_tables(dsp_module *m, uint64_t *n);
  * from different States meet exactly within a few hundred samples); when it
  * does not (an oscillator's phase) the call costs the serial chain plus one
  * pass per warm-up level tried (16x longer each, up to 4096 blocks, within
- * the same call), and then the module renders these Parameters serially.
+ * the same call), and then the module renders these Parameters without
+ * speculation: one lane runs the callback's State updates alone in file order
+ * (its block a private array nothing reads, so the compiler drops the block
+ * arithmetic) and records each block's State, then every segment renders from
+ * its recorded State at once -- when the compiled chain kernel needs no
+ * scratch for the block (a State that depends on the block renders serially).
  * DSP_EXEC_SERIAL_STATE (dspbench.h) forces the serial chain. */
 typedef struct dsp_state_spec_info {
     int32_t used;                /* the module's last State-writing render ran in segments */
@@ -228,6 +233,9 @@ typedef struct dsp_state_spec_info {
     uint32_t serial_reruns;      /* segments the in-order walk rendered again */
     uint32_t levels;             /* pass 1 runs: the learnt warm-up, then 16x longer ones while more
                                     than 1/8 of the guessed segments started wrong (at most 4) */
+    int32_t chain;               /* disabled, and the render ran the State chain on one lane (the
+                                    callback's block arithmetic dropped), then every segment from
+                                    its recorded State in parallel (no speculation) */
 } dsp_state_spec_info;
 /* Waits for the module's last speculative render and describes it. */
 int dsp_module_state_spec(dsp_module *m, dsp_state_spec_info *out);

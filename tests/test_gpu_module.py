@@ -482,5 +482,45 @@ def test_code_objects_carry_the_driver_kernels():
         for k in (b"dspb_sizes", b"dspb_defaults", b"dspb_init", b"dspb_render", b"dspb_callback",
                   b"dspb_render_lds_c2b512", b"dspb_render_st_c2b512"):
             assert k in code, k
-    for k in (b"dspb_seg_c2b512", b"dspb_seg_check", b"dspb_seg_walk_any"):
+    for k in (b"dspb_seg_c2b512", b"dspb_seg_check", b"dspb_seg_walk_any", b"dspb_seg_chain_c2b512"):
         assert k in stateful and k not in stateless, k
+
+
+def _private_sizes(code: bytes) -> dict:
+    """kernel name -> private_segment_fixed_size, from the code object's notes."""
+    import re
+    import subprocess
+    import tempfile
+    tool = "/opt/rocm/lib/llvm/bin/llvm-readelf"
+    if not os.path.exists(tool):
+        pytest.skip("llvm-readelf not found")
+    with tempfile.NamedTemporaryFile(suffix=".co") as f:
+        f.write(code)
+        f.flush()
+        notes = subprocess.run([tool, "--notes", f.name], capture_output=True, text=True, check=True).stdout
+    out = {}
+    for blk in re.split(r"\n\s+- \.", notes):
+        name = re.search(r"\.name:\s+(\S+)", blk)
+        priv = re.search(r"\.private_segment_fixed_size:\s+(\d+)", blk)
+        if name and priv:
+            out[name.group(1)] = int(priv.group(1))
+    return out
+
+
+def test_chain_kernels_drop_the_block_of_a_phase_accumulator():
+    """(CPU) The State chain (plugin_driver_seg.inl dspb_seg_chain) hands the
+    callback a private block nothing reads afterwards: for the reference's
+    sine_test.cpp (a phase in State, a cosine per sample into its block) the
+    compiled chain kernels keep no private memory at all -- the cosine is gone
+    and only the phase update runs -- while biquad.cpp's State depends on its
+    block, which stays in scratch, so module.cpp renders it serially when its
+    segments fail (chain_priv > State + 64 bytes)."""
+    sine = os.path.join(MODS, "mod_sine_test.co")
+    if not os.path.exists(sine):
+        pytest.skip("reference modules not built")
+    with open(sine, "rb") as f:
+        ps = _private_sizes(f.read())
+    pb = _private_sizes(d.module.compile_source(open(os.path.join(PLUGIN_DIR, "biquad.cpp")).read(), "biquad.cpp"))
+    for k in ("dspb_seg_chain_c2b512", "dspb_seg_chain_c2", "dspb_seg_chain_c1", "dspb_seg_chain_c4"):
+        assert ps[k] == 0, (k, ps[k])
+        assert pb[k] > 1024, (k, pb[k])

@@ -56,6 +56,52 @@ void audio_callback(const Parameters& p, State& st, float** out, const u32 C, co
 }
 '''
 
+# an oscillator bank: a phase per channel in State (never forgets), the
+# block written and never read -- the State chain drops the block's arithmetic
+OSC_SRC = r'''
+#include "plugin_header.h"
+struct Parameters { FLOAT_PARAM(20.0f, 2000.0f) freq; FLOAT_PARAM(0.0f, 1.0f) gain; };
+struct State { double phase[4]; };
+Parameters default_parameters() { Parameters p = {440.0f, 0.25f}; return p; }
+State initialize_state(const Parameters& p, const unsigned C, const float sr, void* ctx) {
+    State s = {{0.0, 0.0, 0.0, 0.0}}; return s;
+}
+void audio_callback(const Parameters& p, State& st, float** out, const u32 C, const u32 B, const real32 sr) {
+    for (u32 c = 0; c < C; ++c) {
+        const double step = two_pi * (double)p.freq * (1.0 + 0.01 * (double)(c & 3u)) / (double)sr;
+        double ph = st.phase[c & 3u];
+        for (u32 s = 0; s < B; ++s) {
+            out[c][s] = (float)(sin_64(ph) * (double)p.gain);
+            ph += step;
+            if (ph > two_pi) ph -= two_pi;
+        }
+        st.phase[c & 3u] = ph;
+    }
+}
+'''
+
+# a tremolo: a phase in State (never forgets) that does not depend on the
+# block, which the callback reads and scales: the block stays in the chain
+# kernel's private memory, so it renders serially
+TREMOLO_SRC = r'''
+#include "plugin_header.h"
+struct Parameters { FLOAT_PARAM(0.1f, 20.0f) rate; FLOAT_PARAM(0.0f, 1.0f) depth; };
+struct State { double phase; };
+Parameters default_parameters() { Parameters p = {5.0f, 0.5f}; return p; }
+State initialize_state(const Parameters& p, const unsigned C, const float sr, void* ctx) {
+    State s = {0.0}; return s;
+}
+void audio_callback(const Parameters& p, State& st, float** out, const u32 C, const u32 B, const real32 sr) {
+    const double step = two_pi * (double)p.rate / (double)sr;
+    for (u32 s = 0; s < B; ++s) {
+        const float g = (float)(1.0 - (double)p.depth * (0.5 + 0.5 * cos_64(st.phase)));
+        for (u32 c = 0; c < C; ++c) out[c][s] = out[c][s] * g;
+        st.phase += step;
+        if (st.phase > two_pi) st.phase -= two_pi;
+    }
+}
+'''
+
 # a State of 2 KB: more than a lane copies (serial chain)
 BIG_STATE_SRC = r'''
 #include "plugin_header.h"
@@ -201,7 +247,8 @@ def test_never_forgetting_state_is_exact_and_learned(torch_cuda):
     assert info[0]["used"] and info[0]["levels"] == 2 and info[0]["warmup_blocks"] == 64
     assert info[0]["differed"][0] == info[0]["segments"] - 1 - 64 // seg
     assert info[0]["serial_reruns"] > 0
-    assert info[1]["disabled"] and not info[1]["used"]
+    # (its envelope depends on the block: no State chain, the serial one)
+    assert info[1]["disabled"] and not info[1]["used"] and not info[1]["chain"]
     assert info[2]["disabled"] and not info[2]["used"]
     # new Parameters: learnt again
     p2 = np.frombuffer(params, np.float32).copy()
@@ -214,15 +261,56 @@ def test_never_forgetting_state_is_exact_and_learned(torch_cuda):
 @pytest.mark.gpu
 def test_reference_oscillator_sine_test(torch_cuda):
     """The reference's sine_test.cpp (a phase accumulator in State): exact
-    through the walk."""
+    through the walk on the first call, which learns that it never forgets;
+    the next calls run the State chain (the phase alone, in order, on one
+    lane) and every segment from its recorded State -- exact, no
+    speculation."""
     path = os.path.join(MODS, "mod_sine_test.co")
     if not os.path.exists(path):
         pytest.skip("reference modules not built")
     with open(path, "rb") as f:
         mod = d.module.Module(f.read())
     params = mod.default_parameters()
-    spec, ser, info = both(torch_cuda, mod, params, noise(2, 40_000, 5), 2, 512)
+    spec, ser, info = both(torch_cuda, mod, params, noise(2, 40_000, 5), 2, 512, calls=3)
     assert_same(spec, ser)
+    assert info[0]["used"] and not info[0]["chain"]
+    for i in info[1:]:
+        assert i["disabled"] and i["used"] and i["chain"] and i["segments"] > 1
+    # a long render through the chain: 2 min of stereo, three calls
+    spec, ser, info = both(torch_cuda, mod, params, noise(2, 48000 * 120 + 77, 8), 2, 512, calls=3)
+    assert_same(spec, ser)
+    assert info[1]["chain"] and info[2]["chain"] and info[2]["segments"] > 1000
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("C,cin,B,L,chain", [(2, 2, 512, 300_000, True), (1, 1, 256, 100_000, True),
+                                             (2, 2, 100, 80_001, True), (4, 2, 64, 40_000, True),
+                                             (3, 3, 512, 60_000, False)])
+def test_state_chain_of_an_oscillator_bank(torch_cuda, C, cin, B, L, chain):
+    """An oscillator per channel (phases in State never forget; the block
+    only written): after the first call the State chain kernel of the shape
+    runs (stereo B = 512, any B for 1, 2 or 4 channels) with the sines
+    dropped, and the segments render from its States; three channels have no
+    chain kernel and render serially.  Bit for bit against the serial chain,
+    State included."""
+    mod = module_of(OSC_SRC, "osc_spec")
+    params = mod.default_parameters()
+    spec, ser, info = both(torch_cuda, mod, params, noise(cin, L, 11), C, B, calls=3)
+    assert_same(spec, ser)
+    assert info[2]["disabled"]
+    assert bool(info[2]["chain"]) == chain and bool(info[2]["used"]) == chain
+
+
+@pytest.mark.gpu
+def test_tremolo_reading_its_block_stays_serial(torch_cuda):
+    """A tremolo reads its block: the chain kernel keeps the block in private
+    memory (more than the State there), so after learning that its phase never
+    forgets the module renders it serially -- exact either way."""
+    mod = module_of(TREMOLO_SRC, "tremolo_spec")
+    params = mod.default_parameters()
+    spec, ser, info = both(torch_cuda, mod, params, noise(2, 200_000, 12), 2, 512, calls=3)
+    assert_same(spec, ser)
+    assert info[2]["disabled"] and not info[2]["chain"] and not info[2]["used"]
 
 
 @pytest.mark.gpu
