@@ -934,7 +934,8 @@ int module_seg_collect(dsp_module *m, bool wait) {
         }
         W.pending[i] = false;
         dsp_state_spec_info &r = W.info[i];
-        const unsigned *h = W.h_stats + 16 * i;  // [0, 4) levels, [4] [5] reruns, [7] walk, [8, 12) levels run
+        const unsigned *h = W.h_stats + 16 * i;  // [0, 4) levels, [4] [5] reruns, [7] walk, [8, 12) levels run,
+                                                 // [12] the State chain ran
         const uint32_t first_warm = r.warmup_blocks;
         uint32_t last = 0, warm = first_warm;
         for (uint32_t L = 1; L < r.levels && h[8 + L]; ++L) {
@@ -947,6 +948,7 @@ int module_seg_collect(dsp_module *m, bool wait) {
         r.differed[1] = h[4];
         r.differed[2] = h[5];
         r.serial_reruns = h[7];
+        r.chain = h[12] ? 1 : 0;
         if (W.seq[i] == W.calls) W.last = r;
         // learn only from renders that started with the warm-up now in force
         if (first_warm != W.warm || W.off) continue;
@@ -975,8 +977,9 @@ static bool module_rows_overlap(const float *const *in, uint32_t in_ch, uint64_t
 static int module_render_seg(dsp_module *m, RenderArgsG &A, hipStream_t s, bool chain) {
     const uint32_t C = A.C, B = A.B;
     if (2ull * C * B * sizeof(float) > kStagedLdsBytes) return 1;  // the walk's double buffer
+    // the chain kernel of this shape, if its compiled form dropped the block
     hipFunction_t fc = nullptr;
-    for (int i = 0; i < 4 && chain && !fc; ++i)
+    for (int i = 0; i < 4 && !fc; ++i)
         if (m->f_seg_chain[i] && kChainShapes[i].C == C &&
             (kChainShapes[i].B ? kChainShapes[i].B == B : B <= kChainMaxB) &&
             (uint64_t)m->chain_priv[i] <= (uint64_t)m->state_size + 64)
@@ -1090,6 +1093,14 @@ static int module_render_seg(dsp_module *m, RenderArgsG &A, hipStream_t s, bool 
         MOD_HIP(hipModuleLaunchKernel(m->f_seg_check, gchk, 1, 1, 256, 1, 1, 0, s, args, nullptr));
         ++levels;
     }
+    // the last level failed (decided on the GPU): the State chain and the
+    // exact rerun take over, the reruns and the walk below return at once
+    if (fc) {
+        G.level = levels;
+        G.prev_warm = warm;
+        G.mode = 2;
+        MOD_HIP(hipModuleLaunchKernel(fc, 1, 1, 1, 64, 1, 1, 0, s, args, nullptr));
+    }
     // two reruns of the listed segments, each checked; the last check only flags
     G.level = 0xffffffffu;
     unsigned *listing = W.words;
@@ -1106,6 +1117,11 @@ static int module_render_seg(dsp_module *m, RenderArgsG &A, hipStream_t s, bool 
     }
     MOD_HIP(hipModuleLaunchKernel(fw, 1, 1, 1, 256, 1, 1, (unsigned)(2ull * C * B * sizeof(float)), s, args,
                                   nullptr));
+    if (fc) {
+        G.mode = 1;
+        G.exact = 2;
+        MOD_HIP(hipModuleLaunchKernel(fr, gseg, 1, 1, 256, 1, 1, lds, s, args, nullptr));
+    }
     MOD_HIP(hipMemcpyAsync(W.h_stats + 16 * slot, W.words + 8, 16 * sizeof(unsigned), hipMemcpyDeviceToHost, s));
     MOD_HIP(hipEventRecord(W.ev[slot], s));
     W.pending[slot] = true;

@@ -31,7 +31,8 @@ struct dspb_seg_args {
     unsigned *prev_count;   // a rerun's check: the rerun's count (0: nothing changed, skip)
     unsigned char *flags;   // the last check: 1 = differed
     unsigned *stats;        // [0, 4) segments that differed per warm-up level, [4] / [5] after
-                            // rerun 1 / 2, [7] serial reruns of the walk, [8, 12) levels run
+                            // rerun 1 / 2, [7] serial reruns of the walk, [8, 12) levels run,
+                            // [12] the State chain took over from the levels (dspb_seg_chain)
     unsigned long long seg; // blocks per segment
     unsigned K;             // segments
     unsigned warm;          // pass 1: warm-up blocks
@@ -41,8 +42,11 @@ struct dspb_seg_args {
                             // check: 1 = list the differing ones for a rerun (0: flag only)
     unsigned pass;          // the check's stats slot
     unsigned exact;         // a rerun of every segment from the States the chain kernel recorded
-                            // (dspb_seg_chain): no list, no early stop
+                            // (dspb_seg_chain): no list, no early stop (2: only if the chain ran)
 };
+// the State chain took over within this render: the reruns, their checks and
+// the walk have nothing to do
+__device__ static bool dspb_seg_chained(const dspb_seg_args &G) { return *(volatile unsigned *)&G.stats[12] != 0; }
 // pass 1 at warm-up level L > 0 (and its check) runs only when level L - 1
 // ran and more than 1/8 of the segments it guessed -- those whose warm-up
 // began after block 0 -- started from a State that was not the true one: the
@@ -132,6 +136,8 @@ __device__ static void dspb_segments(const dspb_seg_args &G) {
     if (!G.mode) {  // pass 1: at a warm-up level that runs; it restarts the listing
         if (!dspb_seg_level_runs(G)) return;
         if (G.level && blockIdx.x == 0 && t == 0) *G.count = 0;
+    } else if (G.exact ? (G.exact == 2 && !dspb_seg_chained(G)) : dspb_seg_chained(G)) {
+        return;
     }
     const unsigned nseg = (G.mode && !G.exact) ? *(volatile unsigned *)G.count : G.K;
     if (base >= nseg) return;  // the same for the whole workgroup
@@ -229,6 +235,8 @@ __device__ static void dspb_segments_pf(const dspb_seg_args &G) {
     if (!kRerun) {  // pass 1: at a warm-up level that runs; it restarts the listing
         if (!dspb_seg_level_runs(G)) return;
         if (G.level && blockIdx.x == 0 && t == 0) *G.count = 0;
+    } else if (G.exact ? (G.exact == 2 && !dspb_seg_chained(G)) : dspb_seg_chained(G)) {
+        return;
     }
     const unsigned nseg = (kRerun && !G.exact) ? *(volatile unsigned *)G.count : G.K;
     if (base >= nseg) return;  // the same for the whole workgroup
@@ -368,6 +376,7 @@ DSPB_SEG_KERNEL(dspb_seg, 0, 0)
 // the State's words; a check after a pass that found nothing to rerun
 // returns at once (nothing changed: the flags stand).
 extern "C" __global__ void dspb_seg_check(dspb_seg_args G) {
+    if (dspb_seg_chained(G)) return;
     if (G.level != 0xffffffffu) {  // pass 1's check: where pass 1 ran
         if (!dspb_seg_level_runs(G)) return;
         if (blockIdx.x == 0 && threadIdx.x == 0) G.stats[8 + G.level] = 1;
@@ -419,6 +428,7 @@ __device__ static void dspb_seg_walk(const dspb_seg_args &G) {
     __shared__ int s_bad, s_stop;
     __shared__ unsigned long long s_prev[(sizeof(State) + 7) / 8];  // the predecessor's final State
     const dspb_render_args &A = G.R;
+    if (dspb_seg_chained(G)) return;  // the same for the whole workgroup
     const unsigned B = NB_ ? NB_ : A.B, C = CC ? CC : A.C, CB = C * B, t = threadIdx.x, nt = blockDim.x;
     float *buf0 = dspb_lbuf, *buf1 = dspb_lbuf + CB;
     Parameters prm = dspb_from_global<Parameters>(A.P);
@@ -512,11 +522,19 @@ DSPB_WALK_KERNEL(dspb_seg_walk_any, 0, 0)
 // recorded first State, in parallel -- the serial chain's bits.  The host
 // takes a chain kernel only when its private memory is smaller than the block
 // (module.cpp kChainShapes): a block the State depends on stays in scratch,
-// and such a callback renders serially as before.
+// and such a callback renders serially as before.  Within a speculative
+// render (G.mode 2) the chain runs only when the last warm-up level tried
+// failed (dspb_seg_level_runs on the level after it), and says so in
+// stats[12]: the reruns and the walk then return at once, and the exact
+// rerun (G.exact 2) renders the segments.
 template <unsigned CC, unsigned BB>
 __device__ static void dspb_seg_chain(const dspb_seg_args &G) {
     const dspb_render_args &A = G.R;
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    if (G.mode == 2) {
+        if (!dspb_seg_level_runs(G)) return;
+        G.stats[12] = 1u;
+    }
     constexpr unsigned BMAX = BB ? BB : 4096u;
     const unsigned B = BB ? BB : A.B;
     const Parameters prm = dspb_from_global<Parameters>(A.P);

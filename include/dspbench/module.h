@@ -216,8 +216,8 @@ int dsp_module_retired_tables(dsp_module *m, uint64_t *n);
  * from different States meet exactly within a few hundred samples); when it
  * does not (an oscillator's phase) the call costs the serial chain plus one
  * pass per warm-up level tried (16x longer each, up to 4096 blocks, within
- * the same call), and then the module renders these Parameters without
- * speculation: one lane runs the callback's State updates alone in file order
+ * the same call); then -- within that call, and without speculation for
+ * these Parameters from the next call on -- one lane runs the callback's State updates alone in file order
  * (its block a private array nothing reads, so the compiler drops the block
  * arithmetic) and records each block's State, then every segment renders from
  * its recorded State at once -- when the compiled chain kernel needs no
@@ -233,9 +233,10 @@ typedef struct dsp_state_spec_info {
     uint32_t serial_reruns;      /* segments the in-order walk rendered again */
     uint32_t levels;             /* pass 1 runs: the learnt warm-up, then 16x longer ones while more
                                     than 1/8 of the guessed segments started wrong (at most 4) */
-    int32_t chain;               /* disabled, and the render ran the State chain on one lane (the
-                                    callback's block arithmetic dropped), then every segment from
-                                    its recorded State in parallel (no speculation) */
+    int32_t chain;               /* the render ran the State chain on one lane (the callback's block
+                                    arithmetic dropped), then every segment from its recorded State
+                                    in parallel: after its last warm-up level failed (decided on the
+                                    GPU, within the call), or from the start once learnt (disabled) */
 } dsp_state_spec_info;
 /* Waits for the module's last speculative render and describes it. */
 int dsp_module_state_spec(dsp_module *m, dsp_state_spec_info *out);

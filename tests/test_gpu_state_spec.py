@@ -260,11 +260,11 @@ def test_never_forgetting_state_is_exact_and_learned(torch_cuda):
 
 @pytest.mark.gpu
 def test_reference_oscillator_sine_test(torch_cuda):
-    """The reference's sine_test.cpp (a phase accumulator in State): exact
-    through the walk on the first call, which learns that it never forgets;
-    the next calls run the State chain (the phase alone, in order, on one
-    lane) and every segment from its recorded State -- exact, no
-    speculation."""
+    """The reference's sine_test.cpp (a phase accumulator in State): on the
+    first call every warm-up level fails and the State chain (the phase
+    alone, in order, on one lane) takes over within the call, the walk
+    skipped; the next calls run the chain from the start (learnt) and every
+    segment from its recorded State -- exact, no speculation."""
     path = os.path.join(MODS, "mod_sine_test.co")
     if not os.path.exists(path):
         pytest.skip("reference modules not built")
@@ -273,13 +273,13 @@ def test_reference_oscillator_sine_test(torch_cuda):
     params = mod.default_parameters()
     spec, ser, info = both(torch_cuda, mod, params, noise(2, 40_000, 5), 2, 512, calls=3)
     assert_same(spec, ser)
-    assert info[0]["used"] and not info[0]["chain"]
+    assert info[0]["used"] and info[0]["chain"] and info[0]["levels"] >= 1 and info[0]["serial_reruns"] == 0
     for i in info[1:]:
         assert i["disabled"] and i["used"] and i["chain"] and i["segments"] > 1
     # a long render through the chain: 2 min of stereo, three calls
     spec, ser, info = both(torch_cuda, mod, params, noise(2, 48000 * 120 + 77, 8), 2, 512, calls=3)
     assert_same(spec, ser)
-    assert info[1]["chain"] and info[2]["chain"] and info[2]["segments"] > 1000
+    assert all(i["chain"] for i in info) and info[2]["segments"] > 1000
 
 
 @pytest.mark.gpu
@@ -299,6 +299,7 @@ def test_state_chain_of_an_oscillator_bank(torch_cuda, C, cin, B, L, chain):
     assert_same(spec, ser)
     assert info[2]["disabled"]
     assert bool(info[2]["chain"]) == chain and bool(info[2]["used"]) == chain
+    assert bool(info[0]["chain"]) == chain  # the first call: the chain took over from the levels
 
 
 @pytest.mark.gpu
