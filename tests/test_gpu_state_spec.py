@@ -470,12 +470,18 @@ def test_generated_plugins_match_the_serial_chain(torch_cuda, name):
 
 
 @pytest.mark.gpu
-def test_loop_mode_through_segments(torch_cuda):
+@pytest.mark.parametrize("plugin", ["biquad", "osc"])
+def test_loop_mode_through_segments(torch_cuda, plugin):
     """dsp_render_loop (audio.cpp:100-132: the file wraps from the cursor)
     with a State-writing plugin: the wrapped block stream through the
-    segments equals the serial chain's, cursor and State included."""
+    segments (biquad.cpp) or the State chain (the oscillator bank) equals the
+    serial chain's, cursor and State included."""
     torch = torch_cuda
-    mod, params = biquad_module(700.0, 0.9)
+    if plugin == "biquad":
+        mod, params = biquad_module(700.0, 0.9)
+    else:
+        mod = module_of(OSC_SRC, "osc_spec")
+        params = mod.default_parameters()
     x = torch.from_numpy(noise(2, 33_333, 12)).cuda()
     res = []
     for serial in (False, True):
@@ -484,6 +490,8 @@ def test_loop_mode_through_segments(torch_cuda):
         y1, cur = d.render_loop(x, 2, 512, 700, 48000.0, plug, cursor=1234)
         y2, cur2 = d.render_loop(x, 2, 512, 300, 48000.0, plug, cursor=cur)
         res.append((y1.cpu().numpy(), y2.cpu().numpy(), cur, cur2, mod.read_state()))
+        if not serial and plugin == "osc":
+            assert mod.state_spec()["chain"]
     a, b = res
     assert a[2:4] == b[2:4] and a[4] == b[4]
     for i in (0, 1):
