@@ -4,10 +4,14 @@
 set -o pipefail
 mkdir -p gpurun_out
 rm -f gpurun_out/bench_all.jsonl
-for wl in headline stft96k gain_stft generic generic_stft fir1024 gain10min ch96k wav16 wav24 wav16enc wav24enc ir biquad biquad_src; do
+for wl in headline stft96k gain_stft generic generic_stft fir1024 gain10min ch96k wav16 wav24 wav16enc wav24enc ir biquad biquad_src sine_src; do
   timeout -k 10 200 python -u bench.py --workload $wl --no-cpu-baseline --no-e2e > gpurun_out/bench_$wl.log 2>&1 || exit 1
   tail -1 gpurun_out/bench_$wl.log >> gpurun_out/bench_all.jsonl
 done
+# the gain-table class (a per-position gain plugin on the fused path)
+timeout -k 10 200 python -u bench.py --workload generic_stft --plugin fade_in --no-cpu-baseline --no-e2e \
+  > gpurun_out/bench_generic_stft_fade_in.log 2>&1 || exit 1
+tail -1 gpurun_out/bench_generic_stft_fade_in.log >> gpurun_out/bench_all.jsonl
 python3 - <<'PY'
 import json
 for line in open("gpurun_out/bench_all.jsonl"):
