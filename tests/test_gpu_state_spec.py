@@ -302,6 +302,45 @@ def test_state_chain_of_an_oscillator_bank(torch_cuda, C, cin, B, L, chain):
     assert bool(info[0]["chain"]) == chain  # the first call: the chain took over from the levels
 
 
+# a wavetable oscillator: a 1 KB State (the table plus a phase), the table
+# written once by initialize_state, the phase never forgetting
+WAVETABLE_SRC = r'''
+#include "plugin_header.h"
+struct Parameters { FLOAT_PARAM(20.0f, 2000.0f) freq; };
+struct State { float table[252]; double phase; double pad; };
+Parameters default_parameters() { Parameters p = {330.0f}; return p; }
+State initialize_state(const Parameters& p, const unsigned C, const float sr, void* ctx) {
+    State s;
+    for (int i = 0; i < 252; ++i) s.table[i] = (float)sin_64(two_pi * (double)i / 250.0);
+    s.phase = 0.0; s.pad = 0.0;
+    return s;
+}
+void audio_callback(const Parameters& p, State& st, float** out, const u32 C, const u32 B, const real32 sr) {
+    const double step = 250.0 * (double)p.freq / (double)sr;
+    for (u32 s = 0; s < B; ++s) {
+        const int i = (int)st.phase;
+        const float v = st.table[i];
+        for (u32 c = 0; c < C; ++c) out[c][s] = v * (c == 0 ? 1.0f : 0.5f);
+        st.phase += step;
+        if (st.phase >= 250.0) st.phase -= 250.0;
+    }
+}
+'''
+
+
+@pytest.mark.gpu
+def test_state_chain_with_a_1kb_state(torch_cuda):
+    """A wavetable oscillator whose State is 1,024 bytes (a table the callback
+    only reads, a phase that never forgets): the State chain and the segments
+    copy the whole State per block, bit for bit against the serial chain."""
+    mod = module_of(WAVETABLE_SRC, "wavetable_spec")
+    assert mod.state_size == 1024, mod.state_size
+    params = mod.default_parameters()
+    spec, ser, info = both(torch_cuda, mod, params, noise(2, 250_000, 13), 2, 512, calls=3)
+    assert_same(spec, ser)
+    assert all(i["chain"] for i in info), info
+
+
 @pytest.mark.gpu
 def test_tremolo_reading_its_block_stays_serial(torch_cuda):
     """A tremolo reads its block: the chain kernel keeps the block in private
