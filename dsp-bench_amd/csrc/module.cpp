@@ -1080,6 +1080,11 @@ static int module_render_seg(dsp_module *m, RenderArgsG &A, hipStream_t s, bool 
         if (L > 0) {
             const uint32_t next = std::min<uint32_t>(warm * 16, kSegWarmMax);
             if (next <= warm || 2ull * next >= A.nblocks) break;  // no longer, or as long as the file
+            // with a State chain to fall back on, a level whose rounds (its
+            // warm-up and a segment of full callbacks) exceed 1/16 of the
+            // file costs more than the chain (the State arithmetic alone over
+            // every block) is likely to: not tried
+            if (fc && 16ull * (next + seg) > A.nblocks) break;
             prev = warm;
             warm = next;
         }
