@@ -1009,6 +1009,7 @@ Facts analyze(const std::string &ir, const char *fn) {
         return A.f;
     }
     A.f.analyzed = true;
+    A.f.state_reads_block = A.f.writes_state && ((A.sta_data & D_IN) || A.f.input_control);
     A.check_gain();
     A.check_gain_table();
     if (A.f.input_control && A.f.gain_form) {
@@ -1143,6 +1144,7 @@ std::string encode(const Facts &f) {
     s += "gain_bits=" + std::to_string(f.gain_bits) + "\n";
     s += "gain_table_form=" + std::to_string(f.gain_table_form) + "\n";
     s += "table_why=" + clean(f.table_why.substr(0, 256)) + "\n";
+    s += "state_reads_block=" + std::to_string(f.state_reads_block) + "\n";
     s += "why=" + clean(f.why.substr(0, 512)) + "\n";
     return s;
 }
@@ -1168,6 +1170,7 @@ bool decode(const std::string &s, Facts *f) {
         else if (k == "gain_bits") f->gain_bits = (uint32_t)std::strtoul(v.c_str(), nullptr, 10);
         else if (k == "gain_table_form") f->gain_table_form = v == "1";
         else if (k == "table_why") f->table_why = v;
+        else if (k == "state_reads_block") f->state_reads_block = v == "1";
         else if (k == "why") f->why = v;
     }
     return have_analyzed;

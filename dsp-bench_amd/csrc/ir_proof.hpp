@@ -41,6 +41,10 @@ struct Facts {
     // constant channels (the CFG's natural loops, ir_proof.cpp)
     bool gain_table_form = false;
     std::string table_why;      // why not gain_table_form
+    // a value stored to State, or a branch condition, depends on a block
+    // sample (true unless the analysis completed and showed otherwise): when
+    // false the State's trajectory is the same whatever the block holds
+    bool state_reads_block = true;
     std::string why;            // the first construct that ended the analysis, or why a
                                 // property does not hold
 };

@@ -813,6 +813,7 @@ static void facts_out(const dspb::irp::Facts &f, bool present, dsp_callback_fact
     std::strncpy(o->why, f.why.c_str(), sizeof o->why - 1);
     o->gain_table_form = f.gain_table_form;
     std::strncpy(o->table_why, f.table_why.c_str(), sizeof o->table_why - 1);
+    o->state_reads_block = f.state_reads_block;
 }
 
 int dsp_module_facts(const dsp_module *m, dsp_callback_facts *out) {

@@ -272,6 +272,10 @@ typedef struct dsp_callback_facts {
                               their induction variables) give every store the address
                               (constant or loop channel, loop sample) */
     char table_why[128];   /* (ABI 3) why not gain_table_form */
+    int32_t state_reads_block; /* (ABI 3) a value stored to State, or a branch condition, depends on
+                              a block sample (1 unless the analysis completed and showed
+                              otherwise): 0 = the State's trajectory is the same whatever the
+                              block holds (an oscillator's phase, a tremolo's) */
 } dsp_callback_facts;
 
 /* The facts of a loaded module (present = 0 for a code object without). */

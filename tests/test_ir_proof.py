@@ -274,3 +274,52 @@ def test_numbered_types_do_not_hide_the_arguments():
            "for (u32 c = 0; c < C; ++c) out[c][s] = v; }")
     f = dm.analyze_source(src(osc))
     assert (not f["analyzed"]) or f["writes_state"], f
+
+
+def state_snippet(body):
+    return ("#include \"plugin_header.h\"\n"
+            "struct Parameters { FLOAT_PARAM(0.0f, 1.0f) g; };\nstruct State { double ph; float env; };\n"
+            "Parameters default_parameters() { Parameters p = {0.5f}; return p; }\n"
+            "State initialize_state(const Parameters &p, const unsigned C, const float sr, void *ctx) "
+            "{ State s = {0.0, 0.0f}; return s; }\n"
+            "void audio_callback(const Parameters &p, State &st, float **out, const u32 C, const u32 B, "
+            "const real32 sr) {\n" + body + "\n}\n")
+
+
+# does a value stored to State (or a branch) depend on a block sample?
+STATE_DEP = {
+    "phase_only": ("for (u32 s = 0; s < B; ++s) { out[0][s] = (float)cos_64(st.ph); st.ph += 0.01; "
+                   "if (st.ph > 6.28) st.ph -= 6.28; }", False),
+    "tremolo": ("for (u32 s = 0; s < B; ++s) { out[0][s] *= (float)cos_64(st.ph); st.ph += 0.01; }", False),
+    "envelope": ("for (u32 s = 0; s < B; ++s) { const float x = out[0][s]; st.env = st.env + 0.1f * (x - st.env); "
+                 "out[0][s] = st.env; }", True),
+    "branch_on_a_sample": ("for (u32 s = 0; s < B; ++s) if (out[0][s] > 0.5f) st.ph += 1.0;", True),
+    # a block element read after the loop wrote it: any block load counts
+    # (conservative; a store the compiler forwards to the load is no read)
+    "reads_its_own_output": ("for (u32 s = 0; s < B; ++s) out[0][s] = (float)s; st.env = out[0][B / 2];", True),
+    "forwarded_store": ("out[0][0] = 1.0f; st.env = out[0][0];", False),
+    "state_not_written": ("for (u32 s = 0; s < B; ++s) out[0][s] *= p.g + st.env;", False),
+}
+
+
+@pytest.mark.parametrize("case", sorted(STATE_DEP))
+def test_state_reads_block(case):
+    """state_reads_block (module.h dsp_callback_facts): 0 only when no value
+    stored to State and no branch depends on a block sample -- the State's
+    trajectory is then the same whatever the block holds (an oscillator's
+    phase, a tremolo's), the condition for rendering its State chain apart
+    from its output."""
+    body, want = STATE_DEP[case]
+    f = dm.analyze_source(state_snippet(body))
+    assert f["analyzed"], f
+    assert f["state_reads_block"] == want, (case, f)
+
+
+def test_state_reads_block_of_stock_plugins():
+    """sine_test.cpp's phase ignores its block; biquad.cpp's filter State is
+    its block's history."""
+    bq = os.path.join(os.path.dirname(HERE), "dsp-bench_amd", "plugins", "biquad.cpp")
+    assert facts_of(bq)["state_reads_block"] is True
+    sine = os.path.join(REF, "build/sine_test.cpp")
+    if os.path.exists(sine):
+        assert facts_of(sine)["state_reads_block"] is False
