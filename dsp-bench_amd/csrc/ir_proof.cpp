@@ -42,6 +42,7 @@
 
 #include <amd_comgr/amd_comgr.h>
 
+#include <cctype>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -1122,6 +1123,105 @@ int compile_to_ir(const std::string &tu, const std::vector<std::pair<std::string
         *log = "comgr returned no IR text";
         return -1;
     }
+    return 0;
+}
+
+// ---------------------------------------------------------------------------
+int strip_chain_block_stores(std::string *ir) {
+    std::istringstream in(*ir);
+    std::vector<std::string> lines;
+    for (std::string l; std::getline(in, l);) lines.push_back(l);
+    auto name_at = [](const std::string &l, size_t p) {  // %name starting at p
+        size_t e = p + 1;
+        while (e < l.size() && (std::isalnum((unsigned char)l[e]) || l[e] == '_' || l[e] == '.' || l[e] == '-')) ++e;
+        return l.substr(p, e - p);
+    };
+    int dropped = 0;
+    std::vector<char> keep(lines.size(), 1);
+    for (size_t i = 0; i < lines.size(); ++i) {
+        if (lines[i].compare(0, 6, "define") != 0 || lines[i].find("@dspb_seg_chain_") == std::string::npos) continue;
+        size_t end = i;
+        while (end < lines.size() && lines[end] != "}") ++end;
+        std::set<std::string> blk;
+        for (size_t k = i; k < end; ++k) {
+            const std::string &l = lines[k];
+            const size_t p = l.find("%dspb_chain_blk");
+            if (p != std::string::npos && l.find(" = alloca ") != std::string::npos && l.find('%') == p)
+                blk.insert(name_at(l, p));
+        }
+        for (bool grew = true; grew && !blk.empty();) {  // pointers derived from the block
+            grew = false;
+            for (size_t k = i; k < end; ++k) {
+                const std::string &l = lines[k];
+                const size_t eq = l.find(" = ");
+                if (eq == std::string::npos) continue;
+                const size_t p0 = l.find('%');
+                if (p0 == std::string::npos || p0 > eq) continue;
+                const std::string res = name_at(l, p0);
+                if (blk.count(res)) continue;
+                const std::string rhs = l.substr(eq + 3);
+                if (rhs.compare(0, 13, "getelementptr") && rhs.compare(0, 3, "phi") && rhs.compare(0, 6, "select") &&
+                    rhs.compare(0, 13, "addrspacecast") && rhs.compare(0, 7, "bitcast"))
+                    continue;
+                for (size_t q = rhs.find('%'); q != std::string::npos; q = rhs.find('%', q + 1))
+                    if (blk.count(name_at(rhs, q))) {
+                        blk.insert(res);
+                        grew = true;
+                        break;
+                    }
+            }
+        }
+        for (size_t k = i; k < end && !blk.empty(); ++k) {
+            const std::string &l = lines[k];
+            const size_t st = l.find_first_not_of(' ');
+            if (st == std::string::npos || l.compare(st, 6, "store ") != 0 || l.find("!nontemporal") != std::string::npos)
+                continue;
+            const size_t p = l.find("ptr addrspace(5) %");
+            if (p != std::string::npos && blk.count(name_at(l, p + 17))) {
+                keep[k] = 0;
+                ++dropped;
+            }
+        }
+        i = end;
+    }
+    if (dropped) {
+        std::string o;
+        o.reserve(ir->size());
+        for (size_t i = 0; i < lines.size(); ++i)
+            if (keep[i]) o += lines[i], o += '\n';
+        *ir = o;
+    }
+    return dropped;
+}
+
+int codegen_ir(const std::string &ir, const std::vector<std::string> &options, std::string *code, std::string *log) {
+    Comgr c;
+    amd_comgr_data_set_t exe{};
+    if (amd_comgr_create_data_set(&c.in)) return *log = "comgr: data set", -1;
+    c.have_in = true;
+    if (amd_comgr_create_data_set(&c.out)) return *log = "comgr: data set", -1;
+    c.have_out = true;
+    if (amd_comgr_create_data_set(&exe)) return *log = "comgr: data set", -1;
+    struct Drop {
+        amd_comgr_data_set_t s;
+        ~Drop() { amd_comgr_destroy_data_set(s); }
+    } drop{exe};
+    if (!add_data(c.in, AMD_COMGR_DATA_KIND_BC, ir, "dspb_chain.ll")) return *log = "comgr: input", -1;
+    if (amd_comgr_create_action_info(&c.ai)) return *log = "comgr: action info", -1;
+    c.have_ai = true;
+    std::vector<const char *> opts;
+    for (const auto &o : options) opts.push_back(o.c_str());
+    if (amd_comgr_action_info_set_isa_name(c.ai, "amdgcn-amd-amdhsa--gfx950") ||
+        amd_comgr_action_info_set_option_list(c.ai, opts.data(), opts.size()) ||
+        amd_comgr_action_info_set_logging(c.ai, true))
+        return *log = "comgr: options", -1;
+    if (amd_comgr_do_action(AMD_COMGR_ACTION_CODEGEN_BC_TO_RELOCATABLE, c.ai, c.in, c.out) ||
+        amd_comgr_do_action(AMD_COMGR_ACTION_LINK_RELOCATABLE_TO_EXECUTABLE, c.ai, c.out, exe)) {
+        get_data(c.out, AMD_COMGR_DATA_KIND_LOG, log);
+        if (log->empty()) *log = "comgr: codegen failed";
+        return -1;
+    }
+    if (!get_data(exe, AMD_COMGR_DATA_KIND_EXECUTABLE, code) || code->empty()) return *log = "comgr: no code", -1;
     return 0;
 }
 

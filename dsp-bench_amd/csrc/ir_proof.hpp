@@ -60,6 +60,18 @@ Facts analyze(const std::string &ir, const char *fn);
 int compile_to_ir(const std::string &tu, const std::vector<std::pair<std::string, std::string>> &includes,
                   const std::vector<std::string> &options, std::string *ir, std::string *log);
 
+// The State chain of a callback whose State never depends on its block
+// (facts: writes_state, !state_reads_block): in every `dspb_seg_chain_*`
+// function of the module's IR text, delete the stores through pointers
+// derived from the private block `dspb_chain_blk` other than the copy of the
+// input into it (non-temporal stores) -- the callback's outputs, which by
+// that fact reach no State and no branch -- so that code generation drops the
+// arithmetic that only fed them.  Returns the stores deleted.
+int strip_chain_block_stores(std::string *ir);
+
+// LLVM IR text -> a gfx950 code object (comgr: codegen at `options`, link).
+int codegen_ir(const std::string &ir, const std::vector<std::string> &options, std::string *code, std::string *log);
+
 // Facts <-> the compact text stored in a code object (dspb_callback_facts).
 std::string encode(const Facts &f);
 bool decode(const std::string &s, Facts *f);

@@ -405,6 +405,33 @@ int dsp_module_compile(const char *source, const char *name, void **code, uint64
     }
     hiprtcGetCode(prog, (char *)buf);
     hiprtcDestroyProgram(&prog);
+    // a State that never depends on the block (facts): the same translation
+    // unit through LLVM IR text, the callback's stores to the State chain's
+    // private block deleted (ir_proof.cpp strip_chain_block_stores), so the
+    // chain kernels keep only the State's arithmetic (a tremolo's phase, not
+    // its output); the hiprtc code above stands if any step fails
+    if (facts.analyzed && facts.writes_state && !facts.state_reads_block) {
+        std::string ir, clog, co;
+        int dropped = 0;
+        if (dspb::irp::compile_to_ir(tu, {{"plugin_header.h", kPluginDeviceSrc}, {"dspb_plugin_source.cpp", source}},
+                                     {"-O3", "-std=c++20", "-ffp-contract=off", "-w", "-fno-discard-value-names",
+                                      round},
+                                     &ir, &clog) == 0 &&
+            (dropped = dspb::irp::strip_chain_block_stores(&ir)) > 0 &&
+            dspb::irp::codegen_ir(ir, {"-O3", "-ffp-contract=off"}, &co, &clog) == 0) {
+            void *nb = std::malloc(co.size());
+            if (nb) {
+                std::memcpy(nb, co.data(), co.size());
+                std::free(buf);
+                buf = nb;
+                cs = co.size();
+            }
+        } else if (dropped == 0 && clog.empty()) {
+            note += "State chain: no block store to drop\n";
+        } else {
+            note += "State chain compiled from source: " + clog.substr(0, 200) + "\n";
+        }
+    }
     // the parameter descriptor, validated as the reference's JIT does
     // (compiler.cpp:944-1164): an invalid annotation fails the compile
     dspb::desc::Descriptor d;

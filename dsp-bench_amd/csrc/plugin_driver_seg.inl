@@ -542,15 +542,18 @@ __device__ static void dspb_seg_chain(const dspb_seg_args &G) {
     dspb_copy_state((void *)&st, (const void *)A.S);
     for (unsigned long long b = 0; b < A.nblocks; ++b) {
         dspb_copy_state((void *)&G.st_blk[b], (const void *)&st);
-        float blk[CC * BMAX];
+        // (named, and filled with non-temporal stores, so that the module
+        // compiler can tell the callback's stores to it apart in the IR:
+        // module.cpp compile_chain_ir)
+        float dspb_chain_blk[CC * BMAX];
         float *ptrs[CC];
 #pragma unroll
         for (unsigned c = 0; c < CC; ++c) {
-            ptrs[c] = blk + c * B;
+            ptrs[c] = dspb_chain_blk + c * B;
             const dspb_gfloat *x = (const dspb_gfloat *)A.in[c < A.in_ch ? c : 0];
             for (unsigned i = 0; i < B; ++i) {
                 const unsigned long long gi = b * B + i;
-                blk[c * B + i] = (c < A.in_ch && gi < A.L) ? x[gi] : 0.0f;
+                __builtin_nontemporal_store((c < A.in_ch && gi < A.L) ? x[gi] : 0.0f, &dspb_chain_blk[c * B + i]);
             }
         }
         audio_callback(prm, st, ptrs, CC, B, A.sr);

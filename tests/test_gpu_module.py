@@ -524,3 +524,18 @@ def test_chain_kernels_drop_the_block_of_a_phase_accumulator():
     for k in ("dspb_seg_chain_c2b512", "dspb_seg_chain_c2", "dspb_seg_chain_c1", "dspb_seg_chain_c4"):
         assert ps[k] == 0, (k, ps[k])
         assert pb[k] > 1024, (k, pb[k])
+
+
+def test_chain_kernels_of_a_tremolo_come_from_edited_ir():
+    """(CPU) A tremolo reads its block, so compiled from source its chain
+    kernels keep the block in scratch; its State never depends on the block
+    (facts.state_reads_block = 0), so dsp_module_compile builds the module
+    through IR text with the callback's block stores deleted and the chain
+    kernels keep no private memory."""
+    import sys
+    sys.path.insert(0, HERE)
+    import test_gpu_state_spec as t
+    code = d.module.compile_source(t.TREMOLO_SRC, "tremolo.cpp")
+    ps = _private_sizes(code)
+    for k in ("dspb_seg_chain_c2b512", "dspb_seg_chain_c2", "dspb_seg_chain_c1", "dspb_seg_chain_c4"):
+        assert ps[k] == 0, (k, ps[k])

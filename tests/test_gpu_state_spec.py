@@ -342,15 +342,19 @@ def test_state_chain_with_a_1kb_state(torch_cuda):
 
 
 @pytest.mark.gpu
-def test_tremolo_reading_its_block_stays_serial(torch_cuda):
-    """A tremolo reads its block: the chain kernel keeps the block in private
-    memory (more than the State there), so after learning that its phase never
-    forgets the module renders it serially -- exact either way."""
+def test_tremolo_reading_its_block_takes_the_ir_chain(torch_cuda):
+    """A tremolo reads its block, but its phase never depends on it
+    (facts.state_reads_block = 0): the module compiler builds its chain
+    kernels from IR with the callback's block stores deleted
+    (module.cpp, ir_proof.cpp strip_chain_block_stores), so the chain is the
+    phase update alone and the segments render from its States -- bit for
+    bit against the serial chain, State included."""
     mod = module_of(TREMOLO_SRC, "tremolo_spec")
+    assert mod.facts["writes_state"] and not mod.facts["state_reads_block"]
     params = mod.default_parameters()
     spec, ser, info = both(torch_cuda, mod, params, noise(2, 200_000, 12), 2, 512, calls=3)
     assert_same(spec, ser)
-    assert info[2]["disabled"] and not info[2]["chain"] and not info[2]["used"]
+    assert info[0]["chain"] and info[2]["disabled"] and info[2]["chain"] and info[2]["used"]
 
 
 @pytest.mark.gpu
