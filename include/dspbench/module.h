@@ -221,7 +221,10 @@ int dsp_module_retired_tables(dsp_module *m, uint64_t *n);
  * (its block a private array nothing reads, so the compiler drops the block
  * arithmetic) and records each block's State, then every segment renders from
  * its recorded State at once -- when the compiled chain kernel needs no
- * scratch for the block (a State that depends on the block renders serially).
+ * scratch for the block (a State that depends on the block renders serially;
+ * for a callback that reads its block while its State ignores it,
+ * dsp_callback_facts.state_reads_block = 0, dsp_module_compile builds the
+ * chain kernels from the callback's IR with its block stores deleted).
  * DSP_EXEC_SERIAL_STATE (dspbench.h) forces the serial chain. */
 typedef struct dsp_state_spec_info {
     int32_t used;                /* the module's last State-writing render ran in segments */
