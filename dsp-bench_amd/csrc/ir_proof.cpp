@@ -1174,13 +1174,34 @@ int strip_chain_block_stores(std::string *ir) {
         for (size_t k = i; k < end && !blk.empty(); ++k) {
             const std::string &l = lines[k];
             const size_t st = l.find_first_not_of(' ');
-            if (st == std::string::npos || l.compare(st, 6, "store ") != 0 || l.find("!nontemporal") != std::string::npos)
-                continue;
-            const size_t p = l.find("ptr addrspace(5) %");
-            if (p != std::string::npos && blk.count(name_at(l, p + 17))) {
-                keep[k] = 0;
-                ++dropped;
+            if (st == std::string::npos || l.compare(st, 6, "store ") != 0) continue;
+            // store [atomic] [volatile] <ty> <value>, ptr addrspace(5) <address>[, ...]: the
+            // address is the operand after the first comma outside brackets
+            size_t v = st + 6;
+            for (const char *kw : {"atomic ", "volatile "})
+                if (l.compare(v, std::strlen(kw), kw) == 0) v += std::strlen(kw);
+            size_t comma = std::string::npos;
+            int depth = 0;
+            for (size_t q = v; q < l.size() && comma == std::string::npos; ++q) {
+                const char ch = l[q];
+                if (ch == '(' || ch == '<' || ch == '[' || ch == '{') ++depth;
+                else if (ch == ')' || ch == '>' || ch == ']' || ch == '}') --depth;
+                else if (ch == ',' && depth == 0) comma = q;
             }
+            if (comma == std::string::npos) return -1;  // not a store this parser understands
+            const std::string value = l.substr(v, comma - v);
+            // a pointer derived from the block stored anywhere: outside the
+            // model (the analysis refuses it too); keep the hiprtc code
+            for (size_t q = value.find('%'); q != std::string::npos; q = value.find('%', q + 1))
+                if (blk.count(name_at(value, q)) && value.compare(0, 4, "ptr ") == 0) return -1;
+            size_t a = l.find_first_not_of(' ', comma + 1);
+            static const char kAddr[] = "ptr addrspace(5) %";
+            if (a == std::string::npos || l.compare(a, sizeof kAddr - 1, kAddr) != 0) continue;
+            if (!blk.count(name_at(l, a + sizeof kAddr - 2))) continue;
+            if (l.find("!nontemporal", comma) != std::string::npos) continue;  // the input's copy into the block
+            if (value.compare(0, 4, "ptr ") == 0) return -1;
+            keep[k] = 0;
+            ++dropped;
         }
         i = end;
     }

@@ -121,6 +121,7 @@ struct SegArgsG {
     unsigned mode;
     unsigned pass;
     unsigned exact;
+    unsigned long long perturb;
 };
 
 // kDriver / kSegDriver: the driver kernels (csrc/plugin_driver.inl) and the
@@ -178,6 +179,10 @@ struct dsp_module {
         bool serial = false;           // the module's last State-writing render was the serial chain
         uint32_t warm = 0;             // learned warm-up for `params` (0: not yet)
         bool off = false;              // learned: the chain does not forget its State
+        bool chain_bad = false;        // learned: the State chain's records failed their check
+        uint64_t gen = 0;              // bumped when `params` change (learn only from renders with them)
+        uint64_t slot_gen[2] = {};
+        uint64_t perturb = 0;          // dsp_module_debug: the next State chain's wrong record (block + 1)
         std::vector<unsigned char> params;
     } seg;
     hipFunction_t f_sizes = nullptr, f_defaults = nullptr, f_init = nullptr, f_render = nullptr,
@@ -324,7 +329,7 @@ std::string plugin_prelude() {
 // flattened analysis kernel, at -O2 without vectorisation or unrolling (the
 // same IEEE semantics as the module's -O3 code; scalar IR is what the
 // analysis reads), with the module compile's language options.
-dspb::irp::Facts analyze_source(const char *source) {
+dspb::irp::Facts analyze_source(const char *source, bool shipped = false) {
     static const char *kProof =
         "extern \"C\" __global__ __attribute__((flatten)) void dspb_proof(Parameters *P, State *S, float **out, "
         "unsigned C, unsigned B, float sr) { audio_callback(*P, *S, out, C, B, sr); }\n";
@@ -332,8 +337,10 @@ dspb::irp::Facts analyze_source(const char *source) {
     std::string ir, log;
     const int rc = dspb::irp::compile_to_ir(plugin_prelude() + kProof,
                                             {{"plugin_header.h", kPluginDeviceSrc}, {"dspb_plugin_source.cpp", source}},
-                                            {"-O2", "-std=c++20", "-ffp-contract=off", "-w", "-fno-vectorize",
-                                             "-fno-slp-vectorize", "-fno-unroll-loops"},
+                                            shipped ? std::vector<std::string>{"-O3", "-std=c++20", "-ffp-contract=off", "-w"}
+                                                    : std::vector<std::string>{"-O2", "-std=c++20", "-ffp-contract=off", "-w",
+                                                                               "-fno-vectorize", "-fno-slp-vectorize",
+                                                                               "-fno-unroll-loops"},
                                             &ir, &log);
     if (rc != 0) {
         f.why = "the analysis compile failed: " + log.substr(0, 300);
@@ -426,6 +433,8 @@ int dsp_module_compile(const char *source, const char *name, void **code, uint64
                 buf = nb;
                 cs = co.size();
             }
+        } else if (dropped < 0) {
+            note += "State chain: a store outside the block-store model, compiled from source\n";
         } else if (dropped == 0 && clog.empty()) {
             note += "State chain: no block store to drop\n";
         } else {
@@ -616,7 +625,34 @@ int dsp_module_state_spec(dsp_module *m, dsp_state_spec_info *out) {
     std::lock_guard<std::mutex> lk(m->mu);
     if (int st = dspb::module_seg_collect(m, true)) return st;
     *out = m->seg.serial ? dsp_state_spec_info{} : m->seg.last;
-    out->disabled = m->seg.off ? 1 : 0;
+    out->disabled = (m->seg.off || m->seg.chain_bad) ? 1 : 0;
+    return DSP_OK;
+}
+
+int dsp_ir_strip_chain_stores(const char *ir, char *out, uint64_t out_cap, int32_t *dropped) {
+    if (!ir || !dropped) {
+        set_last_error("dsp_ir_strip_chain_stores: NULL argument");
+        return DSP_ERR_INVALID;
+    }
+    std::string t(ir);
+    *dropped = dspb::irp::strip_chain_block_stores(&t);
+    if (out && out_cap) {
+        if (t.size() + 1 > out_cap) {
+            set_last_error("dsp_ir_strip_chain_stores: %llu bytes needed", (unsigned long long)t.size() + 1);
+            return DSP_ERR_INVALID;
+        }
+        std::memcpy(out, t.c_str(), t.size() + 1);
+    }
+    return DSP_OK;
+}
+
+int dsp_module_debug(dsp_module *m, int what, uint64_t value) {
+    if (!m || what != DSP_MODULE_DEBUG_PERTURB_CHAIN || value == ~0ull) {
+        set_last_error("dsp_module_debug: unknown hook");
+        return DSP_ERR_INVALID;
+    }
+    std::lock_guard<std::mutex> lk(m->mu);
+    m->seg.perturb = value + 1;
     return DSP_OK;
 }
 
@@ -871,6 +907,15 @@ int dsp_plugin_analyze(const char *source, dsp_callback_facts *out) {
     return DSP_OK;
 }
 
+int dsp_plugin_analyze_shipped(const char *source, dsp_callback_facts *out) {
+    if (!source || !out) {
+        set_last_error("dsp_plugin_analyze_shipped: NULL argument");
+        return DSP_ERR_INVALID;
+    }
+    facts_out(analyze_source(source, true), true, out);
+    return DSP_OK;
+}
+
 int dsp_module_read_state(const dsp_module *m, void *state) {
     if (!m || (!state && m->state_size)) return DSP_ERR_INVALID;
     if (int st = wait_uses(const_cast<dsp_module *>(m))) return st;
@@ -965,21 +1010,30 @@ int module_seg_collect(dsp_module *m, bool wait) {
         const unsigned *h = W.h_stats + 16 * i;  // [0, 4) levels, [4] [5] reruns, [7] walk, [8, 12) levels run,
                                                  // [12] the State chain ran
         const uint32_t first_warm = r.warmup_blocks;
+        const bool spec = r.levels > 0;  // a speculative render (else the learnt State chain alone)
         uint32_t last = 0, warm = first_warm;
         for (uint32_t L = 1; L < r.levels && h[8 + L]; ++L) {
             last = L;
             warm = std::min<uint32_t>(warm * 16, kSegWarmMax);
         }
-        r.levels = last + 1;
-        r.warmup_blocks = warm;
-        r.differed[0] = h[last];
-        r.differed[1] = h[4];
-        r.differed[2] = h[5];
+        if (spec) {
+            r.levels = last + 1;
+            r.warmup_blocks = warm;
+            r.differed[0] = h[last];
+            r.differed[1] = h[4];
+            r.differed[2] = h[5];
+        }
         r.serial_reruns = h[7];
-        r.chain = h[12] ? 1 : 0;
+        r.chain = (h[12] || !spec) ? 1 : 0;
+        r.chain_mismatch = h[13];
+        r.chain_records_differed = h[14];
         if (W.seq[i] == W.calls) W.last = r;
+        if (W.slot_gen[i] != W.gen) continue;  // rendered with other Parameters: nothing to learn
+        // the chain's records failed their check (the walk rendered the call
+        // right): these Parameters render serially from now on
+        if (r.chain && (r.chain_mismatch || r.chain_records_differed)) W.off = W.chain_bad = true;
         // learn only from renders that started with the warm-up now in force
-        if (first_warm != W.warm || W.off) continue;
+        if (!spec || first_warm != W.warm || W.off) continue;
         const uint64_t early = std::min<uint64_t>(r.segments - 1, warm / r.blocks_per_segment);
         const uint64_t guessed = r.segments - 1 - early;
         if (guessed && r.differed[0] * 8ull > guessed) W.off = true;  // the longest warm-up it could try failed
@@ -1084,88 +1138,101 @@ static int module_render_seg(dsp_module *m, RenderArgsG &A, hipStream_t s, bool 
     void *args[] = {&G};
     const unsigned lds = (unsigned)(nb * stride * sizeof(float));
     const unsigned gseg = (unsigned)((K + nb - 1) / nb), gchk = (unsigned)((K + 3) / 4);  // 4 segments per 256 threads
+    G.perturb = chain || fc ? W.perturb : 0;  // (test hook: consumed by the render that may run a chain)
+    if (G.perturb) W.perturb = 0;
+    MOD_HIP(hipMemsetAsync(W.words, 0, 32 * sizeof(unsigned), s));
+    // the State chain's records checked: every boundary against the State the
+    // segment before ended with (stats[13]), then the walk renders serially
+    // from the true State whatever differs and writes the live State
+    auto checked = [&](unsigned exact) -> int {
+        G.exact = exact;
+        G.mode = 0;
+        G.pass = 13;
+        G.level = 0xffffffffu;
+        MOD_HIP(hipModuleLaunchKernel(m->f_seg_check, gchk, 1, 1, 256, 1, 1, 0, s, args, nullptr));
+        MOD_HIP(hipModuleLaunchKernel(fw, 1, 1, 1, 256, 1, 1, (unsigned)(2ull * C * B * sizeof(float)), s, args,
+                                      nullptr));
+        return DSP_OK;
+    };
+    uint32_t levels = 0;
     if (chain) {
-        MOD_HIP(hipModuleLaunchKernel(fc, 1, 1, 1, 64, 1, 1, 0, s, args, nullptr));
         G.mode = 1;
+        MOD_HIP(hipModuleLaunchKernel(fc, 1, 1, 1, 64, 1, 1, 0, s, args, nullptr));
         G.exact = 1;
         MOD_HIP(hipModuleLaunchKernel(fr, gseg, 1, 1, 256, 1, 1, lds, s, args, nullptr));
-        W.last = dsp_state_spec_info{};
-        W.last.used = 1;
-        W.last.segments = (uint32_t)K;
-        W.last.blocks_per_segment = (uint32_t)seg;
-        W.last.chain = 1;
-        ++W.calls;  // an older speculative render's counters no longer name the last render
-        MOD_HIP(hipEventRecord(m->use_ev, s));
-        return DSP_OK;
-    }
-    MOD_HIP(hipMemsetAsync(W.words, 0, 32 * sizeof(unsigned), s));
-    // pass 1 and its check at the learnt warm-up, then at 16x longer ones
-    // while too many segments started wrong (each level decides on the GPU
-    // whether it runs: dspb_seg_level_runs)
-    uint32_t warm = W.warm, prev = 0, levels = 0;
-    G.count = W.words;
-    for (uint32_t L = 0; L < kSegLevels; ++L) {
-        if (L > 0) {
-            const uint32_t next = std::min<uint32_t>(warm * 16, kSegWarmMax);
-            if (next <= warm || 2ull * next >= A.nblocks) break;  // no longer, or as long as the file
-            // with a State chain to fall back on, a level whose rounds (its
-            // warm-up and a segment of full callbacks) exceed 1/16 of the
-            // file costs more than the chain (the State arithmetic alone over
-            // every block) is likely to: not tried
-            if (fc && 16ull * (next + seg) > A.nblocks) break;
-            prev = warm;
-            warm = next;
+        if (int st = checked(1)) return st;
+    } else {
+        // pass 1 and its check at the learnt warm-up, then at 16x longer ones
+        // while too many segments started wrong (each level decides on the GPU
+        // whether it runs: dspb_seg_level_runs)
+        uint32_t warm = W.warm, prev = 0;
+        G.count = W.words;
+        for (uint32_t L = 0; L < kSegLevels; ++L) {
+            if (L > 0) {
+                const uint32_t next = std::min<uint32_t>(warm * 16, kSegWarmMax);
+                if (next <= warm || 2ull * next >= A.nblocks) break;  // no longer, or as long as the file
+                // with a State chain to fall back on, a level whose rounds (its
+                // warm-up and a segment of full callbacks) exceed 1/16 of the
+                // file costs more than the chain (the State arithmetic alone over
+                // every block) is likely to: not tried
+                if (fc && 16ull * (next + seg) > A.nblocks) break;
+                prev = warm;
+                warm = next;
+            }
+            G.level = L;
+            G.warm = warm;
+            G.prev_warm = prev;
+            G.mode = 0;
+            MOD_HIP(hipModuleLaunchKernel(f, gseg, 1, 1, 256, 1, 1, lds, s, args, nullptr));
+            G.pass = L;
+            G.mode = 1;  // the check lists the differing segments for the rerun
+            MOD_HIP(hipModuleLaunchKernel(m->f_seg_check, gchk, 1, 1, 256, 1, 1, 0, s, args, nullptr));
+            ++levels;
         }
-        G.level = L;
-        G.warm = warm;
-        G.prev_warm = prev;
-        G.mode = 0;
-        MOD_HIP(hipModuleLaunchKernel(f, gseg, 1, 1, 256, 1, 1, lds, s, args, nullptr));
-        G.pass = L;
-        G.mode = 1;  // the check lists the differing segments for the rerun
-        MOD_HIP(hipModuleLaunchKernel(m->f_seg_check, gchk, 1, 1, 256, 1, 1, 0, s, args, nullptr));
-        ++levels;
-    }
-    // the last level failed (decided on the GPU): the State chain and the
-    // exact rerun take over, the reruns and the walk below return at once
-    if (fc) {
-        G.level = levels;
-        G.prev_warm = warm;
-        G.mode = 2;
-        MOD_HIP(hipModuleLaunchKernel(fc, 1, 1, 1, 64, 1, 1, 0, s, args, nullptr));
-    }
-    // two reruns of the listed segments, each checked; the last check only flags
-    G.level = 0xffffffffu;
-    unsigned *listing = W.words;
-    for (unsigned p = 0; p < 2; ++p) {
-        G.count = listing;
-        G.mode = 1;
-        MOD_HIP(hipModuleLaunchKernel(fr, gseg, 1, 1, 256, 1, 1, lds, s, args, nullptr));
-        G.prev_count = listing;
-        listing = W.words + 2 + p;
-        G.count = listing;
-        G.pass = 4 + p;
-        G.mode = p == 0 ? 1 : 0;
-        MOD_HIP(hipModuleLaunchKernel(m->f_seg_check, gchk, 1, 1, 256, 1, 1, 0, s, args, nullptr));
-    }
-    MOD_HIP(hipModuleLaunchKernel(fw, 1, 1, 1, 256, 1, 1, (unsigned)(2ull * C * B * sizeof(float)), s, args,
-                                  nullptr));
-    if (fc) {
-        G.mode = 1;
-        G.exact = 2;
-        MOD_HIP(hipModuleLaunchKernel(fr, gseg, 1, 1, 256, 1, 1, lds, s, args, nullptr));
+        // the last level failed (decided on the GPU): the State chain and the
+        // exact rerun take over, the reruns and the walk below return at once
+        if (fc) {
+            G.level = levels;
+            G.prev_warm = warm;
+            G.mode = 2;
+            MOD_HIP(hipModuleLaunchKernel(fc, 1, 1, 1, 64, 1, 1, 0, s, args, nullptr));
+        }
+        // two reruns of the listed segments, each checked; the last check only flags
+        G.level = 0xffffffffu;
+        unsigned *listing = W.words;
+        for (unsigned p = 0; p < 2; ++p) {
+            G.count = listing;
+            G.mode = 1;
+            MOD_HIP(hipModuleLaunchKernel(fr, gseg, 1, 1, 256, 1, 1, lds, s, args, nullptr));
+            G.prev_count = listing;
+            listing = W.words + 2 + p;
+            G.count = listing;
+            G.pass = 4 + p;
+            G.mode = p == 0 ? 1 : 0;
+            MOD_HIP(hipModuleLaunchKernel(m->f_seg_check, gchk, 1, 1, 256, 1, 1, 0, s, args, nullptr));
+        }
+        MOD_HIP(hipModuleLaunchKernel(fw, 1, 1, 1, 256, 1, 1, (unsigned)(2ull * C * B * sizeof(float)), s, args,
+                                      nullptr));
+        if (fc) {  // (each returns at once unless the chain ran)
+            G.mode = 1;
+            G.exact = 2;
+            MOD_HIP(hipModuleLaunchKernel(fr, gseg, 1, 1, 256, 1, 1, lds, s, args, nullptr));
+            if (int st = checked(2)) return st;
+        }
     }
     MOD_HIP(hipMemcpyAsync(W.h_stats + 16 * slot, W.words + 8, 16 * sizeof(unsigned), hipMemcpyDeviceToHost, s));
     MOD_HIP(hipEventRecord(W.ev[slot], s));
     W.pending[slot] = true;
     W.seq[slot] = ++W.calls;
+    W.slot_gen[slot] = W.gen;
     dsp_state_spec_info &r = W.info[slot];
     r = dsp_state_spec_info{};
     r.used = 1;
     r.segments = (uint32_t)K;
     r.blocks_per_segment = (uint32_t)seg;
-    r.warmup_blocks = W.warm;  // the first level's; module_seg_collect names the one that stood
-    r.levels = levels;
+    r.warmup_blocks = chain ? 0 : W.warm;  // the first level's; module_seg_collect names the one that stood
+    r.levels = levels;                     // 0: the learnt State chain alone
+    r.chain = chain ? 1 : 0;
     MOD_HIP(hipEventRecord(m->use_ev, s));
     return DSP_OK;
 }
@@ -1268,10 +1335,12 @@ int module_render(dsp_module *m, const void *params, uint32_t params_size, const
         if (!W.warm || W.params.size() != params_size || (params_size && std::memcmp(W.params.data(), pb, params_size))) {
             W.params.assign(pb, pb + params_size);  // new Parameters: learn again
             W.warm = kSegWarm0;
-            W.off = false;
+            W.off = W.chain_bad = false;
+            ++W.gen;
         }
         // (learned never to forget: the State chain, then the segments exactly)
-        const int st = module_render_seg(m, A, s, W.off);
+        // (the chain's records failed their check once: the serial chain)
+        const int st = W.chain_bad ? 1 : module_render_seg(m, A, s, W.off);
         W.serial = st > 0;
         if (st <= 0) return st;
     }

@@ -32,7 +32,10 @@ struct dspb_seg_args {
     unsigned char *flags;   // the last check: 1 = differed
     unsigned *stats;        // [0, 4) segments that differed per warm-up level, [4] / [5] after
                             // rerun 1 / 2, [7] serial reruns of the walk, [8, 12) levels run,
-                            // [12] the State chain took over from the levels (dspb_seg_chain)
+                            // [12] the State chain took over from the levels (dspb_seg_chain),
+                            // [13] segments whose first State (the chain's record) differed from
+                            // the State the segment before ended with, [14] blocks whose State in
+                            // the exact rerun differed from the chain's record
     unsigned long long seg; // blocks per segment
     unsigned K;             // segments
     unsigned warm;          // pass 1: warm-up blocks
@@ -42,11 +45,20 @@ struct dspb_seg_args {
                             // check: 1 = list the differing ones for a rerun (0: flag only)
     unsigned pass;          // the check's stats slot
     unsigned exact;         // a rerun of every segment from the States the chain kernel recorded
-                            // (dspb_seg_chain): no list, no early stop (2: only if the chain ran)
+                            // (dspb_seg_chain): no list, no early stop (2: only if the chain ran);
+                            // the check and the walk after it: every segment boundary
+    unsigned long long perturb;  // test hook (dsp_module_debug): the chain kernel flips a bit of the
+                                 // State it recorded for block perturb - 1 (0: none)
 };
 // the State chain took over within this render: the reruns, their checks and
 // the walk have nothing to do
 __device__ static bool dspb_seg_chained(const dspb_seg_args &G) { return *(volatile unsigned *)&G.stats[12] != 0; }
+// a rerun, check or walk launch with nothing to do: those after the State
+// chain (G.exact: 1 always, 2 only when the chain ran in this render) and the
+// speculative ones (only when it did not)
+__device__ static bool dspb_seg_skip(const dspb_seg_args &G) {
+    return G.exact ? (G.exact == 2 && !dspb_seg_chained(G)) : dspb_seg_chained(G);
+}
 // pass 1 at warm-up level L > 0 (and its check) runs only when level L - 1
 // ran and more than 1/8 of the segments it guessed -- those whose warm-up
 // began after block 0 -- started from a State that was not the true one: the
@@ -116,7 +128,17 @@ template <bool kRerun>
 __device__ static bool dspb_seg_block(const dspb_seg_args &G, unsigned long long b, unsigned r, unsigned w,
                                       State &st) {
     if (r < w) return true;  // warm-up: nothing kept
-    if (kRerun && G.exact) return true;  // rendered from the chain's own States
+    if (kRerun && G.exact) {
+        // from the chain's record of the segment's first State: the record of
+        // every later block is checked against the State the callback renders
+        // it from, and takes that State (so the walk after the boundary check
+        // stops only where it meets what was rendered here)
+        if (r > 0 && !dspb_same_state(&st, &G.st_blk[b])) {
+            atomicAdd(&G.stats[14], 1u);
+            dspb_copy_state((void *)&G.st_blk[b], (const void *)&st);
+        }
+        return true;
+    }
     if (kRerun && r > 0 && dspb_same_state(&st, &G.st_blk[b])) return false;
     dspb_copy_state((void *)&G.st_blk[b], (const void *)&st);
     return true;
@@ -136,7 +158,7 @@ __device__ static void dspb_segments(const dspb_seg_args &G) {
     if (!G.mode) {  // pass 1: at a warm-up level that runs; it restarts the listing
         if (!dspb_seg_level_runs(G)) return;
         if (G.level && blockIdx.x == 0 && t == 0) *G.count = 0;
-    } else if (G.exact ? (G.exact == 2 && !dspb_seg_chained(G)) : dspb_seg_chained(G)) {
+    } else if (dspb_seg_skip(G)) {
         return;
     }
     const unsigned nseg = (G.mode && !G.exact) ? *(volatile unsigned *)G.count : G.K;
@@ -150,7 +172,8 @@ __device__ static void dspb_segments(const dspb_seg_args &G) {
     State st;
     bool stopped = false;
     if (k != 0xffffffffu)
-        dspb_copy_state((void *)&st, G.mode ? (const void *)&G.st_blk[(unsigned long long)k * G.seg] : (const void *)A.S);
+        dspb_copy_state((void *)&st, (G.mode && (k || !G.exact)) ? (const void *)&G.st_blk[(unsigned long long)k * G.seg]
+                                                                 : (const void *)A.S);
     // the channels' rows in LDS (an access by a lane-dependent channel reads
     // them there, not from the argument block in memory)
     __shared__ const float *s_in[16];
@@ -235,7 +258,7 @@ __device__ static void dspb_segments_pf(const dspb_seg_args &G) {
     if (!kRerun) {  // pass 1: at a warm-up level that runs; it restarts the listing
         if (!dspb_seg_level_runs(G)) return;
         if (G.level && blockIdx.x == 0 && t == 0) *G.count = 0;
-    } else if (G.exact ? (G.exact == 2 && !dspb_seg_chained(G)) : dspb_seg_chained(G)) {
+    } else if (dspb_seg_skip(G)) {
         return;
     }
     const unsigned nseg = (kRerun && !G.exact) ? *(volatile unsigned *)G.count : G.K;
@@ -261,7 +284,8 @@ __device__ static void dspb_segments_pf(const dspb_seg_args &G) {
     State st;
     bool stopped = false;
     if (k != 0xffffffffu)
-        dspb_copy_state((void *)&st, kRerun ? (const void *)&G.st_blk[(unsigned long long)k * G.seg] : (const void *)A.S);
+        dspb_copy_state((void *)&st, (kRerun && (k || !G.exact)) ? (const void *)&G.st_blk[(unsigned long long)k * G.seg]
+                                                                  : (const void *)A.S);
     // a constant B prefetches a whole round (PB = PV) while the callbacks run;
     // a runtime B stages in batches of 4 float4 per channel at the round's
     // start (a whole round's registers would spill)
@@ -376,8 +400,12 @@ DSPB_SEG_KERNEL(dspb_seg, 0, 0)
 // the State's words; a check after a pass that found nothing to rerun
 // returns at once (nothing changed: the flags stand).
 extern "C" __global__ void dspb_seg_check(dspb_seg_args G) {
-    if (dspb_seg_chained(G)) return;
-    if (G.level != 0xffffffffu) {  // pass 1's check: where pass 1 ran
+    if (dspb_seg_skip(G)) return;
+    if (G.exact) {
+        // after the State chain's exact rerun: every boundary, the chain's
+        // record of a segment's first State against the State the segment
+        // before ended with (the chain is checked, not trusted)
+    } else if (G.level != 0xffffffffu) {  // pass 1's check: where pass 1 ran
         if (!dspb_seg_level_runs(G)) return;
         if (blockIdx.x == 0 && threadIdx.x == 0) G.stats[8 + G.level] = 1;
     } else if (*(volatile unsigned *)G.prev_count == 0) {
@@ -428,7 +456,7 @@ __device__ static void dspb_seg_walk(const dspb_seg_args &G) {
     __shared__ int s_bad, s_stop;
     __shared__ unsigned long long s_prev[(sizeof(State) + 7) / 8];  // the predecessor's final State
     const dspb_render_args &A = G.R;
-    if (dspb_seg_chained(G)) return;  // the same for the whole workgroup
+    if (dspb_seg_skip(G)) return;  // the same for the whole workgroup
     const unsigned B = NB_ ? NB_ : A.B, C = CC ? CC : A.C, CB = C * B, t = threadIdx.x, nt = blockDim.x;
     float *buf0 = dspb_lbuf, *buf1 = dspb_lbuf + CB;
     Parameters prm = dspb_from_global<Parameters>(A.P);
@@ -526,7 +554,12 @@ DSPB_WALK_KERNEL(dspb_seg_walk_any, 0, 0)
 // render (G.mode 2) the chain runs only when the last warm-up level tried
 // failed (dspb_seg_level_runs on the level after it), and says so in
 // stats[12]: the reruns and the walk then return at once, and the exact
-// rerun (G.exact 2) renders the segments.
+// rerun (G.exact 2) renders the segments.  The chain is checked, not trusted:
+// the exact rerun compares every block's record with the State it renders the
+// block from, a check compares every segment's first State with the State the
+// segment before ended with, and the walk renders serially from the true
+// State whatever differs (stats[13], [14]: the host then stops taking the
+// chain for these Parameters).
 template <unsigned CC, unsigned BB>
 __device__ static void dspb_seg_chain(const dspb_seg_args &G) {
     const dspb_render_args &A = G.R;
@@ -558,7 +591,12 @@ __device__ static void dspb_seg_chain(const dspb_seg_args &G) {
         }
         audio_callback(prm, st, ptrs, CC, B, A.sr);
     }
-    dspb_copy_state((void *)A.S, (const void *)&st);
+    // (the live State is written by the walk after the check, from the States
+    // the exact rerun rendered with, not from this chain's)
+    if (G.perturb && G.perturb - 1 < A.nblocks) {  // test hook: a wrong record (high bit of the first word)
+        constexpr unsigned kByte = (sizeof(State) < 8 ? sizeof(State) : 8) - 1;
+        ((unsigned char *)&G.st_blk[G.perturb - 1])[kByte] ^= 0x40u;
+    }
 }
 #define DSPB_CHAIN_KERNEL(name, CC, BB)                                                \
     extern "C" __global__ __launch_bounds__(64) void name(dspb_seg_args G) { dspb_seg_chain<CC, BB>(G); }

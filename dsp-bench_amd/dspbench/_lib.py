@@ -115,13 +115,16 @@ class dsp_callback_facts(C.Structure):  # module.h
 class dsp_state_spec_info(C.Structure):  # module.h
     _fields_ = [("used", C.c_int32), ("disabled", C.c_int32), ("segments", C.c_uint32),
                 ("blocks_per_segment", C.c_uint32), ("warmup_blocks", C.c_uint32), ("differed", C.c_uint32 * 3),
-                ("serial_reruns", C.c_uint32), ("levels", C.c_uint32), ("chain", C.c_int32)]
+                ("serial_reruns", C.c_uint32), ("levels", C.c_uint32), ("chain", C.c_int32),
+                ("chain_mismatch", C.c_uint32), ("chain_records_differed", C.c_uint32)]
 
     def as_dict(self) -> dict:
         return {"used": bool(self.used), "disabled": bool(self.disabled), "segments": int(self.segments),
                 "blocks_per_segment": int(self.blocks_per_segment), "warmup_blocks": int(self.warmup_blocks),
                 "differed": [int(v) for v in self.differed], "serial_reruns": int(self.serial_reruns),
-                "levels": int(self.levels), "chain": bool(self.chain)}
+                "levels": int(self.levels), "chain": bool(self.chain),
+                "chain_mismatch": int(self.chain_mismatch),
+                "chain_records_differed": int(self.chain_records_differed)}
 
 
 # name -> (restype, argtypes)
@@ -176,7 +179,10 @@ _SIGS = {
                                          C.POINTER(C.c_int32), C.POINTER(C.c_float), C.POINTER(dsp_exec)]),
     "dsp_module_facts": (C.c_int, [C.c_void_p, C.POINTER(dsp_callback_facts)]),
     "dsp_module_state_spec": (C.c_int, [C.c_void_p, C.POINTER(dsp_state_spec_info)]),
+    "dsp_module_debug": (C.c_int, [C.c_void_p, C.c_int, C.c_uint64]),
+    "dsp_ir_strip_chain_stores": (C.c_int, [C.c_char_p, C.c_char_p, C.c_uint64, C.POINTER(C.c_int32)]),
     "dsp_plugin_analyze": (C.c_int, [C.c_char_p, C.POINTER(dsp_callback_facts)]),
+    "dsp_plugin_analyze_shipped": (C.c_int, [C.c_char_p, C.POINTER(dsp_callback_facts)]),
     "dsp_code_facts": (C.c_int, [C.c_void_p, C.c_uint64, C.POINTER(dsp_callback_facts)]),
     "dsp_descriptor_from_code": (C.c_int, [C.c_void_p, C.c_uint64, C.POINTER(C.c_void_p)]),
     "dsp_descriptor_destroy": (None, [C.c_void_p]),

@@ -165,6 +165,14 @@ def analyze_source(source: str) -> dict:
     return f.as_dict()
 
 
+def analyze_source_shipped(source: str) -> dict:
+    """The same analysis of the IR the module's own options (-O3, vectorised,
+    unrolled) give (dsp_plugin_analyze_shipped; no GPU)."""
+    f = L.dsp_callback_facts()
+    check(L.lib().dsp_plugin_analyze_shipped(source.encode(), C.byref(f)), "dsp_plugin_analyze_shipped")
+    return f.as_dict()
+
+
 def code_facts(code: bytes) -> dict:
     """The facts a code object carries (dsp_code_facts; no GPU)."""
     f = L.dsp_callback_facts()
@@ -255,6 +263,12 @@ class Module:
         info = L.dsp_state_spec_info()
         check(L.lib().dsp_module_state_spec(self.handle, C.byref(info)), "dsp_module_state_spec")
         return info.as_dict()
+
+    def debug_perturb_chain(self, block: int) -> None:
+        """Test hook (dsp_module_debug DSP_MODULE_DEBUG_PERTURB_CHAIN): the
+        next render that runs the State chain records a wrong State for
+        `block`; its self-check must still render the serial chain's bits."""
+        check(L.lib().dsp_module_debug(self.handle, 1, int(block)), "dsp_module_debug")
 
     def retired_tables(self) -> int:
         """Evicted TABLE-class blocks not freed yet (dsp_module_retired_tables)."""

@@ -240,9 +240,37 @@ typedef struct dsp_state_spec_info {
                                     arithmetic dropped), then every segment from its recorded State
                                     in parallel: after its last warm-up level failed (decided on the
                                     GPU, within the call), or from the start once learnt (disabled) */
+    /* The State chain is checked, not trusted: the exact rerun compares the
+     * chain's record of every block's State with the State the callback
+     * renders that block from, a check compares every segment's first State
+     * with the State the segment before ended with, and the walk renders
+     * serially from the true State whatever differs -- the call's output and
+     * final State are the serial chain's either way.  Any difference also
+     * makes these Parameters render serially from the next call on. */
+    uint32_t chain_mismatch;     /* segments whose first State (the chain's record) differed from the
+                                    State the segment before ended with: rendered again by the walk */
+    uint32_t chain_records_differed;  /* blocks whose State in the exact rerun differed from the
+                                         chain's record */
 } dsp_state_spec_info;
 /* Waits for the module's last speculative render and describes it. */
 int dsp_module_state_spec(dsp_module *m, dsp_state_spec_info *out);
+
+/* Test hooks (not for production use).  DSP_MODULE_DEBUG_PERTURB_CHAIN: the
+ * module's next render that runs the State chain flips a high bit of the State
+ * the chain records for block `value` (a wrong record, as a miscompiled chain
+ * would make); the render must still come out equal to the serial chain, with
+ * the mismatch reported in dsp_state_spec_info. */
+enum { DSP_MODULE_DEBUG_PERTURB_CHAIN = 1 };
+int dsp_module_debug(dsp_module *m, int what, uint64_t value);
+
+/* Diagnostics (no GPU): the text pass dsp_module_compile applies to the LLVM
+ * IR of the State chain kernels of a callback whose State never reads its
+ * block (ir_proof.cpp strip_chain_block_stores).  *dropped = the stores
+ * deleted (through a pointer derived from the chain's private block
+ * `dspb_chain_blk`, other than the non-temporal copy of the input), or -1
+ * when a store is outside the pass's model (the module then keeps the hiprtc
+ * code); the edited text goes to out (out_cap bytes; NULL: not wanted). */
+int dsp_ir_strip_chain_stores(const char *ir, char *out, uint64_t out_cap, int32_t *dropped);
 
 /* ---- what the callback does with its block (no GPU) ----------------------
  * dsp_module_compile compiles the plugin a second time into an analysis
@@ -287,6 +315,11 @@ int dsp_module_facts(const dsp_module *m, dsp_callback_facts *out);
 int dsp_code_facts(const void *code, uint64_t code_size, dsp_callback_facts *out);
 /* The same analysis of plugin source text, without building a module (no GPU). */
 int dsp_plugin_analyze(const char *source, dsp_callback_facts *out);
+/* Diagnostics (no GPU): the same analysis of IR compiled with the module's own
+ * options (-O3, vectorisation and unrolling on) instead of the analysis
+ * options (-O2 without them): the facts the shipped code would give, where
+ * the analysis can read that IR (analyzed = 0 where it cannot). */
+int dsp_plugin_analyze_shipped(const char *source, dsp_callback_facts *out);
 
 #ifdef __cplusplus
 }

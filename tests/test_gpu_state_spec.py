@@ -586,3 +586,77 @@ def test_state_spec_names_the_last_render(torch_cuda):
     info = mod.state_spec()
     nb = (200_000 + 511) // 512
     assert info["segments"] == (nb + info["blocks_per_segment"] - 1) // info["blocks_per_segment"]
+
+
+def _chain_module(which, probe=False):
+    if which == "sine_test":
+        path = os.path.join(MODS, "mod_sine_test.co")
+        if not os.path.exists(path):
+            pytest.skip("reference modules not built")
+        key = ("sine_test", probe)
+        if key not in _cache:
+            with open(path, "rb") as f:
+                _cache[key] = d.module.Module(f.read())
+        return _cache[key]
+    return module_of({"osc": OSC_SRC, "tremolo": TREMOLO_SRC}[which], f"{which}_spec" + ("_probe" if probe else ""))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("which", ["sine_test", "osc", "tremolo"])
+@pytest.mark.parametrize("when,where", [("learnt", "segment_start"), ("learnt", "mid_segment"),
+                                        ("first_call", "segment_start")])
+def test_state_chain_is_checked_not_trusted(torch_cuda, which, when, where):
+    """A wrong record in the State chain (dsp_module_debug
+    DSP_MODULE_DEBUG_PERTURB_CHAIN flips a high bit of the State the chain
+    recorded for one block, as a miscompiled chain would): the exact rerun
+    compares every record with the State it renders from, a check compares
+    every segment boundary, and the walk renders serially from the true State
+    whatever differs -- the render equals the serial chain bit for bit, State
+    included, the mismatch is reported (chain_mismatch,
+    chain_records_differed), and the module renders these Parameters serially
+    from the next call on.  When the chain runs within the first call (after
+    its warm-up levels failed) and when it runs learnt, from the start."""
+    torch = torch_cuda
+    C, B, L = 2, 512, 300_000
+    x = torch.from_numpy(noise(C, L, 21)).cuda()
+    # the segment layout of this shape, from another instance of the module
+    probe = _chain_module(which, probe=True)
+    pp = probe.default_parameters()
+    probe.initialize_state(pp, C, 48000.0)
+    d.render_offline(x, C, B, 48000.0, probe.plugin(pp))
+    seg = probe.state_spec()["blocks_per_segment"]
+    assert seg >= 1
+    mod = _chain_module(which)
+    params = mod.default_parameters()
+    # forget what earlier renders taught the module: other Parameters once
+    other = bytearray(params)
+    other[0] ^= 1
+    mod.initialize_state(bytes(other), C, 48000.0)
+    d.render_offline(x[:, :B].contiguous(), C, B, 48000.0, mod.plugin(bytes(other)))
+    mod.initialize_state(params, C, 48000.0)
+    ser = mod.plugin(params, serial_state=True)
+    ref = [(d.render_offline(x, C, B, 48000.0, ser).cpu().numpy(), mod.read_state()) for _ in range(3)]
+    mod.initialize_state(params, C, 48000.0)
+    plug = mod.plugin(params)
+    perturbed = 0 if when == "first_call" else 1
+    outs, infos = [], []
+    for call in range(3):
+        if call == perturbed:
+            mod.debug_perturb_chain(7 * seg + (seg // 2 if where == "mid_segment" else 0))
+        y = d.render_offline(x, C, B, 48000.0, plug)
+        outs.append((y.cpu().numpy(), mod.read_state()))
+        infos.append(mod.state_spec())
+    assert_same(outs, ref)
+    hit = infos[perturbed]
+    assert hit["chain"] and hit["chain_records_differed"] >= 1, infos
+    if where == "segment_start":
+        # the perturbed segment and (the phase never forgets) the one after it
+        assert hit["chain_mismatch"] >= 1, infos
+    else:
+        assert hit["chain_mismatch"] == 0, infos
+    # learnt: the serial chain from then on
+    for i in infos[perturbed + 1:]:
+        assert i["disabled"] and not i["used"], infos
+    # a render before it reports nothing
+    for i in infos[:perturbed]:
+        assert i["chain_mismatch"] == 0 and i["chain_records_differed"] == 0, infos

@@ -323,3 +323,105 @@ def test_state_reads_block_of_stock_plugins():
     sine = os.path.join(REF, "build/sine_test.cpp")
     if os.path.exists(sine):
         assert facts_of(sine)["state_reads_block"] is False
+
+
+# ---- the analysis options against the shipped ones --------------------------
+# dsp_module_compile analyses the callback compiled at -O2 without
+# vectorisation or unrolling, and ships code compiled at -O3 with both.  The
+# facts that choose a render path must be the same either way: the -O3 IR
+# (dsp_plugin_analyze_shipped) gives the same facts for every plugin the tests
+# render.
+FACT_KEYS = ("analyzed", "reads_block", "writes_state", "input_control", "gain_form", "gain_table_form",
+             "state_reads_block")
+
+
+def _sources_rendered_by_the_tests():
+    import test_gpu_state_spec as ss
+    srcs = {}
+    for rel in sorted(STOCK):
+        p = os.path.join(REF, rel)
+        if os.path.exists(p):
+            srcs[rel] = open(p).read()
+    for name in sorted(os.listdir(PLUG)):
+        if name.endswith(".cpp"):
+            srcs["tests/plugins/" + name] = open(os.path.join(PLUG, name)).read()
+    srcs["plugins/biquad.cpp"] = open(os.path.join(os.path.dirname(HERE), "dsp-bench_amd", "plugins",
+                                                   "biquad.cpp")).read()
+    for name in ("ONE_POLE_SRC", "COUNTER_SRC", "OSC_SRC", "TREMOLO_SRC", "BIG_STATE_SRC", "WAVETABLE_SRC"):
+        srcs["state_spec/" + name] = getattr(ss, name)
+    for name, body in sorted(ss.GEN_BODIES.items()):
+        srcs["gen/" + name] = ss.GEN_HEAD + body
+    return srcs
+
+
+def test_analysis_facts_equal_the_shipped_o3_facts():
+    """writes_state, state_reads_block and the block-class facts from the
+    analysis compile (-O2, scalar, not unrolled) equal those read from the
+    -O3 IR the module ships, for the reference's stock plugins, every test
+    plugin, biquad.cpp and every State-writing plugin of the GPU tests."""
+    diff = []
+    srcs = _sources_rendered_by_the_tests()
+    assert len(srcs) >= 25
+    for name, src in srcs.items():
+        a, b = dm.analyze_source(src), dm.analyze_source_shipped(src)
+        if tuple(a[k] for k in FACT_KEYS) != tuple(b[k] for k in FACT_KEYS):
+            diff.append((name, {k: (a[k], b[k]) for k in FACT_KEYS if a[k] != b[k]}, b["why"][:120]))
+    assert not diff, diff
+
+
+# ---- the State chain's IR edit (ir_proof.cpp strip_chain_block_stores) ------
+CHAIN_IR = """define amdgpu_kernel void @dspb_seg_chain_c2(ptr addrspace(4) %G) {
+entry:
+  %dspb_chain_blk = alloca [1024 x float], align 4, addrspace(5)
+  %slot = alloca ptr addrspace(5), align 8, addrspace(5)
+  %st = alloca double, align 8, addrspace(5)
+  %p = getelementptr inbounds float, ptr addrspace(5) %dspb_chain_blk, i64 3
+  %q = getelementptr inbounds <2 x float>, ptr addrspace(5) %p, i64 1
+  store float 1.000000e+00, ptr addrspace(5) %p, align 4, !nontemporal !1
+  store float 2.000000e+00, ptr addrspace(5) %p, align 4
+  store <2 x float> <float 1.000000e+00, float 2.000000e+00>, ptr addrspace(5) %q, align 8
+  store double 3.000000e+00, ptr addrspace(5) %st, align 8
+  STORE_OF_A_POINTER
+  ret void
+}
+define amdgpu_kernel void @dspb_render(ptr addrspace(4) %G) {
+entry:
+  %dspb_chain_blk = alloca [4 x float], align 4, addrspace(5)
+  store float 2.000000e+00, ptr addrspace(5) %dspb_chain_blk, align 4
+  ret void
+}
+"""
+
+
+def _strip(ir):
+    import ctypes as C
+    from dspbench import _lib as L
+    out = C.create_string_buffer(len(ir) + 64)
+    n = C.c_int32()
+    assert L.lib().dsp_ir_strip_chain_stores(ir.encode(), out, len(out), C.byref(n)) == 0
+    return n.value, out.value.decode()
+
+
+def test_strip_chain_block_stores_deletes_only_block_stores():
+    """Stores through pointers derived from the chain's private block are
+    deleted (a scalar and a vector store, the vector's constant holding a
+    comma), the non-temporal copy of the input and the State store are kept,
+    and functions other than the chain kernels are left alone."""
+    n, out = _strip(CHAIN_IR.replace("  STORE_OF_A_POINTER\n", ""))
+    assert n == 2, out
+    assert "store float 2.000000e+00, ptr addrspace(5) %p" not in out
+    assert "%q, align 8" not in out
+    assert "!nontemporal" in out and "store double 3.000000e+00, ptr addrspace(5) %st" in out
+    assert "store float 2.000000e+00, ptr addrspace(5) %dspb_chain_blk" in out  # @dspb_render untouched
+
+
+def test_strip_chain_block_stores_reads_the_address_operand():
+    """A store whose VALUE is a pointer derived from the block and whose
+    address is elsewhere (the round-5 parser took the first `ptr addrspace(5)
+    %` of the line for the address, and deleted a store to another location):
+    outside the pass's model, so nothing is edited (-1: the module keeps the
+    hiprtc code)."""
+    ir = CHAIN_IR.replace("STORE_OF_A_POINTER", "store ptr addrspace(5) %p, ptr addrspace(5) %slot, align 8")
+    n, out = _strip(ir)
+    assert n == -1
+    assert out == ir
