@@ -13,7 +13,9 @@
 #include <cstdlib>
 #include <cstring>
 #include <algorithm>
+#include <atomic>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <tuple>
 #include <vector>
@@ -50,15 +52,31 @@ static int invalid(const char *fmt, ...) {
 // ---------------------------------------------------------------------------
 // per-device resources
 // ---------------------------------------------------------------------------
+// A cached device table (FIR taps and spectra, BIQUAD transition powers):
+// each call that maps it holds it until its launches are enqueued; the table
+// is freed when the cache has evicted it and no call holds it, after the
+// device has finished the work already enqueued
+typedef std::shared_ptr<float> DevTable;
+static DevTable dev_table(float *p, int dev) {
+    return DevTable(p, [dev](float *q) {
+        int prev = -1;
+        (void)hipGetDevice(&prev);
+        (void)hipSetDevice(dev);
+        (void)hipDeviceSynchronize();
+        (void)hipFree(q);
+        if (prev >= 0) (void)hipSetDevice(prev);
+    });
+}
+
 struct FirTaps {  // a FIR filter's device taps + overlap-save spectrum
     std::vector<float> taps;
-    float *dev;
+    DevTable dev;
     float h2048r, h2048i;
 };
 
 struct IirTab {  // a biquad cascade's coefficients + state-transition powers (biquad_tables)
     std::vector<float> coef;
-    float *dev;
+    DevTable dev;
     uint32_t window;  // biquad_tables' W
 };
 
@@ -66,7 +84,7 @@ struct IirTab {  // a biquad cascade's coefficients + state-transition powers (b
 // calls on one stream run in order, so a launch only meets words tagged with
 // its own epoch (zeroed at allocation; epochs run 1 .. 2^32 - 1)
 struct IirWork {
-    uint64_t *aggw = nullptr, *inclw = nullptr;  // cap * 16 words each, one allocation
+    uint64_t *aggw = nullptr, *inclw = nullptr;  // cap * 16 words each, one allocation, then the error word
     uint64_t cap = 0;
     uint64_t epoch = 0;
 };
@@ -79,12 +97,14 @@ struct DeviceRes {
     std::vector<FirTaps> fir;                                  // FIR filters seen (plugin_map)
     std::vector<IirTab> iir;                                   // biquad cascades seen (plugin_map)
     std::map<void *, IirWork> iir_work;                        // per stream
-    uint32_t *iir_err_host = nullptr, *iir_err_dev = nullptr;  // host-mapped look-back error word
+    uint32_t *iir_fb_host = nullptr, *iir_fb_dev = nullptr;  // host-mapped counter of repaired launches
     float *delta = nullptr;  // 2048 floats: 1, 0, 0, ... (compute_IR's impulse, read-only)
 };
 
 static std::mutex g_mu;
-static std::map<int, DeviceRes> g_res;
+// (never destroyed: its tables must not be freed after the HIP runtime's own
+// teardown at process exit)
+static std::map<int, DeviceRes> &g_res = *new std::map<int, DeviceRes>;
 
 static int current_device(int *dev) {
     DSPB_HIP(hipGetDevice(dev));
@@ -533,6 +553,13 @@ static uint32_t biquad_tables(const float *cf, uint32_t S, std::vector<float> &h
     return (finite && W <= 192) ? std::max<uint32_t>(W, 1) : 0u;
 }
 
+// sleeps a BIQUAD look-back waits for a predecessor's words before it gives
+// up (a legitimate wait is a few rounds: a tile waits only for waves
+// dispatched before it); the launch is then rendered again serially
+// (iir.hip biquad_repair_kernel, on the same stream)
+constexpr uint32_t kIirSpinLimit = 1u << 16;
+static std::atomic<uint32_t> g_iir_spin_limit{kIirSpinLimit};
+
 // takes the stream's workspace for one launch (a fresh epoch) and launches,
 // under one lock: launches on a stream are enqueued in epoch order
 static int iir_launch(int dev, hipStream_t s, BiquadArgs *A, uint32_t sections, uint32_t nch) {
@@ -546,20 +573,15 @@ static int iir_launch(int dev, hipStream_t s, BiquadArgs *A, uint32_t sections, 
     }
     std::lock_guard<std::mutex> lk(g_mu);
     DeviceRes &r = g_res[dev];
-    if (!r.iir_err_host) {
-        if (int st = refuse_capture(s, "the BIQUAD error word")) return st;
+    if (!r.iir_fb_host) {
+        if (int st = refuse_capture(s, "the BIQUAD repair counter")) return st;
         void *p = nullptr;
         DSPB_HIP(hipHostMalloc(&p, 64, hipHostMallocMapped));
-        r.iir_err_host = (uint32_t *)p;
-        *r.iir_err_host = 0;
+        r.iir_fb_host = (uint32_t *)p;
+        *r.iir_fb_host = 0;
         void *d = nullptr;
         DSPB_HIP(hipHostGetDevicePointer(&d, p, 0));
-        r.iir_err_dev = (uint32_t *)d;
-    }
-    if (*r.iir_err_host) {  // a launch before this one gave up its look-back
-        *r.iir_err_host = 0;
-        set_last_error("a previous BIQUAD render on this device timed out in its look-back: its output is invalid");
-        return DSP_ERR_HIP;
+        r.iir_fb_dev = (uint32_t *)d;
     }
     IirWork &w = r.iir_work[(void *)s];
     if (w.cap < tiles) {
@@ -570,7 +592,7 @@ static int iir_launch(int dev, hipStream_t s, BiquadArgs *A, uint32_t sections, 
             w = IirWork{};
         }
         const uint64_t cap = std::max<uint64_t>(tiles, 1024);
-        const size_t bytes = 2 * cap * 16 * sizeof(uint64_t);  // 16 words: a channel pair's 2 x 8
+        const size_t bytes = (2 * cap * 16 + 1) * sizeof(uint64_t);  // 16 words: a channel pair's 2 x 8
         void *p = nullptr;
         DSPB_HIP(hipMalloc(&p, bytes));
         DSPB_HIP(hipMemsetAsync(p, 0, bytes, s));
@@ -580,15 +602,19 @@ static int iir_launch(int dev, hipStream_t s, BiquadArgs *A, uint32_t sections, 
     }
     A->aggw = w.aggw;
     A->inclw = w.inclw;
-    A->err = r.iir_err_dev;
+    A->err = (uint32_t *)(w.inclw + w.cap * 16);
+    A->repairs = r.iir_fb_dev;
+    A->spin_limit = g_iir_spin_limit.load(std::memory_order_relaxed);
     w.epoch = w.epoch % 0xffffffffull + 1;
     A->epoch = w.epoch;
     if (int st = launch_biquad(*A, sections, nch, s)) return st;
     return DSP_OK;
 }
 
-static int plugin_map(const dsp_plugin *p, uint32_t B, int dev, hipStream_t s, SampleMap *m,
-                      float sr = 48000.f, uint32_t flags = 0) {
+// *table: a hold on the call's cached device table (FIR / BIQUAD), kept by
+// the caller until the call's launches are enqueued
+static int plugin_map(const dsp_plugin *p, uint32_t B, int dev, hipStream_t s, SampleMap *m, float sr,
+                      uint32_t flags, DevTable *table) {
     m->kind = MapKind::Noop;
     m->fir_direct = (flags & DSP_EXEC_FIR_DIRECT) ? 1u : 0u;
     m->a = 1.f;
@@ -649,10 +675,11 @@ static int plugin_map(const dsp_plugin *p, uint32_t B, int dev, hipStream_t s, S
         // cached per device by the taps' bytes (the host FFT and the upload
         // happen once per filter, not once per render)
         std::vector<float> key((const float *)p->params, (const float *)p->params + T);
-        FirTaps *ft = nullptr;
+        float h2048[2] = {0.f, 0.f};
         {
             std::lock_guard<std::mutex> lk(g_mu);
             DeviceRes &r = g_res[dev];
+            const FirTaps *ft = nullptr;
             for (auto &e : r.fir)
                 if (e.taps == key) { ft = &e; break; }
             if (!ft) {
@@ -670,22 +697,23 @@ static int plugin_map(const dsp_plugin *p, uint32_t B, int dev, hipStream_t s, S
                     (void)hipFree(d);
                     return st;
                 }
-                if (r.fir.size() >= 8) {  // small LRU-ish cap
-                    (void)hipFree(r.fir.front().dev);
-                    r.fir.erase(r.fir.begin());
-                }
-                r.fir.push_back(FirTaps{key, d, h[T8 + 8192], h[T8 + 8193]});
+                if (r.fir.size() >= 8) r.fir.erase(r.fir.begin());  // small LRU-ish cap (freed once unheld)
+                r.fir.push_back(FirTaps{key, dev_table(d, dev), h[T8 + 8192], h[T8 + 8193]});
                 ft = &r.fir.back();
             }
+            *table = ft->dev;  // held by the call (copied under the lock)
+            h2048[0] = ft->h2048r;
+            h2048[1] = ft->h2048i;
         }
+        float *tp = table->get();
         m->kind = MapKind::Fir;
-        m->taps = ft->dev;
+        m->taps = tp;
         m->ntaps8 = T8;
         m->ntaps = T;
-        m->olsH = ft->dev + T8;
-        m->pairH = ft->dev + T8 + 8196;  // 16-byte aligned: T8 and 8196 are multiples of 4
-        m->olsH2048[0] = ft->h2048r;
-        m->olsH2048[1] = ft->h2048i;
+        m->olsH = tp + T8;
+        m->pairH = tp + T8 + 8196;  // 16-byte aligned: T8 and 8196 are multiples of 4
+        m->olsH2048[0] = h2048[0];
+        m->olsH2048[1] = h2048[1];
         return DSP_OK;
     }
     case DSP_PLUGIN_BIQUAD: {  // build-defined: Parameters{float coef[5 S]}, S = 1..4 sections
@@ -695,10 +723,11 @@ static int plugin_map(const dsp_plugin *p, uint32_t B, int dev, hipStream_t s, S
         std::vector<float> key((const float *)p->params, (const float *)p->params + 5 * S);
         for (float v : key)
             if (!std::isfinite(v)) return invalid("BIQUAD coefficients must be finite");
-        IirTab *it = nullptr;
+        uint32_t window = 0;
         {
             std::lock_guard<std::mutex> lk(g_mu);
             DeviceRes &r = g_res[dev];
+            const IirTab *it = nullptr;
             for (auto &e : r.iir)
                 if (e.coef == key) { it = &e; break; }
             if (!it) {
@@ -711,19 +740,17 @@ static int plugin_map(const dsp_plugin *p, uint32_t B, int dev, hipStream_t s, S
                     (void)hipFree(d);
                     return st;
                 }
-                if (r.iir.size() >= 8) {  // as the FIR cache: launches before the eviction finished
-                    DSPB_HIP(hipDeviceSynchronize());
-                    (void)hipFree(r.iir.front().dev);
-                    r.iir.erase(r.iir.begin());
-                }
-                r.iir.push_back(IirTab{key, d, W});
+                if (r.iir.size() >= 8) r.iir.erase(r.iir.begin());  // as the FIR cache (freed once unheld)
+                r.iir.push_back(IirTab{key, dev_table(d, dev), W});
                 it = &r.iir.back();
             }
+            *table = it->dev;  // held by the call (copied under the lock)
+            window = it->window;
         }
         m->kind = MapKind::Biquad;
-        m->iir_tab = it->dev;
+        m->iir_tab = table->get();
         m->sections = S;
-        m->iir_window = it->window;
+        m->iir_window = window;
         return DSP_OK;
     }
     case DSP_PLUGIN_GENERIC:  // the plugin's own audio_callback, compiled for gfx950 (module.h)
@@ -762,6 +789,7 @@ struct SpecHold {
     ::dsp_module *m = nullptr;
     void *use = nullptr;
     hipStream_t s = nullptr;
+    DevTable table;  // the call's FIR / BIQUAD table (plugin_map)
     ~SpecHold() {
         if (use) (void)module_spec_done(m, use, s);
     }
@@ -1186,6 +1214,25 @@ int dsp_device_count(void) {
     return n;
 }
 
+int dsp_debug_set(int what, uint64_t value) {
+    if (what != DSP_DEBUG_BIQUAD_SPIN_LIMIT) return invalid("dsp_debug_set: unknown hook %d", what);
+    g_iir_spin_limit.store(value > 0xffffffffull ? kIirSpinLimit : (uint32_t)value);
+    return DSP_OK;
+}
+
+int dsp_debug_get(int what, uint64_t *value) {
+    if (what != DSP_DEBUG_BIQUAD_REPAIRS || !value) return invalid("dsp_debug_get: unknown hook %d", what);
+    int dev = 0;
+    if (int st = current_device(&dev)) return st;
+    std::lock_guard<std::mutex> lk(g_mu);
+    DeviceRes &r = g_res[dev];
+    *value = 0;
+    if (r.iir_fb_host) {
+        *value = __atomic_exchange_n(r.iir_fb_host, 0u, __ATOMIC_SEQ_CST);
+    }
+    return DSP_OK;
+}
+
 int dsp_biquad_plan(const float *coef, uint32_t sections, uint32_t *window) {
     if (!coef || !window || sections == 0 || sections > 4) return invalid("dsp_biquad_plan: 1..4 sections");
     for (uint32_t q = 0; q < 5 * sections; ++q)
@@ -1240,7 +1287,7 @@ int dsp_render_offline(const float *const *in, uint32_t in_channels, uint64_t L,
     }
     SpecHold hold;  // released after the call's launches
     SampleMap map;
-    int st = plugin_map(plugin, B, g.dev, s, &map, sr, ex ? ex->flags : 0);
+    int st = plugin_map(plugin, B, g.dev, s, &map, sr, ex ? ex->flags : 0, &hold.table);
     if (st) return st;
     const SampleMap orig = map;
     if ((st = specialize_generic(&map, C, B, s, ex, rows_overlap(din.data(), in_channels, L, dout.data(), C, Lr), &hold)))
@@ -1296,7 +1343,7 @@ int dsp_render_loop(const float *const *in, uint32_t in_channels, uint64_t L, ui
     const uint64_t Lr = nblocks * B;
     SpecHold hold;  // released after the call's launches
     SampleMap map;
-    int st = plugin_map(plugin, B, g.dev, s, &map, sr, ex ? ex->flags : 0);
+    int st = plugin_map(plugin, B, g.dev, s, &map, sr, ex ? ex->flags : 0, &hold.table);
     if (st) return st;
     // DSP_EXEC_VERIFY_CLASS: loop mode renders with the callback on every
     // block (as an in-place call does) rather than a class it would not check
@@ -1427,7 +1474,7 @@ int dsp_render_stft(const float *const *in, uint32_t in_channels, uint64_t L,
     }
     SpecHold hold;  // released after the call's launches
     SampleMap map;
-    if ((st = plugin_map(plugin, B, g.dev, s, &map, sr, ex ? ex->flags : 0))) return st;
+    if ((st = plugin_map(plugin, B, g.dev, s, &map, sr, ex ? ex->flags : 0, &hold.table))) return st;
     const SampleMap orig = map;
     if ((st = specialize_generic(&map, C, B, s, ex, rows_overlap(din.data(), in_channels, L, dout.data(), C, Lr), &hold)))
         return st;
@@ -1552,7 +1599,8 @@ int dsp_ir_analysis(const dsp_plugin *plugin, uint32_t C, float sr, uint32_t ir_
     }
     // compute_IR (plugin.cpp:27-34): IR[c] = delta, then one callback of ir_len
     SampleMap map;
-    if ((st = plugin_map(plugin, ir_len, g.dev, s, &map, sr, ex ? ex->flags : 0))) return st;
+    DevTable table;  // held until the call's launches are enqueued
+    if ((st = plugin_map(plugin, ir_len, g.dev, s, &map, sr, ex ? ex->flags : 0, &table))) return st;
     if (map.kind == MapKind::Generic) {  // the impulse in place, a fresh scratch State, one callback
         for (uint32_t c0 = 0; c0 < C; c0 += kMaxChannels) {
             const uint32_t cn = (C - c0) < (uint32_t)kMaxChannels ? (C - c0) : kMaxChannels;

@@ -37,9 +37,12 @@
 //      over its registers (pass 2), the real outputs, out through LDS.
 // So every sample is read once and written once from HBM (8 B per sample).
 // Tile g is the wave's place in launch order, so a tile only ever waits for
-// tiles of waves dispatched before it; the wait is bounded anyway
-// (kSpinLimit), and a wave that gives up sets the error word the host checks
-// (capi.cpp iir_launch).
+// tiles of waves dispatched before it.  The wait is bounded anyway
+// (A.spin_limit sleeps): a wave that gives up writes the launch's epoch into
+// its stream's error word, and biquad_repair_kernel, launched behind every
+// scan on the same stream, then renders the launch again as one serial chain
+// per channel -- the call never returns stale words as audio, whatever the
+// dispatch order or the other work on the GPU.
 //
 // Arithmetic: fp32, each section as fma(-a1, y1, fma(-a2, y2, fma(b2, x2,
 // fma(b1, x1, b0 x)))); the matrix powers come from float64 (capi.cpp
@@ -55,7 +58,6 @@ constexpr int kIirT = 32;             // samples per lane
 constexpr int kIirTile = 64 * kIirT;  // samples per wavefront (tile)
 constexpr int kIirWaves = 4;          // wavefronts per workgroup
 constexpr int kIirLdsStride = kIirT + 1;  // floats per lane chunk in LDS (conflict-free column reads)
-constexpr uint32_t kSpinLimit = 1u << 16;  // s_sleep rounds before a wait gives up (legit waits: a few)
 typedef float f4 __attribute__((ext_vector_type(4)));
 
 // a lane's values for NCH channels at once: float (one channel per wave) or
@@ -278,12 +280,12 @@ __global__ __launch_bounds__(256) void biquad_scan_kernel(BiquadArgs A) {
         return ok;
     };
     uint32_t spins = 0;
-    auto give_up = [&]() {  // never with a correct launch: bounded, and loud
-        if (++spins <= kSpinLimit) {
+    auto give_up = [&]() {  // bounded; the launch is then rendered again (biquad_repair_kernel)
+        if (++spins <= A.spin_limit) {
             __builtin_amdgcn_s_sleep(1);
             return false;
         }
-        if (lane == 0) *A.err = 1u;
+        if (lane == 0) __hip_atomic_store(A.err, (uint32_t)A.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return true;
     };
     publish(A.aggw, agg);
@@ -416,6 +418,46 @@ __global__ __launch_bounds__(256) void biquad_scan_kernel(BiquadArgs A) {
     }
 }
 
+// Behind every scan on its stream: when a wave of that launch gave up its
+// look-back (the error word holds the launch's epoch -- epochs are unique per
+// launch on a workspace, so no reset is needed), render the launch again as
+// one serial chain per channel (a workgroup per channel: the wave stages a
+// tile through LDS, lane 0 runs the cascade over it), the same difference
+// equation within the same bound.  Otherwise one load and out.
+template <int S>
+__global__ __launch_bounds__(64) void biquad_repair_kernel(BiquadArgs A) {
+    if (__hip_atomic_load(A.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != (uint32_t)A.epoch) return;
+    __shared__ float buf[kIirTile];
+    const uint32_t c = blockIdx.x, lane = threadIdx.x;
+    if (c == 0 && lane == 0) __hip_atomic_fetch_add(A.repairs, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const float *x = c < A.in_ch ? A.in.p[c] : nullptr;
+    float *y = A.out.p[c];
+    const Cascade<S, 1> cs(A.coef);
+    float st[2 * S], h1 = 0.f, h2 = 0.f;
+#pragma unroll
+    for (int q = 0; q < 2 * S; ++q) st[q] = 0.f;
+    for (uint64_t base = 0; base < A.Ly; base += kIirTile) {
+        for (uint32_t e = lane; e < (uint32_t)kIirTile; e += 64) buf[e] = (x && base + e < A.L) ? x[base + e] : 0.f;
+        __syncthreads();
+        if (lane == 0) {
+            for (int k0 = 0; k0 < kIirTile; k0 += kIirT) {
+                float v[kIirT];
+#pragma unroll
+                for (int n = 0; n < kIirT; ++n) v[n] = buf[k0 + n];
+                const float n1 = v[kIirT - 1], n2 = v[kIirT - 2];  // the next run's x history
+                cs.template run<true>(v, h1, h2, st);
+                h1 = n1;
+                h2 = n2;
+#pragma unroll
+                for (int n = 0; n < kIirT; ++n) buf[k0 + n] = v[n];
+            }
+        }
+        __syncthreads();
+        for (uint32_t e = lane; e < (uint32_t)kIirTile && base + e < A.Ly; e += 64) y[base + e] = buf[e];
+        __syncthreads();
+    }
+}
+
 uint64_t biquad_tiles(uint64_t Ly) { return (Ly + kIirTile - 1) / kIirTile; }
 uint32_t biquad_lane_samples() { return kIirT; }
 
@@ -449,6 +491,14 @@ int launch_biquad(const BiquadArgs &A, uint32_t sections, uint32_t nch, hipStrea
     default: return DSP_ERR_INVALID;
     }
 #undef DSPB_BQ
+    DSPB_HIP(hipGetLastError());
+    const dim3 rgrid(A.C), rblk(64);
+    switch (sections) {
+    case 1: hipLaunchKernelGGL((biquad_repair_kernel<1>), rgrid, rblk, 0, s, A); break;
+    case 2: hipLaunchKernelGGL((biquad_repair_kernel<2>), rgrid, rblk, 0, s, A); break;
+    case 3: hipLaunchKernelGGL((biquad_repair_kernel<3>), rgrid, rblk, 0, s, A); break;
+    default: hipLaunchKernelGGL((biquad_repair_kernel<4>), rgrid, rblk, 0, s, A); break;
+    }
     DSPB_HIP(hipGetLastError());
     return DSP_OK;
 }

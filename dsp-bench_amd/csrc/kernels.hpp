@@ -129,7 +129,9 @@ struct BiquadArgs {
     uint32_t window;       // W: S_in from the W previous tiles' aggregates (0: inclusive look-back)
     uint64_t *aggw, *inclw;  // per tile, nch D words: epoch << 32 | float bits (aggregate, inclusive)
     uint64_t epoch;        // distinct per launch on one workspace (32 bits used)
-    uint32_t *err;         // host-mapped: set when a look-back gives up
+    uint32_t spin_limit;   // sleeps a look-back waits before it gives up
+    uint32_t *err;         // the stream's workspace word: a wave that gave up writes the epoch
+    uint32_t *repairs;     // host-mapped: launches biquad_repair_kernel rendered again (diagnostic)
     uint32_t in_aligned16, out_aligned16;
 };
 uint64_t biquad_tiles(uint64_t Ly);

@@ -179,10 +179,7 @@ _SIGS = {
                                          C.POINTER(C.c_int32), C.POINTER(C.c_float), C.POINTER(dsp_exec)]),
     "dsp_module_facts": (C.c_int, [C.c_void_p, C.POINTER(dsp_callback_facts)]),
     "dsp_module_state_spec": (C.c_int, [C.c_void_p, C.POINTER(dsp_state_spec_info)]),
-    "dsp_module_debug": (C.c_int, [C.c_void_p, C.c_int, C.c_uint64]),
-    "dsp_ir_strip_chain_stores": (C.c_int, [C.c_char_p, C.c_char_p, C.c_uint64, C.POINTER(C.c_int32)]),
     "dsp_plugin_analyze": (C.c_int, [C.c_char_p, C.POINTER(dsp_callback_facts)]),
-    "dsp_plugin_analyze_shipped": (C.c_int, [C.c_char_p, C.POINTER(dsp_callback_facts)]),
     "dsp_code_facts": (C.c_int, [C.c_void_p, C.c_uint64, C.POINTER(dsp_callback_facts)]),
     "dsp_descriptor_from_code": (C.c_int, [C.c_void_p, C.c_uint64, C.POINTER(C.c_void_p)]),
     "dsp_descriptor_destroy": (None, [C.c_void_p]),
@@ -212,6 +209,12 @@ _SIGS = {
 
 # exported only by the A/B tools build (build/ab/libdspbench_ab.so)
 _OPTIONAL_SIGS = {
+    # test hooks and diagnostics (an A/B library built from an older tree may lack them)
+    "dsp_debug_set": (C.c_int, [C.c_int, C.c_uint64]),
+    "dsp_debug_get": (C.c_int, [C.c_int, C.POINTER(C.c_uint64)]),
+    "dsp_module_debug": (C.c_int, [C.c_void_p, C.c_int, C.c_uint64]),
+    "dsp_ir_strip_chain_stores": (C.c_int, [C.c_char_p, C.c_char_p, C.c_uint64, C.POINTER(C.c_int32)]),
+    "dsp_plugin_analyze_shipped": (C.c_int, [C.c_char_p, C.POINTER(dsp_callback_facts)]),
     "dsp_stft_pk_ab_options": (C.c_int, [C.c_int]),
 }
 

@@ -178,7 +178,14 @@ void phasor_32_array(real32 *out, real32 ampl, real32 freq, i32 n, real32 *phase
 void random_uniform_32_array(real32 *out, i32 n, void *rng) { (void)out; (void)n; (void)rng; }
 
 // ---- array moves ----
-void copy_array(real32 *in, real32 *out, i32 n) { if (n > 0) std::memmove(out, in, sizeof(float) * n); }
+// element by element, first to last -- the device build's copy_array
+// (plugin_device.h), so a plugin renders the same on both builds even when its
+// rows overlap (the reference's ippsCopy_32f leaves overlap undefined); a
+// shift right repeats in[0], as it does there
+void copy_array(real32 *in, real32 *out, i32 n) {
+    volatile real32 *o = out;  // (not turned into memmove, whose overlap semantics differ)
+    for (i32 i = 0; i < n; ++i) o[i] = in[i];
+}
 void set_array(real32 v, real32 *out, i32 n) { for (i32 i = 0; i < n; ++i) out[i] = v; }
 void zero_array(real32 *out, i32 n) { if (n > 0) std::memset(out, 0, sizeof(float) * n); }
 void add_array(real32 *a, real32 *b, real32 *out, i32 n) { for (i32 i = 0; i < n; ++i) out[i] = a[i] + b[i]; }

@@ -151,6 +151,19 @@ uint64_t dsp_stft_frame_count(uint64_t L, uint32_t N, uint32_t H);
  * bound, not bitwise reproducible).  DSP_ERR_INVALID for a bad blob. */
 int dsp_biquad_plan(const float *coef, uint32_t sections, uint32_t *window);
 
+/* Test hooks (not for production use).
+ * DSP_DEBUG_BIQUAD_SPIN_LIMIT (set): the sleeps a DSP_PLUGIN_BIQUAD look-back
+ *   waits for a preceding tile's words before it gives up (value ~0 restores
+ *   the default); a launch in which a wave gave up is rendered again, on the
+ *   same stream before the call's later work, as one serial chain per channel
+ *   (within the same bound).  0 gives up wherever a word is not there at the
+ *   first look.
+ * DSP_DEBUG_BIQUAD_REPAIRS (get): launches on the current device rendered
+ *   again that way since the last get (read it after the renders finished). */
+enum { DSP_DEBUG_BIQUAD_SPIN_LIMIT = 1, DSP_DEBUG_BIQUAD_REPAIRS = 2 };
+int dsp_debug_set(int what, uint64_t value);
+int dsp_debug_get(int what, uint64_t *value);
+
 /* Offline render, one-shot:
  *   nblocks = ceil(L / B); out[c] holds nblocks * B floats.
  *   Block b: out = file[cursor .. cursor+B) for c < in_channels, zero past

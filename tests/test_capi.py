@@ -242,6 +242,37 @@ def test_array_services(svc):
     assert not out.any()
 
 
+def overlapping_copy_semantics(h, shift_right):
+    """copy_array(h, h + 1, n - 1) / copy_array(h + 1, h, n - 1) as the device
+    build's copy_array (plugin_device.h: element by element, first to last)
+    does it."""
+    h = h.copy()
+    n = h.size
+    if shift_right:
+        for i in range(n - 1):
+            h[i + 1] = h[i]
+    else:
+        for i in range(n - 1):
+            h[i] = h[i + 1]
+    return h
+
+
+def test_copy_array_overlap_matches_the_device_build(svc):
+    """Overlapping rows (a delay line shifted in place): the host build's
+    copy_array copies first to last like the device build's, so the same
+    plugin source renders the same on both (a shift right repeats h[0]; the
+    GPU side: tests/test_gpu_parity.py::test_copy_array_overlap_on_the_device)."""
+    h = np.arange(1, 65, dtype=np.float32)
+    for right in (True, False):
+        x = h.copy()
+        base = x.ctypes.data
+        if right:
+            svc.copy_array(base, base + 4, 63)
+        else:
+            svc.copy_array(base + 4, base, 63)
+        assert np.array_equal(x, overlapping_copy_semantics(h, right)), right
+
+
 def test_windowing_hamming_service(svc, oracle):
     x = np.ones(2048, np.float32)
     y = np.empty_like(x)

@@ -235,3 +235,73 @@ def test_biquad_full_hour_stereo(torch_cuda, oracle):
         err = float(np.max(np.abs(y.astype(np.float64) - y64)))
         assert err <= bound, (c, err, bound)
         del y64, y
+
+
+def _debug_set(what, value):
+    assert d.lib().dsp_debug_set(what, value) == 0
+
+
+def _repairs():
+    import ctypes as C
+    n = C.c_uint64()
+    assert d.lib().dsp_debug_get(2, C.byref(n)) == 0  # DSP_DEBUG_BIQUAD_REPAIRS
+    return n.value
+
+
+@pytest.mark.parametrize("S", [1, 2, 4])
+def test_biquad_look_back_give_up_is_repaired_in_the_call(torch_cuda, oracle, S):
+    """A look-back that gives up its wait (the call once returned
+    stale words as audio and the error surfaced on a later call): the wave
+    writes the launch's epoch into its stream's error word, and the repair
+    kernel behind the scan on the same stream renders the launch again as one
+    serial chain per channel.  With the wait budget forced to zero
+    (dsp_debug_set DSP_DEBUG_BIQUAD_SPIN_LIMIT) waves give up wherever a word
+    is not there at the first look: the repair runs (counted), the call's
+    own output is within the float64 bound, and the next call with the
+    normal budget renders the scan's bits again."""
+    rng = np.random.default_rng(40 + S)
+    coef = random_cascade(rng, S)
+    assert plan(coef) > 0
+    L = 2048 * 200 + 99
+    x = rng.uniform(-1, 1, (2, L)).astype(np.float32)
+    xt = torch_cuda.from_numpy(x).cuda()
+    p = d.Plugin.biquad(coef)
+    ref = d.render_offline(xt, 2, 512, 48000.0, p)
+    torch_cuda.cuda.synchronize()
+    _repairs()  # reset the counter
+    try:
+        _debug_set(1, 0)
+        got = d.render_offline(xt, 2, 512, 48000.0, p)
+        torch_cuda.cuda.synchronize()
+    finally:
+        _debug_set(1, 2**64 - 1)
+    assert _repairs() > 0
+    check(oracle, got.cpu().numpy(), x, coef, got.shape[1])
+    again = d.render_offline(xt, 2, 512, 48000.0, p)
+    torch_cuda.cuda.synchronize()
+    assert torch_cuda.equal(again, ref)
+    assert _repairs() == 0
+
+
+def test_biquad_look_back_give_up_chain_mode(torch_cuda, oracle):
+    """The same in the chained look-back (W = 0, a marginal resonator): the
+    repaired render stays within the serial fp32 chain's own error."""
+    th = 2 * math.pi * 440 / 48000
+    coef = np.array([[1.0, 0.0, 0.0, -2 * math.cos(th), 1.0]], np.float32)
+    coef[0, 4] = np.float32(0.9999999)
+    assert plan(coef) == 0
+    rng = np.random.default_rng(8)
+    L = 2048 * 300
+    x = np.zeros((1, L), np.float32)
+    x[0, :64] = rng.uniform(-1, 1, 64).astype(np.float32)
+    _repairs()
+    try:
+        _debug_set(1, 0)
+        got = d.render_offline(torch_cuda.from_numpy(x).cuda(), 1, 512, 48000.0, d.Plugin.biquad(coef)).cpu().numpy()
+    finally:
+        _debug_set(1, 2**64 - 1)
+    assert _repairs() > 0
+    y64, _ = oracle.biquad_f64(x[0], coef, got.shape[1])
+    err = float(np.max(np.abs(got[0].astype(np.float64) - y64)))
+    err32 = float(np.max(np.abs(oracle.biquad_f32(x[0], coef, got.shape[1]).astype(np.float64) - y64)))
+    assert err <= 4 * err32 + 1e-6 * float(np.abs(y64).max()), (err, err32)

@@ -539,3 +539,38 @@ def test_chain_kernels_of_a_tremolo_come_from_edited_ir():
     ps = _private_sizes(code)
     for k in ("dspb_seg_chain_c2b512", "dspb_seg_chain_c2", "dspb_seg_chain_c1", "dspb_seg_chain_c4"):
         assert ps[k] == 0, (k, ps[k])
+
+
+SHIFT_SRC = r'''
+#include "plugin_header.h"
+struct Parameters { FLOAT_PARAM(0.0f, 1.0f) g; };
+struct State { float unused; };
+Parameters default_parameters() { Parameters p = {0.5f}; return p; }
+State initialize_state(const Parameters& p, const unsigned C, const float sr, void* ctx) { State s = {0.0f}; return s; }
+void audio_callback(const Parameters& p, State& st, float** out, const u32 C, const u32 B, const real32 sr) {
+    // overlapping rows: a shift right by one on channel 0, a shift left on channel 1
+    copy_array(out[0], out[0] + 1, (i32)B - 1);
+    if (C > 1) copy_array(out[1] + 1, out[1], (i32)B - 1);
+}
+'''
+
+
+@pytest.mark.gpu
+def test_copy_array_overlap_on_the_device(torch_cuda):
+    """copy_array over overlapping rows renders as the host build does
+    (first to last: a shift right repeats the block's first sample, a shift
+    left moves it down; tests/test_capi.py::test_copy_array_overlap_matches_the_device_build
+    holds the host build to the same semantics)."""
+    from test_capi import overlapping_copy_semantics
+    mod = d.module.Module(d.module.compile_source(SHIFT_SRC, "shift.cpp"))
+    params = mod.default_parameters()
+    B, L = 64, 64 * 50 + 7
+    mod.initialize_state(params, 2, 48000.0)
+    x = np.random.default_rng(5).uniform(-1, 1, (2, L)).astype(np.float32)
+    got = d.render_offline(torch_cuda.from_numpy(x).cuda(), 2, B, 48000.0, mod.plugin(params)).cpu().numpy()
+    xp = np.zeros((2, got.shape[1]), np.float32)
+    xp[:, :L] = x
+    for b in range(got.shape[1] // B):
+        blk = xp[:, b * B:(b + 1) * B]
+        assert np.array_equal(got[0, b * B:(b + 1) * B], overlapping_copy_semantics(blk[0], True)), b
+        assert np.array_equal(got[1, b * B:(b + 1) * B], overlapping_copy_semantics(blk[1], False)), b
