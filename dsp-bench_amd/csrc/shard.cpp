@@ -649,8 +649,17 @@ int dsp_render_stft_sharded(const float *const *in, uint32_t in_channels, uint64
         if (int st = dsp_module_sizes((const dsp_module *)plugin->module, nullptr, nullptr, &stateless)) return st;
     }
     const bool stateful_generic = plugin && plugin->kind == DSP_PLUGIN_GENERIC && !stateless;
+    // a State carried from block to block (audio.cpp:160-165) cannot start
+    // mid-file: time shards need blocks that render independently
     if (sh->mode == DSP_SHARD_TIME && sh->world > 1 && stateful_generic)
-        return invalid("time sharding needs a state-free plugin (this module has a State)");
+        return invalid("time sharding needs blocks that render independently: this plugin's callback writes its "
+                       "State, which the reference carries from block to block (audio.cpp:160-165); shard it by "
+                       "channel (DSP_SHARD_CHANNELS)");
+    if (sh->mode == DSP_SHARD_TIME && sh->world > 1 && plugin &&
+        (plugin->kind == DSP_PLUGIN_FIR || plugin->kind == DSP_PLUGIN_BIQUAD))
+        return invalid("time sharding needs blocks that render independently: a %s filter's state runs through "
+                       "the whole file; shard it by channel (DSP_SHARD_CHANNELS)",
+                       plugin->kind == DSP_PLUGIN_FIR ? "FIR" : "BIQUAD");
 
     int prev = -1;
     SH_HIP(hipGetDevice(&prev));
