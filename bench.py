@@ -981,9 +981,12 @@ def main():
                             "the serial chain: one lane runs the callback block after block (a State written "
                             "every block); DESIGN 4.6" if wl in ("biquad_src", "sine_src") and
                             (args.serial_state or not (state_segments or {}).get("used")) else
-                            "the State chain: one lane runs the phase update sample after sample (dependent "
-                            "float64 adds; the callback's block arithmetic compiled away), then the segments "
-                            "in parallel; DESIGN 4.6" if (state_segments or {}).get("chain") else
+                            "the State chain at its ISA floor: one lane runs the phase update frame after frame "
+                            "(the callback's block arithmetic compiled away): v_add_f64 -> v_add_f64 + "
+                            "v_cmp_lt_f64 -> s_nop 1 -> v_cndmask x2, measured alone at 34.3 shader cycles per "
+                            "frame (14.4 ns at 2.39 GHz; a dependent v_add_f64 is 6.3, the VCC round trip the "
+                            "rest: tools/diag/f64_chain_floor.hip, profiles/r06_f64_chain_floor.jsonl), then the "
+                            "segments in parallel; DESIGN 4.6" if (state_segments or {}).get("chain") else
                             "segments: one lane per segment runs the callback's own chain block after block; "
                             "the lanes are the blocks LDS holds (18 per 76 KB workgroup, 36 per CU), so the rounds "
                             "(blocks per segment + warm-up) bound it; DESIGN 4.6"
