@@ -75,7 +75,7 @@ def parse():
     ap.add_argument("--workload", default="headline",
                     choices=["headline", "stft96k", "ch96k", "gain10min", "fir1024", "wav16", "wav24", "ir",
                              "generic", "generic_stft", "gain_stft", "wav16enc", "wav24enc", "biquad", "biquad_src",
-                             "sine_src"],
+                             "sine_src", "envelope_src"],
                     help="headline = IR_test + STFT 48 kHz (the metric); stft96k = BASELINE cfg 4 "
                          "(STFT of 1 h stereo 96 kHz from HBM); gain10min = cfg 2 render; "
                          "wav16 / wav24 = GPU decode of a 1 h stereo int16 / int24 WAV payload; "
@@ -88,7 +88,8 @@ def parse():
                          "planar stereo into an interleaved int16 / int24 WAV payload; biquad = DSP_PLUGIN_BIQUAD "
                          "(plugins/biquad.cpp's low-pass as a block-parallel state scan, 1 h stereo); biquad_src / "
                          "sine_src = plugins/biquad.cpp / the reference's sine_test.cpp compiled unchanged, the "
-                         "serial stateful chain (default 1 min of stereo)")
+                         "serial stateful chain (default 1 min of stereo); envelope_src = plugins/envelope_counter.cpp "
+                         "(an envelope beside a block counter: a split State, 1 h stereo)")
     ap.add_argument("--sections", type=int, default=1, choices=[1, 2, 3, 4],
                     help="biquad: sections in the cascade (1 = plugins/biquad.cpp's low-pass; more add RBJ "
                          "peaking / high-pass sections)")
@@ -133,7 +134,8 @@ def source_plugin(d, pname: str, C: int, B: int, sr: int, specialize: bool = Tru
 
 
 # plugin sources of this repository (tests/plugins/, dsp-bench_amd/plugins/), not the reference's
-OWN_PLUGINS = {"balance": "tests/plugins", "fade_in": "tests/plugins", "biquad": "dsp-bench_amd/plugins"}
+OWN_PLUGINS = {"balance": "tests/plugins", "fade_in": "tests/plugins", "biquad": "dsp-bench_amd/plugins",
+               "envelope_counter": "dsp-bench_amd/plugins"}
 
 
 def source_plugin_name(pname: str, block_class: str) -> str:
@@ -531,7 +533,7 @@ def main():
     F = d.stft_frames(nb * B if wl in ("headline", "ch96k", "gain_stft") else L_in, N_FFT, HOP)
     out = (torch.empty((CH, nb * B), device=dev)
            if wl in ("headline", "ch96k", "gain10min", "fir1024", "generic", "generic_stft", "gain_stft", "biquad",
-                     "biquad_src", "sine_src") else None)
+                     "biquad_src", "sine_src", "envelope_src") else None)
     if wl == "generic_stft":
         F = d.stft_frames(nb * B, N_FFT, HOP)
     LD = args.mag_ld or K_BINS
@@ -676,8 +678,8 @@ def main():
                     f"(B=512), {minutes:g} min of 48 kHz stereo per GPU, block-parallel state scan")
         kname = f"biquad_scan_kernel<{args.sections}> (tile = 64 lanes x 32 samples, windowed look-back)"
         alg_desc = "C*L*(4 + 4) B (each input sample read once + each output sample written once)"
-    elif wl in ("biquad_src", "sine_src"):
-        pname = "biquad" if wl == "biquad_src" else "sine_test"
+    elif wl in ("biquad_src", "sine_src", "envelope_src"):
+        pname = {"biquad_src": "biquad", "sine_src": "sine_test", "envelope_src": "envelope_counter"}[wl]
         gmod, gplug, block_class = source_plugin(d, pname, CH, B, sr, serial_state=args.serial_state)
         plug_name = (f"{pname}.cpp compiled unchanged (DSP_PLUGIN_GENERIC; its callback writes its State: " +
                      ("the serial chain, one lane)" if args.serial_state else
@@ -691,9 +693,13 @@ def main():
                  if args.serial_state else
                  "dspb_seg_c2b512 + dspb_seg_check + dspb_seg_walk (speculative segments, DESIGN 4.6)"
                  if pname == "biquad" else
+                 "dspb_seg_chain_ind_c2b512 + dspb_seg_c2b512 + dspb_seg_check + dspb_seg_walk (a split State: "
+                 "the block counter's chain on one lane, then speculative segments started from it; DESIGN 4.6)"
+                 if pname == "envelope_counter" else
                  "dspb_seg_chain_c2b512 + dspb_seg_c2b512_rerun (a State learned never to forget: the State "
                  "chain on one lane, then every segment from its recorded State; DESIGN 4.6)")
-        alg_desc = "C*L*(4 + 4) B (read + write)" if pname == "biquad" else "C*L*4 B (write; the input is ignored)"
+        alg_desc = ("C*L*(4 + 4) B (read + write)" if pname in ("biquad", "envelope_counter") else
+                    "C*L*4 B (write; the input is ignored)")
     elif wl in ("wav16enc", "wav24enc"):
         # SURVEY 8(f) row 1, the writer: planar float -> interleaved PCM
         # (interleave + convert, audio.h:123-133; round half to even, clip)
@@ -877,7 +883,7 @@ def main():
 
     traffic, traffic_src, traffic_inst = pmc_traffic(pmc_key(wl, block_class, args.sections), bytes_per_launch)
     # the last timed render of a State-writing source plugin (module.h dsp_state_spec_info)
-    state_segments = gmod.state_spec() if wl in ("biquad_src", "sine_src") else None
+    state_segments = gmod.state_spec() if wl in ("biquad_src", "sine_src", "envelope_src") else None
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and wl == "headline":
@@ -890,6 +896,8 @@ def main():
             cpu["note"] = "one section (plugins/biquad.cpp); the kind above runs more"
     elif rank == 0 and world == 1 and not args.no_cpu_baseline and wl == "sine_src":
         cpu = cpu_baseline_generic(min(args.cpu_seconds, 8.0), "sine_test")
+    elif rank == 0 and world == 1 and not args.no_cpu_baseline and wl == "envelope_src":
+        cpu = cpu_baseline_generic(min(args.cpu_seconds, 8.0), "envelope_counter", prefix="libplug_")
 
     def emit(gather_ms, gather_err):
         if rank != 0:
@@ -925,7 +933,7 @@ def main():
                              "dsp_render_stft_sharded), no data-path collective" if wl == "ch96k" else
                              "one independent file per GPU (a stateful plugin's state crosses time chunks: it "
                              "shards by channel or by file, never by time), no data-path collective"
-                             if wl in ("biquad", "biquad_src", "sine_src") else
+                             if wl in ("biquad", "biquad_src", "sine_src", "envelope_src") else
                              "time-chunk per GPU, 4096-sample halo, no data-path collective"),
                 "render_gather_ms": None if gather_ms is None else round(gather_ms, 3),
                 "render_gather_error": gather_err,
@@ -979,7 +987,7 @@ def main():
                             "the read + write stream (render_vec_kernel)" if wl == "generic" else
                             "the read + write stream and the two recurrence passes (DESIGN 4.7)" if wl == "biquad" else
                             "the serial chain: one lane runs the callback block after block (a State written "
-                            "every block); DESIGN 4.6" if wl in ("biquad_src", "sine_src") and
+                            "every block); DESIGN 4.6" if wl in ("biquad_src", "sine_src", "envelope_src") and
                             (args.serial_state or not (state_segments or {}).get("used")) else
                             "the State chain at its ISA floor: one lane runs the phase update frame after frame "
                             "(the callback's block arithmetic compiled away): v_add_f64 -> v_add_f64 + "
@@ -987,10 +995,13 @@ def main():
                             "frame (14.4 ns at 2.39 GHz; a dependent v_add_f64 is 6.3, the VCC round trip the "
                             "rest: tools/diag/f64_chain_floor.hip, profiles/r06_f64_chain_floor.jsonl), then the "
                             "segments in parallel; DESIGN 4.6" if (state_segments or {}).get("chain") else
-                            "segments: one lane per segment runs the callback's own chain block after block; "
+                            ("a split State: the block counter's chain on one lane, then "
+                             "the speculative segments as biquad_src's; DESIGN 4.6"
+                             if (state_segments or {}).get("split") else
+                             "segments: one lane per segment runs the callback's own chain block after block; "
                             "the lanes are the blocks LDS holds (18 per 76 KB workgroup, 36 per CU), so the rounds "
-                            "(blocks per segment + warm-up) bound it; DESIGN 4.6"
-                            if wl in ("biquad_src", "sine_src") else
+                            "(blocks per segment + warm-up) bound it; DESIGN 4.6")
+                            if wl in ("biquad_src", "sine_src", "envelope_src") else
                             "the render (LDS-capacity-bound callbacks) then the power-capped memory STFT, "
                             "serial: DESIGN 4.6, profiles/r02_generic_stft_schedules.txt"
                             if wl == "generic_stft" and block_class == "callback" else

@@ -59,9 +59,31 @@ namespace {
 enum : uint32_t { O_BUF = 1, O_TBL = 2, O_PRM = 4, O_STA = 8, O_LOC = 16, O_GC = 32, O_GM = 64, O_EXT = 128, O_UNK = 256 };
 enum : uint32_t { D_IN = 1, D_VAR = 2, D_ADDR = 4 };
 
+// soff: for a pointer into State alone (org == O_STA), its constant byte
+// offset from the State's base: kSoffUnset before the fixpoint has seen a
+// definition, kSoffUnknown once two disagree or the offset is not a constant
+constexpr int64_t kSoffUnset = -2, kSoffUnknown = -1;
 struct Val {
     uint32_t org = 0, data = 0;
+    int64_t soff = kSoffUnset;
 };
+
+// bytes of an IR scalar or vector type (0: not one this analysis sizes)
+int64_t type_bytes(const std::string &t) {
+    static const std::map<std::string, int64_t> kScalar = {
+        {"i8", 1}, {"i16", 2}, {"i32", 4}, {"i64", 8}, {"half", 2}, {"bfloat", 2}, {"float", 4}, {"double", 8},
+        {"ptr", 8}, {"ptr addrspace(1)", 8}, {"ptr addrspace(5)", 4}, {"i1", 1}};
+    auto it = kScalar.find(t);
+    if (it != kScalar.end()) return it->second;
+    if (t.size() > 4 && t[0] == '<' && t.back() == '>') {  // <N x T>
+        const size_t x = t.find(" x ");
+        if (x == std::string::npos) return 0;
+        const int64_t n = std::strtoll(t.c_str() + 1, nullptr, 10);
+        const int64_t e = type_bytes(t.substr(x + 3, t.size() - x - 4));
+        return (n > 0 && e > 0) ? n * e : 0;
+    }
+    return 0;
+}
 
 struct Inst {
     std::string res, op, text;      // result (or ""), opcode, operand text after the opcode
@@ -181,6 +203,10 @@ struct Analysis {
     std::vector<Inst> body;
     std::vector<std::string> args;  // the kernel's six parameters
     uint32_t loc_data = 0, sta_data = 0;
+    // State stores by byte: the data bits stored at each known offset, and
+    // those of stores whose offset or extent is not known (any byte)
+    std::map<int64_t, uint32_t> sta_byte;
+    uint32_t sta_any = 0;
     Facts f;
     std::string fail;
     std::vector<std::string> blk_name;  // "%label" per basic block; block 0 is the entry
@@ -220,6 +246,27 @@ struct Analysis {
         return false;
     }
 
+    // a store of data bits d through State pointer P of n bytes (0: extent unknown)
+    void state_store(const Val &P, uint32_t d, int64_t n) {
+        f.writes_state = true;
+        sta_data |= d;
+        if (P.org == O_STA && P.soff >= 0 && n > 0)
+            for (int64_t b = P.soff; b < P.soff + n; ++b) sta_byte[b] |= d;
+        else
+            sta_any |= d;
+    }
+    // the data bits a load of n bytes through State pointer P can see
+    uint32_t state_load(const Val &P, int64_t n) const {
+        uint32_t d = sta_any;
+        if (P.org == O_STA && P.soff >= 0 && n > 0) {
+            for (auto it = sta_byte.lower_bound(P.soff); it != sta_byte.end() && it->first < P.soff + n; ++it)
+                d |= it->second;
+        } else {
+            for (const auto &e : sta_byte) d |= e.second;
+        }
+        return d;
+    }
+
     // one transfer step for instruction I; returns true when a value grew
     bool step(const Inst &I, bool final_pass) {
         Val r;
@@ -231,7 +278,7 @@ struct Analysis {
                 r.data |= v.data;
             }
         };
-        auto store_to = [&](const Val &P, const Val &Vv, bool val_is_ptr, const std::string &what) {
+        auto store_to = [&](const Val &P, const Val &Vv, bool val_is_ptr, const std::string &what, int64_t n) {
             if (P.org == 0) {  // (store_to runs in the final pass: every origin has propagated)
                 stop(what + " through a pointer of unknown origin");
                 return;
@@ -245,14 +292,11 @@ struct Analysis {
                 stop("a pointer is stored to memory");
                 return;
             }
-            if (P.org & O_STA) {
-                f.writes_state = true;
-                sta_data |= Vv.data | P.data;
-            }
+            if (P.org & O_STA) state_store(P, Vv.data | P.data, n);
             if (P.org & O_LOC) loc_data |= Vv.data | P.data;
             if ((P.org & O_BUF) && (P.data & D_IN)) f.input_control = true;  // an input-dependent address
         };
-        auto load_from = [&](const Val &P, bool ptr_result) {
+        auto load_from = [&](const Val &P, bool ptr_result, int64_t n) {
             Val v;
             if (final_pass && P.org == 0) stop("a load through a pointer of unknown origin");
             if (P.org & O_GM) stop("a load of mutable global memory");
@@ -263,7 +307,7 @@ struct Analysis {
                 f.reads_block = true;
             }
             if (P.org & O_LOC) v.data |= loc_data | D_VAR;
-            if (P.org & O_STA) v.data |= f.writes_state ? (sta_data | D_VAR) : 0u;
+            if (P.org & O_STA) v.data |= f.writes_state ? (state_load(P, n) | D_VAR) : 0u;
             if (P.org & O_TBL) {
                 if (ptr_result) v.org |= O_BUF;
                 else stop("the block pointer table is read as data");
@@ -280,7 +324,7 @@ struct Analysis {
             const std::string &ty = I.parts[0];
             const bool ptr_result = starts_with(ty, "ptr") || ty.find("x ptr") != std::string::npos ||
                                     starts_with(ty, "volatile ptr");
-            r = load_from(get(first_value(I.parts[1], M)), ptr_result);
+            r = load_from(get(first_value(I.parts[1], M)), ptr_result, type_bytes(ty));
         } else if (op == "store") {
             if (I.parts.size() < 2) return stop("unparsed store: " + I.text), false;
             if (starts_with(I.text, "atomic")) return stop("an atomic store"), false;
@@ -289,12 +333,14 @@ struct Analysis {
             const Val Vv = get(vt);
             const bool val_is_ptr = starts_with(I.parts[0], "ptr") || starts_with(I.parts[0], "volatile ptr") ||
                                     I.parts[0].find("x ptr>") != std::string::npos;
-            if (final_pass) store_to(P, Vv, val_is_ptr, "a store");
+            // the stored value's type: the operand text before its value token
+            std::string vty = I.parts[0];
+            if (starts_with(vty, "volatile ")) vty = vty.substr(9);
+            const size_t vs = vty.rfind(' ');
+            const int64_t n = type_bytes(vs == std::string::npos ? vty : trim(vty.substr(0, vs)));
+            if (final_pass) store_to(P, Vv, val_is_ptr, "a store", n);
             else {
-                if (P.org & O_STA) {
-                    f.writes_state = true;
-                    sta_data |= Vv.data | P.data;
-                }
+                if (P.org & O_STA) state_store(P, Vv.data | P.data, n);
                 if (P.org & O_LOC) loc_data |= Vv.data | P.data;
             }
             return false;
@@ -305,8 +351,24 @@ struct Analysis {
             r.data = b.data;
             for (size_t k = 2; k < I.parts.size(); ++k)
                 for (const auto &t : values_in(I.parts[k], M)) r.data |= get(t).data;
+            // a State pointer plus one constant index of a sized element type
+            r.soff = kSoffUnknown;
+            if (b.org == O_STA && b.soff >= 0 && I.parts.size() == 3) {
+                const int64_t es = type_bytes(I.parts[0]);
+                const std::string &ix = I.parts[2];
+                const size_t sp = ix.find(' ');
+                if (es > 0 && sp != std::string::npos && ix[0] == 'i') {
+                    const std::string lit = trim(ix.substr(sp + 1));
+                    char *e = nullptr;
+                    const long long c = std::strtoll(lit.c_str(), &e, 10);
+                    if (!lit.empty() && e && *e == 0) r.soff = b.soff + c * es;
+                }
+            } else if (b.soff == kSoffUnset) {
+                r.soff = kSoffUnset;
+            }
         } else if (op == "bitcast" || op == "addrspacecast" || op == "freeze") {
             merge_all(I.text);
+            r.soff = get(first_value(I.text, M)).soff;
         } else if (op == "ptrtoint") {
             const Val p = get(first_value(I.text, M));
             if (p.org & (O_BUF | O_TBL | O_LOC | O_STA | O_PRM | O_EXT)) stop("an address is turned into an integer");
@@ -330,6 +392,7 @@ struct Analysis {
                 const Val v = get(first_value(two[0], M));
                 r.org |= v.org;
                 r.data |= v.data;
+                if (v.soff != kSoffUnset) r.soff = (r.soff == kSoffUnset || r.soff == v.soff) ? v.soff : kSoffUnknown;
             }
             r.data |= D_VAR;
         } else if (op == "call") {
@@ -370,12 +433,12 @@ struct Analysis {
             if (starts_with(callee, "@llvm.memcpy") || starts_with(callee, "@llvm.memmove")) {
                 if (a.size() < 3) return stop("unparsed memcpy"), false;
                 const Val src = get(first_value(a[1], M));
-                Val v = load_from(src, false);
+                Val v = load_from(src, false, 0);
                 v.data |= get(first_value(a[2], M)).data;
                 const Val dst = get(first_value(a[0], M));
-                if (final_pass) store_to(dst, v, false, "a memcpy");
+                if (final_pass) store_to(dst, v, false, "a memcpy", 0);
                 else {
-                    if (dst.org & O_STA) { f.writes_state = true; sta_data |= v.data | dst.data; }
+                    if (dst.org & O_STA) state_store(dst, v.data | dst.data, 0);
                     if (dst.org & O_LOC) loc_data |= v.data | dst.data;
                 }
                 if (final_pass && (dst.org & O_BUF)) gain_breakers.insert("a memcpy into the block"),
@@ -387,9 +450,9 @@ struct Analysis {
                 Val v = get(first_value(a[1], M));
                 v.data |= get(first_value(a[2], M)).data;
                 const Val dst = get(first_value(a[0], M));
-                if (final_pass) store_to(dst, v, false, "a memset");
+                if (final_pass) store_to(dst, v, false, "a memset", 0);
                 else {
-                    if (dst.org & O_STA) { f.writes_state = true; sta_data |= v.data | dst.data; }
+                    if (dst.org & O_STA) state_store(dst, v.data | dst.data, 0);
                     if (dst.org & O_LOC) loc_data |= v.data | dst.data;
                 }
                 if (final_pass && (dst.org & O_BUF)) gain_breakers.insert("a memset of the block"),
@@ -431,13 +494,20 @@ struct Analysis {
             return false;
         } else {  // arithmetic, casts, compares, selects, aggregates, vectors
             merge_all(I.text);
+            for (const auto &t : values_in(I.text, M)) {
+                const Val v = get(t);
+                if ((v.org & O_STA) && v.soff != kSoffUnset)
+                    r.soff = (r.soff == kSoffUnset || r.soff == v.soff) ? v.soff : kSoffUnknown;
+            }
         }
         if (I.res.empty()) return false;
         Val &cur = val[I.res];
         const Val before = cur;
         cur.org |= r.org;
         cur.data |= r.data;
-        return cur.org != before.org || cur.data != before.data;
+        if (r.soff != kSoffUnset)
+            cur.soff = (cur.soff == kSoffUnset || cur.soff == r.soff) ? r.soff : kSoffUnknown;
+        return cur.org != before.org || cur.data != before.data || cur.soff != before.soff;
     }
 
     std::set<std::string> gain_breakers, table_breakers;
@@ -991,14 +1061,17 @@ Facts analyze(const std::string &ir, const char *fn) {
         if (!I.res.empty()) A.def[I.res] = &I;
     A.val[A.args[0]].org = O_PRM;
     A.val[A.args[1]].org = O_STA;
+    A.val[A.args[1]].soff = 0;
     A.val[A.args[2]].org = O_TBL;
     bool settled = false;
     for (int it = 0; it < 64 && !settled; ++it) {
         bool grew = false;
-        const uint32_t ld = A.loc_data, sd = A.sta_data;
+        const uint32_t ld = A.loc_data, sd = A.sta_data, sa = A.sta_any;
+        const auto sb = A.sta_byte;
         const bool ws = A.f.writes_state;
         for (const Inst &I : A.body) grew |= A.step(I, false);
-        settled = !grew && ld == A.loc_data && sd == A.sta_data && ws == A.f.writes_state;
+        settled = !grew && ld == A.loc_data && sd == A.sta_data && ws == A.f.writes_state && sa == A.sta_any &&
+                  sb == A.sta_byte;
     }
     // facts from values still growing would not be conservative
     if (!settled) A.stop("no fixpoint after 64 passes");
@@ -1011,6 +1084,22 @@ Facts analyze(const std::string &ir, const char *fn) {
     }
     A.f.analyzed = true;
     A.f.state_reads_block = A.f.writes_state && ((A.sta_data & D_IN) || A.f.input_control);
+    // the State's words by dependence on the block: a word is block-dependent
+    // when a store that may hit it carries a block sample (a store of unknown
+    // offset may hit any word); with a branch on a sample, every word is
+    if (A.f.state_reads_block && !A.f.input_control && !(A.sta_any & D_IN)) {
+        std::set<int64_t> dep, written;
+        for (const auto &e : A.sta_byte) {
+            written.insert(e.first / 4);
+            if (e.second & D_IN) dep.insert(e.first / 4);
+        }
+        bool indep_written = false;
+        for (int64_t w : written) indep_written = indep_written || !dep.count(w);
+        if (indep_written && !dep.empty() && *dep.rbegin() < 256) {
+            A.f.state_dep_words.assign(dep.begin(), dep.end());
+            A.f.state_split = true;
+        }
+    }
     A.check_gain();
     A.check_gain_table();
     if (A.f.input_control && A.f.gain_form) {
@@ -1127,7 +1216,7 @@ int compile_to_ir(const std::string &tu, const std::vector<std::pair<std::string
 }
 
 // ---------------------------------------------------------------------------
-int strip_chain_block_stores(std::string *ir) {
+int strip_chain_block_stores(std::string *ir, const char *prefix) {
     std::istringstream in(*ir);
     std::vector<std::string> lines;
     for (std::string l; std::getline(in, l);) lines.push_back(l);
@@ -1139,7 +1228,7 @@ int strip_chain_block_stores(std::string *ir) {
     int dropped = 0;
     std::vector<char> keep(lines.size(), 1);
     for (size_t i = 0; i < lines.size(); ++i) {
-        if (lines[i].compare(0, 6, "define") != 0 || lines[i].find("@dspb_seg_chain_") == std::string::npos) continue;
+        if (lines[i].compare(0, 6, "define") != 0 || lines[i].find(prefix) == std::string::npos) continue;
         size_t end = i;
         while (end < lines.size() && lines[end] != "}") ++end;
         std::set<std::string> blk;
@@ -1266,6 +1355,10 @@ std::string encode(const Facts &f) {
     s += "gain_table_form=" + std::to_string(f.gain_table_form) + "\n";
     s += "table_why=" + clean(f.table_why.substr(0, 256)) + "\n";
     s += "state_reads_block=" + std::to_string(f.state_reads_block) + "\n";
+    s += "state_split=" + std::to_string(f.state_split) + "\n";
+    s += "state_dep_words=";
+    for (size_t i = 0; i < f.state_dep_words.size(); ++i) s += (i ? "," : "") + std::to_string(f.state_dep_words[i]);
+    s += "\n";
     s += "why=" + clean(f.why.substr(0, 512)) + "\n";
     return s;
 }
@@ -1292,6 +1385,16 @@ bool decode(const std::string &s, Facts *f) {
         else if (k == "gain_table_form") f->gain_table_form = v == "1";
         else if (k == "table_why") f->table_why = v;
         else if (k == "state_reads_block") f->state_reads_block = v == "1";
+        else if (k == "state_split") f->state_split = v == "1";
+        else if (k == "state_dep_words") {
+            f->state_dep_words.clear();
+            for (size_t a = 0; a < v.size();) {
+                size_t b = v.find(',', a);
+                if (b == std::string::npos) b = v.size();
+                if (b > a) f->state_dep_words.push_back(std::strtoll(v.substr(a, b - a).c_str(), nullptr, 10));
+                a = b + 1;
+            }
+        }
         else if (k == "why") f->why = v;
     }
     return have_analyzed;

@@ -45,6 +45,13 @@ struct Facts {
     // sample (true unless the analysis completed and showed otherwise): when
     // false the State's trajectory is the same whatever the block holds
     bool state_reads_block = true;
+    // state_reads_block, but with no branch on a sample and every store of a
+    // block-dependent value at a known offset: the State's 4-byte words split
+    // into the block-dependent ones (state_dep_words, word indices) and the
+    // others, which at least one store writes -- whose trajectory is the same
+    // whatever the block holds (a block counter beside an envelope)
+    bool state_split = false;
+    std::vector<int64_t> state_dep_words;
     std::string why;            // the first construct that ended the analysis, or why a
                                 // property does not hold
 };
@@ -66,8 +73,10 @@ int compile_to_ir(const std::string &tu, const std::vector<std::pair<std::string
 // derived from the private block `dspb_chain_blk` other than the copy of the
 // input into it (non-temporal stores) -- the callback's outputs, which by
 // that fact reach no State and no branch -- so that code generation drops the
-// arithmetic that only fed them.  Returns the stores deleted.
-int strip_chain_block_stores(std::string *ir);
+// arithmetic that only fed them.  `prefix`: the functions edited (the chain
+// of a split State's block-independent words: "@dspb_seg_chain_ind_").
+// Returns the stores deleted, -1 for a store outside the pass's model.
+int strip_chain_block_stores(std::string *ir, const char *prefix = "@dspb_seg_chain_");
 
 // LLVM IR text -> a gfx950 code object (comgr: codegen at `options`, link).
 int codegen_ir(const std::string &ir, const std::vector<std::string> &options, std::string *code, std::string *log);

@@ -78,6 +78,9 @@ constexpr LdsShape kWalkShapes[2] = {{"dspb_seg_walk_c2b512", 2, 512}, {"dspb_se
 // B = 0: any B <= kChainMaxB, the private block sized for it)
 constexpr LdsShape kChainShapes[4] = {{"dspb_seg_chain_c2b512", 2, 512}, {"dspb_seg_chain_c2", 2, 0},
                                       {"dspb_seg_chain_c1", 1, 0}, {"dspb_seg_chain_c4", 4, 0}};
+// the chain of a split State's block-independent words, the same shapes
+constexpr LdsShape kChainIndShapes[4] = {{"dspb_seg_chain_ind_c2b512", 2, 512}, {"dspb_seg_chain_ind_c2", 2, 0},
+                                         {"dspb_seg_chain_ind_c1", 1, 0}, {"dspb_seg_chain_ind_c4", 4, 0}};
 constexpr uint32_t kChainMaxB = 4096;
 constexpr uint32_t kSegMaxState = 1024;   // bytes of State a lane copies (the walk keeps one in LDS)
 constexpr uint32_t kSegWarm0 = 4;         // blocks of warm-up of a first render
@@ -122,6 +125,8 @@ struct SegArgsG {
     unsigned pass;
     unsigned exact;
     unsigned long long perturb;
+    void *st_ind;
+    unsigned split;
 };
 
 // kDriver / kSegDriver: the driver kernels (csrc/plugin_driver.inl) and the
@@ -146,6 +151,7 @@ struct dsp_module {
     dsp_descriptor *desc = nullptr;  // from the code object (NULL for code without one)
     int device = -1;
     hipModule_t mod = nullptr;
+    hipModule_t chain_mod = nullptr;   // the State chain kernels from edited IR (dspb_chain_co), or NULL
     // the LDS-blocks kernels (NULL for code objects compiled before they
     // existed): [0] any (C, B), then the instantiations of kLdsShapes
     hipFunction_t f_render_lds[7] = {};
@@ -158,8 +164,12 @@ struct dsp_module {
     // the State then depends on -- the serial chain renders instead
     hipFunction_t f_seg_chain[4] = {};
     int chain_priv[4] = {};
+    hipFunction_t f_seg_chain_ind[4] = {};  // kChainIndShapes (facts.state_split), private memory as above
+    int chain_ind_priv[4] = {};
     struct SegWork {
         void *blk = nullptr;           // [cap_blk] States: st_blk
+        void *ind = nullptr;           // [cap_ind] States: a split State's independent words (st_ind, 4 K)
+        uint64_t cap_ind = 0;
         void *end = nullptr;           // [cap] States: st_end
         uint64_t cap_blk = 0;
         unsigned *list = nullptr;      // [cap]
@@ -379,7 +389,48 @@ int dsp_module_compile(const char *source, const char *name, void **code, uint64
     tu += kDriver;
     // the segment kernels only where they can run: a callback the analysis
     // bounded that writes its State (the loader treats them as optional)
-    if (facts.analyzed && facts.writes_state) tu += kSegDriver;
+    if (facts.analyzed && facts.writes_state) {
+        // a split State: the words a block-dependent store may hit (kSegDriver
+        // dspb_state_dep_words; the State chain of the others)
+        if (facts.state_split && !facts.state_dep_words.empty()) {
+            tu += "#define DSPB_STATE_DEP_WORDS ";
+            for (size_t i = 0; i < facts.state_dep_words.size(); ++i)
+                tu += (i ? "," : "") + std::to_string(facts.state_dep_words[i]);
+            tu += "\n";
+        }
+        tu += kSegDriver;
+    }
+    const std::string round = "-DDSPB_LDS_ROUND_BYTES=" + std::to_string(kLdsRoundBytes) + "u";
+    // State chain kernels from the callback's IR with its block stores
+    // deleted (ir_proof.cpp strip_chain_block_stores), so that they keep only
+    // the State's arithmetic: every chain kernel when no State value depends
+    // on the block (a tremolo's phase, not its output), the chain of a split
+    // State's block-independent words (dspb_seg_chain_ind_*) when the State
+    // splits.  Compiled through comgr from the same translation unit into a
+    // code object of their own, carried inside the module's as the symbol
+    // dspb_chain_co (dsp_module_load takes the chain kernels from it); every
+    // other kernel is the hiprtc compile below.  Nothing is carried if any
+    // step fails: the hiprtc chain kernels stand.
+    if (facts.analyzed && facts.writes_state && (!facts.state_reads_block || facts.state_split)) {
+        std::string ir, clog, co;
+        int dropped = 0;
+        const char *prefix = facts.state_reads_block ? "@dspb_seg_chain_ind_" : "@dspb_seg_chain_";
+        if (dspb::irp::compile_to_ir(tu, {{"plugin_header.h", kPluginDeviceSrc}, {"dspb_plugin_source.cpp", source}},
+                                     {"-O3", "-std=c++20", "-ffp-contract=off", "-w", "-fno-discard-value-names",
+                                      round},
+                                     &ir, &clog) == 0 &&
+            (dropped = dspb::irp::strip_chain_block_stores(&ir, prefix)) > 0 &&
+            dspb::irp::codegen_ir(ir, {"-O3", "-ffp-contract=off"}, &co, &clog) == 0) {
+            tu += "extern \"C\" __attribute__((used, visibility(\"default\"))) __device__ const unsigned char "
+                  "dspb_chain_co[] = {" + dspb::desc::hex_literal(co) + "};\n";
+        } else if (dropped < 0) {
+            note += "State chain: a store outside the block-store model, compiled from source\n";
+        } else if (dropped == 0 && clog.empty()) {
+            note += "State chain: no block store to drop\n";
+        } else {
+            note += "State chain compiled from source: " + clog.substr(0, 200) + "\n";
+        }
+    }
     std::vector<const char *> hdrs = {kPluginDeviceSrc, source}, hnames = {"plugin_header.h", "dspb_plugin_source.cpp"};
     hiprtcProgram prog;
     if (hiprtcCreateProgram(&prog, tu.c_str(), name ? name : "plugin.cpp", (int)hdrs.size(), hdrs.data(),
@@ -387,7 +438,6 @@ int dsp_module_compile(const char *source, const char *name, void **code, uint64
         set_last_error("hiprtcCreateProgram failed");
         return DSP_ERR_INVALID;
     }
-    const std::string round = "-DDSPB_LDS_ROUND_BYTES=" + std::to_string(kLdsRoundBytes) + "u";
     const char *opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++20", "-ffp-contract=off", "-w", round.c_str()};
     const hiprtcResult rc = hiprtcCompileProgram(prog, (int)(sizeof opts / sizeof *opts), opts);
     size_t ls = 0;
@@ -412,35 +462,6 @@ int dsp_module_compile(const char *source, const char *name, void **code, uint64
     }
     hiprtcGetCode(prog, (char *)buf);
     hiprtcDestroyProgram(&prog);
-    // a State that never depends on the block (facts): the same translation
-    // unit through LLVM IR text, the callback's stores to the State chain's
-    // private block deleted (ir_proof.cpp strip_chain_block_stores), so the
-    // chain kernels keep only the State's arithmetic (a tremolo's phase, not
-    // its output); the hiprtc code above stands if any step fails
-    if (facts.analyzed && facts.writes_state && !facts.state_reads_block) {
-        std::string ir, clog, co;
-        int dropped = 0;
-        if (dspb::irp::compile_to_ir(tu, {{"plugin_header.h", kPluginDeviceSrc}, {"dspb_plugin_source.cpp", source}},
-                                     {"-O3", "-std=c++20", "-ffp-contract=off", "-w", "-fno-discard-value-names",
-                                      round},
-                                     &ir, &clog) == 0 &&
-            (dropped = dspb::irp::strip_chain_block_stores(&ir)) > 0 &&
-            dspb::irp::codegen_ir(ir, {"-O3", "-ffp-contract=off"}, &co, &clog) == 0) {
-            void *nb = std::malloc(co.size());
-            if (nb) {
-                std::memcpy(nb, co.data(), co.size());
-                std::free(buf);
-                buf = nb;
-                cs = co.size();
-            }
-        } else if (dropped < 0) {
-            note += "State chain: a store outside the block-store model, compiled from source\n";
-        } else if (dropped == 0 && clog.empty()) {
-            note += "State chain: no block store to drop\n";
-        } else {
-            note += "State chain compiled from source: " + clog.substr(0, 200) + "\n";
-        }
-    }
     // the parameter descriptor, validated as the reference's JIT does
     // (compiler.cpp:944-1164): an invalid annotation fails the compile
     dspb::desc::Descriptor d;
@@ -525,6 +546,43 @@ int dsp_module_load(const void *code, uint64_t code_size, int device, dsp_module
             (void)hipGetLastError();
             m->f_seg_chain[i] = nullptr;
         }
+        optional(&m->f_seg_chain_ind[i], kChainIndShapes[i].name);
+        if (m->f_seg_chain_ind[i] &&
+            hipFuncGetAttribute(&m->chain_ind_priv[i], HIP_FUNC_ATTRIBUTE_LOCAL_SIZE_BYTES, m->f_seg_chain_ind[i]) !=
+                hipSuccess) {
+            (void)hipGetLastError();
+            m->f_seg_chain_ind[i] = nullptr;
+        }
+    }
+    {
+        // the State chain kernels compiled from the callback's edited IR
+        // (dsp_module_compile: the symbol dspb_chain_co), a code object of
+        // their own; the module's facts say which of them it holds
+        std::string cco, ft;
+        dspb::irp::Facts cf;
+        if (dspb::desc::code_symbol(code, code_size, "dspb_chain_co", &cco) && !cco.empty() &&
+            dspb::desc::code_symbol(code, code_size, "dspb_callback_facts", &ft)) {
+            while (!ft.empty() && ft.back() == '\0') ft.pop_back();
+            if (dspb::irp::decode(ft, &cf) && hipModuleLoadData(&m->chain_mod, cco.data()) == hipSuccess) {
+                auto from_chain = [&](hipFunction_t *f, int *priv, const char *name) {
+                    hipFunction_t g = nullptr;
+                    if (hipModuleGetFunction(&g, m->chain_mod, name) != hipSuccess ||
+                        hipFuncGetAttribute(priv, HIP_FUNC_ATTRIBUTE_LOCAL_SIZE_BYTES, g) != hipSuccess) {
+                        (void)hipGetLastError();
+                        *f = nullptr;  // (the edited chain is all or nothing)
+                        return;
+                    }
+                    *f = g;
+                };
+                for (int i = 0; i < 4; ++i) {
+                    if (!cf.state_reads_block) from_chain(&m->f_seg_chain[i], &m->chain_priv[i], kChainShapes[i].name);
+                    from_chain(&m->f_seg_chain_ind[i], &m->chain_ind_priv[i], kChainIndShapes[i].name);
+                }
+            } else {
+                (void)hipGetLastError();
+                m->chain_mod = nullptr;
+            }
+        }
     }
     unsigned *d_o = nullptr;
     if ((e = hipMalloc(&d_o, 4 * sizeof(unsigned))) != hipSuccess) return fail(dspb::hip_fail(e, "hipMalloc"));
@@ -580,9 +638,11 @@ void dsp_module_destroy(dsp_module *m) {
             }
         if (m->h_params) (void)hipHostFree(m->h_params);
         if (m->seg.h_stats) (void)hipHostFree(m->seg.h_stats);
-        for (void *p : {m->seg.blk, m->seg.end, (void *)m->seg.list, (void *)m->seg.flags, (void *)m->seg.words})
+        for (void *p : {m->seg.blk, m->seg.ind, m->seg.end, (void *)m->seg.list, (void *)m->seg.flags,
+                        (void *)m->seg.words})
             if (p) (void)hipFree(p);
         if (m->mod) (void)hipModuleUnload(m->mod);
+        if (m->chain_mod) (void)hipModuleUnload(m->chain_mod);
         if (prev >= 0 && prev != m->device) (void)hipSetDevice(prev);
     }
     delete m->desc;
@@ -877,6 +937,7 @@ static void facts_out(const dspb::irp::Facts &f, bool present, dsp_callback_fact
     o->gain_table_form = f.gain_table_form;
     std::strncpy(o->table_why, f.table_why.c_str(), sizeof o->table_why - 1);
     o->state_reads_block = f.state_reads_block;
+    o->state_split = f.state_split;
 }
 
 int dsp_module_facts(const dsp_module *m, dsp_callback_facts *out) {
@@ -1027,6 +1088,7 @@ int module_seg_collect(dsp_module *m, bool wait) {
         r.chain = (h[12] || !spec) ? 1 : 0;
         r.chain_mismatch = h[13];
         r.chain_records_differed = h[14];
+        // (split: set at launch, kept)
         if (W.seq[i] == W.calls) W.last = r;
         if (W.slot_gen[i] != W.gen) continue;  // rendered with other Parameters: nothing to learn
         // the chain's records failed their check (the walk rendered the call
@@ -1095,6 +1157,30 @@ static int module_render_seg(dsp_module *m, RenderArgsG &A, hipStream_t s, bool 
     const uint64_t K = (A.nblocks + seg - 1) / seg;
     // (block indices in 32 bits; one recorded State per block, at most 8 GB of them)
     if (K < 2 || A.nblocks >= (1ull << 32) || A.nblocks * m->state_size > (8ull << 30)) return 1;
+    // a split State: the chain of its independent words, when the compiled
+    // kernel of the shape dropped the block (no private block: the words
+    // need no sample), and the records for it
+    hipFunction_t fsplit = nullptr;
+    if (!chain && m->facts.state_split)
+        for (int i = 0; i < 4 && !fsplit; ++i)
+            if (m->f_seg_chain_ind[i] && kChainIndShapes[i].C == C &&
+                (kChainIndShapes[i].B ? kChainIndShapes[i].B == B : B <= kChainMaxB) &&
+                (uint64_t)m->chain_ind_priv[i] <= (uint64_t)m->state_size + 64)
+                fsplit = m->f_seg_chain_ind[i];
+    if (fsplit && 4 * K > W.cap_ind) {
+        if (int st = wait_uses(m)) return st;
+        if (W.ind) (void)hipFree(W.ind);
+        W.ind = nullptr;
+        W.cap_ind = 0;
+        const uint64_t cap = std::max<uint64_t>(4 * K, 4096);
+        if (hipMalloc(&W.ind, cap * m->state_size) != hipSuccess) {
+            (void)hipGetLastError();
+            W.ind = nullptr;
+            fsplit = nullptr;  // no room: plain speculation
+        } else {
+            W.cap_ind = cap;
+        }
+    }
     if (K > W.cap || A.nblocks > W.cap_blk) {
         if (int st = wait_uses(m)) return st;
         for (void *p : {W.blk, W.end, (void *)W.list, (void *)W.flags}) if (p) (void)hipFree(p);
@@ -1162,12 +1248,13 @@ static int module_render_seg(dsp_module *m, RenderArgsG &A, hipStream_t s, bool 
         MOD_HIP(hipModuleLaunchKernel(fr, gseg, 1, 1, 256, 1, 1, lds, s, args, nullptr));
         if (int st = checked(1)) return st;
     } else {
-        // pass 1 and its check at the learnt warm-up, then at 16x longer ones
-        // while too many segments started wrong (each level decides on the GPU
-        // whether it runs: dspb_seg_level_runs)
-        uint32_t warm = W.warm, prev = 0;
-        G.count = W.words;
-        for (uint32_t L = 0; L < kSegLevels; ++L) {
+        // a split State: its independent words' chain first, pass 1 then
+        // starts every warm-up from them (the other words from the live State)
+        // the warm-up of each level pass 1 may run: the learnt one, then 16x
+        // longer ones while too many segments started wrong (each level
+        // decides on the GPU whether it runs: dspb_seg_level_runs)
+        uint32_t lw[kSegLevels] = {}, nlev = 0;
+        for (uint32_t L = 0, warm = W.warm; L < kSegLevels; ++L) {
             if (L > 0) {
                 const uint32_t next = std::min<uint32_t>(warm * 16, kSegWarmMax);
                 if (next <= warm || 2ull * next >= A.nblocks) break;  // no longer, or as long as the file
@@ -1176,12 +1263,26 @@ static int module_render_seg(dsp_module *m, RenderArgsG &A, hipStream_t s, bool 
                 // file costs more than the chain (the State arithmetic alone over
                 // every block) is likely to: not tried
                 if (fc && 16ull * (next + seg) > A.nblocks) break;
-                prev = warm;
                 warm = next;
             }
+            lw[nlev++] = warm;
+        }
+        if (fsplit) {
+            G.st_ind = W.ind;
+            G.split = 1;
+        }
+        uint32_t warm = W.warm, prev = 0;
+        G.count = W.words;
+        for (uint32_t L = 0; L < nlev; ++L) {
+            prev = L ? lw[L - 1] : 0;
+            warm = lw[L];
             G.level = L;
             G.warm = warm;
             G.prev_warm = prev;
+            // a split State: the chain of its independent words first, recording
+            // them where this level's warm-ups start (it runs only where the
+            // level does); pass 1 starts from them and the live State's others
+            if (fsplit) MOD_HIP(hipModuleLaunchKernel(fsplit, 1, 1, 1, 64, 1, 1, 0, s, args, nullptr));
             G.mode = 0;
             MOD_HIP(hipModuleLaunchKernel(f, gseg, 1, 1, 256, 1, 1, lds, s, args, nullptr));
             G.pass = L;
@@ -1233,6 +1334,7 @@ static int module_render_seg(dsp_module *m, RenderArgsG &A, hipStream_t s, bool 
     r.warmup_blocks = chain ? 0 : W.warm;  // the first level's; module_seg_collect names the one that stood
     r.levels = levels;                     // 0: the learnt State chain alone
     r.chain = chain ? 1 : 0;
+    r.split = fsplit ? 1 : 0;
     MOD_HIP(hipEventRecord(m->use_ev, s));
     return DSP_OK;
 }

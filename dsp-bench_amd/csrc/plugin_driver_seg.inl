@@ -49,7 +49,24 @@ struct dspb_seg_args {
                             // the check and the walk after it: every segment boundary
     unsigned long long perturb;  // test hook (dsp_module_debug): the chain kernel flips a bit of the
                                  // State it recorded for block perturb - 1 (0: none)
+    State *st_ind;          // [4][K] a split State's block-independent words where pass 1 at each
+                            // warm-up level starts segment k's warm-up (dspb_seg_chain_ind); the
+                            // other words are not written
+    unsigned split;         // pass 1 starts each segment's warm-up from st_ind's words
 };
+// a split State (dsp_callback_facts.state_split): the 4-byte words a store of
+// a block-dependent value may hit (dsp_module_compile defines the list from
+// the callback's facts; -1: none)
+#ifndef DSPB_STATE_DEP_WORDS
+#define DSPB_STATE_DEP_WORDS -1
+#endif
+static constexpr int dspb_state_dep_words[] = {DSPB_STATE_DEP_WORDS};
+__device__ static constexpr bool dspb_word_dep(unsigned w) {
+    for (int d : dspb_state_dep_words)
+        if (d == (int)w) return true;
+    return false;
+}
+constexpr bool kStateWords = sizeof(State) % 4 == 0 && alignof(State) >= 4;
 // the State chain took over within this render: the reruns, their checks and
 // the walk have nothing to do
 __device__ static bool dspb_seg_chained(const dspb_seg_args &G) { return *(volatile unsigned *)&G.stats[12] != 0; }
@@ -101,6 +118,14 @@ __device__ static bool dspb_same_state(const State *a, const State *b) {
         for (unsigned i = 0; i < sizeof(State); ++i) d |= (unsigned)(x[i] ^ y[i]);
     }
     return d == 0;
+}
+// a split State's block-independent words from src into dst (the others stay)
+__device__ static inline void dspb_copy_ind_words(void *dst, const void *src) {
+    if constexpr (kStateWords) {
+#pragma unroll
+        for (unsigned i = 0; i < sizeof(State) / 4; ++i)
+            if (!dspb_word_dep(i)) ((dspb_word *)dst)[i] = ((const dspb_word *)src)[i];
+    }
 }
 // lane t's segment: its index (~0u: none), first block rendered (warm-up
 // included), warm-up blocks, blocks rendered
@@ -171,9 +196,13 @@ __device__ static void dspb_segments(const dspb_seg_args &G) {
     Parameters prm = dspb_from_global<Parameters>(A.P);
     State st;
     bool stopped = false;
-    if (k != 0xffffffffu)
+    if (k != 0xffffffffu) {
         dspb_copy_state((void *)&st, (G.mode && (k || !G.exact)) ? (const void *)&G.st_blk[(unsigned long long)k * G.seg]
                                                                  : (const void *)A.S);
+        // pass 1 of a split State: the warm-up starts from the independent
+        // words the State chain recorded at its first block
+        if (!G.mode && G.split && k) dspb_copy_ind_words((void *)&st, (const void *)&G.st_ind[G.level * G.K + k]);
+    }
     // the channels' rows in LDS (an access by a lane-dependent channel reads
     // them there, not from the argument block in memory)
     __shared__ const float *s_in[16];
@@ -283,9 +312,13 @@ __device__ static void dspb_segments_pf(const dspb_seg_args &G) {
     Parameters prm = dspb_from_global<Parameters>(A.P);
     State st;
     bool stopped = false;
-    if (k != 0xffffffffu)
+    if (k != 0xffffffffu) {
         dspb_copy_state((void *)&st, (kRerun && (k || !G.exact)) ? (const void *)&G.st_blk[(unsigned long long)k * G.seg]
                                                                   : (const void *)A.S);
+        // pass 1 of a split State: the warm-up starts from the independent
+        // words the State chain recorded at its first block
+        if (!kRerun && G.split && k) dspb_copy_ind_words((void *)&st, (const void *)&G.st_ind[G.level * G.K + k]);
+    }
     // a constant B prefetches a whole round (PB = PV) while the callbacks run;
     // a runtime B stages in batches of 4 float4 per channel at the round's
     // start (a whole round's registers would spill)
@@ -604,3 +637,53 @@ DSPB_CHAIN_KERNEL(dspb_seg_chain_c2b512, 2, 512)
 DSPB_CHAIN_KERNEL(dspb_seg_chain_c2, 2, 0)
 DSPB_CHAIN_KERNEL(dspb_seg_chain_c1, 1, 0)
 DSPB_CHAIN_KERNEL(dspb_seg_chain_c4, 4, 0)
+
+// ---- a split State: the chain of its block-independent words --------------
+// The callback in file order on one lane, as dspb_seg_chain, recording only
+// the words no block-dependent store can hit (dspb_word_dep: compile-time, so
+// the arithmetic that feeds only the other words -- an envelope, and with it
+// the block -- is compiled away and the chain is the counter's alone).  Pass 1
+// then starts each segment's warm-up from these words and the live State's
+// others; the segments are checked bit for bit as always, so a wrong word here
+// costs reruns, never output.
+template <unsigned CC, unsigned BB>
+__device__ static void dspb_seg_chain_ind(const dspb_seg_args &G) {
+    const dspb_render_args &A = G.R;
+    if (threadIdx.x != 0 || blockIdx.x != 0 || !kStateWords) return;
+    if (!dspb_seg_level_runs(G)) return;  // launched before each warm-up level's pass 1
+    constexpr unsigned BMAX = BB ? BB : 4096u;
+    const unsigned B = BB ? BB : A.B;
+    const Parameters prm = dspb_from_global<Parameters>(A.P);
+    State st;
+    dspb_copy_state((void *)&st, (const void *)A.S);
+    // (block indices fit 32 bits: the host renders no longer file this way)
+    const unsigned nb = (unsigned)A.nblocks, seg = (unsigned)G.seg;
+    unsigned b = 0;
+    for (unsigned k = 1; k < G.K; ++k) {
+        // pass 1 at this level starts segment k's warm-up at block p: the
+        // callback up to there (a stretch with no record in it: a counter's
+        // stretch compiles to one add), then the record
+        const unsigned b0 = k * seg, p = b0 > G.warm ? b0 - G.warm : 0u, e = p < nb ? p : nb;
+        for (; b < e; ++b) {
+            float dspb_chain_blk[CC * BMAX];
+            float *ptrs[CC];
+#pragma unroll
+            for (unsigned c = 0; c < CC; ++c) {
+                ptrs[c] = dspb_chain_blk + c * B;
+                const dspb_gfloat *x = (const dspb_gfloat *)A.in[c < A.in_ch ? c : 0];
+                for (unsigned i = 0; i < B; ++i) {
+                    const unsigned long long gi = (unsigned long long)b * B + i;
+                    dspb_chain_blk[c * B + i] = (c < A.in_ch && gi < A.L) ? x[gi] : 0.0f;
+                }
+            }
+            audio_callback(prm, st, ptrs, CC, B, A.sr);
+        }
+        dspb_copy_ind_words((void *)&G.st_ind[(unsigned long long)G.level * G.K + k], (const void *)&st);
+    }
+}
+#define DSPB_CHAIN_IND_KERNEL(name, CC, BB)                                            \
+    extern "C" __global__ __launch_bounds__(64) void name(dspb_seg_args G) { dspb_seg_chain_ind<CC, BB>(G); }
+DSPB_CHAIN_IND_KERNEL(dspb_seg_chain_ind_c2b512, 2, 512)
+DSPB_CHAIN_IND_KERNEL(dspb_seg_chain_ind_c2, 2, 0)
+DSPB_CHAIN_IND_KERNEL(dspb_seg_chain_ind_c1, 1, 0)
+DSPB_CHAIN_IND_KERNEL(dspb_seg_chain_ind_c4, 4, 0)

@@ -98,7 +98,7 @@ class dsp_callback_facts(C.Structure):  # module.h
                 ("writes_state", C.c_int32), ("input_control", C.c_int32), ("gain_form", C.c_int32),
                 ("gain_source", C.c_int32), ("gain_offset", C.c_uint32), ("gain_constant", C.c_float),
                 ("gain", C.c_char * 128), ("why", C.c_char * 256), ("gain_table_form", C.c_int32),
-                ("table_why", C.c_char * 128), ("state_reads_block", C.c_int32)]
+                ("table_why", C.c_char * 128), ("state_reads_block", C.c_int32), ("state_split", C.c_int32)]
 
     def as_dict(self) -> dict:
         return {"present": bool(self.present), "analyzed": bool(self.analyzed),
@@ -109,14 +109,14 @@ class dsp_callback_facts(C.Structure):  # module.h
                 "gain": self.gain.decode(errors="replace"), "why": self.why.decode(errors="replace"),
                 "gain_table_form": bool(self.gain_table_form),
                 "table_why": self.table_why.decode(errors="replace"),
-                "state_reads_block": bool(self.state_reads_block)}
+                "state_reads_block": bool(self.state_reads_block), "state_split": bool(self.state_split)}
 
 
 class dsp_state_spec_info(C.Structure):  # module.h
     _fields_ = [("used", C.c_int32), ("disabled", C.c_int32), ("segments", C.c_uint32),
                 ("blocks_per_segment", C.c_uint32), ("warmup_blocks", C.c_uint32), ("differed", C.c_uint32 * 3),
                 ("serial_reruns", C.c_uint32), ("levels", C.c_uint32), ("chain", C.c_int32),
-                ("chain_mismatch", C.c_uint32), ("chain_records_differed", C.c_uint32)]
+                ("chain_mismatch", C.c_uint32), ("chain_records_differed", C.c_uint32), ("split", C.c_int32)]
 
     def as_dict(self) -> dict:
         return {"used": bool(self.used), "disabled": bool(self.disabled), "segments": int(self.segments),
@@ -124,7 +124,7 @@ class dsp_state_spec_info(C.Structure):  # module.h
                 "differed": [int(v) for v in self.differed], "serial_reruns": int(self.serial_reruns),
                 "levels": int(self.levels), "chain": bool(self.chain),
                 "chain_mismatch": int(self.chain_mismatch),
-                "chain_records_differed": int(self.chain_records_differed)}
+                "chain_records_differed": int(self.chain_records_differed), "split": bool(self.split)}
 
 
 # name -> (restype, argtypes)

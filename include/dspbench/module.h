@@ -251,6 +251,9 @@ typedef struct dsp_state_spec_info {
                                     State the segment before ended with: rendered again by the walk */
     uint32_t chain_records_differed;  /* blocks whose State in the exact rerun differed from the
                                          chain's record */
+    int32_t split;               /* a split State (dsp_callback_facts.state_split): pass 1 started each
+                                    warm-up from the block-independent words a State chain recorded
+                                    there (a block counter), the others from the live State */
 } dsp_state_spec_info;
 /* Waits for the module's last speculative render and describes it. */
 int dsp_module_state_spec(dsp_module *m, dsp_state_spec_info *out);
@@ -307,6 +310,11 @@ typedef struct dsp_callback_facts {
                               a block sample (1 unless the analysis completed and showed
                               otherwise): 0 = the State's trajectory is the same whatever the
                               block holds (an oscillator's phase, a tremolo's) */
+    int32_t state_split;   /* state_reads_block, yet no branch depends on a sample and every store of
+                              a block-dependent value has a known offset: the State's words split into
+                              block-dependent ones and written block-independent ones (an envelope
+                              beside a block counter).  The speculative segments then start each
+                              warm-up from the independent words a State chain recorded there */
 } dsp_callback_facts;
 
 /* The facts of a loaded module (present = 0 for a code object without). */

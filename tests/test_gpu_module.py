@@ -526,19 +526,71 @@ def test_chain_kernels_drop_the_block_of_a_phase_accumulator():
         assert pb[k] > 1024, (k, pb[k])
 
 
+def _embedded_symbol(code: bytes, name: str) -> bytes:
+    """The bytes of data symbol `name` of an ELF64 code object (None if absent)."""
+    import struct
+    shoff, = struct.unpack_from("<Q", code, 0x28)
+    shentsize, shnum = struct.unpack_from("<HH", code, 0x3A)
+    secs = [struct.unpack_from("<IIQQQQIIQQ", code, shoff + i * shentsize) for i in range(shnum)]
+    for sh in secs:
+        if sh[1] != 2:  # SHT_SYMTAB
+            continue
+        strtab = secs[sh[6]]
+        for j in range(sh[5] // 24):
+            st_name, st_info, st_other, st_shndx, st_value, st_size = struct.unpack_from("<IBBHQQ", code,
+                                                                                     sh[4] + j * 24)
+            s0 = strtab[4] + st_name
+            if code[s0:code.index(b"\0", s0)].decode() == name and 0 < st_shndx < shnum:
+                sec = secs[st_shndx]
+                off = sec[4] + (st_value - sec[3])
+                return code[off:off + st_size]
+    return None
+
+
+CHAIN_KERNELS = ("dspb_seg_chain_c2b512", "dspb_seg_chain_c2", "dspb_seg_chain_c1", "dspb_seg_chain_c4")
+
+
 def test_chain_kernels_of_a_tremolo_come_from_edited_ir():
     """(CPU) A tremolo reads its block, so compiled from source its chain
     kernels keep the block in scratch; its State never depends on the block
-    (facts.state_reads_block = 0), so dsp_module_compile builds the module
-    through IR text with the callback's block stores deleted and the chain
-    kernels keep no private memory."""
+    (facts.state_reads_block = 0), so dsp_module_compile compiles the same
+    translation unit through IR text with the callback's block stores deleted
+    into a second code object, carried inside the module's as the symbol
+    dspb_chain_co, whose chain kernels keep no private memory.
+    Every other kernel of the module is the hiprtc compile's."""
     import sys
     sys.path.insert(0, HERE)
     import test_gpu_state_spec as t
     code = d.module.compile_source(t.TREMOLO_SRC, "tremolo.cpp")
     ps = _private_sizes(code)
-    for k in ("dspb_seg_chain_c2b512", "dspb_seg_chain_c2", "dspb_seg_chain_c1", "dspb_seg_chain_c4"):
-        assert ps[k] == 0, (k, ps[k])
+    chain = _embedded_symbol(code, "dspb_chain_co")
+    assert chain is not None and chain[:4] == b"\x7fELF"
+    pc = _private_sizes(chain)
+    for k in CHAIN_KERNELS:
+        assert ps[k] > 1024, (k, ps[k])  # the hiprtc chain kernel keeps the block
+        assert pc[k] == 0, (k, pc[k])    # the edited one does not
+
+
+def test_chain_of_a_split_state_comes_from_edited_ir():
+    """(CPU) envelope_counter.cpp: its State splits (an envelope beside a
+    block counter, dsp_callback_facts.state_split), so the edited code object
+    holds the chain of the counter alone (dspb_seg_chain_ind_*) with no
+    private memory -- the envelope, and with it the block, compiled away --
+    while the full chain kernels stay the hiprtc compile's (the envelope needs
+    the block: no State chain for the whole State)."""
+    code = d.module.compile_source(open(os.path.join(PLUGIN_DIR, "envelope_counter.cpp")).read(),
+                                   "envelope_counter.cpp")
+    assert d.module.code_facts(code)["state_split"]
+    chain = _embedded_symbol(code, "dspb_chain_co")
+    assert chain is not None
+    pc, ps = _private_sizes(chain), _private_sizes(code)
+    for k in CHAIN_KERNELS:
+        ki = k.replace("dspb_seg_chain_", "dspb_seg_chain_ind_")
+        assert pc[ki] == 0, (ki, pc[ki])
+        assert ps[k] > 1024, (k, ps[k])
+    # a plugin whose State does not split carries no edited chain
+    assert _embedded_symbol(d.module.compile_source(open(os.path.join(PLUGIN_DIR, "biquad.cpp")).read(),
+                                                    "biquad.cpp"), "dspb_chain_co") is None
 
 
 SHIFT_SRC = r'''

@@ -56,6 +56,24 @@ void audio_callback(const Parameters& p, State& st, float** out, const u32 C, co
 }
 '''
 
+# a running sum of the input: never forgets and depends on every block (no
+# warm-up level meets it, no State chain can follow it without the block)
+RUNNING_SUM_SRC = r'''
+#include "plugin_header.h"
+struct Parameters { FLOAT_PARAM(0.0f, 1.0f) g; };
+struct State { float sum; };
+Parameters default_parameters() { Parameters p = {0.5f}; return p; }
+State initialize_state(const Parameters& p, const unsigned C, const float sr, void* ctx) {
+    State s = {0.0f}; return s;
+}
+void audio_callback(const Parameters& p, State& st, float** out, const u32 C, const u32 B, const real32 sr) {
+    for (u32 s = 0; s < B; ++s) {
+        st.sum += out[0][s] * 1e-3f;
+        for (u32 c = 0; c < C; ++c) out[c][s] = out[c][s] * p.g + st.sum;
+    }
+}
+'''
+
 # an oscillator bank: a phase per channel in State (never forgets), the
 # block written and never read -- the State chain drops the block's arithmetic
 OSC_SRC = r'''
@@ -232,12 +250,13 @@ def test_one_pole_shapes(torch_cuda, C, cin, B, L):
 
 @pytest.mark.gpu
 def test_never_forgetting_state_is_exact_and_learned(torch_cuda):
-    """A block counter in the State: every speculative segment starts wrong,
-    at every warm-up level the render tries (4, then 64 blocks: a 1,024-block
-    one would be more than half the file), the walk renders them again in
-    order (exact), and the module renders these Parameters serially from the
-    next call on."""
-    mod = module_of(COUNTER_SRC, "counter_spec")
+    """A running sum of the input in the State: every speculative segment
+    starts wrong at every warm-up level the render tries (4, then 64 blocks:
+    a 1,024-block one would be more than half the file), the walk renders them
+    again in order (exact), and the module renders these Parameters serially
+    from the next call on (no State chain can follow a sum of the block)."""
+    mod = module_of(RUNNING_SUM_SRC, "running_sum_spec")
+    assert not mod.facts["state_split"]
     params = mod.default_parameters()
     x = noise(2, 150_000, 4)
     spec, ser, info = both(torch_cuda, mod, params, x, 2, 512, calls=3)
@@ -247,15 +266,42 @@ def test_never_forgetting_state_is_exact_and_learned(torch_cuda):
     assert info[0]["used"] and info[0]["levels"] == 2 and info[0]["warmup_blocks"] == 64
     assert info[0]["differed"][0] == info[0]["segments"] - 1 - 64 // seg
     assert info[0]["serial_reruns"] > 0
-    # (its envelope depends on the block: no State chain, the serial one)
     assert info[1]["disabled"] and not info[1]["used"] and not info[1]["chain"]
     assert info[2]["disabled"] and not info[2]["used"]
     # new Parameters: learnt again
     p2 = np.frombuffer(params, np.float32).copy()
-    p2[0] = 0.02
+    p2[0] = 0.25
     spec, ser, info = both(torch_cuda, mod, p2.tobytes(), x, 2, 512, calls=1)
     assert_same(spec, ser)
     assert info[0]["used"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("src", ["counter", "envelope_counter"])
+@pytest.mark.parametrize("C,cin,B,L", [(2, 2, 512, 300_000), (1, 1, 256, 120_000), (2, 1, 100, 80_001),
+                                       (4, 2, 64, 40_000), (3, 3, 512, 60_000)])
+def test_split_state_counter_beside_an_envelope(torch_cuda, src, C, cin, B, L):
+    """An envelope follower (forgets) beside a block counter (never forgets,
+    never reads the block): the analysis splits the State by 4-byte word
+    (dsp_callback_facts.state_split), a State chain of the counter alone runs
+    on one lane (the envelope and the block compiled away), and pass 1 starts
+    each segment's warm-up from the counter it recorded there and the live
+    State's envelope -- so the segments meet the true State after the warm-up
+    and the render is speculative, not serial.  Bit for bit against the
+    serial chain, State included, over three consecutive renders; three
+    channels have no chain kernel shape and fall back as before."""
+    if src == "counter":
+        mod = module_of(COUNTER_SRC, "counter_spec")
+    else:
+        mod = module_of(open(os.path.join(PLUGIN_DIR, "envelope_counter.cpp")).read(), "envelope_counter")
+    assert mod.facts["state_split"] and mod.facts["state_reads_block"]
+    params = mod.default_parameters()
+    spec, ser, info = both(torch_cuda, mod, params, noise(cin, L, 31), C, B, calls=3)
+    assert_same(spec, ser)
+    if C != 3:
+        for i in info:
+            assert i["used"] and i["split"] and not i["disabled"], info
+        assert info[0]["differed"][0] * 8 <= info[0]["segments"], info
 
 
 @pytest.mark.gpu

@@ -332,7 +332,7 @@ def test_state_reads_block_of_stock_plugins():
 # (dsp_plugin_analyze_shipped) gives the same facts for every plugin the tests
 # render.
 FACT_KEYS = ("analyzed", "reads_block", "writes_state", "input_control", "gain_form", "gain_table_form",
-             "state_reads_block")
+             "state_reads_block", "state_split")
 
 
 def _sources_rendered_by_the_tests():
@@ -347,7 +347,8 @@ def _sources_rendered_by_the_tests():
             srcs["tests/plugins/" + name] = open(os.path.join(PLUG, name)).read()
     srcs["plugins/biquad.cpp"] = open(os.path.join(os.path.dirname(HERE), "dsp-bench_amd", "plugins",
                                                    "biquad.cpp")).read()
-    for name in ("ONE_POLE_SRC", "COUNTER_SRC", "OSC_SRC", "TREMOLO_SRC", "BIG_STATE_SRC", "WAVETABLE_SRC"):
+    for name in ("ONE_POLE_SRC", "COUNTER_SRC", "RUNNING_SUM_SRC", "OSC_SRC", "TREMOLO_SRC", "BIG_STATE_SRC",
+                 "WAVETABLE_SRC"):
         srcs["state_spec/" + name] = getattr(ss, name)
     for name, body in sorted(ss.GEN_BODIES.items()):
         srcs["gen/" + name] = ss.GEN_HEAD + body
@@ -425,3 +426,60 @@ def test_strip_chain_block_stores_reads_the_address_operand():
     n, out = _strip(ir)
     assert n == -1
     assert out == ir
+
+
+# ---- a State that splits by word (dsp_callback_facts.state_split) ----------
+SPLIT = {
+    # an envelope (block-dependent) beside a block counter (independent)
+    "counter": ("struct State { float env; unsigned blocks; };",
+                "for (u32 s = 0; s < B; ++s) { const float x = out[0][s] < 0.0f ? -out[0][s] : out[0][s]; "
+                "st.env = st.env + p.g * (x - st.env); out[0][s] = st.env * (float)(st.blocks & 3u); } "
+                "st.blocks += 1u;", True),
+    # a phase beside a running sum: the phase alone is independent
+    "phase_and_sum": ("struct State { double ph; float sum; };",
+                      "for (u32 s = 0; s < B; ++s) { st.sum += out[0][s]; st.ph += 0.01; out[0][s] = st.sum; }",
+                      True),
+    # every written word depends on the block: nothing to split
+    "sum_only": ("struct State { float sum; float pad; };",
+                 "for (u32 s = 0; s < B; ++s) { st.sum += out[0][s]; out[0][s] = st.sum; }", False),
+    # the counter advances only when the block is loud (a branch on a sample): no split
+    "counter_under_a_branch": ("struct State { float env; unsigned blocks; };",
+                               "for (u32 s = 0; s < B; ++s) { if (out[0][s] > 0.5f) st.blocks += 1u; "
+                               "st.env += out[0][s]; }", False),
+    # the counter is read back into the envelope's update: still independent itself
+    "counter_feeds_env": ("struct State { float env; unsigned blocks; };",
+                          "for (u32 s = 0; s < B; ++s) st.env = st.env * 0.5f + out[0][s] * (float)st.blocks; "
+                          "st.blocks += 1u;", True),
+    # the envelope feeds the counter's increment: both depend on the block
+    "env_feeds_counter": ("struct State { float env; unsigned blocks; };",
+                          "for (u32 s = 0; s < B; ++s) st.env = st.env * 0.5f + out[0][s]; "
+                          "st.blocks += (unsigned)(st.env > 0.0f ? 1 : 2);", False),
+    # a counter in an array indexed by the channel: an offset the analysis cannot name
+    "indexed_words": ("struct State { float env[4]; unsigned blocks; };",
+                      "for (u32 c = 0; c < C && c < 4u; ++c) for (u32 s = 0; s < B; ++s) st.env[c] += out[c][s]; "
+                      "st.blocks += 1u;", False),
+}
+
+
+def split_snippet(state, body):
+    return ("#include \"plugin_header.h\"\n"
+            "struct Parameters { FLOAT_PARAM(0.0f, 1.0f) g; };\n" + state + "\n"
+            "Parameters default_parameters() { Parameters p = {0.5f}; return p; }\n"
+            "State initialize_state(const Parameters &p, const unsigned C, const float sr, void *ctx) "
+            "{ State s = {}; return s; }\n"
+            "void audio_callback(const Parameters &p, State &st, float **out, const u32 C, const u32 B, "
+            "const real32 sr) {\n" + body + "\n}\n")
+
+
+@pytest.mark.parametrize("case", sorted(SPLIT))
+def test_state_split_by_word(case):
+    """state_split: the State's 4-byte words split into those a store of a
+    block-dependent value may hit and written others, with no branch on a
+    sample and every dependent store at an offset the analysis names.  The
+    speculative segments then start each warm-up from the others' State chain
+    (DESIGN 4.6); a wrong split could only cost reruns (every segment is
+    checked bit for bit), so these cases pin the analysis, not the output."""
+    state, body, want = SPLIT[case]
+    f = dm.analyze_source(split_snippet(state, body))
+    assert f["analyzed"] and f["writes_state"] and f["state_reads_block"], (case, f)
+    assert f["state_split"] == want, (case, f)

@@ -30,6 +30,8 @@ OUT = os.environ.get("DSPB_MODULES_DIR", os.path.join(ROOT, "dsp-bench_amd", "mo
 
 # this repository's own example plugins (no reference needed)
 OWN = [os.path.join(ROOT, "dsp-bench_amd", "plugins", "biquad.cpp"),
+       # a split State (an envelope beside a block counter): the bench's envelope_src
+       os.path.join(ROOT, "dsp-bench_amd", "plugins", "envelope_counter.cpp"),
        # test plugins the bench times (the gain-table class: per-channel / per-position gains)
        os.path.join(ROOT, "tests", "plugins", "balance.cpp"), os.path.join(ROOT, "tests", "plugins", "fade_in.cpp")]
 
