@@ -94,11 +94,12 @@ def parse():
                     help="biquad: sections in the cascade (1 = plugins/biquad.cpp's low-pass; more add RBJ "
                          "peaking / high-pass sections)")
     ap.add_argument("--plugin", default=None,
-                    choices=["gain_test", "IR_test", "static_gain_plugin", "balance", "fade_in"],
+                    choices=["gain_test", "IR_test", "static_gain_plugin", "balance", "fade_in", "buffer_test"],
                     help="generic / generic_stft: the reference plugin source (default gain_test / IR_test; "
                          "static_gain_plugin = test/static_gain_plugin.cpp, a State the callback only reads; "
                          "balance / fade_in = tests/plugins/*.cpp, per-channel / per-position gains: the "
-                         "gain-table class)")
+                         "gain-table class; buffer_test = build/buffer_test.cpp, a State written through "
+                         "arena pointers: the serial chain, use --minutes 1)")
     ap.add_argument("--ir-plugin", default="source", choices=["source", "enum"],
                     help="headline / ch96k: source = the reference's IR_test.cpp compiled unchanged for gfx950 "
                          "(dsp-bench_amd/modules/mod_IR_test.co) and dispatched through its probed block class "
@@ -642,7 +643,10 @@ def main():
                 d.render_offline(x, CH, B, float(sr), gplug, out=out)
             workload = (f"{pname}.cpp via the generic plugin driver (B=512), {minutes:g} min of 48 kHz "
                         "stereo per GPU")
-            kname = ("dspb_render_lds (generic driver, hiprtc module)" if block_class == "callback" else
+            serial = not gmod.facts.get("analyzed") or gmod.facts.get("writes_state")
+            kname = ("dspb_render_st_c2b512 (generic driver: one chain through the State, LDS double buffer; "
+                     "the IR analysis cannot bound its stores, DESIGN 4.6)" if serial else
+                     "dspb_render_lds (generic driver, hiprtc module)" if block_class == "callback" else
                      "render_vec_kernel (the plugin's block class)")
             alg_desc = "C*L*(4 + 4) B (read + write)" if block_class != "table" else "C*L*4 B (write)"
         else:
