@@ -59,14 +59,28 @@ namespace {
 enum : uint32_t { O_BUF = 1, O_TBL = 2, O_PRM = 4, O_STA = 8, O_LOC = 16, O_GC = 32, O_GM = 64, O_EXT = 128, O_UNK = 256 };
 enum : uint32_t { D_IN = 1, D_VAR = 2, D_ADDR = 4 };
 
-// soff: for a pointer into State alone (org == O_STA), its constant byte
-// offset from the State's base: kSoffUnset before the fixpoint has seen a
-// definition, kSoffUnknown once two disagree or the offset is not a constant
-constexpr int64_t kSoffUnset = -2, kSoffUnknown = -1;
+// soff / shi: for a pointer into State alone (org == O_STA), the range of its
+// byte offset from the State's base, [soff, shi] (shi = kShiInf: no upper
+// bound -- an index the analysis knows only to be non-negative): kSoffUnset
+// before the fixpoint has seen a definition, kSoffUnknown when no range is
+// known (a negative or unparsed offset)
+constexpr int64_t kSoffUnset = -2, kSoffUnknown = -1, kShiInf = INT64_MAX;
 struct Val {
     uint32_t org = 0, data = 0;
-    int64_t soff = kSoffUnset;
+    int64_t soff = kSoffUnset, shi = kSoffUnset;
 };
+// the hull of two offset ranges
+void join_off(Val &a, const Val &b) {
+    if (b.soff == kSoffUnset) return;
+    if (a.soff == kSoffUnset) {
+        a.soff = b.soff, a.shi = b.shi;
+    } else if (a.soff == kSoffUnknown || b.soff == kSoffUnknown) {
+        a.soff = a.shi = kSoffUnknown;
+    } else {
+        a.soff = std::min(a.soff, b.soff);
+        a.shi = std::max(a.shi, b.shi);
+    }
+}
 
 // bytes of an IR scalar or vector type (0: not one this analysis sizes)
 int64_t type_bytes(const std::string &t) {
@@ -75,20 +89,28 @@ int64_t type_bytes(const std::string &t) {
         {"ptr", 8}, {"ptr addrspace(1)", 8}, {"ptr addrspace(5)", 4}, {"i1", 1}};
     auto it = kScalar.find(t);
     if (it != kScalar.end()) return it->second;
-    if (t.size() > 4 && t[0] == '<' && t.back() == '>') {  // <N x T>
+    if (t.size() > 4 && ((t[0] == '<' && t.back() == '>') || (t[0] == '[' && t.back() == ']'))) {  // <N x T>, [N x T]
         const size_t x = t.find(" x ");
         if (x == std::string::npos) return 0;
         const int64_t n = std::strtoll(t.c_str() + 1, nullptr, 10);
         const int64_t e = type_bytes(t.substr(x + 3, t.size() - x - 4));
-        return (n > 0 && e > 0) ? n * e : 0;
+        return (n > 0 && e > 0 && n < (1ll << 32)) ? n * e : 0;
     }
     return 0;
+}
+// the element type of an array type [N x T] ("" if not one)
+std::string array_elem(const std::string &t) {
+    if (t.size() < 6 || t[0] != '[' || t.back() != ']') return "";
+    const size_t x = t.find(" x ");
+    return x == std::string::npos ? "" : t.substr(x + 3, t.size() - x - 4);
 }
 
 struct Inst {
     std::string res, op, text;      // result (or ""), opcode, operand text after the opcode
     std::vector<std::string> parts; // `text` split at top-level commas
     int blk = 0;                    // its basic block (Analysis::blk_name)
+    bool nuw = false;               // a `nuw` flag (a getelementptr's offsets are non-negative)
+    std::string pred;               // icmp / fcmp: the predicate
 };
 
 bool ident_char(char c) {
@@ -203,9 +225,10 @@ struct Analysis {
     std::vector<Inst> body;
     std::vector<std::string> args;  // the kernel's six parameters
     uint32_t loc_data = 0, sta_data = 0;
-    // State stores by byte: the data bits stored at each known offset, and
-    // those of stores whose offset or extent is not known (any byte)
-    std::map<int64_t, uint32_t> sta_byte;
+    // State stores by byte: the data bits stored at each known offset, those
+    // of stores with a lower bound alone (every byte from there on), and those
+    // of stores whose offset or extent is not known (any byte)
+    std::map<int64_t, uint32_t> sta_byte, sta_tail;
     uint32_t sta_any = 0;
     Facts f;
     std::string fail;
@@ -246,24 +269,34 @@ struct Analysis {
         return false;
     }
 
+    // the bytes [lo, end) a pointer with offset range P touches with an access
+    // of n bytes (end = kShiInf: every byte from lo on); false: unknown
+    static bool extent(const Val &P, int64_t n, int64_t *lo, int64_t *end) {
+        if (P.org != O_STA || P.soff < 0 || n <= 0) return false;
+        *lo = P.soff;
+        *end = (P.shi == kShiInf || P.shi - P.soff > (1 << 16)) ? kShiInf : P.shi + n;
+        return true;
+    }
     // a store of data bits d through State pointer P of n bytes (0: extent unknown)
     void state_store(const Val &P, uint32_t d, int64_t n) {
         f.writes_state = true;
         sta_data |= d;
-        if (P.org == O_STA && P.soff >= 0 && n > 0)
-            for (int64_t b = P.soff; b < P.soff + n; ++b) sta_byte[b] |= d;
-        else
+        int64_t lo, end;
+        if (!extent(P, n, &lo, &end))
             sta_any |= d;
+        else if (end == kShiInf)
+            sta_tail[lo] |= d;
+        else
+            for (int64_t b = lo; b < end; ++b) sta_byte[b] |= d;
     }
     // the data bits a load of n bytes through State pointer P can see
     uint32_t state_load(const Val &P, int64_t n) const {
         uint32_t d = sta_any;
-        if (P.org == O_STA && P.soff >= 0 && n > 0) {
-            for (auto it = sta_byte.lower_bound(P.soff); it != sta_byte.end() && it->first < P.soff + n; ++it)
-                d |= it->second;
-        } else {
-            for (const auto &e : sta_byte) d |= e.second;
-        }
+        int64_t lo = 0, end = kShiInf;
+        if (!extent(P, n, &lo, &end)) lo = 0, end = kShiInf;
+        for (auto it = sta_byte.lower_bound(lo); it != sta_byte.end() && it->first < end; ++it) d |= it->second;
+        for (const auto &t : sta_tail)
+            if (t.first < end) d |= t.second;
         return d;
     }
 
@@ -351,24 +384,36 @@ struct Analysis {
             r.data = b.data;
             for (size_t k = 2; k < I.parts.size(); ++k)
                 for (const auto &t : values_in(I.parts[k], M)) r.data |= get(t).data;
-            // a State pointer plus one constant index of a sized element type
-            r.soff = kSoffUnknown;
-            if (b.org == O_STA && b.soff >= 0 && I.parts.size() == 3) {
-                const int64_t es = type_bytes(I.parts[0]);
-                const std::string &ix = I.parts[2];
-                const size_t sp = ix.find(' ');
-                if (es > 0 && sp != std::string::npos && ix[0] == 'i') {
-                    const std::string lit = trim(ix.substr(sp + 1));
-                    char *e = nullptr;
-                    const long long c = std::strtoll(lit.c_str(), &e, 10);
-                    if (!lit.empty() && e && *e == 0) r.soff = b.soff + c * es;
+            // a State pointer plus one index of a sized element type: a
+            // constant, an index of known range (a loop's counter bounded by
+            // its exit test), or (nuw) any non-negative one
+            // (an older LLVM -- the comgr a process gets once PyTorch's ROCm
+            // libraries are loaded -- keeps array GEPs: [N x T], 0, i; each
+            // index steps through the array types)
+            r.soff = r.shi = kSoffUnknown;
+            if (b.org == O_STA && b.soff >= 0 && I.parts.size() >= 3) {
+                std::string ty = trim(I.parts[0]);
+                int64_t lo = b.soff, hi = b.shi;
+                bool ok = true;
+                for (size_t k = 2; k < I.parts.size() && ok; ++k) {
+                    if (k > 2) ty = array_elem(ty);  // the next index steps inside an array
+                    const int64_t es = ty.empty() ? 0 : type_bytes(ty);
+                    int64_t ilo = 0, ihi = kShiInf;
+                    const bool known = es > 0 && index_range(I.parts[k], &ilo, &ihi);
+                    if (!known && !(es > 0 && I.nuw)) { ok = false; break; }
+                    if (!known || (ilo < 0 && I.nuw)) ilo = 0;  // nuw: the offsets are non-negative
+                    if (ilo > (1ll << 32) || ilo < -(1ll << 32)) { ok = false; break; }
+                    lo += ilo * es;
+                    hi = (hi == kShiInf || ihi == kShiInf || ihi > (1ll << 32)) ? kShiInf : hi + ihi * es;
                 }
+                if (ok && lo >= 0) r.soff = lo, r.shi = hi;
             } else if (b.soff == kSoffUnset) {
-                r.soff = kSoffUnset;
+                r.soff = r.shi = kSoffUnset;
             }
         } else if (op == "bitcast" || op == "addrspacecast" || op == "freeze") {
             merge_all(I.text);
-            r.soff = get(first_value(I.text, M)).soff;
+            const Val p = get(first_value(I.text, M));
+            r.soff = p.soff, r.shi = p.shi;
         } else if (op == "ptrtoint") {
             const Val p = get(first_value(I.text, M));
             if (p.org & (O_BUF | O_TBL | O_LOC | O_STA | O_PRM | O_EXT)) stop("an address is turned into an integer");
@@ -392,7 +437,7 @@ struct Analysis {
                 const Val v = get(first_value(two[0], M));
                 r.org |= v.org;
                 r.data |= v.data;
-                if (v.soff != kSoffUnset) r.soff = (r.soff == kSoffUnset || r.soff == v.soff) ? v.soff : kSoffUnknown;
+                join_off(r, v);
             }
             r.data |= D_VAR;
         } else if (op == "call") {
@@ -496,8 +541,7 @@ struct Analysis {
             merge_all(I.text);
             for (const auto &t : values_in(I.text, M)) {
                 const Val v = get(t);
-                if ((v.org & O_STA) && v.soff != kSoffUnset)
-                    r.soff = (r.soff == kSoffUnset || r.soff == v.soff) ? v.soff : kSoffUnknown;
+                if (v.org & O_STA) join_off(r, v);
             }
         }
         if (I.res.empty()) return false;
@@ -505,9 +549,19 @@ struct Analysis {
         const Val before = cur;
         cur.org |= r.org;
         cur.data |= r.data;
-        if (r.soff != kSoffUnset)
-            cur.soff = (cur.soff == kSoffUnset || cur.soff == r.soff) ? r.soff : kSoffUnknown;
-        return cur.org != before.org || cur.data != before.data || cur.soff != before.soff;
+        // the range this definition has had over every pass, widened: a bound
+        // that moves once more (a pointer stepped through a loop) is dropped,
+        // so that the fixpoint ends
+        if (r.soff != kSoffUnset) {
+            if (cur.soff == kSoffUnset) {
+                cur.soff = r.soff, cur.shi = r.shi;
+            } else if (cur.soff == kSoffUnknown || r.soff == kSoffUnknown || r.soff < cur.soff) {
+                cur.soff = cur.shi = kSoffUnknown;
+            } else if (r.shi > cur.shi) {
+                cur.shi = kShiInf;
+            }
+        }
+        return cur.org != before.org || cur.data != before.data || cur.soff != before.soff || cur.shi != before.shi;
     }
 
     std::set<std::string> gain_breakers, table_breakers;
@@ -526,7 +580,9 @@ struct Analysis {
         std::vector<bool> body;
     };
     std::vector<std::vector<int>> succ_;
+    std::vector<std::vector<bool>> dom_;  // dom_[b][a]: block a dominates block b
     std::vector<Loop> loops_;
+    bool loops_ok_ = false;
 
     static std::vector<std::string> labels_in(const std::string &t) {
         std::vector<std::string> out;
@@ -539,6 +595,8 @@ struct Analysis {
     }
 
     bool build_loops(std::string *why) {
+        loops_.clear();
+        loops_ok_ = false;
         const int n = (int)blk_name.size();
         std::map<std::string, int> id;
         for (int b = 0; b < n; ++b)
@@ -615,6 +673,135 @@ struct Analysis {
                         if (!in[p]) in[p] = true, work.push_back(p);
                 }
             }
+        dom_ = std::move(dom);
+        loops_ok_ = true;
+        return true;
+    }
+
+    // an integer literal operand ("i64 8", or the bare value)
+    static bool int_literal(const std::string &operand, int64_t *c) {
+        std::string lit = trim(operand);
+        const size_t sp = lit.rfind(' ');
+        if (sp != std::string::npos) {
+            if (lit[0] != 'i') return false;
+            lit = trim(lit.substr(sp + 1));
+        }
+        if (lit.empty()) return false;
+        char *e = nullptr;
+        const long long v = std::strtoll(lit.c_str(), &e, 10);
+        if (!e || *e != 0) return false;
+        *c = v;
+        return true;
+    }
+    // an upper bound of a loop-invariant integer: a literal, or
+    // llvm.umin / llvm.smin with a literal argument (through zext)
+    bool int_max(const std::string &operand, int64_t *hi) const {
+        if (int_literal(operand, hi)) return true;
+        std::string tok = first_value(operand, M);
+        for (int hop = 0; hop < 3 && !tok.empty(); ++hop) {
+            auto d = def.find(tok);
+            if (d == def.end()) return false;
+            const Inst &I = *d->second;
+            if (I.op == "zext") {
+                tok = first_value(I.text, M);
+                continue;
+            }
+            if (I.op != "call" || (I.text.find("@llvm.umin.") == std::string::npos &&
+                                   I.text.find("@llvm.smin.") == std::string::npos))
+                return false;
+            const size_t open = I.text.find('(');
+            const size_t close = I.text.rfind(')');
+            if (open == std::string::npos || close == std::string::npos || close <= open) return false;
+            bool have = false;
+            for (const auto &a : split_top(I.text.substr(open + 1, close - open - 1))) {
+                int64_t c;
+                if (int_literal(a, &c)) *hi = have ? std::min(*hi, c) : c, have = true;
+            }
+            return have;
+        }
+        return false;
+    }
+    // the largest value loop li's canonical IV `iv` takes in the loop, from an
+    // exit test every iteration runs (its block dominates each latch) that
+    // compares the IV or its increment with a loop-invariant bound
+    bool iv_max(const std::string &iv, int li, int64_t *hi) const {
+        const Loop &L = loops_[li];
+        const int n = (int)blk_name.size();
+        std::string next;  // the IV's increment (the phi's value from inside)
+        for (const Inst &I : body)
+            if (I.op == "add" && I.parts.size() == 2 && first_value(I.parts[0], M) == iv && trim(I.parts[1]) == "1" &&
+                L.body[I.blk])
+                next = I.res;
+        std::map<std::string, int> id;
+        for (int b = 0; b < n; ++b) id[blk_name[b]] = b;
+        bool found = false;
+        for (const Inst &B : body) {
+            if (B.op != "br" || !L.body[B.blk]) continue;
+            const auto lab = labels_in(B.text);
+            if (lab.size() != 2 || !id.count(lab[0]) || !id.count(lab[1])) continue;
+            const bool out0 = !L.body[id[lab[0]]], out1 = !L.body[id[lab[1]]];
+            if (out0 == out1) continue;
+            bool every = true;  // the test's block dominates every latch
+            for (int t = 0; t < n; ++t)
+                if (L.body[t])
+                    for (int h : succ_[t])
+                        if (h == L.header && !dom_[t][B.blk]) every = false;
+            if (!every) continue;
+            auto c = def.find(first_value(B.text, M));
+            if (c == def.end() || c->second->op != "icmp" || c->second->parts.size() != 2) continue;
+            const Inst &C = *c->second;
+            std::string x = first_value(C.parts[0], M), y = C.parts[1], p = C.pred;
+            // the counter on the left: swap a bound-first test
+            if (x != iv && (x.empty() || x != next)) {
+                x = first_value(C.parts[1], M), y = C.parts[0];
+                static const std::map<std::string, std::string> kSwap = {
+                    {"eq", "eq"}, {"ne", "ne"}, {"ult", "ugt"}, {"ugt", "ult"}, {"ule", "uge"}, {"uge", "ule"},
+                    {"slt", "sgt"}, {"sgt", "slt"}, {"sle", "sge"}, {"sge", "sle"}};
+                auto s = kSwap.find(p);
+                if (s == kSwap.end()) continue;
+                p = s->second;
+            }
+            if (x != iv && (x.empty() || x != next)) continue;
+            // bounds must not change inside the loop
+            const std::string yt = first_value(y, M);
+            if (!yt.empty()) {
+                auto yd = def.find(yt);
+                if (yd != def.end() && L.body[yd->second->blk]) continue;
+            }
+            int64_t bmax;
+            if (!int_max(y, &bmax)) continue;
+            // the loop leaves when the counter reaches the bound: exit on
+            // eq / uge / sge, stay on ne / ult / slt
+            const bool exit_on_true = out0;
+            const bool reach = exit_on_true ? (p == "eq" || p == "uge" || p == "sge")
+                                            : (p == "ne" || p == "ult" || p == "slt");
+            if (!reach) continue;
+            // the IV before the test is at most bound - 1 when the increment
+            // is compared, bound when the IV itself is (its last value runs the
+            // code before the test)
+            const int64_t m = x == next ? bmax - 1 : bmax;
+            *hi = found ? std::min(*hi, m) : m;
+            found = true;
+        }
+        return found;
+    }
+    // the range of an integer index operand: a literal, or a loop's canonical
+    // IV (through zext / sext) with the bound its exit test sets
+    bool index_range(const std::string &operand, int64_t *lo, int64_t *hi) const {
+        int64_t c;
+        if (int_literal(operand, &c)) return *lo = *hi = c, true;
+        if (!loops_ok_) return false;
+        std::string tok = first_value(operand, M);
+        for (int hop = 0; hop < 2 && !tok.empty(); ++hop) {
+            auto d = def.find(tok);
+            if (d == def.end()) return false;
+            if (d->second->op != "zext" && d->second->op != "sext") break;
+            tok = first_value(d->second->text, M);
+        }
+        const int li = iv_loop(tok);
+        int64_t m;
+        if (li < 0 || !iv_max(tok, li, &m) || m < 0) return false;
+        *lo = 0, *hi = m;
         return true;
     }
 
@@ -1029,11 +1216,12 @@ Facts analyze(const std::string &ir, const char *fn) {
         for (;;) {
             const size_t sp = tail.find(' ');
             if (sp == std::string::npos || !kFlags.count(tail.substr(0, sp))) break;
+            if (tail.compare(0, sp, "nuw") == 0) I.nuw = true;
             tail = trim(tail.substr(sp + 1));
         }
         if (I.op == "icmp" || I.op == "fcmp") {  // the predicate
             const size_t sp = tail.find(' ');
-            if (sp != std::string::npos) tail = trim(tail.substr(sp + 1));
+            if (sp != std::string::npos) I.pred = tail.substr(0, sp), tail = trim(tail.substr(sp + 1));
         }
         I.text = tail;
         I.parts = split_top(tail);
@@ -1063,15 +1251,21 @@ Facts analyze(const std::string &ir, const char *fn) {
     A.val[A.args[1]].org = O_STA;
     A.val[A.args[1]].soff = 0;
     A.val[A.args[2]].org = O_TBL;
+    A.val[A.args[1]].shi = 0;
+    // the loops first: the ranges of their counters bound State offsets
+    {
+        std::string why;
+        (void)A.build_loops(&why);  // (irreducible: no ranges; check_gain_table says why)
+    }
     bool settled = false;
     for (int it = 0; it < 64 && !settled; ++it) {
         bool grew = false;
         const uint32_t ld = A.loc_data, sd = A.sta_data, sa = A.sta_any;
-        const auto sb = A.sta_byte;
+        const auto sb = A.sta_byte, stl = A.sta_tail;
         const bool ws = A.f.writes_state;
         for (const Inst &I : A.body) grew |= A.step(I, false);
         settled = !grew && ld == A.loc_data && sd == A.sta_data && ws == A.f.writes_state && sa == A.sta_any &&
-                  sb == A.sta_byte;
+                  sb == A.sta_byte && stl == A.sta_tail;
     }
     // facts from values still growing would not be conservative
     if (!settled) A.stop("no fixpoint after 64 passes");
@@ -1086,17 +1280,28 @@ Facts analyze(const std::string &ir, const char *fn) {
     A.f.state_reads_block = A.f.writes_state && ((A.sta_data & D_IN) || A.f.input_control);
     // the State's words by dependence on the block: a word is block-dependent
     // when a store that may hit it carries a block sample (a store of unknown
-    // offset may hit any word); with a branch on a sample, every word is
+    // offset, or with a lower bound alone, may hit any word / every word from
+    // its bound on); with a branch on a sample, every word is
     if (A.f.state_reads_block && !A.f.input_control && !(A.sta_any & D_IN)) {
         std::set<int64_t> dep, written;
+        int64_t dep_from = kShiInf, written_from = kShiInf;  // the tails' first words
+        for (const auto &e : A.sta_tail) {
+            written_from = std::min(written_from, e.first / 4);
+            if (e.second & D_IN) dep_from = std::min(dep_from, e.first / 4);
+        }
         for (const auto &e : A.sta_byte) {
+            if (e.first / 4 >= dep_from) continue;
             written.insert(e.first / 4);
             if (e.second & D_IN) dep.insert(e.first / 4);
         }
-        bool indep_written = false;
+        bool indep_written = written_from < dep_from;
         for (int64_t w : written) indep_written = indep_written || !dep.count(w);
-        if (indep_written && !dep.empty() && *dep.rbegin() < 256) {
+        const bool any_dep = !dep.empty() || dep_from != kShiInf;
+        const int64_t last = dep_from != kShiInf ? dep_from : dep.empty() ? 0 : *dep.rbegin();
+        if (indep_written && any_dep && last < 256) {
             A.f.state_dep_words.assign(dep.begin(), dep.end());
+            // every word from dep_from on: one entry -(dep_from + 2)
+            if (dep_from != kShiInf) A.f.state_dep_words.push_back(-(dep_from + 2));
             A.f.state_split = true;
         }
     }

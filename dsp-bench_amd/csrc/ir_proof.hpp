@@ -46,10 +46,12 @@ struct Facts {
     // false the State's trajectory is the same whatever the block holds
     bool state_reads_block = true;
     // state_reads_block, but with no branch on a sample and every store of a
-    // block-dependent value at a known offset: the State's 4-byte words split
-    // into the block-dependent ones (state_dep_words, word indices) and the
-    // others, which at least one store writes -- whose trajectory is the same
-    // whatever the block holds (a block counter beside an envelope)
+    // block-dependent value at an offset of known range (a constant, a
+    // channel loop's counter bounded by its exit test) or known lower bound:
+    // the State's 4-byte words split into the block-dependent ones
+    // (state_dep_words: word indices, and -(T + 2) for every word from T on)
+    // and the others, which at least one store writes -- whose trajectory is
+    // the same whatever the block holds (a block counter beside an envelope)
     bool state_split = false;
     std::vector<int64_t> state_dep_words;
     std::string why;            // the first construct that ended the analysis, or why a

@@ -194,6 +194,7 @@ struct dsp_module {
         uint64_t slot_gen[2] = {};
         uint64_t perturb = 0;          // dsp_module_debug: the next State chain's wrong record (block + 1)
         std::vector<unsigned char> params;
+        uint32_t C = 0, B = 0;         // ... and the shape it was learnt with (kernels differ by shape)
     } seg;
     hipFunction_t f_sizes = nullptr, f_defaults = nullptr, f_init = nullptr, f_render = nullptr,
                   f_callback = nullptr;
@@ -938,6 +939,10 @@ static void facts_out(const dspb::irp::Facts &f, bool present, dsp_callback_fact
     std::strncpy(o->table_why, f.table_why.c_str(), sizeof o->table_why - 1);
     o->state_reads_block = f.state_reads_block;
     o->state_split = f.state_split;
+    std::string dw;
+    for (int64_t w : f.state_dep_words)
+        dw += (dw.empty() ? "" : ",") + (w >= 0 ? std::to_string(w) : std::to_string(-w - 2) + "-");
+    std::strncpy(o->state_dep_words, dw.c_str(), sizeof o->state_dep_words - 1);
 }
 
 int dsp_module_facts(const dsp_module *m, dsp_callback_facts *out) {
@@ -1224,7 +1229,7 @@ static int module_render_seg(dsp_module *m, RenderArgsG &A, hipStream_t s, bool 
     void *args[] = {&G};
     const unsigned lds = (unsigned)(nb * stride * sizeof(float));
     const unsigned gseg = (unsigned)((K + nb - 1) / nb), gchk = (unsigned)((K + 3) / 4);  // 4 segments per 256 threads
-    G.perturb = chain || fc ? W.perturb : 0;  // (test hook: consumed by the render that may run a chain)
+    G.perturb = chain || fc || fsplit ? W.perturb : 0;  // (test hook: consumed by the render that may run a chain)
     if (G.perturb) W.perturb = 0;
     MOD_HIP(hipMemsetAsync(W.words, 0, 32 * sizeof(unsigned), s));
     // the State chain's records checked: every boundary against the State the
@@ -1434,8 +1439,12 @@ int module_render(dsp_module *m, const void *params, uint32_t params_size, const
         auto &W = m->seg;
         if (int st = module_seg_collect(m, false)) return st;
         const unsigned char *pb = (const unsigned char *)params;
-        if (!W.warm || W.params.size() != params_size || (params_size && std::memcmp(W.params.data(), pb, params_size))) {
-            W.params.assign(pb, pb + params_size);  // new Parameters: learn again
+        if (!W.warm || W.C != C || W.B != B || W.params.size() != params_size ||
+            (params_size && std::memcmp(W.params.data(), pb, params_size))) {
+            // new Parameters, or a new shape (whether a State chain or a split
+            // State's chain exists depends on it): learn again
+            W.params.assign(pb, pb + params_size);
+            W.C = C, W.B = B;
             W.warm = kSegWarm0;
             W.off = W.chain_bad = false;
             ++W.gen;

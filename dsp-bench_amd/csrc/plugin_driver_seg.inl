@@ -56,17 +56,22 @@ struct dspb_seg_args {
 };
 // a split State (dsp_callback_facts.state_split): the 4-byte words a store of
 // a block-dependent value may hit (dsp_module_compile defines the list from
-// the callback's facts; -1: none)
+// the callback's facts; -1: none; -(T + 2): every word from T on)
 #ifndef DSPB_STATE_DEP_WORDS
 #define DSPB_STATE_DEP_WORDS -1
 #endif
 static constexpr int dspb_state_dep_words[] = {DSPB_STATE_DEP_WORDS};
 __device__ static constexpr bool dspb_word_dep(unsigned w) {
     for (int d : dspb_state_dep_words)
-        if (d == (int)w) return true;
+        if (d == (int)w || (d <= -2 && (int)w >= -d - 2)) return true;  // (-(T + 2): every word from T on)
     return false;
 }
 constexpr bool kStateWords = sizeof(State) % 4 == 0 && alignof(State) >= 4;
+__device__ static constexpr unsigned dspb_first_ind_word() {
+    for (unsigned i = 0; i < sizeof(State) / 4; ++i)
+        if (!dspb_word_dep(i)) return i;
+    return ~0u;
+}
 // the State chain took over within this render: the reruns, their checks and
 // the walk have nothing to do
 __device__ static bool dspb_seg_chained(const dspb_seg_args &G) { return *(volatile unsigned *)&G.stats[12] != 0; }
@@ -678,7 +683,15 @@ __device__ static void dspb_seg_chain_ind(const dspb_seg_args &G) {
             }
             audio_callback(prm, st, ptrs, CC, B, A.sr);
         }
-        dspb_copy_ind_words((void *)&G.st_ind[(unsigned long long)G.level * G.K + k], (const void *)&st);
+        State *rec = &G.st_ind[(unsigned long long)G.level * G.K + k];
+        dspb_copy_ind_words((void *)rec, (const void *)&st);
+        if constexpr (kStateWords) {
+            // test hook: a wrong record (the low bit of the first independent
+            // word) for segment perturb-1 at the first level
+            constexpr unsigned kW = dspb_first_ind_word();
+            if (kW < sizeof(State) / 4 && G.perturb && G.level == 0 && G.perturb - 1 == k)
+                ((dspb_word *)rec)[kW] ^= 1u;
+        }
     }
 }
 #define DSPB_CHAIN_IND_KERNEL(name, CC, BB)                                            \

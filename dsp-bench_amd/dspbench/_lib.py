@@ -98,7 +98,8 @@ class dsp_callback_facts(C.Structure):  # module.h
                 ("writes_state", C.c_int32), ("input_control", C.c_int32), ("gain_form", C.c_int32),
                 ("gain_source", C.c_int32), ("gain_offset", C.c_uint32), ("gain_constant", C.c_float),
                 ("gain", C.c_char * 128), ("why", C.c_char * 256), ("gain_table_form", C.c_int32),
-                ("table_why", C.c_char * 128), ("state_reads_block", C.c_int32), ("state_split", C.c_int32)]
+                ("table_why", C.c_char * 128), ("state_reads_block", C.c_int32), ("state_split", C.c_int32),
+                ("state_dep_words", C.c_char * 64)]
 
     def as_dict(self) -> dict:
         return {"present": bool(self.present), "analyzed": bool(self.analyzed),
@@ -109,7 +110,8 @@ class dsp_callback_facts(C.Structure):  # module.h
                 "gain": self.gain.decode(errors="replace"), "why": self.why.decode(errors="replace"),
                 "gain_table_form": bool(self.gain_table_form),
                 "table_why": self.table_why.decode(errors="replace"),
-                "state_reads_block": bool(self.state_reads_block), "state_split": bool(self.state_split)}
+                "state_reads_block": bool(self.state_reads_block), "state_split": bool(self.state_split),
+                "state_dep_words": self.state_dep_words.decode(errors="replace")}
 
 
 class dsp_state_spec_info(C.Structure):  # module.h

@@ -262,7 +262,10 @@ int dsp_module_state_spec(dsp_module *m, dsp_state_spec_info *out);
  * module's next render that runs the State chain flips a high bit of the State
  * the chain records for block `value` (a wrong record, as a miscompiled chain
  * would make); the render must still come out equal to the serial chain, with
- * the mismatch reported in dsp_state_spec_info. */
+ * the mismatch reported in dsp_state_spec_info.  In a render of a split State
+ * (dsp_state_spec_info.split) the same hook flips the low bit of the first
+ * block-independent word recorded for segment `value` at the first warm-up
+ * level: that segment starts wrong, its check fails and it is rendered again. */
 enum { DSP_MODULE_DEBUG_PERTURB_CHAIN = 1 };
 int dsp_module_debug(dsp_module *m, int what, uint64_t value);
 
@@ -315,6 +318,8 @@ typedef struct dsp_callback_facts {
                               block-dependent ones and written block-independent ones (an envelope
                               beside a block counter).  The speculative segments then start each
                               warm-up from the independent words a State chain recorded there */
+    char state_dep_words[64]; /* state_split: the block-dependent words, comma-separated word
+                              indices, "T-" for every word from T on (diagnostics) */
 } dsp_callback_facts;
 
 /* The facts of a loaded module (present = 0 for a code object without). */

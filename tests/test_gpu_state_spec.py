@@ -305,6 +305,53 @@ def test_split_state_counter_beside_an_envelope(torch_cuda, src, C, cin, B, L):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("src", ["counter", "envelope_counter"])
+@pytest.mark.parametrize("B,L", [(512, 300_000), (64, 40_000)])
+def test_split_state_record_is_checked_not_trusted(torch_cuda, src, B, L):
+    """A wrong record of the split State's independent words
+    (DSP_MODULE_DEBUG_PERTURB_CHAIN in a split render flips the low bit of
+    the block counter recorded for segment 7, as a wrong split would): that
+    segment's warm-up ends in a State unlike the one segment 6 ends with, the
+    boundary check fails and the segment is rendered again from the true
+    State -- output and State equal to the serial chain bit for bit, the
+    miss counted in pass 1's differed, the next calls unaffected."""
+    torch = torch_cuda
+    C = 2
+    # (an instance of its own: nothing learnt by the other tests' renders)
+    if src == "counter":
+        mod = module_of(COUNTER_SRC, f"counter_spec_{B}")
+    else:
+        mod = module_of(open(os.path.join(PLUGIN_DIR, "envelope_counter.cpp")).read(), f"envelope_counter_{B}")
+    params = mod.default_parameters()
+    x = torch.from_numpy(noise(C, L, 41)).cuda()
+    mod.initialize_state(params, C, 48000.0)
+    ser = mod.plugin(params, serial_state=True)
+    ref = [(d.render_offline(x, C, B, 48000.0, ser).cpu().numpy(), mod.read_state()) for _ in range(3)]
+    # a clean speculative render first: what pass 1 misses without the hook
+    mod.initialize_state(params, C, 48000.0)
+    plug = mod.plugin(params)
+    clean = d.render_offline(x, C, B, 48000.0, plug)
+    base = mod.state_spec()
+    assert base["used"] and base["split"] and base["segments"] > 8, base
+    mod.initialize_state(params, C, 48000.0)
+    plug = mod.plugin(params)
+    outs, infos = [], []
+    for call in range(3):
+        if call == 0:
+            mod.debug_perturb_chain(7)
+        y = d.render_offline(x, C, B, 48000.0, plug)
+        outs.append((y.cpu().numpy(), mod.read_state()))
+        infos.append(mod.state_spec())
+    assert_same(outs, ref)
+    assert np.array_equal(clean.cpu().numpy().view(np.uint32), ref[0][0].view(np.uint32))
+    hit = infos[0]
+    assert hit["used"] and hit["split"] and not hit["chain"], infos
+    assert hit["differed"][0] >= 1, (base, infos)
+    for i in infos[1:]:
+        assert i["used"] and i["split"] and i["differed"][0] * 8 <= i["segments"], (base, infos)
+
+
+@pytest.mark.gpu
 def test_reference_oscillator_sine_test(torch_cuda):
     """The reference's sine_test.cpp (a phase accumulator in State): on the
     first call every warm-up level fails and the State chain (the phase
@@ -542,7 +589,48 @@ void audio_callback(const Parameters& p, State& st, float** out, const u32 C, co
     for (u32 c = 0; c < C && c < 16; ++c)
         for (u32 s = 0; s < B; ++s) { st.z[c] = st.z[c] + st.k * (out[c][s] - st.z[c]); out[c][s] = st.z[c] - out[c][s]; }
 }''',
+    # a split State: a wrapping f64 phase (words 0-1, never forgets, never
+    # reads the block) before per-channel envelopes (forget)
+    "split_phase_env": r'''
+struct State { double phase; float env[2]; };
+State initialize_state(const Parameters& p, const unsigned C, const float sr, void* ctx) { State s = {}; return s; }
+void audio_callback(const Parameters& p, State& st, float** out, const u32 C, const u32 B, const real32 sr) {
+    const float g = (float)st.phase;
+    for (u32 c = 0; c < C && c < 2; ++c)
+        for (u32 s = 0; s < B; ++s) {
+            const float x = out[c][s] < 0.0f ? -out[c][s] : out[c][s];
+            st.env[c] += p.a * (x - st.env[c]);
+            out[c][s] = out[c][s] * g + st.env[c];
+        }
+    st.phase += (double)p.b * 0.01;
+    if (st.phase >= 1.0) st.phase -= 1.0;
+}''',
+    # a split State: one-poles before a u64 sample counter (words 2-3)
+    "split_counter_tail": r'''
+struct State { float z[2]; unsigned long long n; };
+State initialize_state(const Parameters& p, const unsigned C, const float sr, void* ctx) { State s = {}; return s; }
+void audio_callback(const Parameters& p, State& st, float** out, const u32 C, const u32 B, const real32 sr) {
+    const float k = (float)(st.n & 15ull) * 0.0625f;
+    for (u32 c = 0; c < C && c < 2; ++c)
+        for (u32 s = 0; s < B; ++s) { st.z[c] += p.a * (out[c][s] - st.z[c]); out[c][s] = st.z[c] + k * out[c][s]; }
+    st.n += B;
+}''',
+    # no split: a 16-bit counter shares its word with a block-dependent flag
+    # (the counter never forgets: the State chain renders it)
+    "shared_word": r'''
+struct State { unsigned short cnt; unsigned short hot; float y; };
+State initialize_state(const Parameters& p, const unsigned C, const float sr, void* ctx) { State s = {}; return s; }
+void audio_callback(const Parameters& p, State& st, float** out, const u32 C, const u32 B, const real32 sr) {
+    for (u32 s = 0; s < B; ++s) st.y += p.a * (out[0][s] - st.y);
+    st.hot = st.y > 0.1f ? 1 : 0;
+    st.cnt += 1;
+    const float g = 1.0f + 0.001f * (float)(st.cnt & 7u), o = st.hot ? 0.01f : 0.0f;
+    for (u32 c = 0; c < C; ++c)
+        for (u32 s = 0; s < B; ++s) out[c][s] = out[c][s] * g + o;
+}''',
 }
+# the generated plugins whose State splits by word (and those that must not)
+GEN_SPLIT = {"split_phase_env": True, "split_counter_tail": True, "shared_word": False}
 
 
 @pytest.mark.gpu
@@ -556,6 +644,11 @@ def test_generated_plugins_match_the_serial_chain(torch_cuda, name):
     assert_same(spec, ser)
     if f["analyzed"] and f["writes_state"] and mod.state_size <= 1024:
         assert info[0]["used"] or info[0]["disabled"]
+    if name in GEN_SPLIT:
+        assert f["state_split"] == GEN_SPLIT[name], str(f)
+        if GEN_SPLIT[name]:
+            # the independent words' chain: every call speculative
+            assert all(i["used"] and i["split"] and not i["chain"] for i in info), info
 
 
 @pytest.mark.gpu

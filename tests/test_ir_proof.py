@@ -430,15 +430,17 @@ def test_strip_chain_block_stores_reads_the_address_operand():
 
 # ---- a State that splits by word (dsp_callback_facts.state_split) ----------
 SPLIT = {
+    # (State, callback body, the block-dependent words -- "T-" every word from
+    # T on -- or False: no split)
     # an envelope (block-dependent) beside a block counter (independent)
     "counter": ("struct State { float env; unsigned blocks; };",
                 "for (u32 s = 0; s < B; ++s) { const float x = out[0][s] < 0.0f ? -out[0][s] : out[0][s]; "
                 "st.env = st.env + p.g * (x - st.env); out[0][s] = st.env * (float)(st.blocks & 3u); } "
-                "st.blocks += 1u;", True),
+                "st.blocks += 1u;", "0"),
     # a phase beside a running sum: the phase alone is independent
     "phase_and_sum": ("struct State { double ph; float sum; };",
                       "for (u32 s = 0; s < B; ++s) { st.sum += out[0][s]; st.ph += 0.01; out[0][s] = st.sum; }",
-                      True),
+                      "2"),
     # every written word depends on the block: nothing to split
     "sum_only": ("struct State { float sum; float pad; };",
                  "for (u32 s = 0; s < B; ++s) { st.sum += out[0][s]; out[0][s] = st.sum; }", False),
@@ -449,15 +451,34 @@ SPLIT = {
     # the counter is read back into the envelope's update: still independent itself
     "counter_feeds_env": ("struct State { float env; unsigned blocks; };",
                           "for (u32 s = 0; s < B; ++s) st.env = st.env * 0.5f + out[0][s] * (float)st.blocks; "
-                          "st.blocks += 1u;", True),
+                          "st.blocks += 1u;", "0"),
     # the envelope feeds the counter's increment: both depend on the block
     "env_feeds_counter": ("struct State { float env; unsigned blocks; };",
                           "for (u32 s = 0; s < B; ++s) st.env = st.env * 0.5f + out[0][s]; "
                           "st.blocks += (unsigned)(st.env > 0.0f ? 1 : 2);", False),
-    # a counter in an array indexed by the channel: an offset the analysis cannot name
+    # envelopes in an array indexed by the channel, the loop bounded by a
+    # constant (c < 4): the offsets' range is the array's
     "indexed_words": ("struct State { float env[4]; unsigned blocks; };",
                       "for (u32 c = 0; c < C && c < 4u; ++c) for (u32 s = 0; s < B; ++s) st.env[c] += out[c][s]; "
-                      "st.blocks += 1u;", False),
+                      "st.blocks += 1u;", "0,1,2,3"),
+    # the same loop bounded by C alone: every word from the array on
+    "indexed_unbounded": ("struct State { unsigned blocks; float env[4]; };",
+                          "for (u32 c = 0; c < C; ++c) for (u32 s = 0; s < B; ++s) st.env[c] += out[c][s]; "
+                          "st.blocks += 1u;", "1-"),
+    # ... which, before the counter, leaves nothing independent
+    "indexed_unbounded_first": ("struct State { float env[4]; unsigned blocks; };",
+                                "for (u32 c = 0; c < C; ++c) for (u32 s = 0; s < B; ++s) st.env[c] += out[c][s]; "
+                                "st.blocks += 1u;", False),
+    # a pointer stepped through the State by a loop (widened: no upper bound)
+    "pointer_walk": ("struct State { unsigned blocks; float env[4]; };",
+                     "float *e = st.env; for (u32 c = 0; c < C && c < 4u; ++c, ++e) "
+                     "for (u32 s = 0; s < B; ++s) *e += out[c][s]; st.blocks += 1u;", "1-"),
+    # a channel loop whose exit test sits under a branch (not run every
+    # iteration): no bound from it
+    "exit_test_under_a_branch": ("struct State { unsigned blocks; float env[4]; };",
+                                 "for (u32 c = 0; ; ++c) { for (u32 s = 0; s < B; ++s) st.env[c] += out[0][s]; "
+                                 "if (p.g > 0.25f) { if (c + 1 >= 4u) break; } else if (c + 1 >= 2u) break; } "
+                                 "st.blocks += 1u;", "1-"),
 }
 
 
@@ -482,4 +503,41 @@ def test_state_split_by_word(case):
     state, body, want = SPLIT[case]
     f = dm.analyze_source(split_snippet(state, body))
     assert f["analyzed"] and f["writes_state"] and f["state_reads_block"], (case, f)
-    assert f["state_split"] == want, (case, f)
+    assert f["state_split"] == bool(want), (case, f)
+    if want:
+        assert f["state_dep_words"] == want, (case, f)
+
+
+def test_state_split_under_the_comgr_torch_brings():
+    """A process that imports PyTorch first resolves comgr and hiprtc to the
+    copies PyTorch ships (an older LLVM, `torch/lib/libamd_comgr.so`): its IR
+    keeps array GEPs ([N x T], 0, i) where the system's folds them to
+    element GEPs -- the split analysis must name the same words from either
+    (the GPU tests import torch before they compile; these tests do not)."""
+    import subprocess
+    import sys
+    code = r'''
+import sys, json
+import torch
+sys.path.insert(0, %r); sys.path.insert(0, %r)
+import test_ir_proof as ti, test_gpu_state_spec as ss
+import dspbench.module as dm
+maps = [l.split()[-1] for l in open("/proc/self/maps") if "comgr" in l]
+out = {"comgr": sorted(set(maps))}
+for n, (st, body, want) in ti.SPLIT.items():
+    a = dm.analyze_source(ti.split_snippet(st, body))
+    out[n] = [a["state_split"], a["state_dep_words"]]
+for n in ss.GEN_SPLIT:
+    a = dm.analyze_source(ss.GEN_HEAD + ss.GEN_BODIES[n])
+    out["gen/" + n] = [a["state_split"], a["state_dep_words"]]
+print(json.dumps(out))
+''' % (HERE, os.path.join(os.path.dirname(HERE), "dsp-bench_amd"))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=600, cwd=HERE)
+    assert r.returncode == 0, r.stderr[-2000:]
+    import json
+    got = json.loads(r.stdout.strip().splitlines()[-1])
+    for n, (st, body, want) in SPLIT.items():
+        assert got[n] == [bool(want), want or ""], (n, got[n], got["comgr"])
+    import test_gpu_state_spec as ss
+    for n, want in ss.GEN_SPLIT.items():
+        assert got["gen/" + n][0] == want, (n, got["gen/" + n], got["comgr"])
