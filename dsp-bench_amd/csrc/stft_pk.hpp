@@ -63,11 +63,6 @@ enum { kPkNoBarDft = 1, kPkNoBarTw = 2, kPkNoBarSplit = 4, kPkRenderCached = 8, 
 // 0.1-0.5% on the memory and gain STFTs, the same VGPRs and spills;
 // profiles/r02_default_opt_ab.txt)
 constexpr int kPkDefaultOpt = kPkNoBarDft | kPkNoBarTw | kPkNoBarSplit;
-// split_y2's partner exchange through LDS float4 slots (1) or ds_bpermute
-// with lane 0's sends selected per value (0); an A/B build sets it
-#ifndef DSPB_SPLIT_LDS
-#define DSPB_SPLIT_LDS 0
-#endif
 // the fused IR_test (PER) kernels of the headline add one wave per workgroup:
 // 0.8-2.2% faster there, but 1-2% slower for the paths that read a signal
 // (memory, gain), whose four-frame workgroups share their hops in L2
@@ -124,55 +119,19 @@ __device__ __forceinline__ void split_y2(const cx2 (&Y2)[32], float *mrow, uint3
     const uint32_t src = ((64u - lane) & 63u) * 4u;
     const bool l0 = lane == 0;
     const v2f wl = tw[lane];  // W8192^l
-    // DSPB_SPLIT_LDS (A/B): the partners through the wave's free tile instead
-    // of 64 ds_bpermute: every lane stores what it sends for all 16 q as one
-    // float4 each, lane 0 then stores its own sends over its slots (one
-    // exec-masked region instead of 64 v_cndmask), one float4 read per q
-    constexpr bool XLDS = DSPB_SPLIT_LDS && !STAGE;
-    float4 *xs = reinterpret_cast<float4 *>(lds);
-    if constexpr (XLDS) {
-#pragma unroll
-        for (int q = 0; q < 16; ++q) {
-            const cx2 b = Y2[31 - q];
-            xs[64 * q + lane] = float4{b.r.x, b.r.y, b.i.x, b.i.y};
-        }
-        if (l0) {
-            // q = 0 pairs Y2[0] with itself unswapped: stored pre-swapped
-            xs[0] = float4{Y2[0].r.y, Y2[0].r.x, Y2[0].i.y, Y2[0].i.x};
-#pragma unroll
-            for (int q = 1; q < 16; ++q) {
-                const cx2 a = Y2[32 - q];
-                xs[64 * q] = float4{a.r.x, a.r.y, a.i.x, a.i.y};
-            }
-        }
-        lds_fence();
-    }
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
         if (BAR) __builtin_amdgcn_sched_barrier(0);
+        const cx2 a = Y2[q == 0 ? 0 : 32 - q], b = Y2[31 - q];
+        // what this lane sends to lane 64 - l (select on values: keeps Y2 in VGPRs)
+        const float sxr = l0 ? (q == 0 ? a.r.x : a.r.y) : b.r.y;
+        const float sxi = l0 ? (q == 0 ? a.i.x : a.i.y) : b.i.y;
+        const float syr = l0 ? (q == 0 ? a.r.y : a.r.x) : b.r.x;
+        const float syi = l0 ? (q == 0 ? a.i.y : a.i.x) : b.i.x;
+        const cx2 Pp = cx2{v2f{bperm(src, sxr), bperm(src, syr)}, v2f{bperm(src, sxi), bperm(src, syi)}};
         const cx2 Z = Y2[q];
-        cx2 E, D;
-        if constexpr (XLDS) {
-            // the partner's halves arrive unswapped: the swap rides on op_sel
-            const float4 t = xs[64 * q + ((64u - lane) & 63u)];
-            const v2f tr = v2f{t.x, t.y}, ti = v2f{t.z, t.w};
-            asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0]" : "=v"(E.r) : "v"(Z.r), "v"(tr));
-            asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1] neg_hi:[0,1]"
-                : "=v"(E.i) : "v"(Z.i), "v"(ti));
-            asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1] neg_hi:[0,1]"
-                : "=v"(D.r) : "v"(Z.r), "v"(tr));
-            asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0]" : "=v"(D.i) : "v"(Z.i), "v"(ti));
-        } else {
-            const cx2 a = Y2[q == 0 ? 0 : 32 - q], b = Y2[31 - q];
-            // what this lane sends to lane 64 - l (select on values: keeps Y2 in VGPRs)
-            const float sxr = l0 ? (q == 0 ? a.r.x : a.r.y) : b.r.y;
-            const float sxi = l0 ? (q == 0 ? a.i.x : a.i.y) : b.i.y;
-            const float syr = l0 ? (q == 0 ? a.r.y : a.r.x) : b.r.x;
-            const float syi = l0 ? (q == 0 ? a.i.y : a.i.x) : b.i.x;
-            const cx2 Pp = cx2{v2f{bperm(src, sxr), bperm(src, syr)}, v2f{bperm(src, sxi), bperm(src, syi)}};
-            E = cx2{Z.r + Pp.r, Z.i - Pp.i};
-            D = cx2{Z.r - Pp.r, Z.i + Pp.i};
-        }
+        const cx2 E = cx2{Z.r + Pp.r, Z.i - Pp.i};
+        const cx2 D = cx2{Z.r - Pp.r, Z.i + Pp.i};
         // u = W8192^(l + 64 q); T = (-i D.x u, -i D.y (-i u)) with U1 = u, U2 = (u.i, -u.r)
         v2f u = wl;
         if (q) u = v2f{wl.x, wl.x} * v2f{kW128_re[q], kW128_im[q]} + v2f{wl.y, wl.y} * v2f{-kW128_im[q], kW128_re[q]};
