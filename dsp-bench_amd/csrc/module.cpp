@@ -399,6 +399,8 @@ int dsp_module_compile(const char *source, const char *name, void **code, uint64
                 tu += (i ? "," : "") + std::to_string(facts.state_dep_words[i]);
             tu += "\n";
         }
+        // diagnostics: pass 1's phase clocks (dsp_module_seg_timing)
+        if (std::getenv("DSPB_SEG_TIMING")) tu += "#define DSPB_SEG_TIMING 1\n";
         tu += kSegDriver;
     }
     const std::string round = "-DDSPB_LDS_ROUND_BYTES=" + std::to_string(kLdsRoundBytes) + "u";
@@ -714,6 +716,16 @@ int dsp_module_debug(dsp_module *m, int what, uint64_t value) {
     }
     std::lock_guard<std::mutex> lk(m->mu);
     m->seg.perturb = value + 1;
+    return DSP_OK;
+}
+
+int dsp_module_seg_timing(dsp_module *m, uint32_t out[8]) {
+    if (!m || !out) return DSP_ERR_INVALID;
+    std::lock_guard<std::mutex> lk(m->mu);
+    std::memset(out, 0, 8 * sizeof(uint32_t));
+    if (!m->seg.words) return DSP_OK;
+    MOD_HIP(hipDeviceSynchronize());
+    MOD_HIP(hipMemcpy(out, m->seg.words + 24, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost));
     return DSP_OK;
 }
 

@@ -365,6 +365,20 @@ __device__ static void dspb_segments_pf(const dspb_seg_args &G) {
             }
         }
     };
+#ifdef DSPB_SEG_TIMING
+    // diagnostics (a module compiled with DSPB_SEG_TIMING set, module.cpp):
+    // where wave 0's lane 0 spends pass 1's rounds, in shader clocks, summed
+    // over the workgroups into stats[16, 24) (dsp_module_seg_timing)
+    unsigned long long tm[5] = {0, 0, 0, 0, 0}, t0 = __builtin_amdgcn_s_memtime(), nr = 0;
+#define DSPB_TMARK(i)                                                   \
+    if (!kRerun && t == 0) {                                            \
+        const unsigned long long tn = __builtin_amdgcn_s_memtime();     \
+        tm[i] += tn - t0;                                               \
+        t0 = tn;                                                        \
+    }
+#else
+#define DSPB_TMARK(i)
+#endif
     if (BB && rounds) load(0, 0);
     for (unsigned r = 0; r < rounds; ++r) {
         if constexpr (BB != 0) {
@@ -376,7 +390,9 @@ __device__ static void dspb_segments_pf(const dspb_seg_args &G) {
             }
         }
         __syncthreads();
+        DSPB_TMARK(0)
         if (BB && r + 1 < rounds) load(r + 1, 0);  // in flight while the callbacks run
+        DSPB_TMARK(1)
         if (k != 0xffffffffu && r < s_len[t]) {
             if (dspb_seg_block<kRerun>(G, (unsigned long long)s_first[t] + r, r, s_warm[t], st)) {
                 float *blk = dspb_lbuf + t * SB;
@@ -388,7 +404,9 @@ __device__ static void dspb_segments_pf(const dspb_seg_args &G) {
                 stopped = true;
             }
         }
+        DSPB_TMARK(2)
         __syncthreads();
+        DSPB_TMARK(3)
 #pragma unroll
         for (unsigned c = 0; c < C; ++c) {
 #pragma unroll
@@ -409,10 +427,261 @@ __device__ static void dspb_segments_pf(const dspb_seg_args &G) {
         __syncthreads();
         rounds = 0;
         for (unsigned i = 0; i < NB; ++i) rounds = s_len[i] > rounds ? s_len[i] : rounds;
+        DSPB_TMARK(4)
+#ifdef DSPB_SEG_TIMING
+        ++nr;
+#endif
     }
     if (k != 0xffffffffu && !stopped) dspb_copy_state((void *)&G.st_end[k], (const void *)&st);
+#ifdef DSPB_SEG_TIMING
+    if (!kRerun && t == 0) {
+        // (phases: 0 staging + barrier, 1 next round's loads issued, 2 the
+        // callbacks, 3 the barrier after them, 4 copy-out + barrier)
+        for (int i = 0; i < 5; ++i) atomicAdd(&G.stats[16 + i], (unsigned)(tm[i] >> 4));
+        atomicAdd(&G.stats[21], 1u);
+        atomicAdd(&G.stats[22], (unsigned)nr);
+    }
+#endif
+#undef DSPB_TMARK
 }
-#define DSPB_SEG_KERNEL(name, CC, BB)                                                  \
+// the same for a constant B, with the work split by role: wave 0 runs the
+// callbacks and nothing else; waves 1-3 move the blocks.  A round's kept
+// blocks go from LDS into registers and the next round's blocks from
+// registers into the same slots (each thread the slots it read: no barrier
+// between), then -- after the barrier that frees wave 0 for the next
+// round's callbacks -- the kept blocks are stored and the round after next
+// is loaded.  The stores and loads (a chip-wide burst of a round's blocks
+// each way) drain while the callbacks run instead of holding up the
+// callback wave's issue (dsp_module_seg_timing: a round of
+// envelope_counter.cpp spent 29% of its clocks issuing the next loads
+// behind the copy-out's stores and 14% in the copy-out).
+template <unsigned CC, unsigned BB, bool kRerun>
+__device__ __attribute__((always_inline, flatten)) static void dspb_segments_roles(const dspb_seg_args &G) {
+    extern __shared__ float dspb_lbuf[];
+    __shared__ unsigned s_first[64], s_warm[64], s_len[64];
+    constexpr unsigned C = CC, B = BB, SB = C * B + 2u, NB = dspb_seg_nb(CC * BB + 2u);
+    // the movers (waves 1-3) move float4 units: one 16-byte load / store per
+    // unit in HBM, two 8-byte LDS accesses (rows are 8-byte aligned: C B + 2
+    // floats apart, so that the callback lanes sit on distinct banks).
+    // (float2 units -- 512 contiguous bytes per LDS instruction, no bank
+    // conflicts -- measured slower: twice the slots' bookkeeping, 16.4k vs
+    // 8.0k clocks per round for the swap; profiles/r06_seg_roles.txt)
+    constexpr unsigned R4 = B / 4u, T4 = NB * R4, NW = 192u;
+    constexpr unsigned PV = (T4 + NW - 1u) / NW;
+    constexpr bool kFull = T4 % NW == 0;
+    static_assert(NB <= 64 && BB % 4 == 0, "one wave runs a round's callbacks");
+    const dspb_render_args &A = G.R;
+    const unsigned t = threadIdx.x;
+    const unsigned base = blockIdx.x * NB;
+    if (!kRerun) {  // pass 1: at a warm-up level that runs; it restarts the listing
+        if (!dspb_seg_level_runs(G)) return;
+        if (G.level && blockIdx.x == 0 && t == 0) *G.count = 0;
+    } else if (dspb_seg_skip(G)) {
+        return;
+    }
+    const unsigned nseg = (kRerun && !G.exact) ? *(volatile unsigned *)G.count : G.K;
+    if (base >= nseg) return;  // the same for the whole workgroup
+    unsigned k = 0xffffffffu;
+    if (t < NB) k = dspb_seg_lane(G, base, t, nseg, s_first, s_warm, s_len);
+    __syncthreads();
+    unsigned rounds = 0;
+    for (unsigned i = 0; i < NB; ++i) rounds = s_len[i] > rounds ? s_len[i] : rounds;
+    const dspb_gfloat *xin[C];
+    dspb_gfloat *xout[C];
+    bool aligned_in = true, aligned_out = true;
+#pragma unroll
+    for (unsigned c = 0; c < C; ++c) {
+        xin[c] = (const dspb_gfloat *)A.in[c < A.in_ch ? c : 0];
+        xout[c] = (dspb_gfloat *)A.out[c];
+        if (c < A.in_ch) aligned_in = aligned_in && !(((unsigned long long)A.in[c]) & 15);
+        aligned_out = aligned_out && !(((unsigned long long)A.out[c]) & 15);
+    }
+    const bool mover = t >= 64u;
+    // (movers only; made opaque once per round, so that the slots' indices
+    // are recomputed where used instead of 24 of them held in registers
+    // across the loop)
+    unsigned tm = t - 64u;
+    // mover slot v: float4 s of block i's row.  A wave's 64 slots of one v
+    // start at a multiple of 64 units and a row holds 128: i is the same for
+    // the whole wave, so the block's first / warm-up / length come from the
+    // lanes' copies (lane l: block l's, read once per round) by readlane,
+    // not from LDS once per slot
+    unsigned m_first = 0, m_warm = 0, m_len = 0;
+    auto refresh = [&]() {
+        const unsigned l = t & 63u;
+        m_first = l < NB ? s_first[l] : 0u;
+        m_warm = l < NB ? s_warm[l] : 0u;
+        m_len = l < NB ? s_len[l] : 0u;
+    };
+    auto slot = [&](unsigned v, unsigned &i, unsigned &s) -> bool {
+        const unsigned q = tm + NW * v;
+        i = __builtin_amdgcn_readfirstlane(q / R4);
+        s = (q - i * R4) * 4u;
+        return kFull || q < T4;
+    };
+    auto len_of = [&](unsigned i) { return (unsigned)__builtin_amdgcn_readlane((int)m_len, (int)i); };
+    auto warm_of = [&](unsigned i) { return (unsigned)__builtin_amdgcn_readlane((int)m_warm, (int)i); };
+    auto first_of = [&](unsigned i) { return (unsigned)__builtin_amdgcn_readlane((int)m_first, (int)i); };
+    typedef __attribute__((address_space(1))) float4 gfloat4;
+    float4 pf[C][PV], ob[C][PV];
+    auto load = [&](unsigned r) {
+#pragma unroll
+        for (unsigned c = 0; c < C; ++c)
+#pragma unroll
+            for (unsigned v = 0; v < PV; ++v) {
+                unsigned i, s;
+                float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (slot(v, i, s) && r < len_of(i) && c < A.in_ch) {
+                    const unsigned long long gi = (unsigned long long)(first_of(i) + r) * B + s;
+                    if (aligned_in && gi + 4 <= A.L) {
+                        x = *(const gfloat4 *)(xin[c] + gi);
+                    } else {
+                        x.x = gi < A.L ? xin[c][gi] : 0.f;
+                        x.y = gi + 1 < A.L ? xin[c][gi + 1] : 0.f;
+                        x.z = gi + 2 < A.L ? xin[c][gi + 2] : 0.f;
+                        x.w = gi + 3 < A.L ? xin[c][gi + 3] : 0.f;
+                    }
+                }
+                pf[c][v] = x;
+            }
+    };
+    auto put = [&](unsigned r) {
+#pragma unroll
+        for (unsigned c = 0; c < C; ++c)
+#pragma unroll
+            for (unsigned v = 0; v < PV; ++v) {
+                unsigned i, s;
+                if (slot(v, i, s) && r < len_of(i)) {
+                    float2 *d = (float2 *)(dspb_lbuf + i * SB + c * B + s);
+                    d[0] = make_float2(pf[c][v].x, pf[c][v].y);
+                    d[1] = make_float2(pf[c][v].z, pf[c][v].w);
+                }
+            }
+    };
+    // round r's kept blocks out of their slots, round r + 1's in (put: r + 1
+    // is rendered), slot by slot: a slot's outgoing unit takes the registers
+    // its incoming one frees (one set of registers live, not two)
+    auto swap = [&](unsigned r, bool put_next) {
+#pragma unroll
+        for (unsigned c = 0; c < C; ++c)
+#pragma unroll
+            for (unsigned v = 0; v < PV; ++v) {
+                unsigned i, s;
+                const bool in = slot(v, i, s);
+                float2 *d = (float2 *)(dspb_lbuf + i * SB + c * B + s);
+                if (in && r >= warm_of(i) && r < len_of(i)) {
+                    const float2 lo = d[0], hi = d[1];
+                    ob[c][v] = make_float4(lo.x, lo.y, hi.x, hi.y);
+                }
+                if (in && put_next && r + 1 < len_of(i)) {
+                    d[0] = make_float2(pf[c][v].x, pf[c][v].y);
+                    d[1] = make_float2(pf[c][v].z, pf[c][v].w);
+                }
+            }
+    };
+    auto send = [&](unsigned r) {
+#pragma unroll
+        for (unsigned c = 0; c < C; ++c)
+#pragma unroll
+            for (unsigned v = 0; v < PV; ++v) {
+                unsigned i, s;
+                if (slot(v, i, s) && r >= warm_of(i) && r < len_of(i)) {
+                    const unsigned long long gi = (unsigned long long)(first_of(i) + r) * B + s;
+                    const float4 o = ob[c][v];
+                    if (aligned_out) {
+                        *(gfloat4 *)(xout[c] + gi) = o;
+                    } else {
+                        xout[c][gi] = o.x, xout[c][gi + 1] = o.y, xout[c][gi + 2] = o.z, xout[c][gi + 3] = o.w;
+                    }
+                }
+            }
+    };
+    Parameters prm = dspb_from_global<Parameters>(A.P);
+    State st;
+    bool stopped = false;
+    if (k != 0xffffffffu) {
+        dspb_copy_state((void *)&st, (kRerun && (k || !G.exact)) ? (const void *)&G.st_blk[(unsigned long long)k * G.seg]
+                                                                  : (const void *)A.S);
+        if (!kRerun && G.split && k) dspb_copy_ind_words((void *)&st, (const void *)&G.st_ind[G.level * G.K + k]);
+    }
+#ifdef DSPB_SEG_TIMING
+    unsigned long long tmk[5] = {0, 0, 0, 0, 0}, t0 = __builtin_amdgcn_s_memtime(), nr = 0;
+#define DSPB_TMARK(i)                                                   \
+    if (!kRerun && t == 0) {                                            \
+        const unsigned long long tn = __builtin_amdgcn_s_memtime();     \
+        tmk[i] += tn - t0;                                              \
+        t0 = tn;                                                        \
+    }
+#else
+#define DSPB_TMARK(i)
+#endif
+    if (mover && rounds) {
+        refresh();
+        load(0);
+        put(0);
+        if (rounds > 1) load(1);
+    }
+    __syncthreads();
+    DSPB_TMARK(0)
+    // two loops, one per role, behind a wave-uniform branch: each wave meets
+    // the same barriers (two per round, the round count read from s_len by
+    // all alike), and the movers' registers (a round's blocks in flight) are
+    // not live across the callbacks' code, which has the registers to itself
+    if (__builtin_amdgcn_readfirstlane(t >> 6) == 0) {
+        for (unsigned r = 0; r < rounds;) {
+            if (k != 0xffffffffu && r < s_len[t]) {
+                if (dspb_seg_block<kRerun>(G, (unsigned long long)s_first[t] + r, r, s_warm[t], st)) {
+                    float *blk = dspb_lbuf + t * SB;
+                    float *ptrs[C];
+                    for (unsigned c = 0; c < C; ++c) ptrs[c] = blk + c * B;
+                    audio_callback(prm, st, ptrs, C, B, A.sr);
+                } else {
+                    s_len[t] = r;  // met the recorded chain: the rest stands
+                    stopped = true;
+                }
+            }
+            DSPB_TMARK(2)
+            __syncthreads();  // (A) the callbacks of round r are done, s_len final for it
+            DSPB_TMARK(3)
+            unsigned next = 0;
+            for (unsigned i = 0; i < NB; ++i) next = s_len[i] > next ? s_len[i] : next;
+            __syncthreads();  // (B) round r + 1 staged by the movers
+            DSPB_TMARK(4)
+            rounds = next;
+            ++r;
+#ifdef DSPB_SEG_TIMING
+            ++nr;
+#endif
+        }
+    } else {
+        for (unsigned r = 0; r < rounds;) {
+            asm volatile("" : "+v"(tm));
+            __syncthreads();  // (A)
+            unsigned next = 0;
+            for (unsigned i = 0; i < NB; ++i) next = s_len[i] > next ? s_len[i] : next;
+            refresh();  // (s_len as the callbacks of round r left it)
+            swap(r, r + 1 < next);  // (each thread the slots it reads)
+            __syncthreads();  // (B)
+            asm volatile("" : "+v"(tm));
+            send(r);
+            if (r + 2 < next) load(r + 2);
+            rounds = next;
+            ++r;
+        }
+    }
+    if (k != 0xffffffffu && !stopped) dspb_copy_state((void *)&G.st_end[k], (const void *)&st);
+#ifdef DSPB_SEG_TIMING
+    if (!kRerun && t == 0) {
+        // (phases: 0 the first round staged, 2 the callbacks, 3 the barrier
+        // after them, 4 take / put + barrier; 1 unused)
+        for (int i = 0; i < 5; ++i) atomicAdd(&G.stats[16 + i], (unsigned)(tmk[i] >> 4));
+        atomicAdd(&G.stats[21], 1u);
+        atomicAdd(&G.stats[22], (unsigned)nr);
+    }
+#endif
+#undef DSPB_TMARK
+}
+#define DSPB_SEG_KERNEL(name, CC, BB)                                                \
     extern "C" __global__ __launch_bounds__(256) void name(dspb_seg_args G) { dspb_segments<CC, BB>(G); }
 // pass 1 and the reruns as kernels of their own: pass 1 carries no
 // comparison (its registers are the callback's)
@@ -422,7 +691,16 @@ __device__ static void dspb_segments_pf(const dspb_seg_args &G) {
 #define DSPB_SEG_PF_KERNEL(name, CC, BB, RR)                                           \
     extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RR ? 1 : 2, 2))) void name(  \
         dspb_seg_args G) { dspb_segments_pf<CC, BB, RR>(G); }
-DSPB_SEG_PF_KERNEL(dspb_seg_c2b512, 2, 512, false)
+// (dspb_segments_roles is flattened: the movers' unrolled code makes it
+// large enough that the inliner would otherwise leave audio_callback a call
+// -- its block pointers through scratch, its LDS accesses flat: 6x slower
+// callbacks, measured)
+#define DSPB_SEG_ROLES_KERNEL(name, CC, BB, RR)                                        \
+    extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RR ? 1 : 2, 2))) void name(  \
+        dspb_seg_args G) { dspb_segments_roles<CC, BB, RR>(G); }
+DSPB_SEG_ROLES_KERNEL(dspb_seg_c2b512, 2, 512, false)
+// (the reruns keep the single-role kernel: the roles' unrolled movers leave
+// the rerun's State comparison no registers, and their arrays go to scratch)
 DSPB_SEG_PF_KERNEL(dspb_seg_c2b512_rerun, 2, 512, true)
 DSPB_SEG_PF_KERNEL(dspb_seg_c2, 2, 0, false)
 DSPB_SEG_PF_KERNEL(dspb_seg_c2_rerun, 2, 0, true)

@@ -217,6 +217,7 @@ _OPTIONAL_SIGS = {
     "dsp_module_debug": (C.c_int, [C.c_void_p, C.c_int, C.c_uint64]),
     "dsp_ir_strip_chain_stores": (C.c_int, [C.c_char_p, C.c_char_p, C.c_uint64, C.POINTER(C.c_int32)]),
     "dsp_plugin_analyze_shipped": (C.c_int, [C.c_char_p, C.POINTER(dsp_callback_facts)]),
+    "dsp_module_seg_timing": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32)]),
     "dsp_stft_pk_ab_options": (C.c_int, [C.c_int]),
 }
 

@@ -278,6 +278,14 @@ int dsp_module_debug(dsp_module *m, int what, uint64_t value);
  * code); the edited text goes to out (out_cap bytes; NULL: not wanted). */
 int dsp_ir_strip_chain_stores(const char *ir, char *out, uint64_t out_cap, int32_t *dropped);
 
+/* Diagnostics: a module compiled with the environment variable
+ * DSPB_SEG_TIMING set carries clocks of its speculative pass 1 (wave 0,
+ * lane 0 of every workgroup, units of 16 shader clocks, summed over the
+ * workgroups): out[0] staging + barrier, [1] the next round's loads issued,
+ * [2] the callbacks, [3] the barrier after them, [4] copy-out + barrier,
+ * [5] workgroups, [6] rounds.  Waits for the device; zeros otherwise. */
+int dsp_module_seg_timing(dsp_module *m, uint32_t out[8]);
+
 /* ---- what the callback does with its block (no GPU) ----------------------
  * dsp_module_compile compiles the plugin a second time into an analysis
  * kernel, dspb_proof(P, S, out, C, B, sr) { audio_callback(*P, *S, out, C, B,
