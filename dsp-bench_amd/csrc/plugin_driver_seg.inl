@@ -922,8 +922,8 @@ DSPB_CHAIN_KERNEL(dspb_seg_chain_c1, 1, 0)
 DSPB_CHAIN_KERNEL(dspb_seg_chain_c4, 4, 0)
 
 // ---- a split State: the chain of its block-independent words --------------
-// The callback in file order on one lane, as dspb_seg_chain, recording only
-// the words no block-dependent store can hit (dspb_word_dep: compile-time, so
+// The callback in file order, as dspb_seg_chain (over 64 lanes' ranges of
+// segments, below), recording only the words no block-dependent store can hit (dspb_word_dep: compile-time, so
 // the arithmetic that feeds only the other words -- an envelope, and with it
 // the block -- is compiled away and the chain is the counter's alone).  Pass 1
 // then starts each segment's warm-up from these words and the live State's
@@ -932,20 +932,30 @@ DSPB_CHAIN_KERNEL(dspb_seg_chain_c4, 4, 0)
 template <unsigned CC, unsigned BB>
 __device__ static void dspb_seg_chain_ind(const dspb_seg_args &G) {
     const dspb_render_args &A = G.R;
-    if (threadIdx.x != 0 || blockIdx.x != 0 || !kStateWords) return;
+    if (blockIdx.x != 0 || !kStateWords) return;
     if (!dspb_seg_level_runs(G)) return;  // launched before each warm-up level's pass 1
     constexpr unsigned BMAX = BB ? BB : 4096u;
     const unsigned B = BB ? BB : A.B;
     const Parameters prm = dspb_from_global<Parameters>(A.P);
-    State st;
-    dspb_copy_state((void *)&st, (const void *)A.S);
     // (block indices fit 32 bits: the host renders no longer file this way)
     const unsigned nb = (unsigned)A.nblocks, seg = (unsigned)G.seg;
+    // the segments 1 .. K - 1 in 64 contiguous ranges, one per lane: a lane
+    // runs the chain from the file's start to its range's first record, then
+    // on through its range.  Each stretch between records is the callback over
+    // the blocks of the stretch, the block compiled away: a counter's or a
+    // phase step's stretch the optimizer closes into a few instructions, so the
+    // lanes' long first stretches cost what a short one does, and the 9,122
+    // records of a stereo hour come from 64 lanes (one lane took 0.58 ms);
+    // a stretch that stays a loop costs the longest lane's blocks, as the one
+    // lane's chain over the whole file did.
+    const unsigned n = G.K - 1, per = (n + 63u) / 64u, lane = threadIdx.x & 63u;
+    const unsigned k0 = 1u + lane * per, k1 = k0 + per < G.K ? k0 + per : G.K;
+    State st;
+    dspb_copy_state((void *)&st, (const void *)A.S);
     unsigned b = 0;
-    for (unsigned k = 1; k < G.K; ++k) {
+    for (unsigned k = k0; k < k1; ++k) {
         // pass 1 at this level starts segment k's warm-up at block p: the
-        // callback up to there (a stretch with no record in it: a counter's
-        // stretch compiles to one add), then the record
+        // callback up to there, then the record
         const unsigned b0 = k * seg, p = b0 > G.warm ? b0 - G.warm : 0u, e = p < nb ? p : nb;
         for (; b < e; ++b) {
             float dspb_chain_blk[CC * BMAX];
