@@ -799,3 +799,46 @@ def test_state_chain_is_checked_not_trusted(torch_cuda, which, when, where):
     # a render before it reports nothing
     for i in infos[:perturbed]:
         assert i["chain_mismatch"] == 0 and i["chain_records_differed"] == 0, infos
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["biquad", "envelope_counter"])
+def test_segments_pinned_to_the_host_build(torch_cuda, oracle, name):
+    """The speculative segments (and the split State's chain for
+    envelope_counter.cpp) against the plugin built for the host the way the
+    reference's JIT builds a plugin (oracle/_ref/libplug_<name>.so: the
+    reference's own wrapper and flags, ref compiler.cpp:507-515) -- not a
+    GPU self-comparison.  That build's flags let the compiler reassociate
+    and contract, so it is not IEEE-per-operation like the module's: the
+    bound is a tolerance (the GPU segments equal the GPU serial chain bit for
+    bit, the other tests).  20 s of stereo, B = 512, two consecutive renders
+    (the State carries), the default Parameters on both sides."""
+    ref_so = os.path.join(os.path.dirname(HERE), "oracle", "_ref", f"libplug_{name}.so")
+    path = os.path.join(MODS, f"mod_{name}.co")
+    if not (os.path.exists(ref_so) and os.path.exists(path)):
+        pytest.skip("oracle/_ref or the modules not built")
+    torch = torch_cuda
+    with open(path, "rb") as f:
+        mod = d.module.Module(f.read())
+    params = mod.default_parameters()
+    ref = oracle.RefPlugin(name, 2, 48000.0, prefix="libplug_")
+    assert bytes(ref.params[:mod.params_size]) == params
+    C, B = 2, 512
+    x = noise(C, 48000 * 20 + 77, 61) * np.float32(0.8)
+    mod.initialize_state(params, C, 48000.0)
+    plug = mod.plugin(params, name)
+    xg = torch.from_numpy(x).cuda()
+    worst = 0.0
+    for call in range(2):
+        got = d.render_offline(xg, C, B, 48000.0, plug).cpu().numpy()
+        info = mod.state_spec()
+        want = oracle.render_offline([x[0], x[1]], C, B, 48000.0, ref.as_oracle())
+        assert got.shape == want.shape
+        assert np.all(np.isfinite(got))
+        err = float(np.max(np.abs(got.astype(np.float64) - want)))
+        worst = max(worst, err)
+        assert info["used"] and not info["chain"], info
+        if name == "envelope_counter":
+            assert info["split"], info
+    print(f"{name}: max |GPU segments - host build| = {worst:.3e}")
+    assert worst <= 1e-4, worst
