@@ -842,3 +842,37 @@ def test_segments_pinned_to_the_host_build(torch_cuda, oracle, name):
             assert info["split"], info
     print(f"{name}: max |GPU segments - host build| = {worst:.3e}")
     assert worst <= 1e-4, worst
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("src", ["one_pole", "counter"])
+def test_role_split_pass_edges(torch_cuda, src):
+    """The role-split pass 1 of stereo B = 512 (dspb_seg_c2b512: wave 0 the
+    callbacks, waves 1-3 the blocks) on its edge paths: one input channel for
+    two output channels (the movers load zeros for the missing one), input
+    and output rows 4 bytes off 16-byte alignment (the movers' dword path),
+    a ragged tail -- against the serial chain bit for bit, State included,
+    over two consecutive renders."""
+    torch = torch_cuda
+    mod = module_of(ONE_POLE_SRC if src == "one_pole" else COUNTER_SRC, f"{src}_roles_edges")
+    params = mod.default_parameters()
+    C, B, L = 2, 512, 300_001
+    nb = (L + B - 1) // B
+    base = torch.from_numpy(noise(1, L + 1, 71)).cuda()
+    x = base[:, 1:]  # 4 bytes past a 16-byte boundary
+    assert x.data_ptr() % 16 == 4
+    res = {}
+    for serial in (False, True):
+        mod.initialize_state(params, C, 48000.0)
+        plug = mod.plugin(params, serial_state=serial)
+        outs = []
+        for _ in range(2):
+            big = torch.empty((C, nb * B + 1), device="cuda")
+            out = big[:, 1:]
+            y = d.render_offline(x, C, B, 48000.0, plug, out=out)
+            outs.append((y.cpu().numpy(), mod.read_state()))
+            if not serial:
+                info = mod.state_spec()
+                assert info["used"] and info["segments"] > 1, info
+        res[serial] = outs
+    assert_same(res[False], res[True])
