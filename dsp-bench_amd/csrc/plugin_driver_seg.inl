@@ -657,9 +657,14 @@ __device__ __attribute__((always_inline, flatten)) static void dspb_segments_rol
         for (unsigned r = 0; r < rounds;) {
             asm volatile("" : "+v"(tm));
             __syncthreads();  // (A)
-            unsigned next = 0;
-            for (unsigned i = 0; i < NB; ++i) next = s_len[i] > next ? s_len[i] : next;
             refresh();  // (s_len as the callbacks of round r left it)
+            // the next round count from the lanes' copies (one LDS read per
+            // lane, then scalar maxima) rather than NB reads in a row
+            unsigned next = 0;
+            for (unsigned i = 0; i < NB; ++i) {
+                const unsigned l = (unsigned)__builtin_amdgcn_readlane((int)m_len, (int)i);
+                next = l > next ? l : next;
+            }
             swap(r, r + 1 < next);  // (each thread the slots it reads)
             __syncthreads();  // (B)
             asm volatile("" : "+v"(tm));
