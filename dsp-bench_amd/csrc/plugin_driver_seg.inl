@@ -513,6 +513,7 @@ __device__ __attribute__((always_inline, flatten)) static void dspb_segments_rol
         m_warm = l < NB ? s_warm[l] : 0u;
         m_len = l < NB ? s_len[l] : 0u;
     };
+    static_assert(R4 % 64u == 0 && NW % 64u == 0, "a wave's 64 units of one slot lie in one block row");
     auto slot = [&](unsigned v, unsigned &i, unsigned &s) -> bool {
         const unsigned q = tm + NW * v;
         i = __builtin_amdgcn_readfirstlane(q / R4);
