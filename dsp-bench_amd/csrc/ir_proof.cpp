@@ -597,6 +597,7 @@ struct Analysis {
     bool build_loops(std::string *why) {
         loops_.clear();
         loops_ok_ = false;
+        iv_max_memo_.clear();
         const int n = (int)blk_name.size();
         std::map<std::string, int> id;
         for (int b = 0; b < n; ++b)
@@ -724,7 +725,20 @@ struct Analysis {
     // the largest value loop li's canonical IV `iv` takes in the loop, from an
     // exit test every iteration runs (its block dominates each latch) that
     // compares the IV or its increment with a loop-invariant bound
+    mutable std::map<std::string, std::pair<bool, int64_t>> iv_max_memo_;  // (the CFG is fixed: per IV once)
     bool iv_max(const std::string &iv, int li, int64_t *hi) const {
+        auto memo = iv_max_memo_.find(iv);
+        if (memo != iv_max_memo_.end()) {
+            if (memo->second.first) *hi = memo->second.second;
+            return memo->second.first;
+        }
+        int64_t m = 0;
+        const bool ok = iv_max_scan(iv, li, &m);
+        iv_max_memo_[iv] = {ok, m};
+        if (ok) *hi = m;
+        return ok;
+    }
+    bool iv_max_scan(const std::string &iv, int li, int64_t *hi) const {
         const Loop &L = loops_[li];
         const int n = (int)blk_name.size();
         std::string next;  // the IV's increment (the phi's value from inside)
