@@ -190,6 +190,8 @@ struct dsp_module {
         uint32_t warm = 0;             // learned warm-up for `params` (0: not yet)
         bool off = false;              // learned: the chain does not forget its State
         bool chain_bad = false;        // learned: the State chain's records failed their check
+        bool one_level = false;        // learned: the first warm-up level suffices (the others not launched)
+        bool slot_one[2] = {};         // the render in the slot was launched with the first level alone
         uint64_t gen = 0;              // bumped when `params` change (learn only from renders with them)
         uint64_t slot_gen[2] = {};
         uint64_t perturb = 0;          // dsp_module_debug: the next State chain's wrong record (block + 1)
@@ -1115,8 +1117,17 @@ int module_seg_collect(dsp_module *m, bool wait) {
         if (!spec || first_warm != W.warm || W.off) continue;
         const uint64_t early = std::min<uint64_t>(r.segments - 1, warm / r.blocks_per_segment);
         const uint64_t guessed = r.segments - 1 - early;
-        if (guessed && r.differed[0] * 8ull > guessed) W.off = true;  // the longest warm-up it could try failed
-        else W.warm = warm;
+        const bool failed = guessed && r.differed[0] * 8ull > guessed;
+        if (W.slot_one[i]) {  // launched with the first level alone
+            if (failed) W.one_level = false;  // the levels again from the next call
+            continue;
+        }
+        if (failed) {
+            W.off = true;  // the longest warm-up it could try failed
+        } else {
+            W.warm = warm;
+            W.one_level = r.levels == 1;  // the first level sufficed
+        }
     }
     return DSP_OK;
 }
@@ -1227,6 +1238,7 @@ static int module_render_seg(dsp_module *m, RenderArgsG &A, hipStream_t s, bool 
         MOD_HIP(hipEventSynchronize(W.ev[slot]));
         if (int st = module_seg_collect(m, false)) return st;
     }
+    W.slot_one[slot] = false;  // (set below when the levels are cut to the first)
     SegArgsG G{};
     G.R = A;
     G.R.lds_nb = (unsigned)nb;
@@ -1284,6 +1296,12 @@ static int module_render_seg(dsp_module *m, RenderArgsG &A, hipStream_t s, bool 
             }
             lw[nlev++] = warm;
         }
+        // learnt: the first level meets the State (the later ones would only
+        // return at once, a launch each of pass 1, its check and the split
+        // chain); a render where it does not is still exact (reruns, walk)
+        // and unlearns it
+        if (W.one_level) nlev = 1;
+        W.slot_one[slot] = W.one_level;
         if (fsplit) {
             G.st_ind = W.ind;
             G.split = 1;
@@ -1458,7 +1476,7 @@ int module_render(dsp_module *m, const void *params, uint32_t params_size, const
             W.params.assign(pb, pb + params_size);
             W.C = C, W.B = B;
             W.warm = kSegWarm0;
-            W.off = W.chain_bad = false;
+            W.off = W.chain_bad = W.one_level = false;
             ++W.gen;
         }
         // (learned never to forget: the State chain, then the segments exactly)
