@@ -84,6 +84,7 @@ constexpr LdsShape kChainIndShapes[4] = {{"dspb_seg_chain_ind_c2b512", 2, 512}, 
 constexpr uint32_t kChainMaxB = 4096;
 constexpr uint32_t kSegMaxState = 1024;   // bytes of State a lane copies (the walk keeps one in LDS)
 constexpr uint32_t kSegWarm0 = 4;         // blocks of warm-up of a first render
+constexpr uint32_t kSegWarmBumps = 2;     // at most this many blocks added for a few misses
 constexpr uint32_t kSegWarmMax = 4096;    // the longest warm-up (blocks); past it, the chain is serial
 constexpr uint32_t kSegLevels = 4;        // warm-up levels a render may try (x16 each)
 constexpr uint32_t kSegMinBlocks = 4;     // blocks per segment at least
@@ -191,6 +192,7 @@ struct dsp_module {
         bool off = false;              // learned: the chain does not forget its State
         bool chain_bad = false;        // learned: the State chain's records failed their check
         bool one_level = false;        // learned: the first warm-up level suffices (the others not launched)
+        uint32_t bumps = 0;            // warm-up blocks added after renders whose few misses took a rerun
         bool slot_one[2] = {};         // the render in the slot was launched with the first level alone
         uint64_t gen = 0;              // bumped when `params` change (learn only from renders with them)
         uint64_t slot_gen[2] = {};
@@ -1119,7 +1121,14 @@ int module_seg_collect(dsp_module *m, bool wait) {
         const uint64_t guessed = r.segments - 1 - early;
         const bool failed = guessed && r.differed[0] * 8ull > guessed;
         if (W.slot_one[i]) {  // launched with the first level alone
-            if (failed) W.one_level = false;  // the levels again from the next call
+            if (failed) {
+                W.one_level = false;  // the levels again from the next call
+            } else if (r.differed[0] && W.bumps < kSegWarmBumps) {
+                // a few segments missed and took a rerun (its rounds cost more
+                // than one more warm-up round for all): one block longer
+                W.warm += 1;
+                ++W.bumps;
+            }
             continue;
         }
         if (failed) {
@@ -1477,6 +1486,7 @@ int module_render(dsp_module *m, const void *params, uint32_t params_size, const
             W.C = C, W.B = B;
             W.warm = kSegWarm0;
             W.off = W.chain_bad = W.one_level = false;
+            W.bumps = 0;
             ++W.gen;
         }
         // (learned never to forget: the State chain, then the segments exactly)
