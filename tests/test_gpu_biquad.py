@@ -294,14 +294,26 @@ def test_biquad_look_back_give_up_chain_mode(torch_cuda, oracle):
     L = 2048 * 300
     x = np.zeros((1, L), np.float32)
     x[0, :64] = rng.uniform(-1, 1, 64).astype(np.float32)
-    _repairs()
-    try:
-        _debug_set(1, 0)
-        got = d.render_offline(torch_cuda.from_numpy(x).cuda(), 1, 512, 48000.0, d.Plugin.biquad(coef)).cpu().numpy()
-    finally:
-        _debug_set(1, 2**64 - 1)
-    assert _repairs() > 0
-    y64, _ = oracle.biquad_f64(x[0], coef, got.shape[1])
-    err = float(np.max(np.abs(got[0].astype(np.float64) - y64)))
-    err32 = float(np.max(np.abs(oracle.biquad_f32(x[0], coef, got.shape[1]).astype(np.float64) - y64)))
-    assert err <= 4 * err32 + 1e-6 * float(np.abs(y64).max()), (err, err32)
+    xt = torch_cuda.from_numpy(x).cuda()
+    y64 = err32 = None
+    # whether a wave finds a word missing at its first look depends on the
+    # launch's timing: a render without a give-up is simply the scan's; up to
+    # five renders, each within the bound, until one gave up and was repaired
+    repaired = 0
+    for _ in range(5):
+        _repairs()
+        try:
+            _debug_set(1, 0)
+            got = d.render_offline(xt, 1, 512, 48000.0, d.Plugin.biquad(coef)).cpu().numpy()
+            torch_cuda.cuda.synchronize()
+        finally:
+            _debug_set(1, 2**64 - 1)
+        repaired = _repairs()
+        if y64 is None:
+            y64, _ = oracle.biquad_f64(x[0], coef, got.shape[1])
+            err32 = float(np.max(np.abs(oracle.biquad_f32(x[0], coef, got.shape[1]).astype(np.float64) - y64)))
+        err = float(np.max(np.abs(got[0].astype(np.float64) - y64)))
+        assert err <= 4 * err32 + 1e-6 * float(np.abs(y64).max()), (err, err32)
+        if repaired:
+            break
+    assert repaired > 0
