@@ -268,15 +268,23 @@ def test_biquad_look_back_give_up_is_repaired_in_the_call(torch_cuda, oracle, S)
     p = d.Plugin.biquad(coef)
     ref = d.render_offline(xt, 2, 512, 48000.0, p)
     torch_cuda.cuda.synchronize()
-    _repairs()  # reset the counter
-    try:
-        _debug_set(1, 0)
-        got = d.render_offline(xt, 2, 512, 48000.0, p)
-        torch_cuda.cuda.synchronize()
-    finally:
-        _debug_set(1, 2**64 - 1)
-    assert _repairs() > 0
-    check(oracle, got.cpu().numpy(), x, coef, got.shape[1])
+    # (a give-up needs a word missing at a wave's first look, which depends
+    # on the launch's timing: up to five renders, each within the bound,
+    # until one gave up and was repaired)
+    repaired = 0
+    for _ in range(5):
+        _repairs()  # reset the counter
+        try:
+            _debug_set(1, 0)
+            got = d.render_offline(xt, 2, 512, 48000.0, p)
+            torch_cuda.cuda.synchronize()
+        finally:
+            _debug_set(1, 2**64 - 1)
+        repaired = _repairs()
+        check(oracle, got.cpu().numpy(), x, coef, got.shape[1])
+        if repaired:
+            break
+    assert repaired > 0
     again = d.render_offline(xt, 2, 512, 48000.0, p)
     torch_cuda.cuda.synchronize()
     assert torch_cuda.equal(again, ref)
