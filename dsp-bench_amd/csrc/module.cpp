@@ -191,9 +191,9 @@ struct dsp_module {
         uint32_t warm = 0;             // learned warm-up for `params` (0: not yet)
         bool off = false;              // learned: the chain does not forget its State
         bool chain_bad = false;        // learned: the State chain's records failed their check
-        bool one_level = false;        // learned: the first warm-up level suffices (the others not launched)
+        bool one_level = false;        // learned: the first warm-up level suffices (two levels launched)
         uint32_t bumps = 0;            // warm-up blocks added after renders whose few misses took a rerun
-        bool slot_one[2] = {};         // the render in the slot was launched with the first level alone
+        bool slot_one[2] = {};         // the render in the slot was launched with the first two levels alone
         uint64_t gen = 0;              // bumped when `params` change (learn only from renders with them)
         uint64_t slot_gen[2] = {};
         uint64_t perturb = 0;          // dsp_module_debug: the next State chain's wrong record (block + 1)
@@ -1120,9 +1120,9 @@ int module_seg_collect(dsp_module *m, bool wait) {
         const uint64_t early = std::min<uint64_t>(r.segments - 1, warm / r.blocks_per_segment);
         const uint64_t guessed = r.segments - 1 - early;
         const bool failed = guessed && r.differed[0] * 8ull > guessed;
-        if (W.slot_one[i]) {  // launched with the first level alone
-            if (failed) {
-                W.one_level = false;  // the levels again from the next call
+        if (W.slot_one[i]) {  // launched with the first two levels alone
+            if (failed || r.levels > 1) {
+                W.one_level = false;  // every level again from the next call
             } else if (r.differed[0] && W.bumps < kSegWarmBumps) {
                 // a few segments missed and took a rerun (its rounds cost more
                 // than one more warm-up round for all): one block longer
@@ -1307,9 +1307,11 @@ static int module_render_seg(dsp_module *m, RenderArgsG &A, hipStream_t s, bool 
         }
         // learnt: the first level meets the State (the later ones would only
         // return at once, a launch each of pass 1, its check and the split
-        // chain); a render where it does not is still exact (reruns, walk)
-        // and unlearns it
-        if (W.one_level) nlev = 1;
+        // chain): the first two levels alone -- the second one is there for
+        // a render whose input keeps the first from meeting the State (it
+        // unlearns this; without it such a render fell to the reruns and the
+        // walk's serial chain, 465 segments of a 20 s peak follower)
+        if (W.one_level) nlev = std::min<uint32_t>(nlev, 2);
         W.slot_one[slot] = W.one_level;
         if (fsplit) {
             G.st_ind = W.ind;

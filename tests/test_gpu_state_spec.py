@@ -901,11 +901,11 @@ void audio_callback(const Parameters& p, State& st, float** out, const u32 C, co
 @pytest.mark.gpu
 def test_one_level_learning_unlearns_when_the_input_stops_forgetting(torch_cuda):
     """Once a render's first warm-up level met the State the module launches
-    that level alone; a later render whose input keeps the segments from
-    meeting the State (a peak follower fed a quiet signal after a loud one)
-    must still come out exact -- the reruns and the walk -- and the module
-    goes back to the levels.  Each render against the serial chain, bit for
-    bit, State included."""
+    the first two levels alone; a later render whose input keeps the first
+    from meeting the State (a peak follower fed a quiet signal after a loud
+    one) takes the second and comes out exact, and the module goes back to
+    every level.  Each render against the serial chain, bit for bit, State
+    included."""
     torch = torch_cuda
     mod = module_of(PEAK_SRC, "peak_follower")
     params = mod.default_parameters()
@@ -928,7 +928,8 @@ def test_one_level_learning_unlearns_when_the_input_stops_forgetting(torch_cuda)
     assert_same(res[False], res[True])
     for i in infos:
         print({k: i[k] for k in ("levels", "warmup_blocks", "differed", "serial_reruns", "chain", "disabled")})
-    # the loud renders: the first level alone once learnt; a quiet render
-    # launched with it missed (and came out exact all the same)
+    # the loud renders: the first level met the State; a quiet render
+    # learnt that way needed the second level (launched for this) and came
+    # out exact
     assert infos[0]["used"] and infos[2]["levels"] == 1, infos
-    assert any(i["levels"] == 1 and i["differed"][0] > 0 for i in infos[3:]), infos
+    assert any(i["levels"] > 1 for i in infos[3:]), infos
