@@ -698,7 +698,7 @@ def main():
                  "dspb_seg_c2b512 + dspb_seg_check + dspb_seg_walk (speculative segments, DESIGN 4.6)"
                  if pname == "biquad" else
                  "dspb_seg_chain_ind_c2b512 + dspb_seg_c2b512 + dspb_seg_check + dspb_seg_walk (a split State: "
-                 "the block counter's chain on one lane, then speculative segments started from it; DESIGN 4.6)"
+                 "the block counter's chain on 64 lanes, then speculative segments started from it; DESIGN 4.6)"
                  if pname == "envelope_counter" else
                  "dspb_seg_chain_c2b512 + dspb_seg_c2b512_rerun (a State learned never to forget: the State "
                  "chain on one lane, then every segment from its recorded State; DESIGN 4.6)")
@@ -999,12 +999,13 @@ def main():
                             "frame (14.4 ns at 2.39 GHz; a dependent v_add_f64 is 6.3, the VCC round trip the "
                             "rest: tools/diag/f64_chain_floor.hip, profiles/r06_f64_chain_floor.jsonl), then the "
                             "segments in parallel; DESIGN 4.6" if (state_segments or {}).get("chain") else
-                            ("a split State: the block counter's chain on one lane, then "
+                            ("a split State: the block counter's chain on 64 lanes, then "
                              "the speculative segments as biquad_src's; DESIGN 4.6"
                              if (state_segments or {}).get("split") else
-                             "segments: one lane per segment runs the callback's own chain block after block; "
-                            "the lanes are the blocks LDS holds (18 per 76 KB workgroup, 36 per CU), so the rounds "
-                            "(blocks per segment + warm-up) bound it; DESIGN 4.6")
+                             "segments: one lane per segment runs the callback's own chain block after block "
+                            "(wave 0 of each workgroup; waves 1-3 move the blocks); the lanes are the blocks LDS "
+                            "holds (18 per 76 KB workgroup, 36 per CU), so the rounds (blocks per segment + "
+                            "warm-up) bound it; DESIGN 4.6")
                             if wl in ("biquad_src", "sine_src", "envelope_src") else
                             "the render (LDS-capacity-bound callbacks) then the power-capped memory STFT, "
                             "serial: DESIGN 4.6, profiles/r02_generic_stft_schedules.txt"
